@@ -1,0 +1,119 @@
+/* mpas_dyn.h -- C-ABI of libmpasdyn, the MI355X (gfx950) drop-in for the RK3 dynamics
+ * hot path of alexaiken/mpas-regent (dynamics/rk_timestep.rg:361-519 and the leaf
+ * tasks of dynamics/dynamics_tasks.rg).
+ *
+ * Boundary.  Each Regent leaf task of the path becomes one extern "C" entry point with
+ * the task's name (prefixed mpas_) and its scalar parameters in the task's order.  The
+ * task's region arguments (cr, cpr, er, vr, vert_r) are the device-resident state owned
+ * by an mpas_ctx; fields move across the boundary with mpas_upload / mpas_download,
+ * which take a plain host pointer and byte strides, so the Legion SOA layout a Regent
+ * binding would hand over (legion_accessor_array_*_raw_rect_ptr: entity stride, level
+ * stride; fortran/examples.rg:21-46) is accepted as is.  Field ids are the Regent field
+ * names (data_structures.rg), looked up with mpas_field_id.
+ *
+ * Conventions.  Every function returns 0 on success or a negative MPAS_E* code; the
+ * message is in mpas_last_error(ctx).  No C++ exception crosses the ABI.  A context owns
+ * one HIP device and its streams and is single-threaded; separate contexts may be
+ * driven from separate host threads.  Task calls are stream-ordered (asynchronous);
+ * mpas_sync waits.  The host arrays passed to upload/download are borrowed for the call.
+ * There is no CPU fallback: without a usable gfx950 device mpas_ctx_create fails.
+ */
+#ifndef MPAS_DYN_H
+#define MPAS_DYN_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPAS_OK 0
+#define MPAS_EINVAL (-1)
+#define MPAS_EHIP (-2)
+#define MPAS_ERCCL (-3)
+#define MPAS_ENOMEM (-4)
+#define MPAS_ENOTSUP (-5)
+
+typedef struct mpas_ctx mpas_ctx;
+
+/* mesh dimensions; constants.rg:18-26 (nCells, nEdges, nVertices, nVertLevels) */
+typedef struct {
+    int32_t nCells;
+    int32_t nEdges;
+    int32_t nVertices;
+    int32_t nVertLevels; /* L; fields carry L+1 levels (main.rg:21-24), L+1 <= 64 */
+} mpas_dims;
+
+/* ---- context and residency ---------------------------------------------------- */
+int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims);
+int mpas_ctx_destroy(mpas_ctx* ctx);
+const char* mpas_last_error(const mpas_ctx* ctx);
+int mpas_sync(mpas_ctx* ctx);
+/* the HIP stream (hipStream_t) the tasks run on, for callers that time with events */
+int mpas_get_stream(mpas_ctx* ctx, void** stream);
+/* options: "exact" = 1 makes the two reassociated kernels (Q10 q sum, acoustic scan)
+ * evaluate the reference's literal order (bit-identical to the oracle, slower). */
+int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
+
+/* field registry (include/mpas_fields.def order) */
+int mpas_field_count(void);
+int mpas_field_id(const char* name);
+const char* mpas_field_name(int field_id);
+int mpas_field_kind(int field_id);  /* 0 C3,1 C3V,2 E3,3 V3,4 C2F,5 C2I,6 E2F,7 E2I,8 V2F,9 V2I,10 C3B,11 ZV */
+int mpas_field_width(int field_id);
+
+/* Host <-> device copy of one field.  Element (entity e, level k, component i) is at
+ * byte offset e*stride_entity + k*stride_level + i*stride_comp of host (levels 0..L,
+ * entities 0..n-1; components only for array fields).  Element type: double for fp64
+ * fields, int32 for integer fields, uint8 for masks.  Entity-id fields are clamped
+ * on upload so that any id outside [0, n] resolves to the zero slot n. */
+int mpas_upload(mpas_ctx* ctx, int field_id, const void* host, int64_t stride_entity, int64_t stride_level,
+                int64_t stride_comp);
+int mpas_download(mpas_ctx* ctx, int field_id, void* host, int64_t stride_entity, int64_t stride_level,
+                  int64_t stride_comp);
+/* Fill every synthetic-distribution field (mpas_fields.def DIST != M) on the device
+ * with the counter-based generator of mpas_synth.h (benchmark inputs). */
+int mpas_fill_synthetic(mpas_ctx* ctx, uint64_t seed);
+
+/* ---- the hot-path tasks (dynamics_tasks.rg) ------------------------------------ */
+/* :747  atm_rk_integration_setup(cr, er) */
+int mpas_atm_rk_integration_setup(mpas_ctx* ctx);
+/* :460  atm_compute_moist_coefficients(cr, er) */
+int mpas_atm_compute_moist_coefficients(mpas_ctx* ctx);
+/* :513  atm_compute_vert_imp_coefs(cr, vert_r, dts) */
+int mpas_atm_compute_vert_imp_coefs(mpas_ctx* ctx, double dts);
+/* :814  atm_compute_dyn_tend_work(cr, er, vr, vert_r, rk_step, dt, config_horiz_mixing,
+ *       config_mpas_cam_coef, config_mix_full, config_rayleigh_damp_u);
+ *       horiz_mixing: 0 "2d_smagorinsky", 1 "2d_fixed", 2 other */
+int mpas_atm_compute_dyn_tend_work(mpas_ctx* ctx, int rk_step, double dt, int config_horiz_mixing,
+                                   double config_mpas_cam_coef, int config_mix_full, int config_rayleigh_damp_u);
+/* :1503 atm_set_smlstep_pert_variables_work(cpr, er, vert_r); cpr = field cprMask */
+int mpas_atm_set_smlstep_pert_variables_work(mpas_ctx* ctx);
+/* :1546 atm_advance_acoustic_step_work(cr, er, vert_r, dts, small_step) */
+int mpas_atm_advance_acoustic_step_work(mpas_ctx* ctx, double dts, int small_step);
+/* :1726 atm_divergence_damping_3d(cpr, er, dts); cpr's isShared = field isShared */
+int mpas_atm_divergence_damping_3d(mpas_ctx* ctx, double dts);
+/* :328  atm_compute_solve_diagnostics(cr, er, vr, hollingsworth, rk_step) */
+int mpas_atm_compute_solve_diagnostics(mpas_ctx* ctx, int hollingsworth, int rk_step);
+/* :1951 atm_rk_dynamics_substep_finish(cr, er, dynamics_substep, dynamics_split) */
+int mpas_atm_rk_dynamics_substep_finish(mpas_ctx* ctx, int dynamics_substep, int dynamics_split);
+
+/* ---- the driver (rk_timestep.rg:361-500) ---------------------------------------- */
+/* schedule 0: the reference's atm_srk3 (Q4: rk_sub_timestep[rk_step] truncated into
+ * dyn_tend's rk_step; Q5: n+1 acoustic substeps); schedule 1: dyn_tend rk_step = 0,1,2
+ * (the MPAS schedule used by the benchmark). */
+int mpas_atm_srk3(mpas_ctx* ctx, double dt, int schedule);
+/* rk_timestep.rg:503 atm_timestep = atm_srk3 with the reference schedule */
+int mpas_atm_timestep(mpas_ctx* ctx, double dt);
+
+/* ---- instrumentation ------------------------------------------------------------ */
+/* With timing on, every task call is bracketed by HIP events on the task stream and its
+ * device time accumulated per task name; mpas_timing_get returns calls and total ms. */
+int mpas_timing_enable(mpas_ctx* ctx, int on);
+int mpas_timing_reset(mpas_ctx* ctx);
+int mpas_timing_count(mpas_ctx* ctx);
+int mpas_timing_get(mpas_ctx* ctx, int idx, const char** name, int64_t* calls, double* total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

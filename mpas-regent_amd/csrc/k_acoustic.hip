@@ -1,0 +1,184 @@
+// k_acoustic.hip -- atm_advance_acoustic_step_work (dynamics_tasks.rg:1546-1705), gfx950.
+//
+// One wavefront per cell column (lane k = level k).  Everything except the vertical
+// recurrence of rw_p is level-parallel: the small-step initialisation, the horizontal
+// flux gather over edgesOnCell (ru_p at the edge, theta_m at cellsOnEdge), rs/ts, and
+// the final rho_pp/rtheta_pp/wwAvg updates.
+//
+// The recurrence (Q20: rw_p(k) reads rw_p, rho_pp, rtheta_pp of level k-1 AFTER their
+// update; Q19: rs(k-1) = ts(k-1) = 0; Q21: no back substitution) is, with those k-1
+// values affine in rw_p(k-1), a first-order linear recurrence
+//        x_k = G_k * x_{k-1} + H_k,   x_0 = rw_p(0) (not updated)
+// solved by an inclusive affine prefix scan over the lanes with wavefront shuffles
+// (log2(LP) steps).  The scan reassociates fp64, so this path agrees with the oracle
+// to rounding (tests/test_gpu_parity.py states the tolerance).  The EXACT=true
+// variant evaluates the literal expression level by level (lane k-1 -> lane k
+// broadcast) and is bit-identical to the oracle; it is the reference for the scan.
+#include "mpas_dev.h"
+
+namespace mpas {
+
+template <int LP, bool EXACT>
+__global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCells) return;
+    const size_t p = (size_t)c * LP + k;
+    double* rtp_f = fw(S, F_rtheta_pp);
+    double* rpp_f = fw(S, F_rho_pp);
+    double* rwp_f = fw(S, F_rw_p);
+    double* ww_f = fw(S, F_wwAvg);
+    double rtp = col_rd(rtp_f, c, k, L, LP), rpp = col_rd(rpp_f, c, k, L, LP);
+    double rwp = col_rd(rwp_f, c, k, L, LP), ww = col_rd(ww_f, c, k, L, LP);
+    // :1615-1636
+    if (k < L) fw(S, F_rtheta_pp_old)[p] = (small_step == 0) ? 0 : rtp;
+    if (small_step == 0) {
+        ww = 0;
+        rwp = 0;
+        if (k < L) {
+            rpp = 0;
+            rtp = 0;
+        }
+    }
+    const double tm = col_rd(fd(S, F_theta_m), c, k, L, LP);
+    const double tend_rho = col_rd(fd(S, F_tend_rho), c, k, L, LP);
+    const double w = col_rd(fd(S, F_w), c, k, L, LP);
+
+    if (fd(S, F_specZoneMaskCell)[c] != 0.0) {  // :1698-1703 (column-uniform branch)
+        if (k < L) {
+            rpp = rpp + dts * tend_rho;
+            rtp = rtp + dts * tm;
+            rwp = rwp + dts * w;
+            ww = ww + 0.5 * (1.0 + epssm) * rwp;
+            rpp_f[p] = rpp;
+            rtp_f[p] = rtp;
+        }
+        if (k <= L) {
+            rwp_f[p] = rwp;
+            ww_f[p] = ww;
+        }
+        return;
+    }
+
+    // ---- horizontal flux (:1644-1652)
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
+    const double invA = fd(S, F_invAreaCell)[c];
+    const double *dvEdge = fd(S, F_dvEdge), *ru_p = fd(S, F_ru_p), *tm_f = fd(S, F_theta_m);
+    const int* coe = fi(S, F_cellsOnEdge);
+    double rs = 0, ts = 0;
+    if (k < L) {
+        for (int i = 0; i < ne; i++) {
+            int iEdge = eoc[i];
+            int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
+            double flux = sgn[i] * dts * dvEdge[iEdge] * ru_p[(size_t)iEdge * LP + k] * invA;
+            rs -= flux;
+            ts -= flux * 0.5 * (tm_f[(size_t)cell2 * LP + k] + tm_f[(size_t)cell1 * LP + k]);
+        }
+    }
+    // ---- rs, ts (:1657-1658) from the OLD rw_p
+    const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    const double coftz = col_rd(fd(S, F_coftz), c, k, L, LP);
+    const double rwp_p = lvl_up<LP>(rwp, k), coftz_p = lvl_up<LP>(coftz, k);
+    rs = rpp + dts * tend_rho + rs - cofrz * resm * (rwp_p - rwp);
+    ts = rtp + dts * tm + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
+
+    // per-level coefficients of the recurrence
+    const double zz = col_rd(fd(S, F_zz), c, k, L, LP), zz_m = lvl_dn<LP>(zz, k);
+    const double rz = col_rd(fd(S, F_rho_zz), c, k, L, LP), rz_m = lvl_dn<LP>(rz, k);
+    const double cofwt = col_rd(fd(S, F_cofwt), c, k, L, LP), cofwt_m = lvl_dn<LP>(cofwt, k);
+    const double cofwz = col_rd(fd(S, F_cofwz), c, k, L, LP), cofwr = col_rd(fd(S, F_cofwr), c, k, L, LP);
+    const double a_tri = col_rd(fd(S, F_a_tri), c, k, L, LP), alpha = col_rd(fd(S, F_alpha_tri), c, k, L, LP);
+    const double rws = col_rd(fd(S, F_rw_save), c, k, L, LP), rw = col_rd(fd(S, F_rw), c, k, L, LP);
+    const double dss = col_rd(fd(S, F_dss), c, k, L, LP);
+    const double tsm = 0.0, rsm = 0.0;  // Q19
+    const double rwold = rwp;
+    double x;  // new rw_p of this level
+
+    if (EXACT) {
+        // literal level-by-level evaluation; lane k-1 hands (rw_p, rho_pp, rtheta_pp) to lane k
+        x = rwold;
+        double rpp_new = rs - cofrz * (rwp_p - x);
+        double rtp_new = ts - rdzw * (coftz_p * rwp_p - coftz * x);
+        const int base = (int)(threadIdx.x & 63) & ~(LP - 1);
+        for (int kk = 1; kk < L; kk++) {
+            double X = __shfl(x, base + kk - 1, 64);
+            double R = __shfl(rpp_new, base + kk - 1, 64);
+            double T = __shfl(rtp_new, base + kk - 1, 64);
+            if (k == kk) {
+                double y = rwold;
+                y += dts * w - cofwz * ((zz * ts - zz_m * tsm) + resm * (zz * rtp - zz_m * T)) -
+                     cofwr * ((rs + rsm) + resm * (rpp + R)) + cofwt * (ts + resm * rtp) + cofwt_m * (tsm + resm * T);
+                y -= a_tri * X;
+                y *= alpha;
+                y += (rws - rw) - dts * dss * (fzm * zz + fzp * zz_m) * (fzm * rz + fzp * rz_m) * w;
+                y /= (1.0 + dts * dss);
+                y -= (rws - rw);
+                x = y;
+                rpp_new = rs - cofrz * (rwp_p - x);
+                rtp_new = ts - rdzw * (coftz_p * rwp_p - coftz * x);
+            }
+        }
+    } else {
+        // x_k = G_k x_{k-1} + H_k with rtheta_pp_new(k-1) = T0 + Tc x_{k-1},
+        // rho_pp_new(k-1) = R0 + Rc x_{k-1}; (T0, Tc, R0, Rc) come from lane k-1
+        const double T0 = ts - rdzw * (coftz_p * rwp_p), Tc = rdzw * coftz;
+        const double R0 = rs - cofrz * rwp_p, Rc = cofrz;
+        const double T0m = lvl_dn<LP>(T0, k), Tcm = lvl_dn<LP>(Tc, k);
+        const double R0m = lvl_dn<LP>(R0, k), Rcm = lvl_dn<LP>(Rc, k);
+        const double x0 = __shfl(rwold, (int)(threadIdx.x & 63) & ~(LP - 1), 64);
+        double G = 1.0, H = 0.0;
+        if (k >= 1 && k < L) {
+            const double P = rwold + dts * w - cofwz * ((zz * ts) + resm * (zz * rtp)) - cofwr * (rs + resm * rpp) +
+                             cofwt * (ts + resm * rtp);
+            const double cT = cofwz * resm * zz_m + cofwt_m * resm;
+            const double cR = cofwr * resm;
+            const double F = 1.0 + dts * dss;
+            const double Dd = rws - rw;
+            const double E = dts * dss * (fzm * zz + fzp * zz_m) * (fzm * rz + fzp * rz_m) * w;
+            const double af = alpha / F;
+            G = af * (cT * Tcm - cR * Rcm - a_tri);
+            H = af * (P + cT * T0m - cR * R0m) + (Dd - E) / F - Dd;
+            if (k == 1) {
+                H = G * x0 + H;
+                G = 0.0;
+            }
+        }
+#pragma unroll
+        for (int off = 1; off < LP; off <<= 1) {
+            double Gp = __shfl_up(G, off, LP);
+            double Hp = __shfl_up(H, off, LP);
+            if (k >= off) {
+                H = G * Hp + H;
+                G = G * Gp;
+            }
+        }
+        x = (k == 0) ? rwold : H;
+    }
+    if (k < L) {
+        if (k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
+        rpp_f[p] = rs - cofrz * (rwp_p - x);
+        rtp_f[p] = ts - rdzw * (coftz_p * rwp_p - coftz * x);
+    }
+    if (k <= L) {
+        rwp_f[p] = (k < L) ? x : rwp;
+        ww_f[p] = ww;
+    }
+}
+
+template <int LP>
+static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {
+    double epssm = kEpssm;
+    double resm = (1.0 - epssm) / (1.0 + epssm);
+    int grid = (S.nCells + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    if (exact) k_acoustic<LP, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
+    else k_acoustic<LP, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
+    return hipGetLastError();
+}
+hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {
+    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact);
+}
+
+}  // namespace mpas

@@ -1,0 +1,490 @@
+// k_dyn.hip -- atm_compute_dyn_tend_work (dynamics_tasks.rg:814-1480), the north-star
+// kernel, for gfx950.  One wavefront (LP lanes) per cell/edge/vertex column, lane k =
+// level k; neighbour columns are contiguous 8*(L+1)-byte gathers; vertical stencils
+// (wduz, wdwz, wdtz, k+-1 reads) are lane shuffles.
+//
+// The reference's ~20 loop nests fold into the global barriers the data flow needs:
+//   A  cells    kdiff (rk0, Q11: own level only), h_divergence, tend_rho + dpdz (rk0),
+//               wc = w after the zeroing, horizontal advection (Q13) and curvature
+//   B  edges    tend_u_euler pressure gradient (rk0), wduz (in-lane), tend_u, q (Q10),
+//               ke gradient, curvature (Q12), delsq_u + del2 (rk0), Rayleigh,
+//               and, when no del4 follows, tend_u += tend_u_euler + tend_ru_physics
+//   C  rk0      vertices: delsq_vorticity; cells: delsq_divergence, delsq_w + del2 of
+//               tend_w_euler, delsq_theta + del2 of tend_theta_euler
+//   D  rk0+del4 edges: del4 of tend_u_euler, tend_u finish
+//   E  cells    del4 of w/theta (rk0), wdwz (in-lane), w scaling (Q14), buoyancy (rk0),
+//               theta advection over advCellsForEdge, perturbation flux (rk>0),
+//               wdtz (Q15, in-lane), tend_theta finish
+// rk_step > 0 runs A, B, E.  Scratch the reference writes to fields (flux_arr,
+// ru_edge_w, wduz, q, wdwz, wdtz, u_mix) stays in registers; only their level-L
+// slots, which the reference never writes, are read from HBM.
+#include "mpas_dev.h"
+
+namespace mpas {
+
+__device__ __forceinline__ double dmin_(double a, double b) { return a < b ? a : b; }
+__device__ __forceinline__ double dmax_(double a, double b) { return a > b ? a : b; }
+
+__device__ __forceinline__ double flux4(double q_im2, double q_im1, double q_i, double q_ip1, double ua) {
+    return ua * (7. * (q_i + q_im1) - (q_ip1 + q_im2)) / 12.0;
+}
+__device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, double q_ip1, double ua, double coef3) {
+    return flux4(q_im2, q_im1, q_i, q_ip1, ua) + coef3 * fabs(ua) * ((q_ip1 - q_im2) - 3. * (q_i - q_im1)) / 12.0;
+}
+
+struct DynK {
+    int rk_step, horiz_mixing, rayleigh, exact_q;
+    double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
+};
+
+// ------------------------------------------------------------------------ A (cells)
+template <int LP>
+__global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCells) return;
+    const size_t p = (size_t)c * LP + k;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+    const double* dvEdge = fd(S, F_dvEdge);
+    const double *u = fd(S, F_u), *v = fd(S, F_v), *ru = fd(S, F_ru);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
+    const bool rk0 = a.rk_step == 0;
+
+    // ---- kdiff (:858-917)
+    if (rk0 && (a.horiz_mixing == 0 || a.horiz_mixing == 1 || a.cam_coef > 0.0)) {
+        double kd;
+        if (a.horiz_mixing == 0) {
+            const double* defa = fd(S, F_defc_a) + (size_t)c * 10;
+            const double* defb = fd(S, F_defc_b) + (size_t)c * 10;
+            double d_diag = 0.0, d_off_diag = 0.0;
+            for (int i = 0; i < ne; i++) {
+                int e = eoc[i];
+                double ue = col_rd(u, e, k, L, LP), ve = col_rd(v, e, k, L, LP);
+                d_diag += defa[i] * ue - defb[i] * ve;
+                d_off_diag += defb[i] * ue + defa[i] * ve;
+            }
+            kd = dmin_(a.cs_l2 * sqrt(d_diag * d_diag + d_off_diag * d_off_diag), a.cap);
+        } else if (a.horiz_mixing == 1) {
+            kd = 0.0;
+        } else {
+            kd = col_rd(fd(S, F_kdiff), c, k, L, LP);
+        }
+        if (a.cam_coef > 0.0 && k >= L - 2 && k <= L) {
+            int pw = k - (L - 2);
+            kd = dmax_(kd, (pw == 0 ? 1.0 : 2.0) * 2.0833 * kLenDisp * a.cam_coef);
+        }
+        if (k < L) fw(S, F_kdiff)[p] = kd;
+    }
+
+    // ---- h_divergence (:924-938)
+    double hd = 0.0;
+    for (int i = 0; i < ne; i++) {
+        int e = eoc[i];
+        double edge_sign = eocs[i] * dvEdge[e];
+        hd += edge_sign * col_rd(ru, e, k, L, LP);
+    }
+    hd *= fd(S, F_invAreaCell)[c];
+    if (k < L) fw(S, F_h_divergence)[p] = hd;
+
+    // ---- tend_rho, dpdz (:942-951)
+    const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
+    const double rw_p1 = lvl_up<LP>(rw, k);
+    if (rk0 && k < L) {
+        fw(S, F_tend_rho)[p] = -hd - rdzw * (rw_p1 - rw + fd(S, F_tend_rho_physics)[p]);
+        double qt = fd(S, F_qtot)[p];
+        fw(S, F_dpdz)[p] = -kGravity * (fd(S, F_rho_base)[p] * (qt) + fd(S, F_rho_p_save)[p] * (1.0 + qt));
+    }
+
+    // ---- w: zeroing (:1170), horizontal advection (:1174-1205, Q13), curvature (:1208-1218)
+    // After the zeroing every w(cell, k<L) read by flux_arr is exactly 0.0 (the zero
+    // slot is 0 too), so flux_arr = sum_j scalar_weight_j * 0.0 of the cell's LAST edge
+    // (flux_arr and ru_edge_w are overwritten per edge); it is evaluated literally so
+    // that non-finite weights propagate as in the reference.
+    double w0 = 0.0;
+    {
+        const int e_last = ne > 0 ? eoc[ne - 1] : S.nEdges;
+        const double ru_l = col_rd(ru, e_last, k, L, LP);
+        const double ru_lm = lvl_dn<LP>(ru_l, k);
+        if (ne > 0 && k > 0 && k < L) {
+            double ru_edge_w = fzm * ru_l + fzp * ru_lm;
+            const int na = fi(S, F_nAdvCellsForEdge)[e_last];
+            const double* ac = fd(S, F_adv_coefs) + (size_t)e_last * 15;
+            const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e_last * 15;
+            double flux_arr = 0.0;
+            const double w_zeroed = 0.0;
+            for (int j = 0; j < na; j++) {
+                double scalar_weight = ac[j] + copysign(1.0, ru_edge_w) * ac3[j];
+                flux_arr += scalar_weight * w_zeroed;
+            }
+            for (int i = 0; i < ne; i++) w0 -= eocs[i] * ru_edge_w * flux_arr;
+        }
+    }
+    const double *rz_f = fd(S, F_rho_zz), *urz_f = fd(S, F_uReconstructZonal), *urm_f = fd(S, F_uReconstructMeridional);
+    const double rz = col_rd(rz_f, c, k, L, LP), urz = col_rd(urz_f, c, k, L, LP), urm = col_rd(urm_f, c, k, L, LP);
+    const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
+    if (k < L) {
+        double wc = w0;
+        if (k > 0) {
+            const double coslat = fd(S, X_cosLatCell)[c];
+            double aa = fzm * urz + fzp * urz_m;
+            double bb = fzm * urm + fzp * urm_m;
+            wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
+                  2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
+        }
+        fw(S, X_wc)[p] = wc;
+    }
+}
+
+// ------------------------------------------------------------------------ B (edges)
+template <int LP>
+__global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, e = m.ent;
+    if (e >= S.nEdges) return;
+    const size_t p = (size_t)e * LP + k;
+    const bool rk0 = a.rk_step == 0;
+    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
+    const double invDc = fd(S, F_invDcEdge)[e];
+    const double* u_f = fd(S, F_u);
+    const double u = col_rd(u_f, e, k, L, LP);
+    const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
+    const double* rw_f = fd(S, F_rw);
+    const double rw1 = col_rd(rw_f, cell1, k, L, LP), rw2 = col_rd(rw_f, cell2, k, L, LP);
+    const double rho_edge = col_rd(fd(S, F_rho_edge), e, k, L, LP);
+
+    // ---- wduz (:972-980); level L is never written by the reference: read it
+    double wduz = 0.0;
+    if (k == 1 || k == L - 1) wduz = 0.5 * (rw1 + rw2) * (fzm * u + fzp * u_m);
+    if (k > 1 && k < L - 1) wduz = flux3(u_m2, u_m, u, u_p, 0.5 * (rw1 + rw2), 1.0);
+    if (k == L) wduz = fd(S, F_wduz)[p];
+    const double wduz_p = lvl_up<LP>(wduz, k);
+
+    // gathers for the ke/h_divergence/curvature terms (all lanes, shuffles below)
+    const double* w_f = fd(S, F_w);
+    const double w1 = col_rd(w_f, cell1, k, L, LP), w2 = col_rd(w_f, cell2, k, L, LP);
+    const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
+    if (k >= L) return;
+
+    // ---- tend_u (:987-1007)
+    double tend_u = -rdzw * (wduz_p - wduz);
+    const double pv = fd(S, F_pv_edge)[p];
+    const int neoe = fi(S, F_nEdgesOnEdge)[e];
+    const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
+    const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
+    const double* pv_f = fd(S, F_pv_edge);
+    double q = 0.0;
+    if (a.exact_q) {
+        for (int j = 0; j < neoe; j++) {  // Q10 literal: each term added nVertLevels times
+            int ee = eoe[j];
+            double ue = u_f[(size_t)ee * LP + k], pve = pv_f[(size_t)ee * LP + k];
+            for (int kk = 0; kk < L; kk++) {
+                double workpv = 0.5 * (pv + pve);
+                q += woe[j] * ue * workpv;
+            }
+        }
+    } else {
+        const double dL = (double)L;
+        for (int j = 0; j < neoe; j++) {  // Q10 value, nVertLevels * term
+            int ee = eoe[j];
+            double ue = u_f[(size_t)ee * LP + k], pve = pv_f[(size_t)ee * LP + k];
+            double workpv = 0.5 * (pv + pve);
+            q += (woe[j] * ue * workpv) * dL;
+        }
+    }
+    const double* ke_f = fd(S, F_ke);
+    const double* hd_f = fd(S, F_h_divergence);
+    const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
+    tend_u += rho_edge * (q - (ke_f[p2] - ke_f[p1]) * invDc) - u * 0.5 * (hd_f[p1] + hd_f[p2]);
+    // ---- curvature (:1011-1017, Q12 literal)
+    {
+        const double cosA = fd(S, X_cosAngleEdge)[e], cosL = fd(S, X_cosLatEdge)[e];
+        tend_u -= (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p)) -
+                  (u * 0.25 * (w1 + w1p + w2 + w2p) * rho_edge * a.inv_r_earth);
+    }
+
+    double tue;
+    if (rk0) {
+        // ---- pressure gradient (:964-970)
+        const double *pp = fd(S, F_pressure_p), *zz = fd(S, F_zz), *dpdz = fd(S, F_dpdz);
+        tue = -fd(S, F_cqu)[p] * ((pp[p2] - pp[p1]) * invDc / (0.5 * (zz[p2] + zz[p1])) -
+                                  0.5 * fd(S, F_zxu)[p] * (dpdz[p1] + dpdz[p2]));
+        // ---- del2 (:1030-1048)
+        const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
+        const double r_dc = invDc;
+        const double r_dv = dmin_(fd(S, F_invDvEdge)[e], 4 * r_dc);
+        const double *div = fd(S, F_divergence), *vor = fd(S, F_vorticity), *kdiff = fd(S, F_kdiff);
+        double u_diffusion = (div[p2] - div[p1]) * r_dc -
+                             (vor[(size_t)vertex2 * LP + k] - vor[(size_t)vertex1 * LP + k]) * r_dv;
+        double delsq_u = 0.0;
+        delsq_u += u_diffusion;
+        fw(S, F_delsq_u)[p] = delsq_u;
+        double kdiffu = 0.5 * (kdiff[p1] + kdiff[p2]);
+        tue += rho_edge * kdiffu * u_diffusion * fd(S, F_meshScalingDel2)[e];
+    } else {
+        tue = fd(S, F_tend_u_euler)[p];
+    }
+    // ---- Rayleigh damping (:1152-1159)
+    if (a.rayleigh && k > L - kRayleighLevels + 1)
+        tend_u -= rho_edge * u * (((double)k - (double)(L - kRayleighLevels)) * a.rayleigh_inv);
+    if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
+        fw(S, F_tend_u_euler)[p] = tue;
+        fw(S, F_tend_u)[p] = tend_u;
+    } else {
+        if (rk0) fw(S, F_tend_u_euler)[p] = tue;
+        tend_u += tue + fd(S, F_tend_ru_physics)[p];  // :1161-1163
+        fw(S, F_tend_u)[p] = tend_u;
+    }
+}
+
+// ------------------------------------------------------------------------ C (rk0)
+template <int LP>
+__global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
+    const int L = S.L;
+    const double* dsu = fd(S, F_delsq_u);
+    if ((int)blockIdx.x < nVB) {  // delsq_vorticity (:1052-1060)
+        ColMap<LP> m;
+        const int vx = m.ent, k = m.k;
+        if (vx >= S.nVertices || k >= L) return;
+        const int* eov = fi(S, F_edgesOnVertex) + (size_t)vx * 3;
+        const double* sgn = fd(S, F_edgesOnVertex_sign) + (size_t)vx * 3;
+        const double iat = fd(S, F_invAreaTriangle)[vx];
+        const double* dcEdge = fd(S, F_dcEdge);
+        double dsv = 0.0;
+        for (int i = 0; i < 3; i++) {
+            int iEdge = eov[i];
+            double edge_sign = iat * dcEdge[iEdge] * sgn[i];
+            dsv += edge_sign * dsu[(size_t)iEdge * LP + k];
+        }
+        fw(S, F_delsq_vorticity)[(size_t)vx * LP + k] = dsv;
+        return;
+    }
+    const int c = (int)(blockIdx.x - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
+    const int k = (int)(threadIdx.x % LP);
+    if (c >= S.nCells) return;
+    const size_t p = (size_t)c * LP + k;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+    const double *dvEdge = fd(S, F_dvEdge), *invDc = fd(S, F_invDcEdge), *msd2 = fd(S, F_meshScalingDel2);
+    const int* coe = fi(S, F_cellsOnEdge);
+    const double *rho_edge = fd(S, F_rho_edge), *wc = fd(S, X_wc), *kdiff = fd(S, F_kdiff), *tm = fd(S, F_theta_m);
+    const double r_areaCell = fd(S, F_invAreaCell)[c];
+    double dsd = 0.0, delsq_w = 0.0, twe = 0.0, delsq_theta = 0.0, tte = 0.0;
+    for (int i = 0; i < ne; i++) {
+        const int iEdge = eoc[i];
+        const int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
+        const size_t q1 = (size_t)cell1 * LP + k, q2 = (size_t)cell2 * LP + k;
+        const double re_k = col_rd(rho_edge, iEdge, k, L, LP);
+        const double re_m = lvl_dn<LP>(re_k, k);
+        const double kd1 = col_rd(kdiff, cell1, k, L, LP), kd2 = col_rd(kdiff, cell2, k, L, LP);
+        const double kd1m = lvl_dn<LP>(kd1, k), kd2m = lvl_dn<LP>(kd2, k);
+        if (k >= L) continue;
+        const double dv = dvEdge[iEdge], idc = invDc[iEdge];
+        if (a.h4 > 0.0) {  // delsq_divergence (:1062-1070)
+            double edge_sign = r_areaCell * dv * eocs[i];
+            dsd += edge_sign * dsu[(size_t)iEdge * LP + k];
+        }
+        {  // delsq_w, tend_w_euler del2 (:1231-1254)
+            double edge_sign = 0.5 * r_areaCell * eocs[i] * dv * idc;
+            if (k > 0) {
+                double w_turb_flux = edge_sign * (re_k + re_m) * (wc[q2] - wc[q1]);
+                delsq_w += w_turb_flux;
+                w_turb_flux *= msd2[iEdge] * 0.25 * (kd1 + kd2 + kd1m + kd2m);
+                twe += w_turb_flux;
+            }
+        }
+        {  // delsq_theta, tend_theta_euler del2 (:1365-1382)
+            double edge_sign = r_areaCell * eocs[i] * dv * idc;
+            double pr_scale = a.prandtl_inv * msd2[iEdge];
+            double theta_turb_flux = edge_sign * (tm[q2] - tm[q1]) * re_k;
+            delsq_theta += theta_turb_flux;
+            theta_turb_flux *= 0.5 * (kd1 + kd2) * pr_scale;
+            tte += theta_turb_flux;
+        }
+    }
+    if (k >= L) return;
+    if (a.h4 > 0.0) fw(S, F_delsq_divergence)[p] = dsd;
+    fw(S, F_delsq_w)[p] = delsq_w;
+    fw(S, F_tend_w_euler)[p] = twe;
+    fw(S, F_delsq_theta)[p] = delsq_theta;
+    fw(S, F_tend_theta_euler)[p] = tte;
+}
+
+// ------------------------------------------------------------------------ D (rk0, del4)
+template <int LP>
+__global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, e = m.ent;
+    if (e >= S.nEdges || k >= L) return;
+    const size_t p = (size_t)e * LP + k;
+    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
+    const double invDc = fd(S, F_invDcEdge)[e];
+    double u_mix_scale = fd(S, F_meshScalingDel4)[e] * a.h4;
+    double r_dc = u_mix_scale * kDel4uDivFactor * invDc;
+    double r_dv = u_mix_scale * dmin_(fd(S, F_invDvEdge)[e], 4 * invDc);
+    const double *dd = fd(S, F_delsq_divergence), *dvv = fd(S, F_delsq_vorticity);
+    double u_diffusion = fd(S, F_rho_edge)[p] * ((dd[(size_t)cell2 * LP + k] - dd[(size_t)cell1 * LP + k]) * r_dc -
+                                                 (dvv[(size_t)vertex2 * LP + k] - dvv[(size_t)vertex1 * LP + k]) * r_dv);
+    double tue = fd(S, F_tend_u_euler)[p];
+    tue -= u_diffusion;
+    fw(S, F_tend_u_euler)[p] = tue;
+    double tend_u = fd(S, F_tend_u)[p];
+    tend_u += tue + fd(S, F_tend_ru_physics)[p];
+    fw(S, F_tend_u)[p] = tend_u;
+}
+
+// ------------------------------------------------------------------------ E (cells)
+template <int LP>
+__global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCells) return;
+    const size_t p = (size_t)c * LP + k;
+    const bool rk0 = a.rk_step == 0;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+    const double *dvEdge = fd(S, F_dvEdge), *invDcE = fd(S, F_invDcEdge), *msd4 = fd(S, F_meshScalingDel4);
+    const int* coe = fi(S, F_cellsOnEdge);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k], rdzu = fd(S, F_rdzu)[k];
+    const double invA = fd(S, F_invAreaCell)[c];
+
+    // ================= W =================
+    double twe = (k < L) ? fd(S, F_tend_w_euler)[p] : 0.0;
+    if (rk0 && a.h4 > 0.0 && k < L) {  // :1258-1272
+        const double* dw = fd(S, F_delsq_w);
+        double r_areaCell = a.h4 * invA;
+        for (int i = 0; i < ne; i++) {
+            int iEdge = eoc[i];
+            int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
+            double edge_sign = msd4[iEdge] * r_areaCell * dvEdge[iEdge] * eocs[i] * invDcE[iEdge];
+            if (k > 0) twe -= edge_sign * (dw[(size_t)cell2 * LP + k] - dw[(size_t)cell1 * LP + k]);
+        }
+    }
+    const double wc = (k < L) ? fd(S, X_wc)[p] : 0.0;
+    const double wc_m = lvl_dn<LP>(wc, k), wc_m2 = lvl_dn2<LP>(wc, k), wc_p = lvl_up<LP>(wc, k);
+    const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
+    const double rw_m = lvl_dn<LP>(rw, k);
+    double wdwz = 0.0;  // :1277-1287
+    if (k == 1 || k == L - 1) wdwz = 0.25 * (rw + rw_m) * (wc + wc_m);
+    if (k > 1 && k < L - 1) wdwz = flux3(wc_m2, wc_m, wc, wc_p, 0.5 * (rw + rw_m), 1.0);
+    if (k == L) wdwz = fd(S, F_wdwz)[p];
+    const double wdwz_p = lvl_up<LP>(wdwz, k);
+    const double pp = col_rd(fd(S, F_pressure_p), c, k, L, LP), dpdz = col_rd(fd(S, F_dpdz), c, k, L, LP);
+    const double pp_m = lvl_dn<LP>(pp, k), dpdz_m = lvl_dn<LP>(dpdz, k);
+    double w = wc;
+    if (k > 0 && k < L) {  // :1289-1302 (Q14 literal), :1318-1322
+        w *= invA - rdzu * (wdwz_p - wdwz);
+        if (rk0) twe -= fd(S, F_cqw)[p] * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
+        w += twe;
+    }
+    if (k < L) {
+        fw(S, F_w)[p] = w;
+        if (rk0) fw(S, F_tend_w_euler)[p] = twe;
+    }
+
+    // ================= theta =================
+    const double *ru = fd(S, F_ru), *tm = fd(S, F_theta_m);
+    double tend_theta = 0.0;  // :1328-1344
+    if (k < L) {
+        const int* nadv = fi(S, F_nAdvCellsForEdge);
+        const int* advc = fi(S, F_advCellsForEdge);
+        const double *ac_f = fd(S, F_adv_coefs), *ac3_f = fd(S, F_adv_coefs_3rd);
+        for (int i = 0; i < ne; i++) {
+            int iEdge = eoc[i];
+            double ru_e = ru[(size_t)iEdge * LP + k];
+            double sg = copysign(1.0, ru_e);
+            int na = nadv[iEdge];
+            const int* ad = advc + (size_t)iEdge * 15;
+            const double* ac = ac_f + (size_t)iEdge * 15;
+            const double* ac3 = ac3_f + (size_t)iEdge * 15;
+            double flux_arr = 0.0;
+            for (int j = 0; j < na; j++) {
+                double scalar_weight = ac[j] + sg * ac3[j];
+                flux_arr += scalar_weight * tm[(size_t)ad[j] * LP + k];
+            }
+            tend_theta -= eocs[i] * ru_e * flux_arr;
+        }
+        if (a.rk_step > 0) {  // :1347-1360
+            const double *rus = fd(S, F_ru_save), *tms = fd(S, F_theta_m_save);
+            for (int i = 0; i < ne; i++) {
+                int iEdge = eoc[i];
+                int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
+                size_t q = (size_t)iEdge * LP + k;
+                double flux = eocs[i] * dvEdge[iEdge] * (rus[q] - ru[q]) * 0.5 *
+                              (tms[(size_t)cell2 * LP + k] + tms[(size_t)cell1 * LP + k]);
+                tend_theta -= flux;
+            }
+        }
+    }
+    double tte = (k < L) ? fd(S, F_tend_theta_euler)[p] : 0.0;
+    if (rk0 && a.h4 > 0.0 && k < L) {  // :1384-1400
+        const double* dth = fd(S, F_delsq_theta);
+        double r_areaCell = a.h4 * a.prandtl_inv * invA;
+        for (int i = 0; i < ne; i++) {
+            int iEdge = eoc[i];
+            double edge_sign = msd4[iEdge] * r_areaCell * dvEdge[iEdge] * eocs[i] * invDcE[iEdge];
+            int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
+            tte -= edge_sign * (dth[(size_t)cell2 * LP + k] - dth[(size_t)cell1 * LP + k]);
+        }
+    }
+    // wdtz (:1406-1420, Q15 literal order); level L read from the never-written field
+    const double *rws_f = fd(S, F_rw_save), *tms_f = fd(S, F_theta_m_save);
+    const double rws = col_rd(rws_f, c, k, L, LP);
+    const double tms = col_rd(tms_f, c, k, L, LP), tmv = col_rd(tm, c, k, L, LP);
+    const double tms_m = lvl_dn<LP>(tms, k), tm_m = lvl_dn<LP>(tmv, k);
+    double wdtz = 0.0;
+    if (k > 0 && k < L - 1) wdtz = ((rws - rw) * (fzm * tms + fzp * tms_m));
+    if (k == 1) wdtz += rw * (fzm * tmv + fzp * tm_m);
+    if (k == L - 1) wdtz = rws * (fzm * tms + fzp * tms_m);
+    if (k == L) wdtz = fd(S, F_wdtz)[p];
+    const double wdtz_p = lvl_up<LP>(wdtz, k);
+    if (k >= L) return;
+    // :1422-1427, :1477-1479
+    const double rho_zz = fd(S, F_rho_zz)[p];
+    tend_theta *= invA - rdzw * (wdtz_p - wdtz);
+    fw(S, F_tend_rtheta_adv)[p] = tend_theta;
+    fw(S, F_rthdynten)[p] = tend_theta / rho_zz;
+    tend_theta += rho_zz * fd(S, F_rt_diabatic_tend)[p];
+    tend_theta += tte + fd(S, F_tend_rtheta_physics)[p];
+    fw(S, F_tend_theta)[p] = tend_theta;
+    if (rk0) fw(S, F_tend_theta_euler)[p] = tte;
+}
+
+template <int LP>
+static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& in) {
+    constexpr int COLS = ColMap<LP>::COLS;
+    DynK a;
+    a.rk_step = in.rk_step;
+    a.horiz_mixing = in.horiz_mixing;
+    a.rayleigh = in.rayleigh_damp_u;
+    a.exact_q = in.exact_q;
+    const double invDt = 1.0 / in.dt;
+    const double c_s = kSmagCoef;
+    a.cs_l2 = (c_s * kLenDisp) * (c_s * kLenDisp);
+    a.cap = (0.01 * (kLenDisp * kLenDisp)) * invDt;
+    a.cam_coef = in.cam_coef;
+    a.h4 = (in.rk_step == 0 && in.horiz_mixing == 0) ? kVisc4_2dsmag * (kLenDisp * kLenDisp * kLenDisp) : 0.0;
+    a.r_earth = kSphereRadius;
+    a.inv_r_earth = 1.0 / a.r_earth;
+    a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
+    a.prandtl_inv = 1.0 / kPrandtl;
+    const int nCB = (S.nCells + COLS - 1) / COLS, nEB = (S.nEdges + COLS - 1) / COLS, nVB = (S.nVertices + COLS - 1) / COLS;
+    k_dyn_A<LP><<<nCB, 256, 0, st>>>(S, a);
+    k_dyn_B<LP><<<nEB, 256, 0, st>>>(S, a);
+    if (a.rk_step == 0) {
+        k_dyn_C<LP><<<(a.h4 > 0.0 ? nVB : 0) + nCB, 256, 0, st>>>(S, a, a.h4 > 0.0 ? nVB : 0);
+        if (a.h4 > 0.0) k_dyn_D<LP><<<nEB, 256, 0, st>>>(S, a);
+    }
+    k_dyn_E<LP><<<nCB, 256, 0, st>>>(S, a);
+    return hipGetLastError();
+}
+hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& in) {
+    MPAS_LP_DISPATCH(S.LP, dyn_lp, S, st, in);
+}
+
+}  // namespace mpas

@@ -1,0 +1,295 @@
+// k_misc.hip -- column-local and streaming tasks of the RK3 step (gfx950):
+//   atm_rk_integration_setup        dynamics_tasks.rg:747-778
+//   atm_compute_moist_coefficients  dynamics_tasks.rg:460-502
+//   atm_compute_vert_imp_coefs      dynamics_tasks.rg:513-592
+//   atm_set_smlstep_pert_variables  dynamics_tasks.rg:1503-1528
+//   atm_divergence_damping_3d       dynamics_tasks.rg:1726-1763
+//   atm_rk_dynamics_substep_finish  dynamics_tasks.rg:1951-2007
+//   synthetic-state fill (mpas_synth.h, identical to the oracle's generator)
+// All are HBM-streaming (fp64, no MFMA).  Expressions are written in the Regent
+// operand order and the library is built with -ffp-contract=off, so results are
+// bit-identical to the oracle's.
+#include "mpas_dev.h"
+#include "mpas_synth.h"
+
+namespace mpas {
+
+// ---------------------------------------------------------------- setup
+__global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
+    const size_t n = (size_t)S.nCells * S.LP;
+    const double *rw = fd(S, F_rw), *rtp = fd(S, F_rtheta_p), *rp = fd(S, F_rho_p), *w = fd(S, F_w);
+    const double *tm = fd(S, F_theta_m), *rz = fd(S, F_rho_zz);
+    double *rws = fw(S, F_rw_save), *rtps = fw(S, F_rtheta_p_save), *rps = fw(S, F_rho_p_save);
+    double *w2 = fw(S, F_w_2), *tm2 = fw(S, F_theta_m_2), *rz2 = fw(S, F_rho_zz_2), *rzo = fw(S, F_rho_zz_old_split);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        if ((int)(i % S.LP) >= S.L) continue;
+        rws[i] = rw[i];
+        rtps[i] = rtp[i];
+        rps[i] = rp[i];
+        w2[i] = w[i];
+        tm2[i] = tm[i];
+        double r = rz[i];
+        rz2[i] = r;
+        rzo[i] = r;
+    }
+}
+__global__ __launch_bounds__(256) void k_setup_edges(DevState S) {
+    const size_t n = (size_t)S.nEdges * S.LP;
+    const double *ru = fd(S, F_ru), *u = fd(S, F_u);
+    double *rus = fw(S, F_ru_save), *u2 = fw(S, F_u_2);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        if ((int)(i % S.LP) >= S.L) continue;
+        rus[i] = ru[i];
+        u2[i] = u[i];
+    }
+}
+static int stream_grid(size_t n) {
+    size_t g = (n + 255) / 256;
+    return (int)(g < 8192 ? (g ? g : 1) : 8192);
+}
+hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st) {
+    k_setup_edges<<<stream_grid((size_t)S.nEdges * S.LP), 256, 0, st>>>(S);
+    k_setup_cells<<<stream_grid((size_t)S.nCells * S.LP), 256, 0, st>>>(S);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- moist
+__global__ __launch_bounds__(256) void k_moist(DevState S) {
+    const size_t n = (size_t)S.nCells * S.LP;
+    double *qtot = fw(S, F_qtot), *cqw = fw(S, F_cqw);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        int k = (int)(i % S.LP);
+        if (k >= S.L) continue;
+        qtot[i] = 0.0;  // :473-482
+        if (k > 0) {    // :484-489, qtot(k) and qtot(k-1) were both just zeroed
+            double q_k = 0.0, q_km1 = 0.0;
+            double qtotal = 0.5 * (q_k + q_km1);
+            cqw[i] = 1.0 / (1.0 + qtotal);
+        }
+    }
+}
+hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
+    k_moist<<<stream_grid((size_t)S.nCells * S.LP), 256, 0, st>>>(S);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- vert_imp
+template <int LP>
+__global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCells) return;
+    const size_t p = (size_t)c * LP + k;
+    const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
+    const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
+    const double rdzw_m = k > 0 ? rdzw_a[k - 1] : 0.0;
+    const double zz = fd(S, F_zz)[p], exner = fd(S, F_exner)[p], tm = fd(S, F_theta_m)[p];
+    const double cqw = fd(S, F_cqw)[p], qtot = fd(S, F_qtot)[p];
+    const double rb = fd(S, F_rho_base)[p], rtb = fd(S, F_rtheta_base)[p], rtp = fd(S, F_rtheta_p)[p];
+    const double exb = fd(S, F_exner_base)[p];
+    const double gamma_old = fd(S, F_gamma_tri)[p];
+    const double coftz_old = fd(S, F_coftz)[p];  // level L keeps its (never written) value
+    const double zz_m = lvl_dn<LP>(zz, k), exner_m = lvl_dn<LP>(exner, k), tm_m = lvl_dn<LP>(tm, k);
+
+    // :550-564
+    double cofwr = 0.0, cofwz = 0.0, coftz = coftz_old, cofwt = 0.0;
+    if (k < L) {
+        if (k > 0) cofwr = .5 * dtseps * kGravity * (fzm * zz + fzp * zz_m);
+        coftz = 0.0;
+        if (k > 0) {
+            cofwz = dtseps * c2 * (fzm * zz + fzp * zz_m) * rdzu * cqw * (fzm * exner + fzp * exner_m);
+            coftz = dtseps * (fzm * tm + fzp * tm_m);
+        }
+        double qtotal = qtot;
+        cofwt = .5 * dtseps * rcv * zz * kGravity * rb / (1.0 + qtotal) * exner / ((rtb + rtp) * exb);
+    }
+    const double coftz_m = lvl_dn<LP>(coftz, k), coftz_p = lvl_up<LP>(coftz, k);
+    const double cofwt_m = lvl_dn<LP>(cofwt, k);
+    const double gamma_m = (k == 1) ? 0.0 : lvl_dn<LP>(gamma_old, k);  // Q17
+    const double cofrz = dtseps * rdzw, cofrz_m = dtseps * rdzw_m;      // :537-539
+
+    if (k < L) {
+        double* o;
+        fw(S, F_coftz)[p] = coftz;
+        fw(S, F_cofwt)[p] = cofwt;
+        if (k == 0) {
+            fw(S, F_gamma_tri)[p] = 0.0;
+        } else {
+            fw(S, F_cofwr)[p] = cofwr;
+            fw(S, F_cofwz)[p] = cofwz;
+            // :566-578 (Q16 literal)
+            double a = -1.0 * cofwz * coftz_m * rdzw_m * zz_m + cofwr * cofrz_m - cofwt_m * coftz_m * rdzw_m;
+            double b = 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) - coftz * (cofwt * rdzw - cofwt * rdzw_m) +
+                       cofwr * ((cofrz - cofrz_m));
+            double cc = -1.0 * cofwz * coftz_p * rdzw * zz - cofwr * cofrz + cofwt * coftz_p * rdzw;
+            double alpha = 1.0 / (b - a * gamma_m);  // :580-585
+            double gamma = cc * alpha;               // :587-591
+            o = fw(S, F_a_tri); o[p] = a;
+            o = fw(S, F_b_tri); o[p] = b;
+            o = fw(S, F_c_tri); o[p] = cc;
+            o = fw(S, F_alpha_tri); o[p] = alpha;
+            o = fw(S, F_gamma_tri); o[p] = gamma;
+        }
+        if (c == 0) fw(S, F_cofrz)[k] = cofrz;
+    }
+}
+template <int LP>
+static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
+    double dtseps = .5 * dts * (1.0 + kEpssm);
+    double rcv = kRgas / (kCp - kRgas);
+    double c2 = kCp * rcv;
+    int grid = (S.nCells + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    k_vert_imp<LP><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
+    return hipGetLastError();
+}
+hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts) {
+    MPAS_LP_DISPATCH(S.LP, vert_imp_lp, S, st, dts);
+}
+
+// ---------------------------------------------------------------- set_smlstep
+template <int LP>
+__global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCells) return;
+    const size_t p = (size_t)c * LP + k;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgn = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+    const double* ut_f = fd(S, F_u_tend);
+    const double* zb = fd(S, F_zb_cell);
+    const double* zb3 = fd(S, F_zb3_cell);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    const double zz = col_rd(fd(S, F_zz), c, k, L, LP);
+    const double zz_m = lvl_dn<LP>(zz, k);
+    double w = col_rd(fd(S, F_w), c, k, L, LP);
+    for (int i = 0; i < ne; i++) {
+        int iEdge = eoc[i];
+        double ut = col_rd(ut_f, iEdge, k, L, LP);
+        double ut_m = lvl_dn<LP>(ut, k);
+        double flux = sgn[i] * (fzm * ut + fzp * ut_m);
+        size_t q = ((size_t)c * 10 + i) * LP + k;
+        w -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+    }
+    w *= (fzm * zz + fzp * zz_m);
+    if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) fw(S, F_w)[p] = w;
+}
+template <int LP>
+static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
+    int grid = (S.nCells + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    k_set_smlstep<LP><<<grid, 256, 0, st>>>(S);
+    return hipGetLastError();
+}
+hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st); }
+
+// ---------------------------------------------------------------- divergence damping
+template <int LP>
+__global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
+    ColMap<LP> m;
+    const int L = S.L, k = m.k, e = m.ent;
+    if (e >= S.nEdges || k >= L) return;
+    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    const int* sh = fi(S, F_isShared);
+    if (sh[cell1] && sh[cell2]) return;
+    const double *rtp = fd(S, F_rtheta_pp), *rtpo = fd(S, F_rtheta_pp_old), *tm = fd(S, F_theta_m);
+    const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
+    double divCell1 = -(rtp[p1] - rtpo[p1]);
+    double divCell2 = -(rtp[p2] - rtpo[p2]);
+    double* rup = fw(S, F_ru_p);
+    const size_t p = (size_t)e * LP + k;
+    rup[p] += coef_divdamp * (divCell2 - divCell1) * (1.0 - fd(S, F_specZoneMaskEdge)[e]) / (tm[p1] + tm[p2]);
+}
+template <int LP>
+static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
+    double smdiv = kSmdiv;
+    double rdts = 1.0 / dts;
+    double coef_divdamp = 2.0 * smdiv * kLenDisp * rdts;
+    int grid = (S.nEdges + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    k_div_damp<LP><<<grid, 256, 0, st>>>(S, coef_divdamp);
+    return hipGetLastError();
+}
+hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts) {
+    MPAS_LP_DISPATCH(S.LP, divdamp_lp, S, st, dts);
+}
+
+// ---------------------------------------------------------------- substep finish
+__global__ __launch_bounds__(256) void k_finish_edges(DevState S, int substep, int split, double inv_split) {
+    const size_t n = (size_t)S.nEdges * S.LP;
+    double *ru_save = fw(S, F_ru_save), *u = fw(S, F_u), *ruAvg = fw(S, F_ruAvg), *ruAvgS = fw(S, F_ruAvg_split);
+    const double *ru = fd(S, F_ru), *u2 = fd(S, F_u_2);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        if ((int)(i % S.LP) >= S.L) continue;
+        if (substep < split) {
+            ru_save[i] = ru[i];
+            u[i] = u2[i];
+        }
+        double s = (substep == 1) ? ruAvg[i] : ruAvg[i] + ruAvgS[i];
+        ruAvgS[i] = s;
+        if (substep == split) ruAvg[i] = s * inv_split;
+    }
+}
+__global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, int split, double inv_split) {
+    const size_t n = (size_t)S.nCells * S.LP;
+    double *wwAvg = fw(S, F_wwAvg), *wwAvgS = fw(S, F_wwAvg_split), *rho_zz = fw(S, F_rho_zz);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        if ((int)(i % S.LP) >= S.L) continue;
+        if (substep < split) {
+            fw(S, F_rw_save)[i] = fd(S, F_rw)[i];
+            fw(S, F_rtheta_p_save)[i] = fd(S, F_rtheta_p)[i];
+            fw(S, F_rho_p_save)[i] = fd(S, F_rho_p)[i];
+            fw(S, F_w)[i] = fd(S, F_w_2)[i];
+            fw(S, F_theta_m)[i] = fd(S, F_theta_m_2)[i];
+            rho_zz[i] = fd(S, F_rho_zz_2)[i];
+        }
+        double s = (substep == 1) ? wwAvg[i] : wwAvg[i] + wwAvgS[i];
+        wwAvgS[i] = s;
+        if (substep == split) {
+            wwAvg[i] = s * inv_split;
+            rho_zz[i] = fd(S, F_rho_zz_old_split)[i];
+        }
+    }
+}
+hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split) {
+    double inv = 1.0 / (double)split;
+    k_finish_edges<<<stream_grid((size_t)S.nEdges * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    k_finish_cells<<<stream_grid((size_t)S.nCells * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- synthetic fill
+__global__ __launch_bounds__(256) void k_fill(void* dst, int fid, int kind, long n, int W, int levels, int LP,
+                                              int dist, double lo, double hi, uint64_t seed) {
+    double* d = (double*)dst;
+    const size_t total = (size_t)n * W * levels;
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+        int k = (int)(t % levels);
+        size_t r = t / levels;
+        int i = (int)(r % W);
+        long e = (long)(r / W);
+        double v = mpas_synth_value(seed, (uint32_t)fid, (uint64_t)e, (uint32_t)k, (uint32_t)i, dist, lo, hi);
+        if (kind == K_ZV) d[k] = v;
+        else if (kind == K_C3V) d[((size_t)e * W + i) * LP + k] = v;
+        else d[(size_t)e * LP + k] = v;
+    }
+}
+hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed) {
+    for (int f = 0; f < F_COUNT; f++) {
+        const FieldInfo& fi_ = kFields[f];
+        if (fi_.dist == D_M) continue;
+        long n = 0;
+        int W = 1;
+        switch (fi_.kind) {
+            case K_C3: n = S.nCells; break;
+            case K_E3: n = S.nEdges; break;
+            case K_V3: n = S.nVertices; break;
+            case K_C3V: n = S.nCells; W = fi_.width; break;
+            case K_ZV: n = 1; break;
+            default: continue;
+        }
+        size_t total = (size_t)n * W * (S.L + 1);
+        k_fill<<<stream_grid(total), 256, 0, st>>>(S.f[f], f, fi_.kind, n, W, S.L + 1, S.LP, fi_.dist, fi_.lo, fi_.hi, seed);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace mpas

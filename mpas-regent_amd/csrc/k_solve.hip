@@ -1,0 +1,137 @@
+// k_solve.hip -- atm_compute_solve_diagnostics (dynamics_tasks.rg:328-454) for gfx950.
+//
+// Two launches instead of the reference's five loop nests:
+//   1. vertices + cells in one grid: vorticity, pv_vertex (vertex columns);
+//      divergence (Q9 literal "s + u"), ke (cell columns; ke_edge of each edge of the
+//      cell is recomputed from u with the edge loop's exact expression, so no
+//      edge->cell barrier is needed)
+//   2. edges: h_edge, ke_edge, v (only rk_step in {-1, 2}, Q23 starts at i = 1), pv_edge
+// Hollingsworth (never true on the path, rk_timestep.rg:467) adds a ke_vertex pass.
+#include "mpas_dev.h"
+
+namespace mpas {
+
+template <int LP>
+__global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int hollingsworth_part) {
+    const int L = S.L;
+    const double* u = fd(S, F_u);
+    const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
+    if ((int)blockIdx.x < nVB) {
+        ColMap<LP> m;
+        const int v = m.ent, k = m.k;
+        if (v >= S.nVertices || k >= L) return;
+        const int* eov = fi(S, F_edgesOnVertex) + (size_t)v * 3;
+        const double* sgn = fd(S, F_edgesOnVertexSign) + (size_t)v * 3;
+        double vort = 0.0;
+        for (int i = 0; i < 3; i++) {
+            int iEdge = eov[i];
+            double s = sgn[i] * dcEdge[iEdge];
+            vort += s * u[(size_t)iEdge * LP + k];
+        }
+        vort *= fd(S, F_invAreaTriangle)[v];
+        const size_t p = (size_t)v * LP + k;
+        fw(S, F_vorticity)[p] = vort;
+        fw(S, F_pv_vertex)[p] = fd(S, F_fVertex)[v] + vort;
+        if (hollingsworth_part) {
+            const double* ke_edge_unused = nullptr;
+            (void)ke_edge_unused;
+            double r = 0.25 * fd(S, F_invAreaTriangle)[v];
+            double kes[3];
+            for (int i = 0; i < 3; i++) {
+                int iEdge = eov[i];
+                double efac = dcEdge[iEdge] * dvEdge[iEdge];
+                double uu = u[(size_t)iEdge * LP + k];
+                kes[i] = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
+            }
+            fw(S, F_ke_vertex)[p] = (kes[0] + kes[1] + kes[2]) * r;
+        }
+        return;
+    }
+    ColMap<LP> m0;
+    const int c = (int)(blockIdx.x - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
+    const int k = m0.k;
+    if (c >= S.nCells || k >= L) return;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
+    const double invA = fd(S, F_invAreaCell)[c];
+    double div = 0.0, ke = 0.0;
+    for (int i = 0; i < ne; i++) {
+        int iEdge = eoc[i];
+        double uu = u[(size_t)iEdge * LP + k];
+        double s = sgn[i] * dvEdge[iEdge];
+        div += s + uu;
+        // ke_edge(iEdge,k) exactly as the edge loop (:352) writes it; the zero slot
+        // row of ke_edge is never written, and its recomputation is 0*0*0 as well
+        double efac = dcEdge[iEdge] * dvEdge[iEdge];
+        double kee = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
+        ke += 0.25 * kee;
+    }
+    div *= invA;
+    ke *= invA;
+    const size_t p = (size_t)c * LP + k;
+    fw(S, F_divergence)[p] = div;
+    fw(S, F_ke)[p] = ke;
+}
+
+// hollingsworth second half (:405-417): cells, needs ke_vertex of the whole mesh
+template <int LP>
+__global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
+    ColMap<LP> m;
+    const int L = S.L, c = m.ent, k = m.k;
+    if (c >= S.nCells || k >= L) return;
+    const size_t p = (size_t)c * LP + k;
+    double ke_fact = 1.0 - 0.375;
+    double ke = fd(S, F_ke)[p] * ke_fact;
+    double r = fd(S, F_invAreaCell)[c];
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    for (int i = 0; i < ne; i++) {
+        int iVertex = fi(S, F_verticesOnCell)[(size_t)c * 10 + i];
+        int j = fi(S, F_kiteForCell)[(size_t)c * 10 + i];
+        double kite = (j >= 0 && j < 3) ? fd(S, F_kiteAreasOnVertex)[(size_t)iVertex * 3 + j] : 0.0;
+        ke += (1.0 - ke_fact) * kite * fd(S, F_ke_vertex)[(size_t)iVertex * LP + k] * r;
+    }
+    fw(S, F_ke)[p] = ke;
+}
+
+template <int LP>
+__global__ __launch_bounds__(256) void k_solve_e(DevState S, int reconstruct_v) {
+    ColMap<LP> m;
+    const int L = S.L, e = m.ent, k = m.k;
+    if (e >= S.nEdges || k >= L) return;
+    const size_t p = (size_t)e * LP + k;
+    const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
+    const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
+    const double* h = fd(S, F_h);
+    const double* u = fd(S, F_u);
+    fw(S, F_h_edge)[p] = 0.5 * (h[(size_t)coe[0] * LP + k] + h[(size_t)coe[1] * LP + k]);
+    double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
+    double uu = u[p];
+    fw(S, F_ke_edge)[p] = efac * (uu * uu);
+    if (reconstruct_v) {
+        const int neoe = fi(S, F_nEdgesOnEdge)[e];
+        const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
+        const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
+        double v = 0;
+        for (int i = 1; i < neoe; i++) v += wts[i] * u[(size_t)eoe[i] * LP + k];
+        fw(S, F_v)[p] = v;
+    }
+    const double* pvv = fd(S, F_pv_vertex);
+    fw(S, F_pv_edge)[p] = 0.5 * (pvv[(size_t)voe[0] * LP + k] + pvv[(size_t)voe[1] * LP + k]);
+}
+
+template <int LP>
+static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
+    constexpr int COLS = ColMap<LP>::COLS;
+    int nVB = (S.nVertices + COLS - 1) / COLS, nCB = (S.nCells + COLS - 1) / COLS, nEB = (S.nEdges + COLS - 1) / COLS;
+    k_solve_vc<LP><<<nVB + nCB, 256, 0, st>>>(S, nVB, hollingsworth);
+    if (hollingsworth) k_solve_holl<LP><<<nCB, 256, 0, st>>>(S);
+    int reconstruct_v = (rk_step != -1 && rk_step != 2) ? 0 : 1;
+    k_solve_e<LP><<<nEB, 256, 0, st>>>(S, reconstruct_v);
+    return hipGetLastError();
+}
+hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
+    MPAS_LP_DISPATCH(S.LP, solve_lp, S, st, hollingsworth, rk_step);
+}
+
+}  // namespace mpas

@@ -1,0 +1,488 @@
+// mpas_ctx.cpp -- libmpasdyn host runtime: context, device residency, the C-ABI task
+// entry points of include/mpas_dyn.h, and the atm_srk3 driver (rk_timestep.rg:361-500).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "mpas_dev.h"
+#include "mpas_dyn.h"
+
+namespace mpas {
+const FieldInfo kFields[X_COUNT] = {
+#define MPAS_FIELD(name, KIND, W, DIST, LO, HI) {#name, K_##KIND, W, D_##DIST, LO, HI},
+#include "mpas_fields.def"
+#undef MPAS_FIELD
+    {"cosAngleEdge", K_E2F, 1, D_M, 0, 0},
+    {"cosLatEdge", K_E2F, 1, D_M, 0, 0},
+    {"cosLatCell", K_C2F, 1, D_M, 0, 0},
+    {"wc", K_C3, 1, D_M, 0, 0},
+};
+}  // namespace mpas
+
+using namespace mpas;
+
+struct TimedCall {
+    int task;
+    hipEvent_t e0, e1;
+};
+
+struct mpas_ctx {
+    int device = 0;
+    mpas_dims dims{};
+    DevState S{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    int exact = 0;
+    bool timing = false;
+    std::vector<std::string> task_names;
+    std::vector<int64_t> task_calls;
+    std::vector<double> task_ms;
+    std::vector<TimedCall> pending;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+struct Fail {
+    int code;
+    std::string msg;
+};
+
+void hipcheck(hipError_t e, const char* what) {
+    if (e != hipSuccess) throw Fail{MPAS_EHIP, std::string(what) + ": " + hipGetErrorString(e)};
+}
+
+int entity_count(const mpas_ctx* c, int kind) {
+    switch (kind) {
+        case K_C3: case K_C3V: case K_C2F: case K_C2I: case K_C3B: return c->dims.nCells;
+        case K_E3: case K_E2F: case K_E2I: return c->dims.nEdges;
+        case K_V3: case K_V2F: case K_V2I: return c->dims.nVertices;
+        default: return 1;
+    }
+}
+size_t elem_size(int kind) {
+    if (kind == K_C2I || kind == K_E2I || kind == K_V2I) return 4;
+    if (kind == K_C3B) return 1;
+    return 8;
+}
+// bytes of one device array (entity rows include the zero slot)
+size_t dev_bytes(const mpas_ctx* c, int f) {
+    const FieldInfo& fi = kFields[f];
+    const size_t LP = c->S.LP;
+    size_t rows = (size_t)entity_count(c, fi.kind) + 1;
+    switch (fi.kind) {
+        case K_C3: case K_E3: case K_V3: return rows * LP * 8;
+        case K_C3V: return rows * fi.width * LP * 8;
+        case K_C3B: return rows * LP;
+        case K_ZV: return LP * 8;
+        default: return rows * fi.width * elem_size(fi.kind);
+    }
+}
+// entity kind an integer field refers to (for the Q1 clamp), -1 if it is not an id
+int id_target(int f) {
+    switch (f) {
+        case F_edgesOnCell: case F_edgesOnEdge: case F_edgesOnEdge_ECP: case F_edgesOnVertex: return K_E3;
+        case F_cellsOnEdge: case F_advCellsForEdge: return K_C3;
+        case F_verticesOnEdge: case F_verticesOnCell: return K_V3;
+        default: return -1;
+    }
+}
+
+int task_index(mpas_ctx* c, const char* name) {
+    for (size_t i = 0; i < c->task_names.size(); i++)
+        if (c->task_names[i] == name) return (int)i;
+    c->task_names.push_back(name);
+    c->task_calls.push_back(0);
+    c->task_ms.push_back(0.0);
+    return (int)c->task_names.size() - 1;
+}
+
+hipEvent_t get_event(mpas_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipcheck(hipEventCreate(&e), "hipEventCreate");
+    return e;
+}
+
+void harvest(mpas_ctx* c) {
+    for (auto& t : c->pending) {
+        hipcheck(hipEventSynchronize(t.e1), "hipEventSynchronize");
+        float ms = 0.f;
+        hipcheck(hipEventElapsedTime(&ms, t.e0, t.e1), "hipEventElapsedTime");
+        c->task_calls[t.task] += 1;
+        c->task_ms[t.task] += ms;
+        c->event_pool.push_back(t.e0);
+        c->event_pool.push_back(t.e1);
+    }
+    c->pending.clear();
+}
+
+// run a task launcher, bracketed by events when timing is on
+template <class Fn>
+void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    int ti = -1;
+    if (c->timing) {
+        ti = task_index(c, name);
+        e0 = get_event(c);
+        e1 = get_event(c);
+        hipcheck(hipEventRecord(e0, c->stream), "hipEventRecord");
+    }
+    hipError_t e = fn();
+    if (e != hipSuccess) throw Fail{MPAS_EHIP, std::string(name) + ": " + hipGetErrorString(e)};
+    if (c->timing) {
+        hipcheck(hipEventRecord(e1, c->stream), "hipEventRecord");
+        c->pending.push_back({ti, e0, e1});
+        if (c->pending.size() > 4096) harvest(c);
+    }
+}
+
+template <class Fn>
+int guarded(mpas_ctx* c, Fn&& fn) {
+    if (!c) return MPAS_EINVAL;
+    try {
+        fn();
+        return MPAS_OK;
+    } catch (const Fail& f) {
+        c->err = f.msg;
+        return f.code;
+    } catch (const std::bad_alloc&) {
+        c->err = "out of host memory";
+        return MPAS_ENOMEM;
+    } catch (const std::exception& ex) {
+        c->err = ex.what();
+        return MPAS_EINVAL;
+    } catch (...) {
+        c->err = "unknown error";
+        return MPAS_EINVAL;
+    }
+}
+
+void srk3(mpas_ctx* c, double dt, int schedule) {
+    // rk_timestep.rg:378-399
+    const int number_of_sub_steps = 2;
+    const int dynamics_split = 1;  // constants.rg:62
+    const double dt_dynamics = dt;
+    const double rk_sub_timestep[3] = {dt_dynamics / 3, dt_dynamics / number_of_sub_steps,
+                                       dt_dynamics / number_of_sub_steps};
+    int number_sub_steps[3];
+    number_sub_steps[0] = (number_of_sub_steps / 2 > 1) ? number_of_sub_steps / 2 : 1;
+    number_sub_steps[1] = number_sub_steps[0];
+    number_sub_steps[2] = number_of_sub_steps;
+    const DevState& S = c->S;
+    hipStream_t st = c->stream;
+    run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
+    run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
+    run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
+    for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
+        if (rk_step == 1)
+            run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
+        DynTendArgs a{};
+        a.rk_step = schedule == 0 ? (int)rk_sub_timestep[rk_step] : rk_step;  // Q4
+        a.dt = dt;
+        a.horiz_mixing = 0;  // constants.rg:57 "2d_smagorinsky"
+        a.cam_coef = 0.0;
+        a.mix_full = 0;
+        a.rayleigh_damp_u = 0;
+        a.exact_q = c->exact;
+        run_task(c, a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]",
+                 [&] { return launch_dyn_tend(S, st, a); });
+        run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
+        for (int small_step = 0; small_step < number_sub_steps[rk_step] + 1; small_step++) {  // Q5
+            run_task(c, "atm_advance_acoustic_step_work",
+                     [&] { return launch_acoustic(S, st, rk_sub_timestep[rk_step], small_step, c->exact); });
+            run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, rk_sub_timestep[rk_step]); });
+        }
+        run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
+    }
+    run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpas_field_count(void) { return F_COUNT; }
+int mpas_field_id(const char* name) {
+    if (!name) return MPAS_EINVAL;
+    for (int f = 0; f < F_COUNT; f++)
+        if (std::strcmp(kFields[f].name, name) == 0) return f;
+    return MPAS_EINVAL;
+}
+const char* mpas_field_name(int f) { return (f >= 0 && f < F_COUNT) ? kFields[f].name : nullptr; }
+int mpas_field_kind(int f) { return (f >= 0 && f < F_COUNT) ? kFields[f].kind : MPAS_EINVAL; }
+int mpas_field_width(int f) { return (f >= 0 && f < F_COUNT) ? kFields[f].width : MPAS_EINVAL; }
+
+static thread_local std::string g_create_err;
+
+int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
+    if (!out || !dims) return MPAS_EINVAL;
+    *out = nullptr;
+    if (dims->nCells <= 0 || dims->nEdges <= 0 || dims->nVertices <= 0 || dims->nVertLevels < 2 ||
+        dims->nVertLevels + 1 > 64)
+        return MPAS_EINVAL;
+    mpas_ctx* c = new (std::nothrow) mpas_ctx();
+    if (!c) return MPAS_ENOMEM;
+    int rc = guarded(c, [&] {
+        int n = 0;
+        hipcheck(hipGetDeviceCount(&n), "hipGetDeviceCount");
+        if (device < 0 || device >= n) throw Fail{MPAS_EINVAL, "no such HIP device"};
+        hipcheck(hipSetDevice(device), "hipSetDevice");
+        hipDeviceProp_t prop;
+        hipcheck(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            throw Fail{MPAS_ENOTSUP, std::string("libmpasdyn is built for gfx950, device is ") + prop.gcnArchName};
+        c->device = device;
+        c->dims = *dims;
+        int LP = 8;
+        while (LP < dims->nVertLevels + 1) LP <<= 1;
+        c->S.nCells = dims->nCells;
+        c->S.nEdges = dims->nEdges;
+        c->S.nVertices = dims->nVertices;
+        c->S.L = dims->nVertLevels;
+        c->S.LP = LP;
+        hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+        for (int f = 0; f < X_COUNT; f++) {
+            size_t b = dev_bytes(c, f);
+            void* p = nullptr;
+            hipError_t e = hipMalloc(&p, b);
+            if (e != hipSuccess) throw Fail{MPAS_ENOMEM, std::string("hipMalloc ") + kFields[f].name};
+            hipcheck(hipMemset(p, 0, b), "hipMemset");
+            c->S.f[f] = p;
+        }
+        hipcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    });
+    if (rc != MPAS_OK) {
+        g_create_err = c->err;
+        fprintf(stderr, "mpas_ctx_create: %s\n", c->err.c_str());
+        mpas_ctx_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return MPAS_OK;
+}
+
+int mpas_ctx_destroy(mpas_ctx* c) {
+    if (!c) return MPAS_EINVAL;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (int f = 0; f < X_COUNT; f++)
+        if (c->S.f[f]) (void)hipFree(c->S.f[f]);
+    for (auto& t : c->pending) {
+        (void)hipEventDestroy(t.e0);
+        (void)hipEventDestroy(t.e1);
+    }
+    for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return MPAS_OK;
+}
+
+const char* mpas_last_error(const mpas_ctx* c) { return c ? c->err.c_str() : g_create_err.c_str(); }
+
+int mpas_sync(mpas_ctx* c) {
+    return guarded(c, [&] {
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    });
+}
+
+int mpas_get_stream(mpas_ctx* c, void** stream) {
+    if (!c || !stream) return MPAS_EINVAL;
+    *stream = (void*)c->stream;
+    return MPAS_OK;
+}
+
+int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
+    return guarded(c, [&] {
+        if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
+        else throw Fail{MPAS_EINVAL, std::string("unknown option ") + (name ? name : "(null)")};
+    });
+}
+
+int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, int64_t sc) {
+    return guarded(c, [&] {
+        if (f < 0 || f >= F_COUNT || !host) throw Fail{MPAS_EINVAL, "mpas_upload: bad field or pointer"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+        const FieldInfo& fi = kFields[f];
+        const int n = entity_count(c, fi.kind), L = c->S.L, LP = c->S.LP, W = fi.width;
+        const char* h = (const char*)host;
+        size_t bytes = dev_bytes(c, f);
+        std::vector<char> buf(bytes, 0);
+        if (fi.kind == K_C3 || fi.kind == K_E3 || fi.kind == K_V3) {
+            double* d = (double*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int k = 0; k <= L; k++) d[(size_t)e * LP + k] = *(const double*)(h + e * se + k * sl);
+        } else if (fi.kind == K_C3V) {
+            double* d = (double*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int i = 0; i < W; i++)
+                    for (int k = 0; k <= L; k++)
+                        d[((size_t)e * W + i) * LP + k] = *(const double*)(h + e * se + k * sl + i * sc);
+        } else if (fi.kind == K_C3B) {
+            uint8_t* d = (uint8_t*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int k = 0; k <= L; k++) d[(size_t)e * LP + k] = *(const uint8_t*)(h + e * se + k * sl);
+        } else if (fi.kind == K_ZV) {
+            double* d = (double*)buf.data();
+            for (int k = 0; k <= L; k++) d[k] = *(const double*)(h + k * sl);
+        } else if (elem_size(fi.kind) == 4) {
+            int32_t* d = (int32_t*)buf.data();
+            int tgt = id_target(f);
+            int lim = tgt < 0 ? 0 : entity_count(c, tgt);
+            for (int e = 0; e < n; e++)
+                for (int i = 0; i < W; i++) {
+                    int32_t v = *(const int32_t*)(h + e * se + i * sc);
+                    if (tgt >= 0 && (v < 0 || v > lim)) v = lim;  // Q1 zero slot
+                    d[(size_t)e * W + i] = v;
+                }
+        } else {
+            double* d = (double*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int i = 0; i < W; i++) d[(size_t)e * W + i] = *(const double*)(h + e * se + i * sc);
+        }
+        hipcheck(hipMemcpy(c->S.f[f], buf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+        // derived mesh arrays: cos() on the host with the same libm as the oracle
+        int derived = -1;
+        if (f == F_angleEdge) derived = X_cosAngleEdge;
+        if (f == F_latEdge) derived = X_cosLatEdge;
+        if (f == F_lat) derived = X_cosLatCell;
+        if (derived >= 0) {
+            std::vector<double> cs((size_t)n + 1, 0.0);
+            const double* d = (const double*)buf.data();
+            for (int e = 0; e < n; e++) cs[e] = std::cos(d[e]);
+            cs[n] = std::cos(0.0);  // zero slot: cos(0) as the oracle computes from its zero row
+            hipcheck(hipMemcpy(c->S.f[derived], cs.data(), cs.size() * 8, hipMemcpyHostToDevice), "hipMemcpy H2D");
+        }
+    });
+}
+
+int mpas_download(mpas_ctx* c, int f, void* host, int64_t se, int64_t sl, int64_t sc) {
+    return guarded(c, [&] {
+        if (f < 0 || f >= F_COUNT || !host) throw Fail{MPAS_EINVAL, "mpas_download: bad field or pointer"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+        const FieldInfo& fi = kFields[f];
+        const int n = entity_count(c, fi.kind), L = c->S.L, LP = c->S.LP, W = fi.width;
+        size_t bytes = dev_bytes(c, f);
+        std::vector<char> buf(bytes);
+        hipcheck(hipMemcpy(buf.data(), c->S.f[f], bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+        char* h = (char*)host;
+        if (fi.kind == K_C3 || fi.kind == K_E3 || fi.kind == K_V3) {
+            const double* d = (const double*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int k = 0; k <= L; k++) *(double*)(h + e * se + k * sl) = d[(size_t)e * LP + k];
+        } else if (fi.kind == K_C3V) {
+            const double* d = (const double*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int i = 0; i < W; i++)
+                    for (int k = 0; k <= L; k++)
+                        *(double*)(h + e * se + k * sl + i * sc) = d[((size_t)e * W + i) * LP + k];
+        } else if (fi.kind == K_C3B) {
+            const uint8_t* d = (const uint8_t*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int k = 0; k <= L; k++) *(uint8_t*)(h + e * se + k * sl) = d[(size_t)e * LP + k];
+        } else if (fi.kind == K_ZV) {
+            const double* d = (const double*)buf.data();
+            for (int k = 0; k <= L; k++) *(double*)(h + k * sl) = d[k];
+        } else if (elem_size(fi.kind) == 4) {
+            const int32_t* d = (const int32_t*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int i = 0; i < W; i++) *(int32_t*)(h + e * se + i * sc) = d[(size_t)e * W + i];
+        } else {
+            const double* d = (const double*)buf.data();
+            for (int e = 0; e < n; e++)
+                for (int i = 0; i < W; i++) *(double*)(h + e * se + i * sc) = d[(size_t)e * W + i];
+        }
+    });
+}
+
+int mpas_fill_synthetic(mpas_ctx* c, uint64_t seed) {
+    return guarded(c, [&] {
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        hipcheck(launch_fill_synthetic(c->S, c->stream, seed), "fill_synthetic");
+        hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    });
+}
+
+#define MPAS_TASK(NAME, CALL) \
+    return guarded(c, [&] { run_task(c, NAME, [&] { return CALL; }); })
+
+int mpas_atm_rk_integration_setup(mpas_ctx* c) {
+    MPAS_TASK("atm_rk_integration_setup", launch_rk_integration_setup(c->S, c->stream));
+}
+int mpas_atm_compute_moist_coefficients(mpas_ctx* c) {
+    MPAS_TASK("atm_compute_moist_coefficients", launch_moist_coefficients(c->S, c->stream));
+}
+int mpas_atm_compute_vert_imp_coefs(mpas_ctx* c, double dts) {
+    MPAS_TASK("atm_compute_vert_imp_coefs", launch_vert_imp_coefs(c->S, c->stream, dts));
+}
+int mpas_atm_compute_dyn_tend_work(mpas_ctx* c, int rk_step, double dt, int horiz_mixing, double cam_coef, int mix_full,
+                                   int rayleigh_damp_u) {
+    if (!c) return MPAS_EINVAL;
+    DynTendArgs a{rk_step, dt, horiz_mixing, cam_coef, mix_full, rayleigh_damp_u, c->exact};
+    MPAS_TASK(rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]",
+              launch_dyn_tend(c->S, c->stream, a));
+}
+int mpas_atm_set_smlstep_pert_variables_work(mpas_ctx* c) {
+    MPAS_TASK("atm_set_smlstep_pert_variables_work", launch_set_smlstep(c->S, c->stream));
+}
+int mpas_atm_advance_acoustic_step_work(mpas_ctx* c, double dts, int small_step) {
+    MPAS_TASK("atm_advance_acoustic_step_work", launch_acoustic(c->S, c->stream, dts, small_step, c->exact));
+}
+int mpas_atm_divergence_damping_3d(mpas_ctx* c, double dts) {
+    MPAS_TASK("atm_divergence_damping_3d", launch_div_damping(c->S, c->stream, dts));
+}
+int mpas_atm_compute_solve_diagnostics(mpas_ctx* c, int hollingsworth, int rk_step) {
+    MPAS_TASK("atm_compute_solve_diagnostics", launch_solve_diagnostics(c->S, c->stream, hollingsworth, rk_step));
+}
+int mpas_atm_rk_dynamics_substep_finish(mpas_ctx* c, int substep, int split) {
+    if (split == 0) return MPAS_EINVAL;
+    MPAS_TASK("atm_rk_dynamics_substep_finish", launch_substep_finish(c->S, c->stream, substep, split));
+}
+
+int mpas_atm_srk3(mpas_ctx* c, double dt, int schedule) {
+    return guarded(c, [&] {
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        srk3(c, dt, schedule);
+    });
+}
+int mpas_atm_timestep(mpas_ctx* c, double dt) { return mpas_atm_srk3(c, dt, 0); }
+
+int mpas_timing_enable(mpas_ctx* c, int on) {
+    return guarded(c, [&] { c->timing = on != 0; });
+}
+int mpas_timing_reset(mpas_ctx* c) {
+    return guarded(c, [&] {
+        harvest(c);
+        for (auto& x : c->task_calls) x = 0;
+        for (auto& x : c->task_ms) x = 0.0;
+    });
+}
+int mpas_timing_count(mpas_ctx* c) {
+    if (!c) return MPAS_EINVAL;
+    int rc = guarded(c, [&] { harvest(c); });
+    return rc != MPAS_OK ? rc : (int)c->task_names.size();
+}
+int mpas_timing_get(mpas_ctx* c, int idx, const char** name, int64_t* calls, double* total_ms) {
+    return guarded(c, [&] {
+        harvest(c);
+        if (idx < 0 || idx >= (int)c->task_names.size()) throw Fail{MPAS_EINVAL, "timing index"};
+        if (name) *name = c->task_names[idx].c_str();
+        if (calls) *calls = c->task_calls[idx];
+        if (total_ms) *total_ms = c->task_ms[idx];
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,142 @@
+// mpas_dev.h -- device-side state layout and kernel launchers of libmpasdyn (gfx950).
+//
+// Device layout (HBM), chosen for one wavefront per column:
+//   C3/E3/V3   f[entity * LP + k]            k = 0..L   (LP = pow2 >= L+1, <= 64)
+//   C3V        f[(entity * W + i) * LP + k]  (zb_cell / zb3_cell: coalesced per component)
+//   C2*/E2*/V2* f[entity * W + i]            (2-D mesh data)
+//   C3B        uint8 f[entity * LP + k]
+//   ZV         f[k]                          (vertical_fs, LP entries)
+// Every entity array has nEntity+1 rows; row nEntity is the all-zero, never-written
+// "zero slot" that raw 1-based MPAS ids equal to nEntity resolve to.
+// A column of LP lanes holds one entity's levels: lane k <-> level k, so a gathered
+// neighbour column is one contiguous 8*(L+1)-byte read and vertical neighbours are
+// register shuffles within the LP-lane segment.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mpas {
+
+enum FieldKind { K_C3, K_C3V, K_E3, K_V3, K_C2F, K_C2I, K_E2F, K_E2I, K_V2F, K_V2I, K_C3B, K_ZV };
+enum FieldDist { D_U = 0, D_Z = 1, D_B = 2, D_M = 3, D_S = 4 };
+
+enum FieldId {
+#define MPAS_FIELD(name, KIND, W, DIST, LO, HI) F_##name,
+#include "mpas_fields.def"
+#undef MPAS_FIELD
+    F_COUNT,
+    // derived mesh arrays (computed at upload time, glibc cos on the host)
+    X_cosAngleEdge = F_COUNT,
+    X_cosLatEdge,
+    X_cosLatCell,
+    // scratch (not reference fields): w after horizontal advection + curvature,
+    // needed because the U section still reads the pre-zeroing w (dyn_tend :1013)
+    X_wc,
+    X_COUNT
+};
+
+struct FieldInfo {
+    const char* name;
+    int kind, width, dist;
+    double lo, hi;
+};
+extern const FieldInfo kFields[X_COUNT];
+
+struct DevState {
+    int nCells, nEdges, nVertices, L, LP;
+    void* f[X_COUNT];
+};
+
+// physical constants (constants.rg:27-66), identical to the oracle's
+constexpr double kRgas = 287.0;
+constexpr double kCp = 7.0 * 287.0 / 2.0;
+constexpr double kGravity = 9.80616;
+constexpr double kOmega = 7.29212E-5;
+constexpr double kEpssm = 0.1;
+constexpr double kPrandtl = 1.0;
+constexpr int kRelaxZone = 5;
+constexpr double kSmdiv = 0.1;
+constexpr double kLenDisp = 120000.0;
+constexpr double kVisc4_2dsmag = 0.05;
+constexpr double kSmagCoef = 0.125;
+constexpr double kDel4uDivFactor = 10.0;
+constexpr int kRayleighLevels = 6;
+constexpr double kRayleighDays = 5.0;
+constexpr double kSecondsPerDay = 86400.0;
+constexpr double kSphereRadius = 6371229.0;
+
+// dyn_tend configuration (the Regent task's scalar arguments, dynamics_tasks.rg:818-823)
+struct DynTendArgs {
+    int rk_step;
+    double dt;
+    int horiz_mixing;  // 0 = 2d_smagorinsky, 1 = 2d_fixed, 2 = none
+    double cam_coef;
+    int mix_full;
+    int rayleigh_damp_u;
+    int exact_q;       // 1: Q10 literal (each q term added nVertLevels times), 0: nVertLevels*term
+};
+
+// ---- launchers (each returns the hipGetLastError of its launches) ----
+hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st);
+hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st);
+hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts);
+hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
+hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
+hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact);
+hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts);
+hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step);
+hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
+hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
+
+// ---- device helpers ----
+#if defined(__HIPCC__)
+template <int LP>
+struct ColMap {
+    static constexpr int COLS = 256 / LP;
+    int ent, k;
+    __device__ __forceinline__ ColMap() {
+        ent = blockIdx.x * COLS + (int)(threadIdx.x / LP);
+        k = (int)(threadIdx.x % LP);
+    }
+};
+
+// value of x held by level k-1 of the same column (0.0 at k == 0: level -1 reads 0)
+template <int LP>
+__device__ __forceinline__ double lvl_dn(double x, int k) {
+    double y = __shfl_up(x, 1, LP);
+    return k == 0 ? 0.0 : y;
+}
+template <int LP>
+__device__ __forceinline__ double lvl_dn2(double x, int k) {
+    double y = __shfl_up(x, 2, LP);
+    return k < 2 ? 0.0 : y;
+}
+// value held by level k+1 (0.0 above the column's last lane)
+template <int LP>
+__device__ __forceinline__ double lvl_up(double x, int k) {
+    double y = __shfl_down(x, 1, LP);
+    return k == LP - 1 ? 0.0 : y;
+}
+
+__device__ __forceinline__ const double* fd(const DevState& S, int id) { return (const double*)S.f[id]; }
+__device__ __forceinline__ double* fw(const DevState& S, int id) { return (double*)S.f[id]; }
+__device__ __forceinline__ const int* fi(const DevState& S, int id) { return (const int*)S.f[id]; }
+
+// column read with the level policy: levels outside 0..L read 0.0
+__device__ __forceinline__ double col_rd(const double* f, int ent, int k, int L, int LP) {
+    return (k <= L) ? f[(size_t)ent * LP + k] : 0.0;
+}
+#endif
+
+}  // namespace mpas
+
+#define MPAS_LP_DISPATCH(LPVAL, FN, ...)                              \
+    do {                                                              \
+        switch (LPVAL) {                                              \
+            case 8: return FN<8>(__VA_ARGS__);                        \
+            case 16: return FN<16>(__VA_ARGS__);                      \
+            case 32: return FN<32>(__VA_ARGS__);                      \
+            case 64: return FN<64>(__VA_ARGS__);                      \
+            default: return hipErrorInvalidValue;                     \
+        }                                                             \
+    } while (0)

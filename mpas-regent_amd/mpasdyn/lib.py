@@ -1,0 +1,177 @@
+"""ctypes binding of libmpasdyn.so (include/mpas_dyn.h).
+
+The library is built in-tree (csrc/Makefile) for gfx950 only.  Loading it or creating a
+context on anything but a gfx950 device fails loudly: there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .registry import FIELDS, BY_NAME, F_COUNT
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmpasdyn.so")
+
+# every symbol include/mpas_dyn.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "mpas_ctx_create", "mpas_ctx_destroy", "mpas_last_error", "mpas_sync", "mpas_get_stream",
+    "mpas_set_option", "mpas_field_count", "mpas_field_id", "mpas_field_name", "mpas_field_kind",
+    "mpas_field_width", "mpas_upload", "mpas_download", "mpas_fill_synthetic",
+    "mpas_atm_rk_integration_setup", "mpas_atm_compute_moist_coefficients",
+    "mpas_atm_compute_vert_imp_coefs", "mpas_atm_compute_dyn_tend_work",
+    "mpas_atm_set_smlstep_pert_variables_work", "mpas_atm_advance_acoustic_step_work",
+    "mpas_atm_divergence_damping_3d", "mpas_atm_compute_solve_diagnostics",
+    "mpas_atm_rk_dynamics_substep_finish", "mpas_atm_srk3", "mpas_atm_timestep",
+    "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
+]
+
+HORIZ_MIXING = {"2d_smagorinsky": 0, "2d_fixed": 1}
+
+
+class MpasError(RuntimeError):
+    pass
+
+
+class Dims(ctypes.Structure):
+    _fields_ = [("nCells", ctypes.c_int32), ("nEdges", ctypes.c_int32),
+                ("nVertices", ctypes.c_int32), ("nVertLevels", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MpasError(f"{LIB_PATH} missing: build it with __graft_entry__.build() (no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+    sig = {
+        "mpas_ctx_create": (i32, [ctypes.POINTER(vp), i32, ctypes.POINTER(Dims)]),
+        "mpas_ctx_destroy": (i32, [vp]),
+        "mpas_last_error": (ctypes.c_char_p, [vp]),
+        "mpas_sync": (i32, [vp]),
+        "mpas_get_stream": (i32, [vp, ctypes.POINTER(vp)]),
+        "mpas_set_option": (i32, [vp, ctypes.c_char_p, i64]),
+        "mpas_field_count": (i32, []),
+        "mpas_field_id": (i32, [ctypes.c_char_p]),
+        "mpas_field_name": (ctypes.c_char_p, [i32]),
+        "mpas_field_kind": (i32, [i32]),
+        "mpas_field_width": (i32, [i32]),
+        "mpas_upload": (i32, [vp, i32, vp, i64, i64, i64]),
+        "mpas_download": (i32, [vp, i32, vp, i64, i64, i64]),
+        "mpas_fill_synthetic": (i32, [vp, ctypes.c_uint64]),
+        "mpas_atm_rk_integration_setup": (i32, [vp]),
+        "mpas_atm_compute_moist_coefficients": (i32, [vp]),
+        "mpas_atm_compute_vert_imp_coefs": (i32, [vp, dbl]),
+        "mpas_atm_compute_dyn_tend_work": (i32, [vp, i32, dbl, i32, dbl, i32, i32]),
+        "mpas_atm_set_smlstep_pert_variables_work": (i32, [vp]),
+        "mpas_atm_advance_acoustic_step_work": (i32, [vp, dbl, i32]),
+        "mpas_atm_divergence_damping_3d": (i32, [vp, dbl]),
+        "mpas_atm_compute_solve_diagnostics": (i32, [vp, i32, i32]),
+        "mpas_atm_rk_dynamics_substep_finish": (i32, [vp, i32, i32]),
+        "mpas_atm_srk3": (i32, [vp, dbl, i32]),
+        "mpas_atm_timestep": (i32, [vp, dbl]),
+        "mpas_timing_enable": (i32, [vp, i32]),
+        "mpas_timing_reset": (i32, [vp]),
+        "mpas_timing_count": (i32, [vp]),
+        "mpas_timing_get": (i32, [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(i64),
+                                  ctypes.POINTER(dbl)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype, fn.argtypes = res, args
+    if L.mpas_field_count() != F_COUNT:
+        raise MpasError("libmpasdyn.so was built from a different mpas_fields.def")
+    _lib = L
+    return L
+
+
+class Context:
+    """One device-resident copy of the regions (cr, er, vr, vert_r) on one GPU."""
+
+    def __init__(self, nCells, nEdges, nVertices, nVertLevels, device=0):
+        self.lib = load()
+        self.dims = (nCells, nEdges, nVertices, nVertLevels)
+        d = Dims(nCells, nEdges, nVertices, nVertLevels)
+        h = ctypes.c_void_p()
+        rc = self.lib.mpas_ctx_create(ctypes.byref(h), device, ctypes.byref(d))
+        if rc != 0:
+            raise MpasError(f"mpas_ctx_create failed ({rc}): {self.lib.mpas_last_error(None).decode()}")
+        self.h = h
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise MpasError(f"{what} failed ({rc}): {self.lib.mpas_last_error(self.h).decode()}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mpas_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---------------------------------------------------------------- residency
+    def upload(self, state, names=None):
+        for f in FIELDS:
+            if names is not None and f.name not in names:
+                continue
+            a = state.arrays[f.name]
+            se, sl, sc = state.byte_strides(f.name)
+            self._check(self.lib.mpas_upload(self.h, f.index, a.ctypes.data_as(ctypes.c_void_p), se, sl, sc),
+                        f"upload {f.name}")
+
+    def download(self, state, names=None):
+        for f in FIELDS:
+            if names is not None and f.name not in names:
+                continue
+            a = state.arrays[f.name]
+            se, sl, sc = state.byte_strides(f.name)
+            self._check(self.lib.mpas_download(self.h, f.index, a.ctypes.data_as(ctypes.c_void_p), se, sl, sc),
+                        f"download {f.name}")
+
+    def fill_synthetic(self, seed):
+        self._check(self.lib.mpas_fill_synthetic(self.h, seed), "fill_synthetic")
+
+    def sync(self):
+        self._check(self.lib.mpas_sync(self.h), "sync")
+
+    def stream(self):
+        p = ctypes.c_void_p()
+        self._check(self.lib.mpas_get_stream(self.h, ctypes.byref(p)), "get_stream")
+        return p.value
+
+    def set_option(self, name, value):
+        self._check(self.lib.mpas_set_option(self.h, name.encode(), int(value)), f"set_option {name}")
+
+    # ---------------------------------------------------------------- timing
+    def timing(self, on=True):
+        self._check(self.lib.mpas_timing_enable(self.h, 1 if on else 0), "timing_enable")
+
+    def timing_reset(self):
+        self._check(self.lib.mpas_timing_reset(self.h), "timing_reset")
+
+    def timing_report(self):
+        n = self.lib.mpas_timing_count(self.h)
+        if n < 0:
+            self._check(n, "timing_count")
+        out = {}
+        for i in range(n):
+            name, calls, ms = ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_double()
+            self._check(self.lib.mpas_timing_get(self.h, i, ctypes.byref(name), ctypes.byref(calls),
+                                                 ctypes.byref(ms)), "timing_get")
+            out[name.value.decode()] = (calls.value, ms.value)
+        return out

@@ -1,0 +1,1003 @@
+/* mpas_oracle.c -- TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference's
+ * RK3 dynamics hot path (alexaiken/mpas-regent), used as the parity checker by
+ * tests/, __graft_entry__.smoke() and the cpu_baseline leg of bench.py.  Nothing in
+ * the product (mpas-regent_amd/) links, loads or calls this file.
+ *
+ * PARITY UNPINNED: the reference is Regent source that cannot be compiled or run here
+ * (no Regent/Legion/Terra) and it ships no tests, fixtures or golden
+ * vectors.  This restatement follows the Regent text line by line; every
+ * function cites the lines it follows.  Undefined behaviour in the reference is
+ * resolved by the written policies of SURVEY §8.0 ("ref" mode):
+ *   Q1  raw ids are used as offsets; every entity array has one extra all-zero row n
+ *       (the "zero slot", never written); any other out-of-range entity -> 0.0.
+ *   Q2  never-written fields are inputs (zero in a literal "ref" state).
+ *   OOB levels (k < 0 or k > nVertLevels) read 0.0.
+ *   pow(x, 2.0) is evaluated as x*x; pow of compile-time constants is folded.
+ *   min(a,b) := a < b ? a : b, max(a,b) := a > b ? a : b.
+ *   Loops run entity-outer / level-inner, which the loop-order note of SURVEY §8.0
+ *   shows equivalent to Legion's point order for every task on the path.
+ * Layout (the reference's int2d region indexing): a cell field f is f[cell*(L+1)+k]
+ * for k = 0..L; C3V fields are f[(cell*(L+1)+k)*W + i]; 2-D mesh fields f[e*W + i].
+ * Build with -ffp-contract=off so that every a*b+c rounds twice, as written.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "mpas_synth.h"
+
+/* ---------------- field registry ---------------- */
+enum {
+#define MPAS_FIELD(name, KIND, W, D, LO, HI) F_##name,
+#include "mpas_fields.def"
+#undef MPAS_FIELD
+    F_COUNT
+};
+
+typedef struct {
+    int32_t nCells, nEdges, nVertices, L; /* L = nVertLevels */
+    void* f[F_COUNT];                     /* host arrays, reference layout */
+} ora_state;
+
+/* constants.rg:27-66 */
+static const double rgas = 287.0;
+#define CP (7.0 * 287.0 / 2.0)
+static const double gravity = 9.80616;
+static const double omega_c = 7.29212E-5;
+static const double config_epssm = 0.1;
+static const double prandtl = 1.0;
+static const int nRelaxZone = 5;
+static const double config_smdiv = 0.1;
+static const double config_len_disp = 120000.0;
+static const double config_visc4_2dsmag = 0.05;
+static const double config_smagorinsky_coef = 0.125;
+static const double config_del4u_div_factor = 10.0;
+static const int config_number_rayleigh_damp_u_levels = 6;
+static const double config_rayleigh_damp_u_timescale_days = 5.0;
+static const double seconds_per_day = 86400.0;
+static const double sphere_radius = 6371229.0;
+
+#define D(name) ((double*)S->f[F_##name])
+#define I(name) ((int32_t*)S->f[F_##name])
+#define B(name) ((uint8_t*)S->f[F_##name])
+#define LV (S->L + 1)
+
+static inline double dmin(double a, double b) { return a < b ? a : b; }
+static inline double dmax(double a, double b) { return a > b ? a : b; }
+
+/* Q1/OOB read policy */
+static inline double rc(const ora_state* S, const double* f, long i, long k) {
+    if (i < 0 || i > S->nCells || k < 0 || k > S->L) return 0.0;
+    return f[i * LV + k];
+}
+static inline double re(const ora_state* S, const double* f, long i, long k) {
+    if (i < 0 || i > S->nEdges || k < 0 || k > S->L) return 0.0;
+    return f[i * LV + k];
+}
+static inline double rv(const ora_state* S, const double* f, long i, long k) {
+    if (i < 0 || i > S->nVertices || k < 0 || k > S->L) return 0.0;
+    return f[i * LV + k];
+}
+static inline double rz(const ora_state* S, const double* f, long k) {
+    if (k < 0 || k > S->L) return 0.0;
+    return f[k];
+}
+static inline double rc2(const ora_state* S, const double* f, long i, int W, int c) {
+    if (i < 0 || i > S->nCells || c < 0 || c >= W) return 0.0;
+    return f[i * W + c];
+}
+static inline double re2(const ora_state* S, const double* f, long i, int W, int c) {
+    if (i < 0 || i > S->nEdges || c < 0 || c >= W) return 0.0;
+    return f[i * W + c];
+}
+static inline double rv2(const ora_state* S, const double* f, long i, int W, int c) {
+    if (i < 0 || i > S->nVertices || c < 0 || c >= W) return 0.0;
+    return f[i * W + c];
+}
+static inline int ic2(const ora_state* S, const int32_t* f, long i, int W, int c) {
+    if (i < 0 || i > S->nCells || c < 0 || c >= W) return 0;
+    return f[i * W + c];
+}
+static inline int ie2(const ora_state* S, const int32_t* f, long i, int W, int c) {
+    if (i < 0 || i > S->nEdges || c < 0 || c >= W) return 0;
+    return f[i * W + c];
+}
+static inline int iv2(const ora_state* S, const int32_t* f, long i, int W, int c) {
+    if (i < 0 || i > S->nVertices || c < 0 || c >= W) return 0;
+    return f[i * W + c];
+}
+static inline double rc3v(const ora_state* S, const double* f, long i, long k, int c) {
+    if (i < 0 || i > S->nCells || k < 0 || k > S->L || c < 0 || c >= 10) return 0.0;
+    return f[(i * LV + k) * 10 + c];
+}
+#define CW(f, i, k) (f)[(long)(i) * LV + (k)] /* own-point write/read */
+
+/* flux4/flux3, dynamics_tasks.rg:780-789 */
+static inline double flux4(double q_im2, double q_im1, double q_i, double q_ip1, double ua) {
+    return ua * (7. * (q_i + q_im1) - (q_ip1 + q_im2)) / 12.0;
+}
+static inline double flux3(double q_im2, double q_im1, double q_i, double q_ip1, double ua, double coef3) {
+    return flux4(q_im2, q_im1, q_i, q_ip1, ua) + coef3 * fabs(ua) * ((q_ip1 - q_im2) - 3. * (q_i - q_im1)) / 12.0;
+}
+/* rayleigh_damp_coef, dynamics_tasks.rg:791-796 */
+static inline double rayleigh_damp_coef(const ora_state* S, double vertLevel) {
+    double inv = 1.0 / ((double)config_number_rayleigh_damp_u_levels *
+                        (config_rayleigh_damp_u_timescale_days * seconds_per_day));
+    return (double)(vertLevel - (S->L - config_number_rayleigh_damp_u_levels)) * inv;
+}
+
+/* ===================== atm_compute_solve_diagnostics, dynamics_tasks.rg:328-454 */
+void ora_atm_compute_solve_diagnostics(ora_state* S, int hollingsworth, int rk_step) {
+    const int L = S->L, nC = S->nCells, nE = S->nEdges, nV = S->nVertices;
+    double *u = D(u), *h = D(h), *h_edge = D(h_edge), *ke_edge = D(ke_edge);
+    double *dcEdge = D(dcEdge), *dvEdge = D(dvEdge);
+    int32_t* cellsOnEdge = I(cellsOnEdge);
+    /* :346-353 */
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        int cell1 = ie2(S, cellsOnEdge, e, 2, 0), cell2 = ie2(S, cellsOnEdge, e, 2, 1);
+        for (int k = 0; k < L; k++) {
+            CW(h_edge, e, k) = 0.5 * (rc(S, h, cell1, k) + rc(S, h, cell2, k));
+            double efac = re2(S, dcEdge, e, 1, 0) * re2(S, dvEdge, e, 1, 0);
+            double uu = CW(u, e, k);
+            CW(ke_edge, e, k) = efac * (uu * uu);
+        }
+    }
+    /* :356-366 */
+    double *vort = D(vorticity);
+#pragma omp parallel for schedule(static)
+    for (long v = 0; v < nV; v++) {
+        for (int k = 0; k < L; k++) {
+            CW(vort, v, k) = 0.0;
+            for (int i = 0; i < 3; i++) {
+                int iEdge = iv2(S, I(edgesOnVertex), v, 3, i);
+                double s = rv2(S, D(edgesOnVertexSign), v, 3, i) * re2(S, dcEdge, iEdge, 1, 0);
+                CW(vort, v, k) += s * re(S, u, iEdge, k);
+            }
+            CW(vort, v, k) *= rv2(S, D(invAreaTriangle), v, 1, 0);
+        }
+    }
+    /* :369-379 (Q9: divergence += s + u, literal) */
+    double *div = D(divergence), *ke = D(ke);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int k = 0; k < L; k++) {
+            CW(div, c, k) = 0.0;
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                double s = rc2(S, D(edgesOnCellSign), c, 10, i) * re2(S, dvEdge, iEdge, 1, 0);
+                CW(div, c, k) += s + re(S, u, iEdge, k);
+            }
+            double r = rc2(S, D(invAreaCell), c, 1, 0);
+            CW(div, c, k) *= r;
+        }
+        /* :382-390 */
+        for (int k = 0; k < L; k++) {
+            CW(ke, c, k) = 0.0;
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                CW(ke, c, k) += 0.25 * re(S, ke_edge, iEdge, k);
+            }
+            CW(ke, c, k) *= rc2(S, D(invAreaCell), c, 1, 0);
+        }
+    }
+    if (hollingsworth) { /* :392-418 */
+        double* ke_vertex = D(ke_vertex);
+#pragma omp parallel for schedule(static)
+        for (long v = 0; v < nV; v++) {
+            double r = 0.25 * rv2(S, D(invAreaTriangle), v, 1, 0);
+            for (int k = 0; k < L; k++) {
+                CW(ke_vertex, v, k) = (re(S, ke_edge, iv2(S, I(edgesOnVertex), v, 3, 0), k) +
+                                       re(S, ke_edge, iv2(S, I(edgesOnVertex), v, 3, 1), k) +
+                                       re(S, ke_edge, iv2(S, I(edgesOnVertex), v, 3, 2), k)) * r;
+            }
+        }
+        double ke_fact = 1.0 - 0.375;
+#pragma omp parallel for schedule(static)
+        for (long c = 0; c < nC; c++) {
+            for (int k = 0; k < L; k++) CW(ke, c, k) *= ke_fact;
+            double r = rc2(S, D(invAreaCell), c, 1, 0);
+            int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+            for (int k = 0; k < L; k++) {
+                for (int i = 0; i < ne; i++) {
+                    int iVertex = ic2(S, I(verticesOnCell), c, 10, i);
+                    int j = ic2(S, I(kiteForCell), c, 10, i);
+                    CW(ke, c, k) += (1.0 - ke_fact) * rv2(S, D(kiteAreasOnVertex), iVertex, 3, j) *
+                                    rv(S, ke_vertex, iVertex, k) * r;
+                }
+            }
+        }
+    }
+    /* :422-439 (Q23: starts at i = 1) */
+    int reconstruct_v = 1;
+    if (rk_step != -1 && rk_step != 2) reconstruct_v = 0;
+    if (reconstruct_v) {
+        double* vv = D(v);
+#pragma omp parallel for schedule(static)
+        for (long e = 0; e < nE; e++) {
+            int neoe = ie2(S, I(nEdgesOnEdge), e, 1, 0);
+            for (int k = 0; k < L; k++) {
+                CW(vv, e, k) = 0;
+                for (int i = 1; i < neoe; i++) {
+                    int eoe = ie2(S, I(edgesOnEdge_ECP), e, 20, i);
+                    CW(vv, e, k) += re2(S, D(weightsOnEdge), e, 20, i) * re(S, u, eoe, k);
+                }
+            }
+        }
+    }
+    /* :443-445 */
+    double* pv_vertex = D(pv_vertex);
+#pragma omp parallel for schedule(static)
+    for (long v = 0; v < nV; v++)
+        for (int k = 0; k < L; k++) CW(pv_vertex, v, k) = rv2(S, D(fVertex), v, 1, 0) + CW(vort, v, k);
+    /* :449-451 */
+    double* pv_edge = D(pv_edge);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        int v1 = ie2(S, I(verticesOnEdge), e, 2, 0), v2 = ie2(S, I(verticesOnEdge), e, 2, 1);
+        for (int k = 0; k < L; k++) CW(pv_edge, e, k) = 0.5 * (rv(S, pv_vertex, v1, k) + rv(S, pv_vertex, v2, k));
+    }
+}
+
+/* ===================== atm_compute_moist_coefficients, dynamics_tasks.rg:460-502 */
+void ora_atm_compute_moist_coefficients(ora_state* S) {
+    const int L = S->L, nC = S->nCells;
+    double *qtot = D(qtot), *cqw = D(cqw);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        for (int k = 0; k < L; k++) CW(qtot, c, k) = 0.0; /* :473-482 */
+        for (int k = 0; k < L; k++) {                      /* :484-489 */
+            if (k > 0) {
+                double qtotal = 0.5 * (CW(qtot, c, k) + CW(qtot, c, k - 1));
+                CW(cqw, c, k) = 1.0 / (1.0 + qtotal);
+            }
+        }
+    }
+    /* :491-501 edge loop body is commented out in the reference: nothing to do */
+}
+
+/* ===================== atm_compute_vert_imp_coefs, dynamics_tasks.rg:513-592 */
+void ora_atm_compute_vert_imp_coefs(ora_state* S, double dts) {
+    const int L = S->L, nC = S->nCells;
+    double dtseps = .5 * dts * (1.0 + config_epssm);
+    double rcv = rgas / (CP - rgas);
+    double c2 = CP * rcv;
+    double *rdzu = D(rdzu), *rdzw = D(rdzw), *fzm = D(fzm), *fzp = D(fzp), *cofrz = D(cofrz);
+    for (int k = 0; k < L; k++) cofrz[k] = dtseps * rdzw[k]; /* :537-539 */
+    double *zz = D(zz), *cofwr = D(cofwr), *cofwz = D(cofwz), *coftz = D(coftz), *cofwt = D(cofwt);
+    double *cqw = D(cqw), *exner = D(exner), *theta_m = D(theta_m), *qtot = D(qtot);
+    double *rho_base = D(rho_base), *rtheta_base = D(rtheta_base), *rtheta_p = D(rtheta_p);
+    double *exner_base = D(exner_base);
+    double *a_tri = D(a_tri), *b_tri = D(b_tri), *c_tri = D(c_tri), *alpha_tri = D(alpha_tri);
+    double* gamma_tri = D(gamma_tri);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        CW(gamma_tri, c, 0) = 0.0; /* :541-547 */
+        for (int k = 0; k < L; k++) { /* :550-564 */
+            if (k > 0)
+                CW(cofwr, c, k) = .5 * dtseps * gravity * (fzm[k] * CW(zz, c, k) + fzp[k] * CW(zz, c, k - 1));
+            CW(coftz, c, k) = 0.0;
+            if (k > 0) {
+                CW(cofwz, c, k) = dtseps * c2 * (fzm[k] * CW(zz, c, k) + fzp[k] * CW(zz, c, k - 1)) * rdzu[k] *
+                                  CW(cqw, c, k) * (fzm[k] * CW(exner, c, k) + fzp[k] * CW(exner, c, k - 1));
+                CW(coftz, c, k) = dtseps * (fzm[k] * CW(theta_m, c, k) + fzp[k] * CW(theta_m, c, k - 1));
+            }
+            double qtotal = CW(qtot, c, k);
+            CW(cofwt, c, k) = .5 * dtseps * rcv * CW(zz, c, k) * gravity * CW(rho_base, c, k) / (1.0 + qtotal) *
+                              CW(exner, c, k) / ((CW(rtheta_base, c, k) + CW(rtheta_p, c, k)) * CW(exner_base, c, k));
+        }
+        for (int k = 1; k < L; k++) { /* :566-578 */
+            CW(a_tri, c, k) = -1.0 * CW(cofwz, c, k) * CW(coftz, c, k - 1) * rdzw[k - 1] * CW(zz, c, k - 1) +
+                              CW(cofwr, c, k) * cofrz[k - 1] -
+                              CW(cofwt, c, k - 1) * CW(coftz, c, k - 1) * rdzw[k - 1];
+            CW(b_tri, c, k) = 1.0 +
+                              CW(cofwz, c, k) * (CW(coftz, c, k) * rdzw[k] * CW(zz, c, k) +
+                                                 CW(coftz, c, k) * rdzw[k - 1] * CW(zz, c, k - 1)) -
+                              CW(coftz, c, k) * (CW(cofwt, c, k) * rdzw[k] - CW(cofwt, c, k) * rdzw[k - 1]) +
+                              CW(cofwr, c, k) * ((cofrz[k] - cofrz[k - 1]));
+            CW(c_tri, c, k) = -1.0 * CW(cofwz, c, k) * rc(S, coftz, c, k + 1) * rdzw[k] * CW(zz, c, k) -
+                              CW(cofwr, c, k) * cofrz[k] + CW(cofwt, c, k) * rc(S, coftz, c, k + 1) * rdzw[k];
+        }
+        for (int k = 1; k < L; k++) /* :580-585 (Q17: gamma of the previous call) */
+            CW(alpha_tri, c, k) = 1.0 / (CW(b_tri, c, k) - CW(a_tri, c, k) * CW(gamma_tri, c, k - 1));
+        for (int k = 1; k < L; k++) /* :587-591 */
+            CW(gamma_tri, c, k) = CW(c_tri, c, k) * CW(alpha_tri, c, k);
+    }
+}
+
+/* ===================== atm_rk_integration_setup, dynamics_tasks.rg:747-778 */
+void ora_atm_rk_integration_setup(ora_state* S) {
+    const int L = S->L;
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < S->nEdges; e++)
+        for (int k = 0; k < L; k++) {
+            CW(D(ru_save), e, k) = CW(D(ru), e, k);
+            CW(D(u_2), e, k) = CW(D(u), e, k);
+        }
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < S->nCells; c++)
+        for (int k = 0; k < L; k++) {
+            CW(D(rw_save), c, k) = CW(D(rw), c, k);
+            CW(D(rtheta_p_save), c, k) = CW(D(rtheta_p), c, k);
+            CW(D(rho_p_save), c, k) = CW(D(rho_p), c, k);
+            CW(D(w_2), c, k) = CW(D(w), c, k);
+            CW(D(theta_m_2), c, k) = CW(D(theta_m), c, k);
+            CW(D(rho_zz_2), c, k) = CW(D(rho_zz), c, k);
+            CW(D(rho_zz_old_split), c, k) = CW(D(rho_zz), c, k);
+        }
+}
+
+/* ===================== atm_compute_dyn_tend_work, dynamics_tasks.rg:814-1480
+ * horiz_mixing: 0 = "2d_smagorinsky", 1 = "2d_fixed", other = neither.
+ * The v_mom/v_theta_eddy_visc2 branches (:1094-1146, :1304-1315, :1430-1475) are dead
+ * code under constants.rg:47-48 (both 0.0) and are not restated.                    */
+void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int horiz_mixing,
+                                   double config_mpas_cam_coef, int config_mix_full,
+                                   int config_rayleigh_damp_u) {
+    (void)config_mix_full;
+    const int L = S->L, nC = S->nCells, nE = S->nEdges, nV = S->nVertices;
+    double prandtl_inv = 1.0 / prandtl;
+    double invDt = 1.0 / dt;
+    double r_earth = sphere_radius;
+    double inv_r_earth = 1.0 / r_earth;
+    double h_mom_eddy_visc4 = 0.0, h_theta_eddy_visc4 = 0.0;
+    double *u = D(u), *v = D(v), *kdiff = D(kdiff), *ru = D(ru), *rw = D(rw);
+    int32_t *nEdgesOnCell = I(nEdgesOnCell), *edgesOnCell = I(edgesOnCell), *cellsOnEdge = I(cellsOnEdge);
+    double *eocs = D(edgesOnCell_sign), *dvEdge = D(dvEdge), *invAreaCell = D(invAreaCell);
+    double *invDcEdge = D(invDcEdge);
+    double *fzm = D(fzm), *fzp = D(fzp), *rdzw = D(rdzw), *rdzu = D(rdzu);
+
+    if (rk_step == 0) {
+        if (horiz_mixing == 0) { /* :861-890 (Q11: only d_diag[k] of the own level is used) */
+            double c_s = config_smagorinsky_coef;
+            double cs_l2 = (c_s * config_len_disp) * (c_s * config_len_disp); /* pow(c_s*len,2.0) */
+            double cap = (0.01 * (config_len_disp * config_len_disp)) * invDt;
+#pragma omp parallel for schedule(static)
+            for (long c = 0; c < nC; c++) {
+                int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+                for (int k = 0; k < L; k++) {
+                    double d_diag = 0.0, d_off_diag = 0.0;
+                    for (int iEdge = 0; iEdge < ne; iEdge++) {
+                        int e = ic2(S, edgesOnCell, c, 10, iEdge);
+                        d_diag += rc2(S, D(defc_a), c, 10, iEdge) * re(S, u, e, k) - rc2(S, D(defc_b), c, 10, iEdge) * re(S, v, e, k);
+                        d_off_diag += rc2(S, D(defc_b), c, 10, iEdge) * re(S, u, e, k) + rc2(S, D(defc_a), c, 10, iEdge) * re(S, v, e, k);
+                    }
+                    CW(kdiff, c, k) = dmin(cs_l2 * sqrt(d_diag * d_diag + d_off_diag * d_off_diag), cap);
+                }
+            }
+            h_mom_eddy_visc4 = config_visc4_2dsmag * (config_len_disp * config_len_disp * config_len_disp);
+            h_theta_eddy_visc4 = h_mom_eddy_visc4;
+        } else if (horiz_mixing == 1) {
+#pragma omp parallel for schedule(static)
+            for (long c = 0; c < nC; c++)
+                for (int k = 0; k < L; k++) CW(kdiff, c, k) = 0.0;
+        }
+        if (config_mpas_cam_coef > 0.0) { /* :898-916 */
+#pragma omp parallel for schedule(static)
+            for (long c = 0; c < nC; c++)
+                for (int k = 0; k < L; k++)
+                    if (k >= L - 2 && k <= L) {
+                        int p = k - (L - 2);
+                        CW(kdiff, c, k) = dmax(CW(kdiff, c, k), pow(2, p) * 2.0833 * config_len_disp * config_mpas_cam_coef);
+                    }
+        }
+    }
+
+    double* h_divergence = D(h_divergence);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) { /* :924-938 */
+        int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+        for (int k = 0; k < L; k++) {
+            CW(h_divergence, c, k) = 0.0;
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                double edge_sign = rc2(S, eocs, c, 10, i) * re2(S, dvEdge, iEdge, 1, 0);
+                CW(h_divergence, c, k) += edge_sign * re(S, ru, iEdge, k);
+            }
+        }
+        for (int k = 0; k < L; k++) {
+            double r = rc2(S, invAreaCell, c, 1, 0);
+            CW(h_divergence, c, k) *= r;
+        }
+    }
+
+    double *tend_rho = D(tend_rho), *dpdz = D(dpdz);
+    if (rk_step == 0) { /* :942-951 */
+#pragma omp parallel for schedule(static)
+        for (long c = 0; c < nC; c++)
+            for (int k = 0; k < L; k++) {
+                CW(tend_rho, c, k) = -CW(h_divergence, c, k) -
+                                     rdzw[k] * (rc(S, rw, c, k + 1) - CW(rw, c, k) + CW(D(tend_rho_physics), c, k));
+                CW(dpdz, c, k) = -gravity * (CW(D(rho_base), c, k) * (CW(D(qtot), c, k)) +
+                                             CW(D(rho_p_save), c, k) * (1.0 + CW(D(qtot), c, k)));
+            }
+    }
+
+    /* -------- U section -------- */
+    double *tend_u_euler = D(tend_u_euler), *wduz = D(wduz), *tend_u = D(tend_u), *q = D(q);
+    double *pressure_p = D(pressure_p), *zz = D(zz), *zxu = D(zxu), *cqu = D(cqu);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) { /* :958-981 */
+        int cell1 = ie2(S, cellsOnEdge, e, 2, 0), cell2 = ie2(S, cellsOnEdge, e, 2, 1);
+        for (int k = 0; k < L; k++) {
+            if (rk_step == 0) {
+                CW(tend_u_euler, e, k) =
+                    -CW(cqu, e, k) * ((rc(S, pressure_p, cell2, k) - rc(S, pressure_p, cell1, k)) * re2(S, invDcEdge, e, 1, 0) /
+                                          (0.5 * (rc(S, zz, cell2, k) + rc(S, zz, cell1, k))) -
+                                      0.5 * CW(zxu, e, k) * (rc(S, dpdz, cell1, k) + rc(S, dpdz, cell2, k)));
+            }
+            CW(wduz, e, k) = 0.0;
+            if (k == 1 || k == L - 1)
+                CW(wduz, e, k) = 0.5 * (rc(S, rw, cell1, k) + rc(S, rw, cell2, k)) *
+                                 (fzm[k] * CW(u, e, k) + fzp[k] * re(S, u, e, k - 1));
+            if (k > 1 && k < L - 1)
+                CW(wduz, e, k) = flux3(re(S, u, e, k - 2), re(S, u, e, k - 1), CW(u, e, k), re(S, u, e, k + 1),
+                                       0.5 * (rc(S, rw, cell1, k) + rc(S, rw, cell2, k)), 1.0);
+        }
+    }
+    double *pv_edge = D(pv_edge), *rho_edge = D(rho_edge), *ke = D(ke), *w = D(w);
+    double *cosA = D(angleEdge), *latE = D(latEdge); /* cos() taken below, glibc */
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) { /* :983-1019 */
+        int cell1 = ie2(S, cellsOnEdge, e, 2, 0), cell2 = ie2(S, cellsOnEdge, e, 2, 1);
+        int neoe = ie2(S, I(nEdgesOnEdge), e, 1, 0);
+        for (int k = 0; k < L; k++) {
+            CW(tend_u, e, k) = -rdzw[k] * (re(S, wduz, e, k + 1) - CW(wduz, e, k));
+            CW(q, e, k) = 0.0;
+            for (int j = 0; j < neoe; j++) { /* Q10: each term accumulated nVertLevels times */
+                int eoe = ie2(S, I(edgesOnEdge), e, 20, j);
+                for (int kk = 0; kk < L; kk++) {
+                    double workpv = 0.5 * (CW(pv_edge, e, k) + re(S, pv_edge, eoe, k));
+                    CW(q, e, k) += re2(S, D(weightsOnEdge), e, 20, j) * re(S, u, eoe, k) * workpv;
+                }
+            }
+            CW(tend_u, e, k) += CW(rho_edge, e, k) * (CW(q, e, k) - (rc(S, ke, cell2, k) - rc(S, ke, cell1, k)) * re2(S, invDcEdge, e, 1, 0)) -
+                                CW(u, e, k) * 0.5 * (rc(S, h_divergence, cell1, k) + rc(S, h_divergence, cell2, k));
+            /* Q12: -= (A) - (B), literal */
+            CW(tend_u, e, k) -= (2.0 * omega_c * cos(re2(S, cosA, e, 1, 0)) * cos(re2(S, latE, e, 1, 0)) * CW(rho_edge, e, k) * 0.25 *
+                                 (rc(S, w, cell1, k) + rc(S, w, cell1, k + 1) + rc(S, w, cell2, k) + rc(S, w, cell2, k + 1))) -
+                                (CW(u, e, k) * 0.25 * (rc(S, w, cell1, k) + rc(S, w, cell1, k + 1) + rc(S, w, cell2, k) + rc(S, w, cell2, k + 1)) *
+                                 CW(rho_edge, e, k) * inv_r_earth);
+        }
+    }
+
+    double *delsq_u = D(delsq_u), *divergence = D(divergence), *vorticity = D(vorticity);
+    double *delsq_vorticity = D(delsq_vorticity), *delsq_divergence = D(delsq_divergence);
+    if (rk_step == 0) { /* :1025-1091 */
+#pragma omp parallel for schedule(static)
+        for (long e = 0; e < nE; e++) {
+            int cell1 = ie2(S, cellsOnEdge, e, 2, 0), cell2 = ie2(S, cellsOnEdge, e, 2, 1);
+            int vertex1 = ie2(S, I(verticesOnEdge), e, 2, 0), vertex2 = ie2(S, I(verticesOnEdge), e, 2, 1);
+            double r_dc = re2(S, invDcEdge, e, 1, 0);
+            double r_dv = dmin(re2(S, D(invDvEdge), e, 1, 0), 4 * r_dc);
+            for (int k = 0; k < L; k++) {
+                CW(delsq_u, e, k) = 0.0;
+                double u_diffusion = (rc(S, divergence, cell2, k) - rc(S, divergence, cell1, k)) * r_dc -
+                                     (rv(S, vorticity, vertex2, k) - rv(S, vorticity, vertex1, k)) * r_dv;
+                CW(delsq_u, e, k) += u_diffusion;
+                double kdiffu = 0.5 * (rc(S, kdiff, cell1, k) + rc(S, kdiff, cell2, k));
+                CW(tend_u_euler, e, k) += CW(rho_edge, e, k) * kdiffu * u_diffusion * re2(S, D(meshScalingDel2), e, 1, 0);
+            }
+        }
+        if (h_mom_eddy_visc4 > 0.0) {
+#pragma omp parallel for schedule(static)
+            for (long vx = 0; vx < nV; vx++)
+                for (int k = 0; k < L; k++) {
+                    CW(delsq_vorticity, vx, k) = 0.0;
+                    for (int i = 0; i < 3; i++) {
+                        int iEdge = iv2(S, I(edgesOnVertex), vx, 3, i);
+                        double edge_sign = rv2(S, D(invAreaTriangle), vx, 1, 0) * re2(S, D(dcEdge), iEdge, 1, 0) *
+                                           rv2(S, D(edgesOnVertex_sign), vx, 3, i);
+                        CW(delsq_vorticity, vx, k) += edge_sign * re(S, delsq_u, iEdge, k);
+                    }
+                }
+#pragma omp parallel for schedule(static)
+            for (long c = 0; c < nC; c++) {
+                int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+                for (int k = 0; k < L; k++) {
+                    CW(delsq_divergence, c, k) = 0.0;
+                    double r = rc2(S, invAreaCell, c, 1, 0);
+                    for (int i = 0; i < ne; i++) {
+                        int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                        double edge_sign = r * re2(S, dvEdge, iEdge, 1, 0) * rc2(S, eocs, c, 10, i);
+                        CW(delsq_divergence, c, k) += edge_sign * re(S, delsq_u, iEdge, k);
+                    }
+                }
+            }
+#pragma omp parallel for schedule(static)
+            for (long e = 0; e < nE; e++) {
+                int cell1 = ie2(S, cellsOnEdge, e, 2, 0), cell2 = ie2(S, cellsOnEdge, e, 2, 1);
+                int vertex1 = ie2(S, I(verticesOnEdge), e, 2, 0), vertex2 = ie2(S, I(verticesOnEdge), e, 2, 1);
+                double u_mix_scale = re2(S, D(meshScalingDel4), e, 1, 0) * h_mom_eddy_visc4;
+                double r_dc = u_mix_scale * config_del4u_div_factor * re2(S, invDcEdge, e, 1, 0);
+                double r_dv = u_mix_scale * dmin(re2(S, D(invDvEdge), e, 1, 0), 4 * re2(S, invDcEdge, e, 1, 0));
+                for (int k = 0; k < L; k++) {
+                    double u_diffusion = CW(rho_edge, e, k) *
+                                         ((rc(S, delsq_divergence, cell2, k) - rc(S, delsq_divergence, cell1, k)) * r_dc -
+                                          (rv(S, delsq_vorticity, vertex2, k) - rv(S, delsq_vorticity, vertex1, k)) * r_dv);
+                    CW(tend_u_euler, e, k) -= u_diffusion;
+                }
+            }
+        }
+    }
+    if (config_rayleigh_damp_u) { /* :1152-1159 */
+#pragma omp parallel for schedule(static)
+        for (long e = 0; e < nE; e++)
+            for (int k = 0; k < L; k++)
+                if (k > L - config_number_rayleigh_damp_u_levels + 1)
+                    CW(tend_u, e, k) -= CW(rho_edge, e, k) * CW(u, e, k) * rayleigh_damp_coef(S, k);
+    }
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) /* :1161-1163 */
+        for (int k = 0; k < L; k++) CW(tend_u, e, k) += CW(tend_u_euler, e, k) + CW(D(tend_ru_physics), e, k);
+
+    /* -------- W section -------- */
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) /* :1170-1172 */
+        for (int k = 0; k < L; k++) CW(w, c, k) = 0.0;
+    double *ru_edge_w = D(ru_edge_w), *flux_arr = D(flux_arr);
+    double *adv_coefs = D(adv_coefs), *adv_coefs_3rd = D(adv_coefs_3rd);
+    int32_t *nAdv = I(nAdvCellsForEdge), *advCells = I(advCellsForEdge);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) { /* :1174-1197 (Q13) */
+        int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+        for (int k = 0; k < L; k++) {
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                if (k > 0) CW(ru_edge_w, c, k) = fzm[k] * re(S, ru, iEdge, k) + fzp[k] * re(S, ru, iEdge, k - 1);
+                CW(flux_arr, c, k) = 0.0;
+                int na = ie2(S, nAdv, iEdge, 1, 0);
+                for (int j = 0; j < na; j++) {
+                    int iAdvCell = ie2(S, advCells, iEdge, 15, j);
+                    if (k > 0) {
+                        double scalar_weight = re2(S, adv_coefs, iEdge, 15, j) +
+                                               copysign(1.0, CW(ru_edge_w, c, k)) * re2(S, adv_coefs_3rd, iEdge, 15, j);
+                        CW(flux_arr, c, k) += scalar_weight * rc(S, w, iAdvCell, k);
+                    }
+                }
+            }
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) { /* :1199-1205 */
+        int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+        for (int k = 0; k < L; k++)
+            for (int i = 0; i < ne; i++)
+                if (k > 0) CW(w, c, k) -= rc2(S, eocs, c, 10, i) * CW(ru_edge_w, c, k) * CW(flux_arr, c, k);
+    }
+    double *rho_zz = D(rho_zz), *uRZ = D(uReconstructZonal), *uRM = D(uReconstructMeridional);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) { /* :1208-1218 */
+        double coslat = cos(rc2(S, D(lat), c, 1, 0));
+        for (int k = 1; k < L; k++) {
+            double a = fzm[k] * CW(uRZ, c, k) + fzp[k] * CW(uRZ, c, k - 1);
+            double b = fzm[k] * CW(uRM, c, k) + fzp[k] * CW(uRM, c, k - 1);
+            CW(w, c, k) += (CW(rho_zz, c, k) * fzm[k] + CW(rho_zz, c, k - 1) * fzp[k]) * ((a * a) + (b * b)) / r_earth +
+                           2.0 * omega_c * coslat * (fzm[k] * CW(uRZ, c, k) + fzp[k] * CW(uRZ, c, k - 1)) *
+                               (CW(rho_zz, c, k) * fzm[k] + CW(rho_zz, c, k - 1) * fzp[k]);
+        }
+    }
+    double *delsq_w = D(delsq_w), *tend_w_euler = D(tend_w_euler);
+    double *msd2 = D(meshScalingDel2), *msd4 = D(meshScalingDel4);
+    if (rk_step == 0) { /* :1224-1274 */
+#pragma omp parallel for schedule(static)
+        for (long c = 0; c < nC; c++) {
+            int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+            for (int k = 0; k < L; k++) {
+                CW(delsq_w, c, k) = 0.0;
+                CW(tend_w_euler, c, k) = 0.0;
+                double r_areaCell = rc2(S, invAreaCell, c, 1, 0);
+                for (int i = 0; i < ne; i++) {
+                    int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                    double edge_sign = 0.5 * r_areaCell * rc2(S, eocs, c, 10, i) * re2(S, dvEdge, iEdge, 1, 0) * re2(S, invDcEdge, iEdge, 1, 0);
+                    int cell1 = ie2(S, cellsOnEdge, iEdge, 2, 0), cell2 = ie2(S, cellsOnEdge, iEdge, 2, 1);
+                    if (k > 0) {
+                        double w_turb_flux = edge_sign * (re(S, rho_edge, iEdge, k) + re(S, rho_edge, iEdge, k - 1)) *
+                                             (rc(S, w, cell2, k) - rc(S, w, cell1, k));
+                        CW(delsq_w, c, k) += w_turb_flux;
+                        w_turb_flux *= re2(S, msd2, iEdge, 1, 0) * 0.25 *
+                                       (rc(S, kdiff, cell1, k) + rc(S, kdiff, cell2, k) + rc(S, kdiff, cell1, k - 1) + rc(S, kdiff, cell2, k - 1));
+                        CW(tend_w_euler, c, k) += w_turb_flux;
+                    }
+                }
+            }
+        }
+        if (h_mom_eddy_visc4 > 0.0) {
+#pragma omp parallel for schedule(static)
+            for (long c = 0; c < nC; c++) {
+                int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+                double r_areaCell = h_mom_eddy_visc4 * rc2(S, invAreaCell, c, 1, 0);
+                for (int k = 0; k < L; k++)
+                    for (int i = 0; i < ne; i++) {
+                        int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                        int cell1 = ie2(S, cellsOnEdge, iEdge, 2, 0), cell2 = ie2(S, cellsOnEdge, iEdge, 2, 1);
+                        double edge_sign = re2(S, msd4, iEdge, 1, 0) * r_areaCell * re2(S, dvEdge, iEdge, 1, 0) *
+                                           rc2(S, eocs, c, 10, i) * re2(S, invDcEdge, iEdge, 1, 0);
+                        if (k > 0) CW(tend_w_euler, c, k) -= edge_sign * (rc(S, delsq_w, cell2, k) - rc(S, delsq_w, cell1, k));
+                    }
+            }
+        }
+    }
+    double *wdwz = D(wdwz), *cqw = D(cqw);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        for (int k = 0; k < L; k++) { /* :1277-1287 */
+            CW(wdwz, c, k) = 0.0;
+            if (k == 1 || k == L - 1)
+                CW(wdwz, c, k) = 0.25 * (CW(rw, c, k) + CW(rw, c, k - 1)) * (CW(w, c, k) + CW(w, c, k - 1));
+            if (k > 1 && k < L - 1)
+                CW(wdwz, c, k) = flux3(CW(w, c, k - 2), CW(w, c, k - 1), CW(w, c, k), rc(S, w, c, k + 1),
+                                       0.5 * (CW(rw, c, k) + CW(rw, c, k - 1)), 1.0);
+        }
+        for (int k = 0; k < L; k++) { /* :1289-1302 (Q14 literal) */
+            if (k > 0) CW(w, c, k) *= rc2(S, invAreaCell, c, 1, 0) - rdzu[k] * (rc(S, wdwz, c, k + 1) - CW(wdwz, c, k));
+            if (rk_step == 0 && k > 0)
+                CW(tend_w_euler, c, k) -= CW(cqw, c, k) * (rdzu[k] * (CW(pressure_p, c, k) - CW(pressure_p, c, k - 1)) -
+                                                           (fzm[k] * CW(dpdz, c, k) + fzp[k] * CW(dpdz, c, k - 1)));
+        }
+        for (int k = 1; k < L; k++) CW(w, c, k) += CW(tend_w_euler, c, k); /* :1318-1322 */
+    }
+
+    /* -------- theta section -------- */
+    double *tend_theta = D(tend_theta), *theta_m = D(theta_m), *ru_save = D(ru_save), *tms = D(theta_m_save);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) { /* :1328-1344 */
+        int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+        for (int k = 0; k < L; k++) {
+            CW(tend_theta, c, k) = 0.0;
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                CW(flux_arr, c, k) = 0.0;
+                int na = ie2(S, nAdv, iEdge, 1, 0);
+                for (int j = 0; j < na; j++) {
+                    int iAdvCell = ie2(S, advCells, iEdge, 15, j);
+                    double scalar_weight = re2(S, adv_coefs, iEdge, 15, j) +
+                                           copysign(1.0, re(S, ru, iEdge, k)) * re2(S, adv_coefs_3rd, iEdge, 15, j);
+                    CW(flux_arr, c, k) += scalar_weight * rc(S, theta_m, iAdvCell, k);
+                }
+                CW(tend_theta, c, k) -= rc2(S, eocs, c, 10, i) * re(S, ru, iEdge, k) * CW(flux_arr, c, k);
+            }
+        }
+    }
+    if (rk_step > 0) { /* :1347-1360 */
+#pragma omp parallel for schedule(static)
+        for (long c = 0; c < nC; c++) {
+            int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+            for (int k = 0; k < L; k++)
+                for (int i = 0; i < ne; i++) {
+                    int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                    int cell1 = ie2(S, cellsOnEdge, iEdge, 2, 0), cell2 = ie2(S, cellsOnEdge, iEdge, 2, 1);
+                    double flux = rc2(S, eocs, c, 10, i) * re2(S, dvEdge, iEdge, 1, 0) *
+                                  (re(S, ru_save, iEdge, k) - re(S, ru, iEdge, k)) * 0.5 *
+                                  (rc(S, tms, cell2, k) + rc(S, tms, cell1, k));
+                    CW(tend_theta, c, k) -= flux;
+                }
+        }
+    }
+    double *delsq_theta = D(delsq_theta), *tend_theta_euler = D(tend_theta_euler);
+    if (rk_step == 0) { /* :1364-1401 */
+#pragma omp parallel for schedule(static)
+        for (long c = 0; c < nC; c++) {
+            int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+            double r_areaCell = rc2(S, invAreaCell, c, 1, 0);
+            for (int k = 0; k < L; k++) {
+                CW(delsq_theta, c, k) = 0.0;
+                CW(tend_theta_euler, c, k) = 0.0;
+                for (int i = 0; i < ne; i++) {
+                    int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                    double edge_sign = r_areaCell * rc2(S, eocs, c, 10, i) * re2(S, dvEdge, iEdge, 1, 0) * re2(S, invDcEdge, iEdge, 1, 0);
+                    double pr_scale = prandtl_inv * re2(S, msd2, iEdge, 1, 0);
+                    int cell1 = ie2(S, cellsOnEdge, iEdge, 2, 0), cell2 = ie2(S, cellsOnEdge, iEdge, 2, 1);
+                    double theta_turb_flux = edge_sign * (rc(S, theta_m, cell2, k) - rc(S, theta_m, cell1, k)) * re(S, rho_edge, iEdge, k);
+                    CW(delsq_theta, c, k) += theta_turb_flux;
+                    theta_turb_flux *= 0.5 * (rc(S, kdiff, cell1, k) + rc(S, kdiff, cell2, k)) * pr_scale;
+                    CW(tend_theta_euler, c, k) += theta_turb_flux;
+                }
+            }
+        }
+        if (h_theta_eddy_visc4 > 0.0) {
+#pragma omp parallel for schedule(static)
+            for (long c = 0; c < nC; c++) {
+                int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+                double r_areaCell = h_theta_eddy_visc4 * prandtl_inv * rc2(S, invAreaCell, c, 1, 0);
+                for (int k = 0; k < L; k++)
+                    for (int i = 0; i < ne; i++) {
+                        int iEdge = ic2(S, edgesOnCell, c, 10, i);
+                        double edge_sign = re2(S, msd4, iEdge, 1, 0) * r_areaCell * re2(S, dvEdge, iEdge, 1, 0) *
+                                           rc2(S, eocs, c, 10, i) * re2(S, invDcEdge, iEdge, 1, 0);
+                        int cell1 = ie2(S, cellsOnEdge, iEdge, 2, 0), cell2 = ie2(S, cellsOnEdge, iEdge, 2, 1);
+                        CW(tend_theta_euler, c, k) -= edge_sign * (rc(S, delsq_theta, cell2, k) - rc(S, delsq_theta, cell1, k));
+                    }
+            }
+        }
+    }
+    double *wdtz = D(wdtz), *rw_save = D(rw_save);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        for (int k = 0; k < L; k++) { /* :1406-1420 (Q15 literal order) */
+            CW(wdtz, c, k) = 0.0;
+            if (k > 0 && k < L - 1)
+                CW(wdtz, c, k) = ((CW(rw_save, c, k) - CW(rw, c, k)) * (fzm[k] * CW(tms, c, k) + fzp[k] * CW(tms, c, k - 1)));
+            if (k == 1) CW(wdtz, c, k) += CW(rw, c, k) * (fzm[k] * CW(theta_m, c, k) + fzp[k] * CW(theta_m, c, k - 1));
+            if (k == L - 1) CW(wdtz, c, k) = CW(rw_save, c, k) * (fzm[k] * CW(tms, c, k) + fzp[k] * rc(S, tms, c, k - 1));
+        }
+        for (int k = 0; k < L; k++) { /* :1422-1427 */
+            CW(tend_theta, c, k) *= rc2(S, invAreaCell, c, 1, 0) - rdzw[k] * (rc(S, wdtz, c, k + 1) - CW(wdtz, c, k));
+            CW(D(tend_rtheta_adv), c, k) = CW(tend_theta, c, k);
+            CW(D(rthdynten), c, k) = CW(tend_theta, c, k) / CW(rho_zz, c, k);
+            CW(tend_theta, c, k) += CW(rho_zz, c, k) * CW(D(rt_diabatic_tend), c, k);
+        }
+        for (int k = 0; k < L; k++) /* :1477-1479 */
+            CW(tend_theta, c, k) += CW(tend_theta_euler, c, k) + CW(D(tend_rtheta_physics), c, k);
+    }
+}
+
+/* ===================== atm_set_smlstep_pert_variables_work, dynamics_tasks.rg:1503-1528
+ * The iteration space "points of cpr" is the explicit mask cprMask[cell][k] (Q6);
+ * "{iCell, iCell.y}" (:1522) is read as {iCell.x, iCell.y} (Q22).                    */
+void ora_atm_set_smlstep_pert_variables_work(ora_state* S) {
+    const int L = S->L, nC = S->nCells;
+    double *w = D(w), *zz = D(zz), *u_tend = D(u_tend), *fzm = D(fzm), *fzp = D(fzp);
+    uint8_t* mask = B(cprMask);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int k = 0; k <= L; k++) {
+            if (!mask[c * LV + k]) continue;
+            if (ic2(S, I(bdyMaskCell), c, 1, 0) <= nRelaxZone) {
+                for (int i = 0; i < ne; i++) {
+                    int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                    double flux = rc2(S, D(edgesOnCell_sign), c, 10, i) *
+                                  (rz(S, fzm, k) * re(S, u_tend, iEdge, k) + rz(S, fzp, k) * re(S, u_tend, iEdge, k - 1));
+                    CW(w, c, k) -= (rc3v(S, D(zb_cell), c, k, i) + copysign(1.0, re(S, u_tend, iEdge, k)) * rc3v(S, D(zb3_cell), c, k, i)) * flux;
+                }
+                CW(w, c, k) *= (rz(S, fzm, k) * CW(zz, c, k) + rz(S, fzp, k) * rc(S, zz, c, k - 1));
+            }
+        }
+    }
+}
+
+/* ===================== atm_advance_acoustic_step_work, dynamics_tasks.rg:1546-1705
+ * Q18 (ru_p update commented out), Q19 (rs/ts reset per point), Q20 (k-1 values read
+ * after their update), Q21 (no back substitution) are all literal.
+ * "{iCell, 0}" at :1638 is read as {iCell.x, 0} (Q22).                               */
+void ora_atm_advance_acoustic_step_work(ora_state* S, double dts, int small_step) {
+    const int L = S->L, nC = S->nCells;
+    double epssm = config_epssm;
+    double rcv = rgas / (CP - rgas);
+    double c2 = CP * rcv;
+    (void)c2;
+    double resm = (1.0 - epssm) / (1.0 + epssm);
+    double *rtheta_pp_old = D(rtheta_pp_old), *rtheta_pp = D(rtheta_pp), *rho_pp = D(rho_pp);
+    double *wwAvg = D(wwAvg), *rw_p = D(rw_p);
+    double *cofrz = D(cofrz), *rdzw = D(rdzw), *fzm = D(fzm), *fzp = D(fzp);
+    double *zz = D(zz), *theta_m = D(theta_m), *ru_p = D(ru_p), *coftz = D(coftz), *w = D(w);
+    /* :1581-1613: both edge-loop bodies are commented out in the reference */
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        double rs[128], ts[128];
+        for (int k = 0; k < L; k++) /* :1615-1623 */
+            CW(rtheta_pp_old, c, k) = (small_step == 0) ? 0 : CW(rtheta_pp, c, k);
+        for (int k = 0; k <= L; k++) /* :1625-1630 */
+            if (small_step == 0) {
+                CW(wwAvg, c, k) = 0;
+                CW(rw_p, c, k) = 0;
+            }
+        for (int k = 0; k < L; k++) { /* :1632-1704 */
+            if (small_step == 0) {
+                CW(rho_pp, c, k) = 0;
+                CW(rtheta_pp, c, k) = 0;
+            }
+            if (rc2(S, D(specZoneMaskCell), c, 1, 0) == 0.0) {
+                for (int i = 0; i < L; i++) {
+                    ts[i] = 0;
+                    rs[i] = 0;
+                }
+                for (int i = 0; i < ne; i++) {
+                    int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                    int cell1 = ie2(S, I(cellsOnEdge), iEdge, 2, 0), cell2 = ie2(S, I(cellsOnEdge), iEdge, 2, 1);
+                    double flux = rc2(S, D(edgesOnCellSign), c, 10, i) * dts * re2(S, D(dvEdge), iEdge, 1, 0) *
+                                  re(S, ru_p, iEdge, k) * rc2(S, D(invAreaCell), c, 1, 0);
+                    rs[k] -= flux;
+                    ts[k] -= flux * 0.5 * (rc(S, theta_m, cell2, k) + rc(S, theta_m, cell1, k));
+                }
+                rs[k] = CW(rho_pp, c, k) + dts * CW(D(tend_rho), c, k) + rs[k] -
+                        cofrz[k] * resm * (rc(S, rw_p, c, k + 1) - CW(rw_p, c, k));
+                ts[k] = CW(rtheta_pp, c, k) + dts * CW(theta_m, c, k) + ts[k] -
+                        resm * rdzw[k] * (rc(S, coftz, c, k + 1) * rc(S, rw_p, c, k + 1) - CW(coftz, c, k) * CW(rw_p, c, k));
+                if (k > 0) {
+                    double tsm = ts[k - 1], rsm = rs[k - 1];
+                    CW(wwAvg, c, k) += 0.5 * (1.0 - epssm) * CW(rw_p, c, k);
+                    CW(rw_p, c, k) += dts * CW(w, c, k) -
+                                      CW(D(cofwz), c, k) * ((CW(zz, c, k) * ts[k] - CW(zz, c, k - 1) * tsm) +
+                                                            resm * (CW(zz, c, k) * CW(rtheta_pp, c, k) - CW(zz, c, k - 1) * CW(rtheta_pp, c, k - 1))) -
+                                      CW(D(cofwr), c, k) * ((rs[k] + rsm) + resm * (CW(rho_pp, c, k) + CW(rho_pp, c, k - 1))) +
+                                      CW(D(cofwt), c, k) * (ts[k] + resm * CW(rtheta_pp, c, k)) +
+                                      CW(D(cofwt), c, k - 1) * (tsm + resm * CW(rtheta_pp, c, k - 1));
+                    CW(rw_p, c, k) -= CW(D(a_tri), c, k) * CW(rw_p, c, k - 1);
+                    CW(rw_p, c, k) *= CW(D(alpha_tri), c, k);
+                }
+                if (k > 0) { /* :1681-1690 */
+                    CW(rw_p, c, k) += (CW(D(rw_save), c, k) - CW(D(rw), c, k)) -
+                                      dts * CW(D(dss), c, k) * (fzm[k] * CW(zz, c, k) + fzp[k] * CW(zz, c, k - 1)) *
+                                          (fzm[k] * CW(D(rho_zz), c, k) + fzp[k] * CW(D(rho_zz), c, k - 1)) * CW(w, c, k);
+                    CW(rw_p, c, k) /= (1.0 + dts * CW(D(dss), c, k));
+                    CW(rw_p, c, k) -= (CW(D(rw_save), c, k) - CW(D(rw), c, k));
+                    CW(wwAvg, c, k) += 0.5 * (1.0 + epssm) * CW(rw_p, c, k);
+                }
+                CW(rho_pp, c, k) = rs[k] - cofrz[k] * (rc(S, rw_p, c, k + 1) - CW(rw_p, c, k));
+                CW(rtheta_pp, c, k) = ts[k] - rdzw[k] * (rc(S, coftz, c, k + 1) * rc(S, rw_p, c, k + 1) - CW(coftz, c, k) * CW(rw_p, c, k));
+            } else { /* :1698-1703 */
+                CW(rho_pp, c, k) = CW(rho_pp, c, k) + dts * CW(D(tend_rho), c, k);
+                CW(rtheta_pp, c, k) = CW(rtheta_pp, c, k) + dts * CW(theta_m, c, k);
+                CW(rw_p, c, k) = CW(rw_p, c, k) + dts * CW(w, c, k);
+                CW(wwAvg, c, k) = CW(wwAvg, c, k) + 0.5 * (1.0 + epssm) * CW(rw_p, c, k);
+            }
+        }
+    }
+}
+
+/* ===================== atm_divergence_damping_3d, dynamics_tasks.rg:1726-1763
+ * cellOne/cellTwo are the rects built from cellsOnEdge (mesh_loading.rg:422-425);
+ * isShared is read at level 0 of the whole cell field (Q6).                          */
+void ora_atm_divergence_damping_3d(ora_state* S, double dts) {
+    const int L = S->L;
+    double smdiv = config_smdiv;
+    double rdts = 1.0 / dts;
+    double coef_divdamp = 2.0 * smdiv * config_len_disp * rdts;
+    double *ru_p = D(ru_p), *rtp = D(rtheta_pp), *rtpo = D(rtheta_pp_old), *tm = D(theta_m);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < S->nEdges; e++) {
+        int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        if (!(ic2(S, I(isShared), cell1, 1, 0) && ic2(S, I(isShared), cell2, 1, 0))) {
+            for (int k = 0; k < L; k++) {
+                double divCell1 = -(rc(S, rtp, cell1, k) - rc(S, rtpo, cell1, k));
+                double divCell2 = -(rc(S, rtp, cell2, k) - rc(S, rtpo, cell2, k));
+                CW(ru_p, e, k) += coef_divdamp * (divCell2 - divCell1) * (1.0 - re2(S, D(specZoneMaskEdge), e, 1, 0)) /
+                                  (rc(S, tm, cell1, k) + rc(S, tm, cell2, k));
+            }
+        }
+    }
+}
+
+/* ===================== atm_rk_dynamics_substep_finish, dynamics_tasks.rg:1951-2007 */
+void ora_atm_rk_dynamics_substep_finish(ora_state* S, int dynamics_substep, int dynamics_split) {
+    const int L = S->L;
+    double inv_dynamics_split = 1.0 / (double)dynamics_split;
+    if (dynamics_substep < dynamics_split) {
+#pragma omp parallel for schedule(static)
+        for (long e = 0; e < S->nEdges; e++)
+            for (int k = 0; k < L; k++) {
+                CW(D(ru_save), e, k) = CW(D(ru), e, k);
+                CW(D(u), e, k) = CW(D(u_2), e, k);
+            }
+#pragma omp parallel for schedule(static)
+        for (long c = 0; c < S->nCells; c++)
+            for (int k = 0; k < L; k++) {
+                CW(D(rw_save), c, k) = CW(D(rw), c, k);
+                CW(D(rtheta_p_save), c, k) = CW(D(rtheta_p), c, k);
+                CW(D(rho_p_save), c, k) = CW(D(rho_p), c, k);
+                CW(D(w), c, k) = CW(D(w_2), c, k);
+                CW(D(theta_m), c, k) = CW(D(theta_m_2), c, k);
+                CW(D(rho_zz), c, k) = CW(D(rho_zz_2), c, k);
+            }
+    }
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < S->nEdges; e++)
+        for (int k = 0; k < L; k++) {
+            if (dynamics_substep == 1) CW(D(ruAvg_split), e, k) = CW(D(ruAvg), e, k);
+            else CW(D(ruAvg_split), e, k) = CW(D(ruAvg), e, k) + CW(D(ruAvg_split), e, k);
+            if (dynamics_substep == dynamics_split) CW(D(ruAvg), e, k) = CW(D(ruAvg_split), e, k) * inv_dynamics_split;
+        }
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < S->nCells; c++)
+        for (int k = 0; k < L; k++) {
+            if (dynamics_substep == 1) CW(D(wwAvg_split), c, k) = CW(D(wwAvg), c, k);
+            else CW(D(wwAvg_split), c, k) = CW(D(wwAvg), c, k) + CW(D(wwAvg_split), c, k);
+            if (dynamics_substep == dynamics_split) {
+                CW(D(wwAvg), c, k) = CW(D(wwAvg_split), c, k) * inv_dynamics_split;
+                CW(D(rho_zz), c, k) = CW(D(rho_zz_old_split), c, k);
+            }
+        }
+}
+
+/* ===================== atm_srk3, rk_timestep.rg:361-500
+ * schedule 0: the reference's own driver, with Q4 (rk_sub_timestep[rk_step] truncated
+ *             into dyn_tend's int rk_step) and Q5 (n+1 acoustic substeps);
+ * schedule 1: dyn_tend gets rk_step = 0,1,2 (the MPAS schedule, SURVEY §8.5 bench).   */
+void ora_atm_srk3(ora_state* S, double dt, int schedule) {
+    int number_of_sub_steps = 2;
+    int dynamics_split = 1;
+    double dt_dynamics = dt;
+    double rk_sub_timestep[3] = {dt_dynamics / 3, dt_dynamics / number_of_sub_steps, dt_dynamics / number_of_sub_steps};
+    int number_sub_steps[3];
+    number_sub_steps[0] = (number_of_sub_steps / 2 > 1) ? number_of_sub_steps / 2 : 1;
+    number_sub_steps[1] = number_sub_steps[0];
+    number_sub_steps[2] = number_of_sub_steps;
+    ora_atm_rk_integration_setup(S);
+    ora_atm_compute_moist_coefficients(S);
+    ora_atm_compute_vert_imp_coefs(S, rk_sub_timestep[0]);
+    for (int rk_step = 0; rk_step < 3; rk_step++) {
+        if (rk_step == 1) ora_atm_compute_vert_imp_coefs(S, rk_sub_timestep[rk_step]);
+        int dyn_rk = schedule == 0 ? (int)rk_sub_timestep[rk_step] : rk_step;
+        ora_atm_compute_dyn_tend_work(S, dyn_rk, dt, 0, 0.0, 0, 0);
+        ora_atm_set_smlstep_pert_variables_work(S);
+        for (int small_step = 0; small_step < number_sub_steps[rk_step] + 1; small_step++) {
+            ora_atm_advance_acoustic_step_work(S, rk_sub_timestep[rk_step], small_step);
+            ora_atm_divergence_damping_3d(S, rk_sub_timestep[rk_step]);
+        }
+        ora_atm_compute_solve_diagnostics(S, 0, rk_step);
+    }
+    ora_atm_rk_dynamics_substep_finish(S, 1, dynamics_split);
+}
+
+/* ===================== synthetic state (test/bench inputs, not reference semantics) */
+static const struct { int kind, width, dist; double lo, hi; } ora_fields[] = {
+#define C3 0
+#define C3V 1
+#define E3 2
+#define V3 3
+#define C2F 4
+#define C2I 5
+#define E2F 6
+#define E2I 7
+#define V2F 8
+#define V2I 9
+#define C3B 10
+#define ZV 11
+#define U MPAS_DIST_U
+#define M MPAS_DIST_M
+#define MPAS_FIELD(name, KIND, W, DIST, LO, HI) {KIND, W, DIST, LO, HI},
+#include "mpas_fields.def"
+#undef MPAS_FIELD
+};
+
+int ora_field_count(void) { return F_COUNT; }
+
+/* Fill every U/Z/B/S field (and, with include_mesh, the fp64 M fields) of the state
+ * from the counter-based generator; row n (zero slot) is left untouched.           */
+void ora_fill_synthetic(ora_state* S, uint64_t seed, int include_mesh) {
+    for (int f = 0; f < F_COUNT; f++) {
+        int kind = ora_fields[f].kind, W = ora_fields[f].width, dist = ora_fields[f].dist;
+        double lo = ora_fields[f].lo, hi = ora_fields[f].hi;
+        if (dist == MPAS_DIST_M) {
+            if (!include_mesh) continue;
+            if (kind != C2F && kind != E2F && kind != V2F) continue;
+            dist = MPAS_DIST_U;
+        }
+        double* p = (double*)S->f[f];
+        long n = 0;
+        int levels = 0;
+        switch (kind) {
+            case C3: n = S->nCells; levels = S->L + 1; break;
+            case E3: n = S->nEdges; levels = S->L + 1; break;
+            case V3: n = S->nVertices; levels = S->L + 1; break;
+            case C3V: n = S->nCells; levels = S->L + 1; break;
+            case C2F: n = S->nCells; break;
+            case E2F: n = S->nEdges; break;
+            case V2F: n = S->nVertices; break;
+            case ZV: n = 1; levels = S->L + 1; break;
+            default: continue;
+        }
+        if (kind == C3 || kind == E3 || kind == V3) {
+#pragma omp parallel for schedule(static)
+            for (long e = 0; e < n; e++)
+                for (int k = 0; k < levels; k++)
+                    p[e * levels + k] = mpas_synth_value(seed, f, e, k, 0, dist, lo, hi);
+        } else if (kind == C3V) {
+#pragma omp parallel for schedule(static)
+            for (long e = 0; e < n; e++)
+                for (int k = 0; k < levels; k++)
+                    for (int i = 0; i < W; i++)
+                        p[(e * levels + k) * W + i] = mpas_synth_value(seed, f, e, k, i, dist, lo, hi);
+        } else if (kind == ZV) {
+            for (int k = 0; k < levels; k++) p[k] = mpas_synth_value(seed, f, 0, k, 0, dist, lo, hi);
+        } else {
+#pragma omp parallel for schedule(static)
+            for (long e = 0; e < n; e++)
+                for (int i = 0; i < W; i++) p[e * W + i] = mpas_synth_value(seed, f, e, 0, i, dist, lo, hi);
+        }
+    }
+}

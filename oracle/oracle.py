@@ -1,0 +1,113 @@
+"""ctypes driver of the CPU oracle (oracle/mpas_oracle.c) -- TEST INFRASTRUCTURE ONLY.
+
+Imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, always as
+the checker, never by the product package.  PARITY UNPINNED (see mpas_oracle.c).
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "mpas-regent_amd"))
+from mpasdyn.registry import FIELDS, F_COUNT  # noqa: E402
+
+LIB_PATH = os.path.join(HERE, "libmpas_oracle.so")
+HORIZ = {"2d_smagorinsky": 0, "2d_fixed": 1}
+
+
+class OraState(ctypes.Structure):
+    _fields_ = [("nCells", ctypes.c_int32), ("nEdges", ctypes.c_int32), ("nVertices", ctypes.c_int32),
+                ("L", ctypes.c_int32), ("f", ctypes.c_void_p * F_COUNT)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        p = ctypes.POINTER(OraState)
+        i32, dbl = ctypes.c_int, ctypes.c_double
+        sig = {
+            "ora_field_count": (i32, []),
+            "ora_fill_synthetic": (None, [p, ctypes.c_uint64, i32]),
+            "ora_atm_rk_integration_setup": (None, [p]),
+            "ora_atm_compute_moist_coefficients": (None, [p]),
+            "ora_atm_compute_vert_imp_coefs": (None, [p, dbl]),
+            "ora_atm_compute_dyn_tend_work": (None, [p, i32, dbl, i32, dbl, i32, i32]),
+            "ora_atm_set_smlstep_pert_variables_work": (None, [p]),
+            "ora_atm_advance_acoustic_step_work": (None, [p, dbl, i32]),
+            "ora_atm_divergence_damping_3d": (None, [p, dbl]),
+            "ora_atm_compute_solve_diagnostics": (None, [p, i32, i32]),
+            "ora_atm_rk_dynamics_substep_finish": (None, [p, i32, i32]),
+            "ora_atm_srk3": (None, [p, dbl, i32]),
+        }
+        for n, (res, args) in sig.items():
+            fn = getattr(L, n)
+            fn.restype, fn.argtypes = res, args
+        assert L.ora_field_count() == F_COUNT, "oracle built from a different mpas_fields.def"
+        _lib = L
+    return _lib
+
+
+class Oracle:
+    """Runs the reference tasks on a HostState in place."""
+
+    def __init__(self, state):
+        self.state = state
+        self.lib = load()
+        s = OraState()
+        s.nCells, s.nEdges, s.nVertices, s.L = state.dims()
+        assert state.L < 128
+        for f in FIELDS:
+            a = state.arrays[f.name]
+            assert a.flags.c_contiguous
+            s.f[f.index] = a.ctypes.data
+        self.s = s
+        self.p = ctypes.byref(s)
+
+    def fill_synthetic(self, seed, include_mesh=False):
+        self.lib.ora_fill_synthetic(self.p, seed, 1 if include_mesh else 0)
+
+    def atm_rk_integration_setup(self):
+        self.lib.ora_atm_rk_integration_setup(self.p)
+
+    def atm_compute_moist_coefficients(self):
+        self.lib.ora_atm_compute_moist_coefficients(self.p)
+
+    def atm_compute_vert_imp_coefs(self, dts):
+        self.lib.ora_atm_compute_vert_imp_coefs(self.p, dts)
+
+    def atm_compute_dyn_tend_work(self, rk_step, dt, config_horiz_mixing="2d_smagorinsky", config_mpas_cam_coef=0.0,
+                                  config_mix_full=False, config_rayleigh_damp_u=False):
+        hm = config_horiz_mixing if isinstance(config_horiz_mixing, int) else HORIZ.get(config_horiz_mixing, 2)
+        self.lib.ora_atm_compute_dyn_tend_work(self.p, rk_step, dt, hm, config_mpas_cam_coef, int(config_mix_full),
+                                               int(config_rayleigh_damp_u))
+
+    def atm_set_smlstep_pert_variables_work(self):
+        self.lib.ora_atm_set_smlstep_pert_variables_work(self.p)
+
+    def atm_advance_acoustic_step_work(self, dts, small_step):
+        self.lib.ora_atm_advance_acoustic_step_work(self.p, dts, small_step)
+
+    def atm_divergence_damping_3d(self, dts):
+        self.lib.ora_atm_divergence_damping_3d(self.p, dts)
+
+    def atm_compute_solve_diagnostics(self, hollingsworth, rk_step):
+        self.lib.ora_atm_compute_solve_diagnostics(self.p, int(hollingsworth), rk_step)
+
+    def atm_rk_dynamics_substep_finish(self, dynamics_substep, dynamics_split):
+        self.lib.ora_atm_rk_dynamics_substep_finish(self.p, dynamics_substep, dynamics_split)
+
+    def atm_srk3(self, dt, schedule=0):
+        self.lib.ora_atm_srk3(self.p, dt, schedule)
