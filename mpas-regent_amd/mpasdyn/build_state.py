@@ -74,7 +74,7 @@ def compute_signs(m, st):
     st["kiteForCell"][:nC] = np.where(valid, kite, 0)
 
 
-def adv_coef_compression(m, st, dcEdge, dvEdge, deriv_two=None):
+def adv_coef_compression_loops(m, st, dcEdge, dvEdge, deriv_two=None):
     """atm_adv_coef_compression, dynamics_tasks.rg:133-269, with its quirks:
     nAdvCellsForEdge = n is the index of the last list entry (so the last cell is never
     used), the list is capped at maxEdges-1 (:175), ids are raw (Q1), deriv_two is a Q2
@@ -154,6 +154,53 @@ def adv_coef_compression(m, st, dcEdge, dvEdge, deriv_two=None):
     st["advCellsForEdge"][:nE] = advc
     st["adv_coefs"][:nE] = ac
     st["adv_coefs_3rd"][:nE] = ac3 * 0.25  # atm_couple_coef_3rd_order, :313-317
+
+
+def adv_coef_compression(m, st, dcEdge, dvEdge):
+    """Vectorised form of adv_coef_compression_loops for deriv_two = 0 (Q2), the case
+    on the path; tests/test_state.py checks it against the loop restatement."""
+    nC, nE = m.nCells, m.nEdges
+    nEoC = np.zeros(nC + 1, np.int64)
+    nEoC[:nC] = m.nEdgesOnCell
+    coc = np.zeros((nC + 1, 10), np.int64)
+    coc[:nC] = m.cellsOnCell
+    cell1 = m.cellsOnEdge[:, 0].astype(np.int64)
+    cell2 = m.cellsOnEdge[:, 1].astype(np.int64)
+    c1, c2 = np.minimum(cell1, nC), np.minimum(cell2, nC)
+    cl = np.zeros((nE, 10), np.int64)
+    cl[:, 0], cl[:, 1] = cell1, cell2
+    n = np.ones(nE, np.int64)
+    rows = np.arange(nE)
+    for i in range(10):
+        cand = coc[c1, i]
+        add = (i < nEoC[c1]) & (cand != cell2)
+        n = np.where(add, n + 1, n)
+        cl[rows[add], n[add]] = cand[add]
+    for ic in range(10):
+        cand = coc[c2, ic]
+        present = np.zeros(nE, bool)
+        for i in range(10):
+            present |= (i < n) & (cl[:, i] == cand)
+        add = (ic < nEoC[c2]) & ~present & (n < 10 - 1)
+        n = np.where(add, n + 1, n)
+        cl[rows[add], n[add]] = cand[add]
+    j = np.arange(15)[None, :]
+    inl = j < n[:, None]
+    advc = np.zeros((nE, 15), np.int32)
+    advc[:, :10] = np.where(inl[:, :10], cl, 0)
+    a = np.where(inl, -0.0, 0.0) * np.ones((nE, 15))  # -1.0*dc^2*0/12 for j < n
+    a3 = a.copy()
+    for target in (cell1, cell2):
+        j_in = np.zeros(nE, np.int64)
+        for jj in range(10):
+            j_in = np.where((jj < n) & (cl[:, jj] == target), jj, j_in)
+        a[rows, j_in] += 0.5
+    a = np.where(inl, a * dvEdge[:, None], a)
+    a3 = np.where(inl, a3 * dvEdge[:, None], a3)
+    st["nAdvCellsForEdge"][:nE, 0] = n
+    st["advCellsForEdge"][:nE] = advc
+    st["adv_coefs"][:nE] = a
+    st["adv_coefs_3rd"][:nE] = a3 * 0.25  # atm_couple_coef_3rd_order, :313-317
 
 
 def mesh_scaling(m, st, meshDensity):

@@ -1,0 +1,110 @@
+"""Algorithmic bytes (B_alg) per task launch, SURVEY §8.5:
+
+    B_alg = sum over the distinct arrays a task reads as inputs (once each)
+          + sum over the distinct arrays it writes (once each)
+
+3-D fp64 arrays count 8*n_entity*nVertLevels, C3V arrays 10x that, 2-D mesh arrays their
+stored bytes.  The read/write sets are the active-branch subsets of each Regent task's
+privilege clause (dynamics_tasks.rg), without per-task scratch (flux_arr, ru_edge_w,
+wduz, q, wdwz, wdtz, u_mix) and without arrays the task itself writes before reading
+(their re-reads are implementation traffic, not algorithmic bytes).  Vertical 1-D
+arrays are negligible and omitted.  This is the figure the benchmark's
+roofline.achieved divides by the measured launch time.
+"""
+
+# name -> (reads, writes); each a list of field names of the registry
+def _sets(task, rk_step=0, small_step=1, reconstruct_v=False):
+    if task == "atm_rk_integration_setup":
+        return (["rho_p", "rho_zz", "rtheta_p", "rw", "theta_m", "w", "ru", "u"],
+                ["rho_p_save", "rho_zz_2", "rho_zz_old_split", "rtheta_p_save", "rw_save", "theta_m_2", "w_2",
+                 "ru_save", "u_2"])
+    if task == "atm_compute_moist_coefficients":
+        return [], ["qtot", "cqw"]
+    if task == "atm_compute_vert_imp_coefs":
+        return (["cqw", "exner", "exner_base", "qtot", "rho_base", "rtheta_base", "rtheta_p", "theta_m", "zz",
+                 "gamma_tri"],
+                ["a_tri", "b_tri", "c_tri", "alpha_tri", "gamma_tri", "coftz", "cofwr", "cofwt", "cofwz"])
+    if task == "atm_compute_dyn_tend_work":
+        mesh = ["nEdgesOnCell", "edgesOnCell", "edgesOnCell_sign", "invAreaCell", "lat", "cellsOnEdge",
+                "verticesOnEdge", "dvEdge", "invDcEdge", "nEdgesOnEdge", "edgesOnEdge", "weightsOnEdge",
+                "nAdvCellsForEdge", "advCellsForEdge", "adv_coefs", "adv_coefs_3rd", "angleEdge", "latEdge"]
+        if rk_step == 0:
+            mesh += ["defc_a", "defc_b", "dcEdge", "invDvEdge", "meshScalingDel2", "meshScalingDel4",
+                     "edgesOnVertex", "edgesOnVertex_sign", "invAreaTriangle"]
+            reads = ["cqw", "divergence", "ke", "pressure_p", "qtot", "rho_base", "rho_zz", "rho_p_save",
+                     "rt_diabatic_tend", "rw", "rw_save", "tend_rho_physics", "tend_rtheta_physics", "theta_m",
+                     "theta_m_save", "uReconstructZonal", "uReconstructMeridional", "w", "zz",
+                     "cqu", "pv_edge", "rho_edge", "ru", "tend_ru_physics", "u", "v", "zxu", "vorticity"]
+            writes = ["rthdynten", "tend_rho", "tend_rtheta_adv", "delsq_divergence", "delsq_theta", "delsq_w",
+                      "dpdz", "h_divergence", "kdiff", "tend_theta", "tend_theta_euler", "w", "tend_w_euler",
+                      "delsq_u", "tend_u", "tend_u_euler", "delsq_vorticity"]
+        else:
+            reads = ["ke", "rho_zz", "rt_diabatic_tend", "rw", "rw_save", "tend_rtheta_physics", "theta_m",
+                     "theta_m_save", "uReconstructZonal", "uReconstructMeridional", "w", "tend_w_euler",
+                     "tend_theta_euler", "pv_edge", "rho_edge", "ru", "ru_save", "tend_ru_physics", "u",
+                     "tend_u_euler"]
+            writes = ["h_divergence", "w", "tend_theta", "tend_rtheta_adv", "rthdynten", "tend_u"]
+        return reads + mesh, writes
+    if task == "atm_set_smlstep_pert_variables_work":
+        return (["zz", "w", "zb_cell", "zb3_cell", "u_tend", "cprMask", "bdyMaskCell", "nEdgesOnCell",
+                 "edgesOnCell", "edgesOnCell_sign"], ["w"])
+    if task == "atm_advance_acoustic_step_work":
+        reads = ["a_tri", "alpha_tri", "coftz", "cofwr", "cofwt", "cofwz", "dss", "rho_zz", "rw", "rw_save",
+                 "tend_rho", "theta_m", "w", "zz", "ru_p", "nEdgesOnCell", "edgesOnCell", "edgesOnCellSign",
+                 "invAreaCell", "cellsOnEdge", "dvEdge", "specZoneMaskCell"]
+        if small_step != 0:
+            reads += ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+        return reads, ["rtheta_pp_old", "rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+    if task == "atm_divergence_damping_3d":
+        return (["rtheta_pp", "rtheta_pp_old", "theta_m", "ru_p", "cellsOnEdge", "isShared", "specZoneMaskEdge"],
+                ["ru_p"])
+    if task == "atm_compute_solve_diagnostics":
+        writes = ["h_edge", "ke_edge", "pv_edge", "divergence", "ke", "vorticity", "pv_vertex"]
+        if reconstruct_v:
+            writes.append("v")
+        return (["h", "u", "cellsOnEdge", "dcEdge", "dvEdge", "edgesOnEdge_ECP", "nEdgesOnEdge", "verticesOnEdge",
+                 "weightsOnEdge", "edgesOnCell", "edgesOnCellSign", "invAreaCell", "nEdgesOnCell", "edgesOnVertex",
+                 "edgesOnVertexSign", "fVertex", "invAreaTriangle"], writes)
+    if task == "atm_rk_dynamics_substep_finish":
+        return (["wwAvg", "rho_zz_old_split", "ruAvg"], ["wwAvg_split", "wwAvg", "rho_zz", "ruAvg_split", "ruAvg"])
+    raise KeyError(task)
+
+
+def field_bytes(name, nCells, nEdges, nVertices, L):
+    from .registry import BY_NAME
+    f = BY_NAME[name]
+    n = {"cell": nCells, "edge": nEdges, "vertex": nVertices, None: 0}[f.entity]
+    if f.kind in ("C3", "E3", "V3"):
+        return 8 * n * L
+    if f.kind == "C3V":
+        return 8 * n * L * f.width
+    if f.kind == "C3B":
+        return n * L
+    if f.kind == "ZV":
+        return 0
+    return n * f.width * (4 if f.kind.endswith("I") else 8)
+
+
+def b_alg(task, dims, **kw):
+    """algorithmic bytes of one launch of `task` at dims = (nCells, nEdges, nVertices, L)"""
+    reads, writes = _sets(task, **kw)
+    return sum(field_bytes(x, *dims) for x in set(reads)) + sum(field_bytes(x, *dims) for x in set(writes))
+
+
+def step_schedule(schedule=1):
+    """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481)"""
+    out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
+           ("atm_compute_vert_imp_coefs", {}, 2)]
+    if schedule == 1:
+        out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
+    out += [("atm_set_smlstep_pert_variables_work", {}, 3),
+            ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
+            ("atm_advance_acoustic_step_work", {"small_step": 1}, 4),
+            ("atm_divergence_damping_3d", {}, 7),
+            ("atm_compute_solve_diagnostics", {}, 2), ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
+            ("atm_rk_dynamics_substep_finish", {}, 1)]
+    return out
+
+
+def b_alg_step(dims, schedule=1):
+    return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule))
