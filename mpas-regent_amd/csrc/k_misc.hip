@@ -105,7 +105,8 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
     }
     const double coftz_m = lvl_dn<LP>(coftz, k), coftz_p = lvl_up<LP>(coftz, k);
     const double cofwt_m = lvl_dn<LP>(cofwt, k);
-    const double gamma_m = (k == 1) ? 0.0 : lvl_dn<LP>(gamma_old, k);  // Q17
+    const double gamma_dn = lvl_dn<LP>(gamma_old, k);  // shuffle outside any branch
+    const double gamma_m = (k == 1) ? 0.0 : gamma_dn;  // Q17: gamma(0) was just zeroed
     const double cofrz = dtseps * rdzw, cofrz_m = dtseps * rdzw_m;      // :537-539
 
     if (k < L) {
