@@ -60,21 +60,34 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         return;
     }
 
-    // ---- horizontal flux (:1644-1652)
+    // ---- horizontal flux (:1644-1652): issue the NF edge gathers, then accumulate
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
+    const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
+    const double* cdv = fd(S, X_ce_dv) + (size_t)c * 10;
     const double invA = fd(S, F_invAreaCell)[c];
-    const double *dvEdge = fd(S, F_dvEdge), *ru_p = fd(S, F_ru_p), *tm_f = fd(S, F_theta_m);
-    const int* coe = fi(S, F_cellsOnEdge);
+    const double *ru_p = fd(S, F_ru_p), *tm_f = fd(S, F_theta_m);
     double rs = 0, ts = 0;
     if (k < L) {
-        for (int i = 0; i < ne; i++) {
-            int iEdge = eoc[i];
-            int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
-            double flux = sgn[i] * dts * dvEdge[iEdge] * ru_p[(size_t)iEdge * LP + k] * invA;
+        double rup_[NF], t1_[NF], t2_[NF];
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            rup_[i] = ru_p[(size_t)eoc[i] * LP + k];
+            t1_[i] = tm_f[(size_t)cc1[i] * LP + k];
+            t2_[i] = tm_f[(size_t)cc2[i] * LP + k];
+        }
+#pragma unroll
+        for (int i = 0; i < NF; i++)
+            if (i < ne) {
+                double flux = sgn[i] * dts * cdv[i] * rup_[i] * invA;
+                rs -= flux;
+                ts -= flux * 0.5 * (t2_[i] + t1_[i]);
+            }
+        for (int i = NF; i < ne; i++) {
+            double flux = sgn[i] * dts * cdv[i] * ru_p[(size_t)eoc[i] * LP + k] * invA;
             rs -= flux;
-            ts -= flux * 0.5 * (tm_f[(size_t)cell2 * LP + k] + tm_f[(size_t)cell1 * LP + k]);
+            ts -= flux * 0.5 * (tm_f[(size_t)cc2[i] * LP + k] + tm_f[(size_t)cc1[i] * LP + k]);
         }
     }
     // ---- rs, ts (:1657-1658) from the OLD rw_p

@@ -7,17 +7,22 @@
 //   A  cells    kdiff (rk0, Q11: own level only), h_divergence, tend_rho + dpdz (rk0),
 //               wc = w after the zeroing, horizontal advection (Q13) and curvature
 //   B  edges    tend_u_euler pressure gradient (rk0), wduz (in-lane), tend_u, q (Q10),
-//               ke gradient, curvature (Q12), delsq_u + del2 (rk0), Rayleigh,
-//               and, when no del4 follows, tend_u += tend_u_euler + tend_ru_physics
+//               ke gradient, curvature (Q12), delsq_u + del2 (rk0), Rayleigh, and, when
+//               no del4 follows, tend_u += tend_u_euler + tend_ru_physics; also the
+//               per-edge theta reconstruction flux_arr (F) used by E
 //   C  rk0      vertices: delsq_vorticity; cells: delsq_divergence, delsq_w + del2 of
 //               tend_w_euler, delsq_theta + del2 of tend_theta_euler
 //   D  rk0+del4 edges: del4 of tend_u_euler, tend_u finish
 //   E  cells    del4 of w/theta (rk0), wdwz (in-lane), w scaling (Q14), buoyancy (rk0),
-//               theta advection over advCellsForEdge, perturbation flux (rk>0),
+//               theta advection (F of the cell's edges), perturbation flux (rk>0),
 //               wdtz (Q15, in-lane), tend_theta finish
 // rk_step > 0 runs A, B, E.  Scratch the reference writes to fields (flux_arr,
 // ru_edge_w, wduz, q, wdwz, wdtz, u_mix) stays in registers; only their level-L
 // slots, which the reference never writes, are read from HBM.
+//
+// Memory-level parallelism: every loop over a connectivity list first issues the
+// loads of the first NF/QF/AF entries unconditionally (padding ids are valid), then
+// accumulates in the reference's order; longer lists finish in a generic tail loop.
 #include "mpas_dev.h"
 
 namespace mpas {
@@ -37,6 +42,8 @@ struct DynK {
     double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
 };
 
+#define GCOL(f, ent) (((size_t)(ent)) * LP + k)
+
 // ------------------------------------------------------------------------ A (cells)
 template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
@@ -44,13 +51,33 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
+    const bool rk0 = a.rk_step == 0;
+    const bool live = k <= L;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
-    const double* dvEdge = fd(S, F_dvEdge);
+    const double* cdv = fd(S, X_ce_dv) + (size_t)c * 10;
     const double *u = fd(S, F_u), *v = fd(S, F_v), *ru = fd(S, F_ru);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
-    const bool rk0 = a.rk_step == 0;
+    const bool smag = rk0 && a.horiz_mixing == 0;
+
+    int e_[NF];
+    double ru_[NF], u_[NF], v_[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) e_[i] = eoc[i];
+#pragma unroll
+    for (int i = 0; i < NF; i++) ru_[i] = live ? ru[GCOL(ru, e_[i])] : 0.0;
+    if (smag) {
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            u_[i] = live ? u[GCOL(u, e_[i])] : 0.0;
+            v_[i] = live ? v[GCOL(v, e_[i])] : 0.0;
+        }
+    }
+    const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
+    const double rz = col_rd(fd(S, F_rho_zz), c, k, L, LP);
+    const double urz = col_rd(fd(S, F_uReconstructZonal), c, k, L, LP);
+    const double urm = col_rd(fd(S, F_uReconstructMeridional), c, k, L, LP);
 
     // ---- kdiff (:858-917)
     if (rk0 && (a.horiz_mixing == 0 || a.horiz_mixing == 1 || a.cam_coef > 0.0)) {
@@ -59,7 +86,13 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
             const double* defa = fd(S, F_defc_a) + (size_t)c * 10;
             const double* defb = fd(S, F_defc_b) + (size_t)c * 10;
             double d_diag = 0.0, d_off_diag = 0.0;
-            for (int i = 0; i < ne; i++) {
+#pragma unroll
+            for (int i = 0; i < NF; i++)
+                if (i < ne) {
+                    d_diag += defa[i] * u_[i] - defb[i] * v_[i];
+                    d_off_diag += defb[i] * u_[i] + defa[i] * v_[i];
+                }
+            for (int i = NF; i < ne; i++) {
                 int e = eoc[i];
                 double ue = col_rd(u, e, k, L, LP), ve = col_rd(v, e, k, L, LP);
                 d_diag += defa[i] * ue - defb[i] * ve;
@@ -80,16 +113,20 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 
     // ---- h_divergence (:924-938)
     double hd = 0.0;
-    for (int i = 0; i < ne; i++) {
-        int e = eoc[i];
-        double edge_sign = eocs[i] * dvEdge[e];
-        hd += edge_sign * col_rd(ru, e, k, L, LP);
+#pragma unroll
+    for (int i = 0; i < NF; i++)
+        if (i < ne) {
+            double edge_sign = eocs[i] * cdv[i];
+            hd += edge_sign * ru_[i];
+        }
+    for (int i = NF; i < ne; i++) {
+        double edge_sign = eocs[i] * cdv[i];
+        hd += edge_sign * col_rd(ru, eoc[i], k, L, LP);
     }
     hd *= fd(S, F_invAreaCell)[c];
     if (k < L) fw(S, F_h_divergence)[p] = hd;
 
     // ---- tend_rho, dpdz (:942-951)
-    const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
     const double rw_p1 = lvl_up<LP>(rw, k);
     if (rk0 && k < L) {
         fw(S, F_tend_rho)[p] = -hd - rdzw * (rw_p1 - rw + fd(S, F_tend_rho_physics)[p]);
@@ -102,39 +139,38 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     // slot is 0 too), so flux_arr = sum_j scalar_weight_j * 0.0 of the cell's LAST edge
     // (flux_arr and ru_edge_w are overwritten per edge); it is evaluated literally so
     // that non-finite weights propagate as in the reference.
-    double w0 = 0.0;
-    {
-        const int e_last = ne > 0 ? eoc[ne - 1] : S.nEdges;
-        const double ru_l = col_rd(ru, e_last, k, L, LP);
-        const double ru_lm = lvl_dn<LP>(ru_l, k);
-        if (ne > 0 && k > 0 && k < L) {
-            double ru_edge_w = fzm * ru_l + fzp * ru_lm;
-            const int na = fi(S, F_nAdvCellsForEdge)[e_last];
-            const double* ac = fd(S, F_adv_coefs) + (size_t)e_last * 15;
-            const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e_last * 15;
-            double flux_arr = 0.0;
-            const double w_zeroed = 0.0;
-            for (int j = 0; j < na; j++) {
-                double scalar_weight = ac[j] + copysign(1.0, ru_edge_w) * ac3[j];
-                flux_arr += scalar_weight * w_zeroed;
-            }
-            for (int i = 0; i < ne; i++) w0 -= eocs[i] * ru_edge_w * flux_arr;
-        }
-    }
-    const double *rz_f = fd(S, F_rho_zz), *urz_f = fd(S, F_uReconstructZonal), *urm_f = fd(S, F_uReconstructMeridional);
-    const double rz = col_rd(rz_f, c, k, L, LP), urz = col_rd(urz_f, c, k, L, LP), urm = col_rd(urm_f, c, k, L, LP);
+    double ru_l = 0.0;
+#pragma unroll
+    for (int i = 0; i < NF; i++)
+        if (i == ne - 1) ru_l = ru_[i];
+    const int e_last = ne > 0 ? eoc[ne - 1] : S.nEdges;
+    if (ne > NF) ru_l = col_rd(ru, e_last, k, L, LP);
+    const double ru_lm = lvl_dn<LP>(ru_l, k);
     const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
-    if (k < L) {
-        double wc = w0;
-        if (k > 0) {
-            const double coslat = fd(S, X_cosLatCell)[c];
-            double aa = fzm * urz + fzp * urz_m;
-            double bb = fzm * urm + fzp * urm_m;
-            wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
-                  2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
+    if (k >= L) return;
+    double w0 = 0.0;
+    if (ne > 0 && k > 0) {
+        double ru_edge_w = fzm * ru_l + fzp * ru_lm;
+        const int na = fi(S, F_nAdvCellsForEdge)[e_last];
+        const double* ac = fd(S, F_adv_coefs) + (size_t)e_last * 15;
+        const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e_last * 15;
+        double flux_arr = 0.0;
+        const double w_zeroed = 0.0;
+        for (int j = 0; j < na; j++) {
+            double scalar_weight = ac[j] + copysign(1.0, ru_edge_w) * ac3[j];
+            flux_arr += scalar_weight * w_zeroed;
         }
-        fw(S, X_wc)[p] = wc;
+        for (int i = 0; i < ne; i++) w0 -= eocs[i] * ru_edge_w * flux_arr;
     }
+    double wc = w0;
+    if (k > 0) {
+        const double coslat = fd(S, X_cosLatCell)[c];
+        double aa = fzm * urz + fzp * urz_m;
+        double bb = fzm * urm + fzp * urm_m;
+        wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
+              2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
+    }
+    fw(S, X_wc)[p] = wc;
 }
 
 // ------------------------------------------------------------------------ B (edges)
@@ -145,61 +181,100 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     if (e >= S.nEdges) return;
     const size_t p = (size_t)e * LP + k;
     const bool rk0 = a.rk_step == 0;
+    const bool live = k <= L;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
     const double invDc = fd(S, F_invDcEdge)[e];
-    const double* u_f = fd(S, F_u);
-    const double u = col_rd(u_f, e, k, L, LP);
-    const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
-    const double* rw_f = fd(S, F_rw);
-    const double rw1 = col_rd(rw_f, cell1, k, L, LP), rw2 = col_rd(rw_f, cell2, k, L, LP);
-    const double rho_edge = col_rd(fd(S, F_rho_edge), e, k, L, LP);
+    const double *u_f = fd(S, F_u), *pv_f = fd(S, F_pv_edge), *tm_f = fd(S, F_theta_m);
+    const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
 
+    // ---- issue every independent load of the column first
+    const double u = live ? u_f[p] : 0.0;
+    const double ru_e = live ? fd(S, F_ru)[p] : 0.0;
+    const double rw1 = live ? fd(S, F_rw)[p1] : 0.0, rw2 = live ? fd(S, F_rw)[p2] : 0.0;
+    const double w1 = live ? fd(S, F_w)[p1] : 0.0, w2 = live ? fd(S, F_w)[p2] : 0.0;
+    const double rho_edge = live ? fd(S, F_rho_edge)[p] : 0.0;
+    const double wduzL = (k == L) ? fd(S, F_wduz)[p] : 0.0;
+    const int neoe = fi(S, F_nEdgesOnEdge)[e];
+    const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
+    const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
+    int ee_[QF];
+    double ue_[QF], pve_[QF];
+#pragma unroll
+    for (int j = 0; j < QF; j++) ee_[j] = eoe[j];
+    const bool kl = k < L;
+#pragma unroll
+    for (int j = 0; j < QF; j++) {
+        ue_[j] = kl ? u_f[GCOL(u_f, ee_[j])] : 0.0;
+        pve_[j] = kl ? pv_f[GCOL(pv_f, ee_[j])] : 0.0;
+    }
+    // theta reconstruction at this edge (:1333-1340), consumed by E
+    const int na = fi(S, F_nAdvCellsForEdge)[e];
+    const int* ad = fi(S, F_advCellsForEdge) + (size_t)e * 15;
+    int ad_[AF];
+    double tv_[AF];
+#pragma unroll
+    for (int j = 0; j < AF; j++) ad_[j] = ad[j];
+#pragma unroll
+    for (int j = 0; j < AF; j++) tv_[j] = kl ? tm_f[GCOL(tm_f, ad_[j])] : 0.0;
+
+    const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
+    const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
     // ---- wduz (:972-980); level L is never written by the reference: read it
     double wduz = 0.0;
     if (k == 1 || k == L - 1) wduz = 0.5 * (rw1 + rw2) * (fzm * u + fzp * u_m);
     if (k > 1 && k < L - 1) wduz = flux3(u_m2, u_m, u, u_p, 0.5 * (rw1 + rw2), 1.0);
-    if (k == L) wduz = fd(S, F_wduz)[p];
+    if (k == L) wduz = wduzL;
     const double wduz_p = lvl_up<LP>(wduz, k);
+    if (!kl) return;
 
-    // gathers for the ke/h_divergence/curvature terms (all lanes, shuffles below)
-    const double* w_f = fd(S, F_w);
-    const double w1 = col_rd(w_f, cell1, k, L, LP), w2 = col_rd(w_f, cell2, k, L, LP);
-    const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
-    if (k >= L) return;
+    {  // flux_arr of this edge
+        const double* ac = fd(S, F_adv_coefs) + (size_t)e * 15;
+        const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e * 15;
+        const double sg = copysign(1.0, ru_e);
+        double flux_arr = 0.0;
+#pragma unroll
+        for (int j = 0; j < AF; j++)
+            if (j < na) {
+                double scalar_weight = ac[j] + sg * ac3[j];
+                flux_arr += scalar_weight * tv_[j];
+            }
+        for (int j = AF; j < na; j++) {
+            double scalar_weight = ac[j] + sg * ac3[j];
+            flux_arr += scalar_weight * tm_f[GCOL(tm_f, ad[j])];
+        }
+        fw(S, X_F)[p] = flux_arr;
+    }
 
     // ---- tend_u (:987-1007)
     double tend_u = -rdzw * (wduz_p - wduz);
-    const double pv = fd(S, F_pv_edge)[p];
-    const int neoe = fi(S, F_nEdgesOnEdge)[e];
-    const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
-    const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
-    const double* pv_f = fd(S, F_pv_edge);
+    const double pv = pv_f[p];
     double q = 0.0;
     if (a.exact_q) {
         for (int j = 0; j < neoe; j++) {  // Q10 literal: each term added nVertLevels times
-            int ee = eoe[j];
-            double ue = u_f[(size_t)ee * LP + k], pve = pv_f[(size_t)ee * LP + k];
+            double ue = u_f[GCOL(u_f, eoe[j])];
+            double pve = pv_f[GCOL(pv_f, eoe[j])];
             for (int kk = 0; kk < L; kk++) {
                 double workpv = 0.5 * (pv + pve);
                 q += woe[j] * ue * workpv;
             }
         }
     } else {
-        const double dL = (double)L;
-        for (int j = 0; j < neoe; j++) {  // Q10 value, nVertLevels * term
-            int ee = eoe[j];
-            double ue = u_f[(size_t)ee * LP + k], pve = pv_f[(size_t)ee * LP + k];
-            double workpv = 0.5 * (pv + pve);
-            q += (woe[j] * ue * workpv) * dL;
+        const double dL = (double)L;  // Q10 value, nVertLevels * term
+#pragma unroll
+        for (int j = 0; j < QF; j++)
+            if (j < neoe) {
+                double workpv = 0.5 * (pv + pve_[j]);
+                q += (woe[j] * ue_[j] * workpv) * dL;
+            }
+        for (int j = QF; j < neoe; j++) {
+            double workpv = 0.5 * (pv + pv_f[GCOL(pv_f, eoe[j])]);
+            q += (woe[j] * u_f[GCOL(u_f, eoe[j])] * workpv) * dL;
         }
     }
-    const double* ke_f = fd(S, F_ke);
-    const double* hd_f = fd(S, F_h_divergence);
-    const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
+    const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
     tend_u += rho_edge * (q - (ke_f[p2] - ke_f[p1]) * invDc) - u * 0.5 * (hd_f[p1] + hd_f[p2]);
-    // ---- curvature (:1011-1017, Q12 literal)
-    {
+    {  // curvature (:1011-1017, Q12 literal)
         const double cosA = fd(S, X_cosAngleEdge)[e], cosL = fd(S, X_cosLatEdge)[e];
         tend_u -= (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p)) -
                   (u * 0.25 * (w1 + w1p + w2 + w2p) * rho_edge * a.inv_r_earth);
@@ -244,69 +319,110 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
-    if ((int)blockIdx.x < nVB) {  // delsq_vorticity (:1052-1060)
-        ColMap<LP> m;
+    ColMap<LP> m;
+    if (m.blk < nVB) {  // delsq_vorticity (:1052-1060)
         const int vx = m.ent, k = m.k;
         if (vx >= S.nVertices || k >= L) return;
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)vx * 3;
         const double* sgn = fd(S, F_edgesOnVertex_sign) + (size_t)vx * 3;
         const double iat = fd(S, F_invAreaTriangle)[vx];
         const double* dcEdge = fd(S, F_dcEdge);
+        int ev[3];
+        double d[3];
+#pragma unroll
+        for (int i = 0; i < 3; i++) ev[i] = eov[i];
+#pragma unroll
+        for (int i = 0; i < 3; i++) d[i] = dsu[(size_t)ev[i] * LP + k];
         double dsv = 0.0;
+#pragma unroll
         for (int i = 0; i < 3; i++) {
-            int iEdge = eov[i];
-            double edge_sign = iat * dcEdge[iEdge] * sgn[i];
-            dsv += edge_sign * dsu[(size_t)iEdge * LP + k];
+            double edge_sign = iat * dcEdge[ev[i]] * sgn[i];
+            dsv += edge_sign * d[i];
         }
         fw(S, F_delsq_vorticity)[(size_t)vx * LP + k] = dsv;
         return;
     }
-    const int c = (int)(blockIdx.x - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
-    const int k = (int)(threadIdx.x % LP);
+    const int c = (m.blk - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
+    const int k = m.k;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
+    const bool live = k <= L, kl = k < L;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
-    const double *dvEdge = fd(S, F_dvEdge), *invDc = fd(S, F_invDcEdge), *msd2 = fd(S, F_meshScalingDel2);
-    const int* coe = fi(S, F_cellsOnEdge);
+    const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
+    const double *cdv = fd(S, X_ce_dv) + (size_t)c * 10, *cidc = fd(S, X_ce_idc) + (size_t)c * 10;
+    const double* cmsd2 = fd(S, X_ce_msd2) + (size_t)c * 10;
     const double *rho_edge = fd(S, F_rho_edge), *wc = fd(S, X_wc), *kdiff = fd(S, F_kdiff), *tm = fd(S, F_theta_m);
     const double r_areaCell = fd(S, F_invAreaCell)[c];
+    const bool del4 = a.h4 > 0.0;
+
+    int e_[NF], c1_[NF], c2_[NF];
+    double re_[NF], kd1_[NF], kd2_[NF], wc1_[NF], wc2_[NF], t1_[NF], t2_[NF], ds_[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        e_[i] = eoc[i];
+        c1_[i] = cc1[i];
+        c2_[i] = cc2[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        re_[i] = live ? rho_edge[GCOL(rho_edge, e_[i])] : 0.0;
+        kd1_[i] = live ? kdiff[GCOL(kdiff, c1_[i])] : 0.0;
+        kd2_[i] = live ? kdiff[GCOL(kdiff, c2_[i])] : 0.0;
+        wc1_[i] = kl ? wc[GCOL(wc, c1_[i])] : 0.0;
+        wc2_[i] = kl ? wc[GCOL(wc, c2_[i])] : 0.0;
+        t1_[i] = kl ? tm[GCOL(tm, c1_[i])] : 0.0;
+        t2_[i] = kl ? tm[GCOL(tm, c2_[i])] : 0.0;
+        ds_[i] = (kl && del4) ? dsu[GCOL(dsu, e_[i])] : 0.0;
+    }
+    double re_m_[NF], kd1m_[NF], kd2m_[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        re_m_[i] = lvl_dn<LP>(re_[i], k);
+        kd1m_[i] = lvl_dn<LP>(kd1_[i], k);
+        kd2m_[i] = lvl_dn<LP>(kd2_[i], k);
+    }
     double dsd = 0.0, delsq_w = 0.0, twe = 0.0, delsq_theta = 0.0, tte = 0.0;
-    for (int i = 0; i < ne; i++) {
-        const int iEdge = eoc[i];
-        const int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
-        const size_t q1 = (size_t)cell1 * LP + k, q2 = (size_t)cell2 * LP + k;
-        const double re_k = col_rd(rho_edge, iEdge, k, L, LP);
-        const double re_m = lvl_dn<LP>(re_k, k);
-        const double kd1 = col_rd(kdiff, cell1, k, L, LP), kd2 = col_rd(kdiff, cell2, k, L, LP);
-        const double kd1m = lvl_dn<LP>(kd1, k), kd2m = lvl_dn<LP>(kd2, k);
-        if (k >= L) continue;
-        const double dv = dvEdge[iEdge], idc = invDc[iEdge];
-        if (a.h4 > 0.0) {  // delsq_divergence (:1062-1070)
+    auto edge_terms = [&](int i, double re_k, double re_m, double kd1, double kd2, double kd1m, double kd2m, double wc1,
+                          double wc2, double tm1, double tm2, double dsue) {
+        const double dv = cdv[i], idc = cidc[i], msd2 = cmsd2[i];
+        if (del4) {  // delsq_divergence (:1062-1070)
             double edge_sign = r_areaCell * dv * eocs[i];
-            dsd += edge_sign * dsu[(size_t)iEdge * LP + k];
+            dsd += edge_sign * dsue;
         }
         {  // delsq_w, tend_w_euler del2 (:1231-1254)
             double edge_sign = 0.5 * r_areaCell * eocs[i] * dv * idc;
             if (k > 0) {
-                double w_turb_flux = edge_sign * (re_k + re_m) * (wc[q2] - wc[q1]);
+                double w_turb_flux = edge_sign * (re_k + re_m) * (wc2 - wc1);
                 delsq_w += w_turb_flux;
-                w_turb_flux *= msd2[iEdge] * 0.25 * (kd1 + kd2 + kd1m + kd2m);
+                w_turb_flux *= msd2 * 0.25 * (kd1 + kd2 + kd1m + kd2m);
                 twe += w_turb_flux;
             }
         }
         {  // delsq_theta, tend_theta_euler del2 (:1365-1382)
             double edge_sign = r_areaCell * eocs[i] * dv * idc;
-            double pr_scale = a.prandtl_inv * msd2[iEdge];
-            double theta_turb_flux = edge_sign * (tm[q2] - tm[q1]) * re_k;
+            double pr_scale = a.prandtl_inv * msd2;
+            double theta_turb_flux = edge_sign * (tm2 - tm1) * re_k;
             delsq_theta += theta_turb_flux;
             theta_turb_flux *= 0.5 * (kd1 + kd2) * pr_scale;
             tte += theta_turb_flux;
         }
+    };
+#pragma unroll
+    for (int i = 0; i < NF; i++)
+        if (i < ne && kl)
+            edge_terms(i, re_[i], re_m_[i], kd1_[i], kd2_[i], kd1m_[i], kd2m_[i], wc1_[i], wc2_[i], t1_[i], t2_[i], ds_[i]);
+    for (int i = NF; i < ne; i++) {  // generic tail (shuffles: whole column takes it)
+        const int e = eoc[i], c1 = cc1[i], c2 = cc2[i];
+        double re_k = col_rd(rho_edge, e, k, L, LP), kd1 = col_rd(kdiff, c1, k, L, LP), kd2 = col_rd(kdiff, c2, k, L, LP);
+        double re_m = lvl_dn<LP>(re_k, k), kd1m = lvl_dn<LP>(kd1, k), kd2m = lvl_dn<LP>(kd2, k);
+        if (kl)
+            edge_terms(i, re_k, re_m, kd1, kd2, kd1m, kd2m, wc[GCOL(wc, c1)], wc[GCOL(wc, c2)], tm[GCOL(tm, c1)],
+                       tm[GCOL(tm, c2)], del4 ? dsu[GCOL(dsu, e)] : 0.0);
     }
-    if (k >= L) return;
-    if (a.h4 > 0.0) fw(S, F_delsq_divergence)[p] = dsd;
+    if (!kl) return;
+    if (del4) fw(S, F_delsq_divergence)[p] = dsd;
     fw(S, F_delsq_w)[p] = delsq_w;
     fw(S, F_tend_w_euler)[p] = twe;
     fw(S, F_delsq_theta)[p] = delsq_theta;
@@ -345,105 +461,132 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
     const bool rk0 = a.rk_step == 0;
+    const bool kl = k < L;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
-    const double *dvEdge = fd(S, F_dvEdge), *invDcE = fd(S, F_invDcEdge), *msd4 = fd(S, F_meshScalingDel4);
-    const int* coe = fi(S, F_cellsOnEdge);
+    const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
+    const double *cdv = fd(S, X_ce_dv) + (size_t)c * 10, *cidc = fd(S, X_ce_idc) + (size_t)c * 10;
+    const double* cmsd4 = fd(S, X_ce_msd4) + (size_t)c * 10;
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k], rdzu = fd(S, F_rdzu)[k];
     const double invA = fd(S, F_invAreaCell)[c];
+    const bool del4 = rk0 && a.h4 > 0.0;
+    const double *ru = fd(S, F_ru), *Ff = fd(S, X_F), *rus = fd(S, F_ru_save), *tms_f = fd(S, F_theta_m_save);
+    const double *dw = fd(S, F_delsq_w), *dth = fd(S, F_delsq_theta), *tm = fd(S, F_theta_m);
 
-    // ================= W =================
-    double twe = (k < L) ? fd(S, F_tend_w_euler)[p] : 0.0;
-    if (rk0 && a.h4 > 0.0 && k < L) {  // :1258-1272
-        const double* dw = fd(S, F_delsq_w);
-        double r_areaCell = a.h4 * invA;
-        for (int i = 0; i < ne; i++) {
-            int iEdge = eoc[i];
-            int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
-            double edge_sign = msd4[iEdge] * r_areaCell * dvEdge[iEdge] * eocs[i] * invDcE[iEdge];
-            if (k > 0) twe -= edge_sign * (dw[(size_t)cell2 * LP + k] - dw[(size_t)cell1 * LP + k]);
+    // ---- issue the independent loads
+    int e_[NF], c1_[NF], c2_[NF];
+    double ru_[NF], F_[NF], rus_[NF], ts1_[NF], ts2_[NF], dw1_[NF], dw2_[NF], dt1_[NF], dt2_[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        e_[i] = eoc[i];
+        c1_[i] = cc1[i];
+        c2_[i] = cc2[i];
+    }
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        ru_[i] = kl ? ru[GCOL(ru, e_[i])] : 0.0;
+        F_[i] = kl ? Ff[GCOL(Ff, e_[i])] : 0.0;
+        rus_[i] = ts1_[i] = ts2_[i] = dw1_[i] = dw2_[i] = dt1_[i] = dt2_[i] = 0.0;
+        if (a.rk_step > 0) {
+            rus_[i] = kl ? rus[GCOL(rus, e_[i])] : 0.0;
+            ts1_[i] = kl ? tms_f[GCOL(tms_f, c1_[i])] : 0.0;
+            ts2_[i] = kl ? tms_f[GCOL(tms_f, c2_[i])] : 0.0;
+        }
+        if (del4) {
+            dw1_[i] = kl ? dw[GCOL(dw, c1_[i])] : 0.0;
+            dw2_[i] = kl ? dw[GCOL(dw, c2_[i])] : 0.0;
+            dt1_[i] = kl ? dth[GCOL(dth, c1_[i])] : 0.0;
+            dt2_[i] = kl ? dth[GCOL(dth, c2_[i])] : 0.0;
         }
     }
-    const double wc = (k < L) ? fd(S, X_wc)[p] : 0.0;
-    const double wc_m = lvl_dn<LP>(wc, k), wc_m2 = lvl_dn2<LP>(wc, k), wc_p = lvl_up<LP>(wc, k);
+    const double wc = kl ? fd(S, X_wc)[p] : 0.0;
     const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
+    const double wdwzL = (k == L) ? fd(S, F_wdwz)[p] : 0.0;
+    const double wdtzL = (k == L) ? fd(S, F_wdtz)[p] : 0.0;
+    const double pp = col_rd(fd(S, F_pressure_p), c, k, L, LP), dpdz = col_rd(fd(S, F_dpdz), c, k, L, LP);
+    const double rws = col_rd(fd(S, F_rw_save), c, k, L, LP);
+    const double tms = col_rd(tms_f, c, k, L, LP), tmv = col_rd(tm, c, k, L, LP);
+    double twe = kl ? fd(S, F_tend_w_euler)[p] : 0.0;
+    double tte = kl ? fd(S, F_tend_theta_euler)[p] : 0.0;
+
+    // ================= W =================
+    if (del4 && kl) {  // :1258-1272
+        double r_areaCell = a.h4 * invA;
+#pragma unroll
+        for (int i = 0; i < NF; i++)
+            if (i < ne) {
+                double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
+                if (k > 0) twe -= edge_sign * (dw2_[i] - dw1_[i]);
+            }
+        for (int i = NF; i < ne; i++) {
+            double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
+            if (k > 0) twe -= edge_sign * (dw[GCOL(dw, cc2[i])] - dw[GCOL(dw, cc1[i])]);
+        }
+    }
+    const double wc_m = lvl_dn<LP>(wc, k), wc_m2 = lvl_dn2<LP>(wc, k), wc_p = lvl_up<LP>(wc, k);
     const double rw_m = lvl_dn<LP>(rw, k);
     double wdwz = 0.0;  // :1277-1287
     if (k == 1 || k == L - 1) wdwz = 0.25 * (rw + rw_m) * (wc + wc_m);
     if (k > 1 && k < L - 1) wdwz = flux3(wc_m2, wc_m, wc, wc_p, 0.5 * (rw + rw_m), 1.0);
-    if (k == L) wdwz = fd(S, F_wdwz)[p];
+    if (k == L) wdwz = wdwzL;
     const double wdwz_p = lvl_up<LP>(wdwz, k);
-    const double pp = col_rd(fd(S, F_pressure_p), c, k, L, LP), dpdz = col_rd(fd(S, F_dpdz), c, k, L, LP);
     const double pp_m = lvl_dn<LP>(pp, k), dpdz_m = lvl_dn<LP>(dpdz, k);
     double w = wc;
-    if (k > 0 && k < L) {  // :1289-1302 (Q14 literal), :1318-1322
+    if (k > 0 && kl) {  // :1289-1302 (Q14 literal), :1318-1322
         w *= invA - rdzu * (wdwz_p - wdwz);
         if (rk0) twe -= fd(S, F_cqw)[p] * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
         w += twe;
     }
-    if (k < L) {
+    if (kl) {
         fw(S, F_w)[p] = w;
         if (rk0) fw(S, F_tend_w_euler)[p] = twe;
     }
 
     // ================= theta =================
-    const double *ru = fd(S, F_ru), *tm = fd(S, F_theta_m);
     double tend_theta = 0.0;  // :1328-1344
-    if (k < L) {
-        const int* nadv = fi(S, F_nAdvCellsForEdge);
-        const int* advc = fi(S, F_advCellsForEdge);
-        const double *ac_f = fd(S, F_adv_coefs), *ac3_f = fd(S, F_adv_coefs_3rd);
-        for (int i = 0; i < ne; i++) {
-            int iEdge = eoc[i];
-            double ru_e = ru[(size_t)iEdge * LP + k];
-            double sg = copysign(1.0, ru_e);
-            int na = nadv[iEdge];
-            const int* ad = advc + (size_t)iEdge * 15;
-            const double* ac = ac_f + (size_t)iEdge * 15;
-            const double* ac3 = ac3_f + (size_t)iEdge * 15;
-            double flux_arr = 0.0;
-            for (int j = 0; j < na; j++) {
-                double scalar_weight = ac[j] + sg * ac3[j];
-                flux_arr += scalar_weight * tm[(size_t)ad[j] * LP + k];
-            }
-            tend_theta -= eocs[i] * ru_e * flux_arr;
-        }
+    if (kl) {
+#pragma unroll
+        for (int i = 0; i < NF; i++)
+            if (i < ne) tend_theta -= eocs[i] * ru_[i] * F_[i];
+        for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * ru[GCOL(ru, eoc[i])] * Ff[GCOL(Ff, eoc[i])];
         if (a.rk_step > 0) {  // :1347-1360
-            const double *rus = fd(S, F_ru_save), *tms = fd(S, F_theta_m_save);
-            for (int i = 0; i < ne; i++) {
-                int iEdge = eoc[i];
-                int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
-                size_t q = (size_t)iEdge * LP + k;
-                double flux = eocs[i] * dvEdge[iEdge] * (rus[q] - ru[q]) * 0.5 *
-                              (tms[(size_t)cell2 * LP + k] + tms[(size_t)cell1 * LP + k]);
+#pragma unroll
+            for (int i = 0; i < NF; i++)
+                if (i < ne) {
+                    double flux = eocs[i] * cdv[i] * (rus_[i] - ru_[i]) * 0.5 * (ts2_[i] + ts1_[i]);
+                    tend_theta -= flux;
+                }
+            for (int i = NF; i < ne; i++) {
+                const int e = eoc[i];
+                double flux = eocs[i] * cdv[i] * (rus[GCOL(rus, e)] - ru[GCOL(ru, e)]) * 0.5 *
+                              (tms_f[GCOL(tms_f, cc2[i])] + tms_f[GCOL(tms_f, cc1[i])]);
                 tend_theta -= flux;
             }
         }
-    }
-    double tte = (k < L) ? fd(S, F_tend_theta_euler)[p] : 0.0;
-    if (rk0 && a.h4 > 0.0 && k < L) {  // :1384-1400
-        const double* dth = fd(S, F_delsq_theta);
-        double r_areaCell = a.h4 * a.prandtl_inv * invA;
-        for (int i = 0; i < ne; i++) {
-            int iEdge = eoc[i];
-            double edge_sign = msd4[iEdge] * r_areaCell * dvEdge[iEdge] * eocs[i] * invDcE[iEdge];
-            int cell1 = coe[(size_t)iEdge * 2], cell2 = coe[(size_t)iEdge * 2 + 1];
-            tte -= edge_sign * (dth[(size_t)cell2 * LP + k] - dth[(size_t)cell1 * LP + k]);
+        if (del4) {  // :1384-1400
+            double r_areaCell = a.h4 * a.prandtl_inv * invA;
+#pragma unroll
+            for (int i = 0; i < NF; i++)
+                if (i < ne) {
+                    double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
+                    tte -= edge_sign * (dt2_[i] - dt1_[i]);
+                }
+            for (int i = NF; i < ne; i++) {
+                double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
+                tte -= edge_sign * (dth[GCOL(dth, cc2[i])] - dth[GCOL(dth, cc1[i])]);
+            }
         }
     }
     // wdtz (:1406-1420, Q15 literal order); level L read from the never-written field
-    const double *rws_f = fd(S, F_rw_save), *tms_f = fd(S, F_theta_m_save);
-    const double rws = col_rd(rws_f, c, k, L, LP);
-    const double tms = col_rd(tms_f, c, k, L, LP), tmv = col_rd(tm, c, k, L, LP);
     const double tms_m = lvl_dn<LP>(tms, k), tm_m = lvl_dn<LP>(tmv, k);
     double wdtz = 0.0;
     if (k > 0 && k < L - 1) wdtz = ((rws - rw) * (fzm * tms + fzp * tms_m));
     if (k == 1) wdtz += rw * (fzm * tmv + fzp * tm_m);
     if (k == L - 1) wdtz = rws * (fzm * tms + fzp * tms_m);
-    if (k == L) wdtz = fd(S, F_wdtz)[p];
+    if (k == L) wdtz = wdtzL;
     const double wdtz_p = lvl_up<LP>(wdtz, k);
-    if (k >= L) return;
+    if (!kl) return;
     // :1422-1427, :1477-1479
     const double rho_zz = fd(S, F_rho_zz)[p];
     tend_theta *= invA - rdzw * (wdtz_p - wdtz);

@@ -164,7 +164,23 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     const double zz = col_rd(fd(S, F_zz), c, k, L, LP);
     const double zz_m = lvl_dn<LP>(zz, k);
     double w = col_rd(fd(S, F_w), c, k, L, LP);
-    for (int i = 0; i < ne; i++) {
+    double ut_[NF], utm_[NF], zb_[NF], zb3_[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        ut_[i] = col_rd(ut_f, eoc[i], k, L, LP);
+        size_t q = ((size_t)c * 10 + i) * LP + k;
+        zb_[i] = zb[q];
+        zb3_[i] = zb3[q];
+    }
+#pragma unroll
+    for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
+#pragma unroll
+    for (int i = 0; i < NF; i++)
+        if (i < ne) {
+            double flux = sgn[i] * (fzm * ut_[i] + fzp * utm_[i]);
+            w -= (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux;
+        }
+    for (int i = NF; i < ne; i++) {
         int iEdge = eoc[i];
         double ut = col_rd(ut_f, iEdge, k, L, LP);
         double ut_m = lvl_dn<LP>(ut, k);
@@ -254,6 +270,26 @@ hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep,
     double inv = 1.0 / (double)split;
     k_finish_edges<<<stream_grid((size_t)S.nEdges * S.LP), 256, 0, st>>>(S, substep, split, inv);
     k_finish_cells<<<stream_grid((size_t)S.nCells * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- derived mesh arrays
+__global__ __launch_bounds__(256) void k_prepare(DevState S) {
+    const size_t n = (size_t)S.nCells * 10;
+    const int* eoc = fi(S, F_edgesOnCell);
+    const int* coe = fi(S, F_cellsOnEdge);
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (size_t)gridDim.x * 256) {
+        int e = eoc[t];
+        ((int*)S.f[X_ce_c1])[t] = coe[(size_t)e * 2];
+        ((int*)S.f[X_ce_c2])[t] = coe[(size_t)e * 2 + 1];
+        fw(S, X_ce_dv)[t] = fd(S, F_dvEdge)[e];
+        fw(S, X_ce_idc)[t] = fd(S, F_invDcEdge)[e];
+        fw(S, X_ce_msd2)[t] = fd(S, F_meshScalingDel2)[e];
+        fw(S, X_ce_msd4)[t] = fd(S, F_meshScalingDel4)[e];
+    }
+}
+hipError_t launch_prepare(const DevState& S, hipStream_t st) {
+    k_prepare<<<stream_grid((size_t)S.nCells * 10), 256, 0, st>>>(S);
     return hipGetLastError();
 }
 

@@ -16,8 +16,8 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     const int L = S.L;
     const double* u = fd(S, F_u);
     const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
-    if ((int)blockIdx.x < nVB) {
-        ColMap<LP> m;
+    ColMap<LP> m;
+    if (m.blk < nVB) {
         const int v = m.ent, k = m.k;
         if (v >= S.nVertices || k >= L) return;
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)v * 3;
@@ -47,18 +47,24 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         }
         return;
     }
-    ColMap<LP> m0;
-    const int c = (int)(blockIdx.x - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
-    const int k = m0.k;
+    const int c = (m.blk - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
+    const int k = m.k;
     if (c >= S.nCells || k >= L) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
     const double invA = fd(S, F_invAreaCell)[c];
     double div = 0.0, ke = 0.0;
+    double u_[NF];
+#pragma unroll
+    for (int i = 0; i < NF; i++) u_[i] = u[(size_t)eoc[i] * LP + k];
     for (int i = 0; i < ne; i++) {
         int iEdge = eoc[i];
-        double uu = u[(size_t)iEdge * LP + k];
+        double uu = 0.0;
+#pragma unroll
+        for (int j = 0; j < NF; j++)
+            if (j == i) uu = u_[j];
+        if (i >= NF) uu = u[(size_t)iEdge * LP + k];
         double s = sgn[i] * dvEdge[iEdge];
         div += s + uu;
         // ke_edge(iEdge,k) exactly as the edge loop (:352) writes it; the zero slot

@@ -21,7 +21,14 @@ const FieldInfo kFields[X_COUNT] = {
     {"cosAngleEdge", K_E2F, 1, D_M, 0, 0},
     {"cosLatEdge", K_E2F, 1, D_M, 0, 0},
     {"cosLatCell", K_C2F, 1, D_M, 0, 0},
+    {"ce_c1", K_C2I, 10, D_M, 0, 0},
+    {"ce_c2", K_C2I, 10, D_M, 0, 0},
+    {"ce_dv", K_C2F, 10, D_M, 0, 0},
+    {"ce_idc", K_C2F, 10, D_M, 0, 0},
+    {"ce_msd2", K_C2F, 10, D_M, 0, 0},
+    {"ce_msd4", K_C2F, 10, D_M, 0, 0},
     {"wc", K_C3, 1, D_M, 0, 0},
+    {"F", K_E3, 1, D_M, 0, 0},
 };
 }  // namespace mpas
 
@@ -40,6 +47,7 @@ struct mpas_ctx {
     std::string err;
     int exact = 0;
     bool timing = false;
+    bool dirty = true;  // derived mesh arrays need k_prepare
     std::vector<std::string> task_names;
     std::vector<int64_t> task_calls;
     std::vector<double> task_ms;
@@ -137,6 +145,10 @@ void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
         e0 = get_event(c);
         e1 = get_event(c);
         hipcheck(hipEventRecord(e0, c->stream), "hipEventRecord");
+    }
+    if (c->dirty) {
+        hipcheck(launch_prepare(c->S, c->stream), "prepare");
+        c->dirty = false;
     }
     hipError_t e = fn();
     if (e != hipSuccess) throw Fail{MPAS_EHIP, std::string(name) + ": " + hipGetErrorString(e)};
@@ -353,6 +365,7 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
                 for (int i = 0; i < W; i++) d[(size_t)e * W + i] = *(const double*)(h + e * se + i * sc);
         }
         hipcheck(hipMemcpy(c->S.f[f], buf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+        c->dirty = true;
         // derived mesh arrays: cos() on the host with the same libm as the oracle
         int derived = -1;
         if (f == F_angleEdge) derived = X_cosAngleEdge;

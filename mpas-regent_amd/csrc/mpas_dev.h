@@ -29,9 +29,19 @@ enum FieldId {
     X_cosAngleEdge = F_COUNT,
     X_cosLatEdge,
     X_cosLatCell,
-    // scratch (not reference fields): w after horizontal advection + curvature,
-    // needed because the U section still reads the pre-zeroing w (dyn_tend :1013)
-    X_wc,
+    // per-cell copies of edge data seen through edgesOnCell (mesh constants computed
+    // on the device after upload, k_prepare): one indirection level less per gather
+    X_ce_c1,    // cellsOnEdge(edgesOnCell(i,c), 0)      C2I x10
+    X_ce_c2,    // cellsOnEdge(edgesOnCell(i,c), 1)      C2I x10
+    X_ce_dv,    // dvEdge(edgesOnCell(i,c))              C2F x10
+    X_ce_idc,   // invDcEdge(edgesOnCell(i,c))           C2F x10
+    X_ce_msd2,  // meshScalingDel2(edgesOnCell(i,c))     C2F x10
+    X_ce_msd4,  // meshScalingDel4(edgesOnCell(i,c))     C2F x10
+    // scratch (not reference fields)
+    X_wc,       // w after zeroing, horizontal advection and curvature (dyn_tend :1170-1218);
+                // the U section still reads the pre-zeroing w (:1013)
+    X_F,        // flux_arr of the theta advection (:1333-1340) per edge and level: it
+                // depends only on the edge, so it is formed once per edge, not per cell
     X_COUNT
 };
 
@@ -87,18 +97,39 @@ hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts);
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step);
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
+hipError_t launch_prepare(const DevState& S, hipStream_t st);
 
 // ---- device helpers ----
 #if defined(__HIPCC__)
+// XCD-aware block order (cdna_hip_programming.md §5.5 T1): the dispatcher deals blocks
+// round-robin over the 8 XCDs, so consecutive blocks -- neighbouring columns of the
+// Morton-ordered mesh -- would land on 8 different L2s and every neighbour gather would
+// miss.  Remap so that the blocks sharing an XCD (b % 8) own one contiguous 1/8 of the
+// virtual block range (bijective for any grid size).  Speed only: any placement is correct.
+__device__ __forceinline__ int xcd_block() {
+    const int b = (int)blockIdx.x, nb = (int)gridDim.x;
+    const int q = nb >> 3, r = nb & 7, x = b & 7, pos = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + pos;
+}
+
 template <int LP>
 struct ColMap {
     static constexpr int COLS = 256 / LP;
-    int ent, k;
+    int blk, ent, k;
     __device__ __forceinline__ ColMap() {
-        ent = blockIdx.x * COLS + (int)(threadIdx.x / LP);
+        blk = xcd_block();
+        ent = blk * COLS + (int)(threadIdx.x / LP);
         k = (int)(threadIdx.x % LP);
     }
 };
+
+// Fast-path unroll widths: x1 meshes have 5-6 edges per cell and <= 10 edgesOnEdge;
+// loads for these many entries are issued unconditionally (padding ids are valid
+// entity ids, clamped on upload) ahead of the in-order accumulation; any entries
+// beyond them are handled by a generic tail loop.
+constexpr int NF = 6;   // edgesOnCell
+constexpr int QF = 10;  // edgesOnEdge
+constexpr int AF = 9;   // advCellsForEdge (the reference's list holds at most 9, :175)
 
 // value of x held by level k-1 of the same column (0.0 at k == 0: level -1 reads 0)
 template <int LP>
