@@ -51,7 +51,8 @@ int mpas_sync(mpas_ctx* ctx);
 /* the HIP stream (hipStream_t) the tasks run on, for callers that time with events */
 int mpas_get_stream(mpas_ctx* ctx, void** stream);
 /* options: "exact" = 1 makes the two reassociated kernels (Q10 q sum, acoustic scan)
- * evaluate the reference's literal order (bit-identical to the oracle, slower). */
+ * evaluate the reference's literal order (bit-identical to the oracle, slower);
+ * "xcd" = 0 disables the XCD-aware block order (A/B measurements; results unchanged). */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
 
 /* field registry (include/mpas_fields.def order) */

@@ -20,7 +20,7 @@ namespace mpas {
 
 template <int LP, bool EXACT>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;

@@ -47,7 +47,7 @@ struct DynK {
 // ------------------------------------------------------------------------ A (cells)
 template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // ------------------------------------------------------------------------ B (edges)
 template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEdges) return;
     const size_t p = (size_t)e * LP + k;
@@ -319,7 +319,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     if (m.blk < nVB) {  // delsq_vorticity (:1052-1060)
         const int vx = m.ent, k = m.k;
         if (vx >= S.nVertices || k >= L) return;
@@ -432,7 +432,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
 // ------------------------------------------------------------------------ D (rk0, del4)
 template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEdges || k >= L) return;
     const size_t p = (size_t)e * LP + k;
@@ -456,7 +456,7 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
 // ------------------------------------------------------------------------ E (cells)
 template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;

@@ -76,7 +76,7 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 // ---------------------------------------------------------------- vert_imp
 template <int LP>
 __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
@@ -150,7 +150,7 @@ hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts) 
 // ---------------------------------------------------------------- set_smlstep
 template <int LP>
 __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
@@ -202,7 +202,7 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPA
 // ---------------------------------------------------------------- divergence damping
 template <int LP>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEdges || k >= L) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];

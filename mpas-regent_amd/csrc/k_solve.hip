@@ -16,7 +16,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     const int L = S.L;
     const double* u = fd(S, F_u);
     const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     if (m.blk < nVB) {
         const int v = m.ent, k = m.k;
         if (v >= S.nVertices || k >= L) return;
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
 // hollingsworth second half (:405-417): cells, needs ke_vertex of the whole mesh
 template <int LP>
 __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, c = m.ent, k = m.k;
     if (c >= S.nCells || k >= L) return;
     const size_t p = (size_t)c * LP + k;
@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
 
 template <int LP>
 __global__ __launch_bounds__(256) void k_solve_e(DevState S, int reconstruct_v) {
-    ColMap<LP> m;
+    ColMap<LP> m(S);
     const int L = S.L, e = m.ent, k = m.k;
     if (e >= S.nEdges || k >= L) return;
     const size_t p = (size_t)e * LP + k;

@@ -263,6 +263,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.nVertices = dims->nVertices;
         c->S.L = dims->nVertLevels;
         c->S.LP = LP;
+        c->S.xcd = 0;
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         for (int f = 0; f < X_COUNT; f++) {
             size_t b = dev_bytes(c, f);
@@ -318,6 +319,7 @@ int mpas_get_stream(mpas_ctx* c, void** stream) {
 int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
     return guarded(c, [&] {
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
+        else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else throw Fail{MPAS_EINVAL, std::string("unknown option ") + (name ? name : "(null)")};
     });
 }

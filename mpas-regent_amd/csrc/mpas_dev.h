@@ -54,6 +54,8 @@ extern const FieldInfo kFields[X_COUNT];
 
 struct DevState {
     int nCells, nEdges, nVertices, L, LP;
+    int xcd;  // 1: XCD-aware block order, 0: dispatcher order (default: measured faster,
+              // the Morton-ordered columns of all XCDs then share one Infinity-Cache window)
     void* f[X_COUNT];
 };
 
@@ -106,18 +108,29 @@ hipError_t launch_prepare(const DevState& S, hipStream_t st);
 // Morton-ordered mesh -- would land on 8 different L2s and every neighbour gather would
 // miss.  Remap so that the blocks sharing an XCD (b % 8) own one contiguous 1/8 of the
 // virtual block range (bijective for any grid size).  Speed only: any placement is correct.
-__device__ __forceinline__ int xcd_block() {
+//   on == 1: each XCD owns one contiguous 1/8 of the grid;
+//   on == G > 1: within every window of 8G consecutive blocks each XCD owns G contiguous
+//   blocks (all XCDs stay inside one Infinity-Cache window, each L2 sees a compact
+//   sub-range); blocks past the last whole window keep the dispatcher order.
+__device__ __forceinline__ int xcd_block(int on) {
     const int b = (int)blockIdx.x, nb = (int)gridDim.x;
-    const int q = nb >> 3, r = nb & 7, x = b & 7, pos = b >> 3;
-    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + pos;
+    if (on <= 0) return b;
+    if (on == 1) {
+        const int q = nb >> 3, r = nb & 7, x = b & 7, pos = b >> 3;
+        return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + pos;
+    }
+    const int W = on << 3;
+    if (b >= (nb / W) * W) return b;
+    const int w = b / W, r = b - w * W;
+    return w * W + (r & 7) * on + (r >> 3);
 }
 
 template <int LP>
 struct ColMap {
     static constexpr int COLS = 256 / LP;
     int blk, ent, k;
-    __device__ __forceinline__ ColMap() {
-        blk = xcd_block();
+    __device__ __forceinline__ explicit ColMap(const DevState& S) {
+        blk = xcd_block(S.xcd);
         ent = blk * COLS + (int)(threadIdx.x / LP);
         k = (int)(threadIdx.x % LP);
     }

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Per-task A/B timing in one process (cdna guide §5.4 rule 24): builds the benchmark
+workload once and runs interleaved rounds of full RK3 steps under each option set,
+reporting the median per-task device time (HIP events on the task stream).
+
+usage: python tools/kbench.py [--ncells 163842] [--levels 56] [--rounds 5] --variants "xcd=1" "xcd=0"
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "mpas-regent_amd")]
+
+import bench  # noqa: E402
+from mpasdyn import lib  # noqa: E402
+from mpasdyn import tasks as T  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ncells", type=int, default=163842)
+    ap.add_argument("--levels", type=int, default=56)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", nargs="+", default=["xcd=1", "xcd=0"])
+    a = ap.parse_args()
+    m, st = bench.build_inputs(a.ncells, a.levels)
+    ctx = lib.Context(m.nCells, m.nEdges, m.nVertices, a.levels)
+    bench.upload_inputs(ctx, st)
+    dt = bench.dt_for(a.ncells)
+    T.atm_srk3(ctx, dt, 1)
+    res = {v: {} for v in a.variants}
+    for r in range(a.rounds):
+        for v in a.variants:
+            for kv in v.split(","):
+                k, val = kv.split("=")
+                ctx.set_option(k, int(val))
+            ctx.timing(True)
+            ctx.timing_reset()
+            T.atm_srk3(ctx, dt, 1)
+            ctx.sync()
+            for name, (calls, ms) in ctx.timing_report().items():
+                res[v].setdefault(name, []).append(ms)
+            ctx.timing(False)
+    out = {}
+    for v in a.variants:
+        out[v] = {n: round(statistics.median(x), 4) for n, x in res[v].items()}
+        out[v]["step_ms"] = round(sum(out[v].values()), 4)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
