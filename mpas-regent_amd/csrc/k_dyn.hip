@@ -66,12 +66,12 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 #pragma unroll
     for (int i = 0; i < NF; i++) e_[i] = eoc[i];
 #pragma unroll
-    for (int i = 0; i < NF; i++) ru_[i] = live ? ru[GCOL(ru, e_[i])] : 0.0;
+    for (int i = 0; i < NF; i++) ru_[i] = ldz(live, ru[GCOL(ru, e_[i])]);
     if (smag) {
 #pragma unroll
         for (int i = 0; i < NF; i++) {
-            u_[i] = live ? u[GCOL(u, e_[i])] : 0.0;
-            v_[i] = live ? v[GCOL(v, e_[i])] : 0.0;
+            u_[i] = ldz(live, u[GCOL(u, e_[i])]);
+            v_[i] = ldz(live, v[GCOL(v, e_[i])]);
         }
     }
     const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
@@ -189,12 +189,12 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
 
     // ---- issue every independent load of the column first
-    const double u = live ? u_f[p] : 0.0;
-    const double ru_e = live ? fd(S, F_ru)[p] : 0.0;
-    const double rw1 = live ? fd(S, F_rw)[p1] : 0.0, rw2 = live ? fd(S, F_rw)[p2] : 0.0;
-    const double w1 = live ? fd(S, F_w)[p1] : 0.0, w2 = live ? fd(S, F_w)[p2] : 0.0;
-    const double rho_edge = live ? fd(S, F_rho_edge)[p] : 0.0;
-    const double wduzL = (k == L) ? fd(S, F_wduz)[p] : 0.0;
+    const double u = ldz(live, u_f[p]);
+    const double ru_e = ldz(live, fd(S, F_ru)[p]);
+    const double rw1 = ldz(live, fd(S, F_rw)[p1]), rw2 = ldz(live, fd(S, F_rw)[p2]);
+    const double w1 = ldz(live, fd(S, F_w)[p1]), w2 = ldz(live, fd(S, F_w)[p2]);
+    const double rho_edge = ldz(live, fd(S, F_rho_edge)[p]);
+    const double wduzL = ldz((k == L), fd(S, F_wduz)[p]);
     const int neoe = fi(S, F_nEdgesOnEdge)[e];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
@@ -205,8 +205,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const bool kl = k < L;
 #pragma unroll
     for (int j = 0; j < QF; j++) {
-        ue_[j] = kl ? u_f[GCOL(u_f, ee_[j])] : 0.0;
-        pve_[j] = kl ? pv_f[GCOL(pv_f, ee_[j])] : 0.0;
+        ue_[j] = ldz(kl, u_f[GCOL(u_f, ee_[j])]);
+        pve_[j] = ldz(kl, pv_f[GCOL(pv_f, ee_[j])]);
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = fi(S, F_nAdvCellsForEdge)[e];
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
 #pragma unroll
     for (int j = 0; j < AF; j++) ad_[j] = ad[j];
 #pragma unroll
-    for (int j = 0; j < AF; j++) tv_[j] = kl ? tm_f[GCOL(tm_f, ad_[j])] : 0.0;
+    for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, tm_f[GCOL(tm_f, ad_[j])]);
 
     const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
     const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         fw(S, F_delsq_vorticity)[(size_t)vx * LP + k] = dsv;
         return;
     }
-    const int c = (m.blk - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
+    const int c = col_of<LP>(m.blk - nVB);
     const int k = m.k;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
@@ -367,14 +367,14 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        re_[i] = live ? rho_edge[GCOL(rho_edge, e_[i])] : 0.0;
-        kd1_[i] = live ? kdiff[GCOL(kdiff, c1_[i])] : 0.0;
-        kd2_[i] = live ? kdiff[GCOL(kdiff, c2_[i])] : 0.0;
-        wc1_[i] = kl ? wc[GCOL(wc, c1_[i])] : 0.0;
-        wc2_[i] = kl ? wc[GCOL(wc, c2_[i])] : 0.0;
-        t1_[i] = kl ? tm[GCOL(tm, c1_[i])] : 0.0;
-        t2_[i] = kl ? tm[GCOL(tm, c2_[i])] : 0.0;
-        ds_[i] = (kl && del4) ? dsu[GCOL(dsu, e_[i])] : 0.0;
+        re_[i] = ldz(live, rho_edge[GCOL(rho_edge, e_[i])]);
+        kd1_[i] = ldz(live, kdiff[GCOL(kdiff, c1_[i])]);
+        kd2_[i] = ldz(live, kdiff[GCOL(kdiff, c2_[i])]);
+        wc1_[i] = ldz(kl, wc[GCOL(wc, c1_[i])]);
+        wc2_[i] = ldz(kl, wc[GCOL(wc, c2_[i])]);
+        t1_[i] = ldz(kl, tm[GCOL(tm, c1_[i])]);
+        t2_[i] = ldz(kl, tm[GCOL(tm, c2_[i])]);
+        ds_[i] = ldz((kl && del4), dsu[GCOL(dsu, e_[i])]);
     }
     double re_m_[NF], kd1m_[NF], kd2m_[NF];
 #pragma unroll
@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         double re_m = lvl_dn<LP>(re_k, k), kd1m = lvl_dn<LP>(kd1, k), kd2m = lvl_dn<LP>(kd2, k);
         if (kl)
             edge_terms(i, re_k, re_m, kd1, kd2, kd1m, kd2m, wc[GCOL(wc, c1)], wc[GCOL(wc, c2)], tm[GCOL(tm, c1)],
-                       tm[GCOL(tm, c2)], del4 ? dsu[GCOL(dsu, e)] : 0.0);
+                       tm[GCOL(tm, c2)], ldz(del4, dsu[GCOL(dsu, e)]));
     }
     if (!kl) return;
     if (del4) fw(S, F_delsq_divergence)[p] = dsd;
@@ -485,30 +485,30 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ru_[i] = kl ? ru[GCOL(ru, e_[i])] : 0.0;
-        F_[i] = kl ? Ff[GCOL(Ff, e_[i])] : 0.0;
+        ru_[i] = ldz(kl, ru[GCOL(ru, e_[i])]);
+        F_[i] = ldz(kl, Ff[GCOL(Ff, e_[i])]);
         rus_[i] = ts1_[i] = ts2_[i] = dw1_[i] = dw2_[i] = dt1_[i] = dt2_[i] = 0.0;
         if (a.rk_step > 0) {
-            rus_[i] = kl ? rus[GCOL(rus, e_[i])] : 0.0;
-            ts1_[i] = kl ? tms_f[GCOL(tms_f, c1_[i])] : 0.0;
-            ts2_[i] = kl ? tms_f[GCOL(tms_f, c2_[i])] : 0.0;
+            rus_[i] = ldz(kl, rus[GCOL(rus, e_[i])]);
+            ts1_[i] = ldz(kl, tms_f[GCOL(tms_f, c1_[i])]);
+            ts2_[i] = ldz(kl, tms_f[GCOL(tms_f, c2_[i])]);
         }
         if (del4) {
-            dw1_[i] = kl ? dw[GCOL(dw, c1_[i])] : 0.0;
-            dw2_[i] = kl ? dw[GCOL(dw, c2_[i])] : 0.0;
-            dt1_[i] = kl ? dth[GCOL(dth, c1_[i])] : 0.0;
-            dt2_[i] = kl ? dth[GCOL(dth, c2_[i])] : 0.0;
+            dw1_[i] = ldz(kl, dw[GCOL(dw, c1_[i])]);
+            dw2_[i] = ldz(kl, dw[GCOL(dw, c2_[i])]);
+            dt1_[i] = ldz(kl, dth[GCOL(dth, c1_[i])]);
+            dt2_[i] = ldz(kl, dth[GCOL(dth, c2_[i])]);
         }
     }
-    const double wc = kl ? fd(S, X_wc)[p] : 0.0;
+    const double wc = ldz(kl, fd(S, X_wc)[p]);
     const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
-    const double wdwzL = (k == L) ? fd(S, F_wdwz)[p] : 0.0;
-    const double wdtzL = (k == L) ? fd(S, F_wdtz)[p] : 0.0;
+    const double wdwzL = ldz((k == L), fd(S, F_wdwz)[p]);
+    const double wdtzL = ldz((k == L), fd(S, F_wdtz)[p]);
     const double pp = col_rd(fd(S, F_pressure_p), c, k, L, LP), dpdz = col_rd(fd(S, F_dpdz), c, k, L, LP);
     const double rws = col_rd(fd(S, F_rw_save), c, k, L, LP);
     const double tms = col_rd(tms_f, c, k, L, LP), tmv = col_rd(tm, c, k, L, LP);
-    double twe = kl ? fd(S, F_tend_w_euler)[p] : 0.0;
-    double tte = kl ? fd(S, F_tend_theta_euler)[p] : 0.0;
+    double twe = ldz(kl, fd(S, F_tend_w_euler)[p]);
+    double tte = ldz(kl, fd(S, F_tend_theta_euler)[p]);
 
     // ================= W =================
     if (del4 && kl) {  // :1258-1272

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         }
         return;
     }
-    const int c = (m.blk - nVB) * ColMap<LP>::COLS + (int)(threadIdx.x / LP);
+    const int c = col_of<LP>(m.blk - nVB);
     const int k = m.k;
     if (c >= S.nCells || k >= L) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];

@@ -125,13 +125,23 @@ __device__ __forceinline__ int xcd_block(int on) {
     return w * W + (r & 7) * on + (r >> 3);
 }
 
+// entity of this lane's column in virtual block blk; at LP == 64 one column per
+// wavefront, made explicit so connectivity and mesh constants of the column come
+// through the scalar unit (s_load) and gathers are SGPR base + lane offset
+template <int LP>
+__device__ __forceinline__ int col_of(int blk) {
+    int e = blk * (256 / LP) + (int)(threadIdx.x / LP);
+    if constexpr (LP == 64) e = __builtin_amdgcn_readfirstlane(e);
+    return e;
+}
+
 template <int LP>
 struct ColMap {
     static constexpr int COLS = 256 / LP;
     int blk, ent, k;
     __device__ __forceinline__ explicit ColMap(const DevState& S) {
         blk = xcd_block(S.xcd);
-        ent = blk * COLS + (int)(threadIdx.x / LP);
+        ent = col_of<LP>(blk);
         k = (int)(threadIdx.x % LP);
     }
 };
@@ -166,9 +176,15 @@ __device__ __forceinline__ const double* fd(const DevState& S, int id) { return 
 __device__ __forceinline__ double* fw(const DevState& S, int id) { return (double*)S.f[id]; }
 __device__ __forceinline__ const int* fi(const DevState& S, int id) { return (const int*)S.f[id]; }
 
+// Masked column values.  Every lane of a column row (LP doubles) is allocated, so the
+// load is issued unconditionally and masked afterwards with a select: a load under a
+// lane condition compiles to a branch around it, which serialises the gathers
+// (s_waitcnt vmcnt(0) at every join) and costs the memory-level parallelism.
+__device__ __forceinline__ double ldz(bool keep, double v) { return keep ? v : 0.0; }
+
 // column read with the level policy: levels outside 0..L read 0.0
 __device__ __forceinline__ double col_rd(const double* f, int ent, int k, int L, int LP) {
-    return (k <= L) ? f[(size_t)ent * LP + k] : 0.0;
+    return ldz(k <= L, f[(size_t)ent * LP + k]);
 }
 #endif
 
