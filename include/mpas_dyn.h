@@ -52,8 +52,15 @@ int mpas_sync(mpas_ctx* ctx);
 int mpas_get_stream(mpas_ctx* ctx, void** stream);
 /* options: "exact" = 1 makes the two reassociated kernels (Q10 q sum, acoustic scan)
  * evaluate the reference's literal order (bit-identical to the oracle, slower);
- * "xcd" = 0 disables the XCD-aware block order (A/B measurements; results unchanged). */
+ * "xcd" = 0 dispatcher block order (default), 1 one contiguous eighth of the columns per XCD,
+ * G > 1 runs of G blocks per XCD inside windows of 8G (A/B measurements; results
+ * unchanged); "self" = 0 disables the SELF gathers (A/B; results unchanged). */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
+/* reads "exact", "xcd", "self" (the SELF-gather switch, default 1: when every cell is
+ * among the cellsOnEdge of its own edges -- mpas-mode ids -- the cell kernels gather
+ * only the other cell of an edge) and "selfc" (read-only: whether the SELF gathers are
+ * in use for the uploaded mesh). */
+int mpas_get_option(mpas_ctx* ctx, const char* name, int64_t* value);
 
 /* field registry (include/mpas_fields.def order) */
 int mpas_field_count(void);

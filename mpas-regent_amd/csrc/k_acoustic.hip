@@ -18,7 +18,7 @@
 
 namespace mpas {
 
-template <int LP, bool EXACT>
+template <int LP, bool EXACT, bool SELF>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
@@ -28,10 +28,10 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     double* rpp_f = fw(S, F_rho_pp);
     double* rwp_f = fw(S, F_rw_p);
     double* ww_f = fw(S, F_wwAvg);
-    double rtp = col_rd(rtp_f, c, k, L, LP), rpp = col_rd(rpp_f, c, k, L, LP);
-    double rwp = col_rd(rwp_f, c, k, L, LP), ww = col_rd(ww_f, c, k, L, LP);
+    double rtp = col_rd<LP>(rtp_f, c, k, L), rpp = col_rd<LP>(rpp_f, c, k, L);
+    double rwp = col_rd<LP>(rwp_f, c, k, L), ww = col_rd<LP>(ww_f, c, k, L);
     // :1615-1636
-    if (k < L) fw(S, F_rtheta_pp_old)[p] = (small_step == 0) ? 0 : rtp;
+    if (k < L) colk(fw(S, F_rtheta_pp_old), c) = (small_step == 0) ? 0 : rtp;
     if (small_step == 0) {
         ww = 0;
         rwp = 0;
@@ -40,9 +40,9 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
             rtp = 0;
         }
     }
-    const double tm = col_rd(fd(S, F_theta_m), c, k, L, LP);
-    const double tend_rho = col_rd(fd(S, F_tend_rho), c, k, L, LP);
-    const double w = col_rd(fd(S, F_w), c, k, L, LP);
+    const double tm = col_rd<LP>(fd(S, F_theta_m), c, k, L);
+    const double tend_rho = col_rd<LP>(fd(S, F_tend_rho), c, k, L);
+    const double w = col_rd<LP>(fd(S, F_w), c, k, L);
 
     if (fd(S, F_specZoneMaskCell)[c] != 0.0) {  // :1698-1703 (column-uniform branch)
         if (k < L) {
@@ -50,12 +50,12 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
             rtp = rtp + dts * tm;
             rwp = rwp + dts * w;
             ww = ww + 0.5 * (1.0 + epssm) * rwp;
-            rpp_f[p] = rpp;
-            rtp_f[p] = rtp;
+            colk(rpp_f, c) = rpp;
+            colk(rtp_f, c) = rtp;
         }
         if (k <= L) {
-            rwp_f[p] = rwp;
-            ww_f[p] = ww;
+            colk(rwp_f, c) = rwp;
+            colk(ww_f, c) = ww;
         }
         return;
     }
@@ -68,14 +68,14 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     const double* cdv = fd(S, X_ce_dv) + (size_t)c * 10;
     const double invA = fd(S, F_invAreaCell)[c];
     const double *ru_p = fd(S, F_ru_p), *tm_f = fd(S, F_theta_m);
+    const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
     double rs = 0, ts = 0;
     if (k < L) {
         double rup_[NF], t1_[NF], t2_[NF];
 #pragma unroll
         for (int i = 0; i < NF; i++) {
-            rup_[i] = ru_p[(size_t)eoc[i] * LP + k];
-            t1_[i] = tm_f[(size_t)cc1[i] * LP + k];
-            t2_[i] = tm_f[(size_t)cc2[i] * LP + k];
+            rup_[i] = colk(ru_p, eoc[i]);
+            cell_pair<LP, SELF>(tm_f, cc1[i], cc2[i], coth[i], cs1[i], tm, k, t1_[i], t2_[i]);
         }
 #pragma unroll
         for (int i = 0; i < NF; i++)
@@ -85,27 +85,27 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
                 ts -= flux * 0.5 * (t2_[i] + t1_[i]);
             }
         for (int i = NF; i < ne; i++) {
-            double flux = sgn[i] * dts * cdv[i] * ru_p[(size_t)eoc[i] * LP + k] * invA;
+            double flux = sgn[i] * dts * cdv[i] * colk(ru_p, eoc[i]) * invA;
             rs -= flux;
-            ts -= flux * 0.5 * (tm_f[(size_t)cc2[i] * LP + k] + tm_f[(size_t)cc1[i] * LP + k]);
+            ts -= flux * 0.5 * (colk(tm_f, cc2[i]) + colk(tm_f, cc1[i]));
         }
     }
     // ---- rs, ts (:1657-1658) from the OLD rw_p
     const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
-    const double coftz = col_rd(fd(S, F_coftz), c, k, L, LP);
+    const double coftz = col_rd<LP>(fd(S, F_coftz), c, k, L);
     const double rwp_p = lvl_up<LP>(rwp, k), coftz_p = lvl_up<LP>(coftz, k);
     rs = rpp + dts * tend_rho + rs - cofrz * resm * (rwp_p - rwp);
     ts = rtp + dts * tm + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
 
     // per-level coefficients of the recurrence
-    const double zz = col_rd(fd(S, F_zz), c, k, L, LP), zz_m = lvl_dn<LP>(zz, k);
-    const double rz = col_rd(fd(S, F_rho_zz), c, k, L, LP), rz_m = lvl_dn<LP>(rz, k);
-    const double cofwt = col_rd(fd(S, F_cofwt), c, k, L, LP), cofwt_m = lvl_dn<LP>(cofwt, k);
-    const double cofwz = col_rd(fd(S, F_cofwz), c, k, L, LP), cofwr = col_rd(fd(S, F_cofwr), c, k, L, LP);
-    const double a_tri = col_rd(fd(S, F_a_tri), c, k, L, LP), alpha = col_rd(fd(S, F_alpha_tri), c, k, L, LP);
-    const double rws = col_rd(fd(S, F_rw_save), c, k, L, LP), rw = col_rd(fd(S, F_rw), c, k, L, LP);
-    const double dss = col_rd(fd(S, F_dss), c, k, L, LP);
+    const double zz = col_rd<LP>(fd(S, F_zz), c, k, L), zz_m = lvl_dn<LP>(zz, k);
+    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L), rz_m = lvl_dn<LP>(rz, k);
+    const double cofwt = col_rd<LP>(fd(S, F_cofwt), c, k, L), cofwt_m = lvl_dn<LP>(cofwt, k);
+    const double cofwz = col_rd<LP>(fd(S, F_cofwz), c, k, L), cofwr = col_rd<LP>(fd(S, F_cofwr), c, k, L);
+    const double a_tri = col_rd<LP>(fd(S, F_a_tri), c, k, L), alpha = col_rd<LP>(fd(S, F_alpha_tri), c, k, L);
+    const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L), rw = col_rd<LP>(fd(S, F_rw), c, k, L);
+    const double dss = col_rd<LP>(fd(S, F_dss), c, k, L);
     const double tsm = 0.0, rsm = 0.0;  // Q19
     const double rwold = rwp;
     double x;  // new rw_p of this level
@@ -172,12 +172,12 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     }
     if (k < L) {
         if (k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
-        rpp_f[p] = rs - cofrz * (rwp_p - x);
-        rtp_f[p] = ts - rdzw * (coftz_p * rwp_p - coftz * x);
+        colk(rpp_f, c) = rs - cofrz * (rwp_p - x);
+        colk(rtp_f, c) = ts - rdzw * (coftz_p * rwp_p - coftz * x);
     }
     if (k <= L) {
-        rwp_f[p] = (k < L) ? x : rwp;
-        ww_f[p] = ww;
+        colk(rwp_f, c) = (k < L) ? x : rwp;
+        colk(ww_f, c) = ww;
     }
 }
 
@@ -186,8 +186,13 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
     int grid = (S.nCells + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
-    if (exact) k_acoustic<LP, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
-    else k_acoustic<LP, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
+    if (exact) {
+        if (S.selfc) k_acoustic<LP, true, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
+        else k_acoustic<LP, true, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
+    } else {
+        if (S.selfc) k_acoustic<LP, false, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
+        else k_acoustic<LP, false, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
+    }
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {

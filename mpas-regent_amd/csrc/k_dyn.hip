@@ -42,16 +42,15 @@ struct DynK {
     double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
 };
 
-#define GCOL(f, ent) (((size_t)(ent)) * LP + k)
 
 // ------------------------------------------------------------------------ A (cells)
-template <int LP>
+template <int LP, bool RK0>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
-    const bool rk0 = a.rk_step == 0;
+    constexpr bool rk0 = RK0;
     const bool live = k <= L;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
@@ -66,18 +65,18 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 #pragma unroll
     for (int i = 0; i < NF; i++) e_[i] = eoc[i];
 #pragma unroll
-    for (int i = 0; i < NF; i++) ru_[i] = ldz(live, ru[GCOL(ru, e_[i])]);
+    for (int i = 0; i < NF; i++) ru_[i] = ldz(live, colk(ru, e_[i]));
     if (smag) {
 #pragma unroll
         for (int i = 0; i < NF; i++) {
-            u_[i] = ldz(live, u[GCOL(u, e_[i])]);
-            v_[i] = ldz(live, v[GCOL(v, e_[i])]);
+            u_[i] = ldz(live, colk(u, e_[i]));
+            v_[i] = ldz(live, colk(v, e_[i]));
         }
     }
-    const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
-    const double rz = col_rd(fd(S, F_rho_zz), c, k, L, LP);
-    const double urz = col_rd(fd(S, F_uReconstructZonal), c, k, L, LP);
-    const double urm = col_rd(fd(S, F_uReconstructMeridional), c, k, L, LP);
+    const double rw = col_rd<LP>(fd(S, F_rw), c, k, L);
+    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L);
+    const double urz = col_rd<LP>(fd(S, F_uReconstructZonal), c, k, L);
+    const double urm = col_rd<LP>(fd(S, F_uReconstructMeridional), c, k, L);
 
     // ---- kdiff (:858-917)
     if (rk0 && (a.horiz_mixing == 0 || a.horiz_mixing == 1 || a.cam_coef > 0.0)) {
@@ -94,7 +93,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
                 }
             for (int i = NF; i < ne; i++) {
                 int e = eoc[i];
-                double ue = col_rd(u, e, k, L, LP), ve = col_rd(v, e, k, L, LP);
+                double ue = col_rd<LP>(u, e, k, L), ve = col_rd<LP>(v, e, k, L);
                 d_diag += defa[i] * ue - defb[i] * ve;
                 d_off_diag += defb[i] * ue + defa[i] * ve;
             }
@@ -102,13 +101,13 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         } else if (a.horiz_mixing == 1) {
             kd = 0.0;
         } else {
-            kd = col_rd(fd(S, F_kdiff), c, k, L, LP);
+            kd = col_rd<LP>(fd(S, F_kdiff), c, k, L);
         }
         if (a.cam_coef > 0.0 && k >= L - 2 && k <= L) {
             int pw = k - (L - 2);
             kd = dmax_(kd, (pw == 0 ? 1.0 : 2.0) * 2.0833 * kLenDisp * a.cam_coef);
         }
-        if (k < L) fw(S, F_kdiff)[p] = kd;
+        if (k < L) colk(fw(S, F_kdiff), c) = kd;
     }
 
     // ---- h_divergence (:924-938)
@@ -121,17 +120,17 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         }
     for (int i = NF; i < ne; i++) {
         double edge_sign = eocs[i] * cdv[i];
-        hd += edge_sign * col_rd(ru, eoc[i], k, L, LP);
+        hd += edge_sign * col_rd<LP>(ru, eoc[i], k, L);
     }
     hd *= fd(S, F_invAreaCell)[c];
-    if (k < L) fw(S, F_h_divergence)[p] = hd;
+    if (k < L) colk(fw(S, F_h_divergence), c) = hd;
 
     // ---- tend_rho, dpdz (:942-951)
     const double rw_p1 = lvl_up<LP>(rw, k);
     if (rk0 && k < L) {
-        fw(S, F_tend_rho)[p] = -hd - rdzw * (rw_p1 - rw + fd(S, F_tend_rho_physics)[p]);
-        double qt = fd(S, F_qtot)[p];
-        fw(S, F_dpdz)[p] = -kGravity * (fd(S, F_rho_base)[p] * (qt) + fd(S, F_rho_p_save)[p] * (1.0 + qt));
+        colk(fw(S, F_tend_rho), c) = -hd - rdzw * (rw_p1 - rw + colk(fd(S, F_tend_rho_physics), c));
+        double qt = colk(fd(S, F_qtot), c);
+        colk(fw(S, F_dpdz), c) = -kGravity * (colk(fd(S, F_rho_base), c) * (qt) + colk(fd(S, F_rho_p_save), c) * (1.0 + qt));
     }
 
     // ---- w: zeroing (:1170), horizontal advection (:1174-1205, Q13), curvature (:1208-1218)
@@ -144,7 +143,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     for (int i = 0; i < NF; i++)
         if (i == ne - 1) ru_l = ru_[i];
     const int e_last = ne > 0 ? eoc[ne - 1] : S.nEdges;
-    if (ne > NF) ru_l = col_rd(ru, e_last, k, L, LP);
+    if (ne > NF) ru_l = col_rd<LP>(ru, e_last, k, L);
     const double ru_lm = lvl_dn<LP>(ru_l, k);
     const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
     if (k >= L) return;
@@ -170,17 +169,17 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
               2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
     }
-    fw(S, X_wc)[p] = wc;
+    colk(fw(S, X_wc), c) = wc;
 }
 
 // ------------------------------------------------------------------------ B (edges)
-template <int LP>
+template <int LP, bool RK0>
 __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEdges) return;
     const size_t p = (size_t)e * LP + k;
-    const bool rk0 = a.rk_step == 0;
+    constexpr bool rk0 = RK0;
     const bool live = k <= L;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
@@ -189,12 +188,12 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
 
     // ---- issue every independent load of the column first
-    const double u = ldz(live, u_f[p]);
-    const double ru_e = ldz(live, fd(S, F_ru)[p]);
-    const double rw1 = ldz(live, fd(S, F_rw)[p1]), rw2 = ldz(live, fd(S, F_rw)[p2]);
-    const double w1 = ldz(live, fd(S, F_w)[p1]), w2 = ldz(live, fd(S, F_w)[p2]);
-    const double rho_edge = ldz(live, fd(S, F_rho_edge)[p]);
-    const double wduzL = ldz((k == L), fd(S, F_wduz)[p]);
+    const double u = ldz(live, colk(u_f, e));
+    const double ru_e = ldz(live, colk(fd(S, F_ru), e));
+    const double rw1 = ldz(live, colk(fd(S, F_rw), cell1)), rw2 = ldz(live, colk(fd(S, F_rw), cell2));
+    const double w1 = ldz(live, colk(fd(S, F_w), cell1)), w2 = ldz(live, colk(fd(S, F_w), cell2));
+    const double rho_edge = ldz(live, colk(fd(S, F_rho_edge), e));
+    const double wduzL = ldz((k == L), colk(fd(S, F_wduz), e));
     const int neoe = fi(S, F_nEdgesOnEdge)[e];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
@@ -205,8 +204,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const bool kl = k < L;
 #pragma unroll
     for (int j = 0; j < QF; j++) {
-        ue_[j] = ldz(kl, u_f[GCOL(u_f, ee_[j])]);
-        pve_[j] = ldz(kl, pv_f[GCOL(pv_f, ee_[j])]);
+        ue_[j] = ldz(kl, colk(u_f, ee_[j]));
+        pve_[j] = ldz(kl, colk(pv_f, ee_[j]));
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = fi(S, F_nAdvCellsForEdge)[e];
@@ -216,7 +215,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
 #pragma unroll
     for (int j = 0; j < AF; j++) ad_[j] = ad[j];
 #pragma unroll
-    for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, tm_f[GCOL(tm_f, ad_[j])]);
+    for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, colk(tm_f, ad_[j]));
 
     const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
     const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
@@ -241,19 +240,19 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
             }
         for (int j = AF; j < na; j++) {
             double scalar_weight = ac[j] + sg * ac3[j];
-            flux_arr += scalar_weight * tm_f[GCOL(tm_f, ad[j])];
+            flux_arr += scalar_weight * colk(tm_f, ad[j]);
         }
-        fw(S, X_F)[p] = flux_arr;
+        colk(fw(S, X_F), e) = flux_arr;
     }
 
     // ---- tend_u (:987-1007)
     double tend_u = -rdzw * (wduz_p - wduz);
-    const double pv = pv_f[p];
+    const double pv = colk(pv_f, e);
     double q = 0.0;
     if (a.exact_q) {
         for (int j = 0; j < neoe; j++) {  // Q10 literal: each term added nVertLevels times
-            double ue = u_f[GCOL(u_f, eoe[j])];
-            double pve = pv_f[GCOL(pv_f, eoe[j])];
+            double ue = colk(u_f, eoe[j]);
+            double pve = colk(pv_f, eoe[j]);
             for (int kk = 0; kk < L; kk++) {
                 double workpv = 0.5 * (pv + pve);
                 q += woe[j] * ue * workpv;
@@ -268,12 +267,12 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
                 q += (woe[j] * ue_[j] * workpv) * dL;
             }
         for (int j = QF; j < neoe; j++) {
-            double workpv = 0.5 * (pv + pv_f[GCOL(pv_f, eoe[j])]);
-            q += (woe[j] * u_f[GCOL(u_f, eoe[j])] * workpv) * dL;
+            double workpv = 0.5 * (pv + colk(pv_f, eoe[j]));
+            q += (woe[j] * colk(u_f, eoe[j]) * workpv) * dL;
         }
     }
     const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
-    tend_u += rho_edge * (q - (ke_f[p2] - ke_f[p1]) * invDc) - u * 0.5 * (hd_f[p1] + hd_f[p2]);
+    tend_u += rho_edge * (q - (colk(ke_f, cell2) - colk(ke_f, cell1)) * invDc) - u * 0.5 * (colk(hd_f, cell1) + colk(hd_f, cell2));
     {  // curvature (:1011-1017, Q12 literal)
         const double cosA = fd(S, X_cosAngleEdge)[e], cosL = fd(S, X_cosLatEdge)[e];
         tend_u -= (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p)) -
@@ -284,38 +283,38 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     if (rk0) {
         // ---- pressure gradient (:964-970)
         const double *pp = fd(S, F_pressure_p), *zz = fd(S, F_zz), *dpdz = fd(S, F_dpdz);
-        tue = -fd(S, F_cqu)[p] * ((pp[p2] - pp[p1]) * invDc / (0.5 * (zz[p2] + zz[p1])) -
-                                  0.5 * fd(S, F_zxu)[p] * (dpdz[p1] + dpdz[p2]));
+        tue = -colk(fd(S, F_cqu), e) * ((colk(pp, cell2) - colk(pp, cell1)) * invDc / (0.5 * (colk(zz, cell2) + colk(zz, cell1))) -
+                                  0.5 * colk(fd(S, F_zxu), e) * (colk(dpdz, cell1) + colk(dpdz, cell2)));
         // ---- del2 (:1030-1048)
         const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
         const double r_dc = invDc;
         const double r_dv = dmin_(fd(S, F_invDvEdge)[e], 4 * r_dc);
         const double *div = fd(S, F_divergence), *vor = fd(S, F_vorticity), *kdiff = fd(S, F_kdiff);
-        double u_diffusion = (div[p2] - div[p1]) * r_dc -
-                             (vor[(size_t)vertex2 * LP + k] - vor[(size_t)vertex1 * LP + k]) * r_dv;
+        double u_diffusion = (colk(div, cell2) - colk(div, cell1)) * r_dc -
+                             (colk(vor, vertex2) - colk(vor, vertex1)) * r_dv;
         double delsq_u = 0.0;
         delsq_u += u_diffusion;
-        fw(S, F_delsq_u)[p] = delsq_u;
-        double kdiffu = 0.5 * (kdiff[p1] + kdiff[p2]);
+        colk(fw(S, F_delsq_u), e) = delsq_u;
+        double kdiffu = 0.5 * (colk(kdiff, cell1) + colk(kdiff, cell2));
         tue += rho_edge * kdiffu * u_diffusion * fd(S, F_meshScalingDel2)[e];
     } else {
-        tue = fd(S, F_tend_u_euler)[p];
+        tue = colk(fd(S, F_tend_u_euler), e);
     }
     // ---- Rayleigh damping (:1152-1159)
     if (a.rayleigh && k > L - kRayleighLevels + 1)
         tend_u -= rho_edge * u * (((double)k - (double)(L - kRayleighLevels)) * a.rayleigh_inv);
     if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
-        fw(S, F_tend_u_euler)[p] = tue;
-        fw(S, F_tend_u)[p] = tend_u;
+        colk(fw(S, F_tend_u_euler), e) = tue;
+        colk(fw(S, F_tend_u), e) = tend_u;
     } else {
-        if (rk0) fw(S, F_tend_u_euler)[p] = tue;
-        tend_u += tue + fd(S, F_tend_ru_physics)[p];  // :1161-1163
-        fw(S, F_tend_u)[p] = tend_u;
+        if (rk0) colk(fw(S, F_tend_u_euler), e) = tue;
+        tend_u += tue + colk(fd(S, F_tend_ru_physics), e);  // :1161-1163
+        colk(fw(S, F_tend_u), e) = tend_u;
     }
 }
 
 // ------------------------------------------------------------------------ C (rk0)
-template <int LP>
+template <int LP, bool SELF>
 __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
@@ -339,7 +338,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
             double edge_sign = iat * dcEdge[ev[i]] * sgn[i];
             dsv += edge_sign * d[i];
         }
-        fw(S, F_delsq_vorticity)[(size_t)vx * LP + k] = dsv;
+        colk(fw(S, F_delsq_vorticity), vx) = dsv;
         return;
     }
     const int c = col_of<LP>(m.blk - nVB);
@@ -357,24 +356,31 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const double r_areaCell = fd(S, F_invAreaCell)[c];
     const bool del4 = a.h4 > 0.0;
 
-    int e_[NF], c1_[NF], c2_[NF];
+    const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
+    int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
     double re_[NF], kd1_[NF], kd2_[NF], wc1_[NF], wc2_[NF], t1_[NF], t2_[NF], ds_[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         e_[i] = eoc[i];
         c1_[i] = cc1[i];
         c2_[i] = cc2[i];
+        o_[i] = coth[i];
+        s1_[i] = cs1[i];
     }
+    const double kd_c = SELF ? colk(kdiff, c) : 0.0, wc_c = SELF ? colk(wc, c) : 0.0, tm_c = SELF ? colk(tm, c) : 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        re_[i] = ldz(live, rho_edge[GCOL(rho_edge, e_[i])]);
-        kd1_[i] = ldz(live, kdiff[GCOL(kdiff, c1_[i])]);
-        kd2_[i] = ldz(live, kdiff[GCOL(kdiff, c2_[i])]);
-        wc1_[i] = ldz(kl, wc[GCOL(wc, c1_[i])]);
-        wc2_[i] = ldz(kl, wc[GCOL(wc, c2_[i])]);
-        t1_[i] = ldz(kl, tm[GCOL(tm, c1_[i])]);
-        t2_[i] = ldz(kl, tm[GCOL(tm, c2_[i])]);
-        ds_[i] = ldz((kl && del4), dsu[GCOL(dsu, e_[i])]);
+        re_[i] = ldz(live, colk(rho_edge, e_[i]));
+        cell_pair<LP, SELF>(kdiff, c1_[i], c2_[i], o_[i], s1_[i], kd_c, k, kd1_[i], kd2_[i]);
+        cell_pair<LP, SELF>(wc, c1_[i], c2_[i], o_[i], s1_[i], wc_c, k, wc1_[i], wc2_[i]);
+        cell_pair<LP, SELF>(tm, c1_[i], c2_[i], o_[i], s1_[i], tm_c, k, t1_[i], t2_[i]);
+        kd1_[i] = ldz(live, kd1_[i]);
+        kd2_[i] = ldz(live, kd2_[i]);
+        wc1_[i] = ldz(kl, wc1_[i]);
+        wc2_[i] = ldz(kl, wc2_[i]);
+        t1_[i] = ldz(kl, t1_[i]);
+        t2_[i] = ldz(kl, t2_[i]);
+        ds_[i] = ldz((kl && del4), colk(dsu, e_[i]));
     }
     double re_m_[NF], kd1m_[NF], kd2m_[NF];
 #pragma unroll
@@ -415,18 +421,18 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
             edge_terms(i, re_[i], re_m_[i], kd1_[i], kd2_[i], kd1m_[i], kd2m_[i], wc1_[i], wc2_[i], t1_[i], t2_[i], ds_[i]);
     for (int i = NF; i < ne; i++) {  // generic tail (shuffles: whole column takes it)
         const int e = eoc[i], c1 = cc1[i], c2 = cc2[i];
-        double re_k = col_rd(rho_edge, e, k, L, LP), kd1 = col_rd(kdiff, c1, k, L, LP), kd2 = col_rd(kdiff, c2, k, L, LP);
+        double re_k = col_rd<LP>(rho_edge, e, k, L), kd1 = col_rd<LP>(kdiff, c1, k, L), kd2 = col_rd<LP>(kdiff, c2, k, L);
         double re_m = lvl_dn<LP>(re_k, k), kd1m = lvl_dn<LP>(kd1, k), kd2m = lvl_dn<LP>(kd2, k);
         if (kl)
-            edge_terms(i, re_k, re_m, kd1, kd2, kd1m, kd2m, wc[GCOL(wc, c1)], wc[GCOL(wc, c2)], tm[GCOL(tm, c1)],
-                       tm[GCOL(tm, c2)], ldz(del4, dsu[GCOL(dsu, e)]));
+            edge_terms(i, re_k, re_m, kd1, kd2, kd1m, kd2m, colk(wc, c1), colk(wc, c2), colk(tm, c1),
+                       colk(tm, c2), ldz(del4, colk(dsu, e)));
     }
     if (!kl) return;
-    if (del4) fw(S, F_delsq_divergence)[p] = dsd;
-    fw(S, F_delsq_w)[p] = delsq_w;
-    fw(S, F_tend_w_euler)[p] = twe;
-    fw(S, F_delsq_theta)[p] = delsq_theta;
-    fw(S, F_tend_theta_euler)[p] = tte;
+    if (del4) colk(fw(S, F_delsq_divergence), c) = dsd;
+    colk(fw(S, F_delsq_w), c) = delsq_w;
+    colk(fw(S, F_tend_w_euler), c) = twe;
+    colk(fw(S, F_delsq_theta), c) = delsq_theta;
+    colk(fw(S, F_tend_theta_euler), c) = tte;
 }
 
 // ------------------------------------------------------------------------ D (rk0, del4)
@@ -443,24 +449,24 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
     double r_dc = u_mix_scale * kDel4uDivFactor * invDc;
     double r_dv = u_mix_scale * dmin_(fd(S, F_invDvEdge)[e], 4 * invDc);
     const double *dd = fd(S, F_delsq_divergence), *dvv = fd(S, F_delsq_vorticity);
-    double u_diffusion = fd(S, F_rho_edge)[p] * ((dd[(size_t)cell2 * LP + k] - dd[(size_t)cell1 * LP + k]) * r_dc -
-                                                 (dvv[(size_t)vertex2 * LP + k] - dvv[(size_t)vertex1 * LP + k]) * r_dv);
-    double tue = fd(S, F_tend_u_euler)[p];
+    double u_diffusion = colk(fd(S, F_rho_edge), e) * ((colk(dd, cell2) - colk(dd, cell1)) * r_dc -
+                                                 (colk(dvv, vertex2) - colk(dvv, vertex1)) * r_dv);
+    double tue = colk(fd(S, F_tend_u_euler), e);
     tue -= u_diffusion;
-    fw(S, F_tend_u_euler)[p] = tue;
-    double tend_u = fd(S, F_tend_u)[p];
-    tend_u += tue + fd(S, F_tend_ru_physics)[p];
-    fw(S, F_tend_u)[p] = tend_u;
+    colk(fw(S, F_tend_u_euler), e) = tue;
+    double tend_u = colk(fd(S, F_tend_u), e);
+    tend_u += tue + colk(fd(S, F_tend_ru_physics), e);
+    colk(fw(S, F_tend_u), e) = tend_u;
 }
 
 // ------------------------------------------------------------------------ E (cells)
-template <int LP>
+template <int LP, bool RK0, bool SELF>
 __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCells) return;
     const size_t p = (size_t)c * LP + k;
-    const bool rk0 = a.rk_step == 0;
+    constexpr bool rk0 = RK0;
     const bool kl = k < L;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
@@ -475,40 +481,48 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     const double *dw = fd(S, F_delsq_w), *dth = fd(S, F_delsq_theta), *tm = fd(S, F_theta_m);
 
     // ---- issue the independent loads
-    int e_[NF], c1_[NF], c2_[NF];
+    const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
+    int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
     double ru_[NF], F_[NF], rus_[NF], ts1_[NF], ts2_[NF], dw1_[NF], dw2_[NF], dt1_[NF], dt2_[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         e_[i] = eoc[i];
         c1_[i] = cc1[i];
         c2_[i] = cc2[i];
+        o_[i] = coth[i];
+        s1_[i] = cs1[i];
     }
+    const double ts_c = (SELF && !rk0) ? colk(tms_f, c) : 0.0;
+    const double dw_c = (SELF && del4) ? colk(dw, c) : 0.0, dt_c = (SELF && del4) ? colk(dth, c) : 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ru_[i] = ldz(kl, ru[GCOL(ru, e_[i])]);
-        F_[i] = ldz(kl, Ff[GCOL(Ff, e_[i])]);
+        ru_[i] = ldz(kl, colk(ru, e_[i]));
+        F_[i] = ldz(kl, colk(Ff, e_[i]));
         rus_[i] = ts1_[i] = ts2_[i] = dw1_[i] = dw2_[i] = dt1_[i] = dt2_[i] = 0.0;
-        if (a.rk_step > 0) {
-            rus_[i] = ldz(kl, rus[GCOL(rus, e_[i])]);
-            ts1_[i] = ldz(kl, tms_f[GCOL(tms_f, c1_[i])]);
-            ts2_[i] = ldz(kl, tms_f[GCOL(tms_f, c2_[i])]);
+        if (!rk0) {
+            rus_[i] = ldz(kl, colk(rus, e_[i]));
+            cell_pair<LP, SELF>(tms_f, c1_[i], c2_[i], o_[i], s1_[i], ts_c, k, ts1_[i], ts2_[i]);
+            ts1_[i] = ldz(kl, ts1_[i]);
+            ts2_[i] = ldz(kl, ts2_[i]);
         }
         if (del4) {
-            dw1_[i] = ldz(kl, dw[GCOL(dw, c1_[i])]);
-            dw2_[i] = ldz(kl, dw[GCOL(dw, c2_[i])]);
-            dt1_[i] = ldz(kl, dth[GCOL(dth, c1_[i])]);
-            dt2_[i] = ldz(kl, dth[GCOL(dth, c2_[i])]);
+            cell_pair<LP, SELF>(dw, c1_[i], c2_[i], o_[i], s1_[i], dw_c, k, dw1_[i], dw2_[i]);
+            cell_pair<LP, SELF>(dth, c1_[i], c2_[i], o_[i], s1_[i], dt_c, k, dt1_[i], dt2_[i]);
+            dw1_[i] = ldz(kl, dw1_[i]);
+            dw2_[i] = ldz(kl, dw2_[i]);
+            dt1_[i] = ldz(kl, dt1_[i]);
+            dt2_[i] = ldz(kl, dt2_[i]);
         }
     }
-    const double wc = ldz(kl, fd(S, X_wc)[p]);
-    const double rw = col_rd(fd(S, F_rw), c, k, L, LP);
-    const double wdwzL = ldz((k == L), fd(S, F_wdwz)[p]);
-    const double wdtzL = ldz((k == L), fd(S, F_wdtz)[p]);
-    const double pp = col_rd(fd(S, F_pressure_p), c, k, L, LP), dpdz = col_rd(fd(S, F_dpdz), c, k, L, LP);
-    const double rws = col_rd(fd(S, F_rw_save), c, k, L, LP);
-    const double tms = col_rd(tms_f, c, k, L, LP), tmv = col_rd(tm, c, k, L, LP);
-    double twe = ldz(kl, fd(S, F_tend_w_euler)[p]);
-    double tte = ldz(kl, fd(S, F_tend_theta_euler)[p]);
+    const double wc = ldz(kl, colk(fd(S, X_wc), c));
+    const double rw = col_rd<LP>(fd(S, F_rw), c, k, L);
+    const double wdwzL = ldz((k == L), colk(fd(S, F_wdwz), c));
+    const double wdtzL = ldz((k == L), colk(fd(S, F_wdtz), c));
+    const double pp = col_rd<LP>(fd(S, F_pressure_p), c, k, L), dpdz = col_rd<LP>(fd(S, F_dpdz), c, k, L);
+    const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L);
+    const double tms = col_rd<LP>(tms_f, c, k, L), tmv = col_rd<LP>(tm, c, k, L);
+    double twe = ldz(kl, colk(fd(S, F_tend_w_euler), c));
+    double tte = ldz(kl, colk(fd(S, F_tend_theta_euler), c));
 
     // ================= W =================
     if (del4 && kl) {  // :1258-1272
@@ -521,7 +535,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
             }
         for (int i = NF; i < ne; i++) {
             double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
-            if (k > 0) twe -= edge_sign * (dw[GCOL(dw, cc2[i])] - dw[GCOL(dw, cc1[i])]);
+            if (k > 0) twe -= edge_sign * (colk(dw, cc2[i]) - colk(dw, cc1[i]));
         }
     }
     const double wc_m = lvl_dn<LP>(wc, k), wc_m2 = lvl_dn2<LP>(wc, k), wc_p = lvl_up<LP>(wc, k);
@@ -535,12 +549,12 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     double w = wc;
     if (k > 0 && kl) {  // :1289-1302 (Q14 literal), :1318-1322
         w *= invA - rdzu * (wdwz_p - wdwz);
-        if (rk0) twe -= fd(S, F_cqw)[p] * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
+        if (rk0) twe -= colk(fd(S, F_cqw), c) * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
         w += twe;
     }
     if (kl) {
-        fw(S, F_w)[p] = w;
-        if (rk0) fw(S, F_tend_w_euler)[p] = twe;
+        colk(fw(S, F_w), c) = w;
+        if (rk0) colk(fw(S, F_tend_w_euler), c) = twe;
     }
 
     // ================= theta =================
@@ -549,8 +563,8 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
 #pragma unroll
         for (int i = 0; i < NF; i++)
             if (i < ne) tend_theta -= eocs[i] * ru_[i] * F_[i];
-        for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * ru[GCOL(ru, eoc[i])] * Ff[GCOL(Ff, eoc[i])];
-        if (a.rk_step > 0) {  // :1347-1360
+        for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(ru, eoc[i]) * colk(Ff, eoc[i]);
+        if (!rk0) {  // :1347-1360
 #pragma unroll
             for (int i = 0; i < NF; i++)
                 if (i < ne) {
@@ -559,8 +573,8 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
                 }
             for (int i = NF; i < ne; i++) {
                 const int e = eoc[i];
-                double flux = eocs[i] * cdv[i] * (rus[GCOL(rus, e)] - ru[GCOL(ru, e)]) * 0.5 *
-                              (tms_f[GCOL(tms_f, cc2[i])] + tms_f[GCOL(tms_f, cc1[i])]);
+                double flux = eocs[i] * cdv[i] * (colk(rus, e) - colk(ru, e)) * 0.5 *
+                              (colk(tms_f, cc2[i]) + colk(tms_f, cc1[i]));
                 tend_theta -= flux;
             }
         }
@@ -574,7 +588,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
                 }
             for (int i = NF; i < ne; i++) {
                 double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
-                tte -= edge_sign * (dth[GCOL(dth, cc2[i])] - dth[GCOL(dth, cc1[i])]);
+                tte -= edge_sign * (colk(dth, cc2[i]) - colk(dth, cc1[i]));
             }
         }
     }
@@ -588,14 +602,14 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     const double wdtz_p = lvl_up<LP>(wdtz, k);
     if (!kl) return;
     // :1422-1427, :1477-1479
-    const double rho_zz = fd(S, F_rho_zz)[p];
+    const double rho_zz = colk(fd(S, F_rho_zz), c);
     tend_theta *= invA - rdzw * (wdtz_p - wdtz);
-    fw(S, F_tend_rtheta_adv)[p] = tend_theta;
-    fw(S, F_rthdynten)[p] = tend_theta / rho_zz;
-    tend_theta += rho_zz * fd(S, F_rt_diabatic_tend)[p];
-    tend_theta += tte + fd(S, F_tend_rtheta_physics)[p];
-    fw(S, F_tend_theta)[p] = tend_theta;
-    if (rk0) fw(S, F_tend_theta_euler)[p] = tte;
+    colk(fw(S, F_tend_rtheta_adv), c) = tend_theta;
+    colk(fw(S, F_rthdynten), c) = tend_theta / rho_zz;
+    tend_theta += rho_zz * colk(fd(S, F_rt_diabatic_tend), c);
+    tend_theta += tte + colk(fd(S, F_tend_rtheta_physics), c);
+    colk(fw(S, F_tend_theta), c) = tend_theta;
+    if (rk0) colk(fw(S, F_tend_theta_euler), c) = tte;
 }
 
 template <int LP>
@@ -617,13 +631,21 @@ static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& i
     a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
     a.prandtl_inv = 1.0 / kPrandtl;
     const int nCB = (S.nCells + COLS - 1) / COLS, nEB = (S.nEdges + COLS - 1) / COLS, nVB = (S.nVertices + COLS - 1) / COLS;
-    k_dyn_A<LP><<<nCB, 256, 0, st>>>(S, a);
-    k_dyn_B<LP><<<nEB, 256, 0, st>>>(S, a);
+    const int nCV = (a.h4 > 0.0 ? nVB : 0) + nCB, nV4 = a.h4 > 0.0 ? nVB : 0;
     if (a.rk_step == 0) {
-        k_dyn_C<LP><<<(a.h4 > 0.0 ? nVB : 0) + nCB, 256, 0, st>>>(S, a, a.h4 > 0.0 ? nVB : 0);
+        k_dyn_A<LP, true><<<nCB, 256, 0, st>>>(S, a);
+        k_dyn_B<LP, true><<<nEB, 256, 0, st>>>(S, a);
+        if (S.selfc) k_dyn_C<LP, true><<<nCV, 256, 0, st>>>(S, a, nV4);
+        else k_dyn_C<LP, false><<<nCV, 256, 0, st>>>(S, a, nV4);
         if (a.h4 > 0.0) k_dyn_D<LP><<<nEB, 256, 0, st>>>(S, a);
+        if (S.selfc) k_dyn_E<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
+        else k_dyn_E<LP, true, false><<<nCB, 256, 0, st>>>(S, a);
+    } else {
+        k_dyn_A<LP, false><<<nCB, 256, 0, st>>>(S, a);
+        k_dyn_B<LP, false><<<nEB, 256, 0, st>>>(S, a);
+        if (S.selfc) k_dyn_E<LP, false, true><<<nCB, 256, 0, st>>>(S, a);
+        else k_dyn_E<LP, false, false><<<nCB, 256, 0, st>>>(S, a);
     }
-    k_dyn_E<LP><<<nCB, 256, 0, st>>>(S, a);
     return hipGetLastError();
 }
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& in) {

@@ -83,12 +83,12 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
     const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
     const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
     const double rdzw_m = k > 0 ? rdzw_a[k - 1] : 0.0;
-    const double zz = fd(S, F_zz)[p], exner = fd(S, F_exner)[p], tm = fd(S, F_theta_m)[p];
-    const double cqw = fd(S, F_cqw)[p], qtot = fd(S, F_qtot)[p];
-    const double rb = fd(S, F_rho_base)[p], rtb = fd(S, F_rtheta_base)[p], rtp = fd(S, F_rtheta_p)[p];
-    const double exb = fd(S, F_exner_base)[p];
-    const double gamma_old = fd(S, F_gamma_tri)[p];
-    const double coftz_old = fd(S, F_coftz)[p];  // level L keeps its (never written) value
+    const double zz = colk(fd(S, F_zz), c), exner = colk(fd(S, F_exner), c), tm = colk(fd(S, F_theta_m), c);
+    const double cqw = colk(fd(S, F_cqw), c), qtot = colk(fd(S, F_qtot), c);
+    const double rb = colk(fd(S, F_rho_base), c), rtb = colk(fd(S, F_rtheta_base), c), rtp = colk(fd(S, F_rtheta_p), c);
+    const double exb = colk(fd(S, F_exner_base), c);
+    const double gamma_old = colk(fd(S, F_gamma_tri), c);
+    const double coftz_old = colk(fd(S, F_coftz), c);  // level L keeps its (never written) value
     const double zz_m = lvl_dn<LP>(zz, k), exner_m = lvl_dn<LP>(exner, k), tm_m = lvl_dn<LP>(tm, k);
 
     // :550-564
@@ -111,13 +111,13 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
 
     if (k < L) {
         double* o;
-        fw(S, F_coftz)[p] = coftz;
-        fw(S, F_cofwt)[p] = cofwt;
+        colk(fw(S, F_coftz), c) = coftz;
+        colk(fw(S, F_cofwt), c) = cofwt;
         if (k == 0) {
-            fw(S, F_gamma_tri)[p] = 0.0;
+            colk(fw(S, F_gamma_tri), c) = 0.0;
         } else {
-            fw(S, F_cofwr)[p] = cofwr;
-            fw(S, F_cofwz)[p] = cofwz;
+            colk(fw(S, F_cofwr), c) = cofwr;
+            colk(fw(S, F_cofwz), c) = cofwz;
             // :566-578 (Q16 literal)
             double a = -1.0 * cofwz * coftz_m * rdzw_m * zz_m + cofwr * cofrz_m - cofwt_m * coftz_m * rdzw_m;
             double b = 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) - coftz * (cofwt * rdzw - cofwt * rdzw_m) +
@@ -125,11 +125,11 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
             double cc = -1.0 * cofwz * coftz_p * rdzw * zz - cofwr * cofrz + cofwt * coftz_p * rdzw;
             double alpha = 1.0 / (b - a * gamma_m);  // :580-585
             double gamma = cc * alpha;               // :587-591
-            o = fw(S, F_a_tri); o[p] = a;
-            o = fw(S, F_b_tri); o[p] = b;
-            o = fw(S, F_c_tri); o[p] = cc;
-            o = fw(S, F_alpha_tri); o[p] = alpha;
-            o = fw(S, F_gamma_tri); o[p] = gamma;
+            o = fw(S, F_a_tri); colk(o, c) = a;
+            o = fw(S, F_b_tri); colk(o, c) = b;
+            o = fw(S, F_c_tri); colk(o, c) = cc;
+            o = fw(S, F_alpha_tri); colk(o, c) = alpha;
+            o = fw(S, F_gamma_tri); colk(o, c) = gamma;
         }
         if (c == 0) fw(S, F_cofrz)[k] = cofrz;
     }
@@ -161,13 +161,13 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     const double* zb = fd(S, F_zb_cell);
     const double* zb3 = fd(S, F_zb3_cell);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
-    const double zz = col_rd(fd(S, F_zz), c, k, L, LP);
+    const double zz = col_rd<LP>(fd(S, F_zz), c, k, L);
     const double zz_m = lvl_dn<LP>(zz, k);
-    double w = col_rd(fd(S, F_w), c, k, L, LP);
+    double w = col_rd<LP>(fd(S, F_w), c, k, L);
     double ut_[NF], utm_[NF], zb_[NF], zb3_[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ut_[i] = col_rd(ut_f, eoc[i], k, L, LP);
+        ut_[i] = col_rd<LP>(ut_f, eoc[i], k, L);
         size_t q = ((size_t)c * 10 + i) * LP + k;
         zb_[i] = zb[q];
         zb3_[i] = zb3[q];
@@ -182,14 +182,14 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
         }
     for (int i = NF; i < ne; i++) {
         int iEdge = eoc[i];
-        double ut = col_rd(ut_f, iEdge, k, L, LP);
+        double ut = col_rd<LP>(ut_f, iEdge, k, L);
         double ut_m = lvl_dn<LP>(ut, k);
         double flux = sgn[i] * (fzm * ut + fzp * ut_m);
         size_t q = ((size_t)c * 10 + i) * LP + k;
         w -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
     }
     w *= (fzm * zz + fzp * zz_m);
-    if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) fw(S, F_w)[p] = w;
+    if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) colk(fw(S, F_w), c) = w;
 }
 template <int LP>
 static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
@@ -210,11 +210,11 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
     if (sh[cell1] && sh[cell2]) return;
     const double *rtp = fd(S, F_rtheta_pp), *rtpo = fd(S, F_rtheta_pp_old), *tm = fd(S, F_theta_m);
     const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
-    double divCell1 = -(rtp[p1] - rtpo[p1]);
-    double divCell2 = -(rtp[p2] - rtpo[p2]);
+    double divCell1 = -(colk(rtp, cell1) - colk(rtpo, cell1));
+    double divCell2 = -(colk(rtp, cell2) - colk(rtpo, cell2));
     double* rup = fw(S, F_ru_p);
     const size_t p = (size_t)e * LP + k;
-    rup[p] += coef_divdamp * (divCell2 - divCell1) * (1.0 - fd(S, F_specZoneMaskEdge)[e]) / (tm[p1] + tm[p2]);
+    colk(rup, e) += coef_divdamp * (divCell2 - divCell1) * (1.0 - fd(S, F_specZoneMaskEdge)[e]) / (colk(tm, cell1) + colk(tm, cell2));
 }
 template <int LP>
 static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
@@ -274,23 +274,41 @@ hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep,
 }
 
 // ---------------------------------------------------------------- derived mesh arrays
-__global__ __launch_bounds__(256) void k_prepare(DevState S) {
+__global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
     const size_t n = (size_t)S.nCells * 10;
     const int* eoc = fi(S, F_edgesOnCell);
     const int* coe = fi(S, F_cellsOnEdge);
     for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (size_t)gridDim.x * 256) {
-        int e = eoc[t];
-        ((int*)S.f[X_ce_c1])[t] = coe[(size_t)e * 2];
-        ((int*)S.f[X_ce_c2])[t] = coe[(size_t)e * 2 + 1];
+        const int e = eoc[t], c = (int)(t / 10), i = (int)(t % 10);
+        const int c1 = coe[(size_t)e * 2], c2 = coe[(size_t)e * 2 + 1];
+        ((int*)S.f[X_ce_c1])[t] = c1;
+        ((int*)S.f[X_ce_c2])[t] = c2;
+        ((int*)S.f[X_ce_oth])[t] = (c1 == c) ? c2 : c1;
+        ((int*)S.f[X_ce_s1])[t] = (c1 == c) ? 1 : 0;
+        if (i < fi(S, F_nEdgesOnCell)[c] && i < NF && c1 != c && c2 != c) atomicAnd(selfc, 0);
         fw(S, X_ce_dv)[t] = fd(S, F_dvEdge)[e];
         fw(S, X_ce_idc)[t] = fd(S, F_invDcEdge)[e];
         fw(S, X_ce_msd2)[t] = fd(S, F_meshScalingDel2)[e];
         fw(S, X_ce_msd4)[t] = fd(S, F_meshScalingDel4)[e];
     }
 }
-hipError_t launch_prepare(const DevState& S, hipStream_t st) {
-    k_prepare<<<stream_grid((size_t)S.nCells * 10), 256, 0, st>>>(S);
-    return hipGetLastError();
+// derived mesh arrays; decides S.selfc (synchronous: runs once after each mesh upload)
+hipError_t launch_prepare(DevState& S, hipStream_t st) {
+    int* flag = nullptr;
+    hipError_t e = hipMalloc(&flag, sizeof(int));
+    if (e != hipSuccess) return e;
+    const int one = 1;
+    int host = 0;
+    e = hipMemcpyAsync(flag, &one, sizeof(int), hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        k_prepare<<<stream_grid((size_t)S.nCells * 10), 256, 0, st>>>(S, flag);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&host, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(flag);
+    if (e == hipSuccess) S.selfc = host;
+    return e;
 }
 
 // ---------------------------------------------------------------- synthetic fill

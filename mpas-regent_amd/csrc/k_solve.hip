@@ -26,12 +26,12 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         for (int i = 0; i < 3; i++) {
             int iEdge = eov[i];
             double s = sgn[i] * dcEdge[iEdge];
-            vort += s * u[(size_t)iEdge * LP + k];
+            vort += s * colk(u, iEdge);
         }
         vort *= fd(S, F_invAreaTriangle)[v];
         const size_t p = (size_t)v * LP + k;
-        fw(S, F_vorticity)[p] = vort;
-        fw(S, F_pv_vertex)[p] = fd(S, F_fVertex)[v] + vort;
+        colk(fw(S, F_vorticity), v) = vort;
+        colk(fw(S, F_pv_vertex), v) = fd(S, F_fVertex)[v] + vort;
         if (hollingsworth_part) {
             const double* ke_edge_unused = nullptr;
             (void)ke_edge_unused;
@@ -40,10 +40,10 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
             for (int i = 0; i < 3; i++) {
                 int iEdge = eov[i];
                 double efac = dcEdge[iEdge] * dvEdge[iEdge];
-                double uu = u[(size_t)iEdge * LP + k];
+                double uu = colk(u, iEdge);
                 kes[i] = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
             }
-            fw(S, F_ke_vertex)[p] = (kes[0] + kes[1] + kes[2]) * r;
+            colk(fw(S, F_ke_vertex), v) = (kes[0] + kes[1] + kes[2]) * r;
         }
         return;
     }
@@ -57,14 +57,14 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     double div = 0.0, ke = 0.0;
     double u_[NF];
 #pragma unroll
-    for (int i = 0; i < NF; i++) u_[i] = u[(size_t)eoc[i] * LP + k];
+    for (int i = 0; i < NF; i++) u_[i] = colk(u, eoc[i]);
     for (int i = 0; i < ne; i++) {
         int iEdge = eoc[i];
         double uu = 0.0;
 #pragma unroll
         for (int j = 0; j < NF; j++)
             if (j == i) uu = u_[j];
-        if (i >= NF) uu = u[(size_t)iEdge * LP + k];
+        if (i >= NF) uu = colk(u, iEdge);
         double s = sgn[i] * dvEdge[iEdge];
         div += s + uu;
         // ke_edge(iEdge,k) exactly as the edge loop (:352) writes it; the zero slot
@@ -76,8 +76,8 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     div *= invA;
     ke *= invA;
     const size_t p = (size_t)c * LP + k;
-    fw(S, F_divergence)[p] = div;
-    fw(S, F_ke)[p] = ke;
+    colk(fw(S, F_divergence), c) = div;
+    colk(fw(S, F_ke), c) = ke;
 }
 
 // hollingsworth second half (:405-417): cells, needs ke_vertex of the whole mesh
@@ -88,16 +88,16 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
     if (c >= S.nCells || k >= L) return;
     const size_t p = (size_t)c * LP + k;
     double ke_fact = 1.0 - 0.375;
-    double ke = fd(S, F_ke)[p] * ke_fact;
+    double ke = colk(fd(S, F_ke), c) * ke_fact;
     double r = fd(S, F_invAreaCell)[c];
     const int ne = fi(S, F_nEdgesOnCell)[c];
     for (int i = 0; i < ne; i++) {
         int iVertex = fi(S, F_verticesOnCell)[(size_t)c * 10 + i];
         int j = fi(S, F_kiteForCell)[(size_t)c * 10 + i];
         double kite = (j >= 0 && j < 3) ? fd(S, F_kiteAreasOnVertex)[(size_t)iVertex * 3 + j] : 0.0;
-        ke += (1.0 - ke_fact) * kite * fd(S, F_ke_vertex)[(size_t)iVertex * LP + k] * r;
+        ke += (1.0 - ke_fact) * kite * colk(fd(S, F_ke_vertex), iVertex) * r;
     }
-    fw(S, F_ke)[p] = ke;
+    colk(fw(S, F_ke), c) = ke;
 }
 
 template <int LP>
@@ -110,20 +110,20 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S, int reconstruct_v) 
     const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
     const double* h = fd(S, F_h);
     const double* u = fd(S, F_u);
-    fw(S, F_h_edge)[p] = 0.5 * (h[(size_t)coe[0] * LP + k] + h[(size_t)coe[1] * LP + k]);
+    colk(fw(S, F_h_edge), e) = 0.5 * (colk(h, coe[0]) + colk(h, coe[1]));
     double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
-    double uu = u[p];
-    fw(S, F_ke_edge)[p] = efac * (uu * uu);
+    double uu = colk(u, e);
+    colk(fw(S, F_ke_edge), e) = efac * (uu * uu);
     if (reconstruct_v) {
         const int neoe = fi(S, F_nEdgesOnEdge)[e];
         const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
         const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
         double v = 0;
-        for (int i = 1; i < neoe; i++) v += wts[i] * u[(size_t)eoe[i] * LP + k];
-        fw(S, F_v)[p] = v;
+        for (int i = 1; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
+        colk(fw(S, F_v), e) = v;
     }
     const double* pvv = fd(S, F_pv_vertex);
-    fw(S, F_pv_edge)[p] = 0.5 * (pvv[(size_t)voe[0] * LP + k] + pvv[(size_t)voe[1] * LP + k]);
+    colk(fw(S, F_pv_edge), e) = 0.5 * (colk(pvv, voe[0]) + colk(pvv, voe[1]));
 }
 
 template <int LP>

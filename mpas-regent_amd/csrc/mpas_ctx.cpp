@@ -27,6 +27,8 @@ const FieldInfo kFields[X_COUNT] = {
     {"ce_idc", K_C2F, 10, D_M, 0, 0},
     {"ce_msd2", K_C2F, 10, D_M, 0, 0},
     {"ce_msd4", K_C2F, 10, D_M, 0, 0},
+    {"ce_oth", K_C2I, 10, D_M, 0, 0},
+    {"ce_s1", K_C2I, 10, D_M, 0, 0},
     {"wc", K_C3, 1, D_M, 0, 0},
     {"F", K_E3, 1, D_M, 0, 0},
 };
@@ -46,6 +48,8 @@ struct mpas_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int exact = 0;
+    int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
+    int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     bool timing = false;
     bool dirty = true;  // derived mesh arrays need k_prepare
     std::vector<std::string> task_names;
@@ -148,6 +152,8 @@ void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
     }
     if (c->dirty) {
         hipcheck(launch_prepare(c->S, c->stream), "prepare");
+        c->self_ok = c->S.selfc;
+        c->S.selfc = c->self_ok && c->self_on;
         c->dirty = false;
     }
     hipError_t e = fn();
@@ -320,7 +326,29 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
     return guarded(c, [&] {
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
-        else throw Fail{MPAS_EINVAL, std::string("unknown option ") + (name ? name : "(null)")};
+        else if (name && std::strcmp(name, "self") == 0) {
+            c->self_on = value ? 1 : 0;
+            c->S.selfc = c->self_ok && c->self_on;
+        } else throw Fail{MPAS_EINVAL, std::string("unknown option ") + (name ? name : "(null)")};
+    });
+}
+
+int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
+    return guarded(c, [&] {
+        if (!value) throw Fail{MPAS_EINVAL, "mpas_get_option: null value"};
+        if (name && std::strcmp(name, "exact") == 0) *value = c->exact;
+        else if (name && std::strcmp(name, "xcd") == 0) *value = c->S.xcd;
+        else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
+        else if (name && std::strcmp(name, "selfc") == 0) {
+            if (c->dirty) {  // decide now (needs the mesh uploaded)
+                hipcheck(hipSetDevice(c->device), "hipSetDevice");
+                hipcheck(launch_prepare(c->S, c->stream), "prepare");
+                c->self_ok = c->S.selfc;
+                c->S.selfc = c->self_ok && c->self_on;
+                c->dirty = false;
+            }
+            *value = c->S.selfc;
+        } else throw Fail{MPAS_EINVAL, std::string("unknown option ") + (name ? name : "(null)")};
     });
 }
 

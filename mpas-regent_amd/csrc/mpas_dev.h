@@ -37,6 +37,8 @@ enum FieldId {
     X_ce_idc,   // invDcEdge(edgesOnCell(i,c))           C2F x10
     X_ce_msd2,  // meshScalingDel2(edgesOnCell(i,c))     C2F x10
     X_ce_msd4,  // meshScalingDel4(edgesOnCell(i,c))     C2F x10
+    X_ce_oth,   // the cell of cellsOnEdge(edgesOnCell(i,c), 0:1) that is not c   C2I x10
+    X_ce_s1,    // 1 if cellsOnEdge(edgesOnCell(i,c), 0) == c                     C2I x10
     // scratch (not reference fields)
     X_wc,       // w after zeroing, horizontal advection and curvature (dyn_tend :1170-1218);
                 // the U section still reads the pre-zeroing w (:1013)
@@ -56,6 +58,10 @@ struct DevState {
     int nCells, nEdges, nVertices, L, LP;
     int xcd;  // 1: XCD-aware block order, 0: dispatcher order (default: measured faster,
               // the Morton-ordered columns of all XCDs then share one Infinity-Cache window)
+    int selfc;  // 1 when every cell is one of the two cellsOnEdge of each of its first
+                // min(nEdgesOnCell, NF) edges (k_prepare): the cell kernels then gather
+                // only the other cell of an edge and use their own column for the cell
+                // itself (SELF path); 0 (e.g. the literal 1-based "ref" ids) gathers both
     void* f[X_COUNT];
 };
 
@@ -99,7 +105,7 @@ hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts);
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step);
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
-hipError_t launch_prepare(const DevState& S, hipStream_t st);
+hipError_t launch_prepare(DevState& S, hipStream_t st);
 
 // ---- device helpers ----
 #if defined(__HIPCC__)
@@ -172,6 +178,44 @@ __device__ __forceinline__ double lvl_up(double x, int k) {
     return k == LP - 1 ? 0.0 : y;
 }
 
+// A wave-uniform pointer held in SGPRs.  Loads through it at a lane offset compile to
+// the saddr + 32-bit voffset form: no per-load 64-bit VALU address add (the compiler
+// otherwise folds the lane offset into a VGPR base and adds the row offset per gather).
+#define MPAS_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ MPAS_GLOBAL T* sgpr_ptr(T* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (MPAS_GLOBAL T*)(((uint64_t)hi << 32) | lo);
+}
+
+// column ent of f (a row of LP values); SGPR-held when one column fills the wavefront
+// (LP == 64, ent wave-uniform), a plain per-lane pointer otherwise
+template <int LP, class T>
+__device__ __forceinline__ MPAS_GLOBAL T* col_row(T* f, int ent) {
+    if constexpr (LP == 64) return sgpr_ptr(f + (size_t)ent * LP);
+    else return (MPAS_GLOBAL T*)(f + (size_t)ent * LP);
+}
+// level k of column ent of field pointer f (needs LP and k in scope)
+#define colk(f, ent) col_row<LP>((f), (ent))[(unsigned)k]
+
+// f at the two cellsOnEdge (x1, x2) of edge slot i of a cell.  SELF (S.selfc): the cell
+// is one of them, so only the other cell `oth` is gathered and `own`, f at the cell
+// itself, stands in for the other (s1: the cell is cellsOnEdge(0)).  Same values either way.
+template <int LP, bool SELF>
+__device__ __forceinline__ void cell_pair(const double* f, int c1, int c2, int oth, int s1, double own, int k,
+                                          double& x1, double& x2) {
+    if constexpr (SELF) {
+        const double xo = colk(f, oth);
+        x1 = s1 ? own : xo;
+        x2 = s1 ? xo : own;
+    } else {
+        x1 = colk(f, c1);
+        x2 = colk(f, c2);
+    }
+}
+
 __device__ __forceinline__ const double* fd(const DevState& S, int id) { return (const double*)S.f[id]; }
 __device__ __forceinline__ double* fw(const DevState& S, int id) { return (double*)S.f[id]; }
 __device__ __forceinline__ const int* fi(const DevState& S, int id) { return (const int*)S.f[id]; }
@@ -183,8 +227,9 @@ __device__ __forceinline__ const int* fi(const DevState& S, int id) { return (co
 __device__ __forceinline__ double ldz(bool keep, double v) { return keep ? v : 0.0; }
 
 // column read with the level policy: levels outside 0..L read 0.0
-__device__ __forceinline__ double col_rd(const double* f, int ent, int k, int L, int LP) {
-    return ldz(k <= L, f[(size_t)ent * LP + k]);
+template <int LP>
+__device__ __forceinline__ double col_rd(const double* f, int ent, int k, int L) {
+    return ldz(k <= L, col_row<LP>(f, ent)[(unsigned)k]);
 }
 #endif
 

@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(HERE, "libmpasdyn.so")
 # every symbol include/mpas_dyn.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "mpas_ctx_create", "mpas_ctx_destroy", "mpas_last_error", "mpas_sync", "mpas_get_stream",
-    "mpas_set_option", "mpas_field_count", "mpas_field_id", "mpas_field_name", "mpas_field_kind",
+    "mpas_set_option", "mpas_get_option", "mpas_field_count", "mpas_field_id", "mpas_field_name", "mpas_field_kind",
     "mpas_field_width", "mpas_upload", "mpas_download", "mpas_fill_synthetic",
     "mpas_atm_rk_integration_setup", "mpas_atm_compute_moist_coefficients",
     "mpas_atm_compute_vert_imp_coefs", "mpas_atm_compute_dyn_tend_work",
@@ -56,6 +56,7 @@ def load():
         "mpas_sync": (i32, [vp]),
         "mpas_get_stream": (i32, [vp, ctypes.POINTER(vp)]),
         "mpas_set_option": (i32, [vp, ctypes.c_char_p, i64]),
+        "mpas_get_option": (i32, [vp, ctypes.c_char_p, ctypes.POINTER(i64)]),
         "mpas_field_count": (i32, []),
         "mpas_field_id": (i32, [ctypes.c_char_p]),
         "mpas_field_name": (ctypes.c_char_p, [i32]),
@@ -156,6 +157,11 @@ class Context:
 
     def set_option(self, name, value):
         self._check(self.lib.mpas_set_option(self.h, name.encode(), int(value)), f"set_option {name}")
+
+    def get_option(self, name):
+        v = ctypes.c_int64(0)
+        self._check(self.lib.mpas_get_option(self.h, name.encode(), ctypes.byref(v)), f"get_option {name}")
+        return int(v.value)
 
     # ---------------------------------------------------------------- timing
     def timing(self, on=True):

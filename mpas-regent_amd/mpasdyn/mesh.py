@@ -268,3 +268,22 @@ def to_zero_based(ids, n):
     """mpas-mode connectivity: 1-based file ids -> 0-based; padding (0) -> zero slot n"""
     z = ids.astype(np.int64) - 1
     return np.where(z < 0, n, z).astype(np.int32)
+
+
+# connectivity arrays of a Mesh and the entity count their ids refer to
+_CONNECTIVITY = {"edgesOnCell": "nEdges", "verticesOnCell": "nVertices", "cellsOnCell": "nCells",
+                 "cellsOnEdge": "nCells", "verticesOnEdge": "nVertices", "edgesOnEdge": "nEdges",
+                 "edgesOnVertex": "nEdges", "cellsOnVertex": "nCells"}
+
+
+def zero_based(m):
+    """a copy of m with every connectivity array in mpas-mode ids (to_zero_based): the
+    hot path then sees each cell among the cellsOnEdge of its own edges, which enables
+    the kernels' SELF gathers (mpas_dev.h cell_pair)"""
+    d = dict(m.__dict__)
+    for name, count in _CONNECTIVITY.items():
+        if name in d:
+            d[name] = to_zero_based(d[name], getattr(m, count))
+    z = Mesh(**{k: v for k, v in d.items() if k not in ("nCells", "nEdges", "nVertices")})
+    return z
+

@@ -68,9 +68,16 @@ _STATES = {}
 
 
 def base_state(mesh, L, variant):
+    """variants: "random", "ref" (build_state) and "mpas0" -- the random state on the
+    same mesh with mpas-mode (0-based) ids, where every cell is among the cellsOnEdge of
+    its edges and the cell kernels take the SELF gathers (mpas_get_option "selfc")"""
     key = (L, variant)
     if key not in _STATES:
-        _STATES[key] = make_state(mesh, L, variant)
+        if variant == "mpas0":
+            from mpasdyn import mesh as M
+            _STATES[key] = make_state(M.zero_based(mesh), L, "random")
+        else:
+            _STATES[key] = make_state(mesh, L, variant)
     return _STATES[key]
 
 
@@ -92,7 +99,7 @@ def run_oracle(st, fn):
 
 
 @pytest.mark.parametrize("L", [5, 56])
-@pytest.mark.parametrize("variant", ["random", "ref"])
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
 @pytest.mark.parametrize("task", TASKS, ids=[t[0] for t in TASKS])
 def test_task_exact(x1_2562, L, variant, task):
     name, ofn, gfn, _ = task
@@ -106,9 +113,10 @@ def test_task_exact(x1_2562, L, variant, task):
 
 @pytest.mark.parametrize("L", [5, 56])
 @pytest.mark.parametrize("task", [t for t in TASKS if t[3]], ids=[t[0] for t in TASKS if t[3]])
-def test_task_fast(x1_2562, L, task):
+@pytest.mark.parametrize("variant", ["random", "mpas0"])
+def test_task_fast(x1_2562, L, variant, task):
     name, ofn, gfn, tol_fields = task
-    st = base_state(x1_2562, L, "random")
+    st = base_state(x1_2562, L, variant)
     ref = run_oracle(st, ofn)
     got = run_gpu(st, gfn, exact=0)
     bad = compare_states(got, ref, rtol=RTOL_FAST, tol_fields=tol_fields)
@@ -116,7 +124,7 @@ def test_task_fast(x1_2562, L, task):
 
 
 @pytest.mark.parametrize("L", [5, 56])
-@pytest.mark.parametrize("variant", ["random", "ref"])
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
 @pytest.mark.parametrize("schedule", [0, 1])
 def test_srk3(x1_2562, L, variant, schedule):
     st = base_state(x1_2562, L, variant)
@@ -138,3 +146,33 @@ def test_timestep_dt_zero_nan(x1_2562):
     assert np.isnan(ref["ru_p"]).any() or np.isinf(ref["ru_p"]).any()
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, f"dt=0 step: {bad[:6]}"
+
+
+@pytest.mark.parametrize("variant,expect", [("ref", 0), ("random", 0), ("mpas0", 1)])
+def test_self_gathers_detected(x1_2562, variant, expect):
+    """the SELF gathers switch on exactly for meshes whose cells are among the
+    cellsOnEdge of their own edges (raw 1-based ids shift every neighbour: off)"""
+    st = base_state(x1_2562, 5, variant)
+    with lib.Context(*st.dims()) as ctx:
+        ctx.upload(st)
+        assert ctx.get_option("selfc") == expect
+        ctx.set_option("self", 0)
+        assert ctx.get_option("selfc") == 0
+
+
+def test_self_gathers_identical(x1_2562):
+    """SELF on and off give value-identical results over a whole step (mpas0 mesh)"""
+    st = base_state(x1_2562, 56, "mpas0")
+    outs = []
+    for on in (1, 0):
+        got = st.copy()
+        with lib.Context(*st.dims()) as ctx:
+            ctx.set_option("self", on)
+            ctx.upload(st)
+            T.atm_srk3(ctx, 720.0, 1)
+            ctx.sync()
+            ctx.download(got)
+        outs.append(got)
+    bad = compare_states(outs[0], outs[1], rtol=0.0)
+    assert not bad, f"SELF on/off differ: {bad[:6]}"
+

@@ -28,9 +28,10 @@ def stats(src):
         c = lambda p: len(re.findall(p, body))
         short = re.sub(r"^_ZN4mpas\d+", "", name).split("ILi")[0]
         v = int(meta.get(name, 0))
-        print("%-22s vgpr %3d  vload %3d  sload %3d  vstore %3d  vmcnt0 %3d  execz %3d  insts %5d" % (
+        print("%-14s vgpr %3d vload %3d sload %3d vstore %3d vmcnt0 %3d execz %3d valu %4d addr64 %3d f64 %4d insts %5d" % (
             short, v, c(r"global_load|buffer_load"), c(r"s_load"), c(r"global_store"), c(r"vmcnt\(0\)"),
-            c(r"execz"), body.count("\n")))
+            c(r"execz"), c(r"\n\s+v_"), c(r"v_lshl_add_u64|v_add_co_u32|v_lshlrev_b64"), c(r"\n\s+v_\w+_f64"),
+            body.count("\n")))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,104 @@
+// gather.hip -- microbenchmark for the column-gather pattern of the dyn_tend cell
+// kernels: each destination cell sums the 512-B columns (64 doubles) of its edges.
+// Variants: lane = level with 8-B loads (one column per wave) vs two levels per lane
+// with 16-B loads (two columns per wave), optional grouped XCD block order.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+__device__ __forceinline__ int xcdmap(int G) {
+    const int b = (int)blockIdx.x, nb = (int)gridDim.x;
+    if (G <= 0) return b;
+    const int W = G << 3;
+    if (b >= (nb / W) * W) return b;
+    const int w = b / W, r = b - w * W;
+    return w * W + (r & 7) * G + (r >> 3);
+}
+
+template <int NG>
+__global__ __launch_bounds__(256) void g8(const double* __restrict__ T, const int* __restrict__ idx, int nd,
+                                          double* __restrict__ out, int G) {
+    int d = xcdmap(G) * 4 + (int)(threadIdx.x >> 6);
+    d = __builtin_amdgcn_readfirstlane(d);
+    if (d >= nd) return;
+    const int k = threadIdx.x & 63;
+    double v[NG];
+#pragma unroll
+    for (int i = 0; i < NG; i++) v[i] = T[(size_t)idx[d * 10 + i] * 64 + k];
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < NG; i++) s += v[i];
+    out[(size_t)d * 64 + k] = s;
+}
+
+template <int NG>
+__global__ __launch_bounds__(256) void g16(const double* __restrict__ T, const int* __restrict__ idx, int nd,
+                                           double* __restrict__ out, int G) {
+    // 32 lanes per column, lane holds levels 2j, 2j+1
+    const int half = (threadIdx.x >> 5) & 1;
+    int d0 = xcdmap(G) * 8 + (int)(threadIdx.x >> 6) * 2;
+    d0 = __builtin_amdgcn_readfirstlane(d0);
+    const int d = d0 + half;
+    if (d0 >= nd) return;
+    const int j = threadIdx.x & 31;
+    const bool ok = d < nd;
+    const int dd = ok ? d : d0;
+    double2 v[NG];
+#pragma unroll
+    for (int i = 0; i < NG; i++) v[i] = *(const double2*)(T + (size_t)idx[dd * 10 + i] * 64 + 2 * j);
+    double2 s = make_double2(0, 0);
+#pragma unroll
+    for (int i = 0; i < NG; i++) {
+        s.x += v[i].x;
+        s.y += v[i].y;
+    }
+    if (ok) *(double2*)(out + (size_t)d * 64 + 2 * j) = s;
+}
+
+extern "C" int ub_gather(int variant, const double* T, const int* idx, int nd, double* out, int G, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (variant == 0) g8<6><<<(nd + 3) / 4, 256, 0, st>>>(T, idx, nd, out, G);
+    else if (variant == 1) g16<6><<<(nd + 7) / 8, 256, 0, st>>>(T, idx, nd, out, G);
+    else if (variant == 2) g8<10><<<(nd + 3) / 4, 256, 0, st>>>(T, idx, nd, out, G);
+    else if (variant == 3) g16<10><<<(nd + 7) / 8, 256, 0, st>>>(T, idx, nd, out, G);
+    return (int)hipGetLastError();
+}
+
+// streaming: dst[row][k] = a[row][k] + b[row][k] for lanes k < W (W = 56, 57 or 64 of a
+// 64-double row): does a write covering part of the last 64-B chunk of a row cost more?
+__global__ __launch_bounds__(256) void s_add(const double* __restrict__ a, const double* __restrict__ b, int n,
+                                             double* __restrict__ d, int W) {
+    int r = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (r >= n) return;
+    const int k = threadIdx.x & 63;
+    double x = a[(size_t)r * 64 + k] + b[(size_t)r * 64 + k];
+    if (k < W) d[(size_t)r * 64 + k] = x;
+}
+extern "C" int ub_stream(const double* a, const double* b, int n, double* d, int W, void* stream) {
+    s_add<<<(n + 3) / 4, 256, 0, (hipStream_t)stream>>>(a, b, n, d, W);
+    return (int)hipGetLastError();
+}
+
+// the same stream with 16-B lanes (two levels per lane, two rows per wavefront)
+__global__ __launch_bounds__(256) void s_add16(const double* __restrict__ a, const double* __restrict__ b, int n,
+                                               double* __restrict__ d) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;  // double2 index
+    if (i >= (size_t)n * 32) return;
+    const double2 x = ((const double2*)a)[i], y = ((const double2*)b)[i];
+    ((double2*)d)[i] = make_double2(x.x + y.x, x.y + y.y);
+}
+extern "C" int ub_stream16(const double* a, const double* b, int n, double* d, void* stream) {
+    s_add16<<<(n * 32 + 255) / 256, 256, 0, (hipStream_t)stream>>>(a, b, n, d);
+    return (int)hipGetLastError();
+}
+// 8-B lanes, plain 1-D (no row structure): the streaming ceiling of dwordx2
+__global__ __launch_bounds__(256) void s_add8(const double* __restrict__ a, const double* __restrict__ b, size_t n,
+                                              double* __restrict__ d) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    d[i] = a[i] + b[i];
+}
+extern "C" int ub_stream8(const double* a, const double* b, int n, double* d, void* stream) {
+    s_add8<<<((size_t)n * 64 + 255) / 256, 256, 0, (hipStream_t)stream>>>(a, b, (size_t)n * 64, d);
+    return (int)hipGetLastError();
+}
