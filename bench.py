@@ -122,6 +122,8 @@ def main():
     ap.add_argument("--levels", type=int, default=56)
     ap.add_argument("--exact", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="extra mpas_set_option (A/B runs, e.g. xcd=32)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -142,6 +144,9 @@ def main():
     dims = (m.nCells, m.nEdges, m.nVertices, L)
     ctx = lib.Context(*dims, device=local_rank)
     ctx.set_option("exact", args.exact)
+    for kv in args.option:
+        k, v = kv.split("=")
+        ctx.set_option(k, int(v))
     upload_inputs(ctx, st)
     hip = Hip()
     stream = ctx.stream()

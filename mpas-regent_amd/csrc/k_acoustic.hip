@@ -22,7 +22,7 @@ template <int LP, bool EXACT, bool SELF>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCells) return;
+    if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
     double* rtp_f = fw(S, F_rtheta_pp);
     double* rpp_f = fw(S, F_rho_pp);
@@ -185,7 +185,7 @@ template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
-    int grid = (S.nCells + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
     if (exact) {
         if (S.selfc) k_acoustic<LP, true, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
         else k_acoustic<LP, true, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);

@@ -48,7 +48,7 @@ template <int LP, bool RK0>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCells) return;
+    if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
     constexpr bool rk0 = RK0;
     const bool live = k <= L;
@@ -77,6 +77,14 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L);
     const double urz = col_rd<LP>(fd(S, F_uReconstructZonal), c, k, L);
     const double urm = col_rd<LP>(fd(S, F_uReconstructMeridional), c, k, L);
+    // rk0 loads of the tend_rho/dpdz section, ahead of the stores (aliasing for the compiler)
+    double trp = 0.0, qt = 0.0, rb = 0.0, rps = 0.0;
+    if (rk0) {
+        trp = colk(fd(S, F_tend_rho_physics), c);
+        qt = colk(fd(S, F_qtot), c);
+        rb = colk(fd(S, F_rho_base), c);
+        rps = colk(fd(S, F_rho_p_save), c);
+    }
 
     // ---- kdiff (:858-917)
     if (rk0 && (a.horiz_mixing == 0 || a.horiz_mixing == 1 || a.cam_coef > 0.0)) {
@@ -128,9 +136,8 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     // ---- tend_rho, dpdz (:942-951)
     const double rw_p1 = lvl_up<LP>(rw, k);
     if (rk0 && k < L) {
-        colk(fw(S, F_tend_rho), c) = -hd - rdzw * (rw_p1 - rw + colk(fd(S, F_tend_rho_physics), c));
-        double qt = colk(fd(S, F_qtot), c);
-        colk(fw(S, F_dpdz), c) = -kGravity * (colk(fd(S, F_rho_base), c) * (qt) + colk(fd(S, F_rho_p_save), c) * (1.0 + qt));
+        colk(fw(S, F_tend_rho), c) = -hd - rdzw * (rw_p1 - rw + trp);
+        colk(fw(S, F_dpdz), c) = -kGravity * (rb * (qt) + rps * (1.0 + qt));
     }
 
     // ---- w: zeroing (:1170), horizontal advection (:1174-1205, Q13), curvature (:1208-1218)
@@ -177,7 +184,7 @@ template <int LP, bool RK0>
 __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, e = m.ent;
-    if (e >= S.nEdges) return;
+    if (e >= S.nEO) return;
     const size_t p = (size_t)e * LP + k;
     constexpr bool rk0 = RK0;
     const bool live = k <= L;
@@ -217,6 +224,17 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
 #pragma unroll
     for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, colk(tm_f, ad_[j]));
 
+    // loads of the later sections, also ahead of every store (a store could alias them
+    // for the compiler, which would then issue them only after it)
+    const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
+    const double pv = colk(pv_f, e);
+    const double ke1 = colk(ke_f, cell1), ke2 = colk(ke_f, cell2);
+    const double hd1 = colk(hd_f, cell1), hd2 = colk(hd_f, cell2);
+    const double tr_phys = colk(fd(S, F_tend_ru_physics), e);
+    // (the rk0-only loads stay in their section: hoisted they cost more in occupancy,
+    // 138 VGPRs, than the second memory round trip)
+    const double tue_in = rk0 ? 0.0 : colk(fd(S, F_tend_u_euler), e);
+
     const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
     const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
     // ---- wduz (:972-980); level L is never written by the reference: read it
@@ -247,7 +265,6 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
 
     // ---- tend_u (:987-1007)
     double tend_u = -rdzw * (wduz_p - wduz);
-    const double pv = colk(pv_f, e);
     double q = 0.0;
     if (a.exact_q) {
         for (int j = 0; j < neoe; j++) {  // Q10 literal: each term added nVertLevels times
@@ -271,8 +288,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
             q += (woe[j] * colk(u_f, eoe[j]) * workpv) * dL;
         }
     }
-    const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
-    tend_u += rho_edge * (q - (colk(ke_f, cell2) - colk(ke_f, cell1)) * invDc) - u * 0.5 * (colk(hd_f, cell1) + colk(hd_f, cell2));
+    tend_u += rho_edge * (q - (ke2 - ke1) * invDc) - u * 0.5 * (hd1 + hd2);
     {  // curvature (:1011-1017, Q12 literal)
         const double cosA = fd(S, X_cosAngleEdge)[e], cosL = fd(S, X_cosLatEdge)[e];
         tend_u -= (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p)) -
@@ -281,24 +297,26 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
 
     double tue;
     if (rk0) {
-        // ---- pressure gradient (:964-970)
         const double *pp = fd(S, F_pressure_p), *zz = fd(S, F_zz), *dpdz = fd(S, F_dpdz);
-        tue = -colk(fd(S, F_cqu), e) * ((colk(pp, cell2) - colk(pp, cell1)) * invDc / (0.5 * (colk(zz, cell2) + colk(zz, cell1))) -
-                                  0.5 * colk(fd(S, F_zxu), e) * (colk(dpdz, cell1) + colk(dpdz, cell2)));
-        // ---- del2 (:1030-1048)
+        const double *div = fd(S, F_divergence), *vor = fd(S, F_vorticity), *kdiff = fd(S, F_kdiff);
         const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
+        const double cqu = colk(fd(S, F_cqu), e), zxu = colk(fd(S, F_zxu), e);
+        const double pp1 = colk(pp, cell1), pp2 = colk(pp, cell2), zz1 = colk(zz, cell1), zz2 = colk(zz, cell2);
+        const double dz1 = colk(dpdz, cell1), dz2 = colk(dpdz, cell2), dv1 = colk(div, cell1), dv2 = colk(div, cell2);
+        const double vo1 = colk(vor, vertex1), vo2 = colk(vor, vertex2), kf1 = colk(kdiff, cell1), kf2 = colk(kdiff, cell2);
+        // ---- pressure gradient (:964-970)
+        tue = -cqu * ((pp2 - pp1) * invDc / (0.5 * (zz2 + zz1)) - 0.5 * zxu * (dz1 + dz2));
+        // ---- del2 (:1030-1048)
         const double r_dc = invDc;
         const double r_dv = dmin_(fd(S, F_invDvEdge)[e], 4 * r_dc);
-        const double *div = fd(S, F_divergence), *vor = fd(S, F_vorticity), *kdiff = fd(S, F_kdiff);
-        double u_diffusion = (colk(div, cell2) - colk(div, cell1)) * r_dc -
-                             (colk(vor, vertex2) - colk(vor, vertex1)) * r_dv;
+        double u_diffusion = (dv2 - dv1) * r_dc - (vo2 - vo1) * r_dv;
         double delsq_u = 0.0;
         delsq_u += u_diffusion;
         colk(fw(S, F_delsq_u), e) = delsq_u;
-        double kdiffu = 0.5 * (colk(kdiff, cell1) + colk(kdiff, cell2));
+        double kdiffu = 0.5 * (kf1 + kf2);
         tue += rho_edge * kdiffu * u_diffusion * fd(S, F_meshScalingDel2)[e];
     } else {
-        tue = colk(fd(S, F_tend_u_euler), e);
+        tue = tue_in;
     }
     // ---- Rayleigh damping (:1152-1159)
     if (a.rayleigh && k > L - kRayleighLevels + 1)
@@ -308,7 +326,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         colk(fw(S, F_tend_u), e) = tend_u;
     } else {
         if (rk0) colk(fw(S, F_tend_u_euler), e) = tue;
-        tend_u += tue + colk(fd(S, F_tend_ru_physics), e);  // :1161-1163
+        tend_u += tue + tr_phys;  // :1161-1163
         colk(fw(S, F_tend_u), e) = tend_u;
     }
 }
@@ -321,7 +339,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     ColMap<LP> m(S);
     if (m.blk < nVB) {  // delsq_vorticity (:1052-1060)
         const int vx = m.ent, k = m.k;
-        if (vx >= S.nVertices || k >= L) return;
+        if (vx >= S.nVO || k >= L) return;
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)vx * 3;
         const double* sgn = fd(S, F_edgesOnVertex_sign) + (size_t)vx * 3;
         const double iat = fd(S, F_invAreaTriangle)[vx];
@@ -343,7 +361,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     }
     const int c = col_of<LP>(m.blk - nVB);
     const int k = m.k;
-    if (c >= S.nCells) return;
+    if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
     const bool live = k <= L, kl = k < L;
     const int ne = fi(S, F_nEdgesOnCell)[c];
@@ -440,7 +458,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, e = m.ent;
-    if (e >= S.nEdges || k >= L) return;
+    if (e >= S.nEO || k >= L) return;
     const size_t p = (size_t)e * LP + k;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
@@ -464,7 +482,7 @@ template <int LP, bool RK0, bool SELF>
 __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCells) return;
+    if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
     constexpr bool rk0 = RK0;
     const bool kl = k < L;
@@ -523,6 +541,10 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     const double tms = col_rd<LP>(tms_f, c, k, L), tmv = col_rd<LP>(tm, c, k, L);
     double twe = ldz(kl, colk(fd(S, F_tend_w_euler), c));
     double tte = ldz(kl, colk(fd(S, F_tend_theta_euler), c));
+    // theta-section loads, ahead of the w stores that could alias them for the compiler
+    const double rho_zz = colk(fd(S, F_rho_zz), c), rt_diab = colk(fd(S, F_rt_diabatic_tend), c);
+    const double trp = colk(fd(S, F_tend_rtheta_physics), c);
+    const double cqw = rk0 ? colk(fd(S, F_cqw), c) : 0.0;
 
     // ================= W =================
     if (del4 && kl) {  // :1258-1272
@@ -549,7 +571,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     double w = wc;
     if (k > 0 && kl) {  // :1289-1302 (Q14 literal), :1318-1322
         w *= invA - rdzu * (wdwz_p - wdwz);
-        if (rk0) twe -= colk(fd(S, F_cqw), c) * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
+        if (rk0) twe -= cqw * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
         w += twe;
     }
     if (kl) {
@@ -602,12 +624,11 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     const double wdtz_p = lvl_up<LP>(wdtz, k);
     if (!kl) return;
     // :1422-1427, :1477-1479
-    const double rho_zz = colk(fd(S, F_rho_zz), c);
     tend_theta *= invA - rdzw * (wdtz_p - wdtz);
     colk(fw(S, F_tend_rtheta_adv), c) = tend_theta;
     colk(fw(S, F_rthdynten), c) = tend_theta / rho_zz;
-    tend_theta += rho_zz * colk(fd(S, F_rt_diabatic_tend), c);
-    tend_theta += tte + colk(fd(S, F_tend_rtheta_physics), c);
+    tend_theta += rho_zz * rt_diab;
+    tend_theta += tte + trp;
     colk(fw(S, F_tend_theta), c) = tend_theta;
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = tte;
 }
@@ -630,7 +651,7 @@ static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& i
     a.inv_r_earth = 1.0 / a.r_earth;
     a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
     a.prandtl_inv = 1.0 / kPrandtl;
-    const int nCB = (S.nCells + COLS - 1) / COLS, nEB = (S.nEdges + COLS - 1) / COLS, nVB = (S.nVertices + COLS - 1) / COLS;
+    const int nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS, nVB = (S.nVO + COLS - 1) / COLS;
     const int nCV = (a.h4 > 0.0 ? nVB : 0) + nCB, nV4 = a.h4 > 0.0 ? nVB : 0;
     if (a.rk_step == 0) {
         k_dyn_A<LP, true><<<nCB, 256, 0, st>>>(S, a);

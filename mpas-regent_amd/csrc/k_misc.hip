@@ -16,7 +16,7 @@ namespace mpas {
 
 // ---------------------------------------------------------------- setup
 __global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
-    const size_t n = (size_t)S.nCells * S.LP;
+    const size_t n = (size_t)S.nCO * S.LP;
     const double *rw = fd(S, F_rw), *rtp = fd(S, F_rtheta_p), *rp = fd(S, F_rho_p), *w = fd(S, F_w);
     const double *tm = fd(S, F_theta_m), *rz = fd(S, F_rho_zz);
     double *rws = fw(S, F_rw_save), *rtps = fw(S, F_rtheta_p_save), *rps = fw(S, F_rho_p_save);
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
     }
 }
 __global__ __launch_bounds__(256) void k_setup_edges(DevState S) {
-    const size_t n = (size_t)S.nEdges * S.LP;
+    const size_t n = (size_t)S.nEO * S.LP;
     const double *ru = fd(S, F_ru), *u = fd(S, F_u);
     double *rus = fw(S, F_ru_save), *u2 = fw(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
@@ -48,14 +48,14 @@ static int stream_grid(size_t n) {
     return (int)(g < 8192 ? (g ? g : 1) : 8192);
 }
 hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st) {
-    k_setup_edges<<<stream_grid((size_t)S.nEdges * S.LP), 256, 0, st>>>(S);
-    k_setup_cells<<<stream_grid((size_t)S.nCells * S.LP), 256, 0, st>>>(S);
+    k_setup_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S);
+    k_setup_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------- moist
 __global__ __launch_bounds__(256) void k_moist(DevState S) {
-    const size_t n = (size_t)S.nCells * S.LP;
+    const size_t n = (size_t)S.nCO * S.LP;
     double *qtot = fw(S, F_qtot), *cqw = fw(S, F_cqw);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         int k = (int)(i % S.LP);
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_moist(DevState S) {
     }
 }
 hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
-    k_moist<<<stream_grid((size_t)S.nCells * S.LP), 256, 0, st>>>(S);
+    k_moist<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
     return hipGetLastError();
 }
 
@@ -78,7 +78,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCells) return;
+    if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
     const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
     const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
@@ -139,7 +139,7 @@ static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
     double dtseps = .5 * dts * (1.0 + kEpssm);
     double rcv = kRgas / (kCp - kRgas);
     double c2 = kCp * rcv;
-    int grid = (S.nCells + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
     k_vert_imp<LP><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
     return hipGetLastError();
 }
@@ -152,7 +152,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCells) return;
+    if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
 }
 template <int LP>
 static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
-    int grid = (S.nCells + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
     k_set_smlstep<LP><<<grid, 256, 0, st>>>(S);
     return hipGetLastError();
 }
@@ -204,7 +204,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
     ColMap<LP> m(S);
     const int L = S.L, k = m.k, e = m.ent;
-    if (e >= S.nEdges || k >= L) return;
+    if (e >= S.nEO || k >= L) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const int* sh = fi(S, F_isShared);
     if (sh[cell1] && sh[cell2]) return;
@@ -221,7 +221,7 @@ static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
     double smdiv = kSmdiv;
     double rdts = 1.0 / dts;
     double coef_divdamp = 2.0 * smdiv * kLenDisp * rdts;
-    int grid = (S.nEdges + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    int grid = (S.nEO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
     k_div_damp<LP><<<grid, 256, 0, st>>>(S, coef_divdamp);
     return hipGetLastError();
 }
@@ -231,7 +231,7 @@ hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts) {
 
 // ---------------------------------------------------------------- substep finish
 __global__ __launch_bounds__(256) void k_finish_edges(DevState S, int substep, int split, double inv_split) {
-    const size_t n = (size_t)S.nEdges * S.LP;
+    const size_t n = (size_t)S.nEO * S.LP;
     double *ru_save = fw(S, F_ru_save), *u = fw(S, F_u), *ruAvg = fw(S, F_ruAvg), *ruAvgS = fw(S, F_ruAvg_split);
     const double *ru = fd(S, F_ru), *u2 = fd(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256) void k_finish_edges(DevState S, int substep, i
     }
 }
 __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, int split, double inv_split) {
-    const size_t n = (size_t)S.nCells * S.LP;
+    const size_t n = (size_t)S.nCO * S.LP;
     double *wwAvg = fw(S, F_wwAvg), *wwAvgS = fw(S, F_wwAvg_split), *rho_zz = fw(S, F_rho_zz);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         if ((int)(i % S.LP) >= S.L) continue;
@@ -268,8 +268,8 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
 }
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split) {
     double inv = 1.0 / (double)split;
-    k_finish_edges<<<stream_grid((size_t)S.nEdges * S.LP), 256, 0, st>>>(S, substep, split, inv);
-    k_finish_cells<<<stream_grid((size_t)S.nCells * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    k_finish_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    k_finish_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S, substep, split, inv);
     return hipGetLastError();
 }
 
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
         ((int*)S.f[X_ce_c2])[t] = c2;
         ((int*)S.f[X_ce_oth])[t] = (c1 == c) ? c2 : c1;
         ((int*)S.f[X_ce_s1])[t] = (c1 == c) ? 1 : 0;
-        if (i < fi(S, F_nEdgesOnCell)[c] && i < NF && c1 != c && c2 != c) atomicAnd(selfc, 0);
+        if (c < S.nCO && i < fi(S, F_nEdgesOnCell)[c] && i < NF && c1 != c && c2 != c) atomicAnd(selfc, 0);
         fw(S, X_ce_dv)[t] = fd(S, F_dvEdge)[e];
         fw(S, X_ce_idc)[t] = fd(S, F_invDcEdge)[e];
         fw(S, X_ce_msd2)[t] = fd(S, F_meshScalingDel2)[e];

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     ColMap<LP> m(S);
     if (m.blk < nVB) {
         const int v = m.ent, k = m.k;
-        if (v >= S.nVertices || k >= L) return;
+        if (v >= S.nVO || k >= L) return;
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)v * 3;
         const double* sgn = fd(S, F_edgesOnVertexSign) + (size_t)v * 3;
         double vort = 0.0;
@@ -49,7 +49,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     }
     const int c = col_of<LP>(m.blk - nVB);
     const int k = m.k;
-    if (c >= S.nCells || k >= L) return;
+    if (c >= S.nCO || k >= L) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
@@ -85,7 +85,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
     ColMap<LP> m(S);
     const int L = S.L, c = m.ent, k = m.k;
-    if (c >= S.nCells || k >= L) return;
+    if (c >= S.nCO || k >= L) return;
     const size_t p = (size_t)c * LP + k;
     double ke_fact = 1.0 - 0.375;
     double ke = colk(fd(S, F_ke), c) * ke_fact;
@@ -100,40 +100,47 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
     colk(fw(S, F_ke), c) = ke;
 }
 
-template <int LP>
-__global__ __launch_bounds__(256) void k_solve_e(DevState S, int reconstruct_v) {
+template <int LP, bool RECON_V>
+__global__ __launch_bounds__(256) void k_solve_e(DevState S) {
     ColMap<LP> m(S);
     const int L = S.L, e = m.ent, k = m.k;
-    if (e >= S.nEdges || k >= L) return;
-    const size_t p = (size_t)e * LP + k;
+    if (e >= S.nEO || k >= L) return;
     const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
     const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
-    const double* h = fd(S, F_h);
-    const double* u = fd(S, F_u);
-    colk(fw(S, F_h_edge), e) = 0.5 * (colk(h, coe[0]) + colk(h, coe[1]));
-    double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
-    double uu = colk(u, e);
+    const double *h = fd(S, F_h), *u = fd(S, F_u), *pvv = fd(S, F_pv_vertex);
+    // every load before the first store (the stores could alias them for the compiler)
+    const double h1 = colk(h, coe[0]), h2 = colk(h, coe[1]), uu = colk(u, e);
+    const double pv1 = colk(pvv, voe[0]), pv2 = colk(pvv, voe[1]);
+    const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
+    double ue[QF];
+    if (RECON_V) {
+#pragma unroll
+        for (int i = 1; i < QF; i++) ue[i] = colk(u, eoe[i]);
+    }
+    colk(fw(S, F_h_edge), e) = 0.5 * (h1 + h2);
+    const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
     colk(fw(S, F_ke_edge), e) = efac * (uu * uu);
-    if (reconstruct_v) {
+    if (RECON_V) {  // Q23: the sum starts at i = 1
         const int neoe = fi(S, F_nEdgesOnEdge)[e];
-        const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
         const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
         double v = 0;
-        for (int i = 1; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
+#pragma unroll
+        for (int i = 1; i < QF; i++)
+            if (i < neoe) v += wts[i] * ue[i];
+        for (int i = QF; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
         colk(fw(S, F_v), e) = v;
     }
-    const double* pvv = fd(S, F_pv_vertex);
-    colk(fw(S, F_pv_edge), e) = 0.5 * (colk(pvv, voe[0]) + colk(pvv, voe[1]));
+    colk(fw(S, F_pv_edge), e) = 0.5 * (pv1 + pv2);
 }
 
 template <int LP>
 static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
     constexpr int COLS = ColMap<LP>::COLS;
-    int nVB = (S.nVertices + COLS - 1) / COLS, nCB = (S.nCells + COLS - 1) / COLS, nEB = (S.nEdges + COLS - 1) / COLS;
+    int nVB = (S.nVO + COLS - 1) / COLS, nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS;
     k_solve_vc<LP><<<nVB + nCB, 256, 0, st>>>(S, nVB, hollingsworth);
     if (hollingsworth) k_solve_holl<LP><<<nCB, 256, 0, st>>>(S);
-    int reconstruct_v = (rk_step != -1 && rk_step != 2) ? 0 : 1;
-    k_solve_e<LP><<<nEB, 256, 0, st>>>(S, reconstruct_v);
+    if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false><<<nEB, 256, 0, st>>>(S);
+    else k_solve_e<LP, true><<<nEB, 256, 0, st>>>(S);
     return hipGetLastError();
 }
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {

@@ -267,6 +267,9 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.nCells = dims->nCells;
         c->S.nEdges = dims->nEdges;
         c->S.nVertices = dims->nVertices;
+        c->S.nCO = dims->nCells;  // all owned until mpas_halo_owned says otherwise
+        c->S.nEO = dims->nEdges;
+        c->S.nVO = dims->nVertices;
         c->S.L = dims->nVertLevels;
         c->S.LP = LP;
         c->S.xcd = 0;

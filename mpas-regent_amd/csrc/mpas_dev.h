@@ -55,7 +55,9 @@ struct FieldInfo {
 extern const FieldInfo kFields[X_COUNT];
 
 struct DevState {
-    int nCells, nEdges, nVertices, L, LP;
+    int nCells, nEdges, nVertices, L, LP;  // local entity counts (= the zero-slot ids)
+    int nCO, nEO, nVO;  // owned entities, the first of the local ones: every kernel's
+                        // grid (= the counts above unless the mesh is decomposed)
     int xcd;  // 1: XCD-aware block order, 0: dispatcher order (default: measured faster,
               // the Morton-ordered columns of all XCDs then share one Infinity-Cache window)
     int selfc;  // 1 when every cell is one of the two cellsOnEdge of each of its first

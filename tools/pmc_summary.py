@@ -1,12 +1,19 @@
 #!/usr/bin/env python3
-"""Summarise rocprofv3 output for the benchmark: per-kernel average duration from the
-kernel trace and per-dispatch HBM bytes from separate FETCH_SIZE / WRITE_SIZE passes.
+"""Summarise rocprofv3 runs of bench.py per hot-path TASK (the reference's operator):
+average device time per task launch from the kernel trace, and HBM bytes per task launch
+from separate FETCH_SIZE and WRITE_SIZE passes.  Writes the JSON that bench.py reads for
+its roofline "traffic" (profiles/pmc_x1.<n>_L<L>.json, key "tasks").
 
-gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128-B read
-request, i.e. half the bytes of a coalesced stream, so fetched bytes = 2 * FETCH_SIZE KB
-* 1024.  The factor is re-derived here from k_setup_cells / k_setup_edges, whose bytes
-are known exactly (pure copies of L levels of each column), and the measured factor is
-what is applied and reported.
+A task is one or more kernels: its per-launch time is the summed kernel
+time over the run divided by the number of task launches (launches per RK3 step x
+steps, the steps counted from k_setup_cells, which runs exactly once per step).
+
+Byte counters (MI355X_MICROARCH.md, HBM/rocprofv3): on gfx950 FETCH_SIZE tallies each
+128-B L2->fabric read request as 64 B, so fetched bytes = 2 x FETCH_SIZE KiB x 1024;
+Infinity-Cache hits are included (gather re-reads served on-die still count).  The
+factor is checked on the pure-copy setup kernels, which fetch 4 whole 128-B lines per
+column (levels 0..L-1 of the LP = 64 padded row).  WRITE_SIZE is calibrated the same
+way against the setup kernels' written bytes (8 x L per column).
 
 usage: pmc_summary.py --trace DIR --fetch DIR --write DIR --dims nC nE nV L --out FILE
 """
@@ -15,16 +22,59 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
+# kernel -> task (first regex that matches the demangled name)
+KERNEL_TASK = [
+    (r"k_setup_(cells|edges)", "atm_rk_integration_setup"),
+    (r"k_moist", "atm_compute_moist_coefficients"),
+    (r"k_vert_imp", "atm_compute_vert_imp_coefs"),
+    (r"k_dyn_[ABE]<64, true", "atm_compute_dyn_tend_work[rk0]"),
+    (r"k_dyn_[CD]<", "atm_compute_dyn_tend_work[rk0]"),
+    (r"k_dyn_[ABE]<64, false", "atm_compute_dyn_tend_work[rk>0]"),
+    (r"k_set_smlstep", "atm_set_smlstep_pert_variables_work"),
+    (r"k_acoustic", "atm_advance_acoustic_step_work"),
+    (r"k_div_damp", "atm_divergence_damping_3d"),
+    (r"k_solve_", "atm_compute_solve_diagnostics"),
+    (r"k_finish_", "atm_rk_dynamics_substep_finish"),
+]
+# task launches per RK3 step (schedule 1, x1.163842: 7 acoustic substeps)
+LAUNCHES = {"atm_rk_integration_setup": 1, "atm_compute_moist_coefficients": 1, "atm_compute_vert_imp_coefs": 2,
+            "atm_compute_dyn_tend_work[rk0]": 1, "atm_compute_dyn_tend_work[rk>0]": 2,
+            "atm_set_smlstep_pert_variables_work": 3, "atm_advance_acoustic_step_work": 7,
+            "atm_divergence_damping_3d": 7, "atm_compute_solve_diagnostics": 3,
+            "atm_rk_dynamics_substep_finish": 1}
 
-def read_counter(d, name):
-    rows = list(csv.DictReader(open(glob.glob(os.path.join(d, "*counter_collection.csv"))[0])))
-    acc = defaultdict(list)
-    for r in rows:
-        if r["Counter_Name"] == name:
-            acc[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+def task_of(name):
+    for pat, task in KERNEL_TASK:
+        if re.search(pat, name):
+            return task
+    return None
+
+
+def short(name):
+    return name.replace("void ", "").replace("mpas::", "").split("(")[0]
+
+
+def read_counter(d, counter):
+    """total counter value and dispatch count per kernel over the run"""
+    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
+    tot, n = defaultdict(float), defaultdict(int)
+    for r in csv.DictReader(open(f)):
+        if r["Counter_Name"] == counter:
+            tot[short(r["Kernel_Name"])] += float(r["Counter_Value"])
+            n[short(r["Kernel_Name"])] += 1
+    return tot, n
+
+
+def read_trace(d):
+    f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)[0]
+    out = {}
+    for r in csv.DictReader(open(f)):
+        out[short(r["Name"])] = (int(r["Calls"]), float(r["TotalDurationNs"]) * 1e-9)
+    return out
 
 
 def main():
@@ -32,42 +82,62 @@ def main():
     ap.add_argument("--trace")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
-    ap.add_argument("--dims", nargs=4, type=int)
-    ap.add_argument("--out")
+    ap.add_argument("--dims", nargs=4, type=int, required=True)
+    ap.add_argument("--out", required=True)
     a = ap.parse_args()
     nC, nE, nV, L = a.dims
-    out = {"dims": a.dims, "kernels": {}}
+    out = {"dims": a.dims, "kernels": {}, "tasks": {}}
+    tasks = defaultdict(lambda: {"kernels": [], "time_s": 0.0, "fetch_B": 0.0, "write_B": 0.0})
+    steps = None
     if a.trace:
-        for r in csv.DictReader(open(glob.glob(os.path.join(a.trace, "*kernel_stats.csv"))[0])):
-            out["kernels"].setdefault(r["Name"], {})["avg_us"] = float(r["AverageNs"]) / 1e3
-            out["kernels"][r["Name"]]["calls"] = int(r["Calls"])
-    fetch, _ = read_counter(a.fetch, "FETCH_SIZE") if a.fetch else ({}, {})
-    write, _ = read_counter(a.write, "WRITE_SIZE") if a.write else ({}, {})
-    # calibration: setup copies read 6 C3 + (cells) / 2 E3 (edges) arrays of L levels
-    known = {"k_setup_cells": 6 * 8 * nC * L, "k_setup_edges": 2 * 8 * nE * L}
-    kn = [k for k in known if any(k in n for n in fetch)]
-    factor = None
-    if kn:
-        ratios = []
-        for k in kn:
-            name = next(n for n in fetch if k in n)
-            ratios.append(known[k] / (fetch[name] * 1024.0))
-        factor = sum(ratios) / len(ratios)
-    out["fetch_factor_measured"] = factor
-    f = factor if factor else 2.0
-    for name in set(fetch) | set(write):
-        short = name.split("(")[0].split("<")[0].split("::")[-1]
-        d = out["kernels"].setdefault(short, {})
-        d["fetch_bytes"] = fetch.get(name, 0.0) * 1024.0 * f
-        d["write_bytes"] = write.get(name, 0.0) * 1024.0
-        d["hbm_bytes"] = d["fetch_bytes"] + d["write_bytes"]
+        tr = read_trace(a.trace)
+        steps = tr.get("k_setup_cells", (None,))[0]
+        for k, (calls, t) in tr.items():
+            out["kernels"][k] = {"calls": calls, "avg_us": round(t / calls * 1e6, 2)}
+            task = task_of(k)
+            if task:
+                tasks[task]["kernels"].append(k)
+                tasks[task]["time_s"] += t
+    fetch, nf = read_counter(a.fetch, "FETCH_SIZE") if a.fetch else ({}, {})
+    write, nw = read_counter(a.write, "WRITE_SIZE") if a.write else ({}, {})
+    pmc_steps = nf.get("k_setup_cells") or nw.get("k_setup_cells")
+    # calibration on the copies: setup_cells reads 6 cell fields and writes 7 (rho_zz
+    # twice), setup_edges reads and writes 2 edge fields
+    lines = {"k_setup_cells": 6 * nC * 4 * 128, "k_setup_edges": 2 * nE * 4 * 128}
+    payload = {"k_setup_cells": 7 * nC * 8 * L, "k_setup_edges": 2 * nE * 8 * L}
+    ff = [lines[k] / (fetch[k] / nf[k] * 1024.0) for k in lines if fetch.get(k)]
+    wf = [payload[k] / (write[k] / nw[k] * 1024.0) for k in payload if write.get(k)]
+    out["fetch_factor_doc"] = 2.0
+    out["fetch_factor_measured"] = round(sum(ff) / len(ff), 4) if ff else None
+    out["write_factor_measured"] = round(sum(wf) / len(wf), 4) if wf else None
+    wfac = out["write_factor_measured"] or 1.0
+    for k in set(fetch) | set(write):
+        d = out["kernels"].setdefault(k, {})
+        if k in fetch:
+            d["fetch_bytes_per_launch"] = 2.0 * fetch[k] / nf[k] * 1024.0
+        if k in write:
+            d["write_bytes_per_launch"] = wfac * write[k] / nw[k] * 1024.0
+        task = task_of(k)
+        if task and pmc_steps:
+            tasks[task]["fetch_B"] += 2.0 * fetch.get(k, 0.0) * 1024.0
+            tasks[task]["write_B"] += wfac * write.get(k, 0.0) * 1024.0
+    for task, v in tasks.items():
+        o = {"kernels": sorted(set(v["kernels"]))}
+        if steps:
+            o["avg_ms"] = round(v["time_s"] / (steps * LAUNCHES[task]) * 1e3, 4)
+        if pmc_steps:
+            n = pmc_steps * LAUNCHES[task]
+            o["fetch_bytes_per_launch"] = v["fetch_B"] / n
+            o["write_bytes_per_launch"] = v["write_B"] / n
+            o["hbm_bytes_per_launch"] = (v["fetch_B"] + v["write_B"]) / n
+        out["tasks"][task] = o
+    out["steps_traced"], out["steps_counted"] = steps, pmc_steps
     with open(a.out, "w") as fo:
         json.dump(out, fo, indent=1, sort_keys=True)
-    for k, v in sorted(out["kernels"].items(), key=lambda kv: -kv[1].get("avg_us", 0) * kv[1].get("calls", 0)):
-        print(f"{k:34s} avg_us={v.get('avg_us', 0):9.1f} calls={v.get('calls', 0):4d} "
-              f"fetch_MB={v.get('fetch_bytes', 0) / 1e6:9.1f} write_MB={v.get('write_bytes', 0) / 1e6:8.1f} "
-              f"GB/s={(v.get('hbm_bytes', 0) / (v.get('avg_us', 1e9) * 1e-6) / 1e9) if v.get('avg_us') else 0:8.1f}")
-    print("fetch factor", factor)
+    for t, v in sorted(out["tasks"].items(), key=lambda kv: -kv[1].get("avg_ms", 0) * LAUNCHES[kv[0]]):
+        print(f"{t:40s} avg_ms={v.get('avg_ms', 0):8.4f} x{LAUNCHES[t]}  "
+              f"hbm_GB/launch={v.get('hbm_bytes_per_launch', 0) / 1e9:7.3f}")
+    print("fetch factor measured", out["fetch_factor_measured"], "write factor", out["write_factor_measured"])
 
 
 if __name__ == "__main__":
