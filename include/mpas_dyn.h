@@ -113,6 +113,32 @@ int mpas_atm_srk3(mpas_ctx* ctx, double dt, int schedule);
 /* rk_timestep.rg:503 atm_timestep = atm_srk3 with the reference schedule */
 int mpas_atm_timestep(mpas_ctx* ctx, double dt);
 
+/* ---- horizontal decomposition (rk_timestep.rg runs on Legion partitions) --
+ * A context may hold one subdomain: the local entities are its owned ones first, then
+ * its ghosts (everything its owned entities reach through an index array), then the
+ * zero slot; mpasdyn/decomp.py builds the local state and the plan.  Every task then
+ * computes owned entities only, and before each kernel the fields it gathers that an
+ * earlier kernel wrote are exchanged on the ghosts (RCCL send/recv per peer, or the
+ * in-process loopback).  Every rank must call the same tasks in the same order. */
+/* owned counts (the first entities of each kind); default: all local entities */
+int mpas_halo_owned(mpas_ctx* ctx, int32_t nCellsOwned, int32_t nEdgesOwned, int32_t nVerticesOwned);
+/* kind 0 cells, 1 edges, 2 vertices: columns this rank sends to / receives from `peer`,
+ * as local ids, in the order the peer receives / sends them */
+int mpas_halo_plan(mpas_ctx* ctx, int kind, int peer, const int32_t* send_ids, int32_t nsend,
+                   const int32_t* recv_ids, int32_t nrecv);
+/* global id of every local entity of `kind` (n = local count): mpas_fill_synthetic then
+ * generates the same values as on the undecomposed mesh */
+int mpas_set_global_ids(mpas_ctx* ctx, int kind, const int32_t* gids, int32_t n);
+/* transports: RCCL (one process per GPU; rank 0 makes the 128-byte id, the caller
+ * broadcasts it) or loopback (n contexts of one process on one device, rank = index,
+ * each driven by its own host thread) */
+int mpas_rccl_unique_id(void* id128);
+/* (after every mpas_halo_plan call of the context: the transports size their buffers) */
+int mpas_halo_rccl(mpas_ctx* ctx, int nranks, int rank, const void* id128);
+int mpas_halo_loopback(mpas_ctx** ctxs, int n);
+/* halo exchanges made so far and fields moved by them */
+int mpas_halo_stats(mpas_ctx* ctx, int64_t* exchanges, int64_t* fields);
+
 /* ---- instrumentation ------------------------------------------------------------ */
 /* With timing on, every task call is bracketed by HIP events on the task stream and its
  * device time accumulated per task name; mpas_timing_get returns calls and total ms. */

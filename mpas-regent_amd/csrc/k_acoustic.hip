@@ -15,6 +15,7 @@
 // variant evaluates the literal expression level by level (lane k-1 -> lane k
 // broadcast) and is bit-identical to the oracle; it is the reference for the scan.
 #include "mpas_dev.h"
+#include "mpas_halo.h"
 
 namespace mpas {
 
@@ -186,6 +187,7 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
     int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    HALO_BEFORE(S, st, F_ru_p, F_theta_m);
     if (exact) {
         if (S.selfc) k_acoustic<LP, true, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
         else k_acoustic<LP, true, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
@@ -193,6 +195,7 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
         if (S.selfc) k_acoustic<LP, false, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
         else k_acoustic<LP, false, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
     }
+    HALO_WROTE(S, F_rtheta_pp_old, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {

@@ -24,6 +24,7 @@
 // loads of the first NF/QF/AF entries unconditionally (padding ids are valid), then
 // accumulates in the reference's order; longer lists finish in a generic tail loop.
 #include "mpas_dev.h"
+#include "mpas_halo.h"
 
 namespace mpas {
 
@@ -653,20 +654,39 @@ static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& i
     a.prandtl_inv = 1.0 / kPrandtl;
     const int nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS, nVB = (S.nVO + COLS - 1) / COLS;
     const int nCV = (a.h4 > 0.0 ? nVB : 0) + nCB, nV4 = a.h4 > 0.0 ? nVB : 0;
-    if (a.rk_step == 0) {
-        k_dyn_A<LP, true><<<nCB, 256, 0, st>>>(S, a);
+    const bool rk0 = a.rk_step == 0, del4 = rk0 && a.h4 > 0.0;
+    // halo: fields each kernel gathers through an index array / fields it writes
+    HALO_BEFORE(S, st, F_ru, F_u, F_v);
+    if (rk0) k_dyn_A<LP, true><<<nCB, 256, 0, st>>>(S, a);
+    else k_dyn_A<LP, false><<<nCB, 256, 0, st>>>(S, a);
+    HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz, X_wc);
+    if (rk0) {
+        HALO_BEFORE(S, st, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p, F_zz, F_dpdz,
+                    F_divergence, F_kdiff, F_vorticity);
         k_dyn_B<LP, true><<<nEB, 256, 0, st>>>(S, a);
+        HALO_WROTE(S, X_F, F_tend_u, F_tend_u_euler, F_delsq_u);
+        HALO_BEFORE(S, st, F_delsq_u, F_rho_edge, F_kdiff, X_wc, F_theta_m);
         if (S.selfc) k_dyn_C<LP, true><<<nCV, 256, 0, st>>>(S, a, nV4);
         else k_dyn_C<LP, false><<<nCV, 256, 0, st>>>(S, a, nV4);
-        if (a.h4 > 0.0) k_dyn_D<LP><<<nEB, 256, 0, st>>>(S, a);
+        HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
+                   F_tend_theta_euler);
+        if (del4) {
+            HALO_BEFORE(S, st, F_delsq_divergence, F_delsq_vorticity);
+            k_dyn_D<LP><<<nEB, 256, 0, st>>>(S, a);
+            HALO_WROTE(S, F_tend_u_euler, F_tend_u);
+        }
+        HALO_BEFORE(S, st, F_ru, X_F, F_delsq_w, F_delsq_theta);
         if (S.selfc) k_dyn_E<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
         else k_dyn_E<LP, true, false><<<nCB, 256, 0, st>>>(S, a);
     } else {
-        k_dyn_A<LP, false><<<nCB, 256, 0, st>>>(S, a);
+        HALO_BEFORE(S, st, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
         k_dyn_B<LP, false><<<nEB, 256, 0, st>>>(S, a);
+        HALO_WROTE(S, X_F, F_tend_u);
+        HALO_BEFORE(S, st, F_ru, X_F, F_ru_save, F_theta_m_save);
         if (S.selfc) k_dyn_E<LP, false, true><<<nCB, 256, 0, st>>>(S, a);
         else k_dyn_E<LP, false, false><<<nCB, 256, 0, st>>>(S, a);
     }
+    HALO_WROTE(S, F_w, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
     return hipGetLastError();
 }
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& in) {

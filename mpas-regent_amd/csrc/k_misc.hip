@@ -10,6 +10,7 @@
 // operand order and the library is built with -ffp-contract=off, so results are
 // bit-identical to the oracle's.
 #include "mpas_dev.h"
+#include "mpas_halo.h"
 #include "mpas_synth.h"
 
 namespace mpas {
@@ -50,6 +51,8 @@ static int stream_grid(size_t n) {
 hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st) {
     k_setup_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S);
     k_setup_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
+    HALO_WROTE(S, F_ru_save, F_u_2, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2,
+               F_rho_zz_old_split);
     return hipGetLastError();
 }
 
@@ -70,6 +73,7 @@ __global__ __launch_bounds__(256) void k_moist(DevState S) {
 }
 hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
     k_moist<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
+    HALO_WROTE(S, F_qtot, F_cqw);
     return hipGetLastError();
 }
 
@@ -141,6 +145,7 @@ static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
     double c2 = kCp * rcv;
     int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
     k_vert_imp<LP><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
+    HALO_WROTE(S, F_coftz, F_cofwt, F_gamma_tri, F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri);
     return hipGetLastError();
 }
 hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts) {
@@ -194,7 +199,9 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
 template <int LP>
 static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
     int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    HALO_BEFORE(S, st, F_u_tend);
     k_set_smlstep<LP><<<grid, 256, 0, st>>>(S);
+    HALO_WROTE(S, F_w);
     return hipGetLastError();
 }
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st); }
@@ -222,7 +229,9 @@ static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
     double rdts = 1.0 / dts;
     double coef_divdamp = 2.0 * smdiv * kLenDisp * rdts;
     int grid = (S.nEO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
+    HALO_BEFORE(S, st, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
     k_div_damp<LP><<<grid, 256, 0, st>>>(S, coef_divdamp);
+    HALO_WROTE(S, F_ru_p);
     return hipGetLastError();
 }
 hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts) {
@@ -270,6 +279,8 @@ hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep,
     double inv = 1.0 / (double)split;
     k_finish_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S, substep, split, inv);
     k_finish_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    HALO_WROTE(S, F_ru_save, F_u, F_ruAvg, F_ruAvg_split, F_wwAvg, F_wwAvg_split, F_rho_zz, F_rw_save,
+               F_rtheta_p_save, F_rho_p_save, F_w, F_theta_m);
     return hipGetLastError();
 }
 
@@ -313,7 +324,7 @@ hipError_t launch_prepare(DevState& S, hipStream_t st) {
 
 // ---------------------------------------------------------------- synthetic fill
 __global__ __launch_bounds__(256) void k_fill(void* dst, int fid, int kind, long n, int W, int levels, int LP,
-                                              int dist, double lo, double hi, uint64_t seed) {
+                                              int dist, double lo, double hi, uint64_t seed, const int* gid) {
     double* d = (double*)dst;
     const size_t total = (size_t)n * W * levels;
     for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
@@ -321,7 +332,8 @@ __global__ __launch_bounds__(256) void k_fill(void* dst, int fid, int kind, long
         size_t r = t / levels;
         int i = (int)(r % W);
         long e = (long)(r / W);
-        double v = mpas_synth_value(seed, (uint32_t)fid, (uint64_t)e, (uint32_t)k, (uint32_t)i, dist, lo, hi);
+        const long g = gid ? (long)gid[e] : e;  // the global entity id: same value on every rank
+        double v = mpas_synth_value(seed, (uint32_t)fid, (uint64_t)g, (uint32_t)k, (uint32_t)i, dist, lo, hi);
         if (kind == K_ZV) d[k] = v;
         else if (kind == K_C3V) d[((size_t)e * W + i) * LP + k] = v;
         else d[(size_t)e * LP + k] = v;
@@ -333,16 +345,18 @@ hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t see
         if (fi_.dist == D_M) continue;
         long n = 0;
         int W = 1;
+        const int* gid = nullptr;
         switch (fi_.kind) {
-            case K_C3: n = S.nCells; break;
-            case K_E3: n = S.nEdges; break;
-            case K_V3: n = S.nVertices; break;
-            case K_C3V: n = S.nCells; W = fi_.width; break;
+            case K_C3: n = S.nCells; gid = S.gid[0]; break;
+            case K_E3: n = S.nEdges; gid = S.gid[1]; break;
+            case K_V3: n = S.nVertices; gid = S.gid[2]; break;
+            case K_C3V: n = S.nCells; W = fi_.width; gid = S.gid[0]; break;
             case K_ZV: n = 1; break;
             default: continue;
         }
         size_t total = (size_t)n * W * (S.L + 1);
-        k_fill<<<stream_grid(total), 256, 0, st>>>(S.f[f], f, fi_.kind, n, W, S.L + 1, S.LP, fi_.dist, fi_.lo, fi_.hi, seed);
+        k_fill<<<stream_grid(total), 256, 0, st>>>(S.f[f], f, fi_.kind, n, W, S.L + 1, S.LP, fi_.dist, fi_.lo, fi_.hi, seed,
+                                                   gid);
     }
     return hipGetLastError();
 }

@@ -8,6 +8,7 @@
 //   2. edges: h_edge, ke_edge, v (only rk_step in {-1, 2}, Q23 starts at i = 1), pv_edge
 // Hollingsworth (never true on the path, rk_timestep.rg:467) adds a ke_vertex pass.
 #include "mpas_dev.h"
+#include "mpas_halo.h"
 
 namespace mpas {
 
@@ -137,10 +138,18 @@ template <int LP>
 static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
     constexpr int COLS = ColMap<LP>::COLS;
     int nVB = (S.nVO + COLS - 1) / COLS, nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS;
+    HALO_BEFORE(S, st, F_u);
     k_solve_vc<LP><<<nVB + nCB, 256, 0, st>>>(S, nVB, hollingsworth);
-    if (hollingsworth) k_solve_holl<LP><<<nCB, 256, 0, st>>>(S);
+    HALO_WROTE(S, F_vorticity, F_pv_vertex, F_ke_vertex, F_divergence, F_ke);
+    if (hollingsworth) {
+        HALO_BEFORE(S, st, F_ke_vertex);
+        k_solve_holl<LP><<<nCB, 256, 0, st>>>(S);
+        HALO_WROTE(S, F_ke);
+    }
+    HALO_BEFORE(S, st, F_h, F_u, F_pv_vertex);
     if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false><<<nEB, 256, 0, st>>>(S);
     else k_solve_e<LP, true><<<nEB, 256, 0, st>>>(S);
+    HALO_WROTE(S, F_h_edge, F_ke_edge, F_v, F_pv_edge);
     return hipGetLastError();
 }
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {

@@ -2,6 +2,8 @@
 // entry points of include/mpas_dyn.h, and the atm_srk3 driver (rk_timestep.rg:361-500).
 #include <hip/hip_runtime.h>
 
+#include <memory>
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -11,6 +13,7 @@
 #include <vector>
 
 #include "mpas_dev.h"
+#include "mpas_halo.h"
 #include "mpas_dyn.h"
 
 namespace mpas {
@@ -57,6 +60,9 @@ struct mpas_ctx {
     std::vector<double> task_ms;
     std::vector<TimedCall> pending;
     std::vector<hipEvent_t> event_pool;
+    std::unique_ptr<Halo> halo;           // decomposed mesh only
+    std::shared_ptr<LoopGroup> loopgrp;   // in-process loopback transport
+    int* gid_dev[3] = {nullptr, nullptr, nullptr};
 };
 
 namespace {
@@ -157,7 +163,11 @@ void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
         c->dirty = false;
     }
     hipError_t e = fn();
-    if (e != hipSuccess) throw Fail{MPAS_EHIP, std::string(name) + ": " + hipGetErrorString(e)};
+    if (e != hipSuccess) {
+        if (c->halo && !c->halo->err.empty())
+            throw Fail{MPAS_ERCCL, std::string(name) + ": halo exchange: " + c->halo->err};
+        throw Fail{MPAS_EHIP, std::string(name) + ": " + hipGetErrorString(e)};
+    }
     if (c->timing) {
         hipcheck(hipEventRecord(e1, c->stream), "hipEventRecord");
         c->pending.push_back({ti, e0, e1});
@@ -305,6 +315,10 @@ int mpas_ctx_destroy(mpas_ctx* c) {
         (void)hipEventDestroy(t.e1);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    c->halo.reset();
+    c->loopgrp.reset();
+    for (auto p : c->gid_dev)
+        if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return MPAS_OK;
@@ -399,6 +413,7 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
         }
         hipcheck(hipMemcpy(c->S.f[f], buf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
         c->dirty = true;
+        if (c->halo) c->halo->stale[f] = 0;  // uploaded ghosts are the global values
         // derived mesh arrays: cos() on the host with the same libm as the oracle
         int derived = -1;
         if (f == F_angleEdge) derived = X_cosAngleEdge;
@@ -459,7 +474,129 @@ int mpas_fill_synthetic(mpas_ctx* c, uint64_t seed) {
         hipcheck(hipSetDevice(c->device), "hipSetDevice");
         hipcheck(launch_fill_synthetic(c->S, c->stream, seed), "fill_synthetic");
         hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+        if (c->halo)  // filled from global ids: ghosts hold the global values
+            for (auto& v : c->halo->stale) v = 0;
     });
+}
+
+// ---- decomposition (mpasdyn/decomp.py builds the local state and the plan) ----------
+namespace {
+Halo* halo_of(mpas_ctx* c) {
+    if (!c->halo) {
+        c->halo.reset(new Halo());
+        c->halo->stale.assign(X_COUNT, 0);
+        c->S.halo = c->halo.get();
+    }
+    return c->halo.get();
+}
+int* dev_ints(const int32_t* h, int n) {
+    int* d = nullptr;
+    hipcheck(hipMalloc(&d, sizeof(int) * (size_t)(n > 0 ? n : 1)), "hipMalloc");
+    if (n > 0) hipcheck(hipMemcpy(d, h, sizeof(int) * (size_t)n, hipMemcpyHostToDevice), "hipMemcpy H2D");
+    return d;
+}
+}  // namespace
+
+int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32_t nVerticesOwned) {
+    return guarded(c, [&] {
+        if (nCellsOwned < 0 || nCellsOwned > c->S.nCells || nEdgesOwned < 0 || nEdgesOwned > c->S.nEdges ||
+            nVerticesOwned < 0 || nVerticesOwned > c->S.nVertices)
+            throw Fail{MPAS_EINVAL, "mpas_halo_owned: owned counts exceed the local counts"};
+        c->S.nCO = nCellsOwned;
+        c->S.nEO = nEdgesOwned;
+        c->S.nVO = nVerticesOwned;
+        c->dirty = true;
+    });
+}
+
+int mpas_halo_plan(mpas_ctx* c, int kind, int peer, const int32_t* send_ids, int32_t nsend, const int32_t* recv_ids,
+                   int32_t nrecv) {
+    return guarded(c, [&] {
+        if (kind < 0 || kind > 2 || peer < 0 || nsend < 0 || nrecv < 0 || (nsend && !send_ids) || (nrecv && !recv_ids))
+            throw Fail{MPAS_EINVAL, "mpas_halo_plan: bad arguments"};
+        const int lim = kind == 0 ? c->S.nCells : kind == 1 ? c->S.nEdges : c->S.nVertices;
+        const int own = kind == 0 ? c->S.nCO : kind == 1 ? c->S.nEO : c->S.nVO;
+        for (int i = 0; i < nsend; i++)
+            if (send_ids[i] < 0 || send_ids[i] >= own) throw Fail{MPAS_EINVAL, "mpas_halo_plan: send id not owned"};
+        for (int i = 0; i < nrecv; i++)
+            if (recv_ids[i] < own || recv_ids[i] >= lim) throw Fail{MPAS_EINVAL, "mpas_halo_plan: recv id not a ghost"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        Halo* h = halo_of(c);
+        HaloPeer p;
+        p.peer = peer;
+        p.nsend = nsend;
+        p.nrecv = nrecv;
+        p.d_send = dev_ints(send_ids, nsend);
+        p.d_recv = dev_ints(recv_ids, nrecv);
+        h->peers[kind].push_back(p);
+    });
+}
+
+int mpas_set_global_ids(mpas_ctx* c, int kind, const int32_t* gids, int32_t n) {
+    return guarded(c, [&] {
+        const int lim = kind == 0 ? c->S.nCells : kind == 1 ? c->S.nEdges : c->S.nVertices;
+        if (kind < 0 || kind > 2 || n != lim || !gids) throw Fail{MPAS_EINVAL, "mpas_set_global_ids: bad arguments"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        if (c->gid_dev[kind]) hipcheck(hipFree(c->gid_dev[kind]), "hipFree");
+        c->gid_dev[kind] = dev_ints(gids, n);
+        c->S.gid[kind] = c->gid_dev[kind];
+    });
+}
+
+int mpas_halo_loopback(mpas_ctx** ctxs, int n) {
+    if (!ctxs || n < 1) return MPAS_EINVAL;
+    for (int i = 0; i < n; i++)
+        if (!ctxs[i] || ctxs[i]->device != ctxs[0]->device) return MPAS_EINVAL;
+    return guarded(ctxs[0], [&] {
+        hipcheck(hipSetDevice(ctxs[0]->device), "hipSetDevice");
+        auto g = std::make_shared<LoopGroup>();
+        g->n = n;
+        g->packed.resize(n);
+        g->copied.resize(n);
+        for (int i = 0; i < n; i++) {
+            hipcheck(hipEventCreateWithFlags(&g->packed[i], hipEventDisableTiming), "hipEventCreate");
+            hipcheck(hipEventCreateWithFlags(&g->copied[i], hipEventDisableTiming), "hipEventCreate");
+            hipcheck(hipEventRecord(g->copied[i], ctxs[i]->stream), "hipEventRecord");
+        }
+        for (int i = 0; i < n; i++) {
+            Halo* h = halo_of(ctxs[i]);
+            hipcheck(h->reserve(ctxs[i]->S.LP), "halo buffers");
+            h->nranks = n;
+            h->rank = i;
+            h->loop = g.get();
+            g->members.push_back(h);
+            g->streams.push_back(ctxs[i]->stream);
+            ctxs[i]->loopgrp = g;
+        }
+    });
+}
+
+int mpas_rccl_unique_id(void* out128) {
+    if (!out128) return MPAS_EINVAL;
+    std::string err;
+    if (rccl_unique_id(out128, err) != 0) {
+        g_create_err = err;
+        return MPAS_ERCCL;
+    }
+    return MPAS_OK;
+}
+
+int mpas_halo_rccl(mpas_ctx* c, int nranks, int rank, const void* id128) {
+    return guarded(c, [&] {
+        if (nranks < 1 || rank < 0 || rank >= nranks || !id128) throw Fail{MPAS_EINVAL, "mpas_halo_rccl: bad arguments"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        Halo* h = halo_of(c);
+        hipcheck(h->reserve(c->S.LP), "halo buffers");
+        std::string err;
+        if (rccl_init(h, nranks, rank, id128, err) != 0) throw Fail{MPAS_ERCCL, err};
+    });
+}
+
+int mpas_halo_stats(mpas_ctx* c, int64_t* exchanges, int64_t* fields) {
+    if (!c || !exchanges || !fields) return MPAS_EINVAL;
+    *exchanges = c->halo ? c->halo->exchanges : 0;
+    *fields = c->halo ? c->halo->fields_moved : 0;
+    return MPAS_OK;
 }
 
 #define MPAS_TASK(NAME, CALL) \

@@ -54,6 +54,8 @@ struct FieldInfo {
 };
 extern const FieldInfo kFields[X_COUNT];
 
+struct Halo;  // mpas_halo.h
+
 struct DevState {
     int nCells, nEdges, nVertices, L, LP;  // local entity counts (= the zero-slot ids)
     int nCO, nEO, nVO;  // owned entities, the first of the local ones: every kernel's
@@ -65,6 +67,9 @@ struct DevState {
                 // only the other cell of an edge and use their own column for the cell
                 // itself (SELF path); 0 (e.g. the literal 1-based "ref" ids) gathers both
     void* f[X_COUNT];
+    Halo* halo;  // host-side halo exchanger of a decomposed mesh, nullptr otherwise
+    const int* gid[3];  // device global ids of the local cells/edges/vertices (decomposed
+                        // meshes: the synthetic fill hashes them), nullptr = identity
 };
 
 // physical constants (constants.rg:27-66), identical to the oracle's

@@ -1,0 +1,100 @@
+// mpas_halo.h -- halo exchange of the horizontally decomposed hot path.
+//
+// Each rank owns a subdomain plus the ghost entities its owned entities reach through
+// the index arrays (mpasdyn/decomp.py builds the local numbering and the plan).  Every
+// kernel computes owned entities only.  A field gathered by a kernel must be fresh on
+// the ghosts: the launchers declare, per kernel, the fields it gathers through an index
+// array (halo_before) and the fields it writes (halo_wrote).  A written field becomes
+// stale; the next kernel that gathers it first exchanges it (one grouped exchange of
+// all its stale gathered fields), after which it is fresh.  Correct by construction
+// given complete gather lists -- the loopback N-shard = 1-shard parity test checks them.
+//
+// Transport: RCCL point-to-point (ncclSend/ncclRecv of one packed buffer per peer inside
+// ncclGroupStart/End, on the task stream; librccl resolved with dlopen, so the process
+// shares the RCCL that torch.distributed loaded) for one process per GPU, or an
+// in-process loopback for N contexts on one device driven by N host threads (hipMemcpy
+// between the contexts' buffers; the single-GPU test of the decomposition).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <condition_variable>
+#include <cstdint>
+#include <initializer_list>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace mpas {
+
+struct DevState;
+
+enum HaloKind { HK_CELL = 0, HK_EDGE = 1, HK_VERTEX = 2 };
+
+struct HaloPeer {
+    int peer = -1;
+    int nsend = 0, nrecv = 0;
+    int* d_send = nullptr;  // local ids, device
+    int* d_recv = nullptr;
+};
+
+struct LoopGroup;  // loopback transport shared by the contexts of one process
+struct RcclComm;   // RCCL transport
+
+struct Halo {
+    int nranks = 1, rank = 0;
+    std::vector<HaloPeer> peers[3];
+    std::vector<uint8_t> stale;  // per field id
+    // per-peer packed buffers: [cell fields][edge fields][vertex fields] columns of LP doubles
+    double* sendbuf = nullptr;
+    double* recvbuf = nullptr;
+    size_t cap = 0;  // doubles per buffer
+    LoopGroup* loop = nullptr;
+    RcclComm* rccl = nullptr;
+    std::string err;
+    int64_t exchanges = 0, fields_moved = 0;
+
+    ~Halo();
+    hipError_t reserve(int LP);  // size the packed buffers for the largest exchange
+    // make every field in `gathers` that is stale fresh on the ghosts
+    hipError_t before(const DevState& S, hipStream_t st, std::initializer_list<int> gathers);
+    void wrote(std::initializer_list<int> fields);
+    hipError_t exchange(const DevState& S, hipStream_t st, const std::vector<int>& fields);
+};
+
+// launchers: no-ops without a decomposition
+#define HALO_BEFORE(S, st, ...)                                                   \
+    do {                                                                          \
+        if ((S).halo) {                                                           \
+            hipError_t he_ = (S).halo->before((S), (st), {__VA_ARGS__});          \
+            if (he_ != hipSuccess) return he_;                                    \
+        }                                                                         \
+    } while (0)
+#define HALO_WROTE(S, ...)                          \
+    do {                                            \
+        if ((S).halo) (S).halo->wrote({__VA_ARGS__}); \
+    } while (0)
+
+// loopback group (one per process, N shards)
+struct LoopGroup {
+    int n = 0;
+    std::vector<Halo*> members;
+    std::vector<hipStream_t> streams;
+    std::vector<hipEvent_t> packed, copied;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    int64_t generation = 0;
+    bool broken = false;
+    bool barrier(double timeout_s);  // false on timeout (a shard stopped driving)
+    ~LoopGroup() {
+        for (auto e : packed) (void)hipEventDestroy(e);
+        for (auto e : copied) (void)hipEventDestroy(e);
+    }
+};
+
+// transports (mpas_halo.hip)
+int rccl_unique_id(void* out128, std::string& err);
+int rccl_init(Halo* h, int nranks, int rank, const void* id128, std::string& err);
+void rccl_free(RcclComm* c);
+
+}  // namespace mpas

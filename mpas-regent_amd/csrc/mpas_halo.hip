@@ -1,0 +1,352 @@
+// mpas_halo.hip -- halo exchange (see mpas_halo.h): pack/unpack kernels, staleness
+// bookkeeping, RCCL and loopback transports.
+#include "mpas_halo.h"
+
+#include <dlfcn.h>
+
+#include <chrono>
+#include <cstring>
+
+#include "mpas_dev.h"
+
+namespace mpas {
+
+// ------------------------------------------------------------------ pack / unpack
+constexpr int kMaxSeg = 128;
+struct SegList {
+    double* f[kMaxSeg];      // field base (LP doubles per column)
+    const int* ids[kMaxSeg];  // local column ids
+    long start[kMaxSeg + 1];  // first packed column of each segment
+    int nseg, LP;
+};
+
+// one thread per packed double: column j of the buffer <-> column ids[j - start] of f
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_halo_copy(SegList sl, double* buf) {
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    const long col = t / sl.LP;
+    const int k = (int)(t % sl.LP);
+    if (col >= sl.start[sl.nseg]) return;
+    int s = 0;
+    while (col >= sl.start[s + 1]) s++;
+    const long j = col - sl.start[s];
+    double* f = sl.f[s] + (size_t)sl.ids[s][j] * sl.LP + k;
+    if (PACK) buf[t] = *f;
+    else *f = buf[t];
+}
+
+static int kind_of_field(int f) {
+    switch (kFields[f].kind) {
+        case K_C3: return HK_CELL;
+        case K_E3: return HK_EDGE;
+        case K_V3: return HK_VERTEX;
+        default: return -1;
+    }
+}
+
+Halo::~Halo() {
+    for (auto& v : peers)
+        for (auto& p : v) {
+            if (p.d_send) (void)hipFree(p.d_send);
+            if (p.d_recv) (void)hipFree(p.d_recv);
+        }
+    if (sendbuf) (void)hipFree(sendbuf);
+    if (recvbuf) (void)hipFree(recvbuf);
+    if (rccl) rccl_free(rccl);
+}
+
+hipError_t Halo::reserve(int LP) {
+    // the largest exchange moves every field of every kind at once
+    long fk[3] = {0, 0, 0};
+    for (int f = 0; f < X_COUNT; f++) {
+        int k = kind_of_field(f);
+        if (k >= 0) fk[k]++;
+    }
+    long s = 0, r = 0;
+    for (int k = 0; k < 3; k++)
+        for (const auto& p : peers[k]) {
+            s += (long)p.nsend * fk[k];
+            r += (long)p.nrecv * fk[k];
+        }
+    const size_t need = (size_t)std::max(std::max(s, r), 1L) * LP;
+    if (need <= cap) return hipSuccess;
+    if (sendbuf) (void)hipFree(sendbuf);
+    if (recvbuf) (void)hipFree(recvbuf);
+    sendbuf = recvbuf = nullptr;
+    cap = 0;
+    hipError_t e;
+    if ((e = hipMalloc(&sendbuf, need * sizeof(double))) != hipSuccess) return e;
+    if ((e = hipMalloc(&recvbuf, need * sizeof(double))) != hipSuccess) return e;
+    cap = need;
+    return hipSuccess;
+}
+
+void Halo::wrote(std::initializer_list<int> fields) {
+    for (int f : fields) stale[f] = 1;
+}
+
+hipError_t Halo::before(const DevState& S, hipStream_t st, std::initializer_list<int> gathers) {
+    std::vector<int> need;
+    for (int f : gathers)
+        if (stale[f]) need.push_back(f);
+    if (need.empty()) return hipSuccess;
+    hipError_t e = exchange(S, st, need);
+    if (e == hipSuccess)
+        for (int f : need) stale[f] = 0;
+    return e;
+}
+
+// ------------------------------------------------------------------ RCCL (dlopen)
+struct Uid128 {
+    char b[128];
+};
+struct RcclApi {
+    void* h = nullptr;
+    int (*GetUniqueId)(Uid128*) = nullptr;
+    int (*CommInitRank)(void**, int, Uid128, int) = nullptr;
+    int (*CommDestroy)(void*) = nullptr;
+    int (*GroupStart)() = nullptr;
+    int (*GroupEnd)() = nullptr;
+    int (*Send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
+    int (*Recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
+    const char* (*GetErrorString)(int) = nullptr;
+};
+constexpr int kNcclFloat64 = 8;  // ncclDouble in rccl.h's ncclDataType_t
+
+static RcclApi* rccl_api(std::string& err) {
+    static RcclApi api;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        // share the RCCL already in the process (torch.distributed), else load ROCm's
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (h) {
+            api.h = h;
+            api.GetUniqueId = (int (*)(Uid128*))dlsym(h, "ncclGetUniqueId");
+            api.CommInitRank = (int (*)(void**, int, Uid128, int))dlsym(h, "ncclCommInitRank");
+            api.CommDestroy = (int (*)(void*))dlsym(h, "ncclCommDestroy");
+            api.GroupStart = (int (*)())dlsym(h, "ncclGroupStart");
+            api.GroupEnd = (int (*)())dlsym(h, "ncclGroupEnd");
+            api.Send = (int (*)(const void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclSend");
+            api.Recv = (int (*)(void*, size_t, int, int, void*, hipStream_t))dlsym(h, "ncclRecv");
+            api.GetErrorString = (const char* (*)(int))dlsym(h, "ncclGetErrorString");
+        }
+    }
+    if (!api.h || !api.GetUniqueId || !api.CommInitRank || !api.GroupStart || !api.GroupEnd || !api.Send ||
+        !api.Recv) {
+        err = "librccl.so.1 not loadable or incomplete";
+        return nullptr;
+    }
+    return &api;
+}
+
+struct RcclComm {
+    void* comm = nullptr;
+    ~RcclComm() {
+        std::string e;
+        RcclApi* a = rccl_api(e);
+        if (a && comm && a->CommDestroy) a->CommDestroy(comm);
+    }
+};
+
+int rccl_unique_id(void* out128, std::string& err) {
+    RcclApi* a = rccl_api(err);
+    if (!a) return -1;
+    int r = a->GetUniqueId((Uid128*)out128);
+    if (r != 0) {
+        err = std::string("ncclGetUniqueId: ") + (a->GetErrorString ? a->GetErrorString(r) : "error");
+        return -1;
+    }
+    return 0;
+}
+
+int rccl_init(Halo* h, int nranks, int rank, const void* id128, std::string& err) {
+    RcclApi* a = rccl_api(err);
+    if (!a) return -1;
+    Uid128 id;
+    std::memcpy(id.b, id128, 128);
+    auto* c = new RcclComm();
+    int r = a->CommInitRank(&c->comm, nranks, id, rank);
+    if (r != 0) {
+        err = std::string("ncclCommInitRank: ") + (a->GetErrorString ? a->GetErrorString(r) : "error");
+        delete c;
+        return -1;
+    }
+    h->rccl = c;
+    h->nranks = nranks;
+    h->rank = rank;
+    return 0;
+}
+void rccl_free(RcclComm* c) { delete c; }
+
+// ------------------------------------------------------------------ loopback barrier
+bool LoopGroup::barrier(double timeout_s) {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return false;
+    const int64_t gen = generation;
+    if (++arrived == n) {
+        arrived = 0;
+        generation++;
+        cv.notify_all();
+        return true;
+    }
+    bool ok = cv.wait_for(lk, std::chrono::duration<double>(timeout_s), [&] { return generation != gen || broken; });
+    if (!ok || broken) {
+        broken = true;
+        cv.notify_all();
+        return false;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ exchange
+// per-peer packed regions, identical order on both sides: cells, edges, vertices; in
+// each kind the fields in the order of `fields` (the same on every rank: the stale sets
+// evolve identically because every rank runs the same task sequence)
+struct Region {
+    int peer;
+    long soff, scols, roff, rcols;  // columns
+};
+
+static void plan_regions(const Halo& h, const std::vector<int>& fields, std::vector<Region>& reg,
+                         std::vector<int> (&byk)[3]) {
+    for (auto& v : byk) v.clear();
+    for (int f : fields) {
+        int k = kind_of_field(f);
+        if (k >= 0) byk[k].push_back(f);
+    }
+    reg.clear();
+    for (int k = 0; k < 3; k++)
+        for (const auto& p : h.peers[k]) {
+            Region* r = nullptr;
+            for (auto& x : reg)
+                if (x.peer == p.peer) r = &x;
+            if (!r) {
+                reg.push_back({p.peer, 0, 0, 0, 0});
+                r = &reg.back();
+            }
+            r->scols += (long)p.nsend * (long)byk[k].size();
+            r->rcols += (long)p.nrecv * (long)byk[k].size();
+        }
+    long so = 0, ro = 0;
+    for (auto& r : reg) {
+        r.soff = so;
+        r.roff = ro;
+        so += r.scols;
+        ro += r.rcols;
+    }
+}
+
+static hipError_t run_copy(const DevState& S, hipStream_t st, const Halo& h, const std::vector<Region>& reg,
+                           const std::vector<int> (&byk)[3], bool pack) {
+    SegList sl{};
+    sl.LP = S.LP;
+    sl.nseg = 0;
+    long col = 0;
+    for (const auto& r : reg) {
+        long c0 = pack ? r.soff : r.roff;
+        col = 0;
+        sl.nseg = 0;
+        for (int k = 0; k < 3; k++) {
+            const HaloPeer* p = nullptr;
+            for (const auto& x : h.peers[k])
+                if (x.peer == r.peer) p = &x;
+            if (!p) continue;
+            const int n = pack ? p->nsend : p->nrecv;
+            if (n == 0) continue;
+            for (int f : byk[k]) {
+                if (sl.nseg == kMaxSeg) {
+                const_cast<Halo&>(h).err = "too many halo segments";
+                return hipErrorInvalidValue;
+            }
+                sl.f[sl.nseg] = (double*)S.f[f];
+                sl.ids[sl.nseg] = pack ? p->d_send : p->d_recv;
+                sl.start[sl.nseg] = col;
+                col += n;
+                sl.nseg++;
+            }
+        }
+        if (sl.nseg == 0) continue;
+        sl.start[sl.nseg] = col;
+        const long tot = col * (long)S.LP;
+        double* buf = (pack ? h.sendbuf : h.recvbuf) + c0 * S.LP;
+        const unsigned grid = (unsigned)((tot + 255) / 256);
+        if (pack) k_halo_copy<true><<<grid, 256, 0, st>>>(sl, buf);
+        else k_halo_copy<false><<<grid, 256, 0, st>>>(sl, buf);
+    }
+    return hipGetLastError();
+}
+
+hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<int>& fields) {
+    std::vector<Region> reg;
+    std::vector<int> byk[3];
+    plan_regions(*this, fields, reg, byk);
+    long stot = 0, rtot = 0;
+    for (auto& r : reg) {
+        stot += r.scols;
+        rtot += r.rcols;
+    }
+    const size_t need = (size_t)std::max(stot, rtot) * S.LP;
+    if (need > cap) {  // reserve() sized the buffers for every halo field at once
+        err = "halo buffers too small";
+        return hipErrorInvalidValue;
+    }
+    exchanges++;
+    fields_moved += (int64_t)fields.size();
+    hipError_t e;
+    if (loop) {
+        // reuse of our send buffer: every peer's copies of the previous exchange are done
+        for (int s = 0; s < loop->n; s++)
+            if (s != rank && (e = hipStreamWaitEvent(st, loop->copied[s], 0)) != hipSuccess) return e;
+    }
+    if ((e = run_copy(S, st, *this, reg, byk, true)) != hipSuccess) return e;
+    if (rccl) {
+        std::string dummy;
+        RcclApi* a = rccl_api(dummy);
+        int r = a->GroupStart();
+        for (auto& x : reg) {
+            if (r == 0 && x.scols) r = a->Send(sendbuf + x.soff * S.LP, (size_t)x.scols * S.LP, kNcclFloat64, x.peer, rccl->comm, st);
+            if (r == 0 && x.rcols) r = a->Recv(recvbuf + x.roff * S.LP, (size_t)x.rcols * S.LP, kNcclFloat64, x.peer, rccl->comm, st);
+        }
+        int r2 = a->GroupEnd();
+        if (r != 0 || r2 != 0) {
+            err = std::string("RCCL halo exchange: ") + (a->GetErrorString ? a->GetErrorString(r ? r : r2) : "error");
+            return hipErrorUnknown;
+        }
+    } else if (loop) {
+        if ((e = hipEventRecord(loop->packed[rank], st)) != hipSuccess) return e;
+        if (!loop->barrier(120.0)) {
+            err = "loopback barrier timed out";
+            return hipErrorUnknown;
+        }
+        for (auto& x : reg) {
+            if (!x.rcols) continue;
+            Halo* ph = loop->members[x.peer];
+            // the peer packed its region for us with the same layout rule
+            std::vector<Region> preg;
+            std::vector<int> pbyk[3];
+            plan_regions(*ph, fields, preg, pbyk);
+            const Region* pr = nullptr;
+            for (auto& y : preg)
+                if (y.peer == rank) pr = &y;
+            if (!pr || pr->scols != x.rcols) {
+                err = "loopback halo plan mismatch";
+                return hipErrorInvalidValue;
+            }
+            if ((e = hipStreamWaitEvent(st, loop->packed[x.peer], 0)) != hipSuccess) return e;
+            if ((e = hipMemcpyAsync(recvbuf + x.roff * S.LP, ph->sendbuf + pr->soff * S.LP,
+                                    (size_t)x.rcols * S.LP * sizeof(double), hipMemcpyDeviceToDevice, st)) != hipSuccess)
+                return e;
+        }
+        if ((e = hipEventRecord(loop->copied[rank], st)) != hipSuccess) return e;
+        if (!loop->barrier(120.0)) {
+            err = "loopback barrier timed out";
+            return hipErrorUnknown;
+        }
+    }
+    return run_copy(S, st, *this, reg, byk, false);
+}
+
+}  // namespace mpas

@@ -1,0 +1,172 @@
+"""Horizontal domain decomposition of the RK3 hot path.
+
+The reference splits the mesh with Legion dependent partitioning over the METIS part
+file (mesh_loading.rg:399-483: owned cells by `graph.info.part`, ghost rings through
+the connectivity).  Here each rank owns
+
+* the cells of its part (a part file, mesh.read_graph_info_part, or contiguous blocks
+  of the renumbered cell order),
+* the edges whose cellsOnEdge(0) it owns, the vertices whose edgesOnVertex(0) it owns
+  (ids resolved with the Q1 policy; an id that resolves to the zero slot falls back to
+  contiguous blocks of that entity's order),
+
+and holds as ghosts every entity its owned entities reach through an index array of
+the path.  The closure is taken over exactly the index arrays the kernels follow
+(ID_ARRAYS, plus cellsOnEdge(edgesOnCell), which k_prepare composes for the cell
+kernels), so one hop from an owned entity never leaves the local set.  Every kernel
+computes owned entities only; a field a kernel gathers is made fresh on the ghosts by
+the device-side halo exchange right before it (mpas_dev.h HaloSet; lazily, only after
+some kernel wrote it).  This keeps the ref-mode ids (raw 1-based offsets, which
+scramble neighbourhoods) exact: no geometric ring assumption anywhere.
+
+Local numbering: owned entities first (global order), then ghosts (global order), then
+the zero slot at index n_local.  Index arrays are mapped to local ids; ids that
+resolve to the global zero slot, or to an entity outside the local set (only ghost
+entities' own connectivity can), map to the local zero slot.
+"""
+import numpy as np
+
+from .registry import FIELDS, BY_NAME
+from .state import HostState
+
+KINDS = ("cell", "edge", "vertex")
+# integer fields holding entity ids -> the entity kind they refer to
+# (mirrors id_target() in csrc/mpas_ctx.cpp: these are clamped to [0, n] on upload)
+ID_ARRAYS = {"edgesOnCell": "edge", "edgesOnEdge": "edge", "edgesOnEdge_ECP": "edge", "edgesOnVertex": "edge",
+             "cellsOnEdge": "cell", "advCellsForEdge": "cell", "verticesOnEdge": "vertex", "verticesOnCell": "vertex"}
+
+
+def _resolve(ids, n):
+    """Q1 policy: any id outside [0, n] is the zero slot n"""
+    ids = np.asarray(ids, dtype=np.int64)
+    return np.where((ids < 0) | (ids > n), n, ids)
+
+
+def _blocks(n, nparts):
+    return (np.arange(n, dtype=np.int64) * nparts // max(n, 1)).astype(np.int32)
+
+
+class Decomposition:
+    """Partition of a global HostState into `nparts` local subdomains."""
+
+    def __init__(self, st, nparts, cell_part=None):
+        self.st, self.nparts = st, int(nparts)
+        self.n = {"cell": st.nCells, "edge": st.nEdges, "vertex": st.nVertices}
+        nC, nE, nV = st.nCells, st.nEdges, st.nVertices
+        cpart = _blocks(nC, nparts) if cell_part is None else np.asarray(cell_part, dtype=np.int32)
+        assert cpart.shape == (nC,) and cpart.min() >= 0 and cpart.max() < nparts
+        c0 = _resolve(st["cellsOnEdge"][:nE, 0], nC)
+        epart = np.where(c0 < nC, cpart[np.minimum(c0, nC - 1)], _blocks(nE, nparts)).astype(np.int32)
+        e0 = _resolve(st["edgesOnVertex"][:nV, 0], nE)
+        vpart = np.where(e0 < nE, epart[np.minimum(e0, nE - 1)], _blocks(nV, nparts)).astype(np.int32)
+        self.part = {"cell": cpart, "edge": epart, "vertex": vpart}
+        # resolved global index arrays, (n, W)
+        self.ids = {f: _resolve(st[f][:self.n[BY_NAME[f].entity]], self.n[t]) for f, t in ID_ARRAYS.items()}
+        coe = np.vstack([self.ids["cellsOnEdge"], np.full((1, 2), nC)])
+        eoc = self.ids["edgesOnCell"]
+        self.cell_cells = np.concatenate([coe[eoc, 0], coe[eoc, 1]], axis=1)  # k_prepare's composition
+        self.owned, self.local, self.g2l = [], [], []
+        for r in range(self.nparts):
+            own = {k: np.flatnonzero(self.part[k] == r) for k in KINDS}
+            need = {k: [own[k]] for k in KINDS}
+            for f, t in ID_ARRAYS.items():
+                src = BY_NAME[f].entity
+                need[t].append(self.ids[f][own[src]].ravel())
+            need["cell"].append(self.cell_cells[own["cell"]].ravel())
+            loc, g2l = {}, {}
+            for k in KINDS:
+                allk = np.unique(np.concatenate(need[k]))
+                allk = allk[allk < self.n[k]]  # the zero slot is not an entity
+                ghosts = np.setdiff1d(allk, own[k], assume_unique=True)
+                loc[k] = np.concatenate([own[k], ghosts]).astype(np.int64)
+                m = np.full(self.n[k] + 1, len(loc[k]), dtype=np.int64)  # default: local zero slot
+                m[loc[k]] = np.arange(len(loc[k]))
+                g2l[k] = m
+            self.owned.append(own)
+            self.local.append(loc)
+            self.g2l.append(g2l)
+
+    # ------------------------------------------------------------------ per rank
+    def n_owned(self, r):
+        return tuple(len(self.owned[r][k]) for k in KINDS)
+
+    def n_local(self, r):
+        return tuple(len(self.local[r][k]) for k in KINDS)
+
+    def local_state(self, r, st=None):
+        """the rank-r HostState: every field restricted to the local entities (owned,
+        then ghosts), index arrays mapped to local ids, zero slots zero"""
+        st = self.st if st is None else st
+        nC, nE, nV = self.n_local(r)
+        out = HostState(nC, nE, nV, st.L)
+        for f in FIELDS:
+            a = st.arrays[f.name]
+            if f.entity is None:
+                out.arrays[f.name][...] = a
+                continue
+            gid = self.local[r][f.entity]
+            b = a[gid]
+            if f.name in ID_ARRAYS:
+                t = ID_ARRAYS[f.name]
+                b = self.g2l[r][t][_resolve(b, self.n[t])].astype(b.dtype)
+            out.arrays[f.name][:len(gid)] = b
+        return out
+
+    def plan(self, r):
+        """halo plan of rank r: {kind: [(peer, send_local_ids, recv_local_ids), ...]}.
+        recv ids are rank r's ghosts owned by `peer`; send ids are rank r's owned
+        entities that are ghosts of `peer`; both in global order, so the k-th sent
+        column is the k-th received one on the other side."""
+        out = {}
+        for k in KINDS:
+            own_r = self.owned[r][k]
+            nown = len(own_r)
+            ghosts_r = self.local[r][k][nown:]
+            lst = []
+            for s in range(self.nparts):
+                if s == r:
+                    continue
+                recv_g = ghosts_r[self.part[k][ghosts_r] == s]
+                ghosts_s = self.local[s][k][len(self.owned[s][k]):]
+                send_g = ghosts_s[self.part[k][ghosts_s] == r]
+                if len(recv_g) == 0 and len(send_g) == 0:
+                    continue
+                lst.append((s, self.g2l[r][k][send_g].astype(np.int32), self.g2l[r][k][recv_g].astype(np.int32)))
+            out[k] = lst
+        return out
+
+    def global_ids(self, r):
+        """global id of every local entity of rank r (fill_synthetic hashes these)"""
+        return {k: self.local[r][k].astype(np.int32) for k in KINDS}
+
+    def assemble(self, locals_, fields=None):
+        """global HostState from the owned parts of the local states"""
+        out = self.st.copy()
+        for f in FIELDS:
+            if fields is not None and f.name not in fields:
+                continue
+            if f.entity is None:
+                out.arrays[f.name][...] = locals_[0].arrays[f.name]
+                continue
+            for r, ls in enumerate(locals_):
+                own = self.owned[r][f.entity]
+                b = ls.arrays[f.name][:len(own)]
+                if f.name in ID_ARRAYS:
+                    continue  # connectivity is not state
+                out.arrays[f.name][own] = b
+        return out
+
+    def check_closure(self):
+        """every id reached from an owned entity (and k_prepare's composed cell ids) is
+        local to that rank; returns the number of violations (0 expected)"""
+        bad = 0
+        for r in range(self.nparts):
+            own = self.owned[r]
+            for f, t in ID_ARRAYS.items():
+                tg = self.ids[f][own[BY_NAME[f].entity]].ravel()
+                tg = tg[tg < self.n[t]]
+                bad += int(np.sum(self.g2l[r][t][tg] >= len(self.local[r][t])))
+            tg = self.cell_cells[own["cell"]].ravel()
+            tg = tg[tg < self.n["cell"]]
+            bad += int(np.sum(self.g2l[r]["cell"][tg] >= len(self.local[r]["cell"])))
+        return bad

@@ -24,7 +24,10 @@ EXPORTS = [
     "mpas_atm_divergence_damping_3d", "mpas_atm_compute_solve_diagnostics",
     "mpas_atm_rk_dynamics_substep_finish", "mpas_atm_srk3", "mpas_atm_timestep",
     "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
+    "mpas_halo_owned", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
+    "mpas_halo_loopback", "mpas_halo_stats",
 ]
+KIND_ID = {"cell": 0, "edge": 1, "vertex": 2}
 
 HORIZ_MIXING = {"2d_smagorinsky": 0, "2d_fixed": 1}
 
@@ -81,6 +84,13 @@ def load():
         "mpas_timing_count": (i32, [vp]),
         "mpas_timing_get": (i32, [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(i64),
                                   ctypes.POINTER(dbl)]),
+        "mpas_halo_owned": (i32, [vp, i32, i32, i32]),
+        "mpas_halo_plan": (i32, [vp, i32, i32, vp, i32, vp, i32]),
+        "mpas_set_global_ids": (i32, [vp, i32, vp, i32]),
+        "mpas_rccl_unique_id": (i32, [vp]),
+        "mpas_halo_rccl": (i32, [vp, i32, i32, vp]),
+        "mpas_halo_loopback": (i32, [ctypes.POINTER(vp), i32]),
+        "mpas_halo_stats": (i32, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -181,3 +191,50 @@ class Context:
                                                  ctypes.byref(ms)), "timing_get")
             out[name.value.decode()] = (calls.value, ms.value)
         return out
+
+
+# ---------------------------------------------------------------------- decomposition
+def setup_subdomain(ctx, dec, r):
+    """give context `ctx` rank r's owned counts, global ids and halo plan of the
+    mpasdyn.decomp.Decomposition `dec` (its local state is uploaded separately)"""
+    L = ctx.lib
+    ctx._check(L.mpas_halo_owned(ctx.h, *dec.n_owned(r)), "mpas_halo_owned")
+    for kind, g in dec.global_ids(r).items():
+        g = np.ascontiguousarray(g, dtype=np.int32)
+        ctx._check(L.mpas_set_global_ids(ctx.h, KIND_ID[kind], g.ctypes.data, len(g)), "mpas_set_global_ids")
+    for kind, lst in dec.plan(r).items():
+        for peer, send, recv in lst:
+            send = np.ascontiguousarray(send, dtype=np.int32)
+            recv = np.ascontiguousarray(recv, dtype=np.int32)
+            ctx._check(L.mpas_halo_plan(ctx.h, KIND_ID[kind], int(peer), send.ctypes.data, len(send),
+                                        recv.ctypes.data, len(recv)), "mpas_halo_plan")
+
+
+def halo_loopback(ctxs):
+    """link contexts of this process (one per rank, same device) by the loopback transport"""
+    L = load()
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.h for c in ctxs])
+    rc = L.mpas_halo_loopback(arr, len(ctxs))
+    if rc != 0:
+        raise MpasError(f"mpas_halo_loopback failed ({rc}): {L.mpas_last_error(ctxs[0].h).decode()}")
+
+
+def rccl_unique_id():
+    L = load()
+    buf = ctypes.create_string_buffer(128)
+    rc = L.mpas_rccl_unique_id(buf)
+    if rc != 0:
+        raise MpasError(f"mpas_rccl_unique_id failed ({rc}): {L.mpas_last_error(None).decode()}")
+    return bytes(buf.raw)
+
+
+def halo_rccl(ctx, nranks, rank, uid):
+    buf = ctypes.create_string_buffer(bytes(uid), 128)
+    ctx._check(ctx.lib.mpas_halo_rccl(ctx.h, nranks, rank, buf), "mpas_halo_rccl")
+
+
+def halo_stats(ctx):
+    a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+    ctx._check(ctx.lib.mpas_halo_stats(ctx.h, ctypes.byref(a), ctypes.byref(b)), "mpas_halo_stats")
+    return a.value, b.value
+

@@ -1,0 +1,130 @@
+"""Decomposed hot path on one GPU: N subdomain contexts in one process, linked by the
+loopback halo transport (mpas_halo_loopback; the same pack/unpack and staleness logic as
+the RCCL transport), each driven by its own host thread.  The owned parts of the N
+local results must equal the single-context result bit for bit -- every kernel computes
+the same expression on the same (fresh) inputs -- over whole RK3 steps, per task, on
+literal-ref ids, random states and mpas-mode ids.  SURVEY §8.6 "invariance check"."""
+import threading
+
+import numpy as np
+import pytest
+
+from helpers import compare_states, make_state
+from mpasdyn import decomp, lib
+from mpasdyn import tasks as T
+
+pytestmark = pytest.mark.gpu
+
+_ST = {}
+
+
+def state(mesh, L, variant):
+    key = (L, variant)
+    if key not in _ST:
+        if variant == "mpas0":
+            from mpasdyn import mesh as M
+            _ST[key] = make_state(M.zero_based(mesh), L, "random")
+        else:
+            _ST[key] = make_state(mesh, L, variant)
+    return _ST[key]
+
+
+def run_single(st, fn, exact):
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.set_option("exact", exact)
+        ctx.upload(st)
+        fn(ctx)
+        ctx.sync()
+        ctx.download(got)
+    return got
+
+
+def run_decomposed(st, nparts, fn, exact, cell_part=None):
+    d = decomp.Decomposition(st, nparts, cell_part=cell_part)
+    locs = [d.local_state(r) for r in range(nparts)]
+    ctxs = [lib.Context(*d.n_local(r), st.L) for r in range(nparts)]
+    try:
+        for r, c in enumerate(ctxs):
+            c.set_option("exact", exact)
+            lib.setup_subdomain(c, d, r)
+            c.upload(locs[r])
+        lib.halo_loopback(ctxs)
+        errs = [None] * nparts
+
+        def drive(r):
+            try:
+                fn(ctxs[r])
+                ctxs[r].sync()
+            except Exception as e:  # noqa: BLE001 -- reported below
+                errs[r] = e
+        th = [threading.Thread(target=drive, args=(r,)) for r in range(nparts)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=600)
+        assert all(e is None for e in errs), errs
+        for r, c in enumerate(ctxs):
+            c.download(locs[r])
+        stats = [lib.halo_stats(c) for c in ctxs]
+    finally:
+        for c in ctxs:
+            c.close()
+    return d.assemble(locs), stats
+
+
+@pytest.mark.parametrize("variant", ["ref", "random", "mpas0"])
+@pytest.mark.parametrize("nparts", [2, 3])
+@pytest.mark.parametrize("L", [5, 56])
+def test_srk3_decomposed_equals_single(x1_2562, variant, nparts, L):
+    st = state(x1_2562, L, variant)
+    for exact in (1, 0):
+        ref = run_single(st, lambda c: T.atm_srk3(c, 720.0, 1), exact)
+        got, stats = run_decomposed(st, nparts, lambda c: T.atm_srk3(c, 720.0, 1), exact)
+        bad = compare_states(got, ref, rtol=0.0)
+        assert not bad, f"exact={exact}: {bad[:6]}"
+        assert all(s[0] > 0 for s in stats)  # the halo was exercised
+
+
+def test_srk3_part_file_16(x1_2562):
+    """the reference's own x1.2562.graph.info.part.16 split, 16 subdomains, schedule 0"""
+    st = state(x1_2562, 5, "random")
+    ref = run_single(st, lambda c: T.atm_srk3(c, 720.0, 0), 1)
+    got, _ = run_decomposed(st, 16, lambda c: T.atm_srk3(c, 720.0, 0), 1, cell_part=x1_2562.part)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("task", ["dyn_tend_rk0", "dyn_tend_rk1", "solve_holl", "acoustic", "div_damp", "smlstep"])
+def test_task_decomposed_equals_single(x1_2562, task):
+    fn = {"dyn_tend_rk0": lambda c: T.atm_compute_dyn_tend_work(c, 0, 720.0),
+          "dyn_tend_rk1": lambda c: T.atm_compute_dyn_tend_work(c, 1, 720.0),
+          "solve_holl": lambda c: T.atm_compute_solve_diagnostics(c, True, -1),
+          "acoustic": lambda c: T.atm_advance_acoustic_step_work(c, 360.0, 1),
+          "div_damp": lambda c: T.atm_divergence_damping_3d(c, 240.0),
+          "smlstep": lambda c: T.atm_set_smlstep_pert_variables_work(c)}[task]
+    st = state(x1_2562, 56, "random")
+    ref = run_single(st, fn, 1)
+    got, _ = run_decomposed(st, 3, fn, 1)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
+def test_fill_synthetic_global_ids(x1_2562):
+    """decomposed synthetic fill = the global fill restricted to the local entities"""
+    st = state(x1_2562, 5, "ref")
+    with lib.Context(*st.dims()) as ctx:
+        ctx.fill_synthetic(7)
+        g = st.copy()
+        ctx.download(g)
+    d = decomp.Decomposition(st, 2)
+    for r in range(2):
+        ls = d.local_state(r)
+        with lib.Context(*d.n_local(r), st.L) as ctx:
+            lib.setup_subdomain(ctx, d, r)
+            ctx.fill_synthetic(7)
+            ctx.download(ls)
+        for f in ("theta_m", "u", "pv_vertex", "zb_cell"):
+            ent = {"theta_m": "cell", "u": "edge", "pv_vertex": "vertex", "zb_cell": "cell"}[f]
+            gid = d.local[r][ent]
+            assert np.array_equal(ls[f][:len(gid)], g[f][gid]), f
