@@ -12,9 +12,14 @@ precompute uploaded from the host, and the 3-D state filled on the device by the
 seeded generator (data: synthetic, seed 20211015).
 
     python bench.py [--gpus N --steps K --warmup W]
-N > 1 runs under torch.distributed.run, one process per GPU; each rank advances its own
-full-mesh replica ("replicas", weak scaling: the halo-exchanged decomposition is not
-in this round).  Prints ONE JSON line on rank 0.
+N > 1 runs under torch.distributed.run, one process per GPU: the same x1.163842 mesh is
+split into N subdomains (mpasdyn/decomp.py: contiguous blocks of the Morton-ordered
+cells, edges/vertices with their first cell/edge, ghosts = everything an owned entity
+reaches through an index array), and the ranks exchange halos with RCCL send/recv
+before every kernel that gathers a field another rank wrote (csrc/mpas_halo.h).  Total
+work is fixed ("scaling": "strong"); `value` = global cell columns / step time.
+`--replicas` instead runs a full-mesh replica per rank (weak scaling, no collective).
+Prints ONE JSON line on rank 0.
 """
 import argparse
 import ctypes
@@ -60,10 +65,11 @@ class Hip:
 
 
 def build_inputs(ncells, L):
+    """the mesh and its one-time precompute (host); the 3-D state is filled on the device"""
     from mpasdyn import build_state as bs
     from mpasdyn import mesh
     m = mesh.icosahedral(LEVEL_OF[ncells])
-    st = bs.build_state(m, L, "physical")
+    st = bs.build_state(m, L, "physical", mesh_only=True)
     return m, st
 
 
@@ -124,6 +130,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="extra mpas_set_option (A/B runs, e.g. xcd=32)")
+    ap.add_argument("--replicas", action="store_true", help="N > 1: full-mesh replicas instead of a decomposition")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -141,8 +148,29 @@ def main():
     ncells, L = args.ncells, args.levels
     dt = dt_for(ncells)
     m, st = build_inputs(ncells, L)
-    dims = (m.nCells, m.nEdges, m.nVertices, L)
-    ctx = lib.Context(*dims, device=local_rank)
+    decomposed = world > 1 and not args.replicas
+    halo_info = None
+    if decomposed:
+        from mpasdyn import decomp
+        dec = decomp.Decomposition(st, world)
+        lst = dec.local_state(rank)
+        dims = (*dec.n_local(rank), L)
+        ctx = lib.Context(*dims, device=local_rank)
+        lib.setup_subdomain(ctx, dec, rank)
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(lib.rccl_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        lib.halo_rccl(ctx, world, rank, uid.cpu().numpy().tobytes())
+        own = dec.n_owned(rank)
+        halo_info = {"partition": f"{world} contiguous Morton blocks of cells", "owned": list(own),
+                     "ghost_frac": [round(1 - o / n, 4) for o, n in zip(own, dims[:3])]}
+        st = lst
+        work_dims = (*own, L)  # what this rank computes
+    else:
+        dims = (m.nCells, m.nEdges, m.nVertices, L)
+        ctx = lib.Context(*dims, device=local_rank)
+        work_dims = dims
     ctx.set_option("exact", args.exact)
     for kv in args.option:
         k, v = kv.split("=")
@@ -192,7 +220,7 @@ def main():
     tasks_out = {}
     for name, (calls, ms) in rep.items():
         task, kw = kw_of.get(name, (name, {}))
-        b = roofline.b_alg(task, dims, **kw)
+        b = roofline.b_alg(task, work_dims, **kw)
         avg = ms / calls
         tasks_out[name] = {"launches_per_step": calls // n_prof, "avg_ms": round(avg, 4),
                            "b_alg_GB": round(b / 1e9, 4), "GBs": round(b / (avg * 1e-3) / 1e9, 1)}
@@ -203,19 +231,26 @@ def main():
     roof = {"bound": "hbm", "kernel": dom, "achieved": dt_["GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(dt_["GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic,
             "b_alg_per_launch_GB": dt_["b_alg_GB"], "avg_launch_ms": dt_["avg_ms"]}
-    b_step = roofline.b_alg_step(dims)
+    b_step = roofline.b_alg_step(work_dims)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
-    value = world * ncells / (ms_step * 1e-3) / 1e6
+    value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
+    if decomposed:
+        ex, fl = lib.halo_stats(ctx)
+        halo_info["exchanges_per_step"] = round(ex / (args.warmup + args.steps + n_prof), 2)
+        halo_info["fields_per_step"] = round(fl / (args.warmup + args.steps + n_prof), 2)
     out = {"metric": METRIC, "value": round(value, 3), "unit": "Mcell-columns/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+           "scaling": "strong" if decomposed else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": f"x1.{ncells} x {L} levels, atm_srk3 (3 dyn_tend rk 0/1/2, 7 acoustic substeps)",
                       "nCells": ncells, "nEdges": m.nEdges, "nVertices": m.nVertices, "nVertLevels": L,
-                      "dt": dt, "parallelism": f"replicas{world}" if world > 1 else "single-gpu",
+                      "dt": dt, "parallelism": (f"decomposed{world}" if decomposed else
+                                                 f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}
+    if halo_info:
+        out["halo"] = halo_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count())))
         out["cpu_baseline"] = cpu_baseline(ncells, L, dt, threads)

@@ -242,11 +242,15 @@ def geometry(m, st):
     st["lat"][:nC, 0] = m.latCell
 
 
-def build_state(m, nVertLevels, variant="ref", seed=20211015, oracle_fill=None, vertical=True):
+MESH_FIELDS = tuple(f.name for f in FIELDS if f.dist == "M" or f.kind == "ZV")
+
+
+def build_state(m, nVertLevels, variant="ref", seed=20211015, oracle_fill=None, vertical=True, mesh_only=False):
     """Return a HostState for mesh m.  ``oracle_fill(state, seed, include_mesh)`` fills the
     synthetic fields on the host (tests pass the oracle's generator); None leaves them 0
-    (the benchmark fills them on the device)."""
-    st = HostState(m.nCells, m.nEdges, m.nVertices, nVertLevels)
+    (the benchmark fills them on the device).  mesh_only: allocate only the mesh and
+    vertical-grid fields (MESH_FIELDS), for device-filled benchmark states."""
+    st = HostState(m.nCells, m.nEdges, m.nVertices, nVertLevels, names=MESH_FIELDS if mesh_only else None)
     nC, nE, nV, L = m.nCells, m.nEdges, m.nVertices, nVertLevels
     R = SPHERE_RADIUS
     connectivity(m, st)

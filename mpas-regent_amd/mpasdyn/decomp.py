@@ -15,7 +15,7 @@ the path.  The closure is taken over exactly the index arrays the kernels follow
 (ID_ARRAYS, plus cellsOnEdge(edgesOnCell), which k_prepare composes for the cell
 kernels), so one hop from an owned entity never leaves the local set.  Every kernel
 computes owned entities only; a field a kernel gathers is made fresh on the ghosts by
-the device-side halo exchange right before it (mpas_dev.h HaloSet; lazily, only after
+the device-side halo exchange right before it (csrc/mpas_halo.h; lazily, only after
 some kernel wrote it).  This keeps the ref-mode ids (raw 1-based offsets, which
 scramble neighbourhoods) exact: no geometric ring assumption anywhere.
 
@@ -98,8 +98,11 @@ class Decomposition:
         then ghosts), index arrays mapped to local ids, zero slots zero"""
         st = self.st if st is None else st
         nC, nE, nV = self.n_local(r)
-        out = HostState(nC, nE, nV, st.L)
+        names = None if len(st.arrays) == len(FIELDS) else tuple(st.arrays)
+        out = HostState(nC, nE, nV, st.L, names=names)
         for f in FIELDS:
+            if f.name not in st.arrays:
+                continue
             a = st.arrays[f.name]
             if f.entity is None:
                 out.arrays[f.name][...] = a

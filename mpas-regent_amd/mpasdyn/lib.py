@@ -138,7 +138,7 @@ class Context:
     # ---------------------------------------------------------------- residency
     def upload(self, state, names=None):
         for f in FIELDS:
-            if names is not None and f.name not in names:
+            if (names is not None and f.name not in names) or f.name not in state.arrays:
                 continue
             a = state.arrays[f.name]
             se, sl, sc = state.byte_strides(f.name)
@@ -147,7 +147,7 @@ class Context:
 
     def download(self, state, names=None):
         for f in FIELDS:
-            if names is not None and f.name not in names:
+            if (names is not None and f.name not in names) or f.name not in state.arrays:
                 continue
             a = state.arrays[f.name]
             se, sl, sc = state.byte_strides(f.name)

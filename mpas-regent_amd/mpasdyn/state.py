@@ -19,12 +19,15 @@ from .registry import FIELDS, BY_NAME
 
 
 class HostState:
-    def __init__(self, nCells, nEdges, nVertices, nVertLevels):
+    def __init__(self, nCells, nEdges, nVertices, nVertLevels, names=None):
+        """names: allocate only these fields (e.g. the mesh fields of a large mesh whose
+        3-D state is generated on the device); None = every field"""
         self.nCells, self.nEdges, self.nVertices = int(nCells), int(nEdges), int(nVertices)
         self.L = int(nVertLevels)
         self.arrays = {}
         for f in FIELDS:
-            self.arrays[f.name] = np.zeros(self.shape_of(f), dtype=f.dtype)
+            if names is None or f.name in names:
+                self.arrays[f.name] = np.zeros(self.shape_of(f), dtype=f.dtype)
 
     # ------------------------------------------------------------------ layout
     def n_of(self, f):

@@ -128,3 +128,24 @@ def test_fill_synthetic_global_ids(x1_2562):
             ent = {"theta_m": "cell", "u": "edge", "pv_vertex": "vertex", "zb_cell": "cell"}[f]
             gid = d.local[r][ent]
             assert np.array_equal(ls[f][:len(gid)], g[f][gid]), f
+
+
+def test_rccl_transport_single_rank(x1_2562):
+    """the RCCL transport end to end on the one GPU of the box: librccl resolved, a
+    1-rank communicator, every exchange a (peer-less) grouped send/recv; the result
+    equals the undecomposed run.  Multi-rank RCCL runs on the 8-GPU node (bench.py)."""
+    st = state(x1_2562, 5, "random")
+    ref = run_single(st, lambda c: T.atm_srk3(c, 720.0, 1), 1)
+    d = decomp.Decomposition(st, 1)
+    got = d.local_state(0)
+    with lib.Context(*d.n_local(0), st.L) as ctx:
+        ctx.set_option("exact", 1)
+        lib.setup_subdomain(ctx, d, 0)
+        ctx.upload(got)
+        lib.halo_rccl(ctx, 1, 0, lib.rccl_unique_id())
+        T.atm_srk3(ctx, 720.0, 1)
+        ctx.sync()
+        ctx.download(got)
+        assert lib.halo_stats(ctx)[0] > 0
+    bad = compare_states(d.assemble([got]), ref, rtol=0.0)
+    assert not bad, bad[:6]
