@@ -29,24 +29,66 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     double* rpp_f = fw(S, F_rho_pp);
     double* rwp_f = fw(S, F_rw_p);
     double* ww_f = fw(S, F_wwAvg);
+    const bool kl = k < L;
+    // ---- every load of the column and of its edge gathers first, ahead of the first
+    // store (which could alias them for the compiler)
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const double spec = fd(S, F_specZoneMaskCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
+    const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
+    const double* cdv = fd(S, X_ce_dv) + (size_t)c * 10;
+    const double invA = fd(S, F_invAreaCell)[c];
+    const double *ru_p = fd(S, F_ru_p), *tm_f = fd(S, F_theta_m);
+    const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
+    int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
+    double sgn_[NF], cdv_[NF], rup_[NF], t1_[NF], t2_[NF];
+    row_ld(eoc, e_);
+    if (SELF) {
+        row_ld(coth, o_);
+        row_ld(cs1, s1_);
+    } else {
+        row_ld(cc1, c1_);
+        row_ld(cc2, c2_);
+    }
+    row_ld(sgn, sgn_);
+    row_ld(cdv, cdv_);
     double rtp = col_rd<LP>(rtp_f, c, k, L), rpp = col_rd<LP>(rpp_f, c, k, L);
     double rwp = col_rd<LP>(rwp_f, c, k, L), ww = col_rd<LP>(ww_f, c, k, L);
+    const double tm = col_rd<LP>(fd(S, F_theta_m), c, k, L);
+    const double tend_rho = col_rd<LP>(fd(S, F_tend_rho), c, k, L);
+    const double w = col_rd<LP>(fd(S, F_w), c, k, L);
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        rup_[i] = ldz(kl, colk(ru_p, e_[i]));
+        cell_pair<LP, SELF>(tm_f, c1_[i], c2_[i], o_[i], s1_[i], tm, k, t1_[i], t2_[i]);
+        t1_[i] = ldz(kl, t1_[i]);
+        t2_[i] = ldz(kl, t2_[i]);
+    }
+    const double coftz = col_rd<LP>(fd(S, F_coftz), c, k, L);
+    const double zz = col_rd<LP>(fd(S, F_zz), c, k, L);
+    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L);
+    const double cofwt = col_rd<LP>(fd(S, F_cofwt), c, k, L);
+    const double cofwz = col_rd<LP>(fd(S, F_cofwz), c, k, L), cofwr = col_rd<LP>(fd(S, F_cofwr), c, k, L);
+    const double a_tri = col_rd<LP>(fd(S, F_a_tri), c, k, L), alpha = col_rd<LP>(fd(S, F_alpha_tri), c, k, L);
+    const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L), rw = col_rd<LP>(fd(S, F_rw), c, k, L);
+    const double dss = col_rd<LP>(fd(S, F_dss), c, k, L);
+    const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+
     // :1615-1636
-    if (k < L) colk(fw(S, F_rtheta_pp_old), c) = (small_step == 0) ? 0 : rtp;
+    if (kl) colk(fw(S, F_rtheta_pp_old), c) = (small_step == 0) ? 0 : rtp;
     if (small_step == 0) {
         ww = 0;
         rwp = 0;
-        if (k < L) {
+        if (kl) {
             rpp = 0;
             rtp = 0;
         }
     }
-    const double tm = col_rd<LP>(fd(S, F_theta_m), c, k, L);
-    const double tend_rho = col_rd<LP>(fd(S, F_tend_rho), c, k, L);
-    const double w = col_rd<LP>(fd(S, F_w), c, k, L);
 
-    if (fd(S, F_specZoneMaskCell)[c] != 0.0) {  // :1698-1703 (column-uniform branch)
-        if (k < L) {
+    if (spec != 0.0) {  // :1698-1703 (column-uniform branch)
+        if (kl) {
             rpp = rpp + dts * tend_rho;
             rtp = rtp + dts * tm;
             rwp = rwp + dts * w;
@@ -61,52 +103,26 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         return;
     }
 
-    // ---- horizontal flux (:1644-1652): issue the NF edge gathers, then accumulate
-    const int ne = fi(S, F_nEdgesOnCell)[c];
-    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
-    const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
-    const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
-    const double* cdv = fd(S, X_ce_dv) + (size_t)c * 10;
-    const double invA = fd(S, F_invAreaCell)[c];
-    const double *ru_p = fd(S, F_ru_p), *tm_f = fd(S, F_theta_m);
-    const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
+    // ---- horizontal flux (:1644-1652), accumulated in the reference's order
     double rs = 0, ts = 0;
-    if (k < L) {
-        double rup_[NF], t1_[NF], t2_[NF];
 #pragma unroll
-        for (int i = 0; i < NF; i++) {
-            rup_[i] = colk(ru_p, eoc[i]);
-            cell_pair<LP, SELF>(tm_f, cc1[i], cc2[i], coth[i], cs1[i], tm, k, t1_[i], t2_[i]);
-        }
-#pragma unroll
-        for (int i = 0; i < NF; i++)
-            if (i < ne) {
-                double flux = sgn[i] * dts * cdv[i] * rup_[i] * invA;
-                rs -= flux;
-                ts -= flux * 0.5 * (t2_[i] + t1_[i]);
-            }
-        for (int i = NF; i < ne; i++) {
-            double flux = sgn[i] * dts * cdv[i] * colk(ru_p, eoc[i]) * invA;
-            rs -= flux;
-            ts -= flux * 0.5 * (colk(tm_f, cc2[i]) + colk(tm_f, cc1[i]));
-        }
+    for (int i = 0; i < NF; i++) {
+        double flux = sgn_[i] * dts * cdv_[i] * rup_[i] * invA;
+        rs = sub_if(i < ne && kl, rs, flux);
+        ts = sub_if(i < ne && kl, ts, flux * 0.5 * (t2_[i] + t1_[i]));
+    }
+    for (int i = NF; i < ne; i++) {
+        double flux = sgn[i] * dts * cdv[i] * ldz(kl, colk(ru_p, eoc[i])) * invA;
+        rs = sub_if(kl, rs, flux);
+        ts = sub_if(kl, ts, flux * 0.5 * (ldz(kl, colk(tm_f, cc2[i])) + ldz(kl, colk(tm_f, cc1[i]))));
     }
     // ---- rs, ts (:1657-1658) from the OLD rw_p
-    const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
-    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
-    const double coftz = col_rd<LP>(fd(S, F_coftz), c, k, L);
     const double rwp_p = lvl_up<LP>(rwp, k), coftz_p = lvl_up<LP>(coftz, k);
     rs = rpp + dts * tend_rho + rs - cofrz * resm * (rwp_p - rwp);
     ts = rtp + dts * tm + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
 
     // per-level coefficients of the recurrence
-    const double zz = col_rd<LP>(fd(S, F_zz), c, k, L), zz_m = lvl_dn<LP>(zz, k);
-    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L), rz_m = lvl_dn<LP>(rz, k);
-    const double cofwt = col_rd<LP>(fd(S, F_cofwt), c, k, L), cofwt_m = lvl_dn<LP>(cofwt, k);
-    const double cofwz = col_rd<LP>(fd(S, F_cofwz), c, k, L), cofwr = col_rd<LP>(fd(S, F_cofwr), c, k, L);
-    const double a_tri = col_rd<LP>(fd(S, F_a_tri), c, k, L), alpha = col_rd<LP>(fd(S, F_alpha_tri), c, k, L);
-    const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L), rw = col_rd<LP>(fd(S, F_rw), c, k, L);
-    const double dss = col_rd<LP>(fd(S, F_dss), c, k, L);
+    const double zz_m = lvl_dn<LP>(zz, k), rz_m = lvl_dn<LP>(rz, k), cofwt_m = lvl_dn<LP>(cofwt, k);
     const double tsm = 0.0, rsm = 0.0;  // Q19
     const double rwold = rwp;
     double x;  // new rw_p of this level

@@ -62,9 +62,11 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     const bool smag = rk0 && a.horiz_mixing == 0;
 
     int e_[NF];
-    double ru_[NF], u_[NF], v_[NF];
-#pragma unroll
-    for (int i = 0; i < NF; i++) e_[i] = eoc[i];
+    double ru_[NF], u_[NF], v_[NF], eocs_[NF], cdv_[NF], wfl[2];
+    row_ld(fd(S, X_wfl) + (size_t)c * 2, wfl);
+    row_ld(eoc, e_);
+    row_ld(eocs, eocs_);
+    row_ld(cdv, cdv_);
 #pragma unroll
     for (int i = 0; i < NF; i++) ru_[i] = ldz(live, colk(ru, e_[i]));
     if (smag) {
@@ -93,13 +95,14 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         if (a.horiz_mixing == 0) {
             const double* defa = fd(S, F_defc_a) + (size_t)c * 10;
             const double* defb = fd(S, F_defc_b) + (size_t)c * 10;
-            double d_diag = 0.0, d_off_diag = 0.0;
+            double d_diag = 0.0, d_off_diag = 0.0, defa_[NF], defb_[NF];
+            row_ld(defa, defa_);
+            row_ld(defb, defb_);
 #pragma unroll
-            for (int i = 0; i < NF; i++)
-                if (i < ne) {
-                    d_diag += defa[i] * u_[i] - defb[i] * v_[i];
-                    d_off_diag += defb[i] * u_[i] + defa[i] * v_[i];
-                }
+            for (int i = 0; i < NF; i++) {
+                d_diag = add_if(i < ne, d_diag, defa_[i] * u_[i] - defb_[i] * v_[i]);
+                d_off_diag = add_if(i < ne, d_off_diag, defb_[i] * u_[i] + defa_[i] * v_[i]);
+            }
             for (int i = NF; i < ne; i++) {
                 int e = eoc[i];
                 double ue = col_rd<LP>(u, e, k, L), ve = col_rd<LP>(v, e, k, L);
@@ -122,11 +125,10 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     // ---- h_divergence (:924-938)
     double hd = 0.0;
 #pragma unroll
-    for (int i = 0; i < NF; i++)
-        if (i < ne) {
-            double edge_sign = eocs[i] * cdv[i];
-            hd += edge_sign * ru_[i];
-        }
+    for (int i = 0; i < NF; i++) {
+        double edge_sign = eocs_[i] * cdv_[i];
+        hd = add_if(i < ne, hd, edge_sign * ru_[i]);
+    }
     for (int i = NF; i < ne; i++) {
         double edge_sign = eocs[i] * cdv[i];
         hd += edge_sign * col_rd<LP>(ru, eoc[i], k, L);
@@ -143,31 +145,27 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 
     // ---- w: zeroing (:1170), horizontal advection (:1174-1205, Q13), curvature (:1208-1218)
     // After the zeroing every w(cell, k<L) read by flux_arr is exactly 0.0 (the zero
-    // slot is 0 too), so flux_arr = sum_j scalar_weight_j * 0.0 of the cell's LAST edge
-    // (flux_arr and ru_edge_w are overwritten per edge); it is evaluated literally so
-    // that non-finite weights propagate as in the reference.
+    // slot is 0 too), so flux_arr = sum_j scalar_weight_j * 0.0 over the advCells of the
+    // cell's LAST edge (flux_arr and ru_edge_w are overwritten per edge): +0.0, or NaN
+    // where a weight is not finite.  It depends only on the mesh and on
+    // copysign(1, ru_edge_w), so k_prepare evaluates it literally for both signs
+    // (X_wfl); the sum over the edges is evaluated literally here, so that non-finite
+    // values propagate as in the reference.
     double ru_l = 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++)
         if (i == ne - 1) ru_l = ru_[i];
-    const int e_last = ne > 0 ? eoc[ne - 1] : S.nEdges;
-    if (ne > NF) ru_l = col_rd<LP>(ru, e_last, k, L);
+    if (ne > NF) ru_l = col_rd<LP>(ru, eoc[ne - 1], k, L);
     const double ru_lm = lvl_dn<LP>(ru_l, k);
     const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
     if (k >= L) return;
     double w0 = 0.0;
     if (ne > 0 && k > 0) {
         double ru_edge_w = fzm * ru_l + fzp * ru_lm;
-        const int na = fi(S, F_nAdvCellsForEdge)[e_last];
-        const double* ac = fd(S, F_adv_coefs) + (size_t)e_last * 15;
-        const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e_last * 15;
-        double flux_arr = 0.0;
-        const double w_zeroed = 0.0;
-        for (int j = 0; j < na; j++) {
-            double scalar_weight = ac[j] + copysign(1.0, ru_edge_w) * ac3[j];
-            flux_arr += scalar_weight * w_zeroed;
-        }
-        for (int i = 0; i < ne; i++) w0 -= eocs[i] * ru_edge_w * flux_arr;
+        const double flux_arr = copysign(1.0, ru_edge_w) > 0.0 ? wfl[0] : wfl[1];
+#pragma unroll
+        for (int i = 0; i < NF; i++) w0 = sub_if(i < ne, w0, eocs_[i] * ru_edge_w * flux_arr);
+        for (int i = NF; i < ne; i++) w0 -= eocs[i] * ru_edge_w * flux_arr;
     }
     double wc = w0;
     if (k > 0) {
@@ -206,9 +204,9 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
     int ee_[QF];
-    double ue_[QF], pve_[QF];
-#pragma unroll
-    for (int j = 0; j < QF; j++) ee_[j] = eoe[j];
+    double ue_[QF], pve_[QF], woe_[QF];
+    row_ld(eoe, ee_);
+    row_ld(woe, woe_);
     const bool kl = k < L;
 #pragma unroll
     for (int j = 0; j < QF; j++) {
@@ -218,10 +216,13 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = fi(S, F_nAdvCellsForEdge)[e];
     const int* ad = fi(S, F_advCellsForEdge) + (size_t)e * 15;
+    const double* ac = fd(S, F_adv_coefs) + (size_t)e * 15;
+    const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e * 15;
     int ad_[AF];
-    double tv_[AF];
-#pragma unroll
-    for (int j = 0; j < AF; j++) ad_[j] = ad[j];
+    double tv_[AF], ac_[AF], ac3_[AF];
+    row_ld(ad, ad_);
+    row_ld(ac, ac_);
+    row_ld(ac3, ac3_);
 #pragma unroll
     for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, colk(tm_f, ad_[j]));
 
@@ -247,16 +248,13 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     if (!kl) return;
 
     {  // flux_arr of this edge
-        const double* ac = fd(S, F_adv_coefs) + (size_t)e * 15;
-        const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e * 15;
         const double sg = copysign(1.0, ru_e);
         double flux_arr = 0.0;
 #pragma unroll
-        for (int j = 0; j < AF; j++)
-            if (j < na) {
-                double scalar_weight = ac[j] + sg * ac3[j];
-                flux_arr += scalar_weight * tv_[j];
-            }
+        for (int j = 0; j < AF; j++) {
+            double scalar_weight = ac_[j] + sg * ac3_[j];
+            flux_arr = add_if(j < na, flux_arr, scalar_weight * tv_[j]);
+        }
         for (int j = AF; j < na; j++) {
             double scalar_weight = ac[j] + sg * ac3[j];
             flux_arr += scalar_weight * colk(tm_f, ad[j]);
@@ -279,11 +277,10 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     } else {
         const double dL = (double)L;  // Q10 value, nVertLevels * term
 #pragma unroll
-        for (int j = 0; j < QF; j++)
-            if (j < neoe) {
-                double workpv = 0.5 * (pv + pve_[j]);
-                q += (woe[j] * ue_[j] * workpv) * dL;
-            }
+        for (int j = 0; j < QF; j++) {
+            double workpv = 0.5 * (pv + pve_[j]);
+            q = add_if(j < neoe, q, (woe_[j] * ue_[j] * workpv) * dL);
+        }
         for (int j = QF; j < neoe; j++) {
             double workpv = 0.5 * (pv + colk(pv_f, eoe[j]));
             q += (woe[j] * colk(u_f, eoe[j]) * workpv) * dL;
@@ -378,14 +375,19 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
     int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
     double re_[NF], kd1_[NF], kd2_[NF], wc1_[NF], wc2_[NF], t1_[NF], t2_[NF], ds_[NF];
-#pragma unroll
-    for (int i = 0; i < NF; i++) {
-        e_[i] = eoc[i];
-        c1_[i] = cc1[i];
-        c2_[i] = cc2[i];
-        o_[i] = coth[i];
-        s1_[i] = cs1[i];
+    double eocs_[NF], cdv_[NF], cidc_[NF], cmsd2_[NF];
+    row_ld(eoc, e_);
+    if (SELF) {
+        row_ld(coth, o_);
+        row_ld(cs1, s1_);
+    } else {
+        row_ld(cc1, c1_);
+        row_ld(cc2, c2_);
     }
+    row_ld(eocs, eocs_);
+    row_ld(cdv, cdv_);
+    row_ld(cidc, cidc_);
+    row_ld(cmsd2, cmsd2_);
     const double kd_c = SELF ? colk(kdiff, c) : 0.0, wc_c = SELF ? colk(wc, c) : 0.0, tm_c = SELF ? colk(tm, c) : 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++) {
@@ -409,42 +411,40 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         kd2m_[i] = lvl_dn<LP>(kd2_[i], k);
     }
     double dsd = 0.0, delsq_w = 0.0, twe = 0.0, delsq_theta = 0.0, tte = 0.0;
-    auto edge_terms = [&](int i, double re_k, double re_m, double kd1, double kd2, double kd1m, double kd2m, double wc1,
-                          double wc2, double tm1, double tm2, double dsue) {
-        const double dv = cdv[i], idc = cidc[i], msd2 = cmsd2[i];
+    // the terms of edge slot i, accumulated where `on` holds (selects: no branches)
+    auto edge_terms = [&](bool on, double eocs_i, double dv, double idc, double msd2, double re_k, double re_m,
+                          double kd1, double kd2, double kd1m, double kd2m, double wc1, double wc2, double tm1,
+                          double tm2, double dsue) {
         if (del4) {  // delsq_divergence (:1062-1070)
-            double edge_sign = r_areaCell * dv * eocs[i];
-            dsd += edge_sign * dsue;
+            double edge_sign = r_areaCell * dv * eocs_i;
+            dsd = add_if(on, dsd, edge_sign * dsue);
         }
         {  // delsq_w, tend_w_euler del2 (:1231-1254)
-            double edge_sign = 0.5 * r_areaCell * eocs[i] * dv * idc;
-            if (k > 0) {
-                double w_turb_flux = edge_sign * (re_k + re_m) * (wc2 - wc1);
-                delsq_w += w_turb_flux;
-                w_turb_flux *= msd2 * 0.25 * (kd1 + kd2 + kd1m + kd2m);
-                twe += w_turb_flux;
-            }
+            double edge_sign = 0.5 * r_areaCell * eocs_i * dv * idc;
+            double w_turb_flux = edge_sign * (re_k + re_m) * (wc2 - wc1);
+            delsq_w = add_if(on && k > 0, delsq_w, w_turb_flux);
+            w_turb_flux *= msd2 * 0.25 * (kd1 + kd2 + kd1m + kd2m);
+            twe = add_if(on && k > 0, twe, w_turb_flux);
         }
         {  // delsq_theta, tend_theta_euler del2 (:1365-1382)
-            double edge_sign = r_areaCell * eocs[i] * dv * idc;
+            double edge_sign = r_areaCell * eocs_i * dv * idc;
             double pr_scale = a.prandtl_inv * msd2;
             double theta_turb_flux = edge_sign * (tm2 - tm1) * re_k;
-            delsq_theta += theta_turb_flux;
+            delsq_theta = add_if(on, delsq_theta, theta_turb_flux);
             theta_turb_flux *= 0.5 * (kd1 + kd2) * pr_scale;
-            tte += theta_turb_flux;
+            tte = add_if(on, tte, theta_turb_flux);
         }
     };
 #pragma unroll
     for (int i = 0; i < NF; i++)
-        if (i < ne && kl)
-            edge_terms(i, re_[i], re_m_[i], kd1_[i], kd2_[i], kd1m_[i], kd2m_[i], wc1_[i], wc2_[i], t1_[i], t2_[i], ds_[i]);
+        edge_terms(i < ne && kl, eocs_[i], cdv_[i], cidc_[i], cmsd2_[i], re_[i], re_m_[i], kd1_[i], kd2_[i],
+                   kd1m_[i], kd2m_[i], wc1_[i], wc2_[i], t1_[i], t2_[i], ds_[i]);
     for (int i = NF; i < ne; i++) {  // generic tail (shuffles: whole column takes it)
         const int e = eoc[i], c1 = cc1[i], c2 = cc2[i];
         double re_k = col_rd<LP>(rho_edge, e, k, L), kd1 = col_rd<LP>(kdiff, c1, k, L), kd2 = col_rd<LP>(kdiff, c2, k, L);
         double re_m = lvl_dn<LP>(re_k, k), kd1m = lvl_dn<LP>(kd1, k), kd2m = lvl_dn<LP>(kd2, k);
-        if (kl)
-            edge_terms(i, re_k, re_m, kd1, kd2, kd1m, kd2m, colk(wc, c1), colk(wc, c2), colk(tm, c1),
-                       colk(tm, c2), ldz(del4, colk(dsu, e)));
+        edge_terms(kl, eocs[i], cdv[i], cidc[i], cmsd2[i], re_k, re_m, kd1, kd2, kd1m, kd2m, ldz(kl, colk(wc, c1)),
+                   ldz(kl, colk(wc, c2)), ldz(kl, colk(tm, c1)), ldz(kl, colk(tm, c2)), ldz(kl && del4, colk(dsu, e)));
     }
     if (!kl) return;
     if (del4) colk(fw(S, F_delsq_divergence), c) = dsd;
@@ -503,13 +503,20 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
     int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
     double ru_[NF], F_[NF], rus_[NF], ts1_[NF], ts2_[NF], dw1_[NF], dw2_[NF], dt1_[NF], dt2_[NF];
-#pragma unroll
-    for (int i = 0; i < NF; i++) {
-        e_[i] = eoc[i];
-        c1_[i] = cc1[i];
-        c2_[i] = cc2[i];
-        o_[i] = coth[i];
-        s1_[i] = cs1[i];
+    double eocs_[NF], cdv_[NF], cidc_[NF], cmsd4_[NF];
+    row_ld(eoc, e_);
+    if (SELF) {
+        row_ld(coth, o_);
+        row_ld(cs1, s1_);
+    } else {
+        row_ld(cc1, c1_);
+        row_ld(cc2, c2_);
+    }
+    row_ld(eocs, eocs_);
+    row_ld(cdv, cdv_);
+    if (rk0) {
+        row_ld(cidc, cidc_);
+        row_ld(cmsd4, cmsd4_);
     }
     const double ts_c = (SELF && !rk0) ? colk(tms_f, c) : 0.0;
     const double dw_c = (SELF && del4) ? colk(dw, c) : 0.0, dt_c = (SELF && del4) ? colk(dth, c) : 0.0;
@@ -551,11 +558,10 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     if (del4 && kl) {  // :1258-1272
         double r_areaCell = a.h4 * invA;
 #pragma unroll
-        for (int i = 0; i < NF; i++)
-            if (i < ne) {
-                double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
-                if (k > 0) twe -= edge_sign * (dw2_[i] - dw1_[i]);
-            }
+        for (int i = 0; i < NF; i++) {
+            double edge_sign = cmsd4_[i] * r_areaCell * cdv_[i] * eocs_[i] * cidc_[i];
+            twe = sub_if(i < ne && k > 0, twe, edge_sign * (dw2_[i] - dw1_[i]));
+        }
         for (int i = NF; i < ne; i++) {
             double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
             if (k > 0) twe -= edge_sign * (colk(dw, cc2[i]) - colk(dw, cc1[i]));
@@ -584,16 +590,14 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     double tend_theta = 0.0;  // :1328-1344
     if (kl) {
 #pragma unroll
-        for (int i = 0; i < NF; i++)
-            if (i < ne) tend_theta -= eocs[i] * ru_[i] * F_[i];
+        for (int i = 0; i < NF; i++) tend_theta = sub_if(i < ne, tend_theta, eocs_[i] * ru_[i] * F_[i]);
         for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(ru, eoc[i]) * colk(Ff, eoc[i]);
         if (!rk0) {  // :1347-1360
 #pragma unroll
-            for (int i = 0; i < NF; i++)
-                if (i < ne) {
-                    double flux = eocs[i] * cdv[i] * (rus_[i] - ru_[i]) * 0.5 * (ts2_[i] + ts1_[i]);
-                    tend_theta -= flux;
-                }
+            for (int i = 0; i < NF; i++) {
+                double flux = eocs_[i] * cdv_[i] * (rus_[i] - ru_[i]) * 0.5 * (ts2_[i] + ts1_[i]);
+                tend_theta = sub_if(i < ne, tend_theta, flux);
+            }
             for (int i = NF; i < ne; i++) {
                 const int e = eoc[i];
                 double flux = eocs[i] * cdv[i] * (colk(rus, e) - colk(ru, e)) * 0.5 *
@@ -604,11 +608,10 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
         if (del4) {  // :1384-1400
             double r_areaCell = a.h4 * a.prandtl_inv * invA;
 #pragma unroll
-            for (int i = 0; i < NF; i++)
-                if (i < ne) {
-                    double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
-                    tte -= edge_sign * (dt2_[i] - dt1_[i]);
-                }
+            for (int i = 0; i < NF; i++) {
+                double edge_sign = cmsd4_[i] * r_areaCell * cdv_[i] * eocs_[i] * cidc_[i];
+                tte = sub_if(i < ne, tte, edge_sign * (dt2_[i] - dt1_[i]));
+            }
             for (int i = NF; i < ne; i++) {
                 double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
                 tte -= edge_sign * (colk(dth, cc2[i]) - colk(dth, cc1[i]));

@@ -169,10 +169,13 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     const double zz = col_rd<LP>(fd(S, F_zz), c, k, L);
     const double zz_m = lvl_dn<LP>(zz, k);
     double w = col_rd<LP>(fd(S, F_w), c, k, L);
-    double ut_[NF], utm_[NF], zb_[NF], zb3_[NF];
+    int e_[NF];
+    double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgn_[NF];
+    row_ld(eoc, e_);
+    row_ld(sgn, sgn_);
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ut_[i] = col_rd<LP>(ut_f, eoc[i], k, L);
+        ut_[i] = col_rd<LP>(ut_f, e_[i], k, L);
         size_t q = ((size_t)c * 10 + i) * LP + k;
         zb_[i] = zb[q];
         zb3_[i] = zb3[q];
@@ -180,11 +183,10 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
 #pragma unroll
     for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
 #pragma unroll
-    for (int i = 0; i < NF; i++)
-        if (i < ne) {
-            double flux = sgn[i] * (fzm * ut_[i] + fzp * utm_[i]);
-            w -= (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux;
-        }
+    for (int i = 0; i < NF; i++) {
+        double flux = sgn_[i] * (fzm * ut_[i] + fzp * utm_[i]);
+        w = sub_if(i < ne, w, (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux);
+    }
     for (int i = NF; i < ne; i++) {
         int iEdge = eoc[i];
         double ut = col_rd<LP>(ut_f, iEdge, k, L);
@@ -214,14 +216,17 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
     if (e >= S.nEO || k >= L) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const int* sh = fi(S, F_isShared);
-    if (sh[cell1] && sh[cell2]) return;
     const double *rtp = fd(S, F_rtheta_pp), *rtpo = fd(S, F_rtheta_pp_old), *tm = fd(S, F_theta_m);
-    const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
-    double divCell1 = -(colk(rtp, cell1) - colk(rtpo, cell1));
-    double divCell2 = -(colk(rtp, cell2) - colk(rtpo, cell2));
     double* rup = fw(S, F_ru_p);
-    const size_t p = (size_t)e * LP + k;
-    colk(rup, e) += coef_divdamp * (divCell2 - divCell1) * (1.0 - fd(S, F_specZoneMaskEdge)[e]) / (colk(tm, cell1) + colk(tm, cell2));
+    // every load first (the isShared test only decides the store)
+    const int sh1 = sh[cell1], sh2 = sh[cell2];
+    const double r1 = colk(rtp, cell1), ro1 = colk(rtpo, cell1), r2 = colk(rtp, cell2), ro2 = colk(rtpo, cell2);
+    const double t1 = colk(tm, cell1), t2 = colk(tm, cell2), ru = colk(rup, e);
+    const double spec = fd(S, F_specZoneMaskEdge)[e];
+    if (sh1 && sh2) return;
+    double divCell1 = -(r1 - ro1);
+    double divCell2 = -(r2 - ro2);
+    colk(rup, e) = ru + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec) / (t1 + t2);
 }
 template <int LP>
 static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
@@ -301,6 +306,22 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
         fw(S, X_ce_idc)[t] = fd(S, F_invDcEdge)[e];
         fw(S, X_ce_msd2)[t] = fd(S, F_meshScalingDel2)[e];
         fw(S, X_ce_msd4)[t] = fd(S, F_meshScalingDel4)[e];
+        if (i == 0) {  // X_wfl (k_dyn_A): the literal flux_arr of :1174-1205 on the zeroed w
+            const int ne = fi(S, F_nEdgesOnCell)[c];
+            const int el = ne > 0 ? eoc[t + ne - 1] : S.nEdges;
+            const int na = fi(S, F_nAdvCellsForEdge)[el];
+            const double* ac = fd(S, F_adv_coefs) + (size_t)el * 15;
+            const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)el * 15;
+            for (int q = 0; q < 2; q++) {
+                const double sg = q == 0 ? 1.0 : -1.0, w_zeroed = 0.0;
+                double flux_arr = 0.0;
+                for (int j = 0; j < na; j++) {
+                    double scalar_weight = ac[j] + sg * ac3[j];
+                    flux_arr += scalar_weight * w_zeroed;
+                }
+                fw(S, X_wfl)[(size_t)c * 2 + q] = flux_arr;
+            }
+        }
     }
 }
 // derived mesh arrays; decides S.selfc (synchronous: runs once after each mesh upload)

@@ -56,20 +56,32 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
     const double invA = fd(S, F_invAreaCell)[c];
     double div = 0.0, ke = 0.0;
-    double u_[NF];
+    int e_[NF];
+    double u_[NF], sgn_[NF], dv_[NF], dc_[NF];
+    row_ld(eoc, e_);
+    row_ld(sgn, sgn_);
+    row_ld(fd(S, X_ce_dv) + (size_t)c * 10, dv_);  // dvEdge(edgesOnCell)
 #pragma unroll
-    for (int i = 0; i < NF; i++) u_[i] = colk(u, eoc[i]);
-    for (int i = 0; i < ne; i++) {
-        int iEdge = eoc[i];
-        double uu = 0.0;
+    for (int i = 0; i < NF; i++) {
+        u_[i] = colk(u, e_[i]);
+        dc_[i] = dcEdge[e_[i]];
+    }
 #pragma unroll
-        for (int j = 0; j < NF; j++)
-            if (j == i) uu = u_[j];
-        if (i >= NF) uu = colk(u, iEdge);
-        double s = sgn[i] * dvEdge[iEdge];
-        div += s + uu;
+    for (int i = 0; i < NF; i++) {
+        const double uu = u_[i];
+        double s = sgn_[i] * dv_[i];
+        div = add_if(i < ne, div, s + uu);
         // ke_edge(iEdge,k) exactly as the edge loop (:352) writes it; the zero slot
         // row of ke_edge is never written, and its recomputation is 0*0*0 as well
+        double efac = dc_[i] * dv_[i];
+        double kee = (e_[i] < S.nEdges) ? efac * (uu * uu) : 0.0;
+        ke = add_if(i < ne, ke, 0.25 * kee);
+    }
+    for (int i = NF; i < ne; i++) {
+        int iEdge = eoc[i];
+        double uu = colk(u, iEdge);
+        double s = sgn[i] * dvEdge[iEdge];
+        div += s + uu;
         double efac = dcEdge[iEdge] * dvEdge[iEdge];
         double kee = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
         ke += 0.25 * kee;
@@ -113,21 +125,23 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
     const double h1 = colk(h, coe[0]), h2 = colk(h, coe[1]), uu = colk(u, e);
     const double pv1 = colk(pvv, voe[0]), pv2 = colk(pvv, voe[1]);
     const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
-    double ue[QF];
+    const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
+    const int neoe = RECON_V ? fi(S, F_nEdgesOnEdge)[e] : 0;
+    int ee_[QF];
+    double ue[QF], wts_[QF];
     if (RECON_V) {
+        row_ld(eoe, ee_);
+        row_ld(wts, wts_);
 #pragma unroll
-        for (int i = 1; i < QF; i++) ue[i] = colk(u, eoe[i]);
+        for (int i = 1; i < QF; i++) ue[i] = colk(u, ee_[i]);
     }
     colk(fw(S, F_h_edge), e) = 0.5 * (h1 + h2);
     const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
     colk(fw(S, F_ke_edge), e) = efac * (uu * uu);
     if (RECON_V) {  // Q23: the sum starts at i = 1
-        const int neoe = fi(S, F_nEdgesOnEdge)[e];
-        const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
         double v = 0;
 #pragma unroll
-        for (int i = 1; i < QF; i++)
-            if (i < neoe) v += wts[i] * ue[i];
+        for (int i = 1; i < QF; i++) v = add_if(i < neoe, v, wts_[i] * ue[i]);
         for (int i = QF; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
         colk(fw(S, F_v), e) = v;
     }

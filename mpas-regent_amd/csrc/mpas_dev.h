@@ -39,6 +39,8 @@ enum FieldId {
     X_ce_msd4,  // meshScalingDel4(edgesOnCell(i,c))     C2F x10
     X_ce_oth,   // the cell of cellsOnEdge(edgesOnCell(i,c), 0:1) that is not c   C2I x10
     X_ce_s1,    // 1 if cellsOnEdge(edgesOnCell(i,c), 0) == c                     C2I x10
+    X_wfl,      // dyn_tend's w-advection flux_arr over the advCells of the cell's last
+                // edge, sum_j (adv_coefs + s adv_coefs_3rd) * 0.0 for s = +1, -1      C2F x2
     // scratch (not reference fields)
     X_wc,       // w after zeroing, horizontal advection and curvature (dyn_tend :1170-1218);
                 // the U section still reads the pre-zeroing w (:1013)
@@ -197,15 +199,21 @@ __device__ __forceinline__ MPAS_GLOBAL T* sgpr_ptr(T* p) {
     return (MPAS_GLOBAL T*)(((uint64_t)hi << 32) | lo);
 }
 
-// column ent of f (a row of LP values); SGPR-held when one column fills the wavefront
-// (LP == 64, ent wave-uniform), a plain per-lane pointer otherwise
-template <int LP, class T>
-__device__ __forceinline__ MPAS_GLOBAL T* col_row(T* f, int ent) {
-    if constexpr (LP == 64) return sgpr_ptr(f + (size_t)ent * LP);
-    else return (MPAS_GLOBAL T*)(f + (size_t)ent * LP);
+// Level k of column ent of field f, addressed as the field's base (wave-uniform, SGPRs)
+// plus a 32-bit byte offset in a VGPR: loads compile to the saddr + voffset form, every
+// field gathered at the same neighbour shares one offset register, and only one SGPR
+// pair per field is live (per-row SGPR pointers run the scalar file out of registers,
+// and the compiler then serialises the connectivity loads).  Every field is < 4 GiB.
+template <int LP>
+__device__ __forceinline__ uint32_t col_off(int ent, int k) {
+    return ((uint32_t)ent * (uint32_t)LP + (uint32_t)k) * (uint32_t)sizeof(double);
+}
+template <class T>
+__device__ __forceinline__ T& at_off(T* f, uint32_t off) {
+    return *(T*)((MPAS_GLOBAL char*)(f) + off);
 }
 // level k of column ent of field pointer f (needs LP and k in scope)
-#define colk(f, ent) col_row<LP>((f), (ent))[(unsigned)k]
+#define colk(f, ent) at_off((f), col_off<LP>((ent), k))
 
 // f at the two cellsOnEdge (x1, x2) of edge slot i of a cell.  SELF (S.selfc): the cell
 // is one of them, so only the other cell `oth` is gathered and `own`, f at the cell
@@ -233,10 +241,24 @@ __device__ __forceinline__ const int* fi(const DevState& S, int id) { return (co
 // (s_waitcnt vmcnt(0) at every join) and costs the memory-level parallelism.
 __device__ __forceinline__ double ldz(bool keep, double v) { return keep ? v : 0.0; }
 
+// acc + t where c holds, acc elsewhere.  A select, not a branch: the operands, loaded
+// ahead, are then not sunk by the compiler into a conditional block (one memory round
+// trip, and one full s_waitcnt vmcnt(0), per list entry).  Bit-identical to `if (c) acc += t`.
+__device__ __forceinline__ double add_if(bool c, double acc, double t) { return c ? acc + t : acc; }
+__device__ __forceinline__ double sub_if(bool c, double acc, double t) { return c ? acc - t : acc; }
+
+// the first N entries of a padded mesh-data row, loaded unconditionally (every row is
+// allocated at its full width, so the entries past the list's length are in bounds)
+template <int N, class T>
+__device__ __forceinline__ void row_ld(const T* p, T (&r)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; i++) r[i] = p[i];
+}
+
 // column read with the level policy: levels outside 0..L read 0.0
 template <int LP>
 __device__ __forceinline__ double col_rd(const double* f, int ent, int k, int L) {
-    return ldz(k <= L, col_row<LP>(f, ent)[(unsigned)k]);
+    return ldz(k <= L, at_off(f, col_off<LP>(ent, k)));
 }
 #endif
 

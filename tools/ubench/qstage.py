@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""edgesOnEdge gather microbenchmark (see qstage.hip) on the x1.163842 mesh, raw
+reference ids as offsets (the benchmark's ids).  Checks every variant against variant 0
+(same summation order: bit-identical) and prints the median time of each.
+
+usage: python tools/ubench/qstage.py   (needs a GPU; libqstage.so is built beforehand on the CPU)
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(HERE, "..", "..", "mpas-regent_amd")]
+from mpasdyn import build_state as bs  # noqa: E402
+from mpasdyn import mesh  # noqa: E402
+
+
+def staging_lists(eoe, nE, E):
+    nb = (nE + E - 1) // E
+    off = np.zeros(nb, np.int32)
+    cnt = np.zeros(nb, np.int32)
+    ul = []
+    lidx = np.zeros((nE, 10), np.uint16)
+    lself = np.zeros(nE, np.uint16)
+    pos = 0
+    for b in range(nb):
+        e0, e1 = b * E, min(nE, b * E + E)
+        u, inv = np.unique(np.concatenate([np.arange(e0, e1), eoe[e0:e1].ravel()]), return_inverse=True)
+        off[b], cnt[b] = pos, len(u)
+        pos += len(u)
+        ul.append(u)
+        n = e1 - e0
+        lself[e0:e1] = inv[:n]
+        lidx[e0:e1] = inv[n:].reshape(n, 10)
+    return off, cnt, np.concatenate(ul).astype(np.int32), lidx, lself
+
+
+def main():
+    import torch
+    so = os.path.join(HERE, "libqstage.so")
+    if not os.path.exists(so):
+        raise SystemExit("build libqstage.so first (hipcc --offload-arch=gfx950 -O3 -shared -fPIC)")
+    lib = ctypes.CDLL(so)
+    lib.ub_q.argtypes = [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int] + [ctypes.c_void_p] * 7
+    m = mesh.icosahedral(7)
+    st = bs.build_state(m, 56, "physical", mesh_only=True)
+    nE = m.nEdges
+    eoe = np.minimum(st["edgesOnEdge"][:nE, :10].astype(np.int64), nE)
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(1)
+    u = torch.rand((nE + 1) * 64, dtype=torch.float64, generator=g).to(dev)
+    pv = torch.rand((nE + 1) * 64, dtype=torch.float64, generator=g).to(dev)
+    w = torch.rand(nE * 10, dtype=torch.float64, generator=g).to(dev)
+    eoe_d = torch.from_numpy(eoe.astype(np.int32).ravel()).to(dev)
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device=dev)
+    st_ = torch.cuda.current_stream().cuda_stream
+    lists = {}
+    for E, maxu in ((16, 120), (32, 160), (64, 240)):
+        off, cnt, ul, lidx, lself = staging_lists(eoe, nE, E)
+        assert cnt.max() <= maxu, (E, cnt.max())
+        lists[E] = [torch.from_numpy(x).to(dev) for x in (off, cnt, ul, lidx.astype(np.int16).ravel(),
+                                                         lself.astype(np.int16))] + [int(cnt.max()), float(cnt.mean())]
+    res = {}
+    ref = None
+    vars_ = [int(x) for x in os.environ.get('QVARS', '0,1,16,19,20,21,22,23').split(',')]
+    for var, E in [(v, {4: 32, 5: 32, 20: 32, 21: 32, 22: 64, 23: 64}.get(v, 16)) for v in vars_]:
+        L = lists[E]
+        out = torch.zeros((nE + 1) * 64, dtype=torch.float64, device=dev)
+        ts = []
+        for rep in range(7):
+            flush.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            rc = lib.ub_q(var, u.data_ptr(), pv.data_ptr(), eoe_d.data_ptr(), w.data_ptr(), nE, out.data_ptr(),
+                          L[0].data_ptr(), L[1].data_ptr(), L[2].data_ptr(), L[3].data_ptr(), L[4].data_ptr(), st_)
+            e1.record()
+            torch.cuda.synchronize()
+            assert rc == 0, rc
+            ts.append(e0.elapsed_time(e1))
+        t = sorted(ts[1:])[len(ts[1:]) // 2]
+        o = out.view(nE + 1, 64)[:nE, :56]
+        if ref is None:
+            ref = o.clone()  # the first variant listed is the reference
+        same = bool(torch.equal(o, ref))
+        res[f"v{var}"] = {"ms": round(t, 4), "same_as_first": same, "E": E if var >= 4 else None,
+                          "union_mean": L[6] if var >= 4 else None, "union_max": L[5] if var >= 4 else None}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
