@@ -105,6 +105,23 @@ int mpas_atm_compute_solve_diagnostics(mpas_ctx* ctx, int hollingsworth, int rk_
 /* :1951 atm_rk_dynamics_substep_finish(cr, er, dynamics_substep, dynamics_split) */
 int mpas_atm_rk_dynamics_substep_finish(mpas_ctx* ctx, int dynamics_substep, int dynamics_split);
 
+/* ---- operators defined beside the RK3 loop but not run inside it ------------------ */
+/* :1766 atm_recover_large_step_variables_work(cr, er, vert_r, ns, rk_step, dt); commented
+ *       out of atm_srk3 (rk_timestep.rg:460, Q7); Q24 literal */
+int mpas_atm_recover_large_step_variables_work(mpas_ctx* ctx, int ns, int rk_step, double dt);
+/* :1893 mpas_reconstruct_2d(cr, er, includeHalos, on_a_sphere); atm_core_init
+ *       (atm_core.rg:33); commented out of atm_srk3 (rk_timestep.rg:487) */
+int mpas_reconstruct_2d(mpas_ctx* ctx, int includeHalos, int on_a_sphere);
+/* rk_timestep.rg:29 summarize_timestep(cr, er, config_print_detailed_minmax_vel,
+ *       config_print_global_minmax_vel, config_print_global_minmax_sca): the values the
+ *       reference prints, into out[31] (host memory; the call synchronises):
+ *       out[0..24] five records {value, index, k, lat_deg, lon_deg}: min w, max w, min u,
+ *       max u, max wind speed; out[25], out[26] NaN seen in w, u; out[27..30] the
+ *       regentlib min/max folds from 0.0 of w and of u.  Blocks whose flag is 0 stay 0
+ *       (the reference calls it with every flag false, rk_timestep.rg:492). */
+int mpas_summarize_timestep(mpas_ctx* ctx, int config_print_detailed_minmax_vel, int config_print_global_minmax_vel,
+                            int config_print_global_minmax_sca, double* out);
+
 /* ---- the driver (rk_timestep.rg:361-500) ---------------------------------------- */
 /* schedule 0: the reference's atm_srk3 (Q4: rk_sub_timestep[rk_step] truncated into
  * dyn_tend's rk_step; Q5: n+1 acoustic substeps); schedule 1: dyn_tend rk_step = 0,1,2

@@ -1,0 +1,371 @@
+// k_diag.hip -- the operators the reference defines next to the RK3 loop but does not run
+// inside it, for gfx950:
+//   atm_recover_large_step_variables_work  dynamics_tasks.rg:1766-1872 (commented out of
+//                                          atm_srk3, rk_timestep.rg:460, Q7)
+//   mpas_reconstruct_2d                    dynamics_tasks.rg:1893-1948 (atm_core_init,
+//                                          atm_core.rg:33; commented out of atm_srk3 :487)
+//   summarize_timestep                     rk_timestep.rg:29-359 (called at :492 with every
+//                                          print flag false: a no-op on the path)
+// Same column mapping as the rest of the library: one wavefront per cell/edge column.
+#include "mpas_dev.h"
+#include "mpas_halo.h"
+
+namespace mpas {
+
+// ---------------------------------------------------------------- recover_large_step
+struct RecK {
+    double invNs, dt, rgas_p0, rgas, rcv;
+    int rk_step;
+};
+
+// :1788-1820 (the loop over cells and levels 0..nVertLevels-1), and the "garbage cell"
+// rho_zz = 1.0 of :1790-1792 (our zero slot)
+template <int LP>
+__global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
+    ColMap<LP> m(S);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (m.blk == 0 && (int)threadIdx.x < L) fw(S, F_rho_zz)[(size_t)S.nCells * LP + threadIdx.x] = 1.0;
+    if (c >= S.nCO) return;
+    const bool kl = k < L;
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    const double zz = col_rd<LP>(fd(S, F_zz), c, k, L), zz_m = lvl_dn<LP>(zz, k);
+    const double rps = colk(fd(S, F_rho_p_save), c), rpp = colk(fd(S, F_rho_pp), c), rb = colk(fd(S, F_rho_base), c);
+    const double ww = colk(fd(S, F_wwAvg), c), rws = colk(fd(S, F_rw_save), c), rwp = colk(fd(S, F_rw_p), c);
+    const double rtps = colk(fd(S, F_rtheta_p_save), c), rtpp = colk(fd(S, F_rtheta_pp), c);
+    const double rtb = colk(fd(S, F_rtheta_base), c);
+    const double rtd = a.rk_step == 2 ? colk(fd(S, F_rt_diabatic_tend), c) : 0.0;
+    const double exb = a.rk_step == 2 ? colk(fd(S, F_exner_base), c) : 0.0;
+    if (!kl) return;
+    const double rho_p = rps + rpp;
+    const double rho_zz = rho_p + rb;
+    double wwAvg = ww;
+    wwAvg *= a.invNs;
+    wwAvg += rws;
+    const double rw = rws + rwp;
+    const double w = rw / (fzm * zz + fzp * zz_m);  // (:1805 sets w = 0.0 first)
+    colk(fw(S, F_rho_p), c) = rho_p;
+    colk(fw(S, F_rho_zz), c) = rho_zz;
+    colk(fw(S, F_wwAvg), c) = wwAvg;
+    colk(fw(S, F_rw), c) = rw;
+    colk(fw(S, F_w), c) = w;
+    if (a.rk_step == 2) {
+        const double rtheta_p = rtps + rtpp - a.dt * rho_zz * rtd;
+        colk(fw(S, F_rtheta_p), c) = rtheta_p;
+        colk(fw(S, F_theta_m), c) = (rtheta_p + rtb) / rho_zz;
+        const double exner = zz * a.rgas_p0 * pow((rtheta_p + rtb), a.rcv);  // Q24 literal
+        colk(fw(S, F_exner), c) = exner;
+        colk(fw(S, F_pressure_p), c) = zz * a.rgas * (exner * rtheta_p + rtb * (exner - exb));
+    } else {
+        const double rtheta_p = rtps + rtpp;
+        colk(fw(S, F_rtheta_p), c) = rtheta_p;
+        colk(fw(S, F_theta_m), c) = (rtheta_p + rtb) / rho_zz;
+    }
+}
+
+// :1830-1837: ruAvg, ru (Q24: ru_save * ru_p), u from the new rho_zz
+template <int LP>
+__global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
+    ColMap<LP> m(S);
+    const int L = S.L, k = m.k, e = m.ent;
+    if (e >= S.nEO || k >= L) return;
+    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    const double* rz = fd(S, F_rho_zz);
+    const double rz1 = colk(rz, cell1), rz2 = colk(rz, cell2);
+    const double ra = colk(fd(S, F_ruAvg), e), rus = colk(fd(S, F_ru_save), e), rup = colk(fd(S, F_ru_p), e);
+    double ruAvg = ra;
+    ruAvg *= a.invNs;
+    ruAvg += rus;
+    const double ru = rus * rup;
+    colk(fw(S, F_ruAvg), e) = ruAvg;
+    colk(fw(S, F_ru), e) = ru;
+    colk(fw(S, F_u), e) = 2 * ru / (rz1 + rz2);
+}
+
+// :1839-1870: the w recovery from (rho*omega)_p over the cell's edges, then the division.
+// The level-0 term (cf1..cf3 flux) is added to w(cell, 0) at every one of the nVertLevels
+// level iterations of the cell; lane 0 replays that sequence in the reference's order.
+template <int LP>
+__global__ __launch_bounds__(256) void k_recover_w(DevState S) {
+    ColMap<LP> m(S);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    if (fi(S, F_bdyMaskCell)[c] > kRelaxZone) return;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    int e_[10];
+    double sg_[10], zb0_[10], zb30_[10], a_[10], b_[10];
+    row_ld(fi(S, F_edgesOnCell) + (size_t)c * 10, e_);
+    row_ld(fd(S, F_edgesOnCell_sign) + (size_t)c * 10, sg_);
+    const double *ru = fd(S, F_ru), *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    const double cf1 = fd(S, F_cf1)[0], cf2 = fd(S, F_cf2)[0], cf3 = fd(S, F_cf3)[0];
+    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L), rz_m = lvl_dn<LP>(rz, k);
+    const double rz1 = __shfl(rz, 1, LP), rz2 = __shfl(rz, 2, LP);
+    double w = col_rd<LP>(fd(S, F_w), c, k, L);
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        const double r = col_rd<LP>(ru, e_[i], k, L), r_m = lvl_dn<LP>(r, k);
+        const double r0 = __shfl(r, 0, LP), r1 = __shfl(r, 1, LP), r2 = __shfl(r, 2, LP);
+        const double z = zb[((size_t)c * 10 + i) * LP + k], z3 = zb3[((size_t)c * 10 + i) * LP + k];
+        zb0_[i] = __shfl(z, 0, LP);
+        zb30_[i] = __shfl(z3, 0, LP);
+        const double flux = (cf1 * r0 + cf2 * r1 + cf3 * r2);
+        a_[i] = sg_[i] * (zb0_[i] + copysign(1.0, flux) * zb30_[i]) * flux;
+        const double flux2 = fzm * r * (fzp * r_m);  // Q24 literal
+        b_[i] = sg_[i] * (z + copysign(1.0, flux2) * z3) * flux2;
+    }
+    if (k == 0) {
+        for (int i = 0; i < ne; i++) {  // level iteration 0
+            w += a_[i];
+            w += b_[i];
+        }
+        for (int kk = 1; kk < L; kk++)  // level iterations 1..nVertLevels-1
+            for (int i = 0; i < ne; i++) w += a_[i];
+        w /= (cf1 * rz + cf2 * rz1 + cf3 * rz2);
+    } else {
+        for (int i = 0; i < ne; i++) w += b_[i];
+        w /= (fzm * rz + fzp * rz_m);
+    }
+    if (k < L) colk(fw(S, F_w), c) = w;
+}
+
+template <int LP>
+static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_step, double dt) {
+    constexpr int COLS = ColMap<LP>::COLS;
+    RecK a;
+    a.invNs = 1 / (double)ns;
+    a.dt = dt;
+    a.rgas = kRgas;
+    a.rgas_p0 = kRgas / 100000;
+    a.rcv = kRgas / (kCp - kRgas);
+    a.rk_step = rk_step;
+    const int nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS;
+    k_recover_cells<LP><<<nCB, 256, 0, st>>>(S, a);
+    HALO_WROTE(S, F_rho_p, F_rho_zz, F_wwAvg, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
+    HALO_BEFORE(S, st, F_rho_zz);
+    k_recover_edges<LP><<<nEB, 256, 0, st>>>(S, a);
+    HALO_WROTE(S, F_ruAvg, F_ru, F_u);
+    HALO_BEFORE(S, st, F_ru);
+    k_recover_w<LP><<<nCB, 256, 0, st>>>(S);
+    HALO_WROTE(S, F_w);
+    return hipGetLastError();
+}
+hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt) {
+    MPAS_LP_DISPATCH(S.LP, recover_lp, S, st, ns, rk_step, dt);
+}
+
+// ---------------------------------------------------------------- reconstruct_2d
+template <int LP>
+__global__ __launch_bounds__(256) void k_reconstruct(DevState S, int on_a_sphere) {
+    ColMap<LP> m(S);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* cr = fd(S, F_coeffs_reconstruct) + (size_t)c * 30;
+    const double* u = fd(S, F_u);
+    int e_[NF];
+    double co_[3 * NF], u_[NF];
+    row_ld(eoc, e_);
+    row_ld(cr, co_);
+#pragma unroll
+    for (int i = 0; i < NF; i++) u_[i] = colk(u, e_[i]);
+    const double clat = fd(S, X_cosLatCell)[c], slat = fd(S, X_sinLatCell)[c];
+    const double clon = fd(S, X_cosLonCell)[c], slon = fd(S, X_sinLonCell)[c];
+    if (k >= L) return;
+    double X = 0.0, Y = 0.0, Z = 0.0;
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        X = add_if(i < ne, X, co_[3 * i + 0] * u_[i]);
+        Y = add_if(i < ne, Y, co_[3 * i + 1] * u_[i]);
+        Z = add_if(i < ne, Z, co_[3 * i + 2] * u_[i]);
+    }
+    for (int i = NF; i < ne; i++) {
+        const double ue = colk(u, eoc[i]);
+        X += cr[3 * i + 0] * ue;
+        Y += cr[3 * i + 1] * ue;
+        Z += cr[3 * i + 2] * ue;
+    }
+    colk(fw(S, F_uReconstructX), c) = X;
+    colk(fw(S, F_uReconstructY), c) = Y;
+    colk(fw(S, F_uReconstructZ), c) = Z;
+    if (on_a_sphere) {
+        colk(fw(S, F_uReconstructZonal), c) = -X * slon + Y * clon;
+        colk(fw(S, F_uReconstructMeridional), c) = -(X * clon + Y * slon) * slat + Z * clat;
+    } else {
+        colk(fw(S, F_uReconstructZonal), c) = X;
+        colk(fw(S, F_uReconstructMeridional), c) = Y;
+    }
+}
+template <int LP>
+static hipError_t reconstruct_lp(const DevState& S, hipStream_t st, int on_a_sphere) {
+    constexpr int COLS = ColMap<LP>::COLS;
+    HALO_BEFORE(S, st, F_u);
+    k_reconstruct<LP><<<(S.nCO + COLS - 1) / COLS, 256, 0, st>>>(S, on_a_sphere);
+    HALO_WROTE(S, F_uReconstructX, F_uReconstructY, F_uReconstructZ, F_uReconstructZonal, F_uReconstructMeridional);
+    return hipGetLastError();
+}
+hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere) {
+    MPAS_LP_DISPATCH(S.LP, reconstruct_lp, S, st, on_a_sphere);
+}
+
+// ---------------------------------------------------------------- summarize_timestep
+// Sequential semantics made parallel.  The points of a field are numbered in the
+// reference's loop order, idx = entity * nVertLevels + k; every thread scans one
+// contiguous chunk in that order and the chunks combine in order:
+//   FirstExt  "if (x < best) ..." from 1e20 (or > from -1e20): the first point holding the
+//             extreme, NaN never taken;
+//   Fold      acc = min(acc, x) with min(a,b) = a < b ? a : b from acc = 0.0: a NaN makes
+//             acc NaN and the next point then replaces it, so the result is the extreme
+//             of the points after the last NaN with ties going to the LATER point (the
+//             0.0 start counts only when there is no NaN), or NaN if the last point is one.
+struct FirstExt {
+    double v;
+    long i;
+};
+struct Fold {
+    long nan;  // index of the last NaN, -1 if none
+    double v;
+    long i;    // -1: no point after the last NaN yet
+};
+struct SumPart {
+    FirstExt mn, mx, spd;
+    Fold fmn, fmx;
+    int has_nan;
+};
+
+__device__ __forceinline__ void fe_take(FirstExt& a, const FirstExt& b, bool is_min) {
+    // b follows a (b's points come after a's): b wins only if strictly better
+    if (b.i < 0) return;
+    if (a.i < 0 || (is_min ? (b.v < a.v) : (b.v > a.v))) a = b;
+}
+__device__ __forceinline__ void fold_take(Fold& a, const Fold& b, bool is_min) {
+    if (b.nan >= 0) {  // everything in a is before b's last NaN
+        a = b;
+        return;
+    }
+    if (b.i < 0) return;
+    if (a.i < 0 || (is_min ? !(a.v < b.v) : !(a.v > b.v))) {  // ties to the later point
+        a.v = b.v;
+        a.i = b.i;
+    }
+}
+__device__ __forceinline__ void part_init(SumPart& p) {
+    p.mn = {1.0e20, -1};
+    p.mx = {-1.0e20, -1};
+    p.spd = {-1.0e20, -1};
+    p.fmn = {-1, 0.0, -1};
+    p.fmx = {-1, 0.0, -1};
+    p.has_nan = 0;
+}
+__device__ __forceinline__ void part_take(SumPart& a, const SumPart& b) {
+    fe_take(a.mn, b.mn, true);
+    fe_take(a.mx, b.mx, false);
+    fe_take(a.spd, b.spd, false);
+    fold_take(a.fmn, b.fmn, true);
+    fold_take(a.fmx, b.fmx, false);
+    a.has_nan |= b.has_nan;
+}
+
+// which = 0: w over the owned cells; 1: u (and the wind speed with v) over the owned edges
+template <int LP>
+__global__ __launch_bounds__(256) void k_sum_scan(DevState S, int which, long chunk, SumPart* parts) {
+    const long n = (long)(which == 0 ? S.nCO : S.nEO) * S.L;
+    const long t = (long)blockIdx.x * 256 + threadIdx.x;
+    const double* x = fd(S, which == 0 ? F_w : F_u);
+    const double* y = fd(S, F_v);
+    SumPart p;
+    part_init(p);
+    for (long idx = t * chunk; idx < n && idx < (t + 1) * chunk; idx++) {
+        const long ent = idx / S.L, k = idx - ent * S.L;
+        const double xv = x[ent * LP + k];
+        if (xv < p.mn.v) p.mn = {xv, idx};
+        if (xv > p.mx.v) p.mx = {xv, idx};
+        if (which == 1) {
+            const double yv = y[ent * LP + k];
+            const double spd = sqrt(xv * xv + yv * yv);
+            if (spd > p.spd.v) p.spd = {spd, idx};
+        }
+        if (isnan(xv)) {
+            p.has_nan = 1;
+            p.fmn = {idx, xv, -1};
+            p.fmx = {idx, xv, -1};
+        } else {
+            if (p.fmn.i < 0 || !(p.fmn.v < xv)) p.fmn.v = xv, p.fmn.i = idx;
+            if (p.fmx.i < 0 || !(p.fmx.v > xv)) p.fmx.v = xv, p.fmx.i = idx;
+        }
+    }
+    parts[t] = p;
+}
+
+// one block: combine the chunk partials in order and finish the printed records
+__global__ __launch_bounds__(256) void k_sum_final(DevState S, int which, const SumPart* parts, int nparts,
+                                                   double* out) {
+    __shared__ SumPart sh[256];
+    const int t = threadIdx.x;
+    const int per = (nparts + 255) / 256;
+    SumPart p;
+    part_init(p);
+    for (int j = t * per; j < nparts && j < (t + 1) * per; j++) part_take(p, parts[j]);
+    sh[t] = p;
+    __syncthreads();
+    for (int s = 1; s < 256; s <<= 1) {
+        if ((t % (2 * s)) == 0 && t + s < 256) part_take(sh[t], sh[t + s]);
+        __syncthreads();
+    }
+    if (t != 0) return;
+    p = sh[0];
+    const double pi_const = 2.0 * asin(1.0);
+    const int L = S.L;
+    const double* lat = fd(S, which == 0 ? F_lat : F_latEdge);
+    const double* lon = fd(S, which == 0 ? F_lon : F_lonEdge);
+    auto rec = [&](double* r, const FirstExt& e, bool level_k_latlon) {
+        const long ent = e.i >= 0 ? e.i / L : -1, k = e.i >= 0 ? e.i % L : -1;
+        double la = 0.0, lo = 0.0;
+        if (ent >= 0 && (!level_k_latlon || k == 0)) {  // 2-D mesh data at level > 0 reads 0 (Q2)
+            la = lat[ent];
+            lo = lon[ent];
+        }
+        r[0] = e.v;
+        r[1] = (double)ent;
+        r[2] = (double)k;
+        la *= 180.0 / pi_const;
+        lo *= 180.0 / pi_const;
+        if (lo > 180.0) lo -= 360.0;
+        r[3] = la;
+        r[4] = lo;
+    };
+    auto fold_end = [&](const Fold& f, bool is_min) {
+        const long n = (long)(which == 0 ? S.nCO : S.nEO) * L;
+        if (f.nan >= 0 && f.nan == n - 1) return f.v;  // the last point is NaN
+        if (f.nan >= 0) return f.v;                    // extreme after the last NaN
+        // no NaN: the 0.0 start precedes every point; ties go to the later point
+        if (f.i < 0) return 0.0;
+        return is_min ? ((0.0 < f.v) ? 0.0 : f.v) : ((0.0 > f.v) ? 0.0 : f.v);
+    };
+    double* o = out + (which == 0 ? 0 : 10);
+    rec(o, p.mn, false);
+    rec(o + 5, p.mx, true);
+    if (which == 1) rec(out + 20, p.spd, false);
+    out[25 + which] = p.has_nan ? 1.0 : 0.0;
+    out[27 + 2 * which] = fold_end(p.fmn, true);
+    out[28 + 2 * which] = fold_end(p.fmx, false);
+}
+
+template <int LP>
+static hipError_t summarize_lp(const DevState& S, hipStream_t st, void* scratch, double* out) {
+    constexpr int T = 64 * 256;  // chunk scanners
+    SumPart* parts = (SumPart*)scratch;
+    for (int which = 0; which < 2; which++) {
+        const long n = (long)(which == 0 ? S.nCO : S.nEO) * S.L;
+        const long chunk = (n + T - 1) / T;
+        k_sum_scan<LP><<<T / 256, 256, 0, st>>>(S, which, chunk > 0 ? chunk : 1, parts);
+        k_sum_final<<<1, 256, 0, st>>>(S, which, parts, T, out);
+    }
+    return hipGetLastError();
+}
+size_t summarize_scratch_bytes() { return (size_t)64 * 256 * sizeof(SumPart); }
+hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, double* out) {
+    MPAS_LP_DISPATCH(S.LP, summarize_lp, S, st, scratch, out);
+}
+
+}  // namespace mpas

@@ -24,6 +24,9 @@ const FieldInfo kFields[X_COUNT] = {
     {"cosAngleEdge", K_E2F, 1, D_M, 0, 0},
     {"cosLatEdge", K_E2F, 1, D_M, 0, 0},
     {"cosLatCell", K_C2F, 1, D_M, 0, 0},
+    {"sinLatCell", K_C2F, 1, D_M, 0, 0},
+    {"cosLonCell", K_C2F, 1, D_M, 0, 0},
+    {"sinLonCell", K_C2F, 1, D_M, 0, 0},
     {"ce_c1", K_C2I, 10, D_M, 0, 0},
     {"ce_c2", K_C2I, 10, D_M, 0, 0},
     {"ce_dv", K_C2F, 10, D_M, 0, 0},
@@ -64,6 +67,8 @@ struct mpas_ctx {
     std::unique_ptr<Halo> halo;           // decomposed mesh only
     std::shared_ptr<LoopGroup> loopgrp;   // in-process loopback transport
     int* gid_dev[3] = {nullptr, nullptr, nullptr};
+    void* sum_scratch = nullptr;  // summarize_timestep partials (allocated on first use)
+    double* sum_out = nullptr;
 };
 
 namespace {
@@ -235,6 +240,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
     }
     run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
+    // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }
 
 }  // namespace
@@ -283,7 +289,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.nVO = dims->nVertices;
         c->S.L = dims->nVertLevels;
         c->S.LP = LP;
-        c->S.xcd = 0;
+        c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         for (int f = 0; f < X_COUNT; f++) {
             size_t b = dev_bytes(c, f);
@@ -320,6 +326,8 @@ int mpas_ctx_destroy(mpas_ctx* c) {
     c->loopgrp.reset();
     for (auto p : c->gid_dev)
         if (p) (void)hipFree(p);
+    if (c->sum_scratch) (void)hipFree(c->sum_scratch);
+    if (c->sum_out) (void)hipFree(c->sum_out);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return MPAS_OK;
@@ -415,17 +423,17 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
         hipcheck(hipMemcpy(c->S.f[f], buf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
         c->dirty = true;
         if (c->halo) c->halo->stale[f] = 0;  // uploaded ghosts are the global values
-        // derived mesh arrays: cos() on the host with the same libm as the oracle
-        int derived = -1;
-        if (f == F_angleEdge) derived = X_cosAngleEdge;
-        if (f == F_latEdge) derived = X_cosLatEdge;
-        if (f == F_lat) derived = X_cosLatCell;
-        if (derived >= 0) {
+        // derived mesh arrays: cos()/sin() on the host with the same libm as the oracle
+        struct { int src, dst; double (*fn)(double); } der[] = {
+            {F_angleEdge, X_cosAngleEdge, ::cos}, {F_latEdge, X_cosLatEdge, ::cos}, {F_lat, X_cosLatCell, ::cos},
+            {F_lat, X_sinLatCell, ::sin},         {F_lon, X_cosLonCell, ::cos},      {F_lon, X_sinLonCell, ::sin}};
+        for (const auto& dv : der) {
+            if (dv.src != f) continue;
             std::vector<double> cs((size_t)n + 1, 0.0);
             const double* d = (const double*)buf.data();
-            for (int e = 0; e < n; e++) cs[e] = std::cos(d[e]);
-            cs[n] = std::cos(0.0);  // zero slot: cos(0) as the oracle computes from its zero row
-            hipcheck(hipMemcpy(c->S.f[derived], cs.data(), cs.size() * 8, hipMemcpyHostToDevice), "hipMemcpy H2D");
+            for (int e = 0; e < n; e++) cs[e] = dv.fn(d[e]);
+            cs[n] = dv.fn(0.0);  // zero slot: as the oracle computes it from its zero row
+            hipcheck(hipMemcpy(c->S.f[dv.dst], cs.data(), cs.size() * 8, hipMemcpyHostToDevice), "hipMemcpy H2D");
         }
     });
 }
@@ -634,6 +642,35 @@ int mpas_atm_compute_solve_diagnostics(mpas_ctx* c, int hollingsworth, int rk_st
 int mpas_atm_rk_dynamics_substep_finish(mpas_ctx* c, int substep, int split) {
     if (split == 0) return MPAS_EINVAL;
     MPAS_TASK("atm_rk_dynamics_substep_finish", launch_substep_finish(c->S, c->stream, substep, split));
+}
+
+int mpas_atm_recover_large_step_variables_work(mpas_ctx* c, int ns, int rk_step, double dt) {
+    if (ns == 0) return MPAS_EINVAL;
+    MPAS_TASK("atm_recover_large_step_variables_work", launch_recover_large_step(c->S, c->stream, ns, rk_step, dt));
+}
+int mpas_reconstruct_2d(mpas_ctx* c, int includeHalos, int on_a_sphere) {
+    (void)includeHalos;  // :1909-1912: the range is nCells either way
+    MPAS_TASK("mpas_reconstruct_2d", launch_reconstruct_2d(c->S, c->stream, on_a_sphere ? 1 : 0));
+}
+int mpas_summarize_timestep(mpas_ctx* c, int detailed, int global_vel, int global_sca, double* out) {
+    (void)global_sca;  // prints a blank line only (rk_timestep.rg:352-357)
+    return guarded(c, [&] {
+        if (!out) throw Fail{MPAS_EINVAL, "mpas_summarize_timestep: null out"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        double h[31] = {0};
+        if (detailed || global_vel) {
+            if (!c->sum_scratch) hipcheck(hipMalloc(&c->sum_scratch, summarize_scratch_bytes()), "hipMalloc");
+            if (!c->sum_out) hipcheck(hipMalloc((void**)&c->sum_out, 31 * sizeof(double)), "hipMalloc");
+            run_task(c, "summarize_timestep", [&] { return launch_summarize(c->S, c->stream, c->sum_scratch, c->sum_out); });
+            hipcheck(hipMemcpyAsync(h, c->sum_out, sizeof h, hipMemcpyDeviceToHost, c->stream), "hipMemcpy D2H");
+            hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+            if (!detailed)
+                for (int i = 0; i < 27; i++) h[i] = 0.0;
+            if (!global_vel)
+                for (int i = 27; i < 31; i++) h[i] = 0.0;
+        }
+        std::memcpy(out, h, sizeof h);
+    });
 }
 
 int mpas_atm_srk3(mpas_ctx* c, double dt, int schedule) {

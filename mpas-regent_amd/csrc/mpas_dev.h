@@ -29,6 +29,9 @@ enum FieldId {
     X_cosAngleEdge = F_COUNT,
     X_cosLatEdge,
     X_cosLatCell,
+    X_sinLatCell,  // (mpas_reconstruct_2d)
+    X_cosLonCell,
+    X_sinLonCell,
     // per-cell copies of edge data seen through edgesOnCell (mesh constants computed
     // on the device after upload, k_prepare): one indirection level less per gather
     X_ce_c1,    // cellsOnEdge(edgesOnCell(i,c), 0)      C2I x10
@@ -115,6 +118,10 @@ hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int holli
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
 hipError_t launch_prepare(DevState& S, hipStream_t st);
+hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt);
+hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
+size_t summarize_scratch_bytes();
+hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, double* out);
 
 // ---- device helpers ----
 #if defined(__HIPCC__)

@@ -240,6 +240,8 @@ def geometry(m, st):
     st["angleEdge"][:nE, 0] = m.angleEdge
     st["latEdge"][:nE, 0] = m.latEdge
     st["lat"][:nC, 0] = m.latCell
+    st["lonEdge"][:nE, 0] = m.lonEdge
+    st["lon"][:nC, 0] = m.lonCell
 
 
 MESH_FIELDS = tuple(f.name for f in FIELDS if f.dist == "M" or f.kind == "ZV")

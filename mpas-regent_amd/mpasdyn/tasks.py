@@ -74,6 +74,36 @@ def atm_rk_dynamics_substep_finish(ctx, dynamics_substep, dynamics_split):
                "atm_rk_dynamics_substep_finish")
 
 
+def atm_recover_large_step_variables_work(ctx, ns, rk_step, dt):
+    """dynamics_tasks.rg:1766 (not called by atm_srk3: rk_timestep.rg:460, Q7)"""
+    ctx._check(ctx.lib.mpas_atm_recover_large_step_variables_work(ctx.h, int(ns), int(rk_step), float(dt)),
+               "atm_recover_large_step_variables_work")
+
+
+atm_recover_large_step_variables = atm_recover_large_step_variables_work  # :1876 wrapper
+
+
+def mpas_reconstruct_2d(ctx, includeHalos=False, on_a_sphere=True):
+    """dynamics_tasks.rg:1893 (atm_core.rg:33 calls it with false, true)"""
+    ctx._check(ctx.lib.mpas_reconstruct_2d(ctx.h, int(bool(includeHalos)), int(bool(on_a_sphere))),
+               "mpas_reconstruct_2d")
+
+
+def summarize_timestep(ctx, config_print_detailed_minmax_vel=False, config_print_global_minmax_vel=False,
+                       config_print_global_minmax_sca=False):
+    """rk_timestep.rg:29; returns the 31 values the reference prints (layout: include/mpas_dyn.h)"""
+    import ctypes
+
+    import numpy as np
+    out = np.zeros(31)
+    ctx._check(ctx.lib.mpas_summarize_timestep(ctx.h, int(bool(config_print_detailed_minmax_vel)),
+                                               int(bool(config_print_global_minmax_vel)),
+                                               int(bool(config_print_global_minmax_sca)),
+                                               out.ctypes.data_as(ctypes.POINTER(ctypes.c_double))),
+               "summarize_timestep")
+    return out
+
+
 def atm_srk3(ctx, dt, schedule=0):
     """rk_timestep.rg:361; schedule 0 = the reference's driver, 1 = rk_step 0,1,2 into dyn_tend"""
     ctx._check(ctx.lib.mpas_atm_srk3(ctx.h, float(dt), int(schedule)), "atm_srk3")
@@ -89,4 +119,4 @@ def atm_do_timestep(ctx, dt):
     atm_timestep(ctx, dt)
 
 
-__all__ = [n for n in dir() if n.startswith("atm_")] + ["MpasError"]
+__all__ = [n for n in dir() if n.startswith("atm_")] + ["mpas_reconstruct_2d", "summarize_timestep", "MpasError"]

@@ -903,6 +903,200 @@ void ora_atm_rk_dynamics_substep_finish(ora_state* S, int dynamics_substep, int 
         }
 }
 
+
+/* ===================== atm_recover_large_step_variables_work, dynamics_tasks.rg:1766-1872
+ * Not called by atm_srk3 (Q7, rk_timestep.rg:460); restated for the operator API.
+ * Literal: Q24 (ru = ru_save * ru_p, flux2 = a * (b), the exner exponent placement);
+ * the level-0 flux term of the w recovery is added at EVERY level iteration of the cell
+ * (:1851-1854 write cr[{iCell.x, 0}].w inside the loop over all points), i.e. nVertLevels
+ * times; "{iCell, 0}" (:1856) is {iCell.x, 0} (Q22).  Every loop covers levels
+ * 0..nVertLevels-1.  The zero slot of rho_zz (the "garbage cell", :1790-1792) is set to
+ * 1.0 at those levels.                                                                  */
+void ora_atm_recover_large_step_variables_work(ora_state* S, int ns, int rk_step, double dt) {
+    const int L = S->L, nC = S->nCells, nE = S->nEdges;
+    const double rcv = rgas / (CP - rgas);
+    const int p0 = 100000;
+    double *rho_zz = D(rho_zz), *w = D(w), *ru = D(ru);
+    for (int k = 0; k < L; k++) CW(rho_zz, nC, k) = 1.0;
+    const double invNs = 1 / (double)ns;
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++)
+        for (int k = 0; k < L; k++) {
+            CW(D(rho_p), c, k) = CW(D(rho_p_save), c, k) + CW(D(rho_pp), c, k);
+            CW(rho_zz, c, k) = CW(D(rho_p), c, k) + CW(D(rho_base), c, k);
+            CW(w, c, k) = 0.0;
+            CW(D(wwAvg), c, k) *= invNs;
+            CW(D(wwAvg), c, k) += CW(D(rw_save), c, k);
+            CW(D(rw), c, k) = CW(D(rw_save), c, k) + CW(D(rw_p), c, k);
+            CW(w, c, k) = CW(D(rw), c, k) / (rz(S, D(fzm), k) * CW(D(zz), c, k) + rz(S, D(fzp), k) * rc(S, D(zz), c, k - 1));
+            if (k == L) CW(w, c, k) = 0.0;
+            if (rk_step == 2) {
+                CW(D(rtheta_p), c, k) = CW(D(rtheta_p_save), c, k) + CW(D(rtheta_pp), c, k) -
+                                        dt * CW(rho_zz, c, k) * CW(D(rt_diabatic_tend), c, k);
+                CW(D(theta_m), c, k) = (CW(D(rtheta_p), c, k) + CW(D(rtheta_base), c, k)) / CW(rho_zz, c, k);
+                CW(D(exner), c, k) = CW(D(zz), c, k) * (rgas / p0) * pow((CW(D(rtheta_p), c, k) + CW(D(rtheta_base), c, k)), rcv);
+                CW(D(pressure_p), c, k) = CW(D(zz), c, k) * rgas *
+                                          (CW(D(exner), c, k) * CW(D(rtheta_p), c, k) +
+                                           CW(D(rtheta_base), c, k) * (CW(D(exner), c, k) - CW(D(exner_base), c, k)));
+            } else {
+                CW(D(rtheta_p), c, k) = CW(D(rtheta_p_save), c, k) + CW(D(rtheta_pp), c, k);
+                CW(D(theta_m), c, k) = (CW(D(rtheta_p), c, k) + CW(D(rtheta_base), c, k)) / CW(rho_zz, c, k);
+            }
+        }
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        for (int k = 0; k < L; k++) {
+            CW(D(ruAvg), e, k) *= invNs;
+            CW(D(ruAvg), e, k) += CW(D(ru_save), e, k);
+            CW(ru, e, k) = CW(D(ru_save), e, k) * CW(D(ru_p), e, k);
+            CW(D(u), e, k) = 2 * CW(ru, e, k) / (rc(S, rho_zz, cell1, k) + rc(S, rho_zz, cell2, k));
+        }
+    }
+    const double cf1 = rz(S, D(cf1), 0), cf2 = rz(S, D(cf2), 0), cf3 = rz(S, D(cf3), 0);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        if (ic2(S, I(bdyMaskCell), c, 1, 0) > nRelaxZone) continue;
+        const int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int k = 0; k < L; k++)
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                double sg = rc2(S, D(edgesOnCell_sign), c, 10, i);
+                double flux = (cf1 * re(S, ru, iEdge, 0) + cf2 * re(S, ru, iEdge, 1) + cf3 * re(S, ru, iEdge, 2));
+                CW(w, c, 0) += sg * (rc3v(S, D(zb_cell), c, 0, i) + copysign(1.0, flux) * rc3v(S, D(zb3_cell), c, 0, i)) * flux;
+                double flux2 = rz(S, D(fzm), k) * re(S, ru, iEdge, k) * (rz(S, D(fzp), k) * re(S, ru, iEdge, k - 1));
+                CW(w, c, k) += sg * (rc3v(S, D(zb_cell), c, k, i) + copysign(1.0, flux2) * rc3v(S, D(zb3_cell), c, k, i)) * flux2;
+            }
+        for (int k = 0; k < L; k++) {
+            if (k == 0) CW(w, c, 0) /= (cf1 * CW(rho_zz, c, 0) + cf2 * rc(S, rho_zz, c, 1) + cf3 * rc(S, rho_zz, c, 2));
+            if (k > 0) CW(w, c, k) /= (rz(S, D(fzm), k) * CW(rho_zz, c, k) + rz(S, D(fzp), k) * CW(rho_zz, c, k - 1));
+        }
+    }
+}
+
+/* ===================== mpas_reconstruct_2d, dynamics_tasks.rg:1893-1948 (levels
+ * 0..nVertLevels-1 of every cell; includeHalos does not change the range there).   */
+void ora_mpas_reconstruct_2d(ora_state* S, int includeHalos, int on_a_sphere) {
+    const int L = S->L, nC = S->nCells;
+    (void)includeHalos;
+    double *X = D(uReconstructX), *Y = D(uReconstructY), *Z = D(uReconstructZ), *u = D(u);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        const int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int k = 0; k < L; k++) {
+            CW(X, c, k) = 0.0;
+            CW(Y, c, k) = 0.0;
+            CW(Z, c, k) = 0.0;
+        }
+        for (int k = 0; k < L; k++)
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                CW(X, c, k) += rc2(S, D(coeffs_reconstruct), c, 30, i * 3 + 0) * re(S, u, iEdge, k);
+                CW(Y, c, k) += rc2(S, D(coeffs_reconstruct), c, 30, i * 3 + 1) * re(S, u, iEdge, k);
+                CW(Z, c, k) += rc2(S, D(coeffs_reconstruct), c, 30, i * 3 + 2) * re(S, u, iEdge, k);
+            }
+        if (on_a_sphere) {
+            double clat = cos(rc2(S, D(lat), c, 1, 0)), slat = sin(rc2(S, D(lat), c, 1, 0));
+            double clon = cos(rc2(S, D(lon), c, 1, 0)), slon = sin(rc2(S, D(lon), c, 1, 0));
+            for (int k = 0; k < L; k++) {
+                CW(D(uReconstructZonal), c, k) = -CW(X, c, k) * slon + CW(Y, c, k) * clon;
+                CW(D(uReconstructMeridional), c, k) = -(CW(X, c, k) * clon + CW(Y, c, k) * slon) * slat + CW(Z, c, k) * clat;
+            }
+        } else {
+            for (int k = 0; k < L; k++) {
+                CW(D(uReconstructZonal), c, k) = CW(X, c, k);
+                CW(D(uReconstructMeridional), c, k) = CW(Y, c, k);
+            }
+        }
+    }
+}
+
+/* ===================== summarize_timestep, rk_timestep.rg:29-359: the values the
+ * reference prints.  out[0..24]: five records {value, index, k, lat_deg, lon_deg} for
+ * min w, max w, min u, max u, max wind speed (first point in cell-major, level-minor
+ * order; comparisons strict against the 1e20 / -1e20 start; the lat/lon of the max
+ * records are read at level k, i.e. 0.0 for k > 0 (2-D data at level > 0, Q2)); out[25],
+ * out[26]: NaN seen in w, u; out[27..30]: the fold min/max of w and of u from 0.0
+ * (regentlib min/max, a < b ? a : b).  detailed / global_vel select the two blocks
+ * (the reference tests constants.config_print_detailed_minmax_vel for the first and its
+ * argument for the second; both are false on the path, rk_timestep.rg:492).         */
+static void ora_rec(double* r, double val, long idx, long k, double lat, double lon) {
+    const double pi_const = 2.0 * asin(1.0);
+    r[0] = val;
+    r[1] = (double)idx;
+    r[2] = (double)k;
+    double la = lat * (180.0 / pi_const), lo = lon * (180.0 / pi_const);
+    if (lo > 180.0) lo -= 360.0;
+    r[3] = la;
+    r[4] = lo;
+}
+void ora_summarize_timestep(ora_state* S, int detailed, int global_vel, double* out) {
+    const int L = S->L, nC = S->nCells, nE = S->nEdges;
+    double *w = D(w), *u = D(u), *v = D(v), *latc = D(lat), *lonc = D(lon), *late = D(latEdge), *lone = D(lonEdge);
+    for (int i = 0; i < 31; i++) out[i] = 0.0;
+    if (detailed) {
+        double mn = 1.0e20, mx = -1.0e20, la = 0, lo = 0, la2 = 0, lo2 = 0;
+        long im = -1, km = -1, ix = -1, kx = -1;
+        for (long c = 0; c < nC; c++)
+            for (int k = 0; k < L; k++) {
+                double x = CW(w, c, k);
+                if (x < mn) { mn = x; im = c; km = k; la = latc[c]; lo = lonc[c]; }
+            }
+        for (long c = 0; c < nC; c++)
+            for (int k = 0; k < L; k++) {
+                double x = CW(w, c, k);
+                if (x > mx) { mx = x; ix = c; kx = k; la2 = k == 0 ? latc[c] : 0.0; lo2 = k == 0 ? lonc[c] : 0.0; }
+            }
+        ora_rec(out + 0, mn, im, km, la, lo);
+        ora_rec(out + 5, mx, ix, kx, la2, lo2);
+        mn = 1.0e20; mx = -1.0e20; im = km = ix = kx = -1; la = lo = la2 = lo2 = 0;
+        for (long e = 0; e < nE; e++)
+            for (int k = 0; k < L; k++) {
+                double x = CW(u, e, k);
+                if (x < mn) { mn = x; im = e; km = k; la = late[e]; lo = lone[e]; }
+            }
+        for (long e = 0; e < nE; e++)
+            for (int k = 0; k < L; k++) {
+                double x = CW(u, e, k);
+                if (x > mx) { mx = x; ix = e; kx = k; la2 = k == 0 ? late[e] : 0.0; lo2 = k == 0 ? lone[e] : 0.0; }
+            }
+        ora_rec(out + 10, mn, im, km, la, lo);
+        ora_rec(out + 15, mx, ix, kx, la2, lo2);
+        mx = -1.0e20; ix = kx = -1; la = lo = 0;
+        for (long e = 0; e < nE; e++)
+            for (int k = 0; k < L; k++) {
+                double spd = sqrt(CW(u, e, k) * CW(u, e, k) + CW(v, e, k) * CW(v, e, k));
+                if (spd > mx) { mx = spd; ix = e; kx = k; la = late[e]; lo = lone[e]; }
+            }
+        ora_rec(out + 20, mx, ix, kx, la, lo);
+        for (long c = 0; c < nC; c++)
+            for (int k = 0; k < L; k++)
+                if (isnan(CW(w, c, k))) out[25] = 1.0;
+        for (long e = 0; e < nE; e++)
+            for (int k = 0; k < L; k++)
+                if (isnan(CW(u, e, k))) out[26] = 1.0;
+    }
+    if (global_vel) {
+        double mn = 0.0, mx = 0.0;
+        for (long c = 0; c < nC; c++)
+            for (int k = 0; k < L; k++) {
+                mn = dmin(mn, CW(w, c, k));
+                mx = dmax(mx, CW(w, c, k));
+            }
+        out[27] = mn;
+        out[28] = mx;
+        mn = 0.0;
+        mx = 0.0;
+        for (long e = 0; e < nE; e++)
+            for (int k = 0; k < L; k++) {
+                mn = dmin(mn, CW(u, e, k));
+                mx = dmax(mx, CW(u, e, k));
+            }
+        out[29] = mn;
+        out[30] = mx;
+    }
+}
+
 /* ===================== atm_srk3, rk_timestep.rg:361-500
  * schedule 0: the reference's own driver, with Q4 (rk_sub_timestep[rk_step] truncated
  *             into dyn_tend's int rk_step) and Q5 (n+1 acoustic substeps);

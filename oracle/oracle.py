@@ -51,6 +51,9 @@ def load():
             "ora_atm_compute_solve_diagnostics": (None, [p, i32, i32]),
             "ora_atm_rk_dynamics_substep_finish": (None, [p, i32, i32]),
             "ora_atm_srk3": (None, [p, dbl, i32]),
+            "ora_atm_recover_large_step_variables_work": (None, [p, i32, i32, dbl]),
+            "ora_mpas_reconstruct_2d": (None, [p, i32, i32]),
+            "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
         }
         for n, (res, args) in sig.items():
             fn = getattr(L, n)
@@ -111,3 +114,17 @@ class Oracle:
 
     def atm_srk3(self, dt, schedule=0):
         self.lib.ora_atm_srk3(self.p, dt, schedule)
+
+    def atm_recover_large_step_variables_work(self, ns, rk_step, dt):
+        self.lib.ora_atm_recover_large_step_variables_work(self.p, ns, rk_step, dt)
+
+    def mpas_reconstruct_2d(self, includeHalos=False, on_a_sphere=True):
+        self.lib.ora_mpas_reconstruct_2d(self.p, int(includeHalos), int(on_a_sphere))
+
+    def summarize_timestep(self, config_print_detailed_minmax_vel=True, config_print_global_minmax_vel=True):
+        """the 31 values the reference prints (layout: mpas_oracle.c ora_summarize_timestep)"""
+        out = np.zeros(31)
+        self.lib.ora_summarize_timestep(self.p, int(config_print_detailed_minmax_vel),
+                                        int(config_print_global_minmax_vel),
+                                        out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        return out

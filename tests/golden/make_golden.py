@@ -31,6 +31,9 @@ CASES = {
     "finish": lambda o: o.atm_rk_dynamics_substep_finish(1, 1),
     "srk3_ref_schedule": lambda o: o.atm_srk3(720.0, 0),
     "srk3_mpas_schedule": lambda o: o.atm_srk3(720.0, 1),
+    "recover_ns2_rk0": lambda o: o.atm_recover_large_step_variables_work(2, 0, 240.0),
+    "recover_ns3_rk2": lambda o: o.atm_recover_large_step_variables_work(3, 2, 240.0),
+    "reconstruct_2d": lambda o: o.mpas_reconstruct_2d(False, True),
 }
 
 
@@ -47,6 +50,7 @@ def generate():
                 fn(O.Oracle(st))
                 out[key][case] = {f.name: digest(st[f.name]) for f in FIELDS
                                   if f.name not in SCRATCH and st[f.name].tobytes() != st0[f.name].tobytes()}
+            out[key]["summarize_timestep"] = digest(O.Oracle(st0.copy()).summarize_timestep(True, True))
     return out
 
 

@@ -176,3 +176,76 @@ def test_self_gathers_identical(x1_2562):
     bad = compare_states(outs[0], outs[1], rtol=0.0)
     assert not bad, f"SELF on/off differ: {bad[:6]}"
 
+
+
+# ---- operators beside the RK3 loop (not run by atm_srk3) ------------------------------
+RTOL_POW = 1e-14  # exner/pressure_p go through pow (device libm vs glibc: a few ulp)
+POW_FIELDS = {"exner", "pressure_p"}
+
+
+@pytest.mark.parametrize("L", [5, 56])
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
+@pytest.mark.parametrize("ns,rk_step", [(1, 0), (2, 1), (3, 2)])
+def test_recover_large_step(x1_2562, L, variant, ns, rk_step):
+    """dynamics_tasks.rg:1766-1872, Q24 literal; the garbage-cell rho_zz = 1.0 lands in
+    the zero slot exactly as in the oracle"""
+    st = base_state(x1_2562, L, variant)
+    ref = run_oracle(st, lambda o: o.atm_recover_large_step_variables_work(ns, rk_step, 240.0))
+    n = st.nCells
+    # downloads cover the n entities, not the zero slot: the device's zero-slot rho_zz is
+    # checked through u, which reads it at every edge whose (raw) cellsOnEdge is n
+    assert variant == "mpas0" or (st["cellsOnEdge"][:st.nEdges] == n).any()
+    for exact in (1, 0):
+        got = run_gpu(st, lambda c: T.atm_recover_large_step_variables_work(c, ns, rk_step, 240.0), exact=exact)
+        got["rho_zz"][n] = ref["rho_zz"][n]
+        bad = compare_states(got, ref, rtol=RTOL_POW, tol_fields=POW_FIELDS)
+        assert not bad, f"recover ns={ns} rk={rk_step}: {bad[:6]}"
+        got.check_zero_slots(written=("rho_zz",))
+    assert (ref["rho_zz"][st.nCells, :L] == 1.0).all()
+
+
+@pytest.mark.parametrize("L", [5, 56])
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
+@pytest.mark.parametrize("on_a_sphere", [True, False])
+def test_reconstruct_2d(x1_2562, L, variant, on_a_sphere):
+    """dynamics_tasks.rg:1893-1948: value-identical (cos/sin of lat/lon from the host libm)"""
+    st = base_state(x1_2562, L, variant)
+    ref = run_oracle(st, lambda o: o.mpas_reconstruct_2d(False, on_a_sphere))
+    got = run_gpu(st, lambda c: T.mpas_reconstruct_2d(c, False, on_a_sphere), exact=0)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, f"reconstruct_2d: {bad[:6]}"
+    got.check_zero_slots()
+
+
+def _summary_gpu(st, detailed, global_vel):
+    with lib.Context(*st.dims()) as ctx:
+        ctx.upload(st)
+        out = T.summarize_timestep(ctx, detailed, global_vel)
+    return out
+
+
+@pytest.mark.parametrize("L", [5, 56])
+@pytest.mark.parametrize("case", ["random", "ref", "nan", "ties"])
+def test_summarize_timestep(x1_2562, L, case):
+    """rk_timestep.rg:29-359: the printed values, bit-identical.  "nan" puts NaNs into w
+    and u (the regentlib min/max fold restarts after the last NaN; the first-extreme
+    search skips them); "ties" makes the extremes occur many times (first point wins in
+    the detailed search, the later point in the fold)."""
+    st = base_state(x1_2562, L, "ref" if case == "ref" else "random").copy()
+    nC, nE = st.nCells, st.nEdges
+    if case == "nan":
+        rng = np.random.default_rng(1)
+        for name, n in (("w", nC), ("u", nE)):
+            a = st[name]
+            for _ in range(5):
+                a[rng.integers(n), rng.integers(L)] = np.nan
+    if case == "ties":
+        st["w"][:nC, :L] = np.round(st["w"][:nC, :L] * 2.0) / 2.0
+        st["u"][:nE, :L] = np.round(st["u"][:nE, :L] / 20.0) * 20.0
+        st["w"][7, 0] = -0.0
+    for detailed, global_vel in ((1, 1), (1, 0), (0, 1), (0, 0)):
+        ref = O.Oracle(st.copy()).summarize_timestep(detailed, global_vel)
+        got = _summary_gpu(st, detailed, global_vel)
+        assert np.array_equal(np.isnan(got), np.isnan(ref)), (detailed, global_vel)
+        ok = np.where(np.isnan(ref), True, (got == ref) & (np.signbit(got) == np.signbit(ref)))
+        assert ok.all(), f"summarize {case} {detailed}{global_vel}: {np.nonzero(~ok)[0]} {got[~ok]} vs {ref[~ok]}"

@@ -49,6 +49,8 @@ def test_oracle_golden(x1_2562, golden, L, variant):
         assert changed == set(g), f"{case}: written field set differs: {changed ^ set(g)}"
         for name in changed:
             _check(digest(st[name]), g[name], f"{case}/{name}")
+    _check(digest(O.Oracle(st0.copy()).summarize_timestep(True, True)), golden[f"L{L}_{variant}"]["summarize_timestep"],
+           "summarize_timestep")
 
 
 def test_oracle_thread_invariance(x1_2562, tmp_path):
@@ -187,3 +189,142 @@ def test_numpy_restatement_div_damping(x1_2562):
         new = ref["ru_p"][:nE, k] + coef * (d2 - d1) * (1.0 - ref["specZoneMaskEdge"][:nE, 0]) / \
             (ref["theta_m"][c1, k] + ref["theta_m"][c2, k])
         assert np.array_equal(st["ru_p"][:nE, k], np.where(on, new, ref["ru_p"][:nE, k]))
+
+
+def test_numpy_restatement_reconstruct_2d(x1_2562):
+    """dynamics_tasks.rg:1913-1947 restated with numpy (on a sphere and not)"""
+    for sphere in (True, False):
+        st = make_state(x1_2562, 5, "random")
+        ref = st.copy()
+        O.Oracle(st).mpas_reconstruct_2d(False, sphere)
+        n, L = st.nCells, st.L
+        ne = ref["nEdgesOnCell"][:n, 0]
+        co = ref["coeffs_reconstruct"][:n].reshape(n, 10, 3)
+        for k in range(L):
+            X, Y, Z = np.zeros(n), np.zeros(n), np.zeros(n)
+            for i in range(10):
+                ue = ref["u"][ref["edgesOnCell"][:n, i], k]
+                X = np.where(i < ne, X + co[:, i, 0] * ue, X)
+                Y = np.where(i < ne, Y + co[:, i, 1] * ue, Y)
+                Z = np.where(i < ne, Z + co[:, i, 2] * ue, Z)
+            assert np.array_equal(st["uReconstructX"][:n, k], X)
+            assert np.array_equal(st["uReconstructZ"][:n, k], Z)
+            lat, lon = ref["lat"][:n, 0], ref["lon"][:n, 0]
+            if sphere:
+                zon = -X * np.sin(lon) + Y * np.cos(lon)
+                mer = -(X * np.cos(lon) + Y * np.sin(lon)) * np.sin(lat) + Z * np.cos(lat)
+            else:
+                zon, mer = X, Y
+            # numpy's sin/cos may differ from glibc's in the last ulp: compare to 1e-14
+            assert np.allclose(st["uReconstructZonal"][:n, k], zon, rtol=1e-14, atol=1e-12)
+            assert np.allclose(st["uReconstructMeridional"][:n, k], mer, rtol=1e-14, atol=1e-12)
+        assert (st["uReconstructX"][:n, L] == ref["uReconstructX"][:n, L]).all()  # level L untouched
+
+
+def test_restatement_recover_large_step(x1_2562):
+    """dynamics_tasks.rg:1788-1870 restated with numpy (loops 1-2) and plain Python for the
+    w recovery of the first 40 cells (the level-0 term added once per level iteration)"""
+    for rk_step, ns in ((0, 2), (2, 3)):
+        st = make_state(x1_2562, 5, "random")
+        ref = st.copy()
+        dt = 240.0
+        O.Oracle(st).atm_recover_large_step_variables_work(ns, rk_step, dt)
+        n, nE, L = st.nCells, st.nEdges, st.L
+        C = lambda nm: ref[nm][:n, :L]  # noqa: E731
+        rho_zz = C("rho_p_save") + C("rho_pp") + C("rho_base")
+        assert np.array_equal(st["rho_zz"][:n, :L], rho_zz)
+        assert (st["rho_zz"][n, :L] == 1.0).all()
+        ww = C("wwAvg") * (1 / ns) + C("rw_save")
+        assert np.array_equal(st["wwAvg"][:n, :L], ww)
+        zz = ref["zz"][:n]
+        zz_m = np.concatenate([np.zeros((n, 1)), zz[:, :L - 1]], axis=1)
+        w1 = (C("rw_save") + C("rw_p")) / (ref["fzm"][:L] * zz[:, :L] + ref["fzp"][:L] * zz_m)
+        if rk_step == 2:
+            rtp = C("rtheta_p_save") + C("rtheta_pp") - dt * rho_zz * C("rt_diabatic_tend")
+            ex = zz[:, :L] * (287.0 / 100000) * np.power(rtp + C("rtheta_base"), 287.0 / (3.5 * 287.0 - 287.0))
+            assert np.allclose(st["exner"][:n, :L], ex, rtol=1e-14, atol=0)
+        else:
+            rtp = C("rtheta_p_save") + C("rtheta_pp")
+        assert np.array_equal(st["rtheta_p"][:n, :L], rtp)
+        assert np.array_equal(st["theta_m"][:n, :L], (rtp + C("rtheta_base")) / rho_zz)
+        rz_full = st["rho_zz"]
+        c1, c2 = ref["cellsOnEdge"][:nE, 0], ref["cellsOnEdge"][:nE, 1]
+        ru = ref["ru_save"][:nE, :L] * ref["ru_p"][:nE, :L]
+        assert np.array_equal(st["ru"][:nE, :L], ru)
+        assert np.array_equal(st["u"][:nE, :L], 2 * ru / (rz_full[c1, :L] + rz_full[c2, :L]))
+        cf1, cf2, cf3 = ref["cf1"][0], ref["cf2"][0], ref["cf3"][0]
+        fzm, fzp = ref["fzm"], ref["fzp"]
+        for c in range(40):
+            if ref["bdyMaskCell"][c, 0] > 5:
+                assert np.array_equal(st["w"][c, :L], w1[c])
+                continue
+            w = list(w1[c])
+            for k in range(L):
+                for i in range(ref["nEdgesOnCell"][c, 0]):
+                    e = ref["edgesOnCell"][c, i]
+                    sg = ref["edgesOnCell_sign"][c, i]
+                    r = st["ru"][e]
+                    flux = (cf1 * r[0] + cf2 * r[1] + cf3 * r[2])
+                    w[0] += sg * (ref["zb_cell"][c, 0, i] + np.copysign(1.0, flux) * ref["zb3_cell"][c, 0, i]) * flux
+                    flux2 = fzm[k] * r[k] * (fzp[k] * (r[k - 1] if k > 0 else 0.0))
+                    w[k] += sg * (ref["zb_cell"][c, k, i] + np.copysign(1.0, flux2) * ref["zb3_cell"][c, k, i]) * flux2
+            rz = st["rho_zz"][c]
+            w[0] /= (cf1 * rz[0] + cf2 * rz[1] + cf3 * rz[2])
+            for k in range(1, L):
+                w[k] /= (fzm[k] * rz[k] + fzp[k] * rz[k - 1])
+            assert np.array_equal(st["w"][c, :L], np.array(w)), c
+
+
+def _summary_python(st):
+    """rk_timestep.rg:54-350 as plain Python loops (the literal sequential semantics)"""
+    import math
+    n, nE, L = st.nCells, st.nEdges, st.L
+    w, u, v = st["w"], st["u"], st["v"]
+    lat, lon, late, lone = st["lat"][:, 0], st["lon"][:, 0], st["latEdge"][:, 0], st["lonEdge"][:, 0]
+    pi_const = 2.0 * math.asin(1.0)
+
+    def rec(val, idx, k, la, lo):
+        la *= 180.0 / pi_const
+        lo *= 180.0 / pi_const
+        if lo > 180.0:
+            lo -= 360.0
+        return [val, float(idx), float(k), la, lo]
+
+    def search(a, m, latf, lonf, better, start, level_k):
+        best, ib, kb, la, lo = start, -1, -1, 0.0, 0.0
+        for i in range(m):
+            for k in range(L):
+                if better(a(i, k), best):
+                    best, ib, kb = a(i, k), i, k
+                    la, lo = (latf[i], lonf[i]) if (not level_k or k == 0) else (0.0, 0.0)
+        return rec(best, ib, kb, la, lo)
+
+    out = []
+    out += search(lambda i, k: w[i, k], n, lat, lon, lambda x, b: x < b, 1.0e20, False)
+    out += search(lambda i, k: w[i, k], n, lat, lon, lambda x, b: x > b, -1.0e20, True)
+    out += search(lambda i, k: u[i, k], nE, late, lone, lambda x, b: x < b, 1.0e20, False)
+    out += search(lambda i, k: u[i, k], nE, late, lone, lambda x, b: x > b, -1.0e20, True)
+    out += search(lambda i, k: math.sqrt(u[i, k] * u[i, k] + v[i, k] * v[i, k]), nE, late, lone,
+                  lambda x, b: x > b, -1.0e20, False)
+    out += [float(np.isnan(w[:n, :L]).any()), float(np.isnan(u[:nE, :L]).any())]
+    for a, m in ((w, n), (u, nE)):
+        mn = mx = 0.0
+        for i in range(m):
+            for k in range(L):
+                mn = mn if mn < a[i, k] else a[i, k]
+                mx = mx if mx > a[i, k] else a[i, k]
+        out += [mn, mx]
+    return np.array(out)
+
+
+@pytest.mark.parametrize("case", ["random", "nan"])
+def test_restatement_summarize_timestep(x1_2562, case):
+    st = make_state(x1_2562, 5, "random")
+    if case == "nan":
+        st["w"][100, 2] = np.nan
+        st["u"][7000, 4] = np.nan
+        st["u"][30, 1] = np.nan
+    got = O.Oracle(st).summarize_timestep(True, True)
+    ref = _summary_python(st)
+    assert np.array_equal(np.isnan(got), np.isnan(ref))
+    assert np.array_equal(np.where(np.isnan(ref), 0, got), np.where(np.isnan(ref), 0, ref))

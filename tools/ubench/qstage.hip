@@ -200,6 +200,63 @@ __global__ __launch_bounds__(TB) void qv4(const double* u, const double* pv, con
     }
 }
 
+
+// LDS staging with lane = level (full 56-level rows), a bounded LDS image of MAXU rows
+// per field and a per-edge fallback: an edge whose neighbours are not all staged
+// (lslot == 255) gathers them from global memory.  Slots come through the scalar unit.
+template <int E, int MAXU>
+__global__ __launch_bounds__(256) void qv5(const double* u, const double* pv, const int* eoe, const double* w, int nE,
+                                           double* out, const int* blk_off, const int* blk_n, const int* ulist,
+                                           const uint8_t* lslot) {
+    __shared__ double su[MAXU * 56];
+    __shared__ double sv[MAXU * 56];
+    const int b = blockIdx.x;
+    const int off = blk_off[b], n = min(blk_n[b], MAXU);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int k = threadIdx.x & 63;
+    for (int s0 = wv; s0 < n; s0 += 32) {
+        double a[8], c[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const int s = min(s0 + 4 * r, n - 1);
+            const int g = __builtin_amdgcn_readfirstlane(ulist[off + s]);
+            a[r] = sp(u + (size_t)g * 64)[k];
+            c[r] = sp(pv + (size_t)g * 64)[k];
+        }
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const int s = s0 + 4 * r;
+            if (s < n && k < 56) {
+                su[s * 56 + k] = a[r];
+                sv[s * 56 + k] = c[r];
+            }
+        }
+    }
+    __syncthreads();
+    if (k >= 56) return;
+    for (int i = 0; i < E / 4; i++) {
+        const int e = __builtin_amdgcn_readfirstlane(b * E + i * 4 + wv);
+        if (e >= nE) return;
+        const uint8_t* ls = lslot + (size_t)e * 11;  // 10 neighbours + the edge itself
+        uint32_t sl[11];
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 11; j++) {
+            sl[j] = ls[j];
+            ok = ok && sl[j] != 255u;
+        }
+        if (ok) {
+            const double p0 = sv[sl[10] * 56 + k];
+            double q = 0;
+#pragma unroll
+            for (int j = 0; j < 10; j++) q += w[e * 10 + j] * su[sl[j] * 56 + k] * 0.5 * (p0 + sv[sl[j] * 56 + k]);
+            sp(out + (size_t)e * 64)[k] = q;
+        } else {
+            q_edge(e, k, u, pv, eoe, w, out);
+        }
+    }
+}
+
 extern "C" int ub_q(int variant, const double* u, const double* pv, const int* eoe, const double* w, int nE,
                     double* out, const int* blk_off, const int* blk_n, const int* ulist, const uint16_t* lidx,
                     const uint16_t* lself, void* stream) {
@@ -229,6 +286,9 @@ extern "C" int ub_q(int variant, const double* u, const double* pv, const int* e
         case 21: qv4<32, 512, 160><<<((nE + 31) / 32) * 4, 512, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, lidx, lself, 4); break;
         case 22: qv4<64, 1024, 240><<<((nE + 63) / 64) * 4, 1024, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, lidx, lself, 4); break;
         case 23: qv4<64, 256, 240><<<((nE + 63) / 64) * 4, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, lidx, lself, 4); break;
+        case 24: qv5<16, 64><<<(nE + 15) / 16, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
+        case 25: qv5<16, 48><<<(nE + 15) / 16, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
+        case 26: qv5<32, 96><<<(nE + 31) / 32, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
         default: return -1;
     }
     return (int)hipGetLastError();

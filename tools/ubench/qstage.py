@@ -63,10 +63,18 @@ def main():
         assert cnt.max() <= maxu, (E, cnt.max())
         lists[E] = [torch.from_numpy(x).to(dev) for x in (off, cnt, ul, lidx.astype(np.int16).ravel(),
                                                          lself.astype(np.int16))] + [int(cnt.max()), float(cnt.mean())]
+    # qv5 slot tables: per edge 10 neighbour slots + its own, 255 = not staged (slot >= MAXU)
+    for E, maxu in ((16, 64), (16, 48), (32, 96)):
+        off, cnt, ul, lidx, lself = staging_lists(eoe, nE, E)
+        sl = np.concatenate([lidx, lself[:, None]], axis=1).astype(np.int64)
+        sl = np.where(sl >= maxu, 255, sl).astype(np.uint8)
+        lists[(E, maxu)] = [torch.from_numpy(x).to(dev) for x in (off, cnt, ul, sl.ravel())] + [None, int(cnt.max()),
+                                                                                             float(cnt.mean())]
+        lists[(E, maxu)].append(float((sl == 255).any(axis=1).mean()))
     res = {}
     ref = None
-    vars_ = [int(x) for x in os.environ.get('QVARS', '0,1,16,19,20,21,22,23').split(',')]
-    for var, E in [(v, {4: 32, 5: 32, 20: 32, 21: 32, 22: 64, 23: 64}.get(v, 16)) for v in vars_]:
+    vars_ = [int(x) for x in os.environ.get('QVARS', '0,1,16,21,24,25,26').split(',')]
+    for var, E in [(v, {4: 32, 5: 32, 20: 32, 21: 32, 22: 64, 23: 64, 24: (16, 64), 25: (16, 48), 26: (32, 96)}.get(v, 16)) for v in vars_]:
         L = lists[E]
         out = torch.zeros((nE + 1) * 64, dtype=torch.float64, device=dev)
         ts = []
@@ -75,7 +83,8 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             rc = lib.ub_q(var, u.data_ptr(), pv.data_ptr(), eoe_d.data_ptr(), w.data_ptr(), nE, out.data_ptr(),
-                          L[0].data_ptr(), L[1].data_ptr(), L[2].data_ptr(), L[3].data_ptr(), L[4].data_ptr(), st_)
+                          L[0].data_ptr(), L[1].data_ptr(), L[2].data_ptr(), L[3].data_ptr(),
+                          L[4].data_ptr() if L[4] is not None else 0, st_)
             e1.record()
             torch.cuda.synchronize()
             assert rc == 0, rc
@@ -86,7 +95,8 @@ def main():
             ref = o.clone()  # the first variant listed is the reference
         same = bool(torch.equal(o, ref))
         res[f"v{var}"] = {"ms": round(t, 4), "same_as_first": same, "E": E if var >= 4 else None,
-                          "union_mean": L[6] if var >= 4 else None, "union_max": L[5] if var >= 4 else None}
+                          "union_mean": L[6] if var >= 4 else None, "union_max": L[5] if var >= 4 else None,
+                          "fallback_frac": L[7] if len(L) > 7 else None}
     print(json.dumps(res, indent=1))
 
 
