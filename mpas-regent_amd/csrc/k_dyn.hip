@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const double rw1 = ldz(live, colk(fd(S, F_rw), cell1)), rw2 = ldz(live, colk(fd(S, F_rw), cell2));
     const double w1 = ldz(live, colk(fd(S, F_w), cell1)), w2 = ldz(live, colk(fd(S, F_w), cell2));
     const double rho_edge = ldz(live, colk(fd(S, F_rho_edge), e));
-    const double wduzL = ldz((k == L), colk(fd(S, F_wduz), e));
+    const double wduzL = fd(S, F_wduz)[(size_t)e * LP + L];  // one value: the level-L slot
     const int neoe = fi(S, F_nEdgesOnEdge)[e];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
@@ -341,17 +341,17 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)vx * 3;
         const double* sgn = fd(S, F_edgesOnVertex_sign) + (size_t)vx * 3;
         const double iat = fd(S, F_invAreaTriangle)[vx];
-        const double* dcEdge = fd(S, F_dcEdge);
         int ev[3];
-        double d[3];
-#pragma unroll
-        for (int i = 0; i < 3; i++) ev[i] = eov[i];
+        double d[3], sg_[3], dc_[3];
+        row_ld(eov, ev);
+        row_ld(sgn, sg_);
+        row_ld(fd(S, X_ve_dc) + (size_t)vx * 3, dc_);  // dcEdge(edgesOnVertex)
 #pragma unroll
         for (int i = 0; i < 3; i++) d[i] = dsu[(size_t)ev[i] * LP + k];
         double dsv = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; i++) {
-            double edge_sign = iat * dcEdge[ev[i]] * sgn[i];
+            double edge_sign = iat * dc_[i] * sg_[i];
             dsv += edge_sign * d[i];
         }
         colk(fw(S, F_delsq_vorticity), vx) = dsv;
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
         row_ld(cmsd4, cmsd4_);
     }
     const double ts_c = (SELF && !rk0) ? colk(tms_f, c) : 0.0;
-    const double dw_c = (SELF && del4) ? colk(dw, c) : 0.0, dt_c = (SELF && del4) ? colk(dth, c) : 0.0;
+    const double dw_c = (SELF && rk0) ? colk(dw, c) : 0.0, dt_c = (SELF && rk0) ? colk(dth, c) : 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         ru_[i] = ldz(kl, colk(ru, e_[i]));
@@ -531,19 +531,18 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
             ts1_[i] = ldz(kl, ts1_[i]);
             ts2_[i] = ldz(kl, ts2_[i]);
         }
-        if (del4) {
+        if (rk0) {  // (compile-time: a runtime `if (del4)` here would put each slot's loads in a branch)
             cell_pair<LP, SELF>(dw, c1_[i], c2_[i], o_[i], s1_[i], dw_c, k, dw1_[i], dw2_[i]);
             cell_pair<LP, SELF>(dth, c1_[i], c2_[i], o_[i], s1_[i], dt_c, k, dt1_[i], dt2_[i]);
-            dw1_[i] = ldz(kl, dw1_[i]);
-            dw2_[i] = ldz(kl, dw2_[i]);
-            dt1_[i] = ldz(kl, dt1_[i]);
-            dt2_[i] = ldz(kl, dt2_[i]);
+            dw1_[i] = ldz(kl && del4, dw1_[i]);
+            dw2_[i] = ldz(kl && del4, dw2_[i]);
+            dt1_[i] = ldz(kl && del4, dt1_[i]);
+            dt2_[i] = ldz(kl && del4, dt2_[i]);
         }
     }
     const double wc = ldz(kl, colk(fd(S, X_wc), c));
     const double rw = col_rd<LP>(fd(S, F_rw), c, k, L);
-    const double wdwzL = ldz((k == L), colk(fd(S, F_wdwz), c));
-    const double wdtzL = ldz((k == L), colk(fd(S, F_wdtz), c));
+    const double wdwzL = fd(S, F_wdwz)[(size_t)c * LP + L], wdtzL = fd(S, F_wdtz)[(size_t)c * LP + L];  // level-L slots
     const double pp = col_rd<LP>(fd(S, F_pressure_p), c, k, L), dpdz = col_rd<LP>(fd(S, F_dpdz), c, k, L);
     const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L);
     const double tms = col_rd<LP>(tms_f, c, k, L), tmv = col_rd<LP>(tm, c, k, L);

@@ -294,6 +294,8 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
     const size_t n = (size_t)S.nCells * 10;
     const int* eoc = fi(S, F_edgesOnCell);
     const int* coe = fi(S, F_cellsOnEdge);
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.nVertices * 3; t += (size_t)gridDim.x * 256)
+        fw(S, X_ve_dc)[t] = fd(S, F_dcEdge)[fi(S, F_edgesOnVertex)[t]];
     for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (size_t)gridDim.x * 256) {
         const int e = eoc[t], c = (int)(t / 10), i = (int)(t % 10);
         const int c1 = coe[(size_t)e * 2], c2 = coe[(size_t)e * 2 + 1];
@@ -303,6 +305,7 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
         ((int*)S.f[X_ce_s1])[t] = (c1 == c) ? 1 : 0;
         if (c < S.nCO && i < fi(S, F_nEdgesOnCell)[c] && i < NF && c1 != c && c2 != c) atomicAnd(selfc, 0);
         fw(S, X_ce_dv)[t] = fd(S, F_dvEdge)[e];
+        fw(S, X_ce_dc)[t] = fd(S, F_dcEdge)[e];
         fw(S, X_ce_idc)[t] = fd(S, F_invDcEdge)[e];
         fw(S, X_ce_msd2)[t] = fd(S, F_meshScalingDel2)[e];
         fw(S, X_ce_msd4)[t] = fd(S, F_meshScalingDel4)[e];

@@ -23,11 +23,18 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         if (v >= S.nVO || k >= L) return;
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)v * 3;
         const double* sgn = fd(S, F_edgesOnVertexSign) + (size_t)v * 3;
+        int ev[3];
+        double sg_[3], dc_[3], u_[3];
+        row_ld(eov, ev);
+        row_ld(sgn, sg_);
+        row_ld(fd(S, X_ve_dc) + (size_t)v * 3, dc_);  // dcEdge(edgesOnVertex)
+#pragma unroll
+        for (int i = 0; i < 3; i++) u_[i] = colk(u, ev[i]);
         double vort = 0.0;
+#pragma unroll
         for (int i = 0; i < 3; i++) {
-            int iEdge = eov[i];
-            double s = sgn[i] * dcEdge[iEdge];
-            vort += s * colk(u, iEdge);
+            double s = sg_[i] * dc_[i];
+            vort += s * u_[i];
         }
         vort *= fd(S, F_invAreaTriangle)[v];
         const size_t p = (size_t)v * LP + k;
@@ -61,11 +68,9 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     row_ld(eoc, e_);
     row_ld(sgn, sgn_);
     row_ld(fd(S, X_ce_dv) + (size_t)c * 10, dv_);  // dvEdge(edgesOnCell)
+    row_ld(fd(S, X_ce_dc) + (size_t)c * 10, dc_);  // dcEdge(edgesOnCell)
 #pragma unroll
-    for (int i = 0; i < NF; i++) {
-        u_[i] = colk(u, e_[i]);
-        dc_[i] = dcEdge[e_[i]];
-    }
+    for (int i = 0; i < NF; i++) u_[i] = colk(u, e_[i]);
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         const double uu = u_[i];

@@ -30,6 +30,8 @@ const FieldInfo kFields[X_COUNT] = {
     {"ce_c1", K_C2I, 10, D_M, 0, 0},
     {"ce_c2", K_C2I, 10, D_M, 0, 0},
     {"ce_dv", K_C2F, 10, D_M, 0, 0},
+    {"ce_dc", K_C2F, 10, D_M, 0, 0},
+    {"ve_dc", K_V2F, 3, D_M, 0, 0},
     {"ce_idc", K_C2F, 10, D_M, 0, 0},
     {"ce_msd2", K_C2F, 10, D_M, 0, 0},
     {"ce_msd4", K_C2F, 10, D_M, 0, 0},

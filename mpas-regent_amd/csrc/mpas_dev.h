@@ -37,6 +37,8 @@ enum FieldId {
     X_ce_c1,    // cellsOnEdge(edgesOnCell(i,c), 0)      C2I x10
     X_ce_c2,    // cellsOnEdge(edgesOnCell(i,c), 1)      C2I x10
     X_ce_dv,    // dvEdge(edgesOnCell(i,c))              C2F x10
+    X_ce_dc,    // dcEdge(edgesOnCell(i,c))              C2F x10
+    X_ve_dc,    // dcEdge(edgesOnVertex(i,v))            V2F x3
     X_ce_idc,   // invDcEdge(edgesOnCell(i,c))           C2F x10
     X_ce_msd2,  // meshScalingDel2(edgesOnCell(i,c))     C2F x10
     X_ce_msd4,  // meshScalingDel4(edgesOnCell(i,c))     C2F x10
