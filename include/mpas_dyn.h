@@ -139,6 +139,11 @@ int mpas_atm_timestep(mpas_ctx* ctx, double dt);
  * in-process loopback).  Every rank must call the same tasks in the same order. */
 /* owned counts (the first entities of each kind); default: all local entities */
 int mpas_halo_owned(mpas_ctx* ctx, int32_t nCellsOwned, int32_t nEdgesOwned, int32_t nVerticesOwned);
+/* the first n*Interior owned entities of each kind reach no ghost through any index array
+ * (mpasdyn/decomp.py numbers them first): a kernel whose gathered fields need an exchange
+ * then computes them while the exchange runs on the context's halo stream, and the
+ * remaining (boundary) owned entities after it (SURVEY §8.6 overlap; option "overlap") */
+int mpas_halo_interior(mpas_ctx* ctx, int32_t nCellsInterior, int32_t nEdgesInterior, int32_t nVerticesInterior);
 /* kind 0 cells, 1 edges, 2 vertices: columns this rank sends to / receives from `peer`,
  * as local ids, in the order the peer receives / sends them */
 int mpas_halo_plan(mpas_ctx* ctx, int kind, int peer, const int32_t* send_ids, int32_t nsend,

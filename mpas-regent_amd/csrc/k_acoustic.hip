@@ -21,7 +21,7 @@ namespace mpas {
 
 template <int LP, bool EXACT, bool SELF>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
@@ -202,15 +202,18 @@ template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
-    int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
-    HALO_BEFORE(S, st, F_ru_p, F_theta_m);
-    if (exact) {
-        if (S.selfc) k_acoustic<LP, true, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
-        else k_acoustic<LP, true, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
-    } else {
-        if (S.selfc) k_acoustic<LP, false, true><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
-        else k_acoustic<LP, false, false><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm);
-    }
+    auto run = [&](const DevState& X) {
+        const int grid = col_blocks<LP>(X, KC);
+        if (!grid) return;
+        if (exact) {
+            if (X.selfc) k_acoustic<LP, true, true><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
+            else k_acoustic<LP, true, false><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
+        } else {
+            if (X.selfc) k_acoustic<LP, false, true><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
+            else k_acoustic<LP, false, false><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
+        }
+    };
+    HALO_RUN(S, st, run, F_ru_p, F_theta_m);
     HALO_WROTE(S, F_rtheta_pp_old, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
     return hipGetLastError();
 }

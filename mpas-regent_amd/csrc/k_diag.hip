@@ -22,7 +22,7 @@ struct RecK {
 // rho_zz = 1.0 of :1790-1792 (our zero slot)
 template <int LP>
 __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (m.blk == 0 && (int)threadIdx.x < L) fw(S, F_rho_zz)[(size_t)S.nCells * LP + threadIdx.x] = 1.0;
     if (c >= S.nCO) return;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
 // :1830-1837: ruAvg, ru (Q24: ru_save * ru_p), u from the new rho_zz
 template <int LP>
 __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO || k >= L) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
 // level iterations of the cell; lane 0 replays that sequence in the reference's order.
 template <int LP>
 __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     if (fi(S, F_bdyMaskCell)[c] > kRelaxZone) return;
@@ -130,7 +130,6 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
 
 template <int LP>
 static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_step, double dt) {
-    constexpr int COLS = ColMap<LP>::COLS;
     RecK a;
     a.invNs = 1 / (double)ns;
     a.dt = dt;
@@ -138,14 +137,20 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
     a.rgas_p0 = kRgas / 100000;
     a.rcv = kRgas / (kCp - kRgas);
     a.rk_step = rk_step;
-    const int nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS;
-    k_recover_cells<LP><<<nCB, 256, 0, st>>>(S, a);
+    const int nCB = col_blocks<LP>(S, KC);
+    if (nCB) k_recover_cells<LP><<<nCB, 256, 0, st>>>(S, a);
     HALO_WROTE(S, F_rho_p, F_rho_zz, F_wwAvg, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
-    HALO_BEFORE(S, st, F_rho_zz);
-    k_recover_edges<LP><<<nEB, 256, 0, st>>>(S, a);
+    auto ke = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KE);
+        if (nb) k_recover_edges<LP><<<nb, 256, 0, st>>>(X, a);
+    };
+    HALO_RUN(S, st, ke, F_rho_zz);
     HALO_WROTE(S, F_ruAvg, F_ru, F_u);
-    HALO_BEFORE(S, st, F_ru);
-    k_recover_w<LP><<<nCB, 256, 0, st>>>(S);
+    auto kw = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (nb) k_recover_w<LP><<<nb, 256, 0, st>>>(X);
+    };
+    HALO_RUN(S, st, kw, F_ru);
     HALO_WROTE(S, F_w);
     return hipGetLastError();
 }
@@ -156,7 +161,7 @@ hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, 
 // ---------------------------------------------------------------- reconstruct_2d
 template <int LP>
 __global__ __launch_bounds__(256) void k_reconstruct(DevState S, int on_a_sphere) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
@@ -198,9 +203,11 @@ __global__ __launch_bounds__(256) void k_reconstruct(DevState S, int on_a_sphere
 }
 template <int LP>
 static hipError_t reconstruct_lp(const DevState& S, hipStream_t st, int on_a_sphere) {
-    constexpr int COLS = ColMap<LP>::COLS;
-    HALO_BEFORE(S, st, F_u);
-    k_reconstruct<LP><<<(S.nCO + COLS - 1) / COLS, 256, 0, st>>>(S, on_a_sphere);
+    auto run = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (nb) k_reconstruct<LP><<<nb, 256, 0, st>>>(X, on_a_sphere);
+    };
+    HALO_RUN(S, st, run, F_u);
     HALO_WROTE(S, F_uReconstructX, F_uReconstructY, F_uReconstructZ, F_uReconstructZonal, F_uReconstructMeridional);
     return hipGetLastError();
 }

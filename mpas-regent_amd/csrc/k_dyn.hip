@@ -47,7 +47,7 @@ struct DynK {
 // ------------------------------------------------------------------------ A (cells)
 template <int LP, bool RK0>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // ------------------------------------------------------------------------ B (edges)
 template <int LP, bool RK0>
 __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
     const size_t p = (size_t)e * LP + k;
@@ -334,7 +334,7 @@ template <int LP, bool SELF>
 __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KV);
     if (m.blk < nVB) {  // delsq_vorticity (:1052-1060)
         const int vx = m.ent, k = m.k;
         if (vx >= S.nVO || k >= L) return;
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         colk(fw(S, F_delsq_vorticity), vx) = dsv;
         return;
     }
-    const int c = col_of<LP>(m.blk - nVB);
+    const int c = col_of<LP>(m.blk - nVB) + S.lo[KC];
     const int k = m.k;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
 // ------------------------------------------------------------------------ D (rk0, del4)
 template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO || k >= L) return;
     const size_t p = (size_t)e * LP + k;
@@ -481,7 +481,7 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
 // ------------------------------------------------------------------------ E (cells)
 template <int LP, bool RK0, bool SELF>
 __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
@@ -638,7 +638,6 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
 
 template <int LP>
 static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& in) {
-    constexpr int COLS = ColMap<LP>::COLS;
     DynK a;
     a.rk_step = in.rk_step;
     a.horiz_mixing = in.horiz_mixing;
@@ -654,39 +653,61 @@ static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& i
     a.inv_r_earth = 1.0 / a.r_earth;
     a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
     a.prandtl_inv = 1.0 / kPrandtl;
-    const int nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS, nVB = (S.nVO + COLS - 1) / COLS;
-    const int nCV = (a.h4 > 0.0 ? nVB : 0) + nCB, nV4 = a.h4 > 0.0 ? nVB : 0;
     const bool rk0 = a.rk_step == 0, del4 = rk0 && a.h4 > 0.0;
+    // kernel launches over the entities of a DevState range (HALO_RUN: interior /
+    // boundary halves around a halo exchange, or all owned entities)
+    auto kA = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (!nb) return;
+        if (rk0) k_dyn_A<LP, true><<<nb, 256, 0, st>>>(X, a);
+        else k_dyn_A<LP, false><<<nb, 256, 0, st>>>(X, a);
+    };
+    auto kB = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KE);
+        if (!nb) return;
+        if (rk0) k_dyn_B<LP, true><<<nb, 256, 0, st>>>(X, a);
+        else k_dyn_B<LP, false><<<nb, 256, 0, st>>>(X, a);
+    };
+    auto kC = [&](const DevState& X) {  // vertex blocks (del4) first, then cell blocks
+        const int nv = del4 ? col_blocks<LP>(X, KV) : 0, nb = nv + col_blocks<LP>(X, KC);
+        if (!nb) return;
+        if (X.selfc) k_dyn_C<LP, true><<<nb, 256, 0, st>>>(X, a, nv);
+        else k_dyn_C<LP, false><<<nb, 256, 0, st>>>(X, a, nv);
+    };
+    auto kD = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KE);
+        if (nb) k_dyn_D<LP><<<nb, 256, 0, st>>>(X, a);
+    };
+    auto kE = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (!nb) return;
+        if (rk0) {
+            if (X.selfc) k_dyn_E<LP, true, true><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_E<LP, true, false><<<nb, 256, 0, st>>>(X, a);
+        } else {
+            if (X.selfc) k_dyn_E<LP, false, true><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_E<LP, false, false><<<nb, 256, 0, st>>>(X, a);
+        }
+    };
     // halo: fields each kernel gathers through an index array / fields it writes
-    HALO_BEFORE(S, st, F_ru, F_u, F_v);
-    if (rk0) k_dyn_A<LP, true><<<nCB, 256, 0, st>>>(S, a);
-    else k_dyn_A<LP, false><<<nCB, 256, 0, st>>>(S, a);
+    HALO_RUN(S, st, kA, F_ru, F_u, F_v);
     HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz, X_wc);
     if (rk0) {
-        HALO_BEFORE(S, st, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p, F_zz, F_dpdz,
-                    F_divergence, F_kdiff, F_vorticity);
-        k_dyn_B<LP, true><<<nEB, 256, 0, st>>>(S, a);
+        HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p, F_zz, F_dpdz,
+                 F_divergence, F_kdiff, F_vorticity);
         HALO_WROTE(S, X_F, F_tend_u, F_tend_u_euler, F_delsq_u);
-        HALO_BEFORE(S, st, F_delsq_u, F_rho_edge, F_kdiff, X_wc, F_theta_m);
-        if (S.selfc) k_dyn_C<LP, true><<<nCV, 256, 0, st>>>(S, a, nV4);
-        else k_dyn_C<LP, false><<<nCV, 256, 0, st>>>(S, a, nV4);
+        HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, X_wc, F_theta_m);
         HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
                    F_tend_theta_euler);
         if (del4) {
-            HALO_BEFORE(S, st, F_delsq_divergence, F_delsq_vorticity);
-            k_dyn_D<LP><<<nEB, 256, 0, st>>>(S, a);
+            HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
             HALO_WROTE(S, F_tend_u_euler, F_tend_u);
         }
-        HALO_BEFORE(S, st, F_ru, X_F, F_delsq_w, F_delsq_theta);
-        if (S.selfc) k_dyn_E<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
-        else k_dyn_E<LP, true, false><<<nCB, 256, 0, st>>>(S, a);
+        HALO_RUN(S, st, kE, F_ru, X_F, F_delsq_w, F_delsq_theta);
     } else {
-        HALO_BEFORE(S, st, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
-        k_dyn_B<LP, false><<<nEB, 256, 0, st>>>(S, a);
+        HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
         HALO_WROTE(S, X_F, F_tend_u);
-        HALO_BEFORE(S, st, F_ru, X_F, F_ru_save, F_theta_m_save);
-        if (S.selfc) k_dyn_E<LP, false, true><<<nCB, 256, 0, st>>>(S, a);
-        else k_dyn_E<LP, false, false><<<nCB, 256, 0, st>>>(S, a);
+        HALO_RUN(S, st, kE, F_ru, X_F, F_ru_save, F_theta_m_save);
     }
     HALO_WROTE(S, F_w, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
     return hipGetLastError();

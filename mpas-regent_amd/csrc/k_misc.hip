@@ -80,7 +80,7 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 // ---------------------------------------------------------------- vert_imp
 template <int LP>
 __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
@@ -143,8 +143,8 @@ static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
     double dtseps = .5 * dts * (1.0 + kEpssm);
     double rcv = kRgas / (kCp - kRgas);
     double c2 = kCp * rcv;
-    int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
-    k_vert_imp<LP><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
+    const int grid = col_blocks<LP>(S, KC);
+    if (grid) k_vert_imp<LP><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
     HALO_WROTE(S, F_coftz, F_cofwt, F_gamma_tri, F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri);
     return hipGetLastError();
 }
@@ -155,7 +155,7 @@ hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts) 
 // ---------------------------------------------------------------- set_smlstep
 template <int LP>
 __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
@@ -200,9 +200,11 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
 }
 template <int LP>
 static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
-    int grid = (S.nCO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
-    HALO_BEFORE(S, st, F_u_tend);
-    k_set_smlstep<LP><<<grid, 256, 0, st>>>(S);
+    auto run = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (nb) k_set_smlstep<LP><<<nb, 256, 0, st>>>(X);
+    };
+    HALO_RUN(S, st, run, F_u_tend);
     HALO_WROTE(S, F_w);
     return hipGetLastError();
 }
@@ -211,7 +213,7 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPA
 // ---------------------------------------------------------------- divergence damping
 template <int LP>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO || k >= L) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
@@ -233,9 +235,11 @@ static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
     double smdiv = kSmdiv;
     double rdts = 1.0 / dts;
     double coef_divdamp = 2.0 * smdiv * kLenDisp * rdts;
-    int grid = (S.nEO + ColMap<LP>::COLS - 1) / ColMap<LP>::COLS;
-    HALO_BEFORE(S, st, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
-    k_div_damp<LP><<<grid, 256, 0, st>>>(S, coef_divdamp);
+    auto run = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KE);
+        if (nb) k_div_damp<LP><<<nb, 256, 0, st>>>(X, coef_divdamp);
+    };
+    HALO_RUN(S, st, run, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
     HALO_WROTE(S, F_ru_p);
     return hipGetLastError();
 }

@@ -17,7 +17,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     const int L = S.L;
     const double* u = fd(S, F_u);
     const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KV);
     if (m.blk < nVB) {
         const int v = m.ent, k = m.k;
         if (v >= S.nVO || k >= L) return;
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         }
         return;
     }
-    const int c = col_of<LP>(m.blk - nVB);
+    const int c = col_of<LP>(m.blk - nVB) + S.lo[KC];
     const int k = m.k;
     if (c >= S.nCO || k >= L) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
 // hollingsworth second half (:405-417): cells, needs ke_vertex of the whole mesh
 template <int LP>
 __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KC);
     const int L = S.L, c = m.ent, k = m.k;
     if (c >= S.nCO || k >= L) return;
     const size_t p = (size_t)c * LP + k;
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
 
 template <int LP, bool RECON_V>
 __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
-    ColMap<LP> m(S);
+    ColMap<LP> m(S, KE);
     const int L = S.L, e = m.ent, k = m.k;
     if (e >= S.nEO || k >= L) return;
     const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
@@ -155,19 +155,27 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
 
 template <int LP>
 static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
-    constexpr int COLS = ColMap<LP>::COLS;
-    int nVB = (S.nVO + COLS - 1) / COLS, nCB = (S.nCO + COLS - 1) / COLS, nEB = (S.nEO + COLS - 1) / COLS;
-    HALO_BEFORE(S, st, F_u);
-    k_solve_vc<LP><<<nVB + nCB, 256, 0, st>>>(S, nVB, hollingsworth);
+    auto kvc = [&](const DevState& X) {  // vertex blocks, then cell blocks
+        const int nv = col_blocks<LP>(X, KV), nb = nv + col_blocks<LP>(X, KC);
+        if (nb) k_solve_vc<LP><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+    };
+    auto kh = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (nb) k_solve_holl<LP><<<nb, 256, 0, st>>>(X);
+    };
+    auto ke = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KE);
+        if (!nb) return;
+        if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false><<<nb, 256, 0, st>>>(X);
+        else k_solve_e<LP, true><<<nb, 256, 0, st>>>(X);
+    };
+    HALO_RUN(S, st, kvc, F_u);
     HALO_WROTE(S, F_vorticity, F_pv_vertex, F_ke_vertex, F_divergence, F_ke);
     if (hollingsworth) {
-        HALO_BEFORE(S, st, F_ke_vertex);
-        k_solve_holl<LP><<<nCB, 256, 0, st>>>(S);
+        HALO_RUN(S, st, kh, F_ke_vertex);
         HALO_WROTE(S, F_ke);
     }
-    HALO_BEFORE(S, st, F_h, F_u, F_pv_vertex);
-    if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false><<<nEB, 256, 0, st>>>(S);
-    else k_solve_e<LP, true><<<nEB, 256, 0, st>>>(S);
+    HALO_RUN(S, st, ke, F_h, F_u, F_pv_vertex);
     HALO_WROTE(S, F_h_edge, F_ke_edge, F_v, F_pv_edge);
     return hipGetLastError();
 }

@@ -59,6 +59,7 @@ struct mpas_ctx {
     int exact = 0;
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
+    int overlap = 1;   // option "overlap": halo exchanges beside interior compute
     bool timing = false;
     bool dirty = true;  // derived mesh arrays need k_prepare
     std::vector<std::string> task_names;
@@ -354,7 +355,10 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
     return guarded(c, [&] {
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
-        else if (name && std::strcmp(name, "self") == 0) {
+        else if (name && std::strcmp(name, "overlap") == 0) {
+            c->overlap = value ? 1 : 0;
+            if (c->halo) c->halo->overlap = c->overlap;
+        } else if (name && std::strcmp(name, "self") == 0) {
             c->self_on = value ? 1 : 0;
             c->S.selfc = c->self_ok && c->self_on;
         } else throw Fail{MPAS_EINVAL, std::string("unknown option ") + (name ? name : "(null)")};
@@ -366,6 +370,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         if (!value) throw Fail{MPAS_EINVAL, "mpas_get_option: null value"};
         if (name && std::strcmp(name, "exact") == 0) *value = c->exact;
         else if (name && std::strcmp(name, "xcd") == 0) *value = c->S.xcd;
+        else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "selfc") == 0) {
             if (c->dirty) {  // decide now (needs the mesh uploaded)
@@ -517,6 +522,27 @@ int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32
         c->S.nEO = nEdgesOwned;
         c->S.nVO = nVerticesOwned;
         c->dirty = true;
+    });
+}
+
+int mpas_halo_interior(mpas_ctx* c, int32_t nCI, int32_t nEI, int32_t nVI) {
+    return guarded(c, [&] {
+        if (nCI < 0 || nCI > c->S.nCO || nEI < 0 || nEI > c->S.nEO || nVI < 0 || nVI > c->S.nVO)
+            throw Fail{MPAS_EINVAL, "mpas_halo_interior: interior counts exceed the owned counts"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        Halo* h = halo_of(c);
+        h->nint[0] = nCI;
+        h->nint[1] = nEI;
+        h->nint[2] = nVI;
+        h->interior = true;
+        h->overlap = c->overlap;
+        if (!h->comm) {  // the halo stream, at the device's highest priority
+            int least = 0, greatest = 0;
+            hipcheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+            hipcheck(hipStreamCreateWithPriority(&h->comm, hipStreamNonBlocking, greatest), "hipStreamCreate");
+            hipcheck(hipEventCreateWithFlags(&h->ev_ready, hipEventDisableTiming), "hipEventCreate");
+            hipcheck(hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming), "hipEventCreate");
+        }
     });
 }
 

@@ -67,6 +67,8 @@ struct DevState {
     int nCells, nEdges, nVertices, L, LP;  // local entity counts (= the zero-slot ids)
     int nCO, nEO, nVO;  // owned entities, the first of the local ones: every kernel's
                         // grid (= the counts above unless the mesh is decomposed)
+    int lo[3];          // first cell / edge / vertex of a launch: kernels compute entities
+                        // [lo, nXO); 0 except for the boundary launch of a halo overlap
     int xcd;  // 1: XCD-aware block order, 0: dispatcher order (default: measured faster,
               // the Morton-ordered columns of all XCDs then share one Infinity-Cache window)
     int selfc;  // 1 when every cell is one of the two cellsOnEdge of each of its first
@@ -107,6 +109,16 @@ struct DynTendArgs {
     int rayleigh_damp_u;
     int exact_q;       // 1: Q10 literal (each q term added nVertLevels times), 0: nVertLevels*term
 };
+
+enum EntityKind { KC = 0, KE = 1, KV = 2 };  // DevState::lo index
+
+// blocks of a column-per-wavefront launch over entities [lo, end) of one kind
+template <int LP>
+inline int col_blocks(const DevState& S, int kind) {
+    const int end = kind == KC ? S.nCO : kind == KE ? S.nEO : S.nVO;
+    const int n = end - S.lo[kind];
+    return n > 0 ? (n + 256 / LP - 1) / (256 / LP) : 0;
+}
 
 // ---- launchers (each returns the hipGetLastError of its launches) ----
 hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st);
@@ -163,9 +175,9 @@ template <int LP>
 struct ColMap {
     static constexpr int COLS = 256 / LP;
     int blk, ent, k;
-    __device__ __forceinline__ explicit ColMap(const DevState& S) {
+    __device__ __forceinline__ ColMap(const DevState& S, int kind) {
         blk = xcd_block(S.xcd);
-        ent = col_of<LP>(blk);
+        ent = col_of<LP>(blk) + S.lo[kind];
         k = (int)(threadIdx.x % LP);
     }
 };

@@ -9,6 +9,12 @@
 // all its stale gathered fields), after which it is fresh.  Correct by construction
 // given complete gather lists -- the loopback N-shard = 1-shard parity test checks them.
 //
+// Overlap: the owned entities are numbered interior first -- an interior
+// entity reaches no ghost through any index array (decomp.py) -- so a kernel that needs
+// an exchange computes its interior entities while the exchange runs on the halo stream
+// (pack, send/recv, unpack), then its boundary entities once the ghosts have arrived.
+// The launchers hand the kernel launch to HALO_RUN as a function of the DevState range.
+//
 // Transport: RCCL point-to-point (ncclSend/ncclRecv of one packed buffer per peer inside
 // ncclGroupStart/End, on the task stream; librccl resolved with dlopen, so the process
 // shares the RCCL that torch.distributed loaded) for one process per GPU, or an
@@ -19,6 +25,7 @@
 
 #include <condition_variable>
 #include <cstdint>
+#include <functional>
 #include <initializer_list>
 #include <mutex>
 #include <string>
@@ -52,6 +59,12 @@ struct Halo {
     RcclComm* rccl = nullptr;
     std::string err;
     int64_t exchanges = 0, fields_moved = 0;
+    // overlap of the exchange with interior compute
+    hipStream_t comm = nullptr;  // the halo stream
+    hipEvent_t ev_ready = nullptr, ev_done = nullptr;
+    int nint[3] = {0, 0, 0};  // interior cells, edges, vertices: the first owned ones
+    bool interior = false;     // nint set (mpas_halo_interior)
+    int overlap = 1;           // option "overlap"
 
     ~Halo();
     hipError_t reserve(int LP);  // size the packed buffers for the largest exchange
@@ -59,15 +72,22 @@ struct Halo {
     hipError_t before(const DevState& S, hipStream_t st, std::initializer_list<int> gathers);
     void wrote(std::initializer_list<int> fields);
     hipError_t exchange(const DevState& S, hipStream_t st, const std::vector<int>& fields);
+    // launch `fn` (a kernel launch over the entities of the DevState it is given) with the
+    // stale fields of `gathers` exchanged first: interior / exchange / boundary when the
+    // overlap is on, else exchange then one launch over every owned entity
+    hipError_t launch(const DevState& S, hipStream_t st, std::initializer_list<int> gathers,
+                      const std::function<void(const DevState&)>& fn);
 };
 
-// launchers: no-ops without a decomposition
-#define HALO_BEFORE(S, st, ...)                                                   \
-    do {                                                                          \
-        if ((S).halo) {                                                           \
-            hipError_t he_ = (S).halo->before((S), (st), {__VA_ARGS__});          \
-            if (he_ != hipSuccess) return he_;                                    \
-        }                                                                         \
+// launchers: without a decomposition HALO_RUN is one call of FN over the owned entities
+#define HALO_RUN(S, st, FN, ...)                                                           \
+    do {                                                                                   \
+        if ((S).halo) {                                                                    \
+            hipError_t he_ = (S).halo->launch((S), (st), {__VA_ARGS__}, (FN));              \
+            if (he_ != hipSuccess) return he_;                                             \
+        } else {                                                                           \
+            (FN)(S);                                                                       \
+        }                                                                                  \
     } while (0)
 #define HALO_WROTE(S, ...)                          \
     do {                                            \

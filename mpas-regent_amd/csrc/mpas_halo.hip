@@ -53,6 +53,12 @@ Halo::~Halo() {
     if (sendbuf) (void)hipFree(sendbuf);
     if (recvbuf) (void)hipFree(recvbuf);
     if (rccl) rccl_free(rccl);
+    if (comm) {
+        (void)hipStreamSynchronize(comm);
+        (void)hipStreamDestroy(comm);
+    }
+    if (ev_ready) (void)hipEventDestroy(ev_ready);
+    if (ev_done) (void)hipEventDestroy(ev_done);
 }
 
 hipError_t Halo::reserve(int LP) {
@@ -94,6 +100,45 @@ hipError_t Halo::before(const DevState& S, hipStream_t st, std::initializer_list
     if (e == hipSuccess)
         for (int f : need) stale[f] = 0;
     return e;
+}
+
+hipError_t Halo::launch(const DevState& S, hipStream_t st, std::initializer_list<int> gathers,
+                        const std::function<void(const DevState&)>& fn) {
+    std::vector<int> need;
+    for (int f : gathers)
+        if (stale[f]) need.push_back(f);
+    hipError_t e;
+    if (need.empty()) {
+        fn(S);
+        return hipGetLastError();
+    }
+    if (!(overlap && interior && comm)) {  // the exchange on the critical path
+        if ((e = exchange(S, st, need)) != hipSuccess) return e;
+        for (int f : need) stale[f] = 0;
+        fn(S);
+        return hipGetLastError();
+    }
+    // the halo stream starts after everything the task stream holds (the stale values
+    // were written there); the interior launch reads no ghost and writes no gathered
+    // field, so it runs beside the pack / send / recv / unpack
+    if ((e = hipEventRecord(ev_ready, st)) != hipSuccess) return e;
+    DevState in = S;
+    in.nCO = nint[0];
+    in.nEO = nint[1];
+    in.nVO = nint[2];
+    fn(in);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(comm, ev_ready, 0)) != hipSuccess) return e;
+    if ((e = exchange(S, comm, need)) != hipSuccess) return e;
+    for (int f : need) stale[f] = 0;
+    if ((e = hipEventRecord(ev_done, comm)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st, ev_done, 0)) != hipSuccess) return e;
+    DevState bd = S;
+    bd.lo[0] = nint[0];
+    bd.lo[1] = nint[1];
+    bd.lo[2] = nint[2];
+    fn(bd);
+    return hipGetLastError();
 }
 
 // ------------------------------------------------------------------ RCCL (dlopen)

@@ -19,8 +19,9 @@ the device-side halo exchange right before it (csrc/mpas_halo.h; lazily, only af
 some kernel wrote it).  This keeps the ref-mode ids (raw 1-based offsets, which
 scramble neighbourhoods) exact: no geometric ring assumption anywhere.
 
-Local numbering: owned entities first (global order), then ghosts (global order), then
-the zero slot at index n_local.  Index arrays are mapped to local ids; ids that
+Local numbering: owned entities first -- the interior ones (reaching no ghost through any
+index array) before the boundary ones, each in global order -- then ghosts (global
+order), then the zero slot at index n_local.  Index arrays are mapped to local ids; ids that
 resolve to the global zero slot, or to an entity outside the local set (only ghost
 entities' own connectivity can), map to the local zero slot.
 """
@@ -65,7 +66,7 @@ class Decomposition:
         coe = np.vstack([self.ids["cellsOnEdge"], np.full((1, 2), nC)])
         eoc = self.ids["edgesOnCell"]
         self.cell_cells = np.concatenate([coe[eoc, 0], coe[eoc, 1]], axis=1)  # k_prepare's composition
-        self.owned, self.local, self.g2l = [], [], []
+        self.owned, self.local, self.g2l, self.n_int = [], [], [], []
         for r in range(self.nparts):
             own = {k: np.flatnonzero(self.part[k] == r) for k in KINDS}
             need = {k: [own[k]] for k in KINDS}
@@ -73,11 +74,29 @@ class Decomposition:
                 src = BY_NAME[f].entity
                 need[t].append(self.ids[f][own[src]].ravel())
             need["cell"].append(self.cell_cells[own["cell"]].ravel())
+            # interior first: an owned entity is interior when every id its index arrays
+            # (and k_prepare's composed cell ids) reach is owned or the zero slot -- its
+            # kernels read no ghost, so they run while a halo exchange is in flight
+            isown = {}
+            for k in KINDS:
+                m = np.zeros(self.n[k] + 1, dtype=bool)
+                m[own[k]] = True
+                m[self.n[k]] = True
+                isown[k] = m
+            bnd = {k: np.zeros(len(own[k]), dtype=bool) for k in KINDS}
+            for f, t in ID_ARRAYS.items():
+                src = BY_NAME[f].entity
+                bnd[src] |= ~isown[t][self.ids[f][own[src]]].all(axis=1)
+            bnd["cell"] |= ~isown["cell"][self.cell_cells[own["cell"]]].all(axis=1)
+            nint = {}
+            for k in KINDS:
+                nint[k] = int(np.count_nonzero(~bnd[k]))
+                own[k] = np.concatenate([own[k][~bnd[k]], own[k][bnd[k]]])
             loc, g2l = {}, {}
             for k in KINDS:
                 allk = np.unique(np.concatenate(need[k]))
                 allk = allk[allk < self.n[k]]  # the zero slot is not an entity
-                ghosts = np.setdiff1d(allk, own[k], assume_unique=True)
+                ghosts = np.setdiff1d(allk, own[k])
                 loc[k] = np.concatenate([own[k], ghosts]).astype(np.int64)
                 m = np.full(self.n[k] + 1, len(loc[k]), dtype=np.int64)  # default: local zero slot
                 m[loc[k]] = np.arange(len(loc[k]))
@@ -85,10 +104,15 @@ class Decomposition:
             self.owned.append(own)
             self.local.append(loc)
             self.g2l.append(g2l)
+            self.n_int.append(nint)
 
     # ------------------------------------------------------------------ per rank
     def n_owned(self, r):
         return tuple(len(self.owned[r][k]) for k in KINDS)
+
+    def n_interior(self, r):
+        """owned entities of rank r whose stencils reach no ghost (numbered first)"""
+        return tuple(self.n_int[r][k] for k in KINDS)
 
     def n_local(self, r):
         return tuple(len(self.local[r][k]) for k in KINDS)

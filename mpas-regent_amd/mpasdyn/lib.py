@@ -25,7 +25,7 @@ EXPORTS = [
     "mpas_atm_rk_dynamics_substep_finish", "mpas_atm_srk3", "mpas_atm_timestep",
     "mpas_atm_recover_large_step_variables_work", "mpas_reconstruct_2d", "mpas_summarize_timestep",
     "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
-    "mpas_halo_owned", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
+    "mpas_halo_owned", "mpas_halo_interior", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
     "mpas_halo_loopback", "mpas_halo_stats",
 ]
 KIND_ID = {"cell": 0, "edge": 1, "vertex": 2}
@@ -89,6 +89,7 @@ def load():
         "mpas_timing_get": (i32, [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(i64),
                                   ctypes.POINTER(dbl)]),
         "mpas_halo_owned": (i32, [vp, i32, i32, i32]),
+        "mpas_halo_interior": (i32, [vp, i32, i32, i32]),
         "mpas_halo_plan": (i32, [vp, i32, i32, vp, i32, vp, i32]),
         "mpas_set_global_ids": (i32, [vp, i32, vp, i32]),
         "mpas_rccl_unique_id": (i32, [vp]),
@@ -203,6 +204,7 @@ def setup_subdomain(ctx, dec, r):
     mpasdyn.decomp.Decomposition `dec` (its local state is uploaded separately)"""
     L = ctx.lib
     ctx._check(L.mpas_halo_owned(ctx.h, *dec.n_owned(r)), "mpas_halo_owned")
+    ctx._check(L.mpas_halo_interior(ctx.h, *dec.n_interior(r)), "mpas_halo_interior")
     for kind, g in dec.global_ids(r).items():
         g = np.ascontiguousarray(g, dtype=np.int32)
         ctx._check(L.mpas_set_global_ids(ctx.h, KIND_ID[kind], g.ctypes.data, len(g)), "mpas_set_global_ids")

@@ -153,3 +153,30 @@ def test_halo_plans_gloo(world, variant):
     for p in procs:
         p.join(timeout=60)
     assert all(res[r] == 0 for r in range(world)), res
+
+
+@pytest.mark.parametrize("variant", ["ref", "mpas0"])
+@pytest.mark.parametrize("nparts", [2, 3, 16])
+def test_interior_first(states, variant, nparts):
+    """the first n_interior owned entities of each kind reach, through every index array
+    of the local state (and the composed cellsOnEdge(edgesOnCell)), only owned entities or
+    the zero slot: the kernels may compute them while a halo exchange is in flight"""
+    st = states[variant]
+    d = decomp.Decomposition(st, nparts)
+    from mpasdyn.registry import BY_NAME
+    for r in range(nparts):
+        ls = d.local_state(r)
+        nown = dict(zip(KINDS, d.n_owned(r)))
+        nloc = dict(zip(KINDS, d.n_local(r)))
+        nint = dict(zip(KINDS, d.n_interior(r)))
+        assert all(0 <= nint[k] <= nown[k] for k in KINDS)
+        for f, t in ID_ARRAYS.items():
+            src = BY_NAME[f].entity
+            ids = ls[f][:nint[src]].astype(np.int64)
+            ok = (ids < nown[t]) | (ids == nloc[t])
+            assert ok.all(), (r, f)
+        coe = ls["cellsOnEdge"].astype(np.int64)
+        cc = coe[ls["edgesOnCell"][:nint["cell"]].astype(np.int64)]
+        assert ((cc < nown["cell"]) | (cc == nloc["cell"])).all(), r
+    if nparts == 16:  # small parts: a real boundary band exists
+        assert sum(d.n_interior(r)[0] for r in range(nparts)) < st.nCells

@@ -40,13 +40,14 @@ def run_single(st, fn, exact):
     return got
 
 
-def run_decomposed(st, nparts, fn, exact, cell_part=None):
+def run_decomposed(st, nparts, fn, exact, cell_part=None, overlap=1):
     d = decomp.Decomposition(st, nparts, cell_part=cell_part)
     locs = [d.local_state(r) for r in range(nparts)]
     ctxs = [lib.Context(*d.n_local(r), st.L) for r in range(nparts)]
     try:
         for r, c in enumerate(ctxs):
             c.set_option("exact", exact)
+            c.set_option("overlap", overlap)
             lib.setup_subdomain(c, d, r)
             c.upload(locs[r])
         lib.halo_loopback(ctxs)
@@ -76,11 +77,13 @@ def run_decomposed(st, nparts, fn, exact, cell_part=None):
 @pytest.mark.parametrize("variant", ["ref", "random", "mpas0"])
 @pytest.mark.parametrize("nparts", [2, 3])
 @pytest.mark.parametrize("L", [5, 56])
-def test_srk3_decomposed_equals_single(x1_2562, variant, nparts, L):
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_srk3_decomposed_equals_single(x1_2562, variant, nparts, L, overlap):
+    """overlap 1: interior entities computed while the exchange runs on the halo stream"""
     st = state(x1_2562, L, variant)
     for exact in (1, 0):
         ref = run_single(st, lambda c: T.atm_srk3(c, 720.0, 1), exact)
-        got, stats = run_decomposed(st, nparts, lambda c: T.atm_srk3(c, 720.0, 1), exact)
+        got, stats = run_decomposed(st, nparts, lambda c: T.atm_srk3(c, 720.0, 1), exact, overlap=overlap)
         bad = compare_states(got, ref, rtol=0.0)
         assert not bad, f"exact={exact}: {bad[:6]}"
         assert all(s[0] > 0 for s in stats)  # the halo was exercised
@@ -95,19 +98,23 @@ def test_srk3_part_file_16(x1_2562):
     assert not bad, bad[:6]
 
 
-@pytest.mark.parametrize("task", ["dyn_tend_rk0", "dyn_tend_rk1", "solve_holl", "acoustic", "div_damp", "smlstep"])
+@pytest.mark.parametrize("task", ["dyn_tend_rk0", "dyn_tend_rk1", "solve_holl", "acoustic", "div_damp", "smlstep",
+                                  "recover", "reconstruct"])
 def test_task_decomposed_equals_single(x1_2562, task):
     fn = {"dyn_tend_rk0": lambda c: T.atm_compute_dyn_tend_work(c, 0, 720.0),
           "dyn_tend_rk1": lambda c: T.atm_compute_dyn_tend_work(c, 1, 720.0),
           "solve_holl": lambda c: T.atm_compute_solve_diagnostics(c, True, -1),
           "acoustic": lambda c: T.atm_advance_acoustic_step_work(c, 360.0, 1),
           "div_damp": lambda c: T.atm_divergence_damping_3d(c, 240.0),
-          "smlstep": lambda c: T.atm_set_smlstep_pert_variables_work(c)}[task]
+          "smlstep": lambda c: T.atm_set_smlstep_pert_variables_work(c),
+          "recover": lambda c: T.atm_recover_large_step_variables_work(c, 2, 2, 240.0),
+          "reconstruct": lambda c: T.mpas_reconstruct_2d(c, False, True)}[task]
     st = state(x1_2562, 56, "random")
     ref = run_single(st, fn, 1)
-    got, _ = run_decomposed(st, 3, fn, 1)
-    bad = compare_states(got, ref, rtol=0.0)
-    assert not bad, bad[:6]
+    for overlap in (1, 0):
+        got, _ = run_decomposed(st, 3, fn, 1, overlap=overlap)
+        bad = compare_states(got, ref, rtol=0.0)
+        assert not bad, (overlap, bad[:6])
 
 
 def test_fill_synthetic_global_ids(x1_2562):
