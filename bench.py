@@ -164,9 +164,13 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(lib.rccl_unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         lib.halo_rccl(ctx, world, rank, uid.cpu().numpy().tobytes())
+        ctx.set_option("overlap", halo_info["overlap"])
         own = dec.n_owned(rank)
+        nint = dec.n_interior(rank)
         halo_info = {"partition": f"{world} contiguous Morton blocks of cells", "owned": list(own),
-                     "ghost_frac": [round(1 - o / n, 4) for o, n in zip(own, dims[:3])]}
+                     "ghost_frac": [round(1 - o / n, 4) for o, n in zip(own, dims[:3])],
+                     "interior_frac": [round(i / max(o, 1), 4) for i, o in zip(nint, own)],
+                     "overlap": int(os.environ.get("MPAS_OVERLAP", "1"))}
         st = lst
         work_dims = (*own, L)  # what this rank computes
     else:

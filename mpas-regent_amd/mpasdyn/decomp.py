@@ -37,6 +37,21 @@ ID_ARRAYS = {"edgesOnCell": "edge", "edgesOnEdge": "edge", "edgesOnEdge_ECP": "e
              "cellsOnEdge": "cell", "advCellsForEdge": "cell", "verticesOnEdge": "vertex", "verticesOnCell": "vertex"}
 
 
+# list lengths of the variable-length index arrays: entries past them are padding the
+# kernels may load (unconditionally, ahead of the accumulation) but never use
+COUNTS = {"edgesOnCell": "nEdgesOnCell", "verticesOnCell": "nEdgesOnCell", "edgesOnEdge": "nEdgesOnEdge",
+          "edgesOnEdge_ECP": "nEdgesOnEdge", "advCellsForEdge": "nAdvCellsForEdge"}
+
+
+def active_mask(st, f, rows):
+    """(len(rows), W) mask of the entries of index array f that the kernels use"""
+    W = st[f].shape[1]
+    if f not in COUNTS:
+        return np.ones((len(rows), W), dtype=bool)
+    cnt = np.asarray(st[COUNTS[f]][rows, 0], dtype=np.int64)
+    return np.arange(W)[None, :] < cnt[:, None]
+
+
 def _resolve(ids, n):
     """Q1 policy: any id outside [0, n] is the zero slot n"""
     ids = np.asarray(ids, dtype=np.int64)
@@ -75,8 +90,9 @@ class Decomposition:
                 need[t].append(self.ids[f][own[src]].ravel())
             need["cell"].append(self.cell_cells[own["cell"]].ravel())
             # interior first: an owned entity is interior when every id its index arrays
-            # (and k_prepare's composed cell ids) reach is owned or the zero slot -- its
-            # kernels read no ghost, so they run while a halo exchange is in flight
+            # (and k_prepare's composed cell ids) reach in their used entries is owned or
+            # the zero slot -- its kernels use no ghost value, so they run while a halo
+            # exchange is in flight (a padding entry they load and discard may be mid-update)
             isown = {}
             for k in KINDS:
                 m = np.zeros(self.n[k] + 1, dtype=bool)
@@ -86,8 +102,10 @@ class Decomposition:
             bnd = {k: np.zeros(len(own[k]), dtype=bool) for k in KINDS}
             for f, t in ID_ARRAYS.items():
                 src = BY_NAME[f].entity
-                bnd[src] |= ~isown[t][self.ids[f][own[src]]].all(axis=1)
-            bnd["cell"] |= ~isown["cell"][self.cell_cells[own["cell"]]].all(axis=1)
+                use = active_mask(st, f, own[src])
+                bnd[src] |= (~isown[t][self.ids[f][own[src]]] & use).any(axis=1)
+            use = np.tile(active_mask(st, "edgesOnCell", own["cell"]), 2)
+            bnd["cell"] |= (~isown["cell"][self.cell_cells[own["cell"]]] & use).any(axis=1)
             nint = {}
             for k in KINDS:
                 nint[k] = int(np.count_nonzero(~bnd[k]))

@@ -158,9 +158,10 @@ def test_halo_plans_gloo(world, variant):
 @pytest.mark.parametrize("variant", ["ref", "mpas0"])
 @pytest.mark.parametrize("nparts", [2, 3, 16])
 def test_interior_first(states, variant, nparts):
-    """the first n_interior owned entities of each kind reach, through every index array
-    of the local state (and the composed cellsOnEdge(edgesOnCell)), only owned entities or
-    the zero slot: the kernels may compute them while a halo exchange is in flight"""
+    """the first n_interior owned entities of each kind reach, through the used entries of
+    every index array of the local state (and the composed cellsOnEdge(edgesOnCell)), only
+    owned entities or the zero slot: the kernels may compute them while a halo exchange is
+    in flight"""
     st = states[variant]
     d = decomp.Decomposition(st, nparts)
     from mpasdyn.registry import BY_NAME
@@ -173,10 +174,13 @@ def test_interior_first(states, variant, nparts):
         for f, t in ID_ARRAYS.items():
             src = BY_NAME[f].entity
             ids = ls[f][:nint[src]].astype(np.int64)
-            ok = (ids < nown[t]) | (ids == nloc[t])
+            use = decomp.active_mask(ls, f, np.arange(nint[src]))
+            ok = (ids < nown[t]) | (ids == nloc[t]) | ~use
             assert ok.all(), (r, f)
         coe = ls["cellsOnEdge"].astype(np.int64)
         cc = coe[ls["edgesOnCell"][:nint["cell"]].astype(np.int64)]
-        assert ((cc < nown["cell"]) | (cc == nloc["cell"])).all(), r
-    if nparts == 16:  # small parts: a real boundary band exists
-        assert sum(d.n_interior(r)[0] for r in range(nparts)) < st.nCells
+        use = decomp.active_mask(ls, "edgesOnCell", np.arange(nint["cell"]))[:, :, None]
+        assert ((cc < nown["cell"]) | (cc == nloc["cell"]) | ~use).all(), r
+    assert sum(d.n_interior(r)[0] for r in range(nparts)) < st.nCells  # a boundary band exists
+    # (the file order of x1.2562 is not spatially local, so contiguous blocks of it are
+    # nearly all boundary; the Morton-ordered benchmark meshes are ~95 % interior at 8 parts)
