@@ -211,24 +211,44 @@ static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st); }
 
 // ---------------------------------------------------------------- divergence damping
-template <int LP>
+template <int LP, int EPW>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
-    ColMap<LP> m(S, KE);
-    const int L = S.L, k = m.k, e = m.ent;
-    if (e >= S.nEO || k >= L) return;
-    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
-    const int* sh = fi(S, F_isShared);
+    ColMapN<LP, EPW> m(S, KE);
+    const int L = S.L, k = m.k;
+    const int *coe = fi(S, F_cellsOnEdge), *sh = fi(S, F_isShared);
     const double *rtp = fd(S, F_rtheta_pp), *rtpo = fd(S, F_rtheta_pp_old), *tm = fd(S, F_theta_m);
+    const double* spz = fd(S, F_specZoneMaskEdge);
     double* rup = fw(S, F_ru_p);
-    // every load first (the isShared test only decides the store)
-    const int sh1 = sh[cell1], sh2 = sh[cell2];
-    const double r1 = colk(rtp, cell1), ro1 = colk(rtpo, cell1), r2 = colk(rtp, cell2), ro2 = colk(rtpo, cell2);
-    const double t1 = colk(tm, cell1), t2 = colk(tm, cell2), ru = colk(rup, e);
-    const double spec = fd(S, F_specZoneMaskEdge)[e];
-    if (sh1 && sh2) return;
-    double divCell1 = -(r1 - ro1);
-    double divCell2 = -(r2 - ro2);
-    colk(rup, e) = ru + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec) / (t1 + t2);
+    // every load of the EPW edges first (the isShared test only decides the store)
+    int c1[EPW], c2[EPW], sh1[EPW], sh2[EPW];
+    double r1[EPW], ro1[EPW], r2[EPW], ro2[EPW], t1[EPW], t2[EPW], ru[EPW], spec[EPW];
+#pragma unroll
+    for (int i = 0; i < EPW; i++) {
+        const int e = min(m.base + i, S.nEO - 1);
+        c1[i] = coe[(size_t)e * 2];
+        c2[i] = coe[(size_t)e * 2 + 1];
+        spec[i] = spz[e];
+        ru[i] = colk(rup, e);
+    }
+#pragma unroll
+    for (int i = 0; i < EPW; i++) {
+        sh1[i] = sh[c1[i]];
+        sh2[i] = sh[c2[i]];
+        r1[i] = colk(rtp, c1[i]);
+        ro1[i] = colk(rtpo, c1[i]);
+        r2[i] = colk(rtp, c2[i]);
+        ro2[i] = colk(rtpo, c2[i]);
+        t1[i] = colk(tm, c1[i]);
+        t2[i] = colk(tm, c2[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < EPW; i++) {
+        const int e = m.base + i;
+        if (e >= S.nEO || k >= L || (sh1[i] && sh2[i])) continue;
+        double divCell1 = -(r1[i] - ro1[i]);
+        double divCell2 = -(r2[i] - ro2[i]);
+        colk(rup, e) = ru[i] + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec[i]) / (t1[i] + t2[i]);
+    }
 }
 template <int LP>
 static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
@@ -236,8 +256,16 @@ static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
     double rdts = 1.0 / dts;
     double coef_divdamp = 2.0 * smdiv * kLenDisp * rdts;
     auto run = [&](const DevState& X) {
-        const int nb = col_blocks<LP>(X, KE);
-        if (nb) k_div_damp<LP><<<nb, 256, 0, st>>>(X, coef_divdamp);
+        if (X.epw == 4) {
+            const int nb = col_blocks_n<LP, 4>(X, KE);
+            if (nb) k_div_damp<LP, 4><<<nb, 256, 0, st>>>(X, coef_divdamp);
+        } else if (X.epw == 2) {
+            const int nb = col_blocks_n<LP, 2>(X, KE);
+            if (nb) k_div_damp<LP, 2><<<nb, 256, 0, st>>>(X, coef_divdamp);
+        } else {
+            const int nb = col_blocks_n<LP, 1>(X, KE);
+            if (nb) k_div_damp<LP, 1><<<nb, 256, 0, st>>>(X, coef_divdamp);
+        }
     };
     HALO_RUN(S, st, run, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
     HALO_WROTE(S, F_ru_p);

@@ -12,90 +12,106 @@
 
 namespace mpas {
 
-template <int LP>
+template <int LP, int EPW>
 __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int hollingsworth_part) {
     const int L = S.L;
     const double* u = fd(S, F_u);
     const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
-    ColMap<LP> m(S, KV);
-    if (m.blk < nVB) {
-        const int v = m.ent, k = m.k;
-        if (v >= S.nVO || k >= L) return;
-        const int* eov = fi(S, F_edgesOnVertex) + (size_t)v * 3;
-        const double* sgn = fd(S, F_edgesOnVertexSign) + (size_t)v * 3;
-        int ev[3];
-        double sg_[3], dc_[3], u_[3];
-        row_ld(eov, ev);
-        row_ld(sgn, sg_);
-        row_ld(fd(S, X_ve_dc) + (size_t)v * 3, dc_);  // dcEdge(edgesOnVertex)
+    ColMapN<LP, EPW> m(S, KV);
+    const int k = m.k;
+    if (m.blk < nVB) {  // EPW vertices: vorticity, pv_vertex (:381-396)
+        int ev[EPW][3];
+        double sg_[EPW][3], dc_[EPW][3], u_[EPW][3], iat[EPW], fv[EPW];
 #pragma unroll
-        for (int i = 0; i < 3; i++) u_[i] = colk(u, ev[i]);
-        double vort = 0.0;
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            double s = sg_[i] * dc_[i];
-            vort += s * u_[i];
+        for (int j = 0; j < EPW; j++) {
+            const int v = min(m.base + j, S.nVO - 1);
+            row_ld(fi(S, F_edgesOnVertex) + (size_t)v * 3, ev[j]);
+            row_ld(fd(S, F_edgesOnVertexSign) + (size_t)v * 3, sg_[j]);
+            row_ld(fd(S, X_ve_dc) + (size_t)v * 3, dc_[j]);  // dcEdge(edgesOnVertex)
+            iat[j] = fd(S, F_invAreaTriangle)[v];
+            fv[j] = fd(S, F_fVertex)[v];
         }
-        vort *= fd(S, F_invAreaTriangle)[v];
-        const size_t p = (size_t)v * LP + k;
-        colk(fw(S, F_vorticity), v) = vort;
-        colk(fw(S, F_pv_vertex), v) = fd(S, F_fVertex)[v] + vort;
-        if (hollingsworth_part) {
-            const double* ke_edge_unused = nullptr;
-            (void)ke_edge_unused;
-            double r = 0.25 * fd(S, F_invAreaTriangle)[v];
-            double kes[3];
+#pragma unroll
+        for (int j = 0; j < EPW; j++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) u_[j][i] = colk(u, ev[j][i]);
+#pragma unroll
+        for (int j = 0; j < EPW; j++) {
+            const int v = m.base + j;
+            if (v >= S.nVO || k >= L) continue;
+            double vort = 0.0;
+#pragma unroll
             for (int i = 0; i < 3; i++) {
-                int iEdge = eov[i];
-                double efac = dcEdge[iEdge] * dvEdge[iEdge];
-                double uu = colk(u, iEdge);
-                kes[i] = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
+                double s = sg_[j][i] * dc_[j][i];
+                vort += s * u_[j][i];
             }
-            colk(fw(S, F_ke_vertex), v) = (kes[0] + kes[1] + kes[2]) * r;
+            vort *= iat[j];
+            colk(fw(S, F_vorticity), v) = vort;
+            colk(fw(S, F_pv_vertex), v) = fv[j] + vort;
+            if (hollingsworth_part) {
+                double r = 0.25 * iat[j];
+                double kes[3];
+                for (int i = 0; i < 3; i++) {
+                    int iEdge = ev[j][i];
+                    double efac = dcEdge[iEdge] * dvEdge[iEdge];
+                    double uu = u_[j][i];
+                    kes[i] = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
+                }
+                colk(fw(S, F_ke_vertex), v) = (kes[0] + kes[1] + kes[2]) * r;
+            }
         }
         return;
     }
-    const int c = col_of<LP>(m.blk - nVB) + S.lo[KC];
-    const int k = m.k;
-    if (c >= S.nCO || k >= L) return;
-    const int ne = fi(S, F_nEdgesOnCell)[c];
-    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
-    const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
-    const double invA = fd(S, F_invAreaCell)[c];
-    double div = 0.0, ke = 0.0;
-    int e_[NF];
-    double u_[NF], sgn_[NF], dv_[NF], dc_[NF];
-    row_ld(eoc, e_);
-    row_ld(sgn, sgn_);
-    row_ld(fd(S, X_ce_dv) + (size_t)c * 10, dv_);  // dvEdge(edgesOnCell)
-    row_ld(fd(S, X_ce_dc) + (size_t)c * 10, dc_);  // dcEdge(edgesOnCell)
+    // EPW cells: divergence (Q9 "s + u") and ke (:369-379, :357-367)
+    const int c0 = col_of<LP>(m.blk - nVB) * EPW + S.lo[KC];
+    int ne[EPW], e_[EPW][NF];
+    double u_[EPW][NF], sgn_[EPW][NF], dv_[EPW][NF], dc_[EPW][NF], invA[EPW];
 #pragma unroll
-    for (int i = 0; i < NF; i++) u_[i] = colk(u, e_[i]);
+    for (int j = 0; j < EPW; j++) {
+        const int c = min(c0 + j, S.nCO - 1);
+        ne[j] = fi(S, F_nEdgesOnCell)[c];
+        invA[j] = fd(S, F_invAreaCell)[c];
+        row_ld(fi(S, F_edgesOnCell) + (size_t)c * 10, e_[j]);
+        row_ld(fd(S, F_edgesOnCellSign) + (size_t)c * 10, sgn_[j]);
+        row_ld(fd(S, X_ce_dv) + (size_t)c * 10, dv_[j]);  // dvEdge(edgesOnCell)
+        row_ld(fd(S, X_ce_dc) + (size_t)c * 10, dc_[j]);  // dcEdge(edgesOnCell)
+    }
 #pragma unroll
-    for (int i = 0; i < NF; i++) {
-        const double uu = u_[i];
-        double s = sgn_[i] * dv_[i];
-        div = add_if(i < ne, div, s + uu);
-        // ke_edge(iEdge,k) exactly as the edge loop (:352) writes it; the zero slot
-        // row of ke_edge is never written, and its recomputation is 0*0*0 as well
-        double efac = dc_[i] * dv_[i];
-        double kee = (e_[i] < S.nEdges) ? efac * (uu * uu) : 0.0;
-        ke = add_if(i < ne, ke, 0.25 * kee);
+    for (int j = 0; j < EPW; j++)
+#pragma unroll
+        for (int i = 0; i < NF; i++) u_[j][i] = colk(u, e_[j][i]);
+#pragma unroll
+    for (int j = 0; j < EPW; j++) {
+        const int c = c0 + j;
+        if (c >= S.nCO || k >= L) continue;
+        double div = 0.0, ke = 0.0;
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const double uu = u_[j][i];
+            double s = sgn_[j][i] * dv_[j][i];
+            div = add_if(i < ne[j], div, s + uu);
+            // ke_edge(iEdge,k) exactly as the edge loop (:352) writes it; the zero slot
+            // row of ke_edge is never written, and its recomputation is 0*0*0 as well
+            double efac = dc_[j][i] * dv_[j][i];
+            double kee = (e_[j][i] < S.nEdges) ? efac * (uu * uu) : 0.0;
+            ke = add_if(i < ne[j], ke, 0.25 * kee);
+        }
+        const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+        const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
+        for (int i = NF; i < ne[j]; i++) {
+            int iEdge = eoc[i];
+            double uu = colk(u, iEdge);
+            double s = sgn[i] * dvEdge[iEdge];
+            div += s + uu;
+            double efac = dcEdge[iEdge] * dvEdge[iEdge];
+            double kee = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
+            ke += 0.25 * kee;
+        }
+        div *= invA[j];
+        ke *= invA[j];
+        colk(fw(S, F_divergence), c) = div;
+        colk(fw(S, F_ke), c) = ke;
     }
-    for (int i = NF; i < ne; i++) {
-        int iEdge = eoc[i];
-        double uu = colk(u, iEdge);
-        double s = sgn[i] * dvEdge[iEdge];
-        div += s + uu;
-        double efac = dcEdge[iEdge] * dvEdge[iEdge];
-        double kee = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
-        ke += 0.25 * kee;
-    }
-    div *= invA;
-    ke *= invA;
-    const size_t p = (size_t)c * LP + k;
-    colk(fw(S, F_divergence), c) = div;
-    colk(fw(S, F_ke), c) = ke;
 }
 
 // hollingsworth second half (:405-417): cells, needs ke_vertex of the whole mesh
@@ -156,8 +172,16 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
 template <int LP>
 static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
     auto kvc = [&](const DevState& X) {  // vertex blocks, then cell blocks
-        const int nv = col_blocks<LP>(X, KV), nb = nv + col_blocks<LP>(X, KC);
-        if (nb) k_solve_vc<LP><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+        if (X.epw == 4) {
+            const int nv = col_blocks_n<LP, 4>(X, KV), nb = nv + col_blocks_n<LP, 4>(X, KC);
+            if (nb) k_solve_vc<LP, 4><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+        } else if (X.epw == 2) {
+            const int nv = col_blocks_n<LP, 2>(X, KV), nb = nv + col_blocks_n<LP, 2>(X, KC);
+            if (nb) k_solve_vc<LP, 2><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+        } else {
+            const int nv = col_blocks_n<LP, 1>(X, KV), nb = nv + col_blocks_n<LP, 1>(X, KC);
+            if (nb) k_solve_vc<LP, 1><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+        }
     };
     auto kh = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);

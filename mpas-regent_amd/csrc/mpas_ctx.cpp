@@ -292,6 +292,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.nVO = dims->nVertices;
         c->S.L = dims->nVertLevels;
         c->S.LP = LP;
+        c->S.epw = 2;  // tools/kbench.py: div_damp -3 %, solve_diagnostics -4 % vs 1
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         for (int f = 0; f < X_COUNT; f++) {
@@ -355,7 +356,10 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
     return guarded(c, [&] {
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
-        else if (name && std::strcmp(name, "overlap") == 0) {
+        else if (name && std::strcmp(name, "epw") == 0) {
+            if (value != 1 && value != 2 && value != 4) throw Fail{MPAS_EINVAL, "epw must be 1, 2 or 4"};
+            c->S.epw = (int)value;
+        } else if (name && std::strcmp(name, "overlap") == 0) {
             c->overlap = value ? 1 : 0;
             if (c->halo) c->halo->overlap = c->overlap;
         } else if (name && std::strcmp(name, "self") == 0) {
@@ -370,6 +374,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         if (!value) throw Fail{MPAS_EINVAL, "mpas_get_option: null value"};
         if (name && std::strcmp(name, "exact") == 0) *value = c->exact;
         else if (name && std::strcmp(name, "xcd") == 0) *value = c->S.xcd;
+        else if (name && std::strcmp(name, "epw") == 0) *value = c->S.epw;
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "selfc") == 0) {

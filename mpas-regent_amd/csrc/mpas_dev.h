@@ -69,8 +69,9 @@ struct DevState {
                         // grid (= the counts above unless the mesh is decomposed)
     int lo[3];          // first cell / edge / vertex of a launch: kernels compute entities
                         // [lo, nXO); 0 except for the boundary launch of a halo overlap
-    int xcd;  // 1: XCD-aware block order, 0: dispatcher order (default: measured faster,
-              // the Morton-ordered columns of all XCDs then share one Infinity-Cache window)
+    int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
+    int xcd;  // block order: 0 dispatcher, 1 one contiguous eighth per XCD, G > 1 runs of G
+              // blocks per XCD in windows of 8G (default 64)
     int selfc;  // 1 when every cell is one of the two cellsOnEdge of each of its first
                 // min(nEdgesOnCell, NF) edges (k_prepare): the cell kernels then gather
                 // only the other cell of an edge and use their own column for the cell
@@ -118,6 +119,13 @@ inline int col_blocks(const DevState& S, int kind) {
     const int end = kind == KC ? S.nCO : kind == KE ? S.nEO : S.nVO;
     const int n = end - S.lo[kind];
     return n > 0 ? (n + 256 / LP - 1) / (256 / LP) : 0;
+}
+
+template <int LP, int EPW>
+inline int col_blocks_n(const DevState& S, int kind) {
+    const int end = kind == KC ? S.nCO : kind == KE ? S.nEO : S.nVO;
+    const int n = end - S.lo[kind], per = (256 / LP) * EPW;
+    return n > 0 ? (n + per - 1) / per : 0;
 }
 
 // ---- launchers (each returns the hipGetLastError of its launches) ----
@@ -178,6 +186,20 @@ struct ColMap {
     __device__ __forceinline__ ColMap(const DevState& S, int kind) {
         blk = xcd_block(S.xcd);
         ent = col_of<LP>(blk) + S.lo[kind];
+        k = (int)(threadIdx.x % LP);
+    }
+};
+
+// EPW consecutive entities per column slot: the kernels with only a few gathers per
+// entity issue the loads of EPW entities together (more memory requests in flight per
+// wavefront; a one-entity wave of such a kernel is latency-bound)
+template <int LP, int EPW>
+struct ColMapN {
+    static constexpr int COLS = 256 / LP;
+    int blk, base, k;
+    __device__ __forceinline__ ColMapN(const DevState& S, int kind) {
+        blk = xcd_block(S.xcd);
+        base = col_of<LP>(blk) * EPW + S.lo[kind];
         k = (int)(threadIdx.x % LP);
     }
 };

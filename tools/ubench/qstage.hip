@@ -257,6 +257,54 @@ __global__ __launch_bounds__(256) void qv5(const double* u, const double* pv, co
     }
 }
 
+
+// qv5 with the staging done by LDS-DMA (global_load_lds_dwordx4: one wave-instruction
+// copies two 512-B rows, lanes 0-31 the first, 32-63 the second; no VGPRs, so every wave
+// keeps all its rows in flight)
+template <int E, int MAXU>
+__global__ __launch_bounds__(256) void qv6(const double* u, const double* pv, const int* eoe, const double* w, int nE,
+                                           double* out, const int* blk_off, const int* blk_n, const int* ulist,
+                                           const uint8_t* lslot) {
+    __shared__ double su[MAXU * 64];
+    __shared__ double sv[MAXU * 64];
+    const int b = blockIdx.x;
+    const int off = blk_off[b], n = min(blk_n[b], MAXU);
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int lane = threadIdx.x & 63, k = lane;
+    for (int s0 = 2 * wv; s0 < n; s0 += 8) {
+        const int r = min(s0 + (lane >> 5), n - 1);
+        const int g = ulist[off + r];
+        const double* src_u = u + (size_t)g * 64 + (lane & 31) * 2;
+        const double* src_v = pv + (size_t)g * 64 + (lane & 31) * 2;
+        __builtin_amdgcn_global_load_lds((const void*)src_u, (__attribute__((address_space(3))) void*)(su + s0 * 64), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)src_v, (__attribute__((address_space(3))) void*)(sv + s0 * 64), 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+    __syncthreads();
+    if (k >= 56) return;
+    for (int i = 0; i < E / 4; i++) {
+        const int e = __builtin_amdgcn_readfirstlane(b * E + i * 4 + wv);
+        if (e >= nE) return;
+        const uint8_t* ls = lslot + (size_t)e * 11;
+        uint32_t sl[11];
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < 11; j++) {
+            sl[j] = ls[j];
+            ok = ok && sl[j] != 255u;
+        }
+        if (ok) {
+            const double p0 = sv[sl[10] * 64 + k];
+            double q = 0;
+#pragma unroll
+            for (int j = 0; j < 10; j++) q += w[e * 10 + j] * su[sl[j] * 64 + k] * 0.5 * (p0 + sv[sl[j] * 64 + k]);
+            sp(out + (size_t)e * 64)[k] = q;
+        } else {
+            q_edge(e, k, u, pv, eoe, w, out);
+        }
+    }
+}
+
 extern "C" int ub_q(int variant, const double* u, const double* pv, const int* eoe, const double* w, int nE,
                     double* out, const int* blk_off, const int* blk_n, const int* ulist, const uint16_t* lidx,
                     const uint16_t* lself, void* stream) {
@@ -289,6 +337,9 @@ extern "C" int ub_q(int variant, const double* u, const double* pv, const int* e
         case 24: qv5<16, 64><<<(nE + 15) / 16, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
         case 25: qv5<16, 48><<<(nE + 15) / 16, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
         case 26: qv5<32, 96><<<(nE + 31) / 32, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
+        case 27: qv6<16, 64><<<(nE + 15) / 16, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
+        case 28: qv6<16, 48><<<(nE + 15) / 16, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
+        case 29: qv6<32, 96><<<(nE + 31) / 32, 256, 0, st>>>(u, pv, eoe, w, nE, out, blk_off, blk_n, ulist, (const uint8_t*)lidx); break;
         default: return -1;
     }
     return (int)hipGetLastError();

@@ -73,8 +73,8 @@ def main():
         lists[(E, maxu)].append(float((sl == 255).any(axis=1).mean()))
     res = {}
     ref = None
-    vars_ = [int(x) for x in os.environ.get('QVARS', '0,1,16,21,24,25,26').split(',')]
-    for var, E in [(v, {4: 32, 5: 32, 20: 32, 21: 32, 22: 64, 23: 64, 24: (16, 64), 25: (16, 48), 26: (32, 96)}.get(v, 16)) for v in vars_]:
+    vars_ = [int(x) for x in os.environ.get('QVARS', '0,16,24,25,27,28,29').split(',')]
+    for var, E in [(v, {4: 32, 5: 32, 20: 32, 21: 32, 22: 64, 23: 64, 24: (16, 64), 25: (16, 48), 26: (32, 96), 27: (16, 64), 28: (16, 48), 29: (32, 96)}.get(v, 16)) for v in vars_]:
         L = lists[E]
         out = torch.zeros((nE + 1) * 64, dtype=torch.float64, device=dev)
         ts = []
