@@ -266,9 +266,12 @@ static thread_local std::string g_create_err;
 int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
     if (!out || !dims) return MPAS_EINVAL;
     *out = nullptr;
-    if (dims->nCells <= 0 || dims->nEdges <= 0 || dims->nVertices <= 0 || dims->nVertLevels < 2 ||
-        dims->nVertLevels + 1 > 64)
+    if (dims->nCells <= 0 || dims->nEdges <= 0 || dims->nVertices <= 0 || dims->nVertLevels < 1 ||
+        dims->nVertLevels + 1 > 64) {
+        g_create_err = "mpas_ctx_create: need nCells, nEdges, nVertices > 0 and 1 <= nVertLevels <= 63 "
+                       "(one wavefront holds a column of nVertLevels + 1 levels)";
         return MPAS_EINVAL;
+    }
     mpas_ctx* c = new (std::nothrow) mpas_ctx();
     if (!c) return MPAS_ENOMEM;
     int rc = guarded(c, [&] {

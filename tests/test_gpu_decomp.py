@@ -176,3 +176,15 @@ def test_overlap_morton_mesh(nparts):
         got, stats = run_decomposed(st, nparts, two_steps, 0, overlap=overlap)
         bad = compare_states(got, ref, rtol=0.0)
         assert not bad, (overlap, bad[:6])
+
+
+def test_ragged_partition(x1_2562):
+    """very uneven subdomains (one rank owns 3 cells): ranges with few or no interior
+    entities, near-empty launches; still bit-identical to the single context"""
+    st = state(x1_2562, 5, "random")
+    part = np.zeros(st.nCells, dtype=np.int32)
+    part[-3:] = 1
+    ref = run_single(st, lambda c: T.atm_srk3(c, 720.0, 1), 1)
+    got, _ = run_decomposed(st, 2, lambda c: T.atm_srk3(c, 720.0, 1), 1, cell_part=part)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]

@@ -249,3 +249,35 @@ def test_summarize_timestep(x1_2562, L, case):
         assert np.array_equal(np.isnan(got), np.isnan(ref)), (detailed, global_vel)
         ok = np.where(np.isnan(ref), True, (got == ref) & (np.signbit(got) == np.signbit(ref)))
         assert ok.all(), f"summarize {case} {detailed}{global_vel}: {np.nonzero(~ok)[0]} {got[~ok]} vs {ref[~ok]}"
+
+
+# ---- edge cases: the smallest and the largest column the device layout holds -----------
+@pytest.mark.parametrize("L", [1, 2, 63])
+@pytest.mark.parametrize("variant", ["random", "ref"])
+def test_srk3_level_extremes(x1_2562, L, variant):
+    """nVertLevels = 1 and 2 (most vertical stencils degenerate: flux3 never applies, the
+    acoustic recurrence is empty) and 63 (LP = 64: level L sits in the last lane of the
+    wavefront, every shuffle edge case at the top); whole RK3 steps, exact and fast"""
+    st = make_state(x1_2562, L, variant)
+    ref = run_oracle(st, lambda o: o.atm_srk3(720.0, 1))
+    got = run_gpu(st, lambda c: T.atm_srk3(c, 720.0, 1), exact=1)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, f"L={L} exact: {bad[:6]}"
+    got = run_gpu(st, lambda c: T.atm_srk3(c, 720.0, 1), exact=0)
+    bad = compare_states(got, ref, rtol=RTOL_STEP)
+    assert not bad, f"L={L} fast: {bad[:6]}"
+
+
+def test_nonfinite_inputs_propagate(x1_2562):
+    """NaN and inf in the state propagate through a step exactly where the oracle puts
+    them (the select-based accumulations must not swallow or invent non-finite values)"""
+    st = make_state(x1_2562, 5, "random").copy()
+    st["theta_m"][17, 2] = np.nan
+    st["u"][333, 1] = np.inf
+    st["rw"][1200, 3] = -np.inf
+    st["pressure_p"][2000, 0] = np.nan
+    ref = run_oracle(st, lambda o: o.atm_srk3(720.0, 1))
+    got = run_gpu(st, lambda c: T.atm_srk3(c, 720.0, 1), exact=1)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+    assert np.isnan(ref["tend_theta"]).any()
