@@ -32,7 +32,6 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     const bool kl = k < L;
     // ---- every load of the column and of its edge gathers first, ahead of the first
     // store (which could alias them for the compiler)
-    const int ne = fi(S, F_nEdgesOnCell)[c];
     const double spec = fd(S, F_specZoneMaskCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
@@ -43,14 +42,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
     int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
     double sgn_[NF], cdv_[NF], rup_[NF], t1_[NF], t2_[NF];
-    row_ld(eoc, e_);
-    if (SELF) {
-        row_ld(coth, o_);
-        row_ld(cs1, s1_);
-    } else {
-        row_ld(cc1, c1_);
-        row_ld(cc2, c2_);
-    }
+    const int ne = SELF ? cell_rec<true>(S, c, e_, o_, s1_) : cell_rec<false>(S, c, e_, c1_, c2_);
     row_ld(sgn, sgn_);
     row_ld(cdv, cdv_);
     double rtp = col_rd<LP>(rtp_f, c, k, L), rpp = col_rd<LP>(rpp_f, c, k, L);

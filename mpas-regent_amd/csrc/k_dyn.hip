@@ -53,7 +53,6 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     const size_t p = (size_t)c * LP + k;
     constexpr bool rk0 = RK0;
     const bool live = k <= L;
-    const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
     const double* cdv = fd(S, X_ce_dv) + (size_t)c * 10;
@@ -64,7 +63,8 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     int e_[NF];
     double ru_[NF], u_[NF], v_[NF], eocs_[NF], cdv_[NF], wfl[2];
     row_ld(fd(S, X_wfl) + (size_t)c * 2, wfl);
-    row_ld(eoc, e_);
+    int c1_[NF], c2_[NF];  // unused: the record's edges and count
+    const int ne = cell_rec<false>(S, c, e_, c1_, c2_);
     row_ld(eocs, eocs_);
     row_ld(cdv, cdv_);
 #pragma unroll
@@ -187,7 +187,10 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const size_t p = (size_t)e * LP + k;
     constexpr bool rk0 = RK0;
     const bool live = k <= L;
-    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    // the edge's index lists in one record (X_eB): one scalar round trip
+    int rec[24];
+    row_ld(fi(S, X_eB) + (size_t)e * 24, rec);
+    const int cell1 = rec[0], cell2 = rec[1];
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
     const double invDc = fd(S, F_invDcEdge)[e];
     const double *u_f = fd(S, F_u), *pv_f = fd(S, F_pv_edge), *tm_f = fd(S, F_theta_m);
@@ -200,12 +203,13 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const double w1 = ldz(live, colk(fd(S, F_w), cell1)), w2 = ldz(live, colk(fd(S, F_w), cell2));
     const double rho_edge = ldz(live, colk(fd(S, F_rho_edge), e));
     const double wduzL = fd(S, F_wduz)[(size_t)e * LP + L];  // one value: the level-L slot
-    const int neoe = fi(S, F_nEdgesOnEdge)[e];
+    const int neoe = rec[21];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
     int ee_[QF];
     double ue_[QF], pve_[QF], woe_[QF];
-    row_ld(eoe, ee_);
+#pragma unroll
+    for (int j = 0; j < QF; j++) ee_[j] = rec[2 + j];
     row_ld(woe, woe_);
     const bool kl = k < L;
 #pragma unroll
@@ -214,13 +218,14 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         pve_[j] = ldz(kl, colk(pv_f, ee_[j]));
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
-    const int na = fi(S, F_nAdvCellsForEdge)[e];
+    const int na = rec[22];
     const int* ad = fi(S, F_advCellsForEdge) + (size_t)e * 15;
     const double* ac = fd(S, F_adv_coefs) + (size_t)e * 15;
     const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e * 15;
     int ad_[AF];
     double tv_[AF], ac_[AF], ac3_[AF];
-    row_ld(ad, ad_);
+#pragma unroll
+    for (int j = 0; j < AF; j++) ad_[j] = rec[12 + j];
     row_ld(ac, ac_);
     row_ld(ac3, ac3_);
 #pragma unroll
@@ -362,7 +367,6 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + k;
     const bool live = k <= L, kl = k < L;
-    const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
     const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
@@ -376,14 +380,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
     double re_[NF], kd1_[NF], kd2_[NF], wc1_[NF], wc2_[NF], t1_[NF], t2_[NF], ds_[NF];
     double eocs_[NF], cdv_[NF], cidc_[NF], cmsd2_[NF];
-    row_ld(eoc, e_);
-    if (SELF) {
-        row_ld(coth, o_);
-        row_ld(cs1, s1_);
-    } else {
-        row_ld(cc1, c1_);
-        row_ld(cc2, c2_);
-    }
+    const int ne = SELF ? cell_rec<true>(S, c, e_, o_, s1_) : cell_rec<false>(S, c, e_, c1_, c2_);
     row_ld(eocs, eocs_);
     row_ld(cdv, cdv_);
     row_ld(cidc, cidc_);
@@ -487,7 +484,6 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     const size_t p = (size_t)c * LP + k;
     constexpr bool rk0 = RK0;
     const bool kl = k < L;
-    const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
     const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
@@ -504,14 +500,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
     double ru_[NF], F_[NF], rus_[NF], ts1_[NF], ts2_[NF], dw1_[NF], dw2_[NF], dt1_[NF], dt2_[NF];
     double eocs_[NF], cdv_[NF], cidc_[NF], cmsd4_[NF];
-    row_ld(eoc, e_);
-    if (SELF) {
-        row_ld(coth, o_);
-        row_ld(cs1, s1_);
-    } else {
-        row_ld(cc1, c1_);
-        row_ld(cc2, c2_);
-    }
+    const int ne = SELF ? cell_rec<true>(S, c, e_, o_, s1_) : cell_rec<false>(S, c, e_, c1_, c2_);
     row_ld(eocs, eocs_);
     row_ld(cdv, cdv_);
     if (rk0) {

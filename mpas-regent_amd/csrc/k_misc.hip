@@ -328,6 +328,17 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
     const int* coe = fi(S, F_cellsOnEdge);
     for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.nVertices * 3; t += (size_t)gridDim.x * 256)
         fw(S, X_ve_dc)[t] = fd(S, F_dcEdge)[fi(S, F_edgesOnVertex)[t]];
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.nEdges * 24; t += (size_t)gridDim.x * 256) {
+        const size_t e = t / 24;
+        const int j = (int)(t % 24);
+        int v = 0;
+        if (j < 2) v = coe[e * 2 + j];
+        else if (j < 12) v = fi(S, F_edgesOnEdge)[e * 20 + (j - 2)];
+        else if (j < 21) v = fi(S, F_advCellsForEdge)[e * 15 + (j - 12)];
+        else if (j == 21) v = fi(S, F_nEdgesOnEdge)[e];
+        else if (j == 22) v = fi(S, F_nAdvCellsForEdge)[e];
+        ((int*)S.f[X_eB])[t] = v;
+    }
     for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (size_t)gridDim.x * 256) {
         const int e = eoc[t], c = (int)(t / 10), i = (int)(t % 10);
         const int c1 = coe[(size_t)e * 2], c2 = coe[(size_t)e * 2 + 1];
@@ -336,6 +347,19 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
         ((int*)S.f[X_ce_oth])[t] = (c1 == c) ? c2 : c1;
         ((int*)S.f[X_ce_s1])[t] = (c1 == c) ? 1 : 0;
         if (c < S.nCO && i < fi(S, F_nEdgesOnCell)[c] && i < NF && c1 != c && c2 != c) atomicAnd(selfc, 0);
+        if (i < NF) {
+            int* r = (int*)S.f[X_cR] + (size_t)c * CREC;
+            int* rs = (int*)S.f[X_cRs] + (size_t)c * CREC;
+            r[i] = rs[i] = e;
+            r[NF + i] = c1;
+            r[2 * NF + i] = c2;
+            rs[NF + i] = (c1 == c) ? c2 : c1;
+            rs[2 * NF + i] = (c1 == c) ? 1 : 0;
+            if (i == 0) {
+                r[3 * NF] = rs[3 * NF] = fi(S, F_nEdgesOnCell)[c];
+                r[3 * NF + 1] = rs[3 * NF + 1] = 0;
+            }
+        }
         fw(S, X_ce_dv)[t] = fd(S, F_dvEdge)[e];
         fw(S, X_ce_dc)[t] = fd(S, F_dcEdge)[e];
         fw(S, X_ce_idc)[t] = fd(S, F_invDcEdge)[e];

@@ -37,6 +37,9 @@ const FieldInfo kFields[X_COUNT] = {
     {"ce_msd4", K_C2F, 10, D_M, 0, 0},
     {"ce_oth", K_C2I, 10, D_M, 0, 0},
     {"ce_s1", K_C2I, 10, D_M, 0, 0},
+    {"eB", K_E2I, 24, D_M, 0, 0},
+    {"cR", K_C2I, CREC, D_M, 0, 0},
+    {"cRs", K_C2I, CREC, D_M, 0, 0},
     {"wfl", K_C2F, 2, D_M, 0, 0},
     {"wc", K_C3, 1, D_M, 0, 0},
     {"F", K_E3, 1, D_M, 0, 0},

@@ -44,6 +44,13 @@ enum FieldId {
     X_ce_msd4,  // meshScalingDel4(edgesOnCell(i,c))     C2F x10
     X_ce_oth,   // the cell of cellsOnEdge(edgesOnCell(i,c), 0:1) that is not c   C2I x10
     X_ce_s1,    // 1 if cellsOnEdge(edgesOnCell(i,c), 0) == c                     C2I x10
+    X_eB,       // per edge, the index lists of dyn_tend's edge kernel in one record:
+                // cellsOnEdge(2), edgesOnEdge(10), advCellsForEdge(9), nEdgesOnEdge,
+                // nAdvCellsForEdge, 0 -- one scalar round trip instead of three   E2I x24
+    X_cR,       // per cell, one record of its first NF edges: edgesOnCell(NF), cell1(NF),
+                // cell2(NF) of each, nEdgesOnCell, 0                             C2I x(3NF+2)
+    X_cRs,      // the same for the SELF path: edgesOnCell(NF), other cell(NF),
+                // "cell is cell1"(NF), nEdgesOnCell, 0                           C2I x(3NF+2)
     X_wfl,      // dyn_tend's w-advection flux_arr over the advCells of the cell's last
                 // edge, sum_j (adv_coefs + s adv_coefs_3rd) * 0.0 for s = +1, -1      C2F x2
     // scratch (not reference fields)
@@ -296,6 +303,22 @@ template <int N, class T>
 __device__ __forceinline__ void row_ld(const T* p, T (&r)[N]) {
 #pragma unroll
     for (int i = 0; i < N; i++) r[i] = p[i];
+}
+
+// a cell's first NF edges and their cells from its record (X_cR / X_cRs): one scalar
+// round trip; a_/b_ = cell1/cell2 of each edge, or (SELF) the other cell / "cell is cell1"
+constexpr int CREC = 3 * NF + 2;
+template <bool SELF>
+__device__ __forceinline__ int cell_rec(const DevState& S, int c, int (&e_)[NF], int (&a_)[NF], int (&b_)[NF]) {
+    int r[CREC];
+    row_ld(fi(S, SELF ? X_cRs : X_cR) + (size_t)c * CREC, r);
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        e_[i] = r[i];
+        a_[i] = r[NF + i];
+        b_[i] = r[2 * NF + i];
+    }
+    return r[3 * NF];
 }
 
 // column read with the level policy: levels outside 0..L read 0.0

@@ -11,7 +11,7 @@ import numpy as np
 from .registry import FIELDS, BY_NAME, F_COUNT
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmpasdyn.so")
+LIB_PATH = os.environ.get("MPAS_LIB") or os.path.join(HERE, "libmpasdyn.so")  # MPAS_LIB: A/B of two builds (tools/)
 
 # every symbol include/mpas_dyn.h declares (checked by tests/test_abi.py)
 EXPORTS = [
