@@ -24,7 +24,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
-    const size_t p = (size_t)c * LP + k;
+    const size_t p = (size_t)c * LP + lpos(LP, k);
     double* rtp_f = fw(S, F_rtheta_pp);
     double* rpp_f = fw(S, F_rho_pp);
     double* rwp_f = fw(S, F_rw_p);

@@ -24,7 +24,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
-    if (m.blk == 0 && (int)threadIdx.x < L) fw(S, F_rho_zz)[(size_t)S.nCells * LP + threadIdx.x] = 1.0;
+    if (m.blk == 0 && (int)threadIdx.x < L) fw(S, F_rho_zz)[(size_t)S.nCells * LP + lpos(LP, threadIdx.x)] = 1.0;
     if (c >= S.nCO) return;
     const bool kl = k < L;
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
     for (int i = 0; i < 10; i++) {
         const double r = col_rd<LP>(ru, e_[i], k, L), r_m = lvl_dn<LP>(r, k);
         const double r0 = __shfl(r, 0, LP), r1 = __shfl(r, 1, LP), r2 = __shfl(r, 2, LP);
-        const double z = zb[((size_t)c * 10 + i) * LP + k], z3 = zb3[((size_t)c * 10 + i) * LP + k];
+        const double z = zb[((size_t)c * 10 + i) * LP + lpos(LP, k)], z3 = zb3[((size_t)c * 10 + i) * LP + lpos(LP, k)];
         zb0_[i] = __shfl(z, 0, LP);
         zb30_[i] = __shfl(z3, 0, LP);
         const double flux = (cf1 * r0 + cf2 * r1 + cf3 * r2);
@@ -284,11 +284,11 @@ __global__ __launch_bounds__(256) void k_sum_scan(DevState S, int which, long ch
     part_init(p);
     for (long idx = t * chunk; idx < n && idx < (t + 1) * chunk; idx++) {
         const long ent = idx / S.L, k = idx - ent * S.L;
-        const double xv = x[ent * LP + k];
+        const double xv = x[ent * LP + lpos(LP, k)];
         if (xv < p.mn.v) p.mn = {xv, idx};
         if (xv > p.mx.v) p.mx = {xv, idx};
         if (which == 1) {
-            const double yv = y[ent * LP + k];
+            const double yv = y[ent * LP + lpos(LP, k)];
             const double spd = sqrt(xv * xv + yv * yv);
             if (spd > p.spd.v) p.spd = {spd, idx};
         }

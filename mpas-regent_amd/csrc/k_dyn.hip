@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
-    const size_t p = (size_t)c * LP + k;
+    const size_t p = (size_t)c * LP + lpos(LP, k);
     constexpr bool rk0 = RK0;
     const bool live = k <= L;
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
-    const size_t p = (size_t)e * LP + k;
+    const size_t p = (size_t)e * LP + lpos(LP, k);
     constexpr bool rk0 = RK0;
     const bool live = k <= L;
     // the edge's index lists in one record (X_eB): one scalar round trip
@@ -194,15 +194,23 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
     const double invDc = fd(S, F_invDcEdge)[e];
     const double *u_f = fd(S, F_u), *pv_f = fd(S, F_pv_edge), *tm_f = fd(S, F_theta_m);
-    const size_t p1 = (size_t)cell1 * LP + k, p2 = (size_t)cell2 * LP + k;
+    const size_t p1 = (size_t)cell1 * LP + lpos(LP, k), p2 = (size_t)cell2 * LP + lpos(LP, k);
 
     // ---- issue every independent load of the column first
-    const double u = ldz(live, colk(u_f, e));
-    const double ru_e = ldz(live, colk(fd(S, F_ru), e));
-    const double rw1 = ldz(live, colk(fd(S, F_rw), cell1)), rw2 = ldz(live, colk(fd(S, F_rw), cell2));
-    const double w1 = ldz(live, colk(fd(S, F_w), cell1)), w2 = ldz(live, colk(fd(S, F_w), cell2));
-    const double rho_edge = ldz(live, colk(fd(S, F_rho_edge), e));
-    const double wduzL = fd(S, F_wduz)[(size_t)e * LP + L];  // one value: the level-L slot
+    // (gather2: two columns per load instruction)
+    double u, ru_e, rw1, rw2, w1, w2, rho_edge, pv;
+    gather2<LP>(u_f, e, fd(S, F_ru), e, k, u, ru_e);
+    gather2<LP>(fd(S, F_rw), cell1, fd(S, F_rw), cell2, k, rw1, rw2);
+    gather2<LP>(fd(S, F_w), cell1, fd(S, F_w), cell2, k, w1, w2);
+    gather2<LP>(fd(S, F_rho_edge), e, pv_f, e, k, rho_edge, pv);
+    u = ldz(live, u);
+    ru_e = ldz(live, ru_e);
+    rw1 = ldz(live, rw1);
+    rw2 = ldz(live, rw2);
+    w1 = ldz(live, w1);
+    w2 = ldz(live, w2);
+    rho_edge = ldz(live, rho_edge);
+    const double wduzL = fd(S, F_wduz)[(size_t)e * LP + lpos(LP, L)];  // one value: the level-L slot
     const int neoe = rec[21];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
@@ -214,8 +222,9 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     const bool kl = k < L;
 #pragma unroll
     for (int j = 0; j < QF; j++) {
-        ue_[j] = ldz(kl, colk(u_f, ee_[j]));
-        pve_[j] = ldz(kl, colk(pv_f, ee_[j]));
+        gather2<LP>(u_f, ee_[j], pv_f, ee_[j], k, ue_[j], pve_[j]);
+        ue_[j] = ldz(kl, ue_[j]);
+        pve_[j] = ldz(kl, pve_[j]);
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = rec[22];
@@ -228,16 +237,20 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     for (int j = 0; j < AF; j++) ad_[j] = rec[12 + j];
     row_ld(ac, ac_);
     row_ld(ac3, ac3_);
+    static_assert(AF == 9, "tv_ pairing below");
+    double tr_phys;
 #pragma unroll
-    for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, colk(tm_f, ad_[j]));
+    for (int j = 0; j < AF - 1; j += 2) gather2<LP>(tm_f, ad_[j], tm_f, ad_[j + 1], k, tv_[j], tv_[j + 1]);
+    gather2<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k, tv_[AF - 1], tr_phys);
+#pragma unroll
+    for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, tv_[j]);
 
     // loads of the later sections, also ahead of every store (a store could alias them
     // for the compiler, which would then issue them only after it)
     const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
-    const double pv = colk(pv_f, e);
-    const double ke1 = colk(ke_f, cell1), ke2 = colk(ke_f, cell2);
-    const double hd1 = colk(hd_f, cell1), hd2 = colk(hd_f, cell2);
-    const double tr_phys = colk(fd(S, F_tend_ru_physics), e);
+    double ke1, ke2, hd1, hd2;
+    gather2<LP>(ke_f, cell1, ke_f, cell2, k, ke1, ke2);
+    gather2<LP>(hd_f, cell1, hd_f, cell2, k, hd1, hd2);
     // (the rk0-only loads stay in their section: hoisted they cost more in occupancy,
     // 138 VGPRs, than the second memory round trip)
     const double tue_in = rk0 ? 0.0 : colk(fd(S, F_tend_u_euler), e);
@@ -352,7 +365,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         row_ld(sgn, sg_);
         row_ld(fd(S, X_ve_dc) + (size_t)vx * 3, dc_);  // dcEdge(edgesOnVertex)
 #pragma unroll
-        for (int i = 0; i < 3; i++) d[i] = dsu[(size_t)ev[i] * LP + k];
+        for (int i = 0; i < 3; i++) d[i] = dsu[(size_t)ev[i] * LP + lpos(LP, k)];
         double dsv = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; i++) {
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int c = col_of<LP>(m.blk - nVB) + S.lo[KC];
     const int k = m.k;
     if (c >= S.nCO) return;
-    const size_t p = (size_t)c * LP + k;
+    const size_t p = (size_t)c * LP + lpos(LP, k);
     const bool live = k <= L, kl = k < L;
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* eocs = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
@@ -457,7 +470,7 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO || k >= L) return;
-    const size_t p = (size_t)e * LP + k;
+    const size_t p = (size_t)e * LP + lpos(LP, k);
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
     const double invDc = fd(S, F_invDcEdge)[e];
@@ -481,7 +494,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
-    const size_t p = (size_t)c * LP + k;
+    const size_t p = (size_t)c * LP + lpos(LP, k);
     constexpr bool rk0 = RK0;
     const bool kl = k < L;
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
@@ -531,7 +544,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     }
     const double wc = ldz(kl, colk(fd(S, X_wc), c));
     const double rw = col_rd<LP>(fd(S, F_rw), c, k, L);
-    const double wdwzL = fd(S, F_wdwz)[(size_t)c * LP + L], wdtzL = fd(S, F_wdtz)[(size_t)c * LP + L];  // level-L slots
+    const double wdwzL = fd(S, F_wdwz)[(size_t)c * LP + lpos(LP, L)], wdtzL = fd(S, F_wdtz)[(size_t)c * LP + lpos(LP, L)];  // level-L slots
     const double pp = col_rd<LP>(fd(S, F_pressure_p), c, k, L), dpdz = col_rd<LP>(fd(S, F_dpdz), c, k, L);
     const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L);
     const double tms = col_rd<LP>(tms_f, c, k, L), tmv = col_rd<LP>(tm, c, k, L);

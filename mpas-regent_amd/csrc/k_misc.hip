@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
     double *rws = fw(S, F_rw_save), *rtps = fw(S, F_rtheta_p_save), *rps = fw(S, F_rho_p_save);
     double *w2 = fw(S, F_w_2), *tm2 = fw(S, F_theta_m_2), *rz2 = fw(S, F_rho_zz_2), *rzo = fw(S, F_rho_zz_old_split);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if ((int)(i % S.LP) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
         rws[i] = rw[i];
         rtps[i] = rtp[i];
         rps[i] = rp[i];
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_setup_edges(DevState S) {
     const double *ru = fd(S, F_ru), *u = fd(S, F_u);
     double *rus = fw(S, F_ru_save), *u2 = fw(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if ((int)(i % S.LP) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
         rus[i] = ru[i];
         u2[i] = u[i];
     }
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_moist(DevState S) {
     const size_t n = (size_t)S.nCO * S.LP;
     double *qtot = fw(S, F_qtot), *cqw = fw(S, F_cqw);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        int k = (int)(i % S.LP);
+        int k = plev(S.LP, (int)(i % S.LP));
         if (k >= S.L) continue;
         qtot[i] = 0.0;  // :473-482
         if (k > 0) {    // :484-489, qtot(k) and qtot(k-1) were both just zeroed
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
-    const size_t p = (size_t)c * LP + k;
+    const size_t p = (size_t)c * LP + lpos(LP, k);
     const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
     const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
     const double rdzw_m = k > 0 ? rdzw_a[k - 1] : 0.0;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
-    const size_t p = (size_t)c * LP + k;
+    const size_t p = (size_t)c * LP + lpos(LP, k);
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* sgn = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         ut_[i] = col_rd<LP>(ut_f, e_[i], k, L);
-        size_t q = ((size_t)c * 10 + i) * LP + k;
+        size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
         zb_[i] = zb[q];
         zb3_[i] = zb3[q];
     }
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
         double ut = col_rd<LP>(ut_f, iEdge, k, L);
         double ut_m = lvl_dn<LP>(ut, k);
         double flux = sgn[i] * (fzm * ut + fzp * ut_m);
-        size_t q = ((size_t)c * 10 + i) * LP + k;
+        size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
         w -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
     }
     w *= (fzm * zz + fzp * zz_m);
@@ -281,7 +281,7 @@ __global__ __launch_bounds__(256) void k_finish_edges(DevState S, int substep, i
     double *ru_save = fw(S, F_ru_save), *u = fw(S, F_u), *ruAvg = fw(S, F_ruAvg), *ruAvgS = fw(S, F_ruAvg_split);
     const double *ru = fd(S, F_ru), *u2 = fd(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if ((int)(i % S.LP) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
         if (substep < split) {
             ru_save[i] = ru[i];
             u[i] = u2[i];
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
     const size_t n = (size_t)S.nCO * S.LP;
     double *wwAvg = fw(S, F_wwAvg), *wwAvgS = fw(S, F_wwAvg_split), *rho_zz = fw(S, F_rho_zz);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if ((int)(i % S.LP) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
         if (substep < split) {
             fw(S, F_rw_save)[i] = fd(S, F_rw)[i];
             fw(S, F_rtheta_p_save)[i] = fd(S, F_rtheta_p)[i];
@@ -415,8 +415,8 @@ __global__ __launch_bounds__(256) void k_fill(void* dst, int fid, int kind, long
         const long g = gid ? (long)gid[e] : e;  // the global entity id: same value on every rank
         double v = mpas_synth_value(seed, (uint32_t)fid, (uint64_t)g, (uint32_t)k, (uint32_t)i, dist, lo, hi);
         if (kind == K_ZV) d[k] = v;
-        else if (kind == K_C3V) d[((size_t)e * W + i) * LP + k] = v;
-        else d[(size_t)e * LP + k] = v;
+        else if (kind == K_C3V) d[((size_t)e * W + i) * LP + lpos(LP, k)] = v;
+        else d[(size_t)e * LP + lpos(LP, k)] = v;
     }
 }
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed) {

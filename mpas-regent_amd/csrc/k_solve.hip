@@ -120,7 +120,7 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
     ColMap<LP> m(S, KC);
     const int L = S.L, c = m.ent, k = m.k;
     if (c >= S.nCO || k >= L) return;
-    const size_t p = (size_t)c * LP + k;
+    const size_t p = (size_t)c * LP + lpos(LP, k);
     double ke_fact = 1.0 - 0.375;
     double ke = colk(fd(S, F_ke), c) * ke_fact;
     double r = fd(S, F_invAreaCell)[c];

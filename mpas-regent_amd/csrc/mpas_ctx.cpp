@@ -409,17 +409,17 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
         if (fi.kind == K_C3 || fi.kind == K_E3 || fi.kind == K_V3) {
             double* d = (double*)buf.data();
             for (int e = 0; e < n; e++)
-                for (int k = 0; k <= L; k++) d[(size_t)e * LP + k] = *(const double*)(h + e * se + k * sl);
+                for (int k = 0; k <= L; k++) d[(size_t)e * LP + lpos(LP, k)] = *(const double*)(h + e * se + k * sl);
         } else if (fi.kind == K_C3V) {
             double* d = (double*)buf.data();
             for (int e = 0; e < n; e++)
                 for (int i = 0; i < W; i++)
                     for (int k = 0; k <= L; k++)
-                        d[((size_t)e * W + i) * LP + k] = *(const double*)(h + e * se + k * sl + i * sc);
+                        d[((size_t)e * W + i) * LP + lpos(LP, k)] = *(const double*)(h + e * se + k * sl + i * sc);
         } else if (fi.kind == K_C3B) {
             uint8_t* d = (uint8_t*)buf.data();
             for (int e = 0; e < n; e++)
-                for (int k = 0; k <= L; k++) d[(size_t)e * LP + k] = *(const uint8_t*)(h + e * se + k * sl);
+                for (int k = 0; k <= L; k++) d[(size_t)e * LP + lpos(LP, k)] = *(const uint8_t*)(h + e * se + k * sl);
         } else if (fi.kind == K_ZV) {
             double* d = (double*)buf.data();
             for (int k = 0; k <= L; k++) d[k] = *(const double*)(h + k * sl);
@@ -470,17 +470,17 @@ int mpas_download(mpas_ctx* c, int f, void* host, int64_t se, int64_t sl, int64_
         if (fi.kind == K_C3 || fi.kind == K_E3 || fi.kind == K_V3) {
             const double* d = (const double*)buf.data();
             for (int e = 0; e < n; e++)
-                for (int k = 0; k <= L; k++) *(double*)(h + e * se + k * sl) = d[(size_t)e * LP + k];
+                for (int k = 0; k <= L; k++) *(double*)(h + e * se + k * sl) = d[(size_t)e * LP + lpos(LP, k)];
         } else if (fi.kind == K_C3V) {
             const double* d = (const double*)buf.data();
             for (int e = 0; e < n; e++)
                 for (int i = 0; i < W; i++)
                     for (int k = 0; k <= L; k++)
-                        *(double*)(h + e * se + k * sl + i * sc) = d[((size_t)e * W + i) * LP + k];
+                        *(double*)(h + e * se + k * sl + i * sc) = d[((size_t)e * W + i) * LP + lpos(LP, k)];
         } else if (fi.kind == K_C3B) {
             const uint8_t* d = (const uint8_t*)buf.data();
             for (int e = 0; e < n; e++)
-                for (int k = 0; k <= L; k++) *(uint8_t*)(h + e * se + k * sl) = d[(size_t)e * LP + k];
+                for (int k = 0; k <= L; k++) *(uint8_t*)(h + e * se + k * sl) = d[(size_t)e * LP + lpos(LP, k)];
         } else if (fi.kind == K_ZV) {
             const double* d = (const double*)buf.data();
             for (int k = 0; k <= L; k++) *(double*)(h + k * sl) = d[k];

@@ -1,21 +1,29 @@
 // mpas_dev.h -- device-side state layout and kernel launchers of libmpasdyn (gfx950).
 //
 // Device layout (HBM), chosen for one wavefront per column:
-//   C3/E3/V3   f[entity * LP + k]            k = 0..L   (LP = pow2 >= L+1, <= 64)
-//   C3V        f[(entity * W + i) * LP + k]  (zb_cell / zb3_cell: coalesced per component)
-//   C2*/E2*/V2* f[entity * W + i]            (2-D mesh data)
-//   C3B        uint8 f[entity * LP + k]
+//   C3/E3/V3   f[entity * LP + lpos(k)]            k = 0..L   (LP = pow2 >= L+1, <= 64)
+//   C3V        f[(entity * W + i) * LP + lpos(k)]  (zb_cell / zb3_cell: coalesced per component)
+//   C2*/E2*/V2* f[entity * W + i]                  (2-D mesh data)
+//   C3B        uint8 f[entity * LP + lpos(k)]
 //   ZV         f[k]                          (vertical_fs, LP entries)
 // Every entity array has nEntity+1 rows; row nEntity is the all-zero, never-written
 // "zero slot" that raw 1-based MPAS ids equal to nEntity resolve to.
 // A column of LP lanes holds one entity's levels: lane k <-> level k, so a gathered
 // neighbour column is one contiguous 8*(L+1)-byte read and vertical neighbours are
 // register shuffles within the LP-lane segment.
+// Level k sits at position lpos(k) of its column: k itself below LP = 64; at LP = 64 the
+// levels are interleaved in pairs, position 2j = level j, 2j+1 = level j+32, so that one
+// 16-B lane load by a wavefront fetches TWO columns (lanes 0-31 one, lanes 32-63 the
+// other) and one permlane32_swap per dword returns both to lane = level (gather2 below):
+// the gathers cost per load instruction, not per byte.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace mpas {
+
+__host__ __device__ constexpr int lpos(int LP, int k) { return LP == 64 ? (((k & 31) << 1) | (k >> 5)) : k; }
+__host__ __device__ constexpr int plev(int LP, int p) { return LP == 64 ? ((p >> 1) | ((p & 1) << 5)) : p; }  // inverse
 
 enum FieldKind { K_C3, K_C3V, K_E3, K_V3, K_C2F, K_C2I, K_E2F, K_E2I, K_V2F, K_V2I, K_C3B, K_ZV };
 enum FieldDist { D_U = 0, D_Z = 1, D_B = 2, D_M = 3, D_S = 4 };
@@ -256,7 +264,7 @@ __device__ __forceinline__ MPAS_GLOBAL T* sgpr_ptr(T* p) {
 // and the compiler then serialises the connectivity loads).  Every field is < 4 GiB.
 template <int LP>
 __device__ __forceinline__ uint32_t col_off(int ent, int k) {
-    return ((uint32_t)ent * (uint32_t)LP + (uint32_t)k) * (uint32_t)sizeof(double);
+    return ((uint32_t)ent * (uint32_t)LP + (uint32_t)lpos(LP, k)) * (uint32_t)sizeof(double);
 }
 template <class T>
 __device__ __forceinline__ T& at_off(T* f, uint32_t off) {
@@ -264,6 +272,40 @@ __device__ __forceinline__ T& at_off(T* f, uint32_t off) {
 }
 // level k of column ent of field pointer f (needs LP and k in scope)
 #define colk(f, ent) at_off((f), col_off<LP>((ent), k))
+
+// Two gathered columns, a = level k of column ia of field fa, b = level k of column ib
+// of field fb (any fields, any entities).  At LP = 64 one 16-B load per lane (lanes 0-31
+// read level pair j = k & 31 of column a, lanes 32-63 that of column b; see lpos) and one
+// permlane32_swap per dword (lanes 32-63 of x <-> lanes 0-31 of y) give both columns back
+// in lane = level order: half the load instructions of two 8-B gathers, which is what
+// the gather kernels are bound by.  Two plain loads below LP 64.
+__device__ __forceinline__ void swap_halves(double& x, double& y) {
+    int2 xi = __builtin_bit_cast(int2, x), yi = __builtin_bit_cast(int2, y);
+    const auto r0 = __builtin_amdgcn_permlane32_swap(xi.x, yi.x, false, false);
+    const auto r1 = __builtin_amdgcn_permlane32_swap(xi.y, yi.y, false, false);
+    xi.x = (int)r0[0];
+    yi.x = (int)r0[1];
+    xi.y = (int)r1[0];
+    yi.y = (int)r1[1];
+    x = __builtin_bit_cast(double, xi);
+    y = __builtin_bit_cast(double, yi);
+}
+template <int LP>
+__device__ __forceinline__ void gather2(const double* fa, int ia, const double* fb, int ib, int k, double& a,
+                                        double& b) {
+    if constexpr (LP == 64) {
+        const bool hi = k >= 32;
+        const char* base = hi ? (const char*)fb + (size_t)(uint32_t)ib * 512 : (const char*)fa + (size_t)(uint32_t)ia * 512;
+        const double2 t = *(const double2*)(base + (k & 31) * 16);
+        double x = t.x, y = t.y;
+        swap_halves(x, y);
+        a = x;
+        b = y;
+    } else {
+        a = colk(fa, ia);
+        b = colk(fb, ib);
+    }
+}
 
 // f at the two cellsOnEdge (x1, x2) of edge slot i of a cell.  SELF (S.selfc): the cell
 // is one of them, so only the other cell `oth` is gathered and `own`, f at the cell

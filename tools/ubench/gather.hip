@@ -54,6 +54,122 @@ __global__ __launch_bounds__(256) void g16(const double* __restrict__ T, const i
     if (ok) *(double2*)(out + (size_t)d * 64 + 2 * j) = s;
 }
 
+// lane-masked gathers: only lanes k < W load (levels 0..W-1 of a 64-double column); do
+// the idle lanes of a column's last 64-B chunk still cost request bandwidth?
+template <int NG>
+__global__ __launch_bounds__(256) void g8m(const double* __restrict__ T, const int* __restrict__ idx, int nd,
+                                           double* __restrict__ out, int G, int W) {
+    int d = xcdmap(G) * 4 + (int)(threadIdx.x >> 6);
+    d = __builtin_amdgcn_readfirstlane(d);
+    if (d >= nd) return;
+    const int k = threadIdx.x & 63;
+    double v[NG];
+    int id[NG];
+#pragma unroll
+    for (int i = 0; i < NG; i++) id[i] = idx[d * 10 + i];
+    if (k < W) {
+#pragma unroll
+        for (int i = 0; i < NG; i++) v[i] = T[(size_t)id[i] * 64 + k];
+    } else {
+#pragma unroll
+        for (int i = 0; i < NG; i++) v[i] = 0.0;
+    }
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < NG; i++) s += v[i];
+    out[(size_t)d * 64 + k] = s;
+}
+
+extern "C" int ub_gather_masked(const double* T, const int* idx, int nd, double* out, int G, int W, void* stream) {
+    g8m<10><<<(nd + 3) / 4, 256, 0, (hipStream_t)stream>>>(T, idx, nd, out, G, W);
+    return (int)hipGetLastError();
+}
+
+// two fields gathered at the same ids: two 8-B loads per id from separate arrays vs one
+// 16-B load from a pair-interleaved array (column = LP (a, b) pairs, 1 KB)
+template <int NG>
+__global__ __launch_bounds__(256) void g8two(const double* __restrict__ A, const double* __restrict__ B,
+                                             const int* __restrict__ idx, int nd, double* __restrict__ out, int G) {
+    int d = xcdmap(G) * 4 + (int)(threadIdx.x >> 6);
+    d = __builtin_amdgcn_readfirstlane(d);
+    if (d >= nd) return;
+    const int k = threadIdx.x & 63;
+    double a[NG], b[NG];
+#pragma unroll
+    for (int i = 0; i < NG; i++) {
+        const size_t o = (size_t)idx[d * 10 + i] * 64 + k;
+        a[i] = A[o];
+        b[i] = B[o];
+    }
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < NG; i++) s += a[i] * b[i];
+    out[(size_t)d * 64 + k] = s;
+}
+template <int NG>
+__global__ __launch_bounds__(256) void g16pair(const double2* __restrict__ AB, const int* __restrict__ idx, int nd,
+                                               double* __restrict__ out, int G) {
+    int d = xcdmap(G) * 4 + (int)(threadIdx.x >> 6);
+    d = __builtin_amdgcn_readfirstlane(d);
+    if (d >= nd) return;
+    const int k = threadIdx.x & 63;
+    double2 v[NG];
+#pragma unroll
+    for (int i = 0; i < NG; i++) v[i] = AB[(size_t)idx[d * 10 + i] * 64 + k];
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < NG; i++) s += v[i].x * v[i].y;
+    out[(size_t)d * 64 + k] = s;
+}
+extern "C" int ub_gather_two(int pair, const double* A, const double* B, const int* idx, int nd, double* out, int G,
+                             void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (pair) g16pair<10><<<(nd + 3) / 4, 256, 0, st>>>((const double2*)A, idx, nd, out, G);
+    else g8two<10><<<(nd + 3) / 4, 256, 0, st>>>(A, B, idx, nd, out, G);
+    return (int)hipGetLastError();
+}
+
+// two columns per 16-B gather with a level-permuted column layout: position 2j holds
+// level j, position 2j+1 level j+32.  Lanes 0-31 load pair j of column A, lanes 32-63
+// pair j of column B; one permlane32_swap per dword puts A and B back in lane = level.
+__device__ __forceinline__ void swap_halves(double& x, double& y) {
+    // lanes 32-63 of x <-> lanes 0-31 of y
+    int2 xi = *reinterpret_cast<int2*>(&x), yi = *reinterpret_cast<int2*>(&y);
+    auto r0 = __builtin_amdgcn_permlane32_swap(xi.x, yi.x, false, false);
+    auto r1 = __builtin_amdgcn_permlane32_swap(xi.y, yi.y, false, false);
+    xi.x = r0[0]; yi.x = r0[1]; xi.y = r1[0]; yi.y = r1[1];
+    x = *reinterpret_cast<double*>(&xi);
+    y = *reinterpret_cast<double*>(&yi);
+}
+template <int NG>
+__global__ __launch_bounds__(256) void g8swap(const double* __restrict__ T, const int* __restrict__ idx, int nd,
+                                              double* __restrict__ out, int G) {
+    int d = xcdmap(G) * 4 + (int)(threadIdx.x >> 6);
+    d = __builtin_amdgcn_readfirstlane(d);
+    if (d >= nd) return;
+    const int k = threadIdx.x & 63;
+    const int hi = k >> 5, j = k & 31;
+    double v[NG];
+#pragma unroll
+    for (int i = 0; i < NG; i += 2) {
+        const int ia = idx[d * 10 + i], ib = idx[d * 10 + i + 1];
+        const int id = hi ? ib : ia;
+        const double2 t = *(const double2*)(T + (size_t)id * 64 + 2 * j);
+        double x = t.x, y = t.y;
+        swap_halves(x, y);
+        v[i] = x;
+        v[i + 1] = y;
+    }
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < NG; i++) s += v[i];
+    out[(size_t)d * 64 + (j * 2 + hi)] = s;
+}
+extern "C" int ub_gather_swap(const double* T, const int* idx, int nd, double* out, int G, void* stream) {
+    g8swap<10><<<(nd + 3) / 4, 256, 0, (hipStream_t)stream>>>(T, idx, nd, out, G);
+    return (int)hipGetLastError();
+}
+
 extern "C" int ub_gather(int variant, const double* T, const int* idx, int nd, double* out, int G, void* stream) {
     hipStream_t st = (hipStream_t)stream;
     if (variant == 0) g8<6><<<(nd + 3) / 4, 256, 0, st>>>(T, idx, nd, out, G);

@@ -59,6 +59,68 @@ for name, (idx, nd) in cases.items():
             ng = 6 if var < 2 else 10
             req = nd * (ng + 1) * 512
             res["%s v%d G%d" % (name, var, G)] = {"ms": round(t, 4), "req_TBs": round(req / t / 1e9, 2)}
+lib.ub_gather_masked.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_void_p]
+idx, nd = cases["edge_eoe"]
+for W in (64, 57, 56, 48, 32, 64, 57, 56):
+    ts = []
+    for rep in range(6):
+        flush.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        lib.ub_gather_masked(T.data_ptr(), idx.data_ptr(), nd, out.data_ptr(), 64, W, st)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    t = sorted(ts[1:])[len(ts[1:]) // 2]
+    res["edge_eoe masked W%d G64" % W] = {"ms": round(t, 4)}
+lib.ub_gather_two.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+T2 = torch.rand((nE + 1) * 64, dtype=torch.float64, device=dev)
+TP = torch.rand((nE + 1) * 128, dtype=torch.float64, device=dev)
+for pair in (0, 1, 0, 1):
+    ts = []
+    for rep in range(6):
+        flush.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        if pair:
+            lib.ub_gather_two(1, TP.data_ptr(), 0, idx.data_ptr(), nd, out.data_ptr(), 64, st)
+        else:
+            lib.ub_gather_two(0, T.data_ptr(), T2.data_ptr(), idx.data_ptr(), nd, out.data_ptr(), 64, st)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    t = sorted(ts[1:])[len(ts[1:]) // 2]
+    res["edge_eoe two fields %s G64" % ("pair16" if pair else "2x8B")] = {"ms": round(t, 4)}
+lib.ub_gather_swap.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                               ctypes.c_void_p]
+# correctness of the permuted layout + swap against the plain gather
+perm = np.empty(64, dtype=np.int64)
+perm[0::2] = np.arange(32)
+perm[1::2] = np.arange(32) + 32
+TPm = T.view(-1, 64)[:, torch.from_numpy(perm).to(dev)].contiguous().view(-1)  # position p holds level perm[p]
+ref_out = torch.empty_like(out)
+lib.ub_gather(2, T.data_ptr(), idx.data_ptr(), nd, ref_out.data_ptr(), 0, st)
+lib.ub_gather_swap(TPm.data_ptr(), idx.data_ptr(), nd, out.data_ptr(), 0, st)
+torch.cuda.synchronize()
+got = out.view(-1, 64)[:nd][:, torch.from_numpy(np.argsort(perm)).to(dev)]
+res["swap parity max|diff|"] = float((got - ref_out.view(-1, 64)[:nd]).abs().max())
+for sw in (0, 1, 0, 1):
+    ts = []
+    for rep in range(6):
+        flush.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        if sw:
+            lib.ub_gather_swap(TPm.data_ptr(), idx.data_ptr(), nd, out.data_ptr(), 64, st)
+        else:
+            lib.ub_gather(2, T.data_ptr(), idx.data_ptr(), nd, out.data_ptr(), 64, st)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    t = sorted(ts[1:])[len(ts[1:]) // 2]
+    res["edge_eoe 10 cols %s G64" % ("swap16" if sw else "plain8")] = {"ms": round(t, 4)}
 lib.ub_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
 A = torch.rand(nE * 64, dtype=torch.float64, device=dev)
 B = torch.rand(nE * 64, dtype=torch.float64, device=dev)
