@@ -45,26 +45,29 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     const int ne = SELF ? cell_rec<true>(S, c, e_, o_, s1_) : cell_rec<false>(S, c, e_, c1_, c2_);
     row_ld(sgn, sgn_);
     row_ld(cdv, cdv_);
-    double rtp = col_rd<LP>(rtp_f, c, k, L), rpp = col_rd<LP>(rpp_f, c, k, L);
-    double rwp = col_rd<LP>(rwp_f, c, k, L), ww = col_rd<LP>(ww_f, c, k, L);
-    const double tm = col_rd<LP>(fd(S, F_theta_m), c, k, L);
-    const double tend_rho = col_rd<LP>(fd(S, F_tend_rho), c, k, L);
-    const double w = col_rd<LP>(fd(S, F_w), c, k, L);
+    // (gather2 / col_rd2: two columns per load instruction)
+    double rtp, rpp, rwp, ww, tm, tend_rho, w, coftz, zz, rz, cofwt, cofwz, cofwr, a_tri, alpha, rws, rw, dss;
+    col_rd2<LP>(rtp_f, rpp_f, c, k, L, rtp, rpp);
+    col_rd2<LP>(rwp_f, ww_f, c, k, L, rwp, ww);
+    col_rd2<LP>(fd(S, F_theta_m), fd(S, F_tend_rho), c, k, L, tm, tend_rho);
+    static_assert(NF % 2 == 0, "slot pairs");
+#pragma unroll
+    for (int i = 0; i < NF; i += 2) {
+        gather2s<LP>(ru_p, e_[i], e_[i + 1], k, rup_[i], rup_[i + 1]);
+        cell_pair2<LP, SELF>(tm_f, c1_, c2_, o_, s1_, tm, i, k, t1_[i], t2_[i], t1_[i + 1], t2_[i + 1]);
+    }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        rup_[i] = ldz(kl, colk(ru_p, e_[i]));
-        cell_pair<LP, SELF>(tm_f, c1_[i], c2_[i], o_[i], s1_[i], tm, k, t1_[i], t2_[i]);
+        rup_[i] = ldz(kl, rup_[i]);
         t1_[i] = ldz(kl, t1_[i]);
         t2_[i] = ldz(kl, t2_[i]);
     }
-    const double coftz = col_rd<LP>(fd(S, F_coftz), c, k, L);
-    const double zz = col_rd<LP>(fd(S, F_zz), c, k, L);
-    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L);
-    const double cofwt = col_rd<LP>(fd(S, F_cofwt), c, k, L);
-    const double cofwz = col_rd<LP>(fd(S, F_cofwz), c, k, L), cofwr = col_rd<LP>(fd(S, F_cofwr), c, k, L);
-    const double a_tri = col_rd<LP>(fd(S, F_a_tri), c, k, L), alpha = col_rd<LP>(fd(S, F_alpha_tri), c, k, L);
-    const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L), rw = col_rd<LP>(fd(S, F_rw), c, k, L);
-    const double dss = col_rd<LP>(fd(S, F_dss), c, k, L);
+    col_rd2<LP>(fd(S, F_w), fd(S, F_coftz), c, k, L, w, coftz);
+    col_rd2<LP>(fd(S, F_zz), fd(S, F_rho_zz), c, k, L, zz, rz);
+    col_rd2<LP>(fd(S, F_cofwt), fd(S, F_cofwz), c, k, L, cofwt, cofwz);
+    col_rd2<LP>(fd(S, F_cofwr), fd(S, F_a_tri), c, k, L, cofwr, a_tri);
+    col_rd2<LP>(fd(S, F_alpha_tri), fd(S, F_rw_save), c, k, L, alpha, rws);
+    col_rd2<LP>(fd(S, F_rw), fd(S, F_dss), c, k, L, rw, dss);
     const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
 

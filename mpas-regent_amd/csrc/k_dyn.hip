@@ -68,18 +68,24 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     row_ld(eocs, eocs_);
     row_ld(cdv, cdv_);
 #pragma unroll
-    for (int i = 0; i < NF; i++) ru_[i] = ldz(live, colk(ru, e_[i]));
+    for (int i = 0; i < NF; i += 2) gather2s<LP>(ru, e_[i], e_[i + 1], k, ru_[i], ru_[i + 1]);
+#pragma unroll
+    for (int i = 0; i < NF; i++) ru_[i] = ldz(live, ru_[i]);
     if (smag) {
 #pragma unroll
+        for (int i = 0; i < NF; i += 2) {
+            gather2s<LP>(u, e_[i], e_[i + 1], k, u_[i], u_[i + 1]);
+            gather2s<LP>(v, e_[i], e_[i + 1], k, v_[i], v_[i + 1]);
+        }
+#pragma unroll
         for (int i = 0; i < NF; i++) {
-            u_[i] = ldz(live, colk(u, e_[i]));
-            v_[i] = ldz(live, colk(v, e_[i]));
+            u_[i] = ldz(live, u_[i]);
+            v_[i] = ldz(live, v_[i]);
         }
     }
-    const double rw = col_rd<LP>(fd(S, F_rw), c, k, L);
-    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L);
-    const double urz = col_rd<LP>(fd(S, F_uReconstructZonal), c, k, L);
-    const double urm = col_rd<LP>(fd(S, F_uReconstructMeridional), c, k, L);
+    double rw, rz, urz, urm;
+    col_rd2<LP>(fd(S, F_rw), fd(S, F_rho_zz), c, k, L, rw, rz);
+    col_rd2<LP>(fd(S, F_uReconstructZonal), fd(S, F_uReconstructMeridional), c, k, L, urz, urm);
     // rk0 loads of the tend_rho/dpdz section, ahead of the stores (aliasing for the compiler)
     double trp = 0.0, qt = 0.0, rb = 0.0, rps = 0.0;
     if (rk0) {
@@ -200,8 +206,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // (gather2: two columns per load instruction)
     double u, ru_e, rw1, rw2, w1, w2, rho_edge, pv;
     gather2<LP>(u_f, e, fd(S, F_ru), e, k, u, ru_e);
-    gather2<LP>(fd(S, F_rw), cell1, fd(S, F_rw), cell2, k, rw1, rw2);
-    gather2<LP>(fd(S, F_w), cell1, fd(S, F_w), cell2, k, w1, w2);
+    gather2s<LP>(fd(S, F_rw), cell1, cell2, k, rw1, rw2);
+    gather2s<LP>(fd(S, F_w), cell1, cell2, k, w1, w2);
     gather2<LP>(fd(S, F_rho_edge), e, pv_f, e, k, rho_edge, pv);
     u = ldz(live, u);
     ru_e = ldz(live, ru_e);
@@ -221,8 +227,12 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     row_ld(woe, woe_);
     const bool kl = k < L;
 #pragma unroll
+    for (int j = 0; j < QF; j += 2) {
+        gather2s<LP>(u_f, ee_[j], ee_[j + 1], k, ue_[j], ue_[j + 1]);
+        gather2s<LP>(pv_f, ee_[j], ee_[j + 1], k, pve_[j], pve_[j + 1]);
+    }
+#pragma unroll
     for (int j = 0; j < QF; j++) {
-        gather2<LP>(u_f, ee_[j], pv_f, ee_[j], k, ue_[j], pve_[j]);
         ue_[j] = ldz(kl, ue_[j]);
         pve_[j] = ldz(kl, pve_[j]);
     }
@@ -240,7 +250,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     static_assert(AF == 9, "tv_ pairing below");
     double tr_phys;
 #pragma unroll
-    for (int j = 0; j < AF - 1; j += 2) gather2<LP>(tm_f, ad_[j], tm_f, ad_[j + 1], k, tv_[j], tv_[j + 1]);
+    for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
     gather2<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k, tv_[AF - 1], tr_phys);
 #pragma unroll
     for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, tv_[j]);
@@ -249,8 +259,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // for the compiler, which would then issue them only after it)
     const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
     double ke1, ke2, hd1, hd2;
-    gather2<LP>(ke_f, cell1, ke_f, cell2, k, ke1, ke2);
-    gather2<LP>(hd_f, cell1, hd_f, cell2, k, hd1, hd2);
+    gather2s<LP>(ke_f, cell1, cell2, k, ke1, ke2);
+    gather2s<LP>(hd_f, cell1, cell2, k, hd1, hd2);
     // (the rk0-only loads stay in their section: hoisted they cost more in occupancy,
     // 138 VGPRs, than the second memory round trip)
     const double tue_in = rk0 ? 0.0 : colk(fd(S, F_tend_u_euler), e);
@@ -355,7 +365,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     ColMap<LP> m(S, KV);
     if (m.blk < nVB) {  // delsq_vorticity (:1052-1060)
         const int vx = m.ent, k = m.k;
-        if (vx >= S.nVO || k >= L) return;
+        if (vx >= S.nVO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)vx * 3;
         const double* sgn = fd(S, F_edgesOnVertex_sign) + (size_t)vx * 3;
         const double iat = fd(S, F_invAreaTriangle)[vx];
@@ -364,8 +374,9 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         row_ld(eov, ev);
         row_ld(sgn, sg_);
         row_ld(fd(S, X_ve_dc) + (size_t)vx * 3, dc_);  // dcEdge(edgesOnVertex)
-#pragma unroll
-        for (int i = 0; i < 3; i++) d[i] = dsu[(size_t)ev[i] * LP + lpos(LP, k)];
+        gather2s<LP>(dsu, ev[0], ev[1], k, d[0], d[1]);
+        d[2] = colk(dsu, ev[2]);
+        if (k >= L) return;
         double dsv = 0.0;
 #pragma unroll
         for (int i = 0; i < 3; i++) {
@@ -400,18 +411,23 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     row_ld(cmsd2, cmsd2_);
     const double kd_c = SELF ? colk(kdiff, c) : 0.0, wc_c = SELF ? colk(wc, c) : 0.0, tm_c = SELF ? colk(tm, c) : 0.0;
 #pragma unroll
+    for (int i = 0; i < NF; i += 2) {
+        gather2s<LP>(rho_edge, e_[i], e_[i + 1], k, re_[i], re_[i + 1]);
+        cell_pair2<LP, SELF>(kdiff, c1_, c2_, o_, s1_, kd_c, i, k, kd1_[i], kd2_[i], kd1_[i + 1], kd2_[i + 1]);
+        cell_pair2<LP, SELF>(wc, c1_, c2_, o_, s1_, wc_c, i, k, wc1_[i], wc2_[i], wc1_[i + 1], wc2_[i + 1]);
+        cell_pair2<LP, SELF>(tm, c1_, c2_, o_, s1_, tm_c, i, k, t1_[i], t2_[i], t1_[i + 1], t2_[i + 1]);
+        gather2s<LP>(dsu, e_[i], e_[i + 1], k, ds_[i], ds_[i + 1]);
+    }
+#pragma unroll
     for (int i = 0; i < NF; i++) {
-        re_[i] = ldz(live, colk(rho_edge, e_[i]));
-        cell_pair<LP, SELF>(kdiff, c1_[i], c2_[i], o_[i], s1_[i], kd_c, k, kd1_[i], kd2_[i]);
-        cell_pair<LP, SELF>(wc, c1_[i], c2_[i], o_[i], s1_[i], wc_c, k, wc1_[i], wc2_[i]);
-        cell_pair<LP, SELF>(tm, c1_[i], c2_[i], o_[i], s1_[i], tm_c, k, t1_[i], t2_[i]);
+        re_[i] = ldz(live, re_[i]);
         kd1_[i] = ldz(live, kd1_[i]);
         kd2_[i] = ldz(live, kd2_[i]);
         wc1_[i] = ldz(kl, wc1_[i]);
         wc2_[i] = ldz(kl, wc2_[i]);
         t1_[i] = ldz(kl, t1_[i]);
         t2_[i] = ldz(kl, t2_[i]);
-        ds_[i] = ldz((kl && del4), colk(dsu, e_[i]));
+        ds_[i] = ldz((kl && del4), ds_[i]);
     }
     double re_m_[NF], kd1m_[NF], kd2m_[NF];
 #pragma unroll
@@ -520,40 +536,65 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
         row_ld(cidc, cidc_);
         row_ld(cmsd4, cmsd4_);
     }
-    const double ts_c = (SELF && !rk0) ? colk(tms_f, c) : 0.0;
-    const double dw_c = (SELF && rk0) ? colk(dw, c) : 0.0, dt_c = (SELF && rk0) ? colk(dth, c) : 0.0;
+    // own columns (gather2: two columns per load instruction; the theta-section loads
+    // too, ahead of the w stores that could alias them for the compiler)
+    double wc, rw, pp, dpdz, rws, tms, tmv, twe, tte, rho_zz, rt_diab, trp, cqw = 0.0, dw_c = 0.0, dt_c = 0.0;
+    gather2<LP>(fd(S, X_wc), c, fd(S, F_rw), c, k, wc, rw);
+    gather2<LP>(fd(S, F_pressure_p), c, fd(S, F_dpdz), c, k, pp, dpdz);
+    gather2<LP>(fd(S, F_rw_save), c, tms_f, c, k, rws, tms);
+    gather2<LP>(tm, c, fd(S, F_tend_w_euler), c, k, tmv, twe);
+    gather2<LP>(fd(S, F_tend_theta_euler), c, fd(S, F_rho_zz), c, k, tte, rho_zz);
+    gather2<LP>(fd(S, F_rt_diabatic_tend), c, fd(S, F_tend_rtheta_physics), c, k, rt_diab, trp);
+    if (rk0) {
+        if (SELF) gather2<LP>(fd(S, F_cqw), c, dw, c, k, cqw, dw_c);
+        else cqw = colk(fd(S, F_cqw), c);
+        if (SELF) dt_c = colk(dth, c);
+    }
+    const double ts_c = tms;  // (SELF, rk > 0: theta_m_save at the cell itself)
+#pragma unroll
+    for (int i = 0; i < NF; i += 2) {
+        gather2s<LP>(ru, e_[i], e_[i + 1], k, ru_[i], ru_[i + 1]);
+        gather2s<LP>(Ff, e_[i], e_[i + 1], k, F_[i], F_[i + 1]);
+    }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ru_[i] = ldz(kl, colk(ru, e_[i]));
-        F_[i] = ldz(kl, colk(Ff, e_[i]));
+        ru_[i] = ldz(kl, ru_[i]);
+        F_[i] = ldz(kl, F_[i]);
         rus_[i] = ts1_[i] = ts2_[i] = dw1_[i] = dw2_[i] = dt1_[i] = dt2_[i] = 0.0;
-        if (!rk0) {
-            rus_[i] = ldz(kl, colk(rus, e_[i]));
-            cell_pair<LP, SELF>(tms_f, c1_[i], c2_[i], o_[i], s1_[i], ts_c, k, ts1_[i], ts2_[i]);
+    }
+    if (!rk0) {
+#pragma unroll
+        for (int i = 0; i < NF; i += 2) {
+            gather2s<LP>(rus, e_[i], e_[i + 1], k, rus_[i], rus_[i + 1]);
+            cell_pair2<LP, SELF>(tms_f, c1_, c2_, o_, s1_, ts_c, i, k, ts1_[i], ts2_[i], ts1_[i + 1], ts2_[i + 1]);
+        }
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            rus_[i] = ldz(kl, rus_[i]);
             ts1_[i] = ldz(kl, ts1_[i]);
             ts2_[i] = ldz(kl, ts2_[i]);
         }
-        if (rk0) {  // (compile-time: a runtime `if (del4)` here would put each slot's loads in a branch)
-            cell_pair<LP, SELF>(dw, c1_[i], c2_[i], o_[i], s1_[i], dw_c, k, dw1_[i], dw2_[i]);
-            cell_pair<LP, SELF>(dth, c1_[i], c2_[i], o_[i], s1_[i], dt_c, k, dt1_[i], dt2_[i]);
+    }
+    if (rk0) {  // (compile-time: a runtime `if (del4)` here would put each slot's loads in a branch)
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            cell_pair_ff<LP, SELF>(dw, dth, c1_, c2_, o_, s1_, dw_c, dt_c, i, k, dw1_[i], dw2_[i], dt1_[i], dt2_[i]);
             dw1_[i] = ldz(kl && del4, dw1_[i]);
             dw2_[i] = ldz(kl && del4, dw2_[i]);
             dt1_[i] = ldz(kl && del4, dt1_[i]);
             dt2_[i] = ldz(kl && del4, dt2_[i]);
         }
     }
-    const double wc = ldz(kl, colk(fd(S, X_wc), c));
-    const double rw = col_rd<LP>(fd(S, F_rw), c, k, L);
+    wc = ldz(kl, wc);
+    rw = ldz(k <= L, rw);
+    pp = ldz(k <= L, pp);
+    dpdz = ldz(k <= L, dpdz);
+    rws = ldz(k <= L, rws);
+    tms = ldz(k <= L, tms);
+    tmv = ldz(k <= L, tmv);
+    twe = ldz(kl, twe);
+    tte = ldz(kl, tte);
     const double wdwzL = fd(S, F_wdwz)[(size_t)c * LP + lpos(LP, L)], wdtzL = fd(S, F_wdtz)[(size_t)c * LP + lpos(LP, L)];  // level-L slots
-    const double pp = col_rd<LP>(fd(S, F_pressure_p), c, k, L), dpdz = col_rd<LP>(fd(S, F_dpdz), c, k, L);
-    const double rws = col_rd<LP>(fd(S, F_rw_save), c, k, L);
-    const double tms = col_rd<LP>(tms_f, c, k, L), tmv = col_rd<LP>(tm, c, k, L);
-    double twe = ldz(kl, colk(fd(S, F_tend_w_euler), c));
-    double tte = ldz(kl, colk(fd(S, F_tend_theta_euler), c));
-    // theta-section loads, ahead of the w stores that could alias them for the compiler
-    const double rho_zz = colk(fd(S, F_rho_zz), c), rt_diab = colk(fd(S, F_rt_diabatic_tend), c);
-    const double trp = colk(fd(S, F_tend_rtheta_physics), c);
-    const double cqw = rk0 ? colk(fd(S, F_cqw), c) : 0.0;
 
     // ================= W =================
     if (del4 && kl) {  // :1258-1272

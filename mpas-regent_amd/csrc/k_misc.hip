@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
     double *rws = fw(S, F_rw_save), *rtps = fw(S, F_rtheta_p_save), *rps = fw(S, F_rho_p_save);
     double *w2 = fw(S, F_w_2), *tm2 = fw(S, F_theta_m_2), *rz2 = fw(S, F_rho_zz_2), *rzo = fw(S, F_rho_zz_old_split);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         rws[i] = rw[i];
         rtps[i] = rtp[i];
         rps[i] = rp[i];
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_setup_edges(DevState S) {
     const double *ru = fd(S, F_ru), *u = fd(S, F_u);
     double *rus = fw(S, F_ru_save), *u2 = fw(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         rus[i] = ru[i];
         u2[i] = u[i];
     }
@@ -62,9 +62,11 @@ __global__ __launch_bounds__(256) void k_moist(DevState S) {
     double *qtot = fw(S, F_qtot), *cqw = fw(S, F_cqw);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         int k = plev(S.LP, (int)(i % S.LP));
-        if (k >= S.L) continue;
+        if (k == S.L) continue;  // (padding levels k > L get zeros: full 64-B sectors)
         qtot[i] = 0.0;  // :473-482
-        if (k > 0) {    // :484-489, qtot(k) and qtot(k-1) were both just zeroed
+        if (k > S.L) {
+            cqw[i] = 0.0;
+        } else if (k > 0) {  // :484-489, qtot(k) and qtot(k-1) were both just zeroed
             double q_k = 0.0, q_km1 = 0.0;
             double qtotal = 0.5 * (q_k + q_km1);
             cqw[i] = 1.0 / (1.0 + qtotal);
@@ -113,15 +115,16 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
     const double gamma_m = (k == 1) ? 0.0 : gamma_dn;  // Q17: gamma(0) was just zeroed
     const double cofrz = dtseps * rdzw, cofrz_m = dtseps * rdzw_m;      // :537-539
 
-    if (k < L) {
+    const bool pad = k > L;  // padding levels: zeros (full 64-B sectors; see PADW)
+    if (k < L || pad) {
         double* o;
-        colk(fw(S, F_coftz), c) = coftz;
-        colk(fw(S, F_cofwt), c) = cofwt;
+        colk(fw(S, F_coftz), c) = PADW(coftz);
+        colk(fw(S, F_cofwt), c) = PADW(cofwt);
         if (k == 0) {
             colk(fw(S, F_gamma_tri), c) = 0.0;
         } else {
-            colk(fw(S, F_cofwr), c) = cofwr;
-            colk(fw(S, F_cofwz), c) = cofwz;
+            colk(fw(S, F_cofwr), c) = PADW(cofwr);
+            colk(fw(S, F_cofwz), c) = PADW(cofwz);
             // :566-578 (Q16 literal)
             double a = -1.0 * cofwz * coftz_m * rdzw_m * zz_m + cofwr * cofrz_m - cofwt_m * coftz_m * rdzw_m;
             double b = 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) - coftz * (cofwt * rdzw - cofwt * rdzw_m) +
@@ -129,13 +132,13 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
             double cc = -1.0 * cofwz * coftz_p * rdzw * zz - cofwr * cofrz + cofwt * coftz_p * rdzw;
             double alpha = 1.0 / (b - a * gamma_m);  // :580-585
             double gamma = cc * alpha;               // :587-591
-            o = fw(S, F_a_tri); colk(o, c) = a;
-            o = fw(S, F_b_tri); colk(o, c) = b;
-            o = fw(S, F_c_tri); colk(o, c) = cc;
-            o = fw(S, F_alpha_tri); colk(o, c) = alpha;
-            o = fw(S, F_gamma_tri); colk(o, c) = gamma;
+            o = fw(S, F_a_tri); colk(o, c) = PADW(a);
+            o = fw(S, F_b_tri); colk(o, c) = PADW(b);
+            o = fw(S, F_c_tri); colk(o, c) = PADW(cc);
+            o = fw(S, F_alpha_tri); colk(o, c) = PADW(alpha);
+            o = fw(S, F_gamma_tri); colk(o, c) = PADW(gamma);
         }
-        if (c == 0) fw(S, F_cofrz)[k] = cofrz;
+        if (c == 0 && !pad) fw(S, F_cofrz)[k] = cofrz;
     }
 }
 template <int LP>
@@ -174,8 +177,10 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     row_ld(eoc, e_);
     row_ld(sgn, sgn_);
 #pragma unroll
+    for (int i = 0; i < NF; i += 2) gather2s<LP>(ut_f, e_[i], e_[i + 1], k, ut_[i], ut_[i + 1]);
+#pragma unroll
     for (int i = 0; i < NF; i++) {
-        ut_[i] = col_rd<LP>(ut_f, e_[i], k, L);
+        ut_[i] = ldz(k <= L, ut_[i]);
         size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
         zb_[i] = zb[q];
         zb3_[i] = zb3[q];
@@ -234,12 +239,9 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
     for (int i = 0; i < EPW; i++) {
         sh1[i] = sh[c1[i]];
         sh2[i] = sh[c2[i]];
-        r1[i] = colk(rtp, c1[i]);
-        ro1[i] = colk(rtpo, c1[i]);
-        r2[i] = colk(rtp, c2[i]);
-        ro2[i] = colk(rtpo, c2[i]);
-        t1[i] = colk(tm, c1[i]);
-        t2[i] = colk(tm, c2[i]);
+        gather2s<LP>(rtp, c1[i], c2[i], k, r1[i], r2[i]);
+        gather2s<LP>(rtpo, c1[i], c2[i], k, ro1[i], ro2[i]);
+        gather2s<LP>(tm, c1[i], c2[i], k, t1[i], t2[i]);
     }
 #pragma unroll
     for (int i = 0; i < EPW; i++) {
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(256) void k_finish_edges(DevState S, int substep, i
     double *ru_save = fw(S, F_ru_save), *u = fw(S, F_u), *ruAvg = fw(S, F_ruAvg), *ruAvgS = fw(S, F_ruAvg_split);
     const double *ru = fd(S, F_ru), *u2 = fd(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         if (substep < split) {
             ru_save[i] = ru[i];
             u[i] = u2[i];
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
     const size_t n = (size_t)S.nCO * S.LP;
     double *wwAvg = fw(S, F_wwAvg), *wwAvgS = fw(S, F_wwAvg_split), *rho_zz = fw(S, F_rho_zz);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) >= S.L) continue;
+        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         if (substep < split) {
             fw(S, F_rw_save)[i] = fd(S, F_rw)[i];
             fw(S, F_rtheta_p_save)[i] = fd(S, F_rtheta_p)[i];

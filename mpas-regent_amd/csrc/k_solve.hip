@@ -32,13 +32,14 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
             fv[j] = fd(S, F_fVertex)[v];
         }
 #pragma unroll
-        for (int j = 0; j < EPW; j++)
+        for (int j = 0; j < EPW; j++) gather2s<LP>(u, ev[j][0], ev[j][1], k, u_[j][0], u_[j][1]);
 #pragma unroll
-            for (int i = 0; i < 3; i++) u_[j][i] = colk(u, ev[j][i]);
+        for (int j = 0; j + 1 < EPW; j += 2) gather2s<LP>(u, ev[j][2], ev[j + 1][2], k, u_[j][2], u_[j + 1][2]);
+        if (EPW % 2) u_[EPW - 1][2] = colk(u, ev[EPW - 1][2]);
 #pragma unroll
         for (int j = 0; j < EPW; j++) {
             const int v = m.base + j;
-            if (v >= S.nVO || k >= L) continue;
+            if (v >= S.nVO || k == L) continue;  // (padding levels: zeros, PADW)
             double vort = 0.0;
 #pragma unroll
             for (int i = 0; i < 3; i++) {
@@ -46,8 +47,8 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
                 vort += s * u_[j][i];
             }
             vort *= iat[j];
-            colk(fw(S, F_vorticity), v) = vort;
-            colk(fw(S, F_pv_vertex), v) = fv[j] + vort;
+            colk(fw(S, F_vorticity), v) = PADW(vort);
+            colk(fw(S, F_pv_vertex), v) = PADW(fv[j] + vort);
             if (hollingsworth_part) {
                 double r = 0.25 * iat[j];
                 double kes[3];
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
                     double uu = u_[j][i];
                     kes[i] = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
                 }
-                colk(fw(S, F_ke_vertex), v) = (kes[0] + kes[1] + kes[2]) * r;
+                colk(fw(S, F_ke_vertex), v) = PADW((kes[0] + kes[1] + kes[2]) * r);
             }
         }
         return;
@@ -79,11 +80,11 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
 #pragma unroll
     for (int j = 0; j < EPW; j++)
 #pragma unroll
-        for (int i = 0; i < NF; i++) u_[j][i] = colk(u, e_[j][i]);
+        for (int i = 0; i < NF; i += 2) gather2s<LP>(u, e_[j][i], e_[j][i + 1], k, u_[j][i], u_[j][i + 1]);
 #pragma unroll
     for (int j = 0; j < EPW; j++) {
         const int c = c0 + j;
-        if (c >= S.nCO || k >= L) continue;
+        if (c >= S.nCO || k == L) continue;  // (padding levels: zeros, PADW)
         double div = 0.0, ke = 0.0;
 #pragma unroll
         for (int i = 0; i < NF; i++) {
@@ -109,8 +110,8 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         }
         div *= invA[j];
         ke *= invA[j];
-        colk(fw(S, F_divergence), c) = div;
-        colk(fw(S, F_ke), c) = ke;
+        colk(fw(S, F_divergence), c) = PADW(div);
+        colk(fw(S, F_ke), c) = PADW(ke);
     }
 }
 
@@ -138,13 +139,14 @@ template <int LP, bool RECON_V>
 __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
     ColMap<LP> m(S, KE);
     const int L = S.L, e = m.ent, k = m.k;
-    if (e >= S.nEO || k >= L) return;
+    if (e >= S.nEO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
     const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
     const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
     const double *h = fd(S, F_h), *u = fd(S, F_u), *pvv = fd(S, F_pv_vertex);
     // every load before the first store (the stores could alias them for the compiler)
-    const double h1 = colk(h, coe[0]), h2 = colk(h, coe[1]), uu = colk(u, e);
-    const double pv1 = colk(pvv, voe[0]), pv2 = colk(pvv, voe[1]);
+    double h1, h2, uu, pv1, pv2;
+    gather2s<LP>(h, coe[0], coe[1], k, h1, h2);
+    gather2s<LP>(pvv, voe[0], voe[1], k, pv1, pv2);
     const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
     const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
     const int neoe = RECON_V ? fi(S, F_nEdgesOnEdge)[e] : 0;
@@ -153,20 +155,25 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
     if (RECON_V) {
         row_ld(eoe, ee_);
         row_ld(wts, wts_);
+        static_assert(QF == 10, "pairs below");
 #pragma unroll
-        for (int i = 1; i < QF; i++) ue[i] = colk(u, ee_[i]);
+        for (int i = 1; i < QF - 1; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
+        gather2s<LP>(u, ee_[QF - 1], e, k, ue[QF - 1], uu);
+    } else {
+        uu = colk(u, e);
     }
-    colk(fw(S, F_h_edge), e) = 0.5 * (h1 + h2);
+    if (k == L) return;  // (padding levels k > L: zeros, PADW)
+    colk(fw(S, F_h_edge), e) = PADW(0.5 * (h1 + h2));
     const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
-    colk(fw(S, F_ke_edge), e) = efac * (uu * uu);
+    colk(fw(S, F_ke_edge), e) = PADW(efac * (uu * uu));
     if (RECON_V) {  // Q23: the sum starts at i = 1
         double v = 0;
 #pragma unroll
         for (int i = 1; i < QF; i++) v = add_if(i < neoe, v, wts_[i] * ue[i]);
         for (int i = QF; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
-        colk(fw(S, F_v), e) = v;
+        colk(fw(S, F_v), e) = PADW(v);
     }
-    colk(fw(S, F_pv_edge), e) = 0.5 * (pv1 + pv2);
+    colk(fw(S, F_pv_edge), e) = PADW(0.5 * (pv1 + pv2));
 }
 
 template <int LP>

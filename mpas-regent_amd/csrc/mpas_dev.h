@@ -224,8 +224,10 @@ struct ColMapN {
 // entity ids, clamped on upload) ahead of the in-order accumulation; any entries
 // beyond them are handled by a generic tail loop.
 constexpr int NF = 6;   // edgesOnCell
+
 constexpr int QF = 10;  // edgesOnEdge
 constexpr int AF = 9;   // advCellsForEdge (the reference's list holds at most 9, :175)
+static_assert(NF % 2 == 0 && QF % 2 == 0, "the gathers go in pairs (gather2)");
 
 // value of x held by level k-1 of the same column (0.0 at k == 0: level -1 reads 0)
 template <int LP>
@@ -323,6 +325,57 @@ __device__ __forceinline__ void cell_pair(const double* f, int c1, int c2, int o
     }
 }
 
+// gather2 of one field at two entities: the field base stays in SGPRs and only the
+// 32-bit offset is selected per lane (the saddr + voffset form of col_off)
+template <int LP>
+__device__ __forceinline__ void gather2s(const double* f, int ia, int ib, int k, double& a, double& b) {
+    if constexpr (LP == 64) {
+        const uint32_t off = (uint32_t)(k >= 32 ? ib : ia) * 512u + (uint32_t)(k & 31) * 16u;
+        const double2 t = at_off((const double2*)f, off);
+        double x = t.x, y = t.y;
+        swap_halves(x, y);
+        a = x;
+        b = y;
+    } else {
+        a = colk(f, ia);
+        b = colk(f, ib);
+    }
+}
+
+// cell_pair for edge slots i and i+1 of one field: two gather2 (SELF: one)
+template <int LP, bool SELF>
+__device__ __forceinline__ void cell_pair2(const double* f, const int* c1, const int* c2, const int* oth, const int* s1,
+                                           double own, int i, int k, double& x1, double& x2, double& y1, double& y2) {
+    if constexpr (SELF) {
+        double xo, yo;
+        gather2s<LP>(f, oth[i], oth[i + 1], k, xo, yo);
+        x1 = s1[i] ? own : xo;
+        x2 = s1[i] ? xo : own;
+        y1 = s1[i + 1] ? own : yo;
+        y2 = s1[i + 1] ? yo : own;
+    } else {
+        gather2s<LP>(f, c1[i], c2[i], k, x1, x2);
+        gather2s<LP>(f, c1[i + 1], c2[i + 1], k, y1, y2);
+    }
+}
+// cell_pair of two fields at edge slot i: (SELF: one gather2 of both fields)
+template <int LP, bool SELF>
+__device__ __forceinline__ void cell_pair_ff(const double* f, const double* g, const int* c1, const int* c2,
+                                             const int* oth, const int* s1, double fown, double gown, int i, int k,
+                                             double& f1, double& f2, double& g1, double& g2) {
+    if constexpr (SELF) {
+        double fo, go;
+        gather2<LP>(f, oth[i], g, oth[i], k, fo, go);
+        f1 = s1[i] ? fown : fo;
+        f2 = s1[i] ? fo : fown;
+        g1 = s1[i] ? gown : go;
+        g2 = s1[i] ? go : gown;
+    } else {
+        gather2s<LP>(f, c1[i], c2[i], k, f1, f2);
+        gather2s<LP>(g, c1[i], c2[i], k, g1, g2);
+    }
+}
+
 __device__ __forceinline__ const double* fd(const DevState& S, int id) { return (const double*)S.f[id]; }
 __device__ __forceinline__ double* fw(const DevState& S, int id) { return (double*)S.f[id]; }
 __device__ __forceinline__ const int* fi(const DevState& S, int id) { return (const int*)S.f[id]; }
@@ -363,10 +416,24 @@ __device__ __forceinline__ int cell_rec(const DevState& S, int c, int (&e_)[NF],
     return r[3 * NF];
 }
 
+// A store masked to the levels below L leaves level L and the padding levels L+1..LP-1
+// unwritten; with the level-pair layout (lpos) those sit at odd positions spread over the
+// last two 64-B sectors of the column, and every partially written sector costs HBM time.
+// Kernels therefore also write the padding levels, with 0.0 (their content everywhere):
+// `if (k < L || k > L) f = PADW(v)`.  Only level L stays unwritten.
+#define PADW(v) (k > L ? 0.0 : (v))
+
 // column read with the level policy: levels outside 0..L read 0.0
 template <int LP>
 __device__ __forceinline__ double col_rd(const double* f, int ent, int k, int L) {
     return ldz(k <= L, at_off(f, col_off<LP>(ent, k)));
+}
+// col_rd of two fields of one column (gather2)
+template <int LP>
+__device__ __forceinline__ void col_rd2(const double* f, const double* g, int ent, int k, int L, double& a, double& b) {
+    gather2<LP>(f, ent, g, ent, k, a, b);
+    a = ldz(k <= L, a);
+    b = ldz(k <= L, b);
 }
 #endif
 

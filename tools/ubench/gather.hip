@@ -190,6 +190,27 @@ __global__ __launch_bounds__(256) void s_add(const double* __restrict__ a, const
     double x = a[(size_t)r * 64 + k] + b[(size_t)r * 64 + k];
     if (k < W) d[(size_t)r * 64 + k] = x;
 }
+// the same with the level-pair layout's holes: mode 0 positions < 56 (contiguous), 1 the
+// positions of levels < 56 (odd positions 49..63 skipped), 2 all but position 49, 3 all
+__global__ __launch_bounds__(256) void s_addp(const double* __restrict__ a, const double* __restrict__ b, int n,
+                                              double* __restrict__ d, int mode) {
+    int r = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (r >= n) return;
+    const int p = threadIdx.x & 63;
+    const int lev = (p >> 1) | ((p & 1) << 5);
+    double x = a[(size_t)r * 64 + p] + b[(size_t)r * 64 + p];
+    bool w = mode == 0 ? p < 56 : mode == 1 ? lev < 56 : mode == 2 ? p != 49 : true;
+    if (mode == 4) {  // position 49 keeps its value: read it back and write the full column
+        if (p == 49) x = d[(size_t)r * 64 + p];
+        w = true;
+    }
+    if (w) d[(size_t)r * 64 + p] = x;
+}
+extern "C" int ub_streamp(const double* a, const double* b, int n, double* d, int mode, void* stream) {
+    s_addp<<<(n + 3) / 4, 256, 0, (hipStream_t)stream>>>(a, b, n, d, mode);
+    return (int)hipGetLastError();
+}
 extern "C" int ub_stream(const double* a, const double* b, int n, double* d, int W, void* stream) {
     s_add<<<(n + 3) / 4, 256, 0, (hipStream_t)stream>>>(a, b, n, d, W);
     return (int)hipGetLastError();

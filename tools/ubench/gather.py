@@ -137,6 +137,19 @@ for W in (56, 57, 64, 56, 57, 64):
         ts.append(e0.elapsed_time(e1))
     t = sorted(ts[1:])[len(ts[1:]) // 2]
     res["stream W%d" % W] = {"ms": round(t, 4), "TBs_3x456B": round(3 * nE * 456 / t / 1e9, 2)}
+lib.ub_streamp.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+for mode in (0, 1, 2, 3, 4, 0, 1, 2, 3, 4):
+    ts = []
+    for rep in range(6):
+        flush.zero_()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        lib.ub_streamp(A.data_ptr(), B.data_ptr(), nE, D.data_ptr(), mode, st)
+        e1.record()
+        torch.cuda.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    t = sorted(ts[1:])[len(ts[1:]) // 2]
+    res["stream holes mode%d" % mode] = {"ms": round(t, 4)}
 for fn in ("ub_stream16", "ub_stream8"):
     f = getattr(lib, fn)
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
