@@ -72,7 +72,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
 
     // :1615-1636
-    if (kl) colk(fw(S, F_rtheta_pp_old), c) = (small_step == 0) ? 0 : rtp;
+    if (k != L) colk(fw(S, F_rtheta_pp_old), c) = PADW((small_step == 0) ? 0 : rtp);  // (PADW: mpas_dev.h)
     if (small_step == 0) {
         ww = 0;
         rwp = 0;
@@ -88,13 +88,13 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
             rtp = rtp + dts * tm;
             rwp = rwp + dts * w;
             ww = ww + 0.5 * (1.0 + epssm) * rwp;
-            colk(rpp_f, c) = rpp;
-            colk(rtp_f, c) = rtp;
         }
-        if (k <= L) {
-            colk(rwp_f, c) = rwp;
-            colk(ww_f, c) = ww;
+        if (k != L) {
+            colk(rpp_f, c) = PADW(rpp);
+            colk(rtp_f, c) = PADW(rtp);
         }
+        colk(rwp_f, c) = PADW(rwp);
+        colk(ww_f, c) = PADW(ww);
         return;
     }
 
@@ -182,15 +182,13 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         }
         x = (k == 0) ? rwold : H;
     }
-    if (k < L) {
-        if (k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
-        colk(rpp_f, c) = rs - cofrz * (rwp_p - x);
-        colk(rtp_f, c) = ts - rdzw * (coftz_p * rwp_p - coftz * x);
+    if (k < L && k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
+    if (k != L) {
+        colk(rpp_f, c) = PADW(rs - cofrz * (rwp_p - x));
+        colk(rtp_f, c) = PADW(ts - rdzw * (coftz_p * rwp_p - coftz * x));
     }
-    if (k <= L) {
-        colk(rwp_f, c) = (k < L) ? x : rwp;
-        colk(ww_f, c) = ww;
-    }
+    colk(rwp_f, c) = PADW((k < L) ? x : rwp);
+    colk(ww_f, c) = PADW(ww);
 }
 
 template <int LP>

@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
             int pw = k - (L - 2);
             kd = dmax_(kd, (pw == 0 ? 1.0 : 2.0) * 2.0833 * kLenDisp * a.cam_coef);
         }
-        if (k < L) colk(fw(S, F_kdiff), c) = kd;
+        if (k != L) colk(fw(S, F_kdiff), c) = PADW(kd);
     }
 
     // ---- h_divergence (:924-938)
@@ -140,13 +140,13 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         hd += edge_sign * col_rd<LP>(ru, eoc[i], k, L);
     }
     hd *= fd(S, F_invAreaCell)[c];
-    if (k < L) colk(fw(S, F_h_divergence), c) = hd;
+    if (k != L) colk(fw(S, F_h_divergence), c) = PADW(hd);
 
     // ---- tend_rho, dpdz (:942-951)
     const double rw_p1 = lvl_up<LP>(rw, k);
-    if (rk0 && k < L) {
-        colk(fw(S, F_tend_rho), c) = -hd - rdzw * (rw_p1 - rw + trp);
-        colk(fw(S, F_dpdz), c) = -kGravity * (rb * (qt) + rps * (1.0 + qt));
+    if (rk0 && k != L) {
+        colk(fw(S, F_tend_rho), c) = PADW(-hd - rdzw * (rw_p1 - rw + trp));
+        colk(fw(S, F_dpdz), c) = PADW(-kGravity * (rb * (qt) + rps * (1.0 + qt)));
     }
 
     // ---- w: zeroing (:1170), horizontal advection (:1174-1205, Q13), curvature (:1208-1218)
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     if (ne > NF) ru_l = col_rd<LP>(ru, eoc[ne - 1], k, L);
     const double ru_lm = lvl_dn<LP>(ru_l, k);
     const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
-    if (k >= L) return;
+    // (every lane goes on: the scratch wc is stored whole, 0.0 from level L up)
     double w0 = 0.0;
     if (ne > 0 && k > 0) {
         double ru_edge_w = fzm * ru_l + fzp * ru_lm;
@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
               2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
     }
-    colk(fw(S, X_wc), c) = wc;
+    colk(fw(S, X_wc), c) = k < L ? wc : 0.0;
 }
 
 // ------------------------------------------------------------------------ B (edges)
@@ -273,7 +273,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     if (k > 1 && k < L - 1) wduz = flux3(u_m2, u_m, u, u_p, 0.5 * (rw1 + rw2), 1.0);
     if (k == L) wduz = wduzL;
     const double wduz_p = lvl_up<LP>(wduz, k);
-    if (!kl) return;
+    // Every lane goes on (gather2 below needs all of them); level L is not stored, the
+    // padding levels get 0.0 (PADW), the scratch F is stored whole.
 
     {  // flux_arr of this edge
         const double sg = copysign(1.0, ru_e);
@@ -287,7 +288,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
             double scalar_weight = ac[j] + sg * ac3[j];
             flux_arr += scalar_weight * colk(tm_f, ad[j]);
         }
-        colk(fw(S, X_F), e) = flux_arr;
+        colk(fw(S, X_F), e) = kl ? flux_arr : 0.0;
     }
 
     // ---- tend_u (:987-1007)
@@ -326,10 +327,14 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         const double *pp = fd(S, F_pressure_p), *zz = fd(S, F_zz), *dpdz = fd(S, F_dpdz);
         const double *div = fd(S, F_divergence), *vor = fd(S, F_vorticity), *kdiff = fd(S, F_kdiff);
         const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
-        const double cqu = colk(fd(S, F_cqu), e), zxu = colk(fd(S, F_zxu), e);
-        const double pp1 = colk(pp, cell1), pp2 = colk(pp, cell2), zz1 = colk(zz, cell1), zz2 = colk(zz, cell2);
-        const double dz1 = colk(dpdz, cell1), dz2 = colk(dpdz, cell2), dv1 = colk(div, cell1), dv2 = colk(div, cell2);
-        const double vo1 = colk(vor, vertex1), vo2 = colk(vor, vertex2), kf1 = colk(kdiff, cell1), kf2 = colk(kdiff, cell2);
+        double cqu, zxu, pp1, pp2, zz1, zz2, dz1, dz2, dv1, dv2, vo1, vo2, kf1, kf2;
+        gather2<LP>(fd(S, F_cqu), e, fd(S, F_zxu), e, k, cqu, zxu);
+        gather2s<LP>(pp, cell1, cell2, k, pp1, pp2);
+        gather2s<LP>(zz, cell1, cell2, k, zz1, zz2);
+        gather2s<LP>(dpdz, cell1, cell2, k, dz1, dz2);
+        gather2s<LP>(div, cell1, cell2, k, dv1, dv2);
+        gather2s<LP>(vor, vertex1, vertex2, k, vo1, vo2);
+        gather2s<LP>(kdiff, cell1, cell2, k, kf1, kf2);
         // ---- pressure gradient (:964-970)
         tue = -cqu * ((pp2 - pp1) * invDc / (0.5 * (zz2 + zz1)) - 0.5 * zxu * (dz1 + dz2));
         // ---- del2 (:1030-1048)
@@ -338,7 +343,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         double u_diffusion = (dv2 - dv1) * r_dc - (vo2 - vo1) * r_dv;
         double delsq_u = 0.0;
         delsq_u += u_diffusion;
-        colk(fw(S, F_delsq_u), e) = delsq_u;
+        if (k != L) colk(fw(S, F_delsq_u), e) = PADW(delsq_u);
         double kdiffu = 0.5 * (kf1 + kf2);
         tue += rho_edge * kdiffu * u_diffusion * fd(S, F_meshScalingDel2)[e];
     } else {
@@ -347,13 +352,14 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // ---- Rayleigh damping (:1152-1159)
     if (a.rayleigh && k > L - kRayleighLevels + 1)
         tend_u -= rho_edge * u * (((double)k - (double)(L - kRayleighLevels)) * a.rayleigh_inv);
+    if (k == L) return;
     if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
-        colk(fw(S, F_tend_u_euler), e) = tue;
-        colk(fw(S, F_tend_u), e) = tend_u;
+        colk(fw(S, F_tend_u_euler), e) = PADW(tue);
+        colk(fw(S, F_tend_u), e) = PADW(tend_u);
     } else {
-        if (rk0) colk(fw(S, F_tend_u_euler), e) = tue;
+        if (rk0) colk(fw(S, F_tend_u_euler), e) = PADW(tue);
         tend_u += tue + tr_phys;  // :1161-1163
-        colk(fw(S, F_tend_u), e) = tend_u;
+        colk(fw(S, F_tend_u), e) = PADW(tend_u);
     }
 }
 
@@ -472,12 +478,12 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         edge_terms(kl, eocs[i], cdv[i], cidc[i], cmsd2[i], re_k, re_m, kd1, kd2, kd1m, kd2m, ldz(kl, colk(wc, c1)),
                    ldz(kl, colk(wc, c2)), ldz(kl, colk(tm, c1)), ldz(kl, colk(tm, c2)), ldz(kl && del4, colk(dsu, e)));
     }
-    if (!kl) return;
-    if (del4) colk(fw(S, F_delsq_divergence), c) = dsd;
-    colk(fw(S, F_delsq_w), c) = delsq_w;
-    colk(fw(S, F_tend_w_euler), c) = twe;
-    colk(fw(S, F_delsq_theta), c) = delsq_theta;
-    colk(fw(S, F_tend_theta_euler), c) = tte;
+    if (k == L) return;  // (padding levels: zeros, PADW)
+    if (del4) colk(fw(S, F_delsq_divergence), c) = PADW(dsd);
+    colk(fw(S, F_delsq_w), c) = PADW(delsq_w);
+    colk(fw(S, F_tend_w_euler), c) = PADW(twe);
+    colk(fw(S, F_delsq_theta), c) = PADW(delsq_theta);
+    colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
 // ------------------------------------------------------------------------ D (rk0, del4)
@@ -485,8 +491,7 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
-    if (e >= S.nEO || k >= L) return;
-    const size_t p = (size_t)e * LP + lpos(LP, k);
+    if (e >= S.nEO) return;  // (k >= L after the gathers: gather2 needs every lane)
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
     const double invDc = fd(S, F_invDcEdge)[e];
@@ -494,14 +499,17 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
     double r_dc = u_mix_scale * kDel4uDivFactor * invDc;
     double r_dv = u_mix_scale * dmin_(fd(S, F_invDvEdge)[e], 4 * invDc);
     const double *dd = fd(S, F_delsq_divergence), *dvv = fd(S, F_delsq_vorticity);
-    double u_diffusion = colk(fd(S, F_rho_edge), e) * ((colk(dd, cell2) - colk(dd, cell1)) * r_dc -
-                                                 (colk(dvv, vertex2) - colk(dvv, vertex1)) * r_dv);
-    double tue = colk(fd(S, F_tend_u_euler), e);
+    double re, tue, dd1, dd2, dv1, dv2, tend_u, trp;
+    gather2<LP>(fd(S, F_rho_edge), e, fd(S, F_tend_u_euler), e, k, re, tue);
+    gather2s<LP>(dd, cell1, cell2, k, dd1, dd2);
+    gather2s<LP>(dvv, vertex1, vertex2, k, dv1, dv2);
+    gather2<LP>(fd(S, F_tend_u), e, fd(S, F_tend_ru_physics), e, k, tend_u, trp);
+    if (k == L) return;  // (padding levels: zeros, PADW)
+    double u_diffusion = re * ((dd2 - dd1) * r_dc - (dv2 - dv1) * r_dv);
     tue -= u_diffusion;
-    colk(fw(S, F_tend_u_euler), e) = tue;
-    double tend_u = colk(fd(S, F_tend_u), e);
-    tend_u += tue + colk(fd(S, F_tend_ru_physics), e);
-    colk(fw(S, F_tend_u), e) = tend_u;
+    colk(fw(S, F_tend_u_euler), e) = PADW(tue);
+    tend_u += tue + trp;
+    colk(fw(S, F_tend_u), e) = PADW(tend_u);
 }
 
 // ------------------------------------------------------------------------ E (cells)
@@ -623,9 +631,9 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
         if (rk0) twe -= cqw * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
         w += twe;
     }
-    if (kl) {
-        colk(fw(S, F_w), c) = w;
-        if (rk0) colk(fw(S, F_tend_w_euler), c) = twe;
+    if (k != L) {  // (padding levels: zeros, PADW)
+        colk(fw(S, F_w), c) = PADW(w);
+        if (rk0) colk(fw(S, F_tend_w_euler), c) = PADW(twe);
     }
 
     // ================= theta =================
@@ -668,15 +676,15 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     if (k == L - 1) wdtz = rws * (fzm * tms + fzp * tms_m);
     if (k == L) wdtz = wdtzL;
     const double wdtz_p = lvl_up<LP>(wdtz, k);
-    if (!kl) return;
+    if (k == L) return;  // (padding levels: zeros, PADW)
     // :1422-1427, :1477-1479
     tend_theta *= invA - rdzw * (wdtz_p - wdtz);
-    colk(fw(S, F_tend_rtheta_adv), c) = tend_theta;
-    colk(fw(S, F_rthdynten), c) = tend_theta / rho_zz;
+    colk(fw(S, F_tend_rtheta_adv), c) = PADW(tend_theta);
+    colk(fw(S, F_rthdynten), c) = PADW(tend_theta / rho_zz);
     tend_theta += rho_zz * rt_diab;
     tend_theta += tte + trp;
-    colk(fw(S, F_tend_theta), c) = tend_theta;
-    if (rk0) colk(fw(S, F_tend_theta_euler), c) = tte;
+    colk(fw(S, F_tend_theta), c) = PADW(tend_theta);
+    if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
 template <int LP>
