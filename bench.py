@@ -133,8 +133,16 @@ def main():
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="extra mpas_set_option (A/B runs, e.g. xcd=32)")
     ap.add_argument("--replicas", action="store_true", help="N > 1: full-mesh replicas instead of a decomposition")
+    ap.add_argument("--decompose", action="store_true",
+                    help="run the decomposed (RCCL halo) path also at N = 1 (a 1-part decomposition)")
     args = ap.parse_args()
 
+    # Libraries print banners on stdout from C (RCCL's version lines at communicator
+    # creation); the contract is ONE JSON line there: route fd 1 to stderr for the run
+    # and print the result through a saved copy of the original stdout.
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -150,7 +158,7 @@ def main():
     ncells, L = args.ncells, args.levels
     dt = dt_for(ncells)
     m, st = build_inputs(ncells, L)
-    decomposed = world > 1 and not args.replicas
+    decomposed = (world > 1 and not args.replicas) or args.decompose
     halo_info = None
     if decomposed:
         from mpasdyn import decomp
@@ -162,15 +170,17 @@ def main():
         uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
         if rank == 0:
             uid.copy_(torch.frombuffer(bytearray(lib.rccl_unique_id()), dtype=torch.uint8))
-        dist.broadcast(uid, 0)
+        if dist is not None:
+            dist.broadcast(uid, 0)
         lib.halo_rccl(ctx, world, rank, uid.cpu().numpy().tobytes())
-        ctx.set_option("overlap", halo_info["overlap"])
+        overlap = int(os.environ.get("MPAS_OVERLAP", "1"))
+        ctx.set_option("overlap", overlap)
         own = dec.n_owned(rank)
         nint = dec.n_interior(rank)
         halo_info = {"partition": f"{world} contiguous Morton blocks of cells", "owned": list(own),
                      "ghost_frac": [round(1 - o / n, 4) for o, n in zip(own, dims[:3])],
                      "interior_frac": [round(i / max(o, 1), 4) for i, o in zip(nint, own)],
-                     "overlap": int(os.environ.get("MPAS_OVERLAP", "1"))}
+                     "overlap": overlap}
         st = lst
         work_dims = (*own, L)  # what this rank computes
     else:
@@ -265,7 +275,7 @@ def main():
         out["cpu_baseline"] = None
     ctx.close()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=json_out, flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -211,6 +211,33 @@ extern "C" int ub_streamp(const double* a, const double* b, int n, double* d, in
     s_addp<<<(n + 3) / 4, 256, 0, (hipStream_t)stream>>>(a, b, n, d, mode);
     return (int)hipGetLastError();
 }
+// streaming-ceiling variants, 16 B per lane, grid-stride over n doubles2:
+// 0 copy a->d, 1 d = a + b, 2 = 1 with nontemporal stores, 3 = 0 with nontemporal
+// stores, 4 read-only (a + b summed per thread, one store per thread block)
+__global__ __launch_bounds__(256) void s_var(const double2* __restrict__ a, const double2* __restrict__ b, size_t n,
+                                             double2* __restrict__ d, int mode) {
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t stride = (size_t)gridDim.x * 256;
+    double acc = 0.0;
+    for (; i < n; i += stride) {
+        double2 x = a[i];
+        if (mode == 0) d[i] = x;
+        else if (mode == 3) { __builtin_nontemporal_store(x.x, &d[i].x); __builtin_nontemporal_store(x.y, &d[i].y); }
+        else {
+            const double2 y = b[i];
+            x.x += y.x;
+            x.y += y.y;
+            if (mode == 1) d[i] = x;
+            else if (mode == 2) { __builtin_nontemporal_store(x.x, &d[i].x); __builtin_nontemporal_store(x.y, &d[i].y); }
+            else acc += x.x + x.y;
+        }
+    }
+    if (mode == 4 && acc == 12345.678) d[0].x = acc;
+}
+extern "C" int ub_svar(const double* a, const double* b, long n2, double* d, int mode, int grid, void* stream) {
+    s_var<<<grid, 256, 0, (hipStream_t)stream>>>((const double2*)a, (const double2*)b, (size_t)n2, (double2*)d, mode);
+    return (int)hipGetLastError();
+}
 extern "C" int ub_stream(const double* a, const double* b, int n, double* d, int W, void* stream) {
     s_add<<<(n + 3) / 4, 256, 0, (hipStream_t)stream>>>(a, b, n, d, W);
     return (int)hipGetLastError();

@@ -150,6 +150,23 @@ for mode in (0, 1, 2, 3, 4, 0, 1, 2, 3, 4):
         ts.append(e0.elapsed_time(e1))
     t = sorted(ts[1:])[len(ts[1:]) // 2]
     res["stream holes mode%d" % mode] = {"ms": round(t, 4)}
+lib.ub_svar.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                        ctypes.c_void_p]
+n2 = nE * 32
+for mode in (0, 1, 2, 3, 4):
+    for grid in (2048, 8192, n2 // 256):
+        ts = []
+        for rep in range(6):
+            flush.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            lib.ub_svar(A.data_ptr(), B.data_ptr(), n2, D.data_ptr(), mode, grid, st)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        t = sorted(ts[1:])[len(ts[1:]) // 2]
+        nb = {0: 2, 1: 3, 2: 3, 3: 2, 4: 2}[mode] * nE * 512
+        res["svar mode%d grid%d" % (mode, grid)] = {"ms": round(t, 4), "TBs": round(nb / t / 1e9, 2)}
 for fn in ("ub_stream16", "ub_stream8"):
     f = getattr(lib, fn)
     f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
