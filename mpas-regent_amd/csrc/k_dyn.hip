@@ -209,13 +209,10 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     gather2s<LP>(fd(S, F_rw), cell1, cell2, k, rw1, rw2);
     gather2s<LP>(fd(S, F_w), cell1, cell2, k, w1, w2);
     gather2<LP>(fd(S, F_rho_edge), e, pv_f, e, k, rho_edge, pv);
-    u = ldz(live, u);
-    ru_e = ldz(live, ru_e);
-    rw1 = ldz(live, rw1);
-    rw2 = ldz(live, rw2);
-    w1 = ldz(live, w1);
-    w2 = ldz(live, w2);
-    rho_edge = ldz(live, rho_edge);
+    // No level masks (ldz) in this kernel: lanes k >= L store nothing (k > L: PADW
+    // zeros), so a value used in its own lane needs none, and the vertical shuffles
+    // (lvl_up/dn) of u and w bring lanes k <= L only levels <= L -- exactly what the
+    // masks kept.  (Each ldz is two v_cndmask per double; B was half VALU-bound.)
     const double wduzL = fd(S, F_wduz)[(size_t)e * LP + lpos(LP, L)];  // one value: the level-L slot
     const int neoe = rec[21];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
@@ -230,11 +227,6 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     for (int j = 0; j < QF; j += 2) {
         gather2s<LP>(u_f, ee_[j], ee_[j + 1], k, ue_[j], ue_[j + 1]);
         gather2s<LP>(pv_f, ee_[j], ee_[j + 1], k, pve_[j], pve_[j + 1]);
-    }
-#pragma unroll
-    for (int j = 0; j < QF; j++) {
-        ue_[j] = ldz(kl, ue_[j]);
-        pve_[j] = ldz(kl, pve_[j]);
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = rec[22];
@@ -252,8 +244,6 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
 #pragma unroll
     for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
     gather2<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k, tv_[AF - 1], tr_phys);
-#pragma unroll
-    for (int j = 0; j < AF; j++) tv_[j] = ldz(kl, tv_[j]);
 
     // loads of the later sections, also ahead of every store (a store could alias them
     // for the compiler, which would then issue them only after it)
