@@ -359,8 +359,9 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
     ColMap<LP> m(S, KV);
-    if (m.blk < nVB) {  // delsq_vorticity (:1052-1060)
-        const int vx = m.ent, k = m.k;
+    int bi;
+    if (vc_block(S, m.blk, nVB, bi)) {  // delsq_vorticity (:1052-1060)
+        const int vx = col_of<LP>(bi) + S.lo[KV], k = m.k;
         if (vx >= S.nVO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
         const int* eov = fi(S, F_edgesOnVertex) + (size_t)vx * 3;
         const double* sgn = fd(S, F_edgesOnVertex_sign) + (size_t)vx * 3;
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         colk(fw(S, F_delsq_vorticity), vx) = dsv;
         return;
     }
-    const int c = col_of<LP>(m.blk - nVB) + S.lo[KC];
+    const int c = col_of<LP>(bi) + S.lo[KC];
     const int k = m.k;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + lpos(LP, k);

@@ -19,7 +19,9 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
     const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
     ColMapN<LP, EPW> m(S, KV);
     const int k = m.k;
-    if (m.blk < nVB) {  // EPW vertices: vorticity, pv_vertex (:381-396)
+    int bi;
+    if (vc_block(S, m.blk, nVB, bi)) {  // EPW vertices: vorticity, pv_vertex (:381-396)
+        m.base = col_of<LP>(bi) * EPW + S.lo[KV];
         int ev[EPW][3];
         double sg_[EPW][3], dc_[EPW][3], u_[EPW][3], iat[EPW], fv[EPW];
 #pragma unroll
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         return;
     }
     // EPW cells: divergence (Q9 "s + u") and ke (:369-379, :357-367)
-    const int c0 = col_of<LP>(m.blk - nVB) * EPW + S.lo[KC];
+    const int c0 = col_of<LP>(bi) * EPW + S.lo[KC];
     int ne[EPW], e_[EPW][NF];
     double u_[EPW][NF], sgn_[EPW][NF], dv_[EPW][NF], dc_[EPW][NF], invA[EPW];
 #pragma unroll

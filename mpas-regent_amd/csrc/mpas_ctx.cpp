@@ -299,6 +299,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.L = dims->nVertLevels;
         c->S.LP = LP;
         c->S.epw = 2;  // tools/kbench.py: div_damp -3 %, solve_diagnostics -4 % vs 1
+        c->S.vcmix = 1;
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         for (int f = 0; f < X_COUNT; f++) {
@@ -365,6 +366,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "epw") == 0) {
             if (value != 1 && value != 2 && value != 4) throw Fail{MPAS_EINVAL, "epw must be 1, 2 or 4"};
             c->S.epw = (int)value;
+        } else if (name && std::strcmp(name, "vcmix") == 0) {
+            c->S.vcmix = value ? 1 : 0;
         } else if (name && std::strcmp(name, "overlap") == 0) {
             c->overlap = value ? 1 : 0;
             if (c->halo) c->halo->overlap = c->overlap;
@@ -381,6 +384,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         if (name && std::strcmp(name, "exact") == 0) *value = c->exact;
         else if (name && std::strcmp(name, "xcd") == 0) *value = c->S.xcd;
         else if (name && std::strcmp(name, "epw") == 0) *value = c->S.epw;
+        else if (name && std::strcmp(name, "vcmix") == 0) *value = c->S.vcmix;
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "selfc") == 0) {

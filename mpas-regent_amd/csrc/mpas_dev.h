@@ -85,6 +85,7 @@ struct DevState {
     int lo[3];          // first cell / edge / vertex of a launch: kernels compute entities
                         // [lo, nXO); 0 except for the boundary launch of a halo overlap
     int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
+    int vcmix;  // 1: the vertex and cell blocks of mixed grids interleaved in proportion (vc_block)
     int xcd;  // block order: 0 dispatcher, 1 one contiguous eighth per XCD, G > 1 runs of G
               // blocks per XCD in windows of 8G (default 64)
     int selfc;  // 1 when every cell is one of the two cellsOnEdge of each of its first
@@ -182,6 +183,23 @@ __device__ __forceinline__ int xcd_block(int on) {
     if (b >= (nb / W) * W) return b;
     const int w = b / W, r = b - w * W;
     return w * W + (r & 7) * on + (r >> 3);
+}
+
+// Mixed vertex + cell grids (dyn_tend C, solve_diagnostics): nVB vertex blocks and
+// nb - nVB cell blocks.  With S.vcmix they are interleaved in proportion -- block b is a
+// vertex block iff floor((b+1) nVB / nb) > floor(b nVB / nb) -- so that the vertex and
+// the cell blocks of one region of the Morton-ordered mesh run at the same time and the
+// edge columns both gather are fetched into L2 once; otherwise all vertex blocks come
+// first.  Returns true for a vertex block; idx = its vertex (or cell) block index.
+__device__ __forceinline__ bool vc_block(const DevState& S, int blk, int nVB, int& idx) {
+    if (!S.vcmix) {
+        idx = blk < nVB ? blk : blk - nVB;
+        return blk < nVB;
+    }
+    const long long nb = (long long)gridDim.x;
+    const int a = (int)((long long)blk * nVB / nb), a1 = (int)((long long)(blk + 1) * nVB / nb);
+    idx = a1 > a ? a : blk - a;
+    return a1 > a;
 }
 
 // entity of this lane's column in virtual block blk; at LP == 64 one column per
