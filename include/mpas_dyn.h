@@ -52,11 +52,14 @@ int mpas_sync(mpas_ctx* ctx);
 int mpas_get_stream(mpas_ctx* ctx, void** stream);
 /* options: "exact" = 1 makes the two reassociated kernels (Q10 q sum, acoustic scan)
  * evaluate the reference's literal order (bit-identical to the oracle, slower);
- * "xcd" = 0 dispatcher block order (default), 1 one contiguous eighth of the columns per XCD,
- * G > 1 runs of G blocks per XCD inside windows of 8G (A/B measurements; results
- * unchanged); "self" = 0 disables the SELF gathers (A/B; results unchanged). */
+ * "xcd" = 0 dispatcher block order, 1 one contiguous eighth of the columns per XCD,
+ * G > 1 runs of G blocks per XCD inside windows of 8G (default 64); "epw" = 1, 2 (default)
+ * or 4 entities per column slot in div_damping / solve_diagnostics; "vcmix" = 1 (default)
+ * interleaves the vertex and cell blocks of the mixed grids; "overlap" = 1 (default)
+ * computes interior entities beside the halo exchange of a decomposed mesh; "self" = 0
+ * disables the SELF gathers.  All but "exact" change only speed, never results. */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
-/* reads "exact", "xcd", "self" (the SELF-gather switch, default 1: when every cell is
+/* reads every option above ("self", default 1: when every cell is
  * among the cellsOnEdge of its own edges -- mpas-mode ids -- the cell kernels gather
  * only the other cell of an edge) and "selfc" (read-only: whether the SELF gathers are
  * in use for the uploaded mesh). */
