@@ -115,6 +115,10 @@ int mpas_atm_recover_large_step_variables_work(mpas_ctx* ctx, int ns, int rk_ste
 /* :1893 mpas_reconstruct_2d(cr, er, includeHalos, on_a_sphere); atm_core_init
  *       (atm_core.rg:33); commented out of atm_srk3 (rk_timestep.rg:487) */
 int mpas_reconstruct_2d(mpas_ctx* ctx, int includeHalos, int on_a_sphere);
+/* :729 atm_compute_output_diagnostics(cr), main.rg:70 after the time loop: rho = rho_zz * zz,
+ *       pressure = pressure_base + pressure_p on levels 0..nVertLevels-1 (theta is in the
+ *       task's write set but its statement is commented out in the reference: unchanged) */
+int mpas_atm_compute_output_diagnostics(mpas_ctx* ctx);
 /* rk_timestep.rg:29 summarize_timestep(cr, er, config_print_detailed_minmax_vel,
  *       config_print_global_minmax_vel, config_print_global_minmax_sca): the values the
  *       reference prints, into out[31] (host memory; the call synchronises):

@@ -215,6 +215,31 @@ hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sph
     MPAS_LP_DISPATCH(S.LP, reconstruct_lp, S, st, on_a_sphere);
 }
 
+// ---------------------------------------------------------------- output diagnostics
+// dynamics_tasks.rg:729-746: rho = rho_zz * zz, pressure = pressure_base + pressure_p over
+// cells x levels 0..nVertLevels-1 (the theta statement is commented out there)
+template <int LP>
+__global__ __launch_bounds__(256) void k_output_diag(DevState S) {
+    ColMap<LP> m(S, KC);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO || k == L) return;
+    double rz, zz, pb, pp;
+    gather2<LP>(fd(S, F_rho_zz), c, fd(S, F_zz), c, k, rz, zz);
+    gather2<LP>(fd(S, F_pressure_base), c, fd(S, F_pressure_p), c, k, pb, pp);
+    colk(fw(S, F_rho), c) = PADW(rz * zz);
+    colk(fw(S, F_pressure), c) = PADW(pb + pp);
+}
+template <int LP>
+static hipError_t output_diag_lp(const DevState& S, hipStream_t st) {
+    const int nb = col_blocks<LP>(S, KC);
+    if (nb) k_output_diag<LP><<<nb, 256, 0, st>>>(S);
+    HALO_WROTE(S, F_rho, F_pressure);
+    return hipGetLastError();
+}
+hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st) {
+    MPAS_LP_DISPATCH(S.LP, output_diag_lp, S, st);
+}
+
 // ---------------------------------------------------------------- summarize_timestep
 // Sequential semantics made parallel.  The points of a field are numbered in the
 // reference's loop order, idx = entity * nVertLevels + k; every thread scans one

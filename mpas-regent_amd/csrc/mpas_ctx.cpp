@@ -695,6 +695,9 @@ int mpas_reconstruct_2d(mpas_ctx* c, int includeHalos, int on_a_sphere) {
     (void)includeHalos;  // :1909-1912: the range is nCells either way
     MPAS_TASK("mpas_reconstruct_2d", launch_reconstruct_2d(c->S, c->stream, on_a_sphere ? 1 : 0));
 }
+int mpas_atm_compute_output_diagnostics(mpas_ctx* c) {
+    MPAS_TASK("atm_compute_output_diagnostics", launch_output_diagnostics(c->S, c->stream));
+}
 int mpas_summarize_timestep(mpas_ctx* c, int detailed, int global_vel, int global_sca, double* out) {
     (void)global_sca;  // prints a blank line only (rk_timestep.rg:352-357)
     return guarded(c, [&] {

@@ -158,6 +158,7 @@ hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t see
 hipError_t launch_prepare(DevState& S, hipStream_t st);
 hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt);
 hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
+hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
 size_t summarize_scratch_bytes();
 hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, double* out);
 

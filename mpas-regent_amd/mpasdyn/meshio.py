@@ -189,6 +189,46 @@ def write_graph_info_part(path, part):
     np.savetxt(path, np.asarray(part, dtype=np.int64), fmt="%d")
 
 
+# write_output_plotting (mesh_loading.rg:810-1191): the mesh variables it defines (those
+# the Mesh holds), then level 0 of the state fields below
+OUTPUT_MESH_VARS = ["latCell", "lonCell", "meshDensity", "xCell", "yCell", "zCell", "latEdge", "lonEdge",
+                    "xEdge", "yEdge", "zEdge", "latVertex", "lonVertex", "xVertex", "yVertex", "zVertex",
+                    "cellsOnEdge", "nEdgesOnCell", "nEdgesOnEdge", "edgesOnCell", "edgesOnEdge", "weightsOnEdge",
+                    "dvEdge", "dv1Edge", "dv2Edge", "dcEdge", "angleEdge", "areaCell", "areaTriangle", "cellsOnCell",
+                    "verticesOnCell", "verticesOnEdge", "edgesOnVertex", "cellsOnVertex", "kiteAreasOnVertex"]
+OUTPUT_STATE_VARS = {"u": "nEdges", "v": "nEdges", "w": "nCells", "pressure": "nCells", "pressure_p": "nCells",
+                     "rho": "nCells", "theta": "nCells", "surface_pressure": "nCells"}
+
+
+def write_output_plotting(path, m, st):
+    """timestep_output.nc as mesh_loading.rg:810-1191 writes it: the grid variables,
+    indexToCellID/EdgeID/VertexID (1-based), and level 0 of u, v (edges), w, pressure,
+    pressure_p, rho, theta, surface_pressure (cells) from the state st (e.g. after
+    atm_compute_output_diagnostics and a download).  Grid variables the Mesh does not
+    hold (dv1Edge, dv2Edge for the generated meshes) are left out."""
+    from scipy.io import netcdf_file
+    dims = {"nCells": m.nCells, "nEdges": m.nEdges, "nVertices": m.nVertices,
+            "maxEdges": m.edgesOnCell.shape[1], "maxEdges2": m.edgesOnEdge.shape[1], "TWO": 2,
+            "vertexDegree": m.edgesOnVertex.shape[1], "nVertLevels": st.L}
+    with netcdf_file(path, "w", version=2) as f:
+        f.createDimension("Time", None)  # (scipy's writer wants the record dimension first)
+        for d, n in dims.items():
+            f.createDimension(d, int(n))
+        for v in OUTPUT_MESH_VARS:
+            if not hasattr(m, v):
+                continue
+            a = np.asarray(getattr(m, v))
+            dv = _DIMS.get(v, ("nEdges",))
+            var = f.createVariable(v, "i4" if a.dtype.kind in "iu" else "f8", dv)
+            var[:] = a
+        for v, n in (("indexToCellID", m.nCells), ("indexToEdgeID", m.nEdges), ("indexToVertexID", m.nVertices)):
+            f.createVariable(v, "i4", ({"indexToCellID": "nCells", "indexToEdgeID": "nEdges"}.get(v, "nVertices"),))[:] = \
+                np.arange(1, n + 1, dtype=np.int32)
+        for v, dim in OUTPUT_STATE_VARS.items():
+            n = dims[dim]
+            f.createVariable(v, "f8", (dim,))[:] = np.asarray(st[v])[:n, 0]
+
+
 def main(argv=None):
     """python -m mpasdyn.meshio GRID.nc [--renumber OUT.nc] [--parts N]: read an MPAS grid,
     optionally write it Morton-renumbered, optionally write OUT's (or GRID's)

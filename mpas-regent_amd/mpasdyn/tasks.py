@@ -89,6 +89,11 @@ def mpas_reconstruct_2d(ctx, includeHalos=False, on_a_sphere=True):
                "mpas_reconstruct_2d")
 
 
+def atm_compute_output_diagnostics(ctx):
+    """dynamics_tasks.rg:729 (main.rg:70, after the time loop): rho, pressure"""
+    ctx._check(ctx.lib.mpas_atm_compute_output_diagnostics(ctx.h), "atm_compute_output_diagnostics")
+
+
 def summarize_timestep(ctx, config_print_detailed_minmax_vel=False, config_print_global_minmax_vel=False,
                        config_print_global_minmax_sca=False):
     """rk_timestep.rg:29; returns the 31 values the reference prints (layout: include/mpas_dyn.h)"""

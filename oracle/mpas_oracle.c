@@ -974,6 +974,20 @@ void ora_atm_recover_large_step_variables_work(ora_state* S, int ns, int rk_step
     }
 }
 
+/* ===================== atm_compute_output_diagnostics, dynamics_tasks.rg:729-746 (the
+ * theta statement :740 is commented out in the reference; theta is left as it is)   */
+void ora_atm_compute_output_diagnostics(ora_state* S) {
+    const int L = S->L, nC = S->nCells;
+    double *rho = D(rho), *pressure = D(pressure);
+    const double *rho_zz = D(rho_zz), *zz = D(zz), *pb = D(pressure_base), *pp = D(pressure_p);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++)
+        for (int k = 0; k < L; k++) {
+            CW(rho, c, k) = CW(rho_zz, c, k) * CW(zz, c, k);
+            CW(pressure, c, k) = CW(pb, c, k) + CW(pp, c, k);
+        }
+}
+
 /* ===================== mpas_reconstruct_2d, dynamics_tasks.rg:1893-1948 (levels
  * 0..nVertLevels-1 of every cell; includeHalos does not change the range there).   */
 void ora_mpas_reconstruct_2d(ora_state* S, int includeHalos, int on_a_sphere) {

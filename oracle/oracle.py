@@ -53,6 +53,7 @@ def load():
             "ora_atm_srk3": (None, [p, dbl, i32]),
             "ora_atm_recover_large_step_variables_work": (None, [p, i32, i32, dbl]),
             "ora_mpas_reconstruct_2d": (None, [p, i32, i32]),
+            "ora_atm_compute_output_diagnostics": (None, [p]),
             "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
         }
         for n, (res, args) in sig.items():
@@ -117,6 +118,9 @@ class Oracle:
 
     def atm_recover_large_step_variables_work(self, ns, rk_step, dt):
         self.lib.ora_atm_recover_large_step_variables_work(self.p, ns, rk_step, dt)
+
+    def atm_compute_output_diagnostics(self):
+        self.lib.ora_atm_compute_output_diagnostics(self.p)
 
     def mpas_reconstruct_2d(self, includeHalos=False, on_a_sphere=True):
         self.lib.ora_mpas_reconstruct_2d(self.p, int(includeHalos), int(on_a_sphere))

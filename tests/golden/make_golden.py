@@ -34,6 +34,7 @@ CASES = {
     "recover_ns2_rk0": lambda o: o.atm_recover_large_step_variables_work(2, 0, 240.0),
     "recover_ns3_rk2": lambda o: o.atm_recover_large_step_variables_work(3, 2, 240.0),
     "reconstruct_2d": lambda o: o.mpas_reconstruct_2d(False, True),
+    "output_diagnostics": lambda o: o.atm_compute_output_diagnostics(),
 }
 
 

@@ -62,6 +62,8 @@ TASKS = [
      set()),
     ("finish_2_2", lambda o: o.atm_rk_dynamics_substep_finish(2, 2), lambda c: T.atm_rk_dynamics_substep_finish(c, 2, 2),
      set()),
+    ("output_diagnostics", lambda o: o.atm_compute_output_diagnostics(), lambda c: T.atm_compute_output_diagnostics(c),
+     set()),
 ]
 
 _STATES = {}

@@ -125,3 +125,21 @@ def test_meshio_cli(tmp_path, x1_2562):
     assert np.array_equal(r.xCell, meshio.renumber(x1_2562)[0].xCell)
     part = meshio.read_graph_info_part(str(tmp_path / "x1.2562.morton.graph.info.part.8"), r.nCells)
     assert np.array_equal(part, meshio.partition_sfc(r, 8))
+
+
+def test_write_output_plotting(tmp_path, x1_2562):
+    """mesh_loading.rg:810-1191: grid variables + level 0 of the output fields, after
+    atm_compute_output_diagnostics (oracle)"""
+    from scipy.io import netcdf_file
+    st = make_state(x1_2562, 5, "random")
+    O.Oracle(st).atm_compute_output_diagnostics()
+    p = tmp_path / "timestep_output.nc"
+    meshio.write_output_plotting(str(p), x1_2562, st)
+    with netcdf_file(str(p), "r", mmap=False) as f:
+        assert f.dimensions["nVertLevels"] == 5 and f.dimensions["Time"] is None
+        assert np.array_equal(f.variables["edgesOnCell"].data, x1_2562.edgesOnCell)
+        assert np.array_equal(f.variables["indexToEdgeID"].data, np.arange(1, x1_2562.nEdges + 1))
+        assert np.array_equal(f.variables["u"].data, st["u"][:x1_2562.nEdges, 0])
+        assert np.array_equal(f.variables["rho"].data, st["rho_zz"][:2562, 0] * st["zz"][:2562, 0])
+        assert np.array_equal(f.variables["pressure"].data, st["pressure"][:2562, 0])
+        assert "dv1Edge" not in f.variables  # not in the grid fixture

@@ -191,6 +191,19 @@ def test_numpy_restatement_div_damping(x1_2562):
         assert np.array_equal(st["ru_p"][:nE, k], np.where(on, new, ref["ru_p"][:nE, k]))
 
 
+def test_numpy_restatement_output_diagnostics(x1_2562):
+    """dynamics_tasks.rg:737-744 restated with numpy; theta untouched (:740 commented out)"""
+    st = make_state(x1_2562, 5, "random")
+    ref = st.copy()
+    O.Oracle(st).atm_compute_output_diagnostics()
+    n, L = st.nCells, st.L
+    assert np.array_equal(st["rho"][:n, :L], ref["rho_zz"][:n, :L] * ref["zz"][:n, :L])
+    assert np.array_equal(st["pressure"][:n, :L], ref["pressure_base"][:n, :L] + ref["pressure_p"][:n, :L])
+    for f in ("rho", "pressure"):  # level nVertLevels and the zero slot are not written
+        assert np.array_equal(st[f][:, L], ref[f][:, L]) and np.array_equal(st[f][n], ref[f][n])
+    assert np.array_equal(st["theta"], ref["theta"])
+
+
 def test_numpy_restatement_reconstruct_2d(x1_2562):
     """dynamics_tasks.rg:1913-1947 restated with numpy (on a sphere and not)"""
     for sphere in (True, False):
