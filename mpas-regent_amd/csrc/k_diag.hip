@@ -222,10 +222,11 @@ template <int LP>
 __global__ __launch_bounds__(256) void k_output_diag(DevState S) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCO || k == L) return;
+    if (c >= S.nCO) return;
     double rz, zz, pb, pp;
-    gather2<LP>(fd(S, F_rho_zz), c, fd(S, F_zz), c, k, rz, zz);
+    gather2<LP>(fd(S, F_rho_zz), c, fd(S, F_zz), c, k, rz, zz);  // (every lane: gather2)
     gather2<LP>(fd(S, F_pressure_base), c, fd(S, F_pressure_p), c, k, pb, pp);
+    if (k == L) return;
     colk(fw(S, F_rho), c) = PADW(rz * zz);
     colk(fw(S, F_pressure), c) = PADW(pb + pp);
 }
