@@ -240,6 +240,10 @@ def main():
         avg = ms / calls
         tasks_out[name] = {"launches_per_step": calls // n_prof, "avg_ms": round(avg, 4),
                            "b_alg_GB": round(b / 1e9, 4), "GBs": round(b / (avg * 1e-3) / 1e9, 1)}
+        tr = pmc_traffic(name, ncells, L) if not decomposed else None
+        if tr:  # SURVEY §8.5 metric 2: measured (FETCH + WRITE) bytes over this run's launch time
+            tasks_out[name]["hbm_GB_measured"] = round(tr / 1e9, 4)
+            tasks_out[name]["hbm_frac_measured"] = round(tr / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     dom = max(tasks_out, key=lambda k: tasks_out[k]["avg_ms"] * tasks_out[k]["launches_per_step"])
     dt_ = tasks_out[dom]
     task, kw = kw_of.get(dom, (dom, {}))
@@ -247,7 +251,8 @@ def main():
     traffic = round(traffic / 1e9, 4) if traffic else None
     roof = {"bound": "hbm", "kernel": dom, "achieved": dt_["GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(dt_["GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "GB/launch",
-            "b_alg_per_launch_GB": dt_["b_alg_GB"], "avg_launch_ms": dt_["avg_ms"]}
+            "b_alg_per_launch_GB": dt_["b_alg_GB"], "avg_launch_ms": dt_["avg_ms"],
+            "traffic_frac": dt_.get("hbm_frac_measured")}
     b_step = roofline.b_alg_step(work_dims)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
