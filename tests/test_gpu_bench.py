@@ -1,0 +1,39 @@
+"""bench.py's contract (one JSON line on stdout, the keys the driver reads) on the GPU, for
+the single-GPU path and for the decomposed (RCCL halo) path at one rank -- the code the
+multi-GPU run executes, short of the peers."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
+
+
+def run_bench(*args):
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", *args], capture_output=True, text=True, timeout=110, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, f"stdout must be ONE JSON line, got {len(lines)}: {p.stdout[:500]}"
+    return json.loads(lines[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["single", "decompose"])
+def test_bench_line(mode):
+    d = run_bench(*(["--decompose"] if mode == "decompose" else []))
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["value"] > 0 and d["ms_per_step"] > 0
+    assert d["unit"] == "Mcell-columns/s" and d["dtype"] == "f64" and d["cpu_baseline"] is None
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    if mode == "decompose":
+        assert d["scaling"] == "strong" and d["config"]["parallelism"] == "decomposed1"
+        assert d["halo"]["exchanges_per_step"] > 0 and d["halo"]["ghost_frac"] == [0.0, 0.0, 0.0]
+    else:
+        assert d["scaling"] == "weak" and d["config"]["parallelism"] == "single-gpu"
