@@ -19,7 +19,9 @@
 
 namespace mpas {
 
-template <int LP, bool EXACT, bool SELF>
+// FIRST: small_step == 0, where rho_pp, rtheta_pp, rw_p and wwAvg start from 0 (:1615-1636):
+// their columns are not read at all (4 of the 19 own columns)
+template <int LP, bool EXACT, bool SELF, bool FIRST>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -47,8 +49,12 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     row_ld(cdv, cdv_);
     // (gather2 / col_rd2: two columns per load instruction)
     double rtp, rpp, rwp, ww, tm, tend_rho, w, coftz, zz, rz, cofwt, cofwz, cofwr, a_tri, alpha, rws, rw, dss;
-    col_rd2<LP>(rtp_f, rpp_f, c, k, L, rtp, rpp);
-    col_rd2<LP>(rwp_f, ww_f, c, k, L, rwp, ww);
+    if constexpr (FIRST) {
+        rtp = rpp = rwp = ww = 0.0;
+    } else {
+        col_rd2<LP>(rtp_f, rpp_f, c, k, L, rtp, rpp);
+        col_rd2<LP>(rwp_f, ww_f, c, k, L, rwp, ww);
+    }
     col_rd2<LP>(fd(S, F_theta_m), fd(S, F_tend_rho), c, k, L, tm, tend_rho);
     static_assert(NF % 2 == 0, "slot pairs");
 #pragma unroll
@@ -198,13 +204,16 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     auto run = [&](const DevState& X) {
         const int grid = col_blocks<LP>(X, KC);
         if (!grid) return;
+#define MPAS_ACOUSTIC(E, SF, F) k_acoustic<LP, E, SF, F><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm)
+        const bool first = small_step == 0;
         if (exact) {
-            if (X.selfc) k_acoustic<LP, true, true><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
-            else k_acoustic<LP, true, false><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
+            if (X.selfc) first ? MPAS_ACOUSTIC(true, true, true) : MPAS_ACOUSTIC(true, true, false);
+            else first ? MPAS_ACOUSTIC(true, false, true) : MPAS_ACOUSTIC(true, false, false);
         } else {
-            if (X.selfc) k_acoustic<LP, false, true><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
-            else k_acoustic<LP, false, false><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm);
+            if (X.selfc) first ? MPAS_ACOUSTIC(false, true, true) : MPAS_ACOUSTIC(false, true, false);
+            else first ? MPAS_ACOUSTIC(false, false, true) : MPAS_ACOUSTIC(false, false, false);
         }
+#undef MPAS_ACOUSTIC
     };
     HALO_RUN(S, st, run, F_ru_p, F_theta_m);
     HALO_WROTE(S, F_rtheta_pp_old, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
