@@ -216,7 +216,10 @@ static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st); }
 
 // ---------------------------------------------------------------- divergence damping
-template <int LP, int EPW>
+// OLD0: rtheta_pp_old is known to be 0.0 (srk3, right after the first acoustic substep
+// of a stage, which sets it so on every cell, :1615-1618): its columns are not read, and
+// -(r - 0.0) is the same value as the literal expression gives
+template <int LP, int EPW, bool OLD0>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
     ColMapN<LP, EPW> m(S, KE);
     const int L = S.L, k = m.k;
@@ -240,7 +243,8 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
         sh1[i] = sh[c1[i]];
         sh2[i] = sh[c2[i]];
         gather2s<LP>(rtp, c1[i], c2[i], k, r1[i], r2[i]);
-        gather2s<LP>(rtpo, c1[i], c2[i], k, ro1[i], ro2[i]);
+        if (OLD0) ro1[i] = ro2[i] = 0.0;
+        else gather2s<LP>(rtpo, c1[i], c2[i], k, ro1[i], ro2[i]);
         gather2s<LP>(tm, c1[i], c2[i], k, t1[i], t2[i]);
     }
 #pragma unroll
@@ -253,28 +257,29 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
     }
 }
 template <int LP>
-static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts) {
+static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts, int old_zero) {
     double smdiv = kSmdiv;
     double rdts = 1.0 / dts;
     double coef_divdamp = 2.0 * smdiv * kLenDisp * rdts;
     auto run = [&](const DevState& X) {
-        if (X.epw == 4) {
-            const int nb = col_blocks_n<LP, 4>(X, KE);
-            if (nb) k_div_damp<LP, 4><<<nb, 256, 0, st>>>(X, coef_divdamp);
-        } else if (X.epw == 2) {
-            const int nb = col_blocks_n<LP, 2>(X, KE);
-            if (nb) k_div_damp<LP, 2><<<nb, 256, 0, st>>>(X, coef_divdamp);
-        } else {
-            const int nb = col_blocks_n<LP, 1>(X, KE);
-            if (nb) k_div_damp<LP, 1><<<nb, 256, 0, st>>>(X, coef_divdamp);
-        }
+#define MPAS_DIVDAMP(EPW)                                                                    \
+    do {                                                                                     \
+        const int nb = col_blocks_n<LP, EPW>(X, KE);                                         \
+        if (nb && old_zero) k_div_damp<LP, EPW, true><<<nb, 256, 0, st>>>(X, coef_divdamp);  \
+        else if (nb) k_div_damp<LP, EPW, false><<<nb, 256, 0, st>>>(X, coef_divdamp);        \
+    } while (0)
+        if (X.epw == 4) MPAS_DIVDAMP(4);
+        else if (X.epw == 2) MPAS_DIVDAMP(2);
+        else MPAS_DIVDAMP(1);
+#undef MPAS_DIVDAMP
     };
-    HALO_RUN(S, st, run, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
+    if (old_zero) HALO_RUN(S, st, run, F_rtheta_pp, F_theta_m);
+    else HALO_RUN(S, st, run, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
     HALO_WROTE(S, F_ru_p);
     return hipGetLastError();
 }
-hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts) {
-    MPAS_LP_DISPATCH(S.LP, divdamp_lp, S, st, dts);
+hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts, int old_zero) {
+    MPAS_LP_DISPATCH(S.LP, divdamp_lp, S, st, dts, old_zero);
 }
 
 // ---------------------------------------------------------------- substep finish

@@ -241,7 +241,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         for (int small_step = 0; small_step < number_sub_steps[rk_step] + 1; small_step++) {  // Q5
             run_task(c, "atm_advance_acoustic_step_work",
                      [&] { return launch_acoustic(S, st, rk_sub_timestep[rk_step], small_step, c->exact); });
-            run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, rk_sub_timestep[rk_step]); });
+            run_task(c, "atm_divergence_damping_3d",
+                     [&] { return launch_div_damping(S, st, rk_sub_timestep[rk_step], small_step == 0); });
         }
         run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
     }

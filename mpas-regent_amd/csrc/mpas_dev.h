@@ -151,7 +151,8 @@ hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts);
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact);
-hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts);
+// old_zero: only from srk3, right after a stage's first acoustic substep (k_div_damp OLD0)
+hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts, int old_zero = 0);
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step);
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
