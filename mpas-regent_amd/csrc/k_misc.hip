@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
     double *rws = fw(S, F_rw_save), *rtps = fw(S, F_rtheta_p_save), *rps = fw(S, F_rho_p_save);
     double *w2 = fw(S, F_w_2), *tm2 = fw(S, F_theta_m_2), *rz2 = fw(S, F_rho_zz_2), *rzo = fw(S, F_rho_zz_old_split);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
+        if (plev(S.LP, (int)(i & (size_t)(S.LP - 1))) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         rws[i] = rw[i];
         rtps[i] = rtp[i];
         rps[i] = rp[i];
@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_setup_edges(DevState S) {
     const double *ru = fd(S, F_ru), *u = fd(S, F_u);
     double *rus = fw(S, F_ru_save), *u2 = fw(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
+        if (plev(S.LP, (int)(i & (size_t)(S.LP - 1))) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         rus[i] = ru[i];
         u2[i] = u[i];
     }
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void k_moist(DevState S) {
     const size_t n = (size_t)S.nCO * S.LP;
     double *qtot = fw(S, F_qtot), *cqw = fw(S, F_cqw);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        int k = plev(S.LP, (int)(i % S.LP));
+        int k = plev(S.LP, (int)(i & (size_t)(S.LP - 1)));
         if (k == S.L) continue;  // (padding levels k > L get zeros: full 64-B sectors)
         qtot[i] = 0.0;  // :473-482
         if (k > S.L) {
@@ -288,7 +288,7 @@ __global__ __launch_bounds__(256) void k_finish_edges(DevState S, int substep, i
     double *ru_save = fw(S, F_ru_save), *u = fw(S, F_u), *ruAvg = fw(S, F_ruAvg), *ruAvgS = fw(S, F_ruAvg_split);
     const double *ru = fd(S, F_ru), *u2 = fd(S, F_u_2);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
+        if (plev(S.LP, (int)(i & (size_t)(S.LP - 1))) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         if (substep < split) {
             ru_save[i] = ru[i];
             u[i] = u2[i];
@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
     const size_t n = (size_t)S.nCO * S.LP;
     double *wwAvg = fw(S, F_wwAvg), *wwAvgS = fw(S, F_wwAvg_split), *rho_zz = fw(S, F_rho_zz);
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        if (plev(S.LP, (int)(i % S.LP)) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
+        if (plev(S.LP, (int)(i & (size_t)(S.LP - 1))) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         if (substep < split) {
             fw(S, F_rw_save)[i] = fd(S, F_rw)[i];
             fw(S, F_rtheta_p_save)[i] = fd(S, F_rtheta_p)[i];
