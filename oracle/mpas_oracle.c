@@ -1141,6 +1141,162 @@ void ora_atm_srk3(ora_state* S, double dt, int schedule) {
     ora_atm_rk_dynamics_substep_finish(S, 1, dynamics_split);
 }
 
+/* ===================== the MPAS vertical solver ("physics" mpas)
+ * The reference's vertically implicit acoustic step with the statements it keeps as
+ * comments restored and its quirks in that solver fixed; every other task is unchanged.
+ *   vert_imp (dynamics_tasks.rg:513-592): Q16 b_tri takes cofwt(k-1) * rdzw(k-1); Q17
+ *     alpha_tri/gamma_tri are the LU recurrence of this call (gamma(0) = 0, k ascending).
+ *   acoustic (:1546-1723): Q18 the ru_p update and the ruAvg accumulation of :1581-1613;
+ *     Q19/Q20 rs, ts of every level first and the explicit rw_p part from the old
+ *     rho_pp/rtheta_pp of level k-1; Q21 the back substitution of :1674-1677; Q8 the
+ *     tendencies dyn_tend produces: tend_ru = tend_u, tend_rt = tend_theta (tend_rw is w,
+ *     where dyn_tend leaves it).  The MPAS-A statement order is kept throughout.
+ *   srk3: the acoustic loop runs number_sub_steps times (Q5).                          */
+void ora_mpas_vert_imp_coefs(ora_state* S, double dts) {
+    ora_atm_compute_vert_imp_coefs(S, dts); /* coefficients, a_tri, c_tri as the reference */
+    const int L = S->L, nC = S->nCells;
+    double *rdzw = D(rdzw), *cofrz = D(cofrz), *zz = D(zz), *cofwr = D(cofwr), *cofwz = D(cofwz);
+    double *coftz = D(coftz), *cofwt = D(cofwt), *a_tri = D(a_tri), *b_tri = D(b_tri), *c_tri = D(c_tri);
+    double *alpha_tri = D(alpha_tri), *gamma_tri = D(gamma_tri);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        for (int k = 1; k < L; k++) /* Q16 */
+            CW(b_tri, c, k) = 1.0 +
+                              CW(cofwz, c, k) * (CW(coftz, c, k) * rdzw[k] * CW(zz, c, k) +
+                                                 CW(coftz, c, k) * rdzw[k - 1] * CW(zz, c, k - 1)) -
+                              CW(coftz, c, k) * (CW(cofwt, c, k) * rdzw[k] - CW(cofwt, c, k - 1) * rdzw[k - 1]) +
+                              CW(cofwr, c, k) * ((cofrz[k] - cofrz[k - 1]));
+        CW(gamma_tri, c, 0) = 0.0;
+        for (int k = 1; k < L; k++) { /* Q17 */
+            CW(alpha_tri, c, k) = 1.0 / (CW(b_tri, c, k) - CW(a_tri, c, k) * CW(gamma_tri, c, k - 1));
+            CW(gamma_tri, c, k) = CW(c_tri, c, k) * CW(alpha_tri, c, k);
+        }
+    }
+}
+
+void ora_mpas_acoustic_step(ora_state* S, double dts, int small_step) {
+    const int L = S->L, nC = S->nCells, nE = S->nEdges;
+    const double epssm = config_epssm, rcv = rgas / (CP - rgas), c2 = CP * rcv;
+    const double resm = (1.0 - epssm) / (1.0 + epssm);
+    double *rtheta_pp_old = D(rtheta_pp_old), *rtheta_pp = D(rtheta_pp), *rho_pp = D(rho_pp);
+    double *wwAvg = D(wwAvg), *rw_p = D(rw_p), *ru_p = D(ru_p), *ruAvg = D(ruAvg);
+    double *cofrz = D(cofrz), *rdzw = D(rdzw), *fzm = D(fzm), *fzp = D(fzp);
+    double *zz = D(zz), *theta_m = D(theta_m), *coftz = D(coftz), *w = D(w);
+    /* :1581-1613 (Q18): horizontal momentum, every edge before any cell */
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        const int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        for (int k = 0; k < L; k++) {
+            if (small_step != 0) {
+                double pgrad = ((rc(S, rtheta_pp, cell2, k) - rc(S, rtheta_pp, cell1, k)) * re2(S, D(invDcEdge), e, 1, 0)) /
+                               (0.5 * (rc(S, zz, cell2, k) + rc(S, zz, cell1, k)));
+                pgrad = CW(D(cqu), e, k) * 0.5 * c2 * (rc(S, D(exner), cell1, k) + rc(S, D(exner), cell2, k)) * pgrad;
+                pgrad = pgrad + 0.5 * CW(D(zxu), e, k) * gravity * (rc(S, rho_pp, cell1, k) + rc(S, rho_pp, cell2, k));
+                CW(ru_p, e, k) = CW(ru_p, e, k) + dts * (CW(D(tend_u), e, k) - (1.0 - re2(S, D(specZoneMaskEdge), e, 1, 0)) * pgrad);
+                CW(ruAvg, e, k) = CW(ruAvg, e, k) + CW(ru_p, e, k);
+            } else {
+                CW(ru_p, e, k) = dts * CW(D(tend_u), e, k);
+                CW(ruAvg, e, k) = CW(ru_p, e, k);
+            }
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        const int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        double rs[128], ts[128], rtp0[128], rpp0[128], rwp0[129];
+        for (int k = 0; k < L; k++) CW(rtheta_pp_old, c, k) = (small_step == 0) ? 0 : CW(rtheta_pp, c, k);
+        if (small_step == 0) {
+            for (int k = 0; k <= L; k++) {
+                CW(wwAvg, c, k) = 0;
+                CW(rw_p, c, k) = 0;
+            }
+            for (int k = 0; k < L; k++) {
+                CW(rho_pp, c, k) = 0;
+                CW(rtheta_pp, c, k) = 0;
+            }
+        }
+        if (rc2(S, D(specZoneMaskCell), c, 1, 0) != 0.0) { /* specified zone */
+            for (int k = 0; k < L; k++) {
+                CW(rho_pp, c, k) = CW(rho_pp, c, k) + dts * CW(D(tend_rho), c, k);
+                CW(rtheta_pp, c, k) = CW(rtheta_pp, c, k) + dts * CW(D(tend_theta), c, k);
+                CW(rw_p, c, k) = CW(rw_p, c, k) + dts * CW(w, c, k);
+                CW(wwAvg, c, k) = CW(wwAvg, c, k) + 0.5 * (1.0 + epssm) * CW(rw_p, c, k);
+            }
+            continue;
+        }
+        for (int k = 0; k < L; k++) {
+            rtp0[k] = CW(rtheta_pp, c, k);
+            rpp0[k] = CW(rho_pp, c, k);
+            ts[k] = 0.0;
+            rs[k] = 0.0;
+        }
+        for (int k = 0; k <= L; k++) rwp0[k] = CW(rw_p, c, k);
+        for (int i = 0; i < ne; i++) {
+            int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+            int cell1 = ie2(S, I(cellsOnEdge), iEdge, 2, 0), cell2 = ie2(S, I(cellsOnEdge), iEdge, 2, 1);
+            for (int k = 0; k < L; k++) {
+                double flux = rc2(S, D(edgesOnCellSign), c, 10, i) * dts * re2(S, D(dvEdge), iEdge, 1, 0) *
+                              re(S, ru_p, iEdge, k) * rc2(S, D(invAreaCell), c, 1, 0);
+                rs[k] = rs[k] - flux;
+                ts[k] = ts[k] - flux * 0.5 * (rc(S, theta_m, cell2, k) + rc(S, theta_m, cell1, k));
+            }
+        }
+        for (int k = 0; k < L; k++) {
+            rs[k] = rpp0[k] + dts * CW(D(tend_rho), c, k) + rs[k] - cofrz[k] * resm * (rwp0[k + 1] - rwp0[k]);
+            ts[k] = rtp0[k] + dts * CW(D(tend_theta), c, k) + ts[k] -
+                    resm * rdzw[k] * (rc(S, coftz, c, k + 1) * rwp0[k + 1] - CW(coftz, c, k) * rwp0[k]);
+        }
+        for (int k = 1; k < L; k++) CW(wwAvg, c, k) = CW(wwAvg, c, k) + 0.5 * (1.0 - epssm) * rwp0[k];
+        for (int k = 1; k < L; k++)
+            CW(rw_p, c, k) = rwp0[k] + dts * CW(w, c, k) -
+                             CW(D(cofwz), c, k) * ((CW(zz, c, k) * ts[k] - CW(zz, c, k - 1) * ts[k - 1]) +
+                                                   resm * (CW(zz, c, k) * rtp0[k] - CW(zz, c, k - 1) * rtp0[k - 1])) -
+                             CW(D(cofwr), c, k) * ((rs[k] + rs[k - 1]) + resm * (rpp0[k] + rpp0[k - 1])) +
+                             CW(D(cofwt), c, k) * (ts[k] + resm * rtp0[k]) + CW(D(cofwt), c, k - 1) * (ts[k - 1] + resm * rtp0[k - 1]);
+        for (int k = 1; k < L; k++) /* tridiagonal solve: up ... */
+            CW(rw_p, c, k) = (CW(rw_p, c, k) - CW(D(a_tri), c, k) * CW(rw_p, c, k - 1)) * CW(D(alpha_tri), c, k);
+        for (int k = L - 1; k >= 0; k--) /* ... and down (Q21) */
+            CW(rw_p, c, k) = CW(rw_p, c, k) - CW(D(gamma_tri), c, k) * CW(rw_p, c, k + 1);
+        for (int k = 1; k < L; k++) { /* implicit Rayleigh damping of w */
+            const double d = CW(D(rw_save), c, k) - CW(D(rw), c, k);
+            CW(rw_p, c, k) = (CW(rw_p, c, k) + d -
+                              dts * CW(D(dss), c, k) * (fzm[k] * CW(zz, c, k) + fzp[k] * CW(zz, c, k - 1)) *
+                                  (fzm[k] * CW(D(rho_zz), c, k) + fzp[k] * CW(D(rho_zz), c, k - 1)) * CW(w, c, k)) /
+                                 (1.0 + dts * CW(D(dss), c, k)) -
+                             d;
+        }
+        for (int k = 1; k < L; k++) CW(wwAvg, c, k) = CW(wwAvg, c, k) + 0.5 * (1.0 + epssm) * CW(rw_p, c, k);
+        for (int k = 0; k < L; k++) {
+            CW(rho_pp, c, k) = rs[k] - cofrz[k] * (rc(S, rw_p, c, k + 1) - CW(rw_p, c, k));
+            CW(rtheta_pp, c, k) = ts[k] - rdzw[k] * (rc(S, coftz, c, k + 1) * rc(S, rw_p, c, k + 1) - CW(coftz, c, k) * CW(rw_p, c, k));
+        }
+    }
+}
+
+void ora_mpas_srk3(ora_state* S, double dt, int schedule) {
+    int number_of_sub_steps = 2;
+    double rk_sub_timestep[3] = {dt / 3, dt / number_of_sub_steps, dt / number_of_sub_steps};
+    int number_sub_steps[3];
+    number_sub_steps[0] = (number_of_sub_steps / 2 > 1) ? number_of_sub_steps / 2 : 1;
+    number_sub_steps[1] = number_sub_steps[0];
+    number_sub_steps[2] = number_of_sub_steps;
+    ora_atm_rk_integration_setup(S);
+    ora_atm_compute_moist_coefficients(S);
+    ora_mpas_vert_imp_coefs(S, rk_sub_timestep[0]);
+    for (int rk_step = 0; rk_step < 3; rk_step++) {
+        if (rk_step == 1) ora_mpas_vert_imp_coefs(S, rk_sub_timestep[rk_step]);
+        int dyn_rk = schedule == 0 ? (int)rk_sub_timestep[rk_step] : rk_step;
+        ora_atm_compute_dyn_tend_work(S, dyn_rk, dt, 0, 0.0, 0, 0);
+        ora_atm_set_smlstep_pert_variables_work(S);
+        for (int small_step = 0; small_step < number_sub_steps[rk_step]; small_step++) { /* Q5 */
+            ora_mpas_acoustic_step(S, rk_sub_timestep[rk_step], small_step);
+            ora_atm_divergence_damping_3d(S, rk_sub_timestep[rk_step]);
+        }
+        ora_atm_compute_solve_diagnostics(S, 0, rk_step);
+    }
+    ora_atm_rk_dynamics_substep_finish(S, 1, 1);
+}
+
 /* ===================== synthetic state (test/bench inputs, not reference semantics) */
 static const struct { int kind, width, dist; double lo, hi; } ora_fields[] = {
 #define C3 0

@@ -54,6 +54,9 @@ def load():
             "ora_atm_recover_large_step_variables_work": (None, [p, i32, i32, dbl]),
             "ora_mpas_reconstruct_2d": (None, [p, i32, i32]),
             "ora_atm_compute_output_diagnostics": (None, [p]),
+            "ora_mpas_vert_imp_coefs": (None, [p, dbl]),
+            "ora_mpas_acoustic_step": (None, [p, dbl, i32]),
+            "ora_mpas_srk3": (None, [p, dbl, i32]),
             "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
         }
         for n, (res, args) in sig.items():
@@ -118,6 +121,16 @@ class Oracle:
 
     def atm_recover_large_step_variables_work(self, ns, rk_step, dt):
         self.lib.ora_atm_recover_large_step_variables_work(self.p, ns, rk_step, dt)
+
+    # the MPAS vertical solver ("physics" mpas; mpas_oracle.c)
+    def mpas_vert_imp_coefs(self, dts):
+        self.lib.ora_mpas_vert_imp_coefs(self.p, dts)
+
+    def mpas_acoustic_step(self, dts, small_step):
+        self.lib.ora_mpas_acoustic_step(self.p, dts, small_step)
+
+    def mpas_srk3(self, dt, schedule=1):
+        self.lib.ora_mpas_srk3(self.p, dt, schedule)
 
     def atm_compute_output_diagnostics(self):
         self.lib.ora_atm_compute_output_diagnostics(self.p)
