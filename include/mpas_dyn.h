@@ -57,7 +57,12 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * or 4 entities per column slot in div_damping / solve_diagnostics; "vcmix" = 1 (default)
  * interleaves the vertex and cell blocks of the mixed grids; "overlap" = 1 (default)
  * computes interior entities beside the halo exchange of a decomposed mesh; "self" = 0
- * disables the SELF gathers.  All but "exact" change only speed, never results. */
+ * disables the SELF gathers.  All but "exact" and "physics" change only speed, never results.
+ * "physics" = 1 selects the MPAS vertical solver: vert_imp with Q16/Q17
+ * fixed, the acoustic step with the ru_p update (Q18), the MPAS statement order (Q19/Q20)
+ * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), and the acoustic
+ * loop of mpas_atm_srk3 run number_sub_steps times (Q5); every other task as the reference.
+ * Default 0: the reference's semantics. */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
 /* reads every option above ("self", default 1: when every cell is
  * among the cellsOnEdge of its own edges -- mpas-mode ids -- the cell kernels gather

@@ -20,8 +20,16 @@
 namespace mpas {
 
 // FIRST: small_step == 0, where rho_pp, rtheta_pp, rw_p and wwAvg start from 0 (:1615-1636):
-// their columns are not read at all (4 of the 19 own columns)
-template <int LP, bool EXACT, bool SELF, bool FIRST>
+// their columns are not read at all (4 of the 19 own columns).
+// MPASV: the MPAS vertical solver (option "physics" = 1, oracle ora_mpas_acoustic_step):
+// rs/ts of every level, the explicit rw_p part from ts(k-1), rs(k-1) and the old
+// rho_pp/rtheta_pp of level k-1 (Q19, Q20), the tridiagonal solve up (forward sweep) and
+// down (the back substitution the reference leaves commented out, Q21), the Rayleigh
+// term, then rho_pp/rtheta_pp; tend_rt = tend_theta (Q8).  Both sweeps are first-order
+// linear recurrences: an affine prefix scan over the wavefront, upward then downward
+// (EXACT: level by level in the reference's order).  The ru_p update (Q18) runs before,
+// in k_acoustic_ru.
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -74,6 +82,9 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     col_rd2<LP>(fd(S, F_cofwr), fd(S, F_a_tri), c, k, L, cofwr, a_tri);
     col_rd2<LP>(fd(S, F_alpha_tri), fd(S, F_rw_save), c, k, L, alpha, rws);
     col_rd2<LP>(fd(S, F_rw), fd(S, F_dss), c, k, L, rw, dss);
+    double gam = 0.0, tend_th = 0.0;
+    if constexpr (MPASV) col_rd2<LP>(fd(S, F_gamma_tri), fd(S, F_tend_theta), c, k, L, gam, tend_th);
+    const double tt = MPASV ? tend_th : tm;  // tend_rt: the reference reads theta_m (Q8)
     const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
 
@@ -91,7 +102,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     if (spec != 0.0) {  // :1698-1703 (column-uniform branch)
         if (kl) {
             rpp = rpp + dts * tend_rho;
-            rtp = rtp + dts * tm;
+            rtp = rtp + dts * tt;
             rwp = rwp + dts * w;
             ww = ww + 0.5 * (1.0 + epssm) * rwp;
         }
@@ -120,7 +131,72 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     // ---- rs, ts (:1657-1658) from the OLD rw_p
     const double rwp_p = lvl_up<LP>(rwp, k), coftz_p = lvl_up<LP>(coftz, k);
     rs = rpp + dts * tend_rho + rs - cofrz * resm * (rwp_p - rwp);
-    ts = rtp + dts * tm + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
+    ts = rtp + dts * tt + ts - resm * rdzw * (coftz_p * rwp_p - coftz * rwp);
+
+    if constexpr (MPASV) {  // the MPAS-A order (mpas_oracle.c ora_mpas_acoustic_step)
+        const double ts_m = lvl_dn<LP>(ts, k), rs_m = lvl_dn<LP>(rs, k);
+        const double rtp_m = lvl_dn<LP>(rtp, k), rpp_m = lvl_dn<LP>(rpp, k);
+        const double zz_m = lvl_dn<LP>(zz, k), rz_m = lvl_dn<LP>(rz, k), cofwt_m = lvl_dn<LP>(cofwt, k);
+        const bool in = k >= 1 && k < L;  // the interior interfaces
+        const double rwold = rwp;
+        if (in) ww = ww + 0.5 * (1.0 - epssm) * rwold;
+        double x = rwold;
+        if (in)
+            x = rwold + dts * w - cofwz * ((zz * ts - zz_m * ts_m) + resm * (zz * rtp - zz_m * rtp_m)) -
+                cofwr * ((rs + rs_m) + resm * (rpp + rpp_m)) + cofwt * (ts + resm * rtp) + cofwt_m * (ts_m + resm * rtp_m);
+        // up: y(k) = (x(k) - a(k) y(k-1)) alpha(k), 1 <= k < L; y(0) = rw_p(0)
+        double y = x;
+        if constexpr (EXACT) {
+            for (int kk = 1; kk < L; kk++) {
+                const double yp = __shfl(y, kk - 1, LP);
+                y = (k == kk) ? (x - a_tri * yp) * alpha : y;
+            }
+        } else {
+            double G = in ? -a_tri * alpha : 0.0, H = in ? x * alpha : x;
+#pragma unroll
+            for (int off = 1; off < LP; off <<= 1) {
+                const double Gp = __shfl_up(G, off, LP), Hp = __shfl_up(H, off, LP);
+                if (k >= off) {
+                    H = G * Hp + H;
+                    G = G * Gp;
+                }
+            }
+            y = H;
+        }
+        // down: z(k) = y(k) - gamma(k) z(k+1), k = L-1 .. 0; z(L) = rw_p(L)
+        double z = y;
+        if constexpr (EXACT) {
+            for (int kk = L - 1; kk >= 0; kk--) {
+                const double zn = __shfl(z, kk + 1, LP);
+                z = (k == kk) ? y - gam * zn : z;
+            }
+        } else {
+            double G = k < L ? -gam : 0.0, H = k <= L ? y : 0.0;
+#pragma unroll
+            for (int off = 1; off < LP; off <<= 1) {
+                const double Gp = __shfl_down(G, off, LP), Hp = __shfl_down(H, off, LP);
+                if (k + off < LP) {
+                    H = G * Hp + H;
+                    G = G * Gp;
+                }
+            }
+            z = H;
+        }
+        double r = (k == L) ? rwold : z;
+        if (in) {  // implicit Rayleigh damping of w
+            const double d = rws - rw;
+            r = (z + d - dts * dss * (fzm * zz + fzp * zz_m) * (fzm * rz + fzp * rz_m) * w) / (1.0 + dts * dss) - d;
+            ww = ww + 0.5 * (1.0 + epssm) * r;
+        }
+        const double r_p = lvl_up<LP>(r, k);
+        if (k != L) {
+            colk(rpp_f, c) = PADW(rs - cofrz * (r_p - r));
+            colk(rtp_f, c) = PADW(ts - rdzw * (coftz_p * r_p - coftz * r));
+        }
+        colk(rwp_f, c) = PADW(r);
+        colk(ww_f, c) = PADW(ww);
+        return;
+    }
 
     // per-level coefficients of the recurrence
     const double zz_m = lvl_dn<LP>(zz, k), rz_m = lvl_dn<LP>(rz, k), cofwt_m = lvl_dn<LP>(cofwt, k);
@@ -197,22 +273,66 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     colk(ww_f, c) = PADW(ww);
 }
 
+// :1581-1613 restored (Q18, MPAS vertical solver only): ru_p and ruAvg of every owned
+// edge, before the cell kernel reads ru_p
+template <int LP>
+__global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int small_step, double c2) {
+    ColMap<LP> m(S, KE);
+    const int L = S.L, k = m.k, e = m.ent;
+    if (e >= S.nEO) return;
+    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    double rp, ra, tu, cqu, zxu;
+    gather2<LP>(fd(S, F_ru_p), e, fd(S, F_ruAvg), e, k, rp, ra);
+    gather2<LP>(fd(S, F_tend_u), e, fd(S, F_cqu), e, k, tu, cqu);
+    zxu = colk(fd(S, F_zxu), e);
+    if (small_step != 0) {  // (uniform)
+        double t1, t2, z1, z2, x1, x2, r1, r2;
+        gather2s<LP>(fd(S, F_rtheta_pp), cell1, cell2, k, t1, t2);
+        gather2s<LP>(fd(S, F_zz), cell1, cell2, k, z1, z2);
+        gather2s<LP>(fd(S, F_exner), cell1, cell2, k, x1, x2);
+        gather2s<LP>(fd(S, F_rho_pp), cell1, cell2, k, r1, r2);
+        const double invDc = fd(S, F_invDcEdge)[e], spec = fd(S, F_specZoneMaskEdge)[e];
+        double pgrad = ((t2 - t1) * invDc) / (0.5 * (z2 + z1));
+        pgrad = cqu * 0.5 * c2 * (x1 + x2) * pgrad;
+        pgrad = pgrad + 0.5 * zxu * kGravity * (r1 + r2);
+        rp = rp + dts * (tu - (1.0 - spec) * pgrad);
+        ra = ra + rp;
+    } else {
+        rp = dts * tu;
+        ra = rp;
+    }
+    if (k == L) return;  // (padding levels: zeros, PADW)
+    colk(fw(S, F_ru_p), e) = PADW(rp);
+    colk(fw(S, F_ruAvg), e) = PADW(ra);
+}
+
 template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
+    if (S.physics) {  // Q18: the edges first
+        const double rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
+        auto ru = [&](const DevState& X) {
+            const int nb = col_blocks<LP>(X, KE);
+            if (nb) k_acoustic_ru<LP><<<nb, 256, 0, st>>>(X, dts, small_step, c2);
+        };
+        HALO_RUN(S, st, ru, F_rtheta_pp, F_zz, F_exner, F_rho_pp);
+        HALO_WROTE(S, F_ru_p, F_ruAvg);
+    }
     auto run = [&](const DevState& X) {
         const int grid = col_blocks<LP>(X, KC);
         if (!grid) return;
-#define MPAS_ACOUSTIC(E, SF, F) k_acoustic<LP, E, SF, F><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm)
+#define MPAS_ACOUSTIC(E, SF, F, M) k_acoustic<LP, E, SF, F, M><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm)
+#define MPAS_ACOUSTIC_M(E, SF, F) (X.physics ? MPAS_ACOUSTIC(E, SF, F, true) : MPAS_ACOUSTIC(E, SF, F, false))
         const bool first = small_step == 0;
         if (exact) {
-            if (X.selfc) first ? MPAS_ACOUSTIC(true, true, true) : MPAS_ACOUSTIC(true, true, false);
-            else first ? MPAS_ACOUSTIC(true, false, true) : MPAS_ACOUSTIC(true, false, false);
+            if (X.selfc) first ? MPAS_ACOUSTIC_M(true, true, true) : MPAS_ACOUSTIC_M(true, true, false);
+            else first ? MPAS_ACOUSTIC_M(true, false, true) : MPAS_ACOUSTIC_M(true, false, false);
         } else {
-            if (X.selfc) first ? MPAS_ACOUSTIC(false, true, true) : MPAS_ACOUSTIC(false, true, false);
-            else first ? MPAS_ACOUSTIC(false, false, true) : MPAS_ACOUSTIC(false, false, false);
+            if (X.selfc) first ? MPAS_ACOUSTIC_M(false, true, true) : MPAS_ACOUSTIC_M(false, true, false);
+            else first ? MPAS_ACOUSTIC_M(false, false, true) : MPAS_ACOUSTIC_M(false, false, false);
         }
+#undef MPAS_ACOUSTIC_M
 #undef MPAS_ACOUSTIC
     };
     HALO_RUN(S, st, run, F_ru_p, F_theta_m);

@@ -80,7 +80,11 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------- vert_imp
-template <int LP>
+// MPASV: the MPAS vertical solver (option "physics" = 1, oracle ora_mpas_vert_imp_coefs):
+// b_tri with cofwt(k-1) (Q16) and the LU recurrence alpha(k) = 1 / (b(k) - a(k) gamma(k-1)),
+// gamma(k) = c(k) alpha(k) from gamma(0) = 0 within the call (Q17), level by level
+// (a nonlinear recurrence: lane k waits for lane k-1's gamma, broadcast by a shuffle)
+template <int LP, bool MPASV>
 __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -115,6 +119,28 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
     const double gamma_m = (k == 1) ? 0.0 : gamma_dn;  // Q17: gamma(0) was just zeroed
     const double cofrz = dtseps * rdzw, cofrz_m = dtseps * rdzw_m;      // :537-539
 
+    // :566-578 (every lane; used at 0 < k < L)
+    const double a = -1.0 * cofwz * coftz_m * rdzw_m * zz_m + cofwr * cofrz_m - cofwt_m * coftz_m * rdzw_m;
+    const double b = MPASV ? 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) -
+                                 coftz * (cofwt * rdzw - cofwt_m * rdzw_m) + cofwr * ((cofrz - cofrz_m))
+                           : 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) -
+                                 coftz * (cofwt * rdzw - cofwt * rdzw_m) + cofwr * ((cofrz - cofrz_m));  // Q16 literal
+    const double cc = -1.0 * cofwz * coftz_p * rdzw * zz - cofwr * cofrz + cofwt * coftz_p * rdzw;
+    double alpha, gamma;
+    if constexpr (MPASV) {
+        double gp = 0.0;
+        alpha = gamma = 0.0;
+        for (int kk = 1; kk < L; kk++) {
+            const double al = 1.0 / (b - a * gp);
+            alpha = (k == kk) ? al : alpha;
+            gamma = (k == kk) ? cc * al : gamma;
+            gp = __shfl(gamma, kk, LP);
+        }
+    } else {
+        alpha = 1.0 / (b - a * gamma_m);  // :580-585
+        gamma = cc * alpha;               // :587-591
+    }
+
     const bool pad = k > L;  // padding levels: zeros (full 64-B sectors; see PADW)
     if (k < L || pad) {
         double* o;
@@ -125,13 +151,6 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
         } else {
             colk(fw(S, F_cofwr), c) = PADW(cofwr);
             colk(fw(S, F_cofwz), c) = PADW(cofwz);
-            // :566-578 (Q16 literal)
-            double a = -1.0 * cofwz * coftz_m * rdzw_m * zz_m + cofwr * cofrz_m - cofwt_m * coftz_m * rdzw_m;
-            double b = 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) - coftz * (cofwt * rdzw - cofwt * rdzw_m) +
-                       cofwr * ((cofrz - cofrz_m));
-            double cc = -1.0 * cofwz * coftz_p * rdzw * zz - cofwr * cofrz + cofwt * coftz_p * rdzw;
-            double alpha = 1.0 / (b - a * gamma_m);  // :580-585
-            double gamma = cc * alpha;               // :587-591
             o = fw(S, F_a_tri); colk(o, c) = PADW(a);
             o = fw(S, F_b_tri); colk(o, c) = PADW(b);
             o = fw(S, F_c_tri); colk(o, c) = PADW(cc);
@@ -147,7 +166,8 @@ static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
     double rcv = kRgas / (kCp - kRgas);
     double c2 = kCp * rcv;
     const int grid = col_blocks<LP>(S, KC);
-    if (grid) k_vert_imp<LP><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
+    if (grid && S.physics) k_vert_imp<LP, true><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
+    else if (grid) k_vert_imp<LP, false><<<grid, 256, 0, st>>>(S, dtseps, rcv, c2);
     HALO_WROTE(S, F_coftz, F_cofwt, F_gamma_tri, F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri);
     return hipGetLastError();
 }

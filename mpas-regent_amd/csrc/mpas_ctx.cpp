@@ -238,7 +238,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]",
                  [&] { return launch_dyn_tend(S, st, a); });
         run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
-        for (int small_step = 0; small_step < number_sub_steps[rk_step] + 1; small_step++) {  // Q5
+        const int n_small = number_sub_steps[rk_step] + (S.physics ? 0 : 1);  // Q5 (the MPAS form: n)
+        for (int small_step = 0; small_step < n_small; small_step++) {
             run_task(c, "atm_advance_acoustic_step_work",
                      [&] { return launch_acoustic(S, st, rk_sub_timestep[rk_step], small_step, c->exact); });
             run_task(c, "atm_divergence_damping_3d",
@@ -301,6 +302,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.LP = LP;
         c->S.epw = 2;  // tools/kbench.py: div_damp -3 %, solve_diagnostics -4 % vs 1
         c->S.vcmix = 1;
+        c->S.physics = 0;
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         for (int f = 0; f < X_COUNT; f++) {
@@ -369,6 +371,9 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             c->S.epw = (int)value;
         } else if (name && std::strcmp(name, "vcmix") == 0) {
             c->S.vcmix = value ? 1 : 0;
+        } else if (name && std::strcmp(name, "physics") == 0) {
+            if (value != 0 && value != 1) throw Fail{MPAS_EINVAL, "physics must be 0 (reference) or 1 (MPAS vertical solver)"};
+            c->S.physics = (int)value;
         } else if (name && std::strcmp(name, "overlap") == 0) {
             c->overlap = value ? 1 : 0;
             if (c->halo) c->halo->overlap = c->overlap;
@@ -386,6 +391,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "xcd") == 0) *value = c->S.xcd;
         else if (name && std::strcmp(name, "epw") == 0) *value = c->S.epw;
         else if (name && std::strcmp(name, "vcmix") == 0) *value = c->S.vcmix;
+        else if (name && std::strcmp(name, "physics") == 0) *value = c->S.physics;
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "selfc") == 0) {

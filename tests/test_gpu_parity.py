@@ -283,3 +283,58 @@ def test_nonfinite_inputs_propagate(x1_2562):
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
     assert np.isnan(ref["tend_theta"]).any()
+
+
+# ---------------------------------------------------------------- the MPAS vertical solver
+def run_gpu_mpas(st, fn, exact):
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.set_option("exact", exact)
+        ctx.set_option("physics", 1)
+        ctx.upload(st)
+        fn(ctx)
+        ctx.sync()
+        ctx.download(got)
+    return got
+
+
+def mpas_solver_state(mesh, L, variant):
+    st = base_state(mesh, L, variant).copy()
+    O.Oracle(st).mpas_vert_imp_coefs(240.0)  # a factored system for the acoustic step
+    return st
+
+
+@pytest.mark.parametrize("L", [5, 56, 63])
+@pytest.mark.parametrize("variant", ["random", "mpas0"])
+def test_mpas_vert_imp(x1_2562, L, variant):
+    """option physics = 1: b_tri with cofwt(k-1) and the LU recurrence of the call"""
+    st = base_state(x1_2562, L, variant)
+    ref = run_oracle(st, lambda o: o.mpas_vert_imp_coefs(240.0))
+    for exact in (1, 0):
+        got = run_gpu_mpas(st, lambda c: T.atm_compute_vert_imp_coefs(c, 240.0), exact)
+        bad = compare_states(got, ref, rtol=0.0)
+        assert not bad, f"exact={exact}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("L", [5, 56, 63])
+@pytest.mark.parametrize("variant", ["random", "mpas0"])
+@pytest.mark.parametrize("small_step", [0, 1])
+def test_mpas_acoustic(x1_2562, L, variant, small_step):
+    """option physics = 1: ru_p update, MPAS order, up and down sweeps of the tridiagonal
+    solve (exact: level by level, bit-identical; fast: two affine scans, 1e-11)"""
+    st = mpas_solver_state(x1_2562, L, variant)
+    ref = run_oracle(st, lambda o: o.mpas_acoustic_step(240.0, small_step))
+    for exact, tol in ((1, 0.0), (0, RTOL_FAST)):
+        got = run_gpu_mpas(st, lambda c: T.atm_advance_acoustic_step_work(c, 240.0, small_step), exact)
+        bad = compare_states(got, ref, rtol=tol)
+        assert not bad, f"exact={exact}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("L", [5, 56])
+def test_mpas_srk3(x1_2562, L):
+    st = base_state(x1_2562, L, "mpas0")
+    ref = run_oracle(st, lambda o: o.mpas_srk3(720.0, 1))
+    for exact, tol in ((1, 0.0), (0, RTOL_STEP)):
+        got = run_gpu_mpas(st, lambda c: T.atm_srk3(c, 720.0, 1), exact)
+        bad = compare_states(got, ref, rtol=tol)
+        assert not bad, f"exact={exact}: {bad[:6]}"
