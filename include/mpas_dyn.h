@@ -60,8 +60,9 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * disables the SELF gathers.  All but "exact" and "physics" change only speed, never results.
  * "physics" = 1 selects the MPAS vertical solver: vert_imp with Q16/Q17
  * fixed, the acoustic step with the ru_p update (Q18), the MPAS statement order (Q19/Q20)
- * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), and the acoustic
- * loop of mpas_atm_srk3 run number_sub_steps times (Q5); every other task as the reference.
+ * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), recover_large_step
+ * with Q24 fixed, and in mpas_atm_srk3 number_sub_steps acoustic substeps (Q5) followed by
+ * recover (Q7); every other task as the reference.
  * Default 0: the reference's semantics. */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
 /* reads every option above ("self", default 1: when every cell is

@@ -19,8 +19,10 @@ struct RecK {
 };
 
 // :1788-1820 (the loop over cells and levels 0..nVertLevels-1), and the "garbage cell"
-// rho_zz = 1.0 of :1790-1792 (our zero slot)
-template <int LP>
+// rho_zz = 1.0 of :1790-1792 (our zero slot).  MPASV (option physics = 1, oracle
+// ora_mpas_recover): w(0) = 0, w(L) = 0, rw/wwAvg/w of the interior interfaces only,
+// exner = (zz rgas/p0 (rtheta_p + rtheta_base))^rcv
+template <int LP, bool MPASV>
 __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -35,6 +37,7 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     const double rtb = colk(fd(S, F_rtheta_base), c);
     const double rtd = a.rk_step == 2 ? colk(fd(S, F_rt_diabatic_tend), c) : 0.0;
     const double exb = a.rk_step == 2 ? colk(fd(S, F_exner_base), c) : 0.0;
+    if (MPASV && k == L) colk(fw(S, F_w), c) = 0.0;
     if (!kl) return;
     const double rho_p = rps + rpp;
     const double rho_zz = rho_p + rb;
@@ -45,14 +48,17 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     const double w = rw / (fzm * zz + fzp * zz_m);  // (:1805 sets w = 0.0 first)
     colk(fw(S, F_rho_p), c) = rho_p;
     colk(fw(S, F_rho_zz), c) = rho_zz;
-    colk(fw(S, F_wwAvg), c) = wwAvg;
-    colk(fw(S, F_rw), c) = rw;
-    colk(fw(S, F_w), c) = w;
+    if (!MPASV || k > 0) {
+        colk(fw(S, F_wwAvg), c) = wwAvg;
+        colk(fw(S, F_rw), c) = rw;
+    }
+    colk(fw(S, F_w), c) = (MPASV && k == 0) ? 0.0 : w;
     if (a.rk_step == 2) {
         const double rtheta_p = rtps + rtpp - a.dt * rho_zz * rtd;
         colk(fw(S, F_rtheta_p), c) = rtheta_p;
         colk(fw(S, F_theta_m), c) = (rtheta_p + rtb) / rho_zz;
-        const double exner = zz * a.rgas_p0 * pow((rtheta_p + rtb), a.rcv);  // Q24 literal
+        const double exner = MPASV ? pow(zz * a.rgas_p0 * (rtheta_p + rtb), a.rcv)
+                                   : zz * a.rgas_p0 * pow((rtheta_p + rtb), a.rcv);  // Q24 literal
         colk(fw(S, F_exner), c) = exner;
         colk(fw(S, F_pressure_p), c) = zz * a.rgas * (exner * rtheta_p + rtb * (exner - exb));
     } else {
@@ -62,8 +68,8 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     }
 }
 
-// :1830-1837: ruAvg, ru (Q24: ru_save * ru_p), u from the new rho_zz
-template <int LP>
+// :1830-1837: ruAvg, ru (Q24: ru_save * ru_p; MPASV: ru_save + ru_p), u from the new rho_zz
+template <int LP, bool MPASV>
 __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
@@ -75,7 +81,7 @@ __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
     double ruAvg = ra;
     ruAvg *= a.invNs;
     ruAvg += rus;
-    const double ru = rus * rup;
+    const double ru = MPASV ? rus + rup : rus * rup;
     colk(fw(S, F_ruAvg), e) = ruAvg;
     colk(fw(S, F_ru), e) = ru;
     colk(fw(S, F_u), e) = 2 * ru / (rz1 + rz2);
@@ -84,7 +90,8 @@ __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
 // :1839-1870: the w recovery from (rho*omega)_p over the cell's edges, then the division.
 // The level-0 term (cf1..cf3 flux) is added to w(cell, 0) at every one of the nVertLevels
 // level iterations of the cell; lane 0 replays that sequence in the reference's order.
-template <int LP>
+// MPASV: the level-0 term once per edge, flux2 = fzm ru(k) + fzp ru(k-1) (Q24).
+template <int LP, bool MPASV>
 __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -110,10 +117,13 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
         zb30_[i] = __shfl(z3, 0, LP);
         const double flux = (cf1 * r0 + cf2 * r1 + cf3 * r2);
         a_[i] = sg_[i] * (zb0_[i] + copysign(1.0, flux) * zb30_[i]) * flux;
-        const double flux2 = fzm * r * (fzp * r_m);  // Q24 literal
+        const double flux2 = MPASV ? fzm * r + fzp * r_m : fzm * r * (fzp * r_m);  // (ref: Q24 literal)
         b_[i] = sg_[i] * (z + copysign(1.0, flux2) * z3) * flux2;
     }
-    if (k == 0) {
+    if (k == 0 && MPASV) {
+        for (int i = 0; i < ne; i++) w = w + a_[i];
+        w = w / (cf1 * rz + cf2 * rz1 + cf3 * rz2);
+    } else if (k == 0) {
         for (int i = 0; i < ne; i++) {  // level iteration 0
             w += a_[i];
             w += b_[i];
@@ -138,17 +148,20 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
     a.rcv = kRgas / (kCp - kRgas);
     a.rk_step = rk_step;
     const int nCB = col_blocks<LP>(S, KC);
-    if (nCB) k_recover_cells<LP><<<nCB, 256, 0, st>>>(S, a);
+    if (nCB && S.physics) k_recover_cells<LP, true><<<nCB, 256, 0, st>>>(S, a);
+    else if (nCB) k_recover_cells<LP, false><<<nCB, 256, 0, st>>>(S, a);
     HALO_WROTE(S, F_rho_p, F_rho_zz, F_wwAvg, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
     auto ke = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
-        if (nb) k_recover_edges<LP><<<nb, 256, 0, st>>>(X, a);
+        if (nb && X.physics) k_recover_edges<LP, true><<<nb, 256, 0, st>>>(X, a);
+        else if (nb) k_recover_edges<LP, false><<<nb, 256, 0, st>>>(X, a);
     };
     HALO_RUN(S, st, ke, F_rho_zz);
     HALO_WROTE(S, F_ruAvg, F_ru, F_u);
     auto kw = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
-        if (nb) k_recover_w<LP><<<nb, 256, 0, st>>>(X);
+        if (nb && X.physics) k_recover_w<LP, true><<<nb, 256, 0, st>>>(X);
+        else if (nb) k_recover_w<LP, false><<<nb, 256, 0, st>>>(X);
     };
     HALO_RUN(S, st, kw, F_ru);
     HALO_WROTE(S, F_w);

@@ -245,6 +245,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             run_task(c, "atm_divergence_damping_3d",
                      [&] { return launch_div_damping(S, st, rk_sub_timestep[rk_step], small_step == 0); });
         }
+        if (S.physics)  // rk_timestep.rg:460, commented out in the reference (Q7)
+            run_task(c, "atm_recover_large_step_variables_work",
+                     [&] { return launch_recover_large_step(S, st, number_sub_steps[rk_step], rk_step, dt); });
         run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
     }
     run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });

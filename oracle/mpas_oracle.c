@@ -1151,7 +1151,9 @@ void ora_atm_srk3(ora_state* S, double dt, int schedule) {
  *     rho_pp/rtheta_pp of level k-1; Q21 the back substitution of :1674-1677; Q8 the
  *     tendencies dyn_tend produces: tend_ru = tend_u, tend_rt = tend_theta (tend_rw is w,
  *     where dyn_tend leaves it).  The MPAS-A statement order is kept throughout.
- *   srk3: the acoustic loop runs number_sub_steps times (Q5).                          */
+ *   recover (:1766-1872): Q24 fixed, w of the interior interfaces (ora_mpas_recover).
+ *   srk3: the acoustic loop runs number_sub_steps times (Q5) and recover runs after it
+ *     (the call rk_timestep.rg:460 keeps commented, Q7).                               */
 void ora_mpas_vert_imp_coefs(ora_state* S, double dts) {
     ora_atm_compute_vert_imp_coefs(S, dts); /* coefficients, a_tri, c_tri as the reference */
     const int L = S->L, nC = S->nCells;
@@ -1273,6 +1275,74 @@ void ora_mpas_acoustic_step(ora_state* S, double dts, int small_step) {
     }
 }
 
+/* atm_recover_large_step_variables_work (:1766-1872) in the MPAS form: ru = ru_save + ru_p
+ * and flux2 = fzm ru(k) + fzp ru(k-1) (Q24), exner = (zz rgas/p0 (rtheta_p + rtheta_base))^rcv,
+ * w(0) = 0 and w(L) = 0 with rw, wwAvg, w of the interior interfaces only, the lower
+ * boundary flux added to w(0) once per edge.                                         */
+void ora_mpas_recover(ora_state* S, int ns, int rk_step, double dt) {
+    const int L = S->L, nC = S->nCells, nE = S->nEdges;
+    const double rcv = rgas / (CP - rgas), p0 = 1.0e5;
+    double *rho_zz = D(rho_zz), *w = D(w), *ru = D(ru);
+    for (int k = 0; k < L; k++) CW(rho_zz, nC, k) = 1.0;
+    const double invNs = 1 / (double)ns;
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        for (int k = 0; k < L; k++) {
+            CW(D(rho_p), c, k) = CW(D(rho_p_save), c, k) + CW(D(rho_pp), c, k);
+            CW(rho_zz, c, k) = CW(D(rho_p), c, k) + CW(D(rho_base), c, k);
+        }
+        CW(w, c, 0) = 0.0;
+        for (int k = 1; k < L; k++) {
+            CW(D(wwAvg), c, k) = CW(D(rw_save), c, k) + (CW(D(wwAvg), c, k) * invNs);
+            CW(D(rw), c, k) = CW(D(rw_save), c, k) + CW(D(rw_p), c, k);
+            CW(w, c, k) = CW(D(rw), c, k) / (rz(S, D(fzm), k) * CW(D(zz), c, k) + rz(S, D(fzp), k) * CW(D(zz), c, k - 1));
+        }
+        CW(w, c, L) = 0.0;
+        for (int k = 0; k < L; k++) {
+            if (rk_step == 2) {
+                CW(D(rtheta_p), c, k) = CW(D(rtheta_p_save), c, k) + CW(D(rtheta_pp), c, k) -
+                                        dt * CW(rho_zz, c, k) * CW(D(rt_diabatic_tend), c, k);
+                CW(D(theta_m), c, k) = (CW(D(rtheta_p), c, k) + CW(D(rtheta_base), c, k)) / CW(rho_zz, c, k);
+                CW(D(exner), c, k) = pow(CW(D(zz), c, k) * (rgas / p0) * (CW(D(rtheta_p), c, k) + CW(D(rtheta_base), c, k)), rcv);
+                CW(D(pressure_p), c, k) = CW(D(zz), c, k) * rgas *
+                                          (CW(D(exner), c, k) * CW(D(rtheta_p), c, k) +
+                                           CW(D(rtheta_base), c, k) * (CW(D(exner), c, k) - CW(D(exner_base), c, k)));
+            } else {
+                CW(D(rtheta_p), c, k) = CW(D(rtheta_p_save), c, k) + CW(D(rtheta_pp), c, k);
+                CW(D(theta_m), c, k) = (CW(D(rtheta_p), c, k) + CW(D(rtheta_base), c, k)) / CW(rho_zz, c, k);
+            }
+        }
+    }
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        for (int k = 0; k < L; k++) {
+            CW(D(ruAvg), e, k) = CW(D(ru_save), e, k) + (CW(D(ruAvg), e, k) * invNs);
+            CW(ru, e, k) = CW(D(ru_save), e, k) + CW(D(ru_p), e, k);
+            CW(D(u), e, k) = 2. * CW(ru, e, k) / (rc(S, rho_zz, cell1, k) + rc(S, rho_zz, cell2, k));
+        }
+    }
+    const double cf1 = rz(S, D(cf1), 0), cf2 = rz(S, D(cf2), 0), cf3 = rz(S, D(cf3), 0);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        if (ic2(S, I(bdyMaskCell), c, 1, 0) > nRelaxZone) continue;
+        const int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int i = 0; i < ne; i++) {
+            int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+            double sg = rc2(S, D(edgesOnCell_sign), c, 10, i);
+            double flux = (cf1 * re(S, ru, iEdge, 0) + cf2 * re(S, ru, iEdge, 1) + cf3 * re(S, ru, iEdge, 2));
+            CW(w, c, 0) = CW(w, c, 0) + sg * (rc3v(S, D(zb_cell), c, 0, i) + copysign(1.0, flux) * rc3v(S, D(zb3_cell), c, 0, i)) * flux;
+            for (int k = 1; k < L; k++) {
+                flux = (rz(S, D(fzm), k) * re(S, ru, iEdge, k) + rz(S, D(fzp), k) * re(S, ru, iEdge, k - 1));
+                CW(w, c, k) = CW(w, c, k) + sg * (rc3v(S, D(zb_cell), c, k, i) + copysign(1.0, flux) * rc3v(S, D(zb3_cell), c, k, i)) * flux;
+            }
+        }
+        CW(w, c, 0) = CW(w, c, 0) / (cf1 * CW(rho_zz, c, 0) + cf2 * rc(S, rho_zz, c, 1) + cf3 * rc(S, rho_zz, c, 2));
+        for (int k = 1; k < L; k++)
+            CW(w, c, k) = CW(w, c, k) / (rz(S, D(fzm), k) * CW(rho_zz, c, k) + rz(S, D(fzp), k) * CW(rho_zz, c, k - 1));
+    }
+}
+
 void ora_mpas_srk3(ora_state* S, double dt, int schedule) {
     int number_of_sub_steps = 2;
     double rk_sub_timestep[3] = {dt / 3, dt / number_of_sub_steps, dt / number_of_sub_steps};
@@ -1292,6 +1362,7 @@ void ora_mpas_srk3(ora_state* S, double dt, int schedule) {
             ora_mpas_acoustic_step(S, rk_sub_timestep[rk_step], small_step);
             ora_atm_divergence_damping_3d(S, rk_sub_timestep[rk_step]);
         }
+        ora_mpas_recover(S, number_sub_steps[rk_step], rk_step, dt); /* rk_timestep.rg:460 (Q7) */
         ora_atm_compute_solve_diagnostics(S, 0, rk_step);
     }
     ora_atm_rk_dynamics_substep_finish(S, 1, 1);

@@ -57,6 +57,7 @@ def load():
             "ora_mpas_vert_imp_coefs": (None, [p, dbl]),
             "ora_mpas_acoustic_step": (None, [p, dbl, i32]),
             "ora_mpas_srk3": (None, [p, dbl, i32]),
+            "ora_mpas_recover": (None, [p, i32, i32, dbl]),
             "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
         }
         for n, (res, args) in sig.items():
@@ -128,6 +129,9 @@ class Oracle:
 
     def mpas_acoustic_step(self, dts, small_step):
         self.lib.ora_mpas_acoustic_step(self.p, dts, small_step)
+
+    def mpas_recover(self, ns, rk_step, dt):
+        self.lib.ora_mpas_recover(self.p, ns, rk_step, dt)
 
     def mpas_srk3(self, dt, schedule=1):
         self.lib.ora_mpas_srk3(self.p, dt, schedule)

@@ -183,3 +183,41 @@ def test_mpas_srk3_runs(x1_2562):
     O.Oracle(st).mpas_srk3(720.0, 1)
     for name in ("rw_p", "rho_pp", "rtheta_pp", "ru_p", "u", "w"):
         assert np.isfinite(st[name]).all(), name
+
+
+@pytest.mark.parametrize("rk_step", [0, 2])
+def test_mpas_recover_numpy(x1_2562, rk_step):
+    """ora_mpas_recover against NumPy: ru = ru_save + ru_p (Q24), rw/wwAvg/w of the
+    interior interfaces, w(L) = 0, exner = (zz rgas/p0 (rtheta_p + rtheta_base))^rcv, and
+    the lower-boundary flux added to w(0) once per edge"""
+    from mpasdyn import mesh as M
+    st = make_state(M.zero_based(x1_2562), 5, "random")
+    st["bdyMaskCell"][...] = 0
+    got = st.copy()
+    O.Oracle(got).mpas_recover(3, rk_step, 240.0)
+    n, nE, L = st.nCells, st.nEdges, st.L
+    rho_zz = st["rho_p_save"][:n, :L] + st["rho_pp"][:n, :L] + st["rho_base"][:n, :L]
+    assert np.array_equal(got["rho_zz"][:n, :L], rho_zz)
+    ru = st["ru_save"][:nE, :L] + st["ru_p"][:nE, :L]
+    assert np.array_equal(got["ru"][:nE, :L], ru)
+    c1, c2 = st["cellsOnEdge"][:nE, 0], st["cellsOnEdge"][:nE, 1]
+    rzf = got["rho_zz"]
+    assert np.array_equal(got["u"][:nE, :L], 2.0 * ru / (rzf[c1, :L] + rzf[c2, :L]))
+    rw = st["rw_save"][:n, 1:L] + st["rw_p"][:n, 1:L]
+    assert np.array_equal(got["rw"][:n, 1:L], rw) and np.array_equal(got["rw"][:n, 0], st["rw"][:n, 0])
+    assert (got["w"][:n, L] == 0.0).all()
+    if rk_step == 2:
+        rtp = got["rtheta_p"][:n, :L]
+        ex = (st["zz"][:n, :L] * (287.0 / 1.0e5) * (rtp + st["rtheta_base"][:n, :L])) ** (287.0 / (7.0 * 287.0 / 2.0 - 287.0))
+        assert np.allclose(got["exner"][:n, :L], ex, rtol=1e-14, atol=0)
+    # w(0): the boundary flux of every edge once, over the cf-weighted density
+    cf1, cf2, cf3 = st["cf1"][0], st["cf2"][0], st["cf3"][0]
+    ne = st["nEdgesOnCell"][:n, 0]
+    w0 = np.zeros(n)
+    for i in range(10):
+        e = st["edgesOnCell"][:n, i]
+        flux = cf1 * got["ru"][e, 0] + cf2 * got["ru"][e, 1] + cf3 * got["ru"][e, 2]
+        term = st["edgesOnCell_sign"][:n, i] * (st["zb_cell"][:n, 0, i] + np.copysign(1.0, flux) * st["zb3_cell"][:n, 0, i]) * flux
+        w0 = np.where(i < ne, w0 + term, w0)
+    w0 = w0 / (cf1 * rzf[:n, 0] + cf2 * rzf[:n, 1] + cf3 * rzf[:n, 2])
+    assert np.array_equal(got["w"][:n, 0], w0)
