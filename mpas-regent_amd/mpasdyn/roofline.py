@@ -65,6 +65,15 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False):
         return (["h", "u", "cellsOnEdge", "dcEdge", "dvEdge", "edgesOnEdge_ECP", "nEdgesOnEdge", "verticesOnEdge",
                  "weightsOnEdge", "edgesOnCell", "edgesOnCellSign", "invAreaCell", "nEdgesOnCell", "edgesOnVertex",
                  "edgesOnVertexSign", "fVertex", "invAreaTriangle"], writes)
+    if task == "atm_recover_large_step_variables_work":  # (:1766-1872; rk_step 2 adds the exner part)
+        reads = ["rho_p_save", "rho_pp", "rho_base", "wwAvg", "rw_save", "rw_p", "zz", "rtheta_p_save", "rtheta_pp",
+                 "rtheta_base", "ruAvg", "ru_save", "ru_p", "zb_cell", "zb3_cell", "edgesOnCell", "edgesOnCell_sign",
+                 "nEdgesOnCell", "cellsOnEdge", "bdyMaskCell"]
+        writes = ["rho_p", "rho_zz", "wwAvg", "rw", "w", "rtheta_p", "theta_m", "ruAvg", "ru", "u"]
+        if rk_step == 2:
+            reads += ["rt_diabatic_tend", "exner_base"]
+            writes += ["exner", "pressure_p"]
+        return reads, writes
     if task == "atm_rk_dynamics_substep_finish":
         return (["wwAvg", "rho_zz_old_split", "ruAvg"], ["wwAvg_split", "wwAvg", "rho_zz", "ruAvg_split", "ruAvg"])
     raise KeyError(task)
