@@ -87,6 +87,21 @@ __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
     colk(fw(S, F_u), e) = 2 * ru / (rz1 + rz2);
 }
 
+// One slot's two terms: a = level-0 flux term (lanes 0..2 of ru, level 0 of zb/zb3), b = this
+// level's term.
+template <int LP, bool MPASV>
+__device__ __forceinline__ void recover_w_slot(double r, double z, double z3, double sg, int k, double fzm,
+                                               double fzp, double cf1, double cf2, double cf3, double& a,
+                                               double& b) {
+    const double r_m = lvl_dn<LP>(r, k);
+    const double r0 = __shfl(r, 0, LP), r1 = __shfl(r, 1, LP), r2 = __shfl(r, 2, LP);
+    const double zb0 = __shfl(z, 0, LP), zb30 = __shfl(z3, 0, LP);
+    const double flux = (cf1 * r0 + cf2 * r1 + cf3 * r2);
+    a = sg * (zb0 + copysign(1.0, flux) * zb30) * flux;
+    const double flux2 = MPASV ? fzm * r + fzp * r_m : fzm * r * (fzp * r_m);  // (ref: Q24 literal)
+    b = sg * (z + copysign(1.0, flux2) * z3) * flux2;
+}
+
 // :1839-1870: the w recovery from (rho*omega)_p over the cell's edges, then the division.
 // The level-0 term (cf1..cf3 flux) is added to w(cell, 0) at every one of the nVertLevels
 // level iterations of the cell; lane 0 replays that sequence in the reference's order.
@@ -98,41 +113,59 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
     if (c >= S.nCO) return;
     if (fi(S, F_bdyMaskCell)[c] > kRelaxZone) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
-    int e_[10];
-    double sg_[10], zb0_[10], zb30_[10], a_[10], b_[10];
-    row_ld(fi(S, F_edgesOnCell) + (size_t)c * 10, e_);
-    row_ld(fd(S, F_edgesOnCell_sign) + (size_t)c * 10, sg_);
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgn = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+    int e_[NF];
+    double sg_[NF];
+    row_ld(eoc, e_);
+    row_ld(sgn, sg_);
     const double *ru = fd(S, F_ru), *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double cf1 = fd(S, F_cf1)[0], cf2 = fd(S, F_cf2)[0], cf3 = fd(S, F_cf3)[0];
-    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L), rz_m = lvl_dn<LP>(rz, k);
-    const double rz1 = __shfl(rz, 1, LP), rz2 = __shfl(rz, 2, LP);
-    double w = col_rd<LP>(fd(S, F_w), c, k, L);
+    double rz, w;
+    col_rd2<LP>(fd(S, F_rho_zz), fd(S, F_w), c, k, L, rz, w);
+    const double rz_m = lvl_dn<LP>(rz, k), rz1 = __shfl(rz, 1, LP), rz2 = __shfl(rz, 2, LP);
+    // the first NF slots: loads issued unconditionally, in pairs (every lane is active);
+    // slots NF..9 (cells with more edges) one at a time under wave-uniform guards
+    double r_[NF], z_[NF], z3_[NF], a_[10], b_[10];
 #pragma unroll
-    for (int i = 0; i < 10; i++) {
-        const double r = col_rd<LP>(ru, e_[i], k, L), r_m = lvl_dn<LP>(r, k);
-        const double r0 = __shfl(r, 0, LP), r1 = __shfl(r, 1, LP), r2 = __shfl(r, 2, LP);
-        const double z = zb[((size_t)c * 10 + i) * LP + lpos(LP, k)], z3 = zb3[((size_t)c * 10 + i) * LP + lpos(LP, k)];
-        zb0_[i] = __shfl(z, 0, LP);
-        zb30_[i] = __shfl(z3, 0, LP);
-        const double flux = (cf1 * r0 + cf2 * r1 + cf3 * r2);
-        a_[i] = sg_[i] * (zb0_[i] + copysign(1.0, flux) * zb30_[i]) * flux;
-        const double flux2 = MPASV ? fzm * r + fzp * r_m : fzm * r * (fzp * r_m);  // (ref: Q24 literal)
-        b_[i] = sg_[i] * (z + copysign(1.0, flux2) * z3) * flux2;
+    for (int i = 0; i < NF; i += 2) {
+        gather2s<LP>(ru, e_[i], e_[i + 1], k, r_[i], r_[i + 1]);
+        gather2<LP>(zb, c * 10 + i, zb3, c * 10 + i, k, z_[i], z3_[i]);
+        gather2<LP>(zb, c * 10 + i + 1, zb3, c * 10 + i + 1, k, z_[i + 1], z3_[i + 1]);
+    }
+#pragma unroll
+    for (int i = 0; i < NF; i++)
+        recover_w_slot<LP, MPASV>(r_[i], z_[i], z3_[i], sg_[i], k, fzm, fzp, cf1, cf2, cf3, a_[i], b_[i]);
+#pragma unroll
+    for (int i = NF; i < 10; i++) {
+        a_[i] = b_[i] = 0.0;
+        if (i < ne) {
+            const double r = colk(ru, eoc[i]), z = colk(zb, c * 10 + i), z3 = colk(zb3, c * 10 + i);
+            recover_w_slot<LP, MPASV>(r, z, z3, sgn[i], k, fzm, fzp, cf1, cf2, cf3, a_[i], b_[i]);
+        }
     }
     if (k == 0 && MPASV) {
-        for (int i = 0; i < ne; i++) w = w + a_[i];
+#pragma unroll
+        for (int i = 0; i < 10; i++)
+            if (i < ne) w = w + a_[i];
         w = w / (cf1 * rz + cf2 * rz1 + cf3 * rz2);
     } else if (k == 0) {
-        for (int i = 0; i < ne; i++) {  // level iteration 0
-            w += a_[i];
-            w += b_[i];
-        }
+#pragma unroll
+        for (int i = 0; i < 10; i++)  // level iteration 0
+            if (i < ne) {
+                w += a_[i];
+                w += b_[i];
+            }
         for (int kk = 1; kk < L; kk++)  // level iterations 1..nVertLevels-1
-            for (int i = 0; i < ne; i++) w += a_[i];
+#pragma unroll
+            for (int i = 0; i < 10; i++)
+                if (i < ne) w += a_[i];
         w /= (cf1 * rz + cf2 * rz1 + cf3 * rz2);
     } else {
-        for (int i = 0; i < ne; i++) w += b_[i];
+#pragma unroll
+        for (int i = 0; i < 10; i++)
+            if (i < ne) w += b_[i];
         w /= (fzm * rz + fzp * rz_m);
     }
     if (k < L) colk(fw(S, F_w), c) = w;
