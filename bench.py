@@ -86,7 +86,7 @@ def upload_inputs(ctx, st):
     ctx.sync()
 
 
-def cpu_baseline(ncells, L, dt, threads):
+def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False):
     """the oracle (C restatement, -O3, OpenMP) on the host cores: one RK3 step of the
     same workload; kind "port" (the Regent/Legion reference cannot be built or run)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -100,11 +100,16 @@ def cpu_baseline(ncells, L, dt, threads):
     o = O.Oracle(st)
     n, t0 = 0, time.perf_counter()
     while n < 8 and (n == 0 or time.perf_counter() - t0 < 10.0):  # a bounded ~10 s sample
-        o.atm_srk3(dt, 1)
+        if physics:
+            o.mpas_srk3(dt, 1, transport=transport)
+        else:
+            o.atm_srk3(dt, 1)
         n += 1
     t = (time.perf_counter() - t0) / n
+    what = "MPAS-solver " if physics else ""
+    what += "RK3 steps with scalar transport" if transport else "RK3 steps"
     return {"value": round(ncells / t / 1e6, 6), "unit": "Mcell-columns/s", "cores": threads, "kind": "port",
-            "sample": f"{n} RK3 steps (schedule 0,1,2) of x1.{ncells} x {L} levels by oracle/mpas_oracle.c "
+            "sample": f"{n} {what} (schedule 0,1,2) of x1.{ncells} x {L} levels by oracle/mpas_oracle.c "
                       f"(-O3, OpenMP {threads} threads), {t:.2f} s per step"}
 
 
@@ -135,7 +140,13 @@ def main():
     ap.add_argument("--replicas", action="store_true", help="N > 1: full-mesh replicas instead of a decomposition")
     ap.add_argument("--decompose", action="store_true",
                     help="run the decomposed (RCCL halo) path also at N = 1 (a 1-part decomposition)")
+    ap.add_argument("--physics", action="store_true",
+                    help="the MPAS vertical solver (option physics = 1: 4 acoustic substeps + recover per step)")
+    ap.add_argument("--transport", action="store_true",
+                    help="physics = 1 plus the monotonic transport of the 8 scalars in every step (single GPU)")
     args = ap.parse_args()
+    if args.transport:
+        args.physics = True
 
     # Libraries print banners on stdout from C (RCCL's version lines at communicator
     # creation); the contract is ONE JSON line there: route fd 1 to stderr for the run
@@ -188,6 +199,8 @@ def main():
         ctx = lib.Context(*dims, device=local_rank)
         work_dims = dims
     ctx.set_option("exact", args.exact)
+    ctx.set_option("physics", int(args.physics))
+    ctx.set_option("transport", int(args.transport))
     for kv in args.option:
         k, v = kv.split("=")
         ctx.set_option(k, int(v))
@@ -232,7 +245,8 @@ def main():
     rep = ctx.timing_report()
     ctx.timing(False)
     kw_of = {"atm_compute_dyn_tend_work[rk0]": ("atm_compute_dyn_tend_work", {"rk_step": 0}),
-             "atm_compute_dyn_tend_work[rk>0]": ("atm_compute_dyn_tend_work", {"rk_step": 1})}
+             "atm_compute_dyn_tend_work[rk>0]": ("atm_compute_dyn_tend_work", {"rk_step": 1}),
+             "atm_recover_large_step_variables_work": ("atm_recover_large_step_variables_work", {"rk_step": 2})}
     tasks_out = {}
     for name, (calls, ms) in rep.items():
         task, kw = kw_of.get(name, (name, {}))
@@ -253,7 +267,7 @@ def main():
             "frac": round(dt_["GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "GB/launch",
             "b_alg_per_launch_GB": dt_["b_alg_GB"], "avg_launch_ms": dt_["avg_ms"],
             "traffic_frac": dt_.get("hbm_frac_measured")}
-    b_step = roofline.b_alg_step(work_dims)
+    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport))
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -264,18 +278,21 @@ def main():
     out = {"metric": METRIC, "value": round(value, 3), "unit": "Mcell-columns/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
            "scaling": "strong" if decomposed else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-           "config": {"workload": f"x1.{ncells} x {L} levels, atm_srk3 (3 dyn_tend rk 0/1/2, 7 acoustic substeps)",
+           "config": {"workload": f"x1.{ncells} x {L} levels, atm_srk3 (3 dyn_tend rk 0/1/2, " +
+                                  ("4 acoustic substeps + recover (MPAS vertical solver)" if args.physics
+                                   else "7 acoustic substeps") +
+                                  (", monotonic transport of 8 scalars" if args.transport else "") + ")",
                       "nCells": ncells, "nEdges": m.nEdges, "nVertices": m.nVertices, "nVertLevels": L,
                       "dt": dt, "parallelism": (f"decomposed{world}" if decomposed else
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
-                      "exact": args.exact},
+                      "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport)},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}
     if halo_info:
         out["halo"] = halo_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count())))
-        out["cpu_baseline"] = cpu_baseline(ncells, L, dt, threads)
+        out["cpu_baseline"] = cpu_baseline(ncells, L, dt, threads, args.physics, args.transport)
     elif rank == 0:
         out["cpu_baseline"] = None
     ctx.close()

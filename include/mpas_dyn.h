@@ -63,7 +63,10 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), recover_large_step
  * with Q24 fixed, and in mpas_atm_srk3 number_sub_steps acoustic substeps (Q5) followed by
  * recover (Q7); every other task as the reference.
- * Default 0: the reference's semantics. */
+ * Default 0: the reference's semantics.
+ * "transport" = 1 (needs "physics" = 1; single subdomain) makes mpas_atm_srk3 copy scalars
+ * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
+ * recover, before atm_rk_dynamics_substep_finish.  Default 0. */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
 /* reads every option above ("self", default 1: when every cell is
  * among the cellsOnEdge of its own edges -- mpas-mode ids -- the cell kernels gather
@@ -125,6 +128,16 @@ int mpas_reconstruct_2d(mpas_ctx* ctx, int includeHalos, int on_a_sphere);
  *       pressure = pressure_base + pressure_p on levels 0..nVertLevels-1 (theta is in the
  *       task's write set but its statement is commented out in the reference: unchanged) */
 int mpas_atm_compute_output_diagnostics(mpas_ctx* ctx);
+/* Monotonic scalar transport.  Replaces no reference entry point: the
+ *       reference has none (Q26 -- scalars:double[8], data_structures.rg:36, is declared and
+ *       never used; the north star names the transport).  MPAS-A's atm_advance_scalars_mono
+ *       (flux-corrected transport): the 8 scalars of scalars_old are advected over dt by the
+ *       mass fluxes ruAvg (edges) and wwAvg (interfaces) from density rho_zz_old_split to
+ *       rho_zz with 3rd-order fluxes (adv_coefs, adv_coefs_3rd; flux3 vertically, coef 0.25)
+ *       limited so that no new extrema appear; result in scalars (levels 0..nVertLevels-1).
+ *       Statement order: oracle/mpas_oracle.c ora_mpas_advance_scalars_mono.  MPAS_ENOTSUP
+ *       on a decomposed context. */
+int mpas_atm_advance_scalars_mono(mpas_ctx* ctx, double dt);
 /* rk_timestep.rg:29 summarize_timestep(cr, er, config_print_detailed_minmax_vel,
  *       config_print_global_minmax_vel, config_print_global_minmax_sca): the values the
  *       reference prints, into out[31] (host memory; the call synchronises):

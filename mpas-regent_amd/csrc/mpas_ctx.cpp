@@ -43,6 +43,10 @@ const FieldInfo kFields[X_COUNT] = {
     {"wfl", K_C2F, 2, D_M, 0, 0},
     {"wc", K_C3, 1, D_M, 0, 0},
     {"F", K_E3, 1, D_M, 0, 0},
+    {"Ah", K_E3, 8, D_M, 0, 0},
+    {"Rp", K_C3V, 8, D_M, 0, 0},
+    {"Rm", K_C3V, 8, D_M, 0, 0},
+    {"su", K_C3V, 8, D_M, 0, 0},
 };
 }  // namespace mpas
 
@@ -60,6 +64,7 @@ struct mpas_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int exact = 0;
+    int transport = 0;  // option "transport": atm_srk3 runs the monotonic scalar transport (physics = 1)
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     int overlap = 1;   // option "overlap": halo exchanges beside interior compute
@@ -107,7 +112,7 @@ size_t dev_bytes(const mpas_ctx* c, int f) {
     const size_t LP = c->S.LP;
     size_t rows = (size_t)entity_count(c, fi.kind) + 1;
     switch (fi.kind) {
-        case K_C3: case K_E3: case K_V3: return rows * LP * 8;
+        case K_C3: case K_E3: case K_V3: return rows * fi.width * LP * 8;
         case K_C3V: return rows * fi.width * LP * 8;
         case K_C3B: return rows * LP;
         case K_ZV: return LP * 8;
@@ -221,6 +226,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     number_sub_steps[2] = number_of_sub_steps;
     const DevState& S = c->S;
     hipStream_t st = c->stream;
+    if (c->transport) {
+        if (c->halo) throw Fail{MPAS_ENOTSUP, "transport: decomposed meshes are not supported (single subdomain only)"};
+        // the time level the transport starts from (MPAS-A scalars(time level 1))
+        run_task(c, "scalars_save", [&] {
+            return hipMemcpyAsync(S.f[F_scalars_old], S.f[F_scalars], dev_bytes(c, F_scalars), hipMemcpyDeviceToDevice, st);
+        });
+    }
     run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
     run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
     run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
@@ -250,6 +262,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                      [&] { return launch_recover_large_step(S, st, number_sub_steps[rk_step], rk_step, dt); });
         run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
     }
+    if (c->transport)  // after the last stage's recover: ruAvg / wwAvg / rho_zz of the step
+        run_task(c, "atm_advance_scalars_mono", [&] { return launch_advance_scalars_mono(S, st, dt); });
     run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
     // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }
@@ -377,6 +391,10 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "physics") == 0) {
             if (value != 0 && value != 1) throw Fail{MPAS_EINVAL, "physics must be 0 (reference) or 1 (MPAS vertical solver)"};
             c->S.physics = (int)value;
+            if (!value) c->transport = 0;
+        } else if (name && std::strcmp(name, "transport") == 0) {
+            if (value && !c->S.physics) throw Fail{MPAS_EINVAL, "transport needs physics = 1 (it reads the recovered ruAvg, wwAvg, rho_zz)"};
+            c->transport = value ? 1 : 0;
         } else if (name && std::strcmp(name, "overlap") == 0) {
             c->overlap = value ? 1 : 0;
             if (c->halo) c->halo->overlap = c->overlap;
@@ -395,6 +413,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "epw") == 0) *value = c->S.epw;
         else if (name && std::strcmp(name, "vcmix") == 0) *value = c->S.vcmix;
         else if (name && std::strcmp(name, "physics") == 0) *value = c->S.physics;
+        else if (name && std::strcmp(name, "transport") == 0) *value = c->transport;
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "selfc") == 0) {
@@ -704,6 +723,14 @@ int mpas_atm_recover_large_step_variables_work(mpas_ctx* c, int ns, int rk_step,
 int mpas_reconstruct_2d(mpas_ctx* c, int includeHalos, int on_a_sphere) {
     (void)includeHalos;  // :1909-1912: the range is nCells either way
     MPAS_TASK("mpas_reconstruct_2d", launch_reconstruct_2d(c->S, c->stream, on_a_sphere ? 1 : 0));
+}
+int mpas_atm_advance_scalars_mono(mpas_ctx* c, double dt) {
+    if (!c) return MPAS_EINVAL;
+    if (c->halo) {
+        c->err = "atm_advance_scalars_mono: decomposed meshes are not supported (single subdomain only)";
+        return MPAS_ENOTSUP;
+    }
+    MPAS_TASK("atm_advance_scalars_mono", launch_advance_scalars_mono(c->S, c->stream, dt));
 }
 int mpas_atm_compute_output_diagnostics(mpas_ctx* c) {
     MPAS_TASK("atm_compute_output_diagnostics", launch_output_diagnostics(c->S, c->stream));

@@ -2,6 +2,7 @@
 //
 // Device layout (HBM), chosen for one wavefront per column:
 //   C3/E3/V3   f[entity * LP + lpos(k)]            k = 0..L   (LP = pow2 >= L+1, <= 64)
+//              (width W > 1, transport scratch only: f[(entity * W + i) * LP + lpos(k)])
 //   C3V        f[(entity * W + i) * LP + lpos(k)]  (zb_cell / zb3_cell: coalesced per component)
 //   C2*/E2*/V2* f[entity * W + i]                  (2-D mesh data)
 //   C3B        uint8 f[entity * LP + lpos(k)]
@@ -66,6 +67,11 @@ enum FieldId {
                 // the U section still reads the pre-zeroing w (:1013)
     X_F,        // flux_arr of the theta advection (:1333-1340) per edge and level: it
                 // depends only on the edge, so it is formed once per edge, not per cell
+    // monotonic scalar transport (k_transport.hip), one column per (entity, scalar)
+    X_Ah,       // antidiffusive edge flux                                      E3 x 8
+    X_Rp,       // R+ (fraction of the incoming antidiffusive flux allowed)     C3V x 8
+    X_Rm,       // R- (outgoing)                                                C3V x 8
+    X_su,       // the upwind update                                            C3V x 8
     X_COUNT
 };
 
@@ -161,6 +167,7 @@ hipError_t launch_prepare(DevState& S, hipStream_t st);
 hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt);
 hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
 hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
+hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt);
 size_t summarize_scratch_bytes();
 hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, double* out);
 

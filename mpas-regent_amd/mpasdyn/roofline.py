@@ -76,6 +76,12 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False):
         return reads, writes
     if task == "atm_rk_dynamics_substep_finish":
         return (["wwAvg", "rho_zz_old_split", "ruAvg"], ["wwAvg_split", "wwAvg", "rho_zz", "ruAvg_split", "ruAvg"])
+    if task == "atm_advance_scalars_mono":  # k_transport.hip (Q26: MPAS-A's, not the reference's)
+        return (["scalars_old", "ruAvg", "wwAvg", "rho_zz_old_split", "rho_zz", "cellsOnEdge", "advCellsForEdge",
+                 "nAdvCellsForEdge", "adv_coefs", "adv_coefs_3rd", "dvEdge", "edgesOnCell", "nEdgesOnCell",
+                 "invAreaCell"], ["scalars"])
+    if task == "scalars_save":  # srk3 with transport: scalars_old = scalars
+        return ["scalars"], ["scalars_old"]
     raise KeyError(task)
 
 
@@ -100,8 +106,26 @@ def b_alg(task, dims, **kw):
     return sum(field_bytes(x, *dims) for x in set(reads)) + sum(field_bytes(x, *dims) for x in set(writes))
 
 
-def step_schedule(schedule=1):
-    """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481)"""
+def step_schedule(schedule=1, physics=0, transport=0):
+    """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
+    (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
+    recover after each stage; transport = 1 adds the scalar save and the transport"""
+    if physics:
+        out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
+               ("atm_compute_vert_imp_coefs", {}, 2)]
+        if schedule == 1:
+            out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
+        out += [("atm_set_smlstep_pert_variables_work", {}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1}, 1),
+                ("atm_divergence_damping_3d", {}, 4),
+                ("atm_recover_large_step_variables_work", {"rk_step": 0}, 2),
+                ("atm_recover_large_step_variables_work", {"rk_step": 2}, 1),
+                ("atm_compute_solve_diagnostics", {}, 2), ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
+                ("atm_rk_dynamics_substep_finish", {}, 1)]
+        if transport:
+            out += [("scalars_save", {}, 1), ("atm_advance_scalars_mono", {}, 1)]
+        return out
     out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
            ("atm_compute_vert_imp_coefs", {}, 2)]
     if schedule == 1:
@@ -115,5 +139,5 @@ def step_schedule(schedule=1):
     return out
 
 
-def b_alg_step(dims, schedule=1):
-    return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule))
+def b_alg_step(dims, schedule=1, physics=0, transport=0):
+    return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport))

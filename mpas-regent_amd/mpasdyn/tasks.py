@@ -94,6 +94,12 @@ def atm_compute_output_diagnostics(ctx):
     ctx._check(ctx.lib.mpas_atm_compute_output_diagnostics(ctx.h), "atm_compute_output_diagnostics")
 
 
+def atm_advance_scalars_mono(ctx, dt):
+    """Monotonic scalar transport of scalars_old into scalars over dt (SURVEY §8.7 row 4;
+    no reference task exists, Q26 -- MPAS-A's atm_advance_scalars_mono; include/mpas_dyn.h)"""
+    ctx._check(ctx.lib.mpas_atm_advance_scalars_mono(ctx.h, float(dt)), "atm_advance_scalars_mono")
+
+
 def summarize_timestep(ctx, config_print_detailed_minmax_vel=False, config_print_global_minmax_vel=False,
                        config_print_global_minmax_sca=False):
     """rk_timestep.rg:29; returns the 31 values the reference prints (layout: include/mpas_dyn.h)"""

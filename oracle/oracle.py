@@ -57,6 +57,8 @@ def load():
             "ora_mpas_vert_imp_coefs": (None, [p, dbl]),
             "ora_mpas_acoustic_step": (None, [p, dbl, i32]),
             "ora_mpas_srk3": (None, [p, dbl, i32]),
+            "ora_mpas_srk3_ex": (None, [p, dbl, i32, i32]),
+            "ora_mpas_advance_scalars_mono": (None, [p, dbl]),
             "ora_mpas_recover": (None, [p, i32, i32, dbl]),
             "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
         }
@@ -133,8 +135,12 @@ class Oracle:
     def mpas_recover(self, ns, rk_step, dt):
         self.lib.ora_mpas_recover(self.p, ns, rk_step, dt)
 
-    def mpas_srk3(self, dt, schedule=1):
-        self.lib.ora_mpas_srk3(self.p, dt, schedule)
+    def mpas_srk3(self, dt, schedule=1, transport=False):
+        self.lib.ora_mpas_srk3_ex(self.p, dt, schedule, int(bool(transport)))
+
+    def mpas_advance_scalars_mono(self, dt):
+        """monotonic scalar transport (Q26: not in the reference; mpas_oracle.c)"""
+        self.lib.ora_mpas_advance_scalars_mono(self.p, dt)
 
     def atm_compute_output_diagnostics(self):
         self.lib.ora_atm_compute_output_diagnostics(self.p)

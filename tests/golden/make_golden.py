@@ -35,6 +35,9 @@ CASES = {
     "recover_ns3_rk2": lambda o: o.atm_recover_large_step_variables_work(3, 2, 240.0),
     "reconstruct_2d": lambda o: o.mpas_reconstruct_2d(False, True),
     "output_diagnostics": lambda o: o.atm_compute_output_diagnostics(),
+    # monotonic scalar transport (Q26, mpas mode; parity unpinned, tests/test_transport.py)
+    "scalars_mono": lambda o: o.mpas_advance_scalars_mono(600.0),
+    "mpas_srk3_transport": lambda o: o.mpas_srk3(720.0, 1, transport=True),
 }
 
 

@@ -63,3 +63,50 @@ def digest(a):
         return {"sum": float(np.sum(r)), "l2": float(np.sqrt(np.sum(r * r))), "min": float(np.min(r)),
                 "max": float(np.max(r)), "sha": hashlib.sha256(a.tobytes()).hexdigest()[:32]}
     return {"sum": int(np.sum(a, dtype=np.int64)), "sha": hashlib.sha256(a.tobytes()).hexdigest()[:32]}
+
+
+def transport_state(mesh, L, dt, seed=SEED, const=None):
+    """A state for the monotonic scalar transport (Q26; mpas mode): the real x1 geometry in
+    0-based ids ("physical" variant), a smooth rotating flow plus noise in ruAvg, a
+    random vertical mass flux wwAvg (0 at the bottom and top interfaces), rho_zz_old_split
+    random and rho_zz the density the same fluxes leave after dt (mass-consistent, so the
+    upwind update of a constant is that constant), scalars_old random in [0, 0.02] or the
+    constant `const`.  Returns (state, cell volumes [nCells, L])."""
+    from mpasdyn import mesh as M
+    m0 = M.zero_based(mesh)
+    st = make_state(m0, L, "physical", seed=seed)
+    rng = np.random.default_rng(seed)
+    nC, nE = st.nCells, st.nEdges
+    lat = st["latEdge"][:nE, 0]
+    ang = st["angleEdge"][:nE, 0]
+    kk = np.arange(L)[None, :]
+    ru = 20.0 * np.cos(lat)[:, None] * np.cos(ang)[:, None] * (1 + 0.5 * np.sin(0.3 * kk)) \
+        + 2.0 * rng.standard_normal((nE, L))
+    st["ruAvg"][:nE, :L] = ru
+    st["ruAvg"][:nE, L] = 0.0
+    ww = 0.01 * rng.standard_normal((nC, L + 1))  # vertical Courant number <~ 0.1
+    ww[:, 0] = 0.0
+    ww[:, L] = 0.0
+    st["wwAvg"][:nC] = ww
+    ro = 0.8 + 0.4 * rng.random((nC, L))
+    st["rho_zz_old_split"][:nC, :L] = ro
+    invA = st["invAreaCell"][:nC, 0]
+    dv = st["dvEdge"][:nE, 0]
+    rdzw = st["rdzw"][:L]
+    eoc = st["edgesOnCell"][:nC]
+    coe = st["cellsOnEdge"][:nE]
+    ne = st["nEdgesOnCell"][:nC, 0]
+    div = np.zeros((nC, L))
+    for j in range(eoc.shape[1]):
+        on = j < ne
+        e = np.where(on, eoc[:, j], 0)
+        sg = np.where(coe[e, 0] == np.arange(nC), 1.0, -1.0)
+        div += np.where(on[:, None], sg[:, None] * dv[e][:, None] * ru[e], 0.0)
+    div = div * invA[:, None] + (ww[:, 1:] - ww[:, :L]) * rdzw[None, :]
+    st["rho_zz"][:nC, :L] = ro - dt * div
+    if const is None:
+        st["scalars_old"][:nC, :L] = 0.02 * rng.random((nC, L, 8))
+    else:
+        st["scalars_old"][:nC, :L] = const
+    vol = 1.0 / (invA[:, None] * rdzw[None, :])
+    return st, vol

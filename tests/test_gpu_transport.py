@@ -1,0 +1,101 @@
+"""GPU (libmpasdyn k_transport.hip) vs oracle parity of the monotonic scalar transport
+(Q26: no reference transport exists, the oracle restates MPAS-A's
+atm_advance_scalars_mono and is pinned by tests/test_transport.py's properties).
+
+Tolerances: the kernels evaluate the oracle's expressions in its operand order (built
+with -ffp-contract=off), so the task is value-identical to the oracle.  Inside a whole
+RK3 step with physics = 1 the inputs come from the dynamics: exact mode is
+value-identical except the pow fields (RTOL_POW), fast mode within RTOL_STEP = 1e-9.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import compare_states, make_state, transport_state
+from mpasdyn import lib, tasks as T
+
+pytestmark = pytest.mark.gpu
+
+DT = 600.0
+RTOL_STEP = 1e-9
+RTOL_POW = 1e-14
+POW_FIELDS = {"exner", "pressure_p"}
+
+
+def gpu(st, fn, exact=1, physics=1, transport=0):
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.set_option("exact", exact)
+        ctx.set_option("physics", physics)
+        ctx.set_option("transport", transport)
+        ctx.upload(st)
+        fn(ctx)
+        ctx.sync()
+        ctx.download(got)
+    return got
+
+
+@pytest.mark.parametrize("L", [5, 56])
+@pytest.mark.parametrize("const", [None, 0.0123])
+def test_transport_task(x1_2562, L, const):
+    st, vol = transport_state(x1_2562, L, DT, const=const)
+    ref = st.copy()
+    O.Oracle(ref).mpas_advance_scalars_mono(DT)
+    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT))
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+    # and the properties hold on the GPU result
+    nC = st.nCells
+    m_old = np.einsum("ck,cki->i", st["rho_zz_old_split"][:nC, :L] * vol, st["scalars_old"][:nC, :L])
+    m_new = np.einsum("ck,cki->i", got["rho_zz"][:nC, :L] * vol, got["scalars"][:nC, :L])
+    assert np.allclose(m_new, m_old, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("L", [1, 2, 63])
+def test_transport_task_edge_levels(x1_2562, L):
+    """nVertLevels 1 (no interior interface), 2 (2nd-order only), 63 (LP 64, full column)"""
+    st, _ = transport_state(x1_2562, L, DT)
+    ref = st.copy()
+    O.Oracle(ref).mpas_advance_scalars_mono(DT)
+    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT))
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
+def test_transport_task_random_ids(x1_2562):
+    """the literal 1-based ids of the reference's mesh (cells not among their edges'
+    cells: the non-SELF gathers) and every input synthetic"""
+    st = make_state(x1_2562, 5, "random")
+    ref = st.copy()
+    O.Oracle(ref).mpas_advance_scalars_mono(DT)
+    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT))
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("L", [5, 56])
+def test_srk3_transport(x1_2562, L):
+    """option transport = 1: scalars saved to scalars_old, then the transport after the
+    last stage's recover, inside mpas_atm_srk3"""
+    from mpasdyn import mesh as M
+    st = make_state(M.zero_based(x1_2562), L, "random")
+    ref = st.copy()
+    O.Oracle(ref).mpas_srk3(720.0, 1, transport=True)
+    assert not np.array_equal(ref["scalars"], st["scalars"])
+    for exact, tol, tf in ((1, RTOL_POW, POW_FIELDS), (0, RTOL_STEP, None)):
+        got = gpu(st, lambda c: T.atm_srk3(c, 720.0, 1), exact=exact, transport=1)
+        got["rho_zz"][st.nCells] = ref["rho_zz"][st.nCells]
+        bad = compare_states(got, ref, rtol=tol, tol_fields=tf)
+        assert not bad, f"exact={exact}: {bad[:6]}"
+
+
+def test_transport_option_rules(x1_2562):
+    st = make_state(x1_2562, 5, "random")
+    with lib.Context(*st.dims()) as ctx:
+        with pytest.raises(lib.MpasError):
+            ctx.set_option("transport", 1)  # needs physics = 1
+        ctx.set_option("physics", 1)
+        ctx.set_option("transport", 1)
+        assert ctx.get_option("transport") == 1
+        ctx.set_option("physics", 0)
+        assert ctx.get_option("transport") == 0
