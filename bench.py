@@ -64,11 +64,15 @@ class Hip:
         return float(ms.value)
 
 
-def build_inputs(ncells, L):
-    """the mesh and its one-time precompute (host); the 3-D state is filled on the device"""
+def build_inputs(ncells, L, zero_based=False):
+    """the mesh and its one-time precompute (host); the 3-D state is filled on the device.
+    zero_based: mpas-mode (0-based) connectivity, the ids the MPAS solver and the transport
+    are defined on (the default keeps the reference's raw 1-based ids, Q1)"""
     from mpasdyn import build_state as bs
     from mpasdyn import mesh
     m = mesh.icosahedral(LEVEL_OF[ncells])
+    if zero_based:
+        m = mesh.zero_based(m)
     st = bs.build_state(m, L, "physical", mesh_only=True)
     return m, st
 
@@ -94,6 +98,8 @@ def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False):
     from mpasdyn import build_state as bs
     from mpasdyn import mesh
     m = mesh.icosahedral(LEVEL_OF[ncells])
+    if physics:
+        m = mesh.zero_based(m)
     st = bs.build_state(m, L, "physical", oracle_fill=lambda s, seed, inc: O.Oracle(s).fill_synthetic(seed, False))
     rdzw, rdzu, fzm, fzp = bs.vertical_grid(st)
     st["rdzw"], st["rdzu"], st["fzm"], st["fzp"] = rdzw, rdzu, fzm, fzp
@@ -113,11 +119,11 @@ def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False):
                       f"(-O3, OpenMP {threads} threads), {t:.2f} s per step"}
 
 
-def pmc_traffic(task, ncells, L):
+def pmc_traffic(task, ncells, L, physics=False):
     """per-launch HBM bytes of `task` from a committed rocprofv3 PMC summary, if one
     exists for this configuration (profiles/pmc_x1.<n>_L<L>.json, written by
     tools/pmc_summary.py with the gfx950 FETCH_SIZE correction)"""
-    p = os.path.join(REPO, "profiles", f"pmc_x1.{ncells}_L{L}.json")
+    p = os.path.join(REPO, "profiles", f"pmc_{'transport_' if physics else ''}x1.{ncells}_L{L}.json")
     if not os.path.exists(p):
         return None
     with open(p) as f:
@@ -168,7 +174,7 @@ def main():
 
     ncells, L = args.ncells, args.levels
     dt = dt_for(ncells)
-    m, st = build_inputs(ncells, L)
+    m, st = build_inputs(ncells, L, zero_based=args.physics)
     decomposed = (world > 1 and not args.replicas) or args.decompose
     halo_info = None
     if decomposed:
@@ -254,14 +260,14 @@ def main():
         avg = ms / calls
         tasks_out[name] = {"launches_per_step": calls // n_prof, "avg_ms": round(avg, 4),
                            "b_alg_GB": round(b / 1e9, 4), "GBs": round(b / (avg * 1e-3) / 1e9, 1)}
-        tr = pmc_traffic(name, ncells, L) if not decomposed else None
+        tr = pmc_traffic(name, ncells, L, args.physics) if not decomposed else None
         if tr:  # SURVEY §8.5 metric 2: measured (FETCH + WRITE) bytes over this run's launch time
             tasks_out[name]["hbm_GB_measured"] = round(tr / 1e9, 4)
             tasks_out[name]["hbm_frac_measured"] = round(tr / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
     dom = max(tasks_out, key=lambda k: tasks_out[k]["avg_ms"] * tasks_out[k]["launches_per_step"])
     dt_ = tasks_out[dom]
     task, kw = kw_of.get(dom, (dom, {}))
-    traffic = pmc_traffic(dom, ncells, L) if not decomposed else None
+    traffic = pmc_traffic(dom, ncells, L, args.physics) if not decomposed else None
     traffic = round(traffic / 1e9, 4) if traffic else None
     roof = {"bound": "hbm", "kernel": dom, "achieved": dt_["GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(dt_["GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "GB/launch",

@@ -14,10 +14,12 @@
 //                cell, and R+ / R- (X_su, X_Rp, X_Rm, C3V x 8)
 //   k_tr_update  per cell: every A scaled by min(R- of its source, R+ of its receiver),
 //                s_new = su - dt div(scaled A) / rho_new  (scalars)
-// Column slot = (entity, scalar): the 8 scalars of an entity are 8 consecutive columns,
-// so the 8 wavefronts of an entity read the same connectivity, mass fluxes and densities
-// (one HBM fetch, then L2 hits).  One wavefront per column at 57 levels (LP = 64); the
-// vertical neighbours are lane shuffles.
+// Column slot = (entity, scalar pair): the 8 scalars of an entity are 8 consecutive
+// columns; a wavefront computes two of them (one 16-B lane load fetches a gathered column
+// pair: the gathers cost per load instruction), and the 4 wavefronts of an
+// entity read the same connectivity, mass fluxes and densities (one HBM fetch, then L2
+// hits).  One wavefront per column pair at 57 levels (LP = 64); the vertical neighbours
+// are lane shuffles.
 #include "mpas_dev.h"
 #include "mpas_halo.h"
 
@@ -31,20 +33,46 @@ __device__ __forceinline__ double tr_flux3(double q_im2, double q_im1, double q_
     return f4 + kCoef3 * fabs(ua) * ((q_ip1 - q_im2) - 3. * (q_i - q_im1)) / 12.0;
 }
 
-// entity and scalar of this lane's column slot
+// entity and scalar pair of this lane's column slot: a wavefront computes two scalars,
+// 2p and 2p+1, of one entity (their columns are adjacent, so one 16-B lane load fetches
+// both: ld2 below)
 template <int LP>
-__device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, int& isc) {
+__device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, int& p) {
     const int slot = col_of<LP>(xcd_block(S.xcd));
-    ent = (slot >> 3) + S.lo[kind];
-    isc = slot & (NSC - 1);
+    ent = (slot >> 2) + S.lo[kind];
+    p = (slot & 3) * 2;
 }
 
-// level k of the column of scalar isc of entity ent in a x8 field (64-bit offsets: the
-// edge scratch exceeds 4 GiB on the largest meshes)
+// level k of columns ia and ib of field f (64-bit column ids: the edge scratch exceeds
+// 4 GiB on the largest meshes).  At LP = 64 one 16-B load per lane (lanes 0-31 the level
+// pair k & 31 of column ia, lanes 32-63 that of column ib, the lpos layout) and a
+// permlane32 swap (gather2 of mpas_dev.h); two loads below LP 64.
 template <int LP>
-__device__ __forceinline__ size_t tr_at(int ent, int isc, int k) {
-    return ((size_t)ent * NSC + isc) * LP + lpos(LP, k);
+__device__ __forceinline__ void ld2(const double* f, size_t ia, size_t ib, int k, double& a, double& b) {
+    if constexpr (LP == 64) {
+        const double2 t = *(const double2*)((const char*)f + (k >= 32 ? ib : ia) * 512 + (size_t)(k & 31) * 16);
+        double x = t.x, y = t.y;
+        swap_halves(x, y);
+        a = x;
+        b = y;
+    } else {
+        a = f[ia * LP + lpos(LP, k)];
+        b = f[ib * LP + lpos(LP, k)];
+    }
 }
+// the inverse: store a (column ia) and b (column ib) at every level of the lane; at
+// LP = 64 one 16-B store per lane (every lane of the wavefront must take part)
+template <int LP>
+__device__ __forceinline__ void st2(double* f, size_t ia, size_t ib, int k, double a, double b) {
+    if constexpr (LP == 64) {
+        swap_halves(a, b);
+        *(double2*)((char*)f + (k >= 32 ? ib : ia) * 512 + (size_t)(k & 31) * 16) = make_double2(a, b);
+    } else {
+        f[ia * LP + lpos(LP, k)] = a;
+        f[ib * LP + lpos(LP, k)] = b;
+    }
+}
+__device__ __forceinline__ size_t col8(int ent, int i) { return (size_t)ent * NSC + i; }
 
 // interface k of a column: upwind (lo) and antidiffusive (A) vertical flux of the lane's
 // level; no flux through interfaces 0 and L
@@ -61,8 +89,8 @@ __device__ __forceinline__ void tr_vflux(double s, double w, int k, int L, doubl
 
 template <int LP>
 __global__ __launch_bounds__(256) void k_tr_edge(DevState S) {
-    int e, isc;
-    tr_slot<LP>(S, KE, e, isc);
+    int e, p;
+    tr_slot<LP>(S, KE, e, p);
     const int L = S.L, k = (int)(threadIdx.x % LP);
     if (e >= S.nEO) return;
     const int* rec = fi(S, X_eB) + (size_t)e * 24;  // cellsOnEdge(2) .. advCellsForEdge(9) @12, nAdv @22
@@ -76,21 +104,37 @@ __global__ __launch_bounds__(256) void k_tr_edge(DevState S) {
     const double dv = fd(S, F_dvEdge)[e];
     const double* so = fd(S, F_scalars_old);
     const double u = colk(fd(S, F_ruAvg), e);
-    double x[AF];
+    double xa[AF], xb[AF], s1a, s1b, s2a, s2b;
 #pragma unroll
-    for (int j = 0; j < AF; j++) x[j] = colk(so, adv[j] * NSC + isc);
-    const double s1 = colk(so, c1 * NSC + isc), s2 = colk(so, c2 * NSC + isc);
+    for (int j = 0; j < AF; j++) ld2<LP>(so, col8(adv[j], p), col8(adv[j], p + 1), k, xa[j], xb[j]);
+    // the upwind flux's two cells are normally advCellsForEdge(0) and (1) (MPAS's list
+    // construction): take their columns from the list; gather them only where they are not
+    // (wave-uniform branch, the same column either way)
+    if (na >= 2 && adv[0] == c1 && adv[1] == c2) {
+        s1a = xa[0], s1b = xb[0], s2a = xa[1], s2b = xb[1];
+    } else {
+        ld2<LP>(so, col8(c1, p), col8(c1, p + 1), k, s1a, s1b);
+        ld2<LP>(so, col8(c2, p), col8(c2, p + 1), k, s2a, s2b);
+    }
     const double sgn = copysign(1.0, u);
-    double acc = 0.0;
+    double acca = 0.0, accb = 0.0;
 #pragma unroll
-    for (int j = 0; j < AF; j++) acc = add_if(j < na, acc, (ac[j] + sgn * ac3[j]) * x[j]);
+    for (int j = 0; j < AF; j++) {
+        const double wgt = ac[j] + sgn * ac3[j];
+        acca = add_if(j < na, acca, wgt * xa[j]);
+        accb = add_if(j < na, accb, wgt * xb[j]);
+    }
     for (int j = AF; j < na; j++) {  // lists longer than the reference's 9 (width 15)
         const int cj = fi(S, F_advCellsForEdge)[(size_t)e * 15 + j];
         const double wgt = fd(S, F_adv_coefs)[(size_t)e * 15 + j] + sgn * fd(S, F_adv_coefs_3rd)[(size_t)e * 15 + j];
-        acc = acc + wgt * colk(so, cj * NSC + isc);
+        double ya, yb;
+        ld2<LP>(so, col8(cj, p), col8(cj, p + 1), k, ya, yb);
+        acca = acca + wgt * ya;
+        accb = accb + wgt * yb;
     }
-    const double lo = dv * (fmax(u, 0.0) * s1 + fmin(u, 0.0) * s2);
-    if (k != L) fw(S, X_Ah)[tr_at<LP>(e, isc, k)] = PADW(u * acc - lo);
+    const double loa = dv * (fmax(u, 0.0) * s1a + fmin(u, 0.0) * s2a);
+    const double lob = dv * (fmax(u, 0.0) * s1b + fmin(u, 0.0) * s2b);
+    st2<LP>(fw(S, X_Ah), col8(e, p), col8(e, p + 1), k, PADW(u * acca - loa), PADW(u * accb - lob));
 }
 
 // the first NF edge slots of a cell: edge, cells of the edge, "cell is cellsOnEdge(0)",
@@ -109,26 +153,52 @@ __device__ __forceinline__ void tr_slots(const DevState& S, int c, TrSlots& t) {
     row_ld(fd(S, X_ce_dv) + r, t.dv);
 }
 
-// one edge slot of k_tr_bounds: the upwind flux's contribution, the antidiffusive in/out
-// sums and the other cell's value in the bounds
-template <int LP>
+// one scalar's running sums of k_tr_bounds
+struct TrAcc {
+    double hlo = 0.0, pin = 0.0, pout = 0.0, smax, smin;
+};
+// one edge slot of k_tr_bounds for one scalar: the upwind flux's contribution, the
+// antidiffusive in/out sums and the other cell's value in the bounds
 __device__ __forceinline__ void tr_bound_slot(bool on, int s1f, double dv, double u, double x1, double x2, double A,
-                                              double& hlo, double& pin, double& pout, double& smax, double& smin) {
+                                              TrAcc& r) {
     const double sg = s1f ? 1.0 : -1.0;
     const double lo = dv * (fmax(u, 0.0) * x1 + fmin(u, 0.0) * x2);
-    hlo = add_if(on, hlo, sg * lo);
+    r.hlo = add_if(on, r.hlo, sg * lo);
     const double a = -sg * A;
-    pin = add_if(on, pin, fmax(a, 0.0));
-    pout = sub_if(on, pout, fmin(a, 0.0));
+    r.pin = add_if(on, r.pin, fmax(a, 0.0));
+    r.pout = sub_if(on, r.pout, fmin(a, 0.0));
     const double xo = s1f ? x2 : x1;
-    smax = on ? fmax(smax, xo) : smax;
-    smin = on ? fmin(smin, xo) : smin;
+    r.smax = on ? fmax(r.smax, xo) : r.smax;
+    r.smin = on ? fmin(r.smin, xo) : r.smin;
+}
+
+// the rest of k_tr_bounds for one scalar: vertical bounds and fluxes, su, R+ / R-
+template <int LP>
+__device__ __forceinline__ void tr_bound_fin(TrAcc& r, double s, double w, double r_o, double r_n, double invA,
+                                             double rdzw, double fzm, double fzp, double dt, int k, int L,
+                                             double& Rp, double& Rm, double& su) {
+    const double sm1 = lvl_dn<LP>(s, k), sp1 = lvl_up<LP>(s, k);
+    r.smax = k > 0 ? fmax(r.smax, sm1) : r.smax;
+    r.smin = k > 0 ? fmin(r.smin, sm1) : r.smin;
+    r.smax = k < L - 1 ? fmax(r.smax, sp1) : r.smax;
+    r.smin = k < L - 1 ? fmin(r.smin, sp1) : r.smin;
+    double lob, Ab;
+    tr_vflux<LP>(s, w, k, L, fzm, fzp, lob, Ab);
+    const double lot = lvl_up<LP>(lob, k), At = lvl_up<LP>(Ab, k);
+    su = (s * r_o - dt * (r.hlo * invA + (lot - lob) * rdzw)) / r_n;
+    r.smax = fmax(r.smax, su);
+    r.smin = fmin(r.smin, su);
+    const double pin_t = dt * (r.pin * invA + (fmax(Ab, 0.0) - fmin(At, 0.0)) * rdzw);
+    const double pout_t = dt * (r.pout * invA + (fmax(At, 0.0) - fmin(Ab, 0.0)) * rdzw);
+    const double qin = (r.smax - su) * r_n, qout = (su - r.smin) * r_n;
+    Rp = pin_t > 0.0 ? fmin(1.0, qin / pin_t) : 0.0;
+    Rm = pout_t > 0.0 ? fmin(1.0, qout / pout_t) : 0.0;
 }
 
 template <int LP, bool SELF>
 __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
-    int c, isc;
-    tr_slot<LP>(S, KC, c, isc);
+    int c, p;
+    tr_slot<LP>(S, KC, c, p);
     const int L = S.L, k = (int)(threadIdx.x % LP);
     if (c >= S.nCO) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
@@ -138,60 +208,75 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double *so = fd(S, F_scalars_old), *ru = fd(S, F_ruAvg);
     const double* Ah = fd(S, X_Ah);
-    const double s = colk(so, c * NSC + isc);
+    double sa, sb;
+    ld2<LP>(so, col8(c, p), col8(c, p + 1), k, sa, sb);
     const double w = colk(fd(S, F_wwAvg), c), r_o = colk(fd(S, F_rho_zz_old_split), c), r_n = colk(fd(S, F_rho_zz), c);
-    double u_[NF], x1_[NF], x2_[NF], A_[NF];
+    double u_[NF], x1a[NF], x2a[NF], x1b[NF], x2b[NF], Aa[NF], Ab[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         u_[i] = colk(ru, t.e[i]);
-        A_[i] = Ah[tr_at<LP>(t.e[i], isc, k)];
+        ld2<LP>(Ah, col8(t.e[i], p), col8(t.e[i], p + 1), k, Aa[i], Ab[i]);
         if constexpr (SELF) {
-            const double xo = colk(so, t.oth[i] * NSC + isc);
-            x1_[i] = t.s1[i] ? s : xo;
-            x2_[i] = t.s1[i] ? xo : s;
+            double xa, xb;
+            ld2<LP>(so, col8(t.oth[i], p), col8(t.oth[i], p + 1), k, xa, xb);
+            x1a[i] = t.s1[i] ? sa : xa;
+            x2a[i] = t.s1[i] ? xa : sa;
+            x1b[i] = t.s1[i] ? sb : xb;
+            x2b[i] = t.s1[i] ? xb : sb;
         } else {
-            x1_[i] = colk(so, t.c1[i] * NSC + isc);
-            x2_[i] = colk(so, t.c2[i] * NSC + isc);
+            ld2<LP>(so, col8(t.c1[i], p), col8(t.c1[i], p + 1), k, x1a[i], x1b[i]);
+            ld2<LP>(so, col8(t.c2[i], p), col8(t.c2[i], p + 1), k, x2a[i], x2b[i]);
         }
     }
-    double hlo = 0.0, pin = 0.0, pout = 0.0, smax = s, smin = s;
+    TrAcc ra, rb;
+    ra.smax = ra.smin = sa;
+    rb.smax = rb.smin = sb;
 #pragma unroll
-    for (int i = 0; i < NF; i++)
-        tr_bound_slot<LP>(i < ne, t.s1[i], t.dv[i], u_[i], x1_[i], x2_[i], A_[i], hlo, pin, pout, smax, smin);
+    for (int i = 0; i < NF; i++) {
+        tr_bound_slot(i < ne, t.s1[i], t.dv[i], u_[i], x1a[i], x2a[i], Aa[i], ra);
+        tr_bound_slot(i < ne, t.s1[i], t.dv[i], u_[i], x1b[i], x2b[i], Ab[i], rb);
+    }
     for (int i = NF; i < ne; i++) {  // cells with more than NF edges
         const size_t r = (size_t)c * 10 + i;
         const int e = fi(S, F_edgesOnCell)[r], c1 = fi(S, X_ce_c1)[r], c2 = fi(S, X_ce_c2)[r];
-        tr_bound_slot<LP>(true, fi(S, X_ce_s1)[r], fd(S, X_ce_dv)[r], colk(ru, e), colk(so, c1 * NSC + isc),
-                          colk(so, c2 * NSC + isc), Ah[tr_at<LP>(e, isc, k)], hlo, pin, pout, smax, smin);
+        const int s1f = fi(S, X_ce_s1)[r];
+        const double dv = fd(S, X_ce_dv)[r], u = colk(ru, e);
+        double y1a, y1b, y2a, y2b, Ba, Bb;
+        ld2<LP>(so, col8(c1, p), col8(c1, p + 1), k, y1a, y1b);
+        ld2<LP>(so, col8(c2, p), col8(c2, p + 1), k, y2a, y2b);
+        ld2<LP>(Ah, col8(e, p), col8(e, p + 1), k, Ba, Bb);
+        tr_bound_slot(true, s1f, dv, u, y1a, y2a, Ba, ra);
+        tr_bound_slot(true, s1f, dv, u, y1b, y2b, Bb, rb);
     }
-    const double sm1 = lvl_dn<LP>(s, k), sp1 = lvl_up<LP>(s, k);
-    smax = k > 0 ? fmax(smax, sm1) : smax;
-    smin = k > 0 ? fmin(smin, sm1) : smin;
-    smax = k < L - 1 ? fmax(smax, sp1) : smax;
-    smin = k < L - 1 ? fmin(smin, sp1) : smin;
-    double lob, Ab;
-    tr_vflux<LP>(s, w, k, L, fzm, fzp, lob, Ab);
-    const double lot = lvl_up<LP>(lob, k), At = lvl_up<LP>(Ab, k);
-    const double su = (s * r_o - dt * (hlo * invA + (lot - lob) * rdzw)) / r_n;
-    smax = fmax(smax, su);
-    smin = fmin(smin, su);
-    const double pin_t = dt * (pin * invA + (fmax(Ab, 0.0) - fmin(At, 0.0)) * rdzw);
-    const double pout_t = dt * (pout * invA + (fmax(At, 0.0) - fmin(Ab, 0.0)) * rdzw);
-    const double qin = (smax - su) * r_n, qout = (su - smin) * r_n;
-    const double Rp = pin_t > 0.0 ? fmin(1.0, qin / pin_t) : 0.0;
-    const double Rm = pout_t > 0.0 ? fmin(1.0, qout / pout_t) : 0.0;
-    if (k < L || k > L) {
-        const size_t o = tr_at<LP>(c, isc, k);
-        fw(S, X_Rp)[o] = PADW(Rp);
-        fw(S, X_Rm)[o] = PADW(Rm);
-        fw(S, X_su)[o] = PADW(su);
-    }
+    double Rpa, Rma, sua, Rpb, Rmb, sub;
+    tr_bound_fin<LP>(ra, sa, w, r_o, r_n, invA, rdzw, fzm, fzp, dt, k, L, Rpa, Rma, sua);
+    tr_bound_fin<LP>(rb, sb, w, r_o, r_n, invA, rdzw, fzm, fzp, dt, k, L, Rpb, Rmb, sub);
+    // level L and the padding levels of the scratch are never read
+    st2<LP>(fw(S, X_Rp), col8(c, p), col8(c, p + 1), k, Rpa, Rpb);
+    st2<LP>(fw(S, X_Rm), col8(c, p), col8(c, p + 1), k, Rma, Rmb);
+    st2<LP>(fw(S, X_su), col8(c, p), col8(c, p + 1), k, sua, sub);
 }
 
+// the limited update of one scalar
 template <int LP>
+__device__ __forceinline__ double tr_update_fin(double hc, double s, double w, double su, double rp, double rm,
+                                                double r_n, double invA, double rdzw, double fzm, double fzp,
+                                                double dt, int k, int L) {
+    double lo, A;
+    tr_vflux<LP>(s, w, k, L, fzm, fzp, lo, A);
+    const double rp_b = lvl_dn<LP>(rp, k), rm_b = lvl_dn<LP>(rm, k);
+    const double fcb = (k >= 1 && k <= L - 1) ? (A >= 0.0 ? fmin(rm_b, rp) : fmin(rp_b, rm)) * A : 0.0;
+    const double fct = lvl_up<LP>(fcb, k);
+    return su - dt * (hc * invA + (fct - fcb) * rdzw) / r_n;
+}
+__device__ __forceinline__ double tr_limited(double A, double m1, double p2, double p1, double m2) {
+    return (A >= 0.0 ? fmin(m1, p2) : fmin(p1, m2)) * A;
+}
+
+template <int LP, bool SELF>
 __global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
-    int c, isc;
-    tr_slot<LP>(S, KC, c, isc);
+    int c, p;
+    tr_slot<LP>(S, KC, c, p);
     const int L = S.L, k = (int)(threadIdx.x % LP);
     if (c >= S.nCO) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
@@ -200,54 +285,74 @@ __global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
     const double invA = fd(S, F_invAreaCell)[c];
     const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double *Ah = fd(S, X_Ah), *Rp = fd(S, X_Rp), *Rm = fd(S, X_Rm);
-    const size_t o = tr_at<LP>(c, isc, k);
-    const double s = colk(fd(S, F_scalars_old), c * NSC + isc);
+    const size_t ca = col8(c, p), cb = col8(c, p + 1);
+    double sa, sb, sua, sub, rpa, rpb, rma, rmb;
+    ld2<LP>(fd(S, F_scalars_old), ca, cb, k, sa, sb);
+    ld2<LP>(fd(S, X_su), ca, cb, k, sua, sub);
+    ld2<LP>(Rp, ca, cb, k, rpa, rpb);
+    ld2<LP>(Rm, ca, cb, k, rma, rmb);
     const double w = colk(fd(S, F_wwAvg), c), r_n = colk(fd(S, F_rho_zz), c);
-    const double su = fd(S, X_su)[o], rp = Rp[o], rm = Rm[o];
-    double A_[NF], p1_[NF], m1_[NF], p2_[NF], m2_[NF];
+    double Aa[NF], Ab[NF], p1a[NF], p1b[NF], m1a[NF], m1b[NF], p2a[NF], p2b[NF], m2a[NF], m2b[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        A_[i] = Ah[tr_at<LP>(t.e[i], isc, k)];
-        p1_[i] = Rp[tr_at<LP>(t.c1[i], isc, k)];
-        m1_[i] = Rm[tr_at<LP>(t.c1[i], isc, k)];
-        p2_[i] = Rp[tr_at<LP>(t.c2[i], isc, k)];
-        m2_[i] = Rm[tr_at<LP>(t.c2[i], isc, k)];
+        ld2<LP>(Ah, col8(t.e[i], p), col8(t.e[i], p + 1), k, Aa[i], Ab[i]);
+        if constexpr (SELF) {  // the cell is one of the two: gather only the other
+            double qa, qb, na, nb;
+            ld2<LP>(Rp, col8(t.oth[i], p), col8(t.oth[i], p + 1), k, qa, qb);
+            ld2<LP>(Rm, col8(t.oth[i], p), col8(t.oth[i], p + 1), k, na, nb);
+            const bool f = t.s1[i];
+            p1a[i] = f ? rpa : qa, p1b[i] = f ? rpb : qb, m1a[i] = f ? rma : na, m1b[i] = f ? rmb : nb;
+            p2a[i] = f ? qa : rpa, p2b[i] = f ? qb : rpb, m2a[i] = f ? na : rma, m2b[i] = f ? nb : rmb;
+        } else {
+            ld2<LP>(Rp, col8(t.c1[i], p), col8(t.c1[i], p + 1), k, p1a[i], p1b[i]);
+            ld2<LP>(Rm, col8(t.c1[i], p), col8(t.c1[i], p + 1), k, m1a[i], m1b[i]);
+            ld2<LP>(Rp, col8(t.c2[i], p), col8(t.c2[i], p + 1), k, p2a[i], p2b[i]);
+            ld2<LP>(Rm, col8(t.c2[i], p), col8(t.c2[i], p + 1), k, m2a[i], m2b[i]);
+        }
     }
-    double hc = 0.0;
+    double hca = 0.0, hcb = 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         const double sg = t.s1[i] ? 1.0 : -1.0;
-        const double C = A_[i] >= 0.0 ? fmin(m1_[i], p2_[i]) : fmin(p1_[i], m2_[i]);
-        hc = add_if(i < ne, hc, sg * (C * A_[i]));
+        hca = add_if(i < ne, hca, sg * tr_limited(Aa[i], m1a[i], p2a[i], p1a[i], m2a[i]));
+        hcb = add_if(i < ne, hcb, sg * tr_limited(Ab[i], m1b[i], p2b[i], p1b[i], m2b[i]));
     }
     for (int i = NF; i < ne; i++) {
         const size_t r = (size_t)c * 10 + i;
         const int e = fi(S, F_edgesOnCell)[r], c1 = fi(S, X_ce_c1)[r], c2 = fi(S, X_ce_c2)[r];
         const double sg = fi(S, X_ce_s1)[r] ? 1.0 : -1.0;
-        const double A = Ah[tr_at<LP>(e, isc, k)];
-        const double C = A >= 0.0 ? fmin(Rm[tr_at<LP>(c1, isc, k)], Rp[tr_at<LP>(c2, isc, k)])
-                                  : fmin(Rp[tr_at<LP>(c1, isc, k)], Rm[tr_at<LP>(c2, isc, k)]);
-        hc = hc + sg * (C * A);
+        double Ba, Bb, q1a, q1b, n1a, n1b, q2a, q2b, n2a, n2b;
+        ld2<LP>(Ah, col8(e, p), col8(e, p + 1), k, Ba, Bb);
+        ld2<LP>(Rp, col8(c1, p), col8(c1, p + 1), k, q1a, q1b);
+        ld2<LP>(Rm, col8(c1, p), col8(c1, p + 1), k, n1a, n1b);
+        ld2<LP>(Rp, col8(c2, p), col8(c2, p + 1), k, q2a, q2b);
+        ld2<LP>(Rm, col8(c2, p), col8(c2, p + 1), k, n2a, n2b);
+        hca = hca + sg * tr_limited(Ba, n1a, q2a, q1a, n2a);
+        hcb = hcb + sg * tr_limited(Bb, n1b, q2b, q1b, n2b);
     }
-    double lo, A;
-    tr_vflux<LP>(s, w, k, L, fzm, fzp, lo, A);
-    const double rp_b = lvl_dn<LP>(rp, k), rm_b = lvl_dn<LP>(rm, k);
-    const double fcb = (k >= 1 && k <= L - 1) ? (A >= 0.0 ? fmin(rm_b, rp) : fmin(rp_b, rm)) * A : 0.0;
-    const double fct = lvl_up<LP>(fcb, k);
-    const double sn = su - dt * (hc * invA + (fct - fcb) * rdzw) / r_n;
-    if (k < L) colk(fw(S, F_scalars), c * NSC + isc) = sn;
+    const double na = tr_update_fin<LP>(hca, sa, w, sua, rpa, rma, r_n, invA, rdzw, fzm, fzp, dt, k, L);
+    const double nb = tr_update_fin<LP>(hcb, sb, w, sub, rpb, rmb, r_n, invA, rdzw, fzm, fzp, dt, k, L);
+    if (k < L) {  // level L of scalars keeps its value (the oracle writes levels 0..L-1)
+        double* sn = fw(S, F_scalars);
+        sn[ca * LP + lpos(LP, k)] = na;
+        sn[cb * LP + lpos(LP, k)] = nb;
+    }
 }
 
 template <int LP>
 static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
-    constexpr int COLS = 256 / LP;
-    const long ne = (long)(S.nEO - S.lo[KE]) * NSC, nc = (long)(S.nCO - S.lo[KC]) * NSC;
+    constexpr int COLS = 256 / LP;  // column slots per block; a slot = one entity, two scalars
+    const long ne = (long)(S.nEO - S.lo[KE]) * (NSC / 2), nc = (long)(S.nCO - S.lo[KC]) * (NSC / 2);
     const int nEB = (int)((ne + COLS - 1) / COLS), nCB = (int)((nc + COLS - 1) / COLS);
     if (nEB > 0) k_tr_edge<LP><<<nEB, 256, 0, st>>>(S);
     if (nCB > 0) {
-        if (S.selfc) k_tr_bounds<LP, true><<<nCB, 256, 0, st>>>(S, dt);
-        else k_tr_bounds<LP, false><<<nCB, 256, 0, st>>>(S, dt);
-        k_tr_update<LP><<<nCB, 256, 0, st>>>(S, dt);
+        if (S.selfc) {
+            k_tr_bounds<LP, true><<<nCB, 256, 0, st>>>(S, dt);
+            k_tr_update<LP, true><<<nCB, 256, 0, st>>>(S, dt);
+        } else {
+            k_tr_bounds<LP, false><<<nCB, 256, 0, st>>>(S, dt);
+            k_tr_update<LP, false><<<nCB, 256, 0, st>>>(S, dt);
+        }
     }
     return hipGetLastError();
 }

@@ -38,6 +38,8 @@ KERNEL_TASK = [
     (r"k_div_damp", "atm_divergence_damping_3d"),
     (r"k_solve_", "atm_compute_solve_diagnostics"),
     (r"k_finish_", "atm_rk_dynamics_substep_finish"),
+    (r"k_recover_", "atm_recover_large_step_variables_work"),
+    (r"k_tr_", "atm_advance_scalars_mono"),
 ]
 # task launches per RK3 step (schedule 1, x1.163842: 7 acoustic substeps)
 LAUNCHES = {"atm_rk_integration_setup": 1, "atm_compute_moist_coefficients": 1, "atm_compute_vert_imp_coefs": 2,
@@ -45,6 +47,10 @@ LAUNCHES = {"atm_rk_integration_setup": 1, "atm_compute_moist_coefficients": 1, 
             "atm_set_smlstep_pert_variables_work": 3, "atm_advance_acoustic_step_work": 7,
             "atm_divergence_damping_3d": 7, "atm_compute_solve_diagnostics": 3,
             "atm_rk_dynamics_substep_finish": 1}
+# bench.py --physics / --transport (the MPAS vertical solver: 4 acoustic substeps, recover
+# after every stage, the scalar transport once per step)
+LAUNCHES_PHYSICS = dict(LAUNCHES, atm_advance_acoustic_step_work=4, atm_divergence_damping_3d=4,
+                        atm_recover_large_step_variables_work=3, atm_advance_scalars_mono=1)
 
 
 def task_of(name):
@@ -84,7 +90,11 @@ def main():
     ap.add_argument("--write")
     ap.add_argument("--dims", nargs=4, type=int, required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--physics", action="store_true", help="the run was bench.py --physics or --transport")
     a = ap.parse_args()
+    global LAUNCHES
+    if a.physics:
+        LAUNCHES = LAUNCHES_PHYSICS
     nC, nE, nV, L = a.dims
     out = {"dims": a.dims, "kernels": {}, "tasks": {}}
     tasks = defaultdict(lambda: {"kernels": [], "time_s": 0.0, "fetch_B": 0.0, "write_B": 0.0})
@@ -95,7 +105,7 @@ def main():
         for k, (calls, t) in tr.items():
             out["kernels"][k] = {"calls": calls, "avg_us": round(t / calls * 1e6, 2)}
             task = task_of(k)
-            if task:
+            if task and task in LAUNCHES:
                 tasks[task]["kernels"].append(k)
                 tasks[task]["time_s"] += t
     fetch, nf = read_counter(a.fetch, "FETCH_SIZE") if a.fetch else ({}, {})
@@ -118,7 +128,7 @@ def main():
         if k in write:
             d["write_bytes_per_launch"] = wfac * write[k] / nw[k] * 1024.0
         task = task_of(k)
-        if task and pmc_steps:
+        if task and pmc_steps and task in LAUNCHES:
             tasks[task]["fetch_B"] += 2.0 * fetch.get(k, 0.0) * 1024.0
             tasks[task]["write_B"] += wfac * write.get(k, 0.0) * 1024.0
     for task, v in tasks.items():
