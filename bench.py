@@ -149,7 +149,7 @@ def main():
     ap.add_argument("--physics", action="store_true",
                     help="the MPAS vertical solver (option physics = 1: 4 acoustic substeps + recover per step)")
     ap.add_argument("--transport", action="store_true",
-                    help="physics = 1 plus the monotonic transport of the 8 scalars in every step (single GPU)")
+                    help="physics = 1 plus the monotonic transport of the 8 scalars in every step")
     args = ap.parse_args()
     if args.transport:
         args.physics = True

@@ -64,7 +64,7 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * with Q24 fixed, and in mpas_atm_srk3 number_sub_steps acoustic substeps (Q5) followed by
  * recover (Q7); every other task as the reference.
  * Default 0: the reference's semantics.
- * "transport" = 1 (needs "physics" = 1; single subdomain) makes mpas_atm_srk3 copy scalars
+ * "transport" = 1 (needs "physics" = 1) makes mpas_atm_srk3 copy scalars
  * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
  * recover, before atm_rk_dynamics_substep_finish.  Default 0. */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
@@ -135,8 +135,8 @@ int mpas_atm_compute_output_diagnostics(mpas_ctx* ctx);
  *       mass fluxes ruAvg (edges) and wwAvg (interfaces) from density rho_zz_old_split to
  *       rho_zz with 3rd-order fluxes (adv_coefs, adv_coefs_3rd; flux3 vertically, coef 0.25)
  *       limited so that no new extrema appear; result in scalars (levels 0..nVertLevels-1).
- *       Statement order: oracle/mpas_oracle.c ora_mpas_advance_scalars_mono.  MPAS_ENOTSUP
- *       on a decomposed context. */
+ *       Statement order: oracle/mpas_oracle.c ora_mpas_advance_scalars_mono.  Decomposed
+ *       contexts exchange scalars_old and the scratch on their ghosts like every task. */
 int mpas_atm_advance_scalars_mono(mpas_ctx* ctx, double dt);
 /* rk_timestep.rg:29 summarize_timestep(cr, er, config_print_detailed_minmax_vel,
  *       config_print_global_minmax_vel, config_print_global_minmax_sca): the values the

@@ -342,22 +342,37 @@ __global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
 template <int LP>
 static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
     constexpr int COLS = 256 / LP;  // column slots per block; a slot = one entity, two scalars
-    const long ne = (long)(S.nEO - S.lo[KE]) * (NSC / 2), nc = (long)(S.nCO - S.lo[KC]) * (NSC / 2);
-    const int nEB = (int)((ne + COLS - 1) / COLS), nCB = (int)((nc + COLS - 1) / COLS);
-    if (nEB > 0) k_tr_edge<LP><<<nEB, 256, 0, st>>>(S);
-    if (nCB > 0) {
-        if (S.selfc) {
-            k_tr_bounds<LP, true><<<nCB, 256, 0, st>>>(S, dt);
-            k_tr_update<LP, true><<<nCB, 256, 0, st>>>(S, dt);
-        } else {
-            k_tr_bounds<LP, false><<<nCB, 256, 0, st>>>(S, dt);
-            k_tr_update<LP, false><<<nCB, 256, 0, st>>>(S, dt);
-        }
-    }
+    auto blocks = [](const DevState& X, int kind) {
+        const int end = kind == KC ? X.nCO : X.nEO;
+        const long n = (long)(end - X.lo[kind]) * (NSC / 2);
+        return n > 0 ? (int)((n + COLS - 1) / COLS) : 0;
+    };
+    // decomposed meshes: the gathered fields are exchanged first (HALO_RUN: scalars_old
+    // on two rings for the adv lists, A on the ghost edges of owned cells, R+/R- on the
+    // neighbour cells); the x8 fields move as 8 columns per entity (mpas_halo.hip)
+    auto ke = [&](const DevState& X) {
+        const int nb = blocks(X, KE);
+        if (nb) k_tr_edge<LP><<<nb, 256, 0, st>>>(X);
+    };
+    HALO_RUN(S, st, ke, F_scalars_old, F_ruAvg);
+    HALO_WROTE(S, X_Ah);
+    auto kb = [&](const DevState& X) {
+        const int nb = blocks(X, KC);
+        if (nb && X.selfc) k_tr_bounds<LP, true><<<nb, 256, 0, st>>>(X, dt);
+        else if (nb) k_tr_bounds<LP, false><<<nb, 256, 0, st>>>(X, dt);
+    };
+    HALO_RUN(S, st, kb, F_scalars_old, F_ruAvg, X_Ah);
+    HALO_WROTE(S, X_Rp, X_Rm, X_su);
+    auto ku = [&](const DevState& X) {
+        const int nb = blocks(X, KC);
+        if (nb && X.selfc) k_tr_update<LP, true><<<nb, 256, 0, st>>>(X, dt);
+        else if (nb) k_tr_update<LP, false><<<nb, 256, 0, st>>>(X, dt);
+    };
+    HALO_RUN(S, st, ku, X_Ah, X_Rp, X_Rm);
+    HALO_WROTE(S, F_scalars);
     return hipGetLastError();
 }
 hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt) {
-    if (S.halo) return hipErrorNotSupported;  // single subdomain only
     MPAS_LP_DISPATCH(S.LP, transport_lp, S, st, dt);
 }
 

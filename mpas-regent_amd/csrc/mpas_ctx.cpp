@@ -227,10 +227,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     const DevState& S = c->S;
     hipStream_t st = c->stream;
     if (c->transport) {
-        if (c->halo) throw Fail{MPAS_ENOTSUP, "transport: decomposed meshes are not supported (single subdomain only)"};
-        // the time level the transport starts from (MPAS-A scalars(time level 1))
+        // the time level the transport starts from (MPAS-A scalars(time level 1)); the
+        // copy carries the ghosts of scalars, fresh or not, so scalars_old is as stale
         run_task(c, "scalars_save", [&] {
-            return hipMemcpyAsync(S.f[F_scalars_old], S.f[F_scalars], dev_bytes(c, F_scalars), hipMemcpyDeviceToDevice, st);
+            hipError_t e = hipMemcpyAsync(S.f[F_scalars_old], S.f[F_scalars], dev_bytes(c, F_scalars),
+                                          hipMemcpyDeviceToDevice, st);
+            if (S.halo && S.halo->stale[F_scalars]) S.halo->wrote({F_scalars_old});
+            return e;
         });
     }
     run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
@@ -726,10 +729,6 @@ int mpas_reconstruct_2d(mpas_ctx* c, int includeHalos, int on_a_sphere) {
 }
 int mpas_atm_advance_scalars_mono(mpas_ctx* c, double dt) {
     if (!c) return MPAS_EINVAL;
-    if (c->halo) {
-        c->err = "atm_advance_scalars_mono: decomposed meshes are not supported (single subdomain only)";
-        return MPAS_ENOTSUP;
-    }
     MPAS_TASK("atm_advance_scalars_mono", launch_advance_scalars_mono(c->S, c->stream, dt));
 }
 int mpas_atm_compute_output_diagnostics(mpas_ctx* c) {

@@ -15,7 +15,9 @@ namespace mpas {
 constexpr int kMaxSeg = 128;
 struct SegList {
     double* f[kMaxSeg];      // field base (LP doubles per column)
-    const int* ids[kMaxSeg];  // local column ids
+    const int* ids[kMaxSeg];  // local entity ids
+    int W[kMaxSeg], comp[kMaxSeg];  // columns per entity and the one this segment moves
+                                    // (x8 transport fields: column = entity * W + comp)
     long start[kMaxSeg + 1];  // first packed column of each segment
     int nseg, LP;
 };
@@ -30,14 +32,14 @@ __global__ __launch_bounds__(256) void k_halo_copy(SegList sl, double* buf) {
     int s = 0;
     while (col >= sl.start[s + 1]) s++;
     const long j = col - sl.start[s];
-    double* f = sl.f[s] + (size_t)sl.ids[s][j] * sl.LP + k;
+    double* f = sl.f[s] + ((size_t)sl.ids[s][j] * sl.W[s] + sl.comp[s]) * sl.LP + k;
     if (PACK) buf[t] = *f;
     else *f = buf[t];
 }
 
 static int kind_of_field(int f) {
     switch (kFields[f].kind) {
-        case K_C3: return HK_CELL;
+        case K_C3: case K_C3V: return HK_CELL;
         case K_E3: return HK_EDGE;
         case K_V3: return HK_VERTEX;
         default: return -1;
@@ -66,7 +68,7 @@ hipError_t Halo::reserve(int LP) {
     long fk[3] = {0, 0, 0};
     for (int f = 0; f < X_COUNT; f++) {
         int k = kind_of_field(f);
-        if (k >= 0) fk[k]++;
+        if (k >= 0) fk[k] += kFields[f].width;  // columns per entity
     }
     long s = 0, r = 0;
     for (int k = 0; k < 3; k++)
@@ -272,8 +274,10 @@ static void plan_regions(const Halo& h, const std::vector<int>& fields, std::vec
                 reg.push_back({p.peer, 0, 0, 0, 0});
                 r = &reg.back();
             }
-            r->scols += (long)p.nsend * (long)byk[k].size();
-            r->rcols += (long)p.nrecv * (long)byk[k].size();
+            long w = 0;  // columns per entity of the kind's fields
+            for (int f : byk[k]) w += kFields[f].width;
+            r->scols += (long)p.nsend * w;
+            r->rcols += (long)p.nrecv * w;
         }
     long so = 0, ro = 0;
     for (auto& r : reg) {
@@ -301,17 +305,20 @@ static hipError_t run_copy(const DevState& S, hipStream_t st, const Halo& h, con
             if (!p) continue;
             const int n = pack ? p->nsend : p->nrecv;
             if (n == 0) continue;
-            for (int f : byk[k]) {
-                if (sl.nseg == kMaxSeg) {
-                const_cast<Halo&>(h).err = "too many halo segments";
-                return hipErrorInvalidValue;
-            }
-                sl.f[sl.nseg] = (double*)S.f[f];
-                sl.ids[sl.nseg] = pack ? p->d_send : p->d_recv;
-                sl.start[sl.nseg] = col;
-                col += n;
-                sl.nseg++;
-            }
+            for (int f : byk[k])
+                for (int comp = 0; comp < kFields[f].width; comp++) {
+                    if (sl.nseg == kMaxSeg) {
+                        const_cast<Halo&>(h).err = "too many halo segments";
+                        return hipErrorInvalidValue;
+                    }
+                    sl.f[sl.nseg] = (double*)S.f[f];
+                    sl.ids[sl.nseg] = pack ? p->d_send : p->d_recv;
+                    sl.W[sl.nseg] = kFields[f].width;
+                    sl.comp[sl.nseg] = comp;
+                    sl.start[sl.nseg] = col;
+                    col += n;
+                    sl.nseg++;
+                }
         }
         if (sl.nseg == 0) continue;
         sl.start[sl.nseg] = col;

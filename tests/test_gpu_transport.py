@@ -99,3 +99,39 @@ def test_transport_option_rules(x1_2562):
         assert ctx.get_option("transport") == 1
         ctx.set_option("physics", 0)
         assert ctx.get_option("transport") == 0
+
+
+def _with(opts, fn):
+    def g(c):
+        for k, v in opts.items():
+            c.set_option(k, v)
+        fn(c)
+    return g
+
+
+@pytest.mark.parametrize("nparts", [2, 3])
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_transport_decomposed_equals_single(x1_2562, nparts, overlap):
+    """N subdomains (loopback halo: the x8 fields move as 8 columns per entity) give the
+    single-context result bit for bit"""
+    from test_gpu_decomp import run_decomposed, run_single
+    st, _ = transport_state(x1_2562, 56, DT)
+    fn = _with({"physics": 1}, lambda c: T.atm_advance_scalars_mono(c, DT))
+    ref = run_single(st, fn, 1)
+    got, stats = run_decomposed(st, nparts, fn, 1, overlap=overlap)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+    assert all(s[0] > 0 for s in stats)
+
+
+@pytest.mark.parametrize("L", [5, 56])
+def test_srk3_transport_decomposed(x1_2562, L):
+    from mpasdyn import mesh as M
+    from test_gpu_decomp import run_decomposed, run_single
+    st = make_state(M.zero_based(x1_2562), L, "random")
+    fn = _with({"physics": 1, "transport": 1}, lambda c: T.atm_srk3(c, 720.0, 1))
+    for exact in (1, 0):
+        ref = run_single(st, fn, exact)
+        got, _ = run_decomposed(st, 3, fn, exact)
+        bad = compare_states(got, ref, rtol=0.0)
+        assert not bad, f"exact={exact}: {bad[:6]}"
