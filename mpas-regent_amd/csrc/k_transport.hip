@@ -36,11 +36,23 @@ __device__ __forceinline__ double tr_flux3(double q_im2, double q_im1, double q_
 // entity and scalar pair of this lane's column slot: a wavefront computes two scalars,
 // 2p and 2p+1, of one entity (their columns are adjacent, so one 16-B lane load fetches
 // both: ld2 below)
+// Slot order (option "trorder"): 0 entity-major (the 4 pairs of an entity in adjacent
+// slots: they share its connectivity and mass-flux loads), 1 pair-major (all entities for
+// pair 0, then pair 1, ...: a quarter of the per-entity footprint in L2, so the entities
+// in flight span 4x the mesh and share more neighbour columns)
 template <int LP>
 __device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, int& p) {
     const int slot = col_of<LP>(xcd_block(S.xcd));
-    ent = (slot >> 2) + S.lo[kind];
-    p = (slot & 3) * 2;
+    if (S.tro) {
+        const int n = (kind == KC ? S.nCO : S.nEO) - S.lo[kind];
+        const int q = slot / n;
+        ent = slot - q * n + S.lo[kind];
+        p = q * 2;
+        if (q >= NSC / 2) ent = 0x7fffffff;  // past the grid's last slot (caller returns)
+    } else {
+        ent = (slot >> 2) + S.lo[kind];
+        p = (slot & 3) * 2;
+    }
 }
 
 // level k of columns ia and ib of field f (64-bit column ids: the edge scratch exceeds

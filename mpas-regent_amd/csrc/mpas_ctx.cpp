@@ -395,6 +395,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             if (value != 0 && value != 1) throw Fail{MPAS_EINVAL, "physics must be 0 (reference) or 1 (MPAS vertical solver)"};
             c->S.physics = (int)value;
             if (!value) c->transport = 0;
+        } else if (name && std::strcmp(name, "trorder") == 0) {
+            c->S.tro = value ? 1 : 0;
         } else if (name && std::strcmp(name, "transport") == 0) {
             if (value && !c->S.physics) throw Fail{MPAS_EINVAL, "transport needs physics = 1 (it reads the recovered ruAvg, wwAvg, rho_zz)"};
             c->transport = value ? 1 : 0;
@@ -417,6 +419,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "vcmix") == 0) *value = c->S.vcmix;
         else if (name && std::strcmp(name, "physics") == 0) *value = c->S.physics;
         else if (name && std::strcmp(name, "transport") == 0) *value = c->transport;
+        else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "selfc") == 0) {

@@ -92,6 +92,7 @@ struct DevState {
                         // [lo, nXO); 0 except for the boundary launch of a halo overlap
     int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
     int vcmix;  // 1: the vertex and cell blocks of mixed grids interleaved in proportion (vc_block)
+    int tro;      // transport slot order (k_transport.hip tr_slot): 0 entity-major, 1 pair-major
     int physics;  // 0: the reference's vertical solver (quirks Q16-Q21), 1: the MPAS form (option "physics")
     int xcd;  // block order: 0 dispatcher, 1 one contiguous eighth per XCD, G > 1 runs of G
               // blocks per XCD in windows of 8G (default 64)

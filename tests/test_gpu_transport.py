@@ -22,12 +22,13 @@ RTOL_POW = 1e-14
 POW_FIELDS = {"exner", "pressure_p"}
 
 
-def gpu(st, fn, exact=1, physics=1, transport=0):
+def gpu(st, fn, exact=1, physics=1, transport=0, trorder=0):
     got = st.copy()
     with lib.Context(*st.dims()) as ctx:
         ctx.set_option("exact", exact)
         ctx.set_option("physics", physics)
         ctx.set_option("transport", transport)
+        ctx.set_option("trorder", trorder)
         ctx.upload(st)
         fn(ctx)
         ctx.sync()
@@ -49,6 +50,17 @@ def test_transport_task(x1_2562, L, const):
     m_old = np.einsum("ck,cki->i", st["rho_zz_old_split"][:nC, :L] * vol, st["scalars_old"][:nC, :L])
     m_new = np.einsum("ck,cki->i", got["rho_zz"][:nC, :L] * vol, got["scalars"][:nC, :L])
     assert np.allclose(m_new, m_old, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("L", [5, 56])
+def test_transport_task_pair_major(x1_2562, L):
+    """option trorder = 1 (pair-major slot order: speed only)"""
+    st, _ = transport_state(x1_2562, L, DT)
+    ref = st.copy()
+    O.Oracle(ref).mpas_advance_scalars_mono(DT)
+    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT), trorder=1)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
 
 
 @pytest.mark.parametrize("L", [1, 2, 63])
