@@ -1,0 +1,49 @@
+"""The JW initial state on the GPU: RK3 steps from it match the oracle bit for bit (exact
+mode), and the end-to-end driver (mpasdyn/driver.py, main.rg's loop) writes
+timestep_output.nc."""
+import numpy as np
+import pytest
+
+import oracle as O
+from helpers import compare_states
+from mpasdyn import jw, lib
+from mpasdyn import mesh as M
+from mpasdyn import tasks as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("L", [26, 56])
+def test_jw_steps_match_oracle(x1_2562, L):
+    st = jw.jw_state(M.zero_based(x1_2562), L)
+    ref = st.copy()
+    o = O.Oracle(ref)
+    for _ in range(2):
+        o.atm_srk3(720.0, 1)
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.set_option("exact", 1)
+        ctx.upload(st)
+        for _ in range(2):
+            T.atm_srk3(ctx, 720.0, 1)
+        ctx.sync()
+        ctx.download(got)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
+def test_driver_end_to_end(x1_2562, tmp_path):
+    from scipy.io import netcdf_file
+    from mpasdyn import driver
+    out = str(tmp_path / "timestep_output.nc")
+    lines = []
+    st = driver.run(x1_2562, 26, 3, 720.0, out=out, log=lines.append)
+    assert len(lines) == 3
+    with netcdf_file(out, "r", mmap=False) as f:
+        sp = f.variables["surface_pressure"][:].copy()
+        u = f.variables["u"][:].copy()
+        rho = f.variables["rho"][:].copy()
+    assert np.allclose(sp, 1.0e5, rtol=1e-12)
+    assert np.array_equal(u, st["u"][:st.nEdges, 0])  # level 0 (the jet peaks aloft)
+    assert 34.0 < np.abs(st["u"][:st.nEdges, :26]).max() <= 35.0  # u unchanged by the steps (Q7)
+    assert np.allclose(rho, st["rho_zz"][:st.nCells, 0] * st["zz"][:st.nCells, 0], rtol=1e-15)
