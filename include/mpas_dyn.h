@@ -128,6 +128,13 @@ int mpas_reconstruct_2d(mpas_ctx* ctx, int includeHalos, int on_a_sphere);
  *       pressure = pressure_base + pressure_p on levels 0..nVertLevels-1 (theta is in the
  *       task's write set but its statement is commented out in the reference: unchanged) */
 int mpas_atm_compute_output_diagnostics(mpas_ctx* ctx);
+/* One-time tasks of atm_core_init (atm_core.rg:22-42) that run on the device:
+ * :274 atm_compute_damping_coefs(config_zd, config_xnutr, cr) (atm_core.rg:41, defaults
+ *       22000.0 and 0.2): dss of the upper damping layer */
+int mpas_atm_compute_damping_coefs(mpas_ctx* ctx, double config_zd, double config_xnutr);
+/* :651 atm_init_coupled_diagnostics(cr, er, vert_r) (atm_core.rg:31): rho_zz /= zz, ru, rw,
+ *       rho_p, rtheta_base, rtheta_p, exner, exner_base, pressure_p, pressure_base */
+int mpas_atm_init_coupled_diagnostics(mpas_ctx* ctx);
 /* Monotonic scalar transport.  Replaces no reference entry point: the
  *       reference has none (Q26 -- scalars:double[8], data_structures.rg:36, is declared and
  *       never used; the north star names the transport).  MPAS-A's atm_advance_scalars_mono

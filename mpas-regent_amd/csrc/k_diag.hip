@@ -204,6 +204,124 @@ hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, 
     MPAS_LP_DISPATCH(S.LP, recover_lp, S, st, ns, rk_step, dt);
 }
 
+// ---------------------------------------------------------------- damping coefficients
+// atm_compute_damping_coefs (dynamics_tasks.rg:274-300; atm_core_init, atm_core.rg:41):
+// dss of levels 0..L-1 from the layer's mid height; pow(x, 2.0) as x * x
+template <int LP>
+__global__ __launch_bounds__(256) void k_damping(DevState S, double zd, double xnutr, double pii) {
+    ColMap<LP> m(S, KC);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    const double zg = col_rd<LP>(fd(S, F_zgrid), c, k, L);
+    const double zg_up = lvl_up<LP>(zg, k), zt = __shfl(zg, L, LP);
+    const double md = fd(S, F_meshDensity)[c];
+    double dss = 0.0;
+    const double z = 0.5 * (zg + zg_up);
+    if (z > zd) {
+        const double sn = sin(0.5 * pii * (z - zd) / (zt - zd));
+        dss = xnutr * (sn * sn);
+        dss /= pow(md, (0.25 * 1.0));
+    }
+    if (k < L || k > L) colk(fw(S, F_dss), c) = PADW(dss);
+}
+template <int LP>
+static hipError_t damping_lp(const DevState& S, hipStream_t st, double zd, double xnutr) {
+    const int nb = col_blocks<LP>(S, KC);
+    if (nb) k_damping<LP><<<nb, 256, 0, st>>>(S, zd, xnutr, acos(-1.0));
+    HALO_WROTE(S, F_dss);
+    return hipGetLastError();
+}
+hipError_t launch_damping_coefs(const DevState& S, hipStream_t st, double zd, double xnutr) {
+    MPAS_LP_DISPATCH(S.LP, damping_lp, S, st, zd, xnutr);
+}
+
+// ---------------------------------------------------------------- init_coupled_diagnostics
+// atm_init_coupled_diagnostics (dynamics_tasks.rg:651-726; atm_core.rg:31): three phases
+// with the data flow's barriers -- rho_zz /= zz (cells), ru from u and the new rho_zz
+// (edges), then rw (the w part, minus the slope flux of ru over the cell's edges) and the
+// thermodynamic diagnostics (cells)
+template <int LP>
+__global__ __launch_bounds__(256) void k_icd_rho(DevState S) {
+    ColMap<LP> m(S, KC);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO || k >= L) return;
+    double* rz = fw(S, F_rho_zz);
+    const double zz = colk(fd(S, F_zz), c);
+    colk(rz, c) = colk(rz, c) / zz;
+}
+template <int LP>
+__global__ __launch_bounds__(256) void k_icd_ru(DevState S) {
+    ColMap<LP> m(S, KE);
+    const int L = S.L, k = m.k, e = m.ent;
+    if (e >= S.nEO || k >= L) return;
+    const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    const double* rz = fd(S, F_rho_zz);
+    const double r1 = colk(rz, cell1), r2 = colk(rz, cell2);
+    colk(fw(S, F_ru), e) = 0.5 * colk(fd(S, F_u), e) * (r1 + r2);
+}
+template <int LP>
+__global__ __launch_bounds__(256) void k_icd_cells(DevState S, double rgas_p0, double rgas, double rcv) {
+    ColMap<LP> m(S, KC);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    const int ne = fi(S, F_nEdgesOnCell)[c];
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgn = fd(S, F_edgesOnCellSign) + (size_t)c * 10;
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    const double rz = col_rd<LP>(fd(S, F_rho_zz), c, k, L), zz = col_rd<LP>(fd(S, F_zz), c, k, L);
+    const double rz_m = lvl_dn<LP>(rz, k), zz_m = lvl_dn<LP>(zz, k);
+    const double w = colk(fd(S, F_w), c);
+    const double *ru = fd(S, F_ru), *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
+    double rw = 0.0;
+    if (k > 0) rw = w * (fzp * rz_m + fzm * rz) * (fzp * zz_m + fzm * zz);
+    const double zfac = fzp * zz_m + fzm * zz;
+    for (int i = 0; i < ne; i++) {  // every lane takes part (the shuffle below)
+        const double r = colk(ru, eoc[i]);
+        const double r_m = lvl_dn<LP>(r, k);
+        const double flux = fzm * r + fzp * r_m;
+        const double z = colk(zb, c * 10 + i), z3 = colk(zb3, c * 10 + i);
+        const double t = sgn[i] * (z + copysign(1.0, flux) * z3) * flux * zfac;
+        rw = (k > 0) ? rw - t : rw;
+    }
+    if (k >= L) return;
+    colk(fw(S, F_rw), c) = rw;
+    const double rb = colk(fd(S, F_rho_base), c), tb = colk(fd(S, F_theta_base), c), tm = colk(fd(S, F_theta_m), c);
+    const double rho_p = rz - rb;
+    const double rtheta_base = tb * rb;
+    const double rtheta_p = tm * rho_p + rb * (tm - tb);
+    const double exner = pow(zz * rgas_p0 * (rtheta_p + rtheta_base), rcv);
+    const double exner_base = pow(zz * rgas_p0 * (rtheta_base), rcv);
+    colk(fw(S, F_rho_p), c) = rho_p;
+    colk(fw(S, F_rtheta_base), c) = rtheta_base;
+    colk(fw(S, F_rtheta_p), c) = rtheta_p;
+    colk(fw(S, F_exner), c) = exner;
+    colk(fw(S, F_exner_base), c) = exner_base;
+    colk(fw(S, F_pressure_p), c) = zz * rgas * (exner * rtheta_p + rtheta_base * (exner - exner_base));
+    colk(fw(S, F_pressure_base), c) = zz * rgas * exner_base * rtheta_base;
+}
+template <int LP>
+static hipError_t icd_lp(const DevState& S, hipStream_t st) {
+    const int nCB = col_blocks<LP>(S, KC);
+    if (nCB) k_icd_rho<LP><<<nCB, 256, 0, st>>>(S);
+    HALO_WROTE(S, F_rho_zz);
+    auto ke = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KE);
+        if (nb) k_icd_ru<LP><<<nb, 256, 0, st>>>(X);
+    };
+    HALO_RUN(S, st, ke, F_rho_zz);
+    HALO_WROTE(S, F_ru);
+    auto kc = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (nb) k_icd_cells<LP><<<nb, 256, 0, st>>>(X, kRgas / 100000, kRgas, kRgas / (kCp - kRgas));
+    };
+    HALO_RUN(S, st, kc, F_ru);
+    HALO_WROTE(S, F_rw, F_rho_p, F_rtheta_base, F_rtheta_p, F_exner, F_exner_base, F_pressure_p, F_pressure_base);
+    return hipGetLastError();
+}
+hipError_t launch_init_coupled_diagnostics(const DevState& S, hipStream_t st) {
+    MPAS_LP_DISPATCH(S.LP, icd_lp, S, st);
+}
+
 // ---------------------------------------------------------------- reconstruct_2d
 template <int LP>
 __global__ __launch_bounds__(256) void k_reconstruct(DevState S, int on_a_sphere) {

@@ -730,6 +730,12 @@ int mpas_reconstruct_2d(mpas_ctx* c, int includeHalos, int on_a_sphere) {
     (void)includeHalos;  // :1909-1912: the range is nCells either way
     MPAS_TASK("mpas_reconstruct_2d", launch_reconstruct_2d(c->S, c->stream, on_a_sphere ? 1 : 0));
 }
+int mpas_atm_compute_damping_coefs(mpas_ctx* c, double config_zd, double config_xnutr) {
+    MPAS_TASK("atm_compute_damping_coefs", launch_damping_coefs(c->S, c->stream, config_zd, config_xnutr));
+}
+int mpas_atm_init_coupled_diagnostics(mpas_ctx* c) {
+    MPAS_TASK("atm_init_coupled_diagnostics", launch_init_coupled_diagnostics(c->S, c->stream));
+}
 int mpas_atm_advance_scalars_mono(mpas_ctx* c, double dt) {
     if (!c) return MPAS_EINVAL;
     MPAS_TASK("atm_advance_scalars_mono", launch_advance_scalars_mono(c->S, c->stream, dt));

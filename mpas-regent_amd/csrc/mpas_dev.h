@@ -169,6 +169,8 @@ hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, 
 hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
 hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
 hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt);
+hipError_t launch_damping_coefs(const DevState& S, hipStream_t st, double zd, double xnutr);
+hipError_t launch_init_coupled_diagnostics(const DevState& S, hipStream_t st);
 size_t summarize_scratch_bytes();
 hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, double* out);
 

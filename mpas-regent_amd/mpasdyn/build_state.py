@@ -229,6 +229,8 @@ def connectivity(m, st):
     st["edgesOnVertex"][:nV] = m.edgesOnVertex
     st["weightsOnEdge"][:nE] = m.weightsOnEdge
     st["kiteAreasOnVertex"][:nV] = m.kiteAreasOnVertex  # (init scales [vertexDegree] only: OOB, no effect)
+    md = getattr(m, "meshDensity", None)
+    st["meshDensity"][:nC, 0] = 1.0 if md is None else md  # atm_compute_damping_coefs
 
 
 def geometry(m, st):

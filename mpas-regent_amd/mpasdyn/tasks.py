@@ -94,6 +94,17 @@ def atm_compute_output_diagnostics(ctx):
     ctx._check(ctx.lib.mpas_atm_compute_output_diagnostics(ctx.h), "atm_compute_output_diagnostics")
 
 
+def atm_compute_damping_coefs(ctx, config_zd=22000.0, config_xnutr=0.2):
+    """dynamics_tasks.rg:274 (atm_core_init, atm_core.rg:41; constants.rg defaults)"""
+    ctx._check(ctx.lib.mpas_atm_compute_damping_coefs(ctx.h, float(config_zd), float(config_xnutr)),
+               "atm_compute_damping_coefs")
+
+
+def atm_init_coupled_diagnostics(ctx):
+    """dynamics_tasks.rg:651 (atm_core_init, atm_core.rg:31)"""
+    ctx._check(ctx.lib.mpas_atm_init_coupled_diagnostics(ctx.h), "atm_init_coupled_diagnostics")
+
+
 def atm_advance_scalars_mono(ctx, dt):
     """Monotonic scalar transport of scalars_old into scalars over dt (SURVEY §8.7 row 4;
     no reference task exists, Q26 -- MPAS-A's atm_advance_scalars_mono; include/mpas_dyn.h)"""

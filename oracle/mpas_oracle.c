@@ -1142,6 +1142,74 @@ void ora_atm_srk3(ora_state* S, double dt, int schedule) {
     ora_atm_rk_dynamics_substep_finish(S, 1, dynamics_split);
 }
 
+/* ===================== one-time tasks of atm_core_init (atm_core.rg:22-42) on the device
+ * atm_compute_damping_coefs, dynamics_tasks.rg:274-300: dss of the upper damping layer
+ * (pow(x, 2.0) evaluated as x * x, the policy of DESIGN.md §2) */
+void ora_atm_compute_damping_coefs(ora_state* S, double config_zd, double config_xnutr) {
+    const int L = S->L, nC = S->nCells;
+    const double pii = acos(-1.0), dx_scale_power = 1.0;
+    double *dss = D(dss), *zgrid = D(zgrid);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++)
+        for (int k = 0; k < L; k++) {
+            CW(dss, c, k) = 0.0;
+            const double zt = CW(zgrid, c, L);
+            const double z = 0.5 * (CW(zgrid, c, k) + CW(zgrid, c, k + 1));
+            if (z > config_zd) {
+                const double sn = sin(0.5 * pii * (z - config_zd) / (zt - config_zd));
+                CW(dss, c, k) = config_xnutr * (sn * sn);
+                CW(dss, c, k) /= pow(rc2(S, D(meshDensity), c, 1, 0), (0.25 * dx_scale_power));
+            }
+        }
+}
+
+/* atm_init_coupled_diagnostics, dynamics_tasks.rg:651-726: rho_zz /= zz, ru from u, rw
+ * from w and the slope flux of ru, then rho_p, rtheta_base/_p, exner(_base), pressure */
+void ora_atm_init_coupled_diagnostics(ora_state* S) {
+    const int L = S->L, nC = S->nCells, nE = S->nEdges;
+    const double rgas_ = rgas, rcv = rgas / (CP - rgas), p0 = 100000;
+    double *rho_zz = D(rho_zz), *zz = D(zz), *ru = D(ru), *rw = D(rw), *fzm = D(fzm), *fzp = D(fzp);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++)
+        for (int k = 0; k < L; k++) CW(rho_zz, c, k) /= CW(zz, c, k);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        const int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        for (int k = 0; k < L; k++)
+            CW(ru, e, k) = 0.5 * CW(D(u), e, k) * (rc(S, rho_zz, cell1, k) + rc(S, rho_zz, cell2, k));
+    }
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        for (int k = 0; k < L; k++) {
+            CW(rw, c, k) = 0;
+            if (k > 0)
+                CW(rw, c, k) = CW(D(w), c, k) * (rz(S, fzp, k) * CW(rho_zz, c, k - 1) + rz(S, fzm, k) * CW(rho_zz, c, k)) *
+                               (rz(S, fzp, k) * CW(zz, c, k - 1) + rz(S, fzm, k) * CW(zz, c, k));
+        }
+        const int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int k = 1; k < L; k++)
+            for (int i = 0; i < ne; i++) {
+                const int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                const double flux = rz(S, fzm, k) * re(S, ru, iEdge, k) + rz(S, fzp, k) * re(S, ru, iEdge, k - 1);
+                CW(rw, c, k) -= rc2(S, D(edgesOnCellSign), c, 10, i) *
+                                (rc3v(S, D(zb_cell), c, k, i) + copysign(1.0, flux) * rc3v(S, D(zb3_cell), c, k, i)) * flux *
+                                (rz(S, fzp, k) * CW(zz, c, k - 1) + rz(S, fzm, k) * CW(zz, c, k));
+            }
+        for (int k = 0; k < L; k++) {
+            CW(D(rho_p), c, k) = CW(rho_zz, c, k) - CW(D(rho_base), c, k);
+            CW(D(rtheta_base), c, k) = CW(D(theta_base), c, k) * CW(D(rho_base), c, k);
+            CW(D(rtheta_p), c, k) = CW(D(theta_m), c, k) * CW(D(rho_p), c, k) +
+                                    CW(D(rho_base), c, k) * (CW(D(theta_m), c, k) - CW(D(theta_base), c, k));
+            CW(D(exner), c, k) = pow(CW(zz, c, k) * (rgas_ / p0) * (CW(D(rtheta_p), c, k) + CW(D(rtheta_base), c, k)), rcv);
+            CW(D(exner_base), c, k) = pow(CW(zz, c, k) * (rgas_ / p0) * (CW(D(rtheta_base), c, k)), rcv);
+            CW(D(pressure_p), c, k) = CW(zz, c, k) * rgas_ *
+                                      (CW(D(exner), c, k) * CW(D(rtheta_p), c, k) +
+                                       CW(D(rtheta_base), c, k) * (CW(D(exner), c, k) - CW(D(exner_base), c, k)));
+            CW(D(pressure_base), c, k) = CW(zz, c, k) * rgas_ * CW(D(exner_base), c, k) * CW(D(rtheta_base), c, k);
+        }
+    }
+}
+
 /* ===================== the MPAS vertical solver ("physics" mpas)
  * The reference's vertically implicit acoustic step with the statements it keeps as
  * comments restored and its quirks in that solver fixed; every other task is unchanged.

@@ -59,6 +59,8 @@ def load():
             "ora_mpas_srk3": (None, [p, dbl, i32]),
             "ora_mpas_srk3_ex": (None, [p, dbl, i32, i32]),
             "ora_mpas_advance_scalars_mono": (None, [p, dbl]),
+            "ora_atm_compute_damping_coefs": (None, [p, dbl, dbl]),
+            "ora_atm_init_coupled_diagnostics": (None, [p]),
             "ora_mpas_recover": (None, [p, i32, i32, dbl]),
             "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
         }
@@ -137,6 +139,12 @@ class Oracle:
 
     def mpas_srk3(self, dt, schedule=1, transport=False):
         self.lib.ora_mpas_srk3_ex(self.p, dt, schedule, int(bool(transport)))
+
+    def atm_compute_damping_coefs(self, config_zd=22000.0, config_xnutr=0.2):
+        self.lib.ora_atm_compute_damping_coefs(self.p, config_zd, config_xnutr)
+
+    def atm_init_coupled_diagnostics(self):
+        self.lib.ora_atm_init_coupled_diagnostics(self.p)
 
     def mpas_advance_scalars_mono(self, dt):
         """monotonic scalar transport (Q26: not in the reference; mpas_oracle.c)"""

@@ -38,6 +38,9 @@ CASES = {
     # monotonic scalar transport (Q26, mpas mode; parity unpinned, tests/test_transport.py)
     "scalars_mono": lambda o: o.mpas_advance_scalars_mono(600.0),
     "mpas_srk3_transport": lambda o: o.mpas_srk3(720.0, 1, transport=True),
+    # the one-time tasks of atm_core_init on the device
+    "damping_coefs": lambda o: o.atm_compute_damping_coefs(22000.0, 0.2),
+    "init_coupled_diagnostics": lambda o: o.atm_init_coupled_diagnostics(),
 }
 
 

@@ -353,3 +353,26 @@ def test_mpas_srk3(x1_2562, L):
         got["rho_zz"][st.nCells] = ref["rho_zz"][st.nCells]
         bad = compare_states(got, ref, rtol=tol, tol_fields=tf)
         assert not bad, f"exact={exact}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("L", [5, 56])
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
+@pytest.mark.parametrize("task", ["damping", "init_coupled"])
+def test_init_tasks(x1_2562, L, variant, task):
+    """the one-time tasks of atm_core_init on the device (dynamics_tasks.rg:274, :651):
+    value-identical except the libm results (sin, pow: device vs glibc, RTOL_POW)"""
+    ofn, gfn, tf = {
+        "damping": (lambda o: o.atm_compute_damping_coefs(22000.0, 0.2),
+                    lambda c: T.atm_compute_damping_coefs(c, 22000.0, 0.2), {"dss"}),
+        "init_coupled": (lambda o: o.atm_init_coupled_diagnostics(), lambda c: T.atm_init_coupled_diagnostics(c),
+                         {"exner", "exner_base", "pressure_p", "pressure_base"}),
+    }[task]
+    st = base_state(x1_2562, L, variant).copy()
+    if task == "damping":  # a monotone column so the damping layer exists (zd = 22 km)
+        st["zgrid"][:st.nCells] = np.linspace(0.0, 30000.0, L + 1)[None, :]
+    ref = run_oracle(st, ofn)
+    got = run_gpu(st, gfn, exact=1)
+    bad = compare_states(got, ref, rtol=RTOL_POW, tol_fields=tf)
+    assert not bad, bad[:6]
+    if task == "damping":
+        assert np.any(ref["dss"][:st.nCells] > 0)
