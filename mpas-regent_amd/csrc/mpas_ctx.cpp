@@ -6,6 +6,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <new>
@@ -68,6 +69,7 @@ struct mpas_ctx {
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     int overlap = 1;   // option "overlap": halo exchanges beside interior compute
+    void* raw[X_COUNT] = {};  // the allocations behind S.f (S.f[f] = raw[f] + stagger)
     bool timing = false;
     bool dirty = true;  // derived mesh arrays need k_prepare
     std::vector<std::string> task_names;
@@ -325,13 +327,20 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.physics = 0;
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+        // Field f starts (f % 16) * stagger bytes into its allocation (env MPAS_ALLOC_STAGGER,
+        // a multiple of 512: whole columns stay aligned; default 2048): equal-sized arrays
+        // read together then do not start on the same HBM channel.  Measured at x1.163842 x 56
+        // (interleaved A/B on one box): dyn_tend rk>0 -4 %, rk0 -2 %, step -1.5 % against 0
+        size_t stagger = 2048;
+        if (const char* v = std::getenv("MPAS_ALLOC_STAGGER")) stagger = (size_t)std::strtoull(v, nullptr, 10) / 512 * 512;
         for (int f = 0; f < X_COUNT; f++) {
-            size_t b = dev_bytes(c, f);
+            const size_t b = dev_bytes(c, f), off = (size_t)(f % 16) * stagger;
             void* p = nullptr;
-            hipError_t e = hipMalloc(&p, b);
+            hipError_t e = hipMalloc(&p, b + off);
             if (e != hipSuccess) throw Fail{MPAS_ENOMEM, std::string("hipMalloc ") + kFields[f].name};
-            hipcheck(hipMemset(p, 0, b), "hipMemset");
-            c->S.f[f] = p;
+            hipcheck(hipMemset(p, 0, b + off), "hipMemset");
+            c->raw[f] = p;
+            c->S.f[f] = (char*)p + off;
         }
         hipcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
     });
@@ -350,7 +359,7 @@ int mpas_ctx_destroy(mpas_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int f = 0; f < X_COUNT; f++)
-        if (c->S.f[f]) (void)hipFree(c->S.f[f]);
+        if (c->raw[f]) (void)hipFree(c->raw[f]);
     for (auto& t : c->pending) {
         (void)hipEventDestroy(t.e0);
         (void)hipEventDestroy(t.e1);
