@@ -135,6 +135,13 @@ int mpas_atm_compute_damping_coefs(mpas_ctx* ctx, double config_zd, double confi
 /* :651 atm_init_coupled_diagnostics(cr, er, vert_r) (atm_core.rg:31): rho_zz /= zz, ru, rw,
  *       rho_p, rtheta_base, rtheta_p, exner, exner_base, pressure_p, pressure_base */
 int mpas_atm_init_coupled_diagnostics(mpas_ctx* ctx);
+/* atm_core.rg:22 atm_core_init: the device part in the reference's order --
+ *       init_coupled_diagnostics, solve_diagnostics(hollingsworth = false, rk_step = -1),
+ *       mpas_reconstruct_2d(false, true), compute_damping_coefs(config_zd = 22000,
+ *       config_xnutr = 0.2; constants.rg:103-104).  atm_compute_signs, atm_adv_coef_compression,
+ *       atm_couple_coef_3rd_order and atm_compute_mesh_scaling are mesh preparation the
+ *       caller uploads (host side, mpasdyn/build_state.py); physics_init is a stub. */
+int mpas_atm_core_init(mpas_ctx* ctx);
 /* Monotonic scalar transport.  Replaces no reference entry point: the
  *       reference has none (Q26 -- scalars:double[8], data_structures.rg:36, is declared and
  *       never used; the north star names the transport).  MPAS-A's atm_advance_scalars_mono

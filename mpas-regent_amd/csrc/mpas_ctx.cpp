@@ -745,6 +745,20 @@ int mpas_atm_compute_damping_coefs(mpas_ctx* c, double config_zd, double config_
 int mpas_atm_init_coupled_diagnostics(mpas_ctx* c) {
     MPAS_TASK("atm_init_coupled_diagnostics", launch_init_coupled_diagnostics(c->S, c->stream));
 }
+int mpas_atm_core_init(mpas_ctx* c) {
+    // atm_core.rg:22-42 in order; the mesh tasks (atm_compute_signs, atm_adv_coef_compression,
+    // atm_couple_coef_3rd_order, atm_compute_mesh_scaling) are host-side preparation whose
+    // outputs the caller uploads (mpasdyn/build_state.py); physics_init is a stub
+    return guarded(c, [&] {
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        const DevState& S = c->S;
+        hipStream_t st = c->stream;
+        run_task(c, "atm_init_coupled_diagnostics", [&] { return launch_init_coupled_diagnostics(S, st); });
+        run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, -1); });
+        run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });
+        run_task(c, "atm_compute_damping_coefs", [&] { return launch_damping_coefs(S, st, 22000.0, 0.2); });
+    });
+}
 int mpas_atm_advance_scalars_mono(mpas_ctx* c, double dt) {
     if (!c) return MPAS_EINVAL;
     MPAS_TASK("atm_advance_scalars_mono", launch_advance_scalars_mono(c->S, c->stream, dt));

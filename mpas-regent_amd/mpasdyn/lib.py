@@ -25,7 +25,7 @@ EXPORTS = [
     "mpas_atm_rk_dynamics_substep_finish", "mpas_atm_srk3", "mpas_atm_timestep",
     "mpas_atm_recover_large_step_variables_work", "mpas_reconstruct_2d", "mpas_summarize_timestep",
     "mpas_atm_compute_output_diagnostics", "mpas_atm_advance_scalars_mono",
-    "mpas_atm_compute_damping_coefs", "mpas_atm_init_coupled_diagnostics",
+    "mpas_atm_compute_damping_coefs", "mpas_atm_init_coupled_diagnostics", "mpas_atm_core_init",
     "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
     "mpas_halo_owned", "mpas_halo_interior", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
     "mpas_halo_loopback", "mpas_halo_stats",
@@ -88,6 +88,7 @@ def load():
         "mpas_atm_advance_scalars_mono": (i32, [vp, dbl]),
         "mpas_atm_compute_damping_coefs": (i32, [vp, dbl, dbl]),
         "mpas_atm_init_coupled_diagnostics": (i32, [vp]),
+        "mpas_atm_core_init": (i32, [vp]),
         "mpas_summarize_timestep": (i32, [vp, i32, i32, i32, ctypes.POINTER(dbl)]),
         "mpas_timing_enable": (i32, [vp, i32]),
         "mpas_timing_reset": (i32, [vp]),

@@ -105,6 +105,11 @@ def atm_init_coupled_diagnostics(ctx):
     ctx._check(ctx.lib.mpas_atm_init_coupled_diagnostics(ctx.h), "atm_init_coupled_diagnostics")
 
 
+def atm_core_init(ctx):
+    """atm_core.rg:22: the device tasks of atm_core_init (the mesh preparation is uploaded)"""
+    ctx._check(ctx.lib.mpas_atm_core_init(ctx.h), "atm_core_init")
+
+
 def atm_advance_scalars_mono(ctx, dt):
     """Monotonic scalar transport of scalars_old into scalars over dt (SURVEY §8.7 row 4;
     no reference task exists, Q26 -- MPAS-A's atm_advance_scalars_mono; include/mpas_dyn.h)"""

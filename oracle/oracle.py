@@ -146,6 +146,13 @@ class Oracle:
     def atm_init_coupled_diagnostics(self):
         self.lib.ora_atm_init_coupled_diagnostics(self.p)
 
+    def atm_core_init(self):
+        """atm_core.rg:22-42, the state tasks in order (mesh preparation: build_state)"""
+        self.atm_init_coupled_diagnostics()
+        self.atm_compute_solve_diagnostics(0, -1)
+        self.mpas_reconstruct_2d(False, True)
+        self.atm_compute_damping_coefs(22000.0, 0.2)
+
     def mpas_advance_scalars_mono(self, dt):
         """monotonic scalar transport (Q26: not in the reference; mpas_oracle.c)"""
         self.lib.ora_mpas_advance_scalars_mono(self.p, dt)

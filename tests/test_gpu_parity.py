@@ -376,3 +376,16 @@ def test_init_tasks(x1_2562, L, variant, task):
     assert not bad, bad[:6]
     if task == "damping":
         assert np.any(ref["dss"][:st.nCells] > 0)
+
+
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
+def test_atm_core_init(x1_2562, variant):
+    """mpas_atm_core_init = the device tasks of atm_core_init in the reference's order"""
+    st = base_state(x1_2562, 56, variant).copy()
+    st["zgrid"][:st.nCells] = np.linspace(0.0, 30000.0, 57)[None, :]
+    ref = run_oracle(st, lambda o: o.atm_core_init())
+    got = run_gpu(st, lambda c: T.atm_core_init(c), exact=1)
+    tf = {"dss", "exner", "exner_base", "pressure_p", "pressure_base", "uReconstructX", "uReconstructY",
+          "uReconstructZ", "uReconstructZonal", "uReconstructMeridional"}
+    bad = compare_states(got, ref, rtol=RTOL_POW, tol_fields=tf)
+    assert not bad, bad[:6]
