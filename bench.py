@@ -254,6 +254,8 @@ def main():
              "atm_compute_dyn_tend_work[rk>0]": ("atm_compute_dyn_tend_work", {"rk_step": 1}),
              "atm_recover_large_step_variables_work": ("atm_recover_large_step_variables_work", {"rk_step": 2})}
     tasks_out = {}
+    if args.physics:  # the acoustic task's MPAS form also updates ru_p / ruAvg
+        kw_of["atm_advance_acoustic_step_work"] = ("atm_advance_acoustic_step_work", {"physics": 1})
     for name, (calls, ms) in rep.items():
         task, kw = kw_of.get(name, (name, {}))
         b = roofline.b_alg(task, work_dims, **kw)

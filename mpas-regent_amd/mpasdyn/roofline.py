@@ -13,7 +13,7 @@ roofline.achieved divides by the measured launch time.
 """
 
 # name -> (reads, writes); each a list of field names of the registry
-def _sets(task, rk_step=0, small_step=1, reconstruct_v=False):
+def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0):
     if task == "atm_rk_integration_setup":
         return (["rho_p", "rho_zz", "rtheta_p", "rw", "theta_m", "w", "ru", "u"],
                 ["rho_p_save", "rho_zz_2", "rho_zz_old_split", "rtheta_p_save", "rw_save", "theta_m_2", "w_2",
@@ -54,7 +54,13 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False):
                  "invAreaCell", "cellsOnEdge", "dvEdge", "specZoneMaskCell"]
         if small_step != 0:
             reads += ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
-        return reads, ["rtheta_pp_old", "rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+        writes = ["rtheta_pp_old", "rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+        if physics:  # the MPAS form (option physics = 1): the ru_p / ruAvg update of :1581-1613
+            reads += ["tend_u", "tend_theta", "c_tri", "gamma_tri", "specZoneMaskEdge"]
+            if small_step != 0:
+                reads += ["ru_p", "ruAvg", "exner", "cqu", "zxu", "invDcEdge"]
+            writes += ["ru_p", "ruAvg"]
+        return reads, writes
     if task == "atm_divergence_damping_3d":
         return (["rtheta_pp", "rtheta_pp_old", "theta_m", "ru_p", "cellsOnEdge", "isShared", "specZoneMaskEdge"],
                 ["ru_p"])
@@ -116,8 +122,8 @@ def step_schedule(schedule=1, physics=0, transport=0):
         if schedule == 1:
             out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
         out += [("atm_set_smlstep_pert_variables_work", {}, 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 1}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "physics": 1}, 1),
                 ("atm_divergence_damping_3d", {}, 4),
                 ("atm_recover_large_step_variables_work", {"rk_step": 0}, 2),
                 ("atm_recover_large_step_variables_work", {"rk_step": 2}, 1),

@@ -37,3 +37,13 @@ def test_bench_line(mode):
         assert d["halo"]["exchanges_per_step"] > 0 and d["halo"]["ghost_frac"] == [0.0, 0.0, 0.0]
     else:
         assert d["scaling"] == "weak" and d["config"]["parallelism"] == "single-gpu"
+
+
+@pytest.mark.gpu
+def test_bench_line_transport():
+    """--transport: the MPAS solver and the scalar transport inside the timed step"""
+    d = run_bench("--transport")
+    assert KEYS <= set(d)
+    assert d["config"]["physics"] == 1 and d["config"]["transport"] == 1
+    assert "atm_advance_scalars_mono" in d["tasks"] and d["tasks"]["atm_advance_scalars_mono"]["launches_per_step"] == 1
+    assert d["tasks"]["atm_advance_acoustic_step_work"]["launches_per_step"] == 4
