@@ -66,7 +66,8 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * Default 0: the reference's semantics.
  * "transport" = 1 (needs "physics" = 1) makes mpas_atm_srk3 copy scalars
  * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
- * recover, before atm_rk_dynamics_substep_finish.  Default 0. */
+ * recover, before atm_rk_dynamics_substep_finish.  Default 0.  "trorder" = 1 (speed only)
+ * orders the transport's column slots pair-major instead of entity-major. */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
 /* reads every option above ("self", default 1: when every cell is
  * among the cellsOnEdge of its own edges -- mpas-mode ids -- the cell kernels gather
