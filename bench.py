@@ -2,7 +2,7 @@
 """Benchmark of the RK3 dynamics hot path (atm_srk3, rk_timestep.rg:361-500) on MI355X.
 
 Metric (BASELINE.json): Mcell-columns/s per RK3 step at x1.163842 x 56 levels, plus the
-achieved HBM bandwidth of the dominant kernel against the 8 TB/s roofline.
+achieved HBM bandwidth of the dominant task against the 8 TB/s roofline.
 
 One step = one atm_srk3 call: setup, moist, 2x vert_imp, 3x dyn_tend (rk_step 0,1,2 --
 the MPAS schedule of SURVEY §8.5), 3x smlstep, 7x acoustic + 7x divergence damping,
@@ -12,20 +12,37 @@ precompute uploaded from the host, and the 3-D state filled on the device by the
 seeded generator (data: synthetic, seed 20211015).
 
     python bench.py [--gpus N --steps K --warmup W]
-N > 1 runs under torch.distributed.run, one process per GPU: the same x1.163842 mesh is
-split into N subdomains (mpasdyn/decomp.py: contiguous blocks of the Morton-ordered
-cells, edges/vertices with their first cell/edge, ghosts = everything an owned entity
-reaches through an index array), and the ranks exchange halos with RCCL send/recv
-before every kernel that gathers a field another rank wrote (csrc/mpas_halo.h).  Total
-work is fixed ("scaling": "strong"); `value` = global cell columns / step time.
-`--replicas` instead runs a full-mesh replica per rank (weak scaling, no collective).
+
+N > 1: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) the ranks are
+the launcher's and WORLD_SIZE must equal N; without it bench.py starts the N rank
+processes itself (children with RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT, before
+any GPU call; rank 0's stdout is the JSON line).  The x1.163842 mesh is split into N
+subdomains (mpasdyn/decomp.py: contiguous blocks of the Morton-ordered cells,
+edges/vertices with their first cell/edge, ghosts = everything an owned entity reaches
+through an index array), and the ranks exchange halos with RCCL send/recv before every
+kernel that gathers a field another rank wrote (csrc/mpas_halo.h).  Total work is fixed
+("scaling": "strong"); `value` = global cell columns / step time.  `--replicas` instead
+runs a full-mesh replica per rank (weak scaling, no collective).
+
+roofline: the task with the largest device time per step (atm_compute_dyn_tend_work, the
+north-star kernel; its rk_step 0 and rk_step > 0 launches are one Regent task),
+achieved = its algorithmic bytes per step (mpasdyn/roofline.py) / its
+device time per step (HIP events on the task stream), i.e. the launch-weighted average;
+traffic = its HBM bytes per launch from rocprofv3 FETCH_SIZE and WRITE_SIZE passes over
+this same workload, run by this script before it touches the GPU (--traffic auto).
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import ctypes
 import json
 import os
+import shutil
+import socket
+import statistics
+import subprocess
 import sys
+import tempfile
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -37,6 +54,7 @@ METRIC = "Mcell-columns/sec per RK3 step; achieved HBM GB/s; x1.163842×56L"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, HBM3E peak
 LEVEL_OF = {2562: 4, 10242: 5, 40962: 6, 163842: 7, 655362: 8}
 SEED = 20211015
+NORTH_STAR = "atm_compute_dyn_tend_work"
 
 
 class Hip:
@@ -90,9 +108,22 @@ def upload_inputs(ctx, st):
     ctx.sync()
 
 
-def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False):
-    """the oracle (C restatement, -O3, OpenMP) on the host cores: one RK3 step of the
-    same workload; kind "port" (the Regent/Legion reference cannot be built or run)."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False, budget_s=20.0):
+    """the oracle (C restatement, -O3, OpenMP) on the host cores, RK3 steps of the same
+    workload; kind "port" (the Regent/Legion reference cannot be built or run).  Two
+    untimed warm-up steps, then steps timed one by one until `budget_s` (at least 3,
+    at most 20); value from the median step."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from mpasdyn import build_state as bs
@@ -104,32 +135,172 @@ def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False):
     rdzw, rdzu, fzm, fzp = bs.vertical_grid(st)
     st["rdzw"], st["rdzu"], st["fzm"], st["fzp"] = rdzw, rdzu, fzm, fzp
     o = O.Oracle(st)
-    n, t0 = 0, time.perf_counter()
-    while n < 8 and (n == 0 or time.perf_counter() - t0 < 10.0):  # a bounded ~10 s sample
+
+    def step():
         if physics:
             o.mpas_srk3(dt, 1, transport=transport)
         else:
             o.atm_srk3(dt, 1)
-        n += 1
-    t = (time.perf_counter() - t0) / n
+
+    warm = 2
+    for _ in range(warm):
+        step()
+    times, t0 = [], time.perf_counter()
+    while len(times) < 20 and (len(times) < 3 or time.perf_counter() - t0 < budget_s):
+        t1 = time.perf_counter()
+        step()
+        times.append(time.perf_counter() - t1)
+    t = statistics.median(times)
     what = "MPAS-solver " if physics else ""
     what += "RK3 steps with scalar transport" if transport else "RK3 steps"
     return {"value": round(ncells / t / 1e6, 6), "unit": "Mcell-columns/s", "cores": threads, "kind": "port",
-            "sample": f"{n} {what} (schedule 0,1,2) of x1.{ncells} x {L} levels by oracle/mpas_oracle.c "
-                      f"(-O3, OpenMP {threads} threads), {t:.2f} s per step"}
+            "cpu_model": cpu_model(), "omp_num_threads": threads, "nproc": os.cpu_count(),
+            "sample": f"median of {len(times)} {what} (schedule 0,1,2) after {warm} warm-up steps, x1.{ncells} x {L} "
+                      f"levels, oracle/mpas_oracle.c (-O3, OpenMP {threads} threads): {t:.3f} s per step "
+                      f"(min {min(times):.3f}, max {max(times):.3f}); bounded to ~{budget_s:.0f} s of CPU time, "
+                      f"fewer than the 20 steps SURVEY §8.5 asks when a step is slower than {budget_s / 20:.1f} s"}
 
 
-def pmc_traffic(task, ncells, L, physics=False):
-    """per-launch HBM bytes of `task` from a committed rocprofv3 PMC summary, if one
-    exists for this configuration (profiles/pmc_x1.<n>_L<L>.json, written by
-    tools/pmc_summary.py with the gfx950 FETCH_SIZE correction)"""
-    p = os.path.join(REPO, "profiles", f"pmc_{'transport_' if physics else ''}x1.{ncells}_L{L}.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        d = json.load(f)
-    v = d.get("tasks", {}).get(task)
-    return v.get("hbm_bytes_per_launch") if v else None
+# ------------------------------------------------------------------ process launch
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n, argv):
+    """start N rank processes of this script (no GPU touched here); rank 0 inherits
+    stdout (the JSON line), the others write theirs to stderr.  Returns the exit code."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                c = p.poll()
+                if c is None:
+                    continue
+                pending.remove(p)
+                if c != 0 and rc == 0:
+                    rc = c
+                    for q in pending:  # one rank failed: the others would wait forever
+                        q.terminate()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    return rc if rc >= 0 else 128 - rc
+
+
+# ------------------------------------------------------------------ live HBM traffic
+def measure_traffic(args):
+    """run this workload (one RK3 step, no warm-up) under `rocprofv3 --pmc FETCH_SIZE`
+    and under `--pmc WRITE_SIZE` (separate passes, MI355X_MICROARCH.md) in child
+    processes, before this process touches the GPU; returns {timing key: HBM bytes per
+    step} and a note, or (None, reason)."""
+    from mpasdyn import pmc
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "1", "--warmup", "0",
+             "--ncells", str(args.ncells), "--levels", str(args.levels), "--exact", str(args.exact)]
+    child += [f"--option={o}" for o in args.option]
+    if args.physics:
+        child.append("--physics")
+    if args.transport:
+        child.append("--transport")
+    res = {}
+    tmp = tempfile.mkdtemp(prefix="mpas_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", "240", prof, "--pmc", counter, "-d", d, "-o", "pmc",
+                   "--output-format", "csv", "--"] + child
+            p = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True, cwd=REPO)
+            if p.returncode != 0:
+                return None, f"rocprofv3 --pmc {counter} exited {p.returncode}: {p.stderr[-300:]}"
+            res[counter] = pmc.read_counter(d, counter)
+    except Exception as e:  # noqa: BLE001 -- traffic is optional; report why it is null
+        return None, f"{type(e).__name__}: {e}"
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    m_cells = args.ncells
+    m_edges = 3 * (m_cells - 2)
+    wfac = pmc.write_factor(res["WRITE_SIZE"], m_cells, m_edges, args.levels)
+    if wfac is None:
+        return None, "WRITE_SIZE calibration kernels missing"
+    by = pmc.bytes_per_step(res["FETCH_SIZE"], res["WRITE_SIZE"], 1, wfac)
+    return by, (f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of 1 RK3 step of this workload; "
+                f"fetch x{pmc.FETCH_FACTOR} (gfx950), write x{wfac:.3f} (calibrated on the setup copies)")
+
+
+def pmc_child(args):
+    """the workload rocprofv3 counts: 1 RK3 step after upload, nothing else"""
+    from mpasdyn import lib
+    from mpasdyn import tasks as T
+    m, st = build_inputs(args.ncells, args.levels, zero_based=args.physics)
+    ctx = lib.Context(m.nCells, m.nEdges, m.nVertices, args.levels, device=0)
+    ctx.set_option("exact", args.exact)
+    ctx.set_option("physics", int(args.physics))
+    ctx.set_option("transport", int(args.transport))
+    for kv in args.option:
+        k, v = kv.split("=")
+        ctx.set_option(k, int(v))
+    upload_inputs(ctx, st)
+    dt = dt_for(args.ncells)
+    for _ in range(args.steps):
+        T.atm_srk3(ctx, dt, 1)
+    ctx.sync()
+    ctx.close()
+
+
+# ------------------------------------------------------------------ roofline
+def task_table(rep, work_dims, n_prof, physics):
+    """per timing key (a task, split by the arguments that change its read/write set)
+    and aggregated per Regent task: launches and device ms per step, B_alg per step"""
+    from mpasdyn import roofline
+    kw_of = {"atm_compute_dyn_tend_work[rk0]": {"rk_step": 0}, "atm_compute_dyn_tend_work[rk>0]": {"rk_step": 1},
+             "atm_advance_acoustic_step_work[ss0]": {"small_step": 0},
+             "atm_advance_acoustic_step_work[ss>0]": {"small_step": 1},
+             "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
+             "atm_recover_large_step_variables_work[rk2]": {"rk_step": 2}}
+    variants, tasks = {}, {}
+    for name, (calls, ms) in rep.items():
+        task = name.split("[")[0]
+        kw = dict(kw_of.get(name, {}))
+        if physics and task == "atm_advance_acoustic_step_work":
+            kw["physics"] = 1  # the acoustic task's MPAS form also updates ru_p / ruAvg
+        b = roofline.b_alg(task, work_dims, **kw)
+        avg = ms / calls
+        n = calls / n_prof
+        variants[name] = {"launches_per_step": round(n, 3), "avg_ms": round(avg, 4), "b_alg_GB": round(b / 1e9, 4),
+                          "GBs": round(b / (avg * 1e-3) / 1e9, 1)}
+        t = tasks.setdefault(task, {"launches_per_step": 0.0, "ms_per_step": 0.0, "b_alg_GB_per_step": 0.0})
+        t["launches_per_step"] += n
+        t["ms_per_step"] += n * avg
+        t["b_alg_GB_per_step"] += n * b / 1e9
+    for name, t in tasks.items():
+        t["avg_ms"] = round(t["ms_per_step"] / t["launches_per_step"], 4)
+        t["b_alg_GB"] = round(t["b_alg_GB_per_step"] / t["launches_per_step"], 4)  # per launch
+        t["GBs"] = round(t["b_alg_GB_per_step"] / (t["ms_per_step"] * 1e-3), 1)
+        t["frac"] = round(t["GBs"] / HBM_PEAK_GBS, 4)
+        t["launches_per_step"] = round(t["launches_per_step"], 3)
+        t["ms_per_step"] = round(t["ms_per_step"], 4)
+        t["b_alg_GB_per_step"] = round(t["b_alg_GB_per_step"], 4)
+        vs = {k[len(name):]: v for k, v in variants.items() if k.split("[")[0] == name and "[" in k}
+        if vs:
+            t["variants"] = vs
+    return tasks
 
 
 def main():
@@ -141,6 +312,11 @@ def main():
     ap.add_argument("--levels", type=int, default=56)
     ap.add_argument("--exact", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of oracle steps in the cpu_baseline leg")
+    ap.add_argument("--traffic", choices=["auto", "off"], default="auto",
+                    help="auto: rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this workload (N = 1, rank 0)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true", help="print each rank's launch environment and exit")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="extra mpas_set_option (A/B runs, e.g. xcd=32)")
     ap.add_argument("--replicas", action="store_true", help="N > 1: full-mesh replicas instead of a decomposition")
@@ -153,6 +329,30 @@ def main():
     args = ap.parse_args()
     if args.transport:
         args.physics = True
+    if args.pmc_child:
+        return pmc_child(args)
+
+    # ranks: the launcher's (torch.distributed.run) or our own children
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if world != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+            return 2
+    elif args.gpus > 1:
+        return spawn_ranks(args.gpus, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus,
+                          "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}),
+              flush=True)
+        return 0
+
+    # live traffic first: the profiled children start before this process touches the GPU
+    traffic_by, traffic_note = None, "off"
+    if args.traffic == "auto" and world == 1 and rank == 0 and not args.decompose:
+        traffic_by, traffic_note = measure_traffic(args)
 
     # Libraries print banners on stdout from C (RCCL's version lines at communicator
     # creation); the contract is ONE JSON line there: route fd 1 to stderr for the run
@@ -160,9 +360,6 @@ def main():
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
     if world > 1:
@@ -250,31 +447,28 @@ def main():
     ctx.sync()
     rep = ctx.timing_report()
     ctx.timing(False)
-    kw_of = {"atm_compute_dyn_tend_work[rk0]": ("atm_compute_dyn_tend_work", {"rk_step": 0}),
-             "atm_compute_dyn_tend_work[rk>0]": ("atm_compute_dyn_tend_work", {"rk_step": 1}),
-             "atm_recover_large_step_variables_work": ("atm_recover_large_step_variables_work", {"rk_step": 2})}
-    tasks_out = {}
-    if args.physics:  # the acoustic task's MPAS form also updates ru_p / ruAvg
-        kw_of["atm_advance_acoustic_step_work"] = ("atm_advance_acoustic_step_work", {"physics": 1})
-    for name, (calls, ms) in rep.items():
-        task, kw = kw_of.get(name, (name, {}))
-        b = roofline.b_alg(task, work_dims, **kw)
-        avg = ms / calls
-        tasks_out[name] = {"launches_per_step": calls // n_prof, "avg_ms": round(avg, 4),
-                           "b_alg_GB": round(b / 1e9, 4), "GBs": round(b / (avg * 1e-3) / 1e9, 1)}
-        tr = pmc_traffic(name, ncells, L, args.physics) if not decomposed else None
-        if tr:  # SURVEY §8.5 metric 2: measured (FETCH + WRITE) bytes over this run's launch time
-            tasks_out[name]["hbm_GB_measured"] = round(tr / 1e9, 4)
-            tasks_out[name]["hbm_frac_measured"] = round(tr / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-    dom = max(tasks_out, key=lambda k: tasks_out[k]["avg_ms"] * tasks_out[k]["launches_per_step"])
-    dt_ = tasks_out[dom]
-    task, kw = kw_of.get(dom, (dom, {}))
-    traffic = pmc_traffic(dom, ncells, L, args.physics) if not decomposed else None
-    traffic = round(traffic / 1e9, 4) if traffic else None
-    roof = {"bound": "hbm", "kernel": dom, "achieved": dt_["GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(dt_["GBs"] / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_unit": "GB/launch",
-            "b_alg_per_launch_GB": dt_["b_alg_GB"], "avg_launch_ms": dt_["avg_ms"],
-            "traffic_frac": dt_.get("hbm_frac_measured")}
+    tasks_out = task_table(rep, work_dims, n_prof, args.physics)
+    if traffic_by:
+        for name, t in tasks_out.items():
+            keys = [k for k in traffic_by if k.split("[")[0] == name]
+            if keys:  # SURVEY §8.5 metric 2: measured (FETCH + WRITE) bytes over this run's device time
+                b = sum(sum(traffic_by[k]) for k in keys)
+                t["hbm_GB_measured_per_step"] = round(b / 1e9, 4)
+                t["hbm_frac_measured"] = round(b / (t["ms_per_step"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+    dom = max(tasks_out, key=lambda k: tasks_out[k]["ms_per_step"])
+    ns = tasks_out[NORTH_STAR]
+    traffic = None
+    if "hbm_GB_measured_per_step" in ns:
+        traffic = round(ns["hbm_GB_measured_per_step"] / ns["launches_per_step"], 4)
+    roof = {"bound": "hbm", "kernel": NORTH_STAR, "achieved": ns["GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": ns["frac"], "traffic": traffic, "traffic_unit": "GB/launch",
+            "traffic_over_b_alg": round(traffic / ns["b_alg_GB"], 3) if traffic else None,
+            "traffic_frac": ns.get("hbm_frac_measured"), "traffic_source": traffic_note,
+            "b_alg_per_launch_GB": ns["b_alg_GB"], "avg_launch_ms": ns["avg_ms"],
+            "launches_per_step": ns["launches_per_step"], "ms_per_step": ns["ms_per_step"],
+            "variants": ns.get("variants"), "dominant_task": dom,
+            "note": "achieved = B_alg per step / device time per step of the task (launch-weighted average of its "
+                    "rk_step 0 and rk_step > 0 launches); frac = achieved / peak"}
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport))
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
@@ -300,7 +494,7 @@ def main():
         out["halo"] = halo_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count())))
-        out["cpu_baseline"] = cpu_baseline(ncells, L, dt, threads, args.physics, args.transport)
+        out["cpu_baseline"] = cpu_baseline(ncells, L, dt, threads, args.physics, args.transport, args.cpu_budget)
     elif rank == 0:
         out["cpu_baseline"] = None
     ctx.close()
@@ -309,7 +503,8 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,5 +1,6 @@
 // mpas_ctx.cpp -- libmpasdyn host runtime: context, device residency, the C-ABI task
 // entry points of include/mpas_dyn.h, and the atm_srk3 driver (rk_timestep.rg:361-500).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <memory>
@@ -165,8 +166,38 @@ void harvest(mpas_ctx* c) {
 }
 
 // run a task launcher, bracketed by events when timing is on
+// roctx ranges per task (SURVEY §5 tracing): env MPAS_ROCTX=1 loads libroctx64 at the
+// first task and brackets every task launch, so rocprofv3 --marker-trace shows the
+// Regent task names over their kernels.  Off: no library, no cost.
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+    Roctx() {
+        const char* v = std::getenv("MPAS_ROCTX");
+        if (!v || !*v || *v == '0') return;
+        void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        push = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+        pop = (int (*)())dlsym(h, "roctxRangePop");
+        if (!push || !pop) push = nullptr, pop = nullptr;
+    }
+};
+const Roctx& roctx() {
+    static Roctx r;
+    return r;
+}
+
 template <class Fn>
 void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
+    const Roctx& rx = roctx();
+    if (rx.push) rx.push(name);
+    struct Pop {
+        const Roctx& r;
+        ~Pop() {
+            if (r.pop) r.pop();
+        }
+    } pop_at_exit{rx};
     hipEvent_t e0 = nullptr, e1 = nullptr;
     int ti = -1;
     if (c->timing) {
@@ -187,6 +218,7 @@ void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
             throw Fail{MPAS_ERCCL, std::string(name) + ": halo exchange: " + c->halo->err};
         throw Fail{MPAS_EHIP, std::string(name) + ": " + hipGetErrorString(e)};
     }
+    if (c->halo && !c->halo->race.empty()) throw Fail{MPAS_EINVAL, std::string(name) + ": " + c->halo->race};
     if (c->timing) {
         hipcheck(hipEventRecord(e1, c->stream), "hipEventRecord");
         c->pending.push_back({ti, e0, e1});
@@ -213,6 +245,15 @@ int guarded(mpas_ctx* c, Fn&& fn) {
         c->err = "unknown error";
         return MPAS_EINVAL;
     }
+}
+
+// timing keys: one Regent task, split where its read/write set (B_alg) differs by argument
+// (bench.py aggregates the variants per task)
+const char* acoustic_name(int small_step) {
+    return small_step == 0 ? "atm_advance_acoustic_step_work[ss0]" : "atm_advance_acoustic_step_work[ss>0]";
+}
+const char* recover_name(int rk_step) {
+    return rk_step == 2 ? "atm_recover_large_step_variables_work[rk2]" : "atm_recover_large_step_variables_work[rk<2]";
 }
 
 void srk3(mpas_ctx* c, double dt, int schedule) {
@@ -257,13 +298,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
         const int n_small = number_sub_steps[rk_step] + (S.physics ? 0 : 1);  // Q5 (the MPAS form: n)
         for (int small_step = 0; small_step < n_small; small_step++) {
-            run_task(c, "atm_advance_acoustic_step_work",
+            run_task(c, acoustic_name(small_step),
                      [&] { return launch_acoustic(S, st, rk_sub_timestep[rk_step], small_step, c->exact); });
             run_task(c, "atm_divergence_damping_3d",
                      [&] { return launch_div_damping(S, st, rk_sub_timestep[rk_step], small_step == 0); });
         }
         if (S.physics)  // rk_timestep.rg:460, commented out in the reference (Q7)
-            run_task(c, "atm_recover_large_step_variables_work",
+            run_task(c, recover_name(rk_step),
                      [&] { return launch_recover_large_step(S, st, number_sub_steps[rk_step], rk_step, dt); });
         run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
     }
@@ -718,7 +759,7 @@ int mpas_atm_set_smlstep_pert_variables_work(mpas_ctx* c) {
     MPAS_TASK("atm_set_smlstep_pert_variables_work", launch_set_smlstep(c->S, c->stream));
 }
 int mpas_atm_advance_acoustic_step_work(mpas_ctx* c, double dts, int small_step) {
-    MPAS_TASK("atm_advance_acoustic_step_work", launch_acoustic(c->S, c->stream, dts, small_step, c->exact));
+    MPAS_TASK(acoustic_name(small_step), launch_acoustic(c->S, c->stream, dts, small_step, c->exact));
 }
 int mpas_atm_divergence_damping_3d(mpas_ctx* c, double dts) {
     MPAS_TASK("atm_divergence_damping_3d", launch_div_damping(c->S, c->stream, dts));
@@ -733,7 +774,7 @@ int mpas_atm_rk_dynamics_substep_finish(mpas_ctx* c, int substep, int split) {
 
 int mpas_atm_recover_large_step_variables_work(mpas_ctx* c, int ns, int rk_step, double dt) {
     if (ns == 0) return MPAS_EINVAL;
-    MPAS_TASK("atm_recover_large_step_variables_work", launch_recover_large_step(c->S, c->stream, ns, rk_step, dt));
+    MPAS_TASK(recover_name(rk_step), launch_recover_large_step(c->S, c->stream, ns, rk_step, dt));
 }
 int mpas_reconstruct_2d(mpas_ctx* c, int includeHalos, int on_a_sphere) {
     (void)includeHalos;  // :1909-1912: the range is nCells either way

@@ -65,6 +65,8 @@ struct Halo {
     int nint[3] = {0, 0, 0};  // interior cells, edges, vertices: the first owned ones
     bool interior = false;     // nint set (mpas_halo_interior)
     int overlap = 1;           // option "overlap"
+    std::vector<int> overlapped;  // fields exchanged beside the last interior launch
+    std::string race;             // set by wrote() when a kernel wrote one of them
 
     ~Halo();
     hipError_t reserve(int LP);  // size the packed buffers for the largest exchange

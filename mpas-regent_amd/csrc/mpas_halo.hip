@@ -90,7 +90,19 @@ hipError_t Halo::reserve(int LP) {
 }
 
 void Halo::wrote(std::initializer_list<int> fields) {
-    for (int f : fields) stale[f] = 1;
+    // Overlap safety: the interior launch of the kernel that just ran executed beside the
+    // pack of `overlapped`.  If that kernel writes one of those fields, the pack may read
+    // a half-updated column (send entities can be interior).  Flag it; run_task turns it
+    // into an error of the task (every rank runs the same launcher sequence, so the
+    // loopback tests catch a launcher that breaks the invariant).
+    for (int f : fields) {
+        for (int g : overlapped)
+            if (g == f && race.empty())
+                race = std::string("field ") + kFields[f].name +
+                       " is written by a kernel whose interior launch overlapped its halo exchange";
+        stale[f] = 1;
+    }
+    overlapped.clear();
 }
 
 hipError_t Halo::before(const DevState& S, hipStream_t st, std::initializer_list<int> gathers) {
@@ -110,6 +122,7 @@ hipError_t Halo::launch(const DevState& S, hipStream_t st, std::initializer_list
     for (int f : gathers)
         if (stale[f]) need.push_back(f);
     hipError_t e;
+    overlapped.clear();
     if (need.empty()) {
         fn(S);
         return hipGetLastError();
@@ -124,6 +137,7 @@ hipError_t Halo::launch(const DevState& S, hipStream_t st, std::initializer_list
     // were written there); the interior launch reads no ghost and writes no gathered
     // field, so it runs beside the pack / send / recv / unpack
     if ((e = hipEventRecord(ev_ready, st)) != hipSuccess) return e;
+    overlapped = need;  // checked against the kernel's writes by wrote()
     DevState in = S;
     in.nCO = nint[0];
     in.nEO = nint[1];

@@ -3,8 +3,9 @@
     B_alg = sum over the distinct arrays a task reads as inputs (once each)
           + sum over the distinct arrays it writes (once each)
 
-3-D fp64 arrays count 8*n_entity*nVertLevels, C3V arrays 10x that, 2-D mesh arrays their
-stored bytes.  The read/write sets are the active-branch subsets of each Regent task's
+3-D fp64 arrays count 8*n_entity*nVertLevels, C3V arrays the components a task reads
+(zb_cell/zb3_cell: the nEdgesOnCell = 6 edge slots of a hexagon of their 10), 2-D mesh
+arrays their stored bytes.  The read/write sets are the active-branch subsets of each Regent task's
 privilege clause (dynamics_tasks.rg), without per-task scratch (flux_arr, ru_edge_w,
 wduz, q, wdwz, wdtz, u_mix) and without arrays the task itself writes before reading
 (their re-reads are implementation traffic, not algorithmic bytes).  Vertical 1-D
@@ -106,10 +107,21 @@ def field_bytes(name, nCells, nEdges, nVertices, L):
     return n * f.width * (4 if f.kind.endswith("I") else 8)
 
 
+# C3V arrays indexed by a cell's edge slot (zb_cell / zb3_cell: one component per
+# edgesOnCell entry): the tasks read nEdgesOnCell of their 10 components, 6 on the
+# hexagons of an x1 mesh (5 on its 12 pentagons)
+SLOT_FIELDS = {"zb_cell", "zb3_cell"}
+SLOTS_READ = 6
+
+
 def b_alg(task, dims, **kw):
     """algorithmic bytes of one launch of `task` at dims = (nCells, nEdges, nVertices, L)"""
     reads, writes = _sets(task, **kw)
-    return sum(field_bytes(x, *dims) for x in set(reads)) + sum(field_bytes(x, *dims) for x in set(writes))
+
+    def fb(x):
+        b = field_bytes(x, *dims)
+        return b * SLOTS_READ // 10 if x in SLOT_FIELDS else b
+    return sum(fb(x) for x in set(reads)) + sum(fb(x) for x in set(writes))
 
 
 def step_schedule(schedule=1, physics=0, transport=0):

@@ -1,0 +1,76 @@
+"""bench.py host logic on the CPU: the --gpus N launcher (N rank processes with the
+rendezvous environment, started before any GPU call), the WORLD_SIZE check, and the
+per-task roofline aggregation (one Regent task = all its timing variants)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def _run(args, env=None):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=120, cwd=REPO, env=e)
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_launcher_starts_n_ranks(n):
+    p = _run(["--gpus", str(n), "--dry-run"])
+    assert p.returncode == 0, p.stderr
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.strip()]
+    lines += [json.loads(x) for x in p.stderr.splitlines() if x.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == list(range(n))
+    assert all(d["world_size"] == n and d["gpus"] == n and d["local_rank"] == d["rank"] for d in lines)
+    masters = {d["master"] for d in lines}
+    assert len(masters) == 1 and masters.pop().startswith("127.0.0.1:")
+
+
+def test_launcher_single_rank_runs_in_process():
+    p = _run(["--dry-run"])
+    assert p.returncode == 0, p.stderr
+    d = json.loads(p.stdout.strip())
+    assert d == {**d, "rank": 0, "world_size": 1, "gpus": 1}
+
+
+def test_world_size_must_match_gpus():
+    p = _run(["--gpus", "4", "--dry-run"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode == 2 and "WORLD_SIZE=2" in p.stderr
+
+
+def test_launcher_propagates_rank_failure():
+    # an unknown option makes every rank exit 2 (argparse) -> the launcher exits non-zero
+    p = _run(["--gpus", "2", "--no-such-flag"])
+    assert p.returncode != 0
+
+
+def test_task_table_aggregates_variants():
+    import bench
+    from mpasdyn import roofline
+    dims = (163842, 491520, 327680, 56)
+    # two profiled steps: dyn_tend 1 rk0 + 2 rk>0 launches per step, acoustic 3 + 4
+    rep = {"atm_compute_dyn_tend_work[rk0]": (2, 2 * 2.7), "atm_compute_dyn_tend_work[rk>0]": (4, 4 * 1.3),
+           "atm_advance_acoustic_step_work[ss0]": (6, 6 * 0.35), "atm_advance_acoustic_step_work[ss>0]": (8, 8 * 0.44),
+           "atm_divergence_damping_3d": (14, 14 * 0.14)}
+    t = bench.task_table(rep, dims, 2, physics=False)
+    dyn = t["atm_compute_dyn_tend_work"]
+    b0 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0)
+    b1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1)
+    assert dyn["launches_per_step"] == 3 and abs(dyn["ms_per_step"] - (2.7 + 2 * 1.3)) < 1e-9
+    gbs = (b0 + 2 * b1) / ((2.7 + 2 * 1.3) * 1e-3) / 1e9
+    assert abs(dyn["GBs"] - gbs) < 0.1 and abs(dyn["frac"] - gbs / 8000.0) < 1e-4
+    assert set(dyn["variants"]) == {"[rk0]", "[rk>0]"}
+    ac = t["atm_advance_acoustic_step_work"]
+    a0 = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=0)
+    a1 = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=1)
+    assert a0 < a1  # the first substep reads four columns fewer
+    assert abs(ac["b_alg_GB_per_step"] - (3 * a0 + 4 * a1) / 1e9) < 1e-3
+    # the task with the most device time per step is dyn_tend, not the 7-launch acoustic task
+    assert max(t, key=lambda k: t[k]["ms_per_step"]) == "atm_compute_dyn_tend_work"

@@ -15,7 +15,7 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
 
 def run_bench(*args):
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
-                        "--no-cpu-baseline", *args], capture_output=True, text=True, timeout=110, cwd=REPO)
+                        "--no-cpu-baseline", "--traffic", "off", *args], capture_output=True, text=True, timeout=110, cwd=REPO)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, f"stdout must be ONE JSON line, got {len(lines)}: {p.stdout[:500]}"
@@ -47,3 +47,22 @@ def test_bench_line_transport():
     assert d["config"]["physics"] == 1 and d["config"]["transport"] == 1
     assert "atm_advance_scalars_mono" in d["tasks"] and d["tasks"]["atm_advance_scalars_mono"]["launches_per_step"] == 1
     assert d["tasks"]["atm_advance_acoustic_step_work"]["launches_per_step"] == 4
+
+
+@pytest.mark.gpu
+def test_bench_roofline_is_dyn_tend_with_live_traffic():
+    """the roofline names the north-star task (dyn_tend: rk0 + 2 rk>0 launches per step),
+    and its traffic comes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of the same
+    workload run by bench.py itself (x1.40962 keeps the passes short)"""
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--no-cpu-baseline", "--ncells", "40962"], capture_output=True, text=True, timeout=300,
+                       cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip())
+    r = d["roofline"]
+    assert r["kernel"] == "atm_compute_dyn_tend_work" and r["launches_per_step"] == 3
+    assert set(r["variants"]) == {"[rk0]", "[rk>0]"}
+    assert r["traffic"] is not None, r["traffic_source"]
+    # measured traffic cannot be below the distinct arrays the task must touch (minus the
+    # 2-D mesh rows, which may stay in cache), nor absurdly above
+    assert 0.5 * r["b_alg_per_launch_GB"] < r["traffic"] < 10 * r["b_alg_per_launch_GB"]

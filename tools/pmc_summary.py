@@ -22,25 +22,12 @@ import csv
 import glob
 import json
 import os
-import re
+import sys
 from collections import defaultdict
 
-# kernel -> task (first regex that matches the demangled name)
-KERNEL_TASK = [
-    (r"k_setup_(cells|edges)", "atm_rk_integration_setup"),
-    (r"k_moist", "atm_compute_moist_coefficients"),
-    (r"k_vert_imp", "atm_compute_vert_imp_coefs"),
-    (r"k_dyn_[ABE]<64, true", "atm_compute_dyn_tend_work[rk0]"),
-    (r"k_dyn_[CD]<", "atm_compute_dyn_tend_work[rk0]"),
-    (r"k_dyn_[ABE]<64, false", "atm_compute_dyn_tend_work[rk>0]"),
-    (r"k_set_smlstep", "atm_set_smlstep_pert_variables_work"),
-    (r"k_acoustic", "atm_advance_acoustic_step_work"),
-    (r"k_div_damp", "atm_divergence_damping_3d"),
-    (r"k_solve_", "atm_compute_solve_diagnostics"),
-    (r"k_finish_", "atm_rk_dynamics_substep_finish"),
-    (r"k_recover_", "atm_recover_large_step_variables_work"),
-    (r"k_tr_", "atm_advance_scalars_mono"),
-]
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpas-regent_amd"))
+from mpasdyn.pmc import read_trace, short, task_of  # noqa: E402,F401  (kernel -> task map shared with bench.py)
+
 # task launches per RK3 step (schedule 1, x1.163842: 7 acoustic substeps)
 LAUNCHES = {"atm_rk_integration_setup": 1, "atm_compute_moist_coefficients": 1, "atm_compute_vert_imp_coefs": 2,
             "atm_compute_dyn_tend_work[rk0]": 1, "atm_compute_dyn_tend_work[rk>0]": 2,
@@ -53,34 +40,11 @@ LAUNCHES_PHYSICS = dict(LAUNCHES, atm_advance_acoustic_step_work=4, atm_divergen
                         atm_recover_large_step_variables_work=3, atm_advance_scalars_mono=1)
 
 
-def task_of(name):
-    for pat, task in KERNEL_TASK:
-        if re.search(pat, name):
-            return task
-    return None
-
-
-def short(name):
-    return name.replace("void ", "").replace("mpas::", "").split("(")[0]
-
-
 def read_counter(d, counter):
     """total counter value and dispatch count per kernel over the run"""
-    f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-    tot, n = defaultdict(float), defaultdict(int)
-    for r in csv.DictReader(open(f)):
-        if r["Counter_Name"] == counter:
-            tot[short(r["Kernel_Name"])] += float(r["Counter_Value"])
-            n[short(r["Kernel_Name"])] += 1
-    return tot, n
-
-
-def read_trace(d):
-    f = glob.glob(os.path.join(d, "**", "*kernel_stats.csv"), recursive=True)[0]
-    out = {}
-    for r in csv.DictReader(open(f)):
-        out[short(r["Name"])] = (int(r["Calls"]), float(r["TotalDurationNs"]) * 1e-9)
-    return out
+    from mpasdyn.pmc import read_counter as rc
+    r = rc(d, counter)
+    return {k: v[0] for k, v in r.items()}, {k: v[1] for k, v in r.items()}
 
 
 def main():
