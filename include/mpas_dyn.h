@@ -63,8 +63,15 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), recover_large_step
  * with Q24 fixed, and in mpas_atm_srk3 number_sub_steps acoustic substeps (Q5) followed by
  * recover (Q7); every other task as the reference.
+ * "physics" = 2 adds the MPAS dynamics (every remaining quirk of the path fixed, so the JW
+ * state evolves as a dynamical core): dyn_tend with the w tendency in tend_w computed from
+ * the state w (Q8, Q13, Q14), q once (Q10), the MPAS curvature (Q12) and wdtz (Q15);
+ * solve_diagnostics with h = rho_zz, rho_edge = h_edge, divergence sign*u (Q9) and v over
+ * every edgesOnEdge entry (Q23); set_smlstep on tend_u / tend_w (Q2); setup also saving
+ * theta_m_save; moist setting cqu (Q25); mpas_reconstruct_2d after the RK loop; the substep
+ * finish keeping rho_zz; atm_compute_output_diagnostics also writing surface_pressure.
  * Default 0: the reference's semantics.
- * "transport" = 1 (needs "physics" = 1) makes mpas_atm_srk3 copy scalars
+ * "transport" = 1 (needs "physics" >= 1) makes mpas_atm_srk3 copy scalars
  * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
  * recover, before atm_rk_dynamics_substep_finish.  Default 0.  "trorder" = 1 (speed only)
  * orders the transport's column slots pair-major instead of entity-major. */

@@ -77,6 +77,9 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         t2_[i] = ldz(kl, t2_[i]);
     }
     col_rd2<LP>(fd(S, F_w), fd(S, F_coftz), c, k, L, w, coftz);
+    // the w tendency: the state w in the reference and under physics = 1 (Q8), tend_w under
+    // the MPAS dynamics (physics = 2); the implicit Rayleigh term reads the state w
+    const double tw = (MPASV && S.physics == 2) ? col_rd<LP>(fd(S, F_tend_w), c, k, L) : w;
     col_rd2<LP>(fd(S, F_zz), fd(S, F_rho_zz), c, k, L, zz, rz);
     col_rd2<LP>(fd(S, F_cofwt), fd(S, F_cofwz), c, k, L, cofwt, cofwz);
     col_rd2<LP>(fd(S, F_cofwr), fd(S, F_a_tri), c, k, L, cofwr, a_tri);
@@ -103,7 +106,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         if (kl) {
             rpp = rpp + dts * tend_rho;
             rtp = rtp + dts * tt;
-            rwp = rwp + dts * w;
+            rwp = rwp + dts * tw;
             ww = ww + 0.5 * (1.0 + epssm) * rwp;
         }
         if (k != L) {
@@ -142,7 +145,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         if (in) ww = ww + 0.5 * (1.0 - epssm) * rwold;
         double x = rwold;
         if (in)
-            x = rwold + dts * w - cofwz * ((zz * ts - zz_m * ts_m) + resm * (zz * rtp - zz_m * rtp_m)) -
+            x = rwold + dts * tw - cofwz * ((zz * ts - zz_m * ts_m) + resm * (zz * rtp - zz_m * rtp_m)) -
                 cofwr * ((rs + rs_m) + resm * (rpp + rpp_m)) + cofwt * (ts + resm * rtp) + cofwt_m * (ts_m + resm * rtp_m);
         // up: y(k) = (x(k) - a(k) y(k-1)) alpha(k), 1 <= k < L; y(0) = rw_p(0)
         double y = x;

@@ -381,7 +381,9 @@ hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sph
 
 // ---------------------------------------------------------------- output diagnostics
 // dynamics_tasks.rg:729-746: rho = rho_zz * zz, pressure = pressure_base + pressure_p over
-// cells x levels 0..nVertLevels-1 (the theta statement is commented out there)
+// cells x levels 0..nVertLevels-1 (the theta statement is commented out there); under the
+// MPAS dynamics (physics = 2) also MPAS-A's surface pressure, the hydrostatic extrapolation
+// init_atm_case_jw uses (init_atm_cases.rg:519-520)
 template <int LP>
 __global__ __launch_bounds__(256) void k_output_diag(DevState S) {
     ColMap<LP> m(S, KC);
@@ -390,6 +392,12 @@ __global__ __launch_bounds__(256) void k_output_diag(DevState S) {
     double rz, zz, pb, pp;
     gather2<LP>(fd(S, F_rho_zz), c, fd(S, F_zz), c, k, rz, zz);  // (every lane: gather2)
     gather2<LP>(fd(S, F_pressure_base), c, fd(S, F_pressure_p), c, k, pb, pp);
+    if (S.physics == 2) {  // the MPAS dynamics: surface pressure (ora_mpas_surface_pressure)
+        const double q = colk(fd(S, F_qtot), c);
+        const double rq = rz * (1.0 + q), rq1 = lvl_up<LP>(rq, k);
+        const double dz0 = 1.0 / fd(S, F_rdzw)[0];
+        if (k == 0) colk(fw(S, F_surface_pressure), c) = 0.5 * dz0 * kGravity * (1.25 * rq - 0.25 * rq1) + pp + pb;
+    }
     if (k == L) return;
     colk(fw(S, F_rho), c) = PADW(rz * zz);
     colk(fw(S, F_pressure), c) = PADW(pb + pp);
@@ -399,6 +407,7 @@ static hipError_t output_diag_lp(const DevState& S, hipStream_t st) {
     const int nb = col_blocks<LP>(S, KC);
     if (nb) k_output_diag<LP><<<nb, 256, 0, st>>>(S);
     HALO_WROTE(S, F_rho, F_pressure);
+    if (S.physics == 2) HALO_WROTE(S, F_surface_pressure);
     return hipGetLastError();
 }
 hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st) {

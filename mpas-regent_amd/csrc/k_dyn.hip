@@ -16,7 +16,15 @@
 //   E  cells    del4 of w/theta (rk0), wdwz (in-lane), w scaling (Q14), buoyancy (rk0),
 //               theta advection (F of the cell's edges), perturbation flux (rk>0),
 //               wdtz (Q15, in-lane), tend_theta finish
-// rk_step > 0 runs A, B, E.  Scratch the reference writes to fields (flux_arr,
+// rk_step > 0 runs A, B, E.
+// MD (option physics = 2, the MPAS dynamics; oracle dyn_tend_impl with mpas = 1): the w
+// tendency goes to tend_w and is computed from the state w, which dyn_tend no longer
+// touches (Q8): B forms each edge's w reconstruction flux_arr (Fw, every edge: Q13) beside
+// the theta one (F), E accumulates it over the cell's edges, scales by invAreaCell, adds the
+// curvature and the vertical flux (Q14); C mixes the state w; A skips wc; q is summed once
+// (Q10), the curvature is -A - B (Q12), the top wduz/wdwz/wdtz are 0, wdtz is MPAS-A's
+// 3rd-order flux (Q15), tend_rho keeps the physics term outside the flux divergence.
+// Scratch the reference writes to fields (flux_arr,
 // ru_edge_w, wduz, q, wdwz, wdtz, u_mix) stays in registers; only their level-L
 // slots, which the reference never writes, are read from HBM.
 //
@@ -45,7 +53,7 @@ struct DynK {
 
 
 // ------------------------------------------------------------------------ A (cells)
-template <int LP, bool RK0>
+template <int LP, bool RK0, bool MD>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -145,7 +153,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     // ---- tend_rho, dpdz (:942-951)
     const double rw_p1 = lvl_up<LP>(rw, k);
     if (rk0 && k != L) {
-        colk(fw(S, F_tend_rho), c) = PADW(-hd - rdzw * (rw_p1 - rw + trp));
+        colk(fw(S, F_tend_rho), c) = PADW(MD ? -hd - rdzw * (rw_p1 - rw) + trp : -hd - rdzw * (rw_p1 - rw + trp));
         colk(fw(S, F_dpdz), c) = PADW(-kGravity * (rb * (qt) + rps * (1.0 + qt)));
     }
 
@@ -164,6 +172,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     if (ne > NF) ru_l = col_rd<LP>(ru, eoc[ne - 1], k, L);
     const double ru_lm = lvl_dn<LP>(ru_l, k);
     const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
+    if constexpr (MD) return;  // (the w tendency is formed in E from the state w)
     // (every lane goes on: the scratch wc is stored whole, 0.0 from level L up)
     double w0 = 0.0;
     if (ne > 0 && k > 0) {
@@ -185,7 +194,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 }
 
 // ------------------------------------------------------------------------ B (edges)
-template <int LP, bool RK0>
+template <int LP, bool RK0, bool MD>
 __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
@@ -213,7 +222,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // zeros), so a value used in its own lane needs none, and the vertical shuffles
     // (lvl_up/dn) of u and w bring lanes k <= L only levels <= L -- exactly what the
     // masks kept.  (Each ldz is two v_cndmask per double; B was half VALU-bound.)
-    const double wduzL = fd(S, F_wduz)[(size_t)e * LP + lpos(LP, L)];  // one value: the level-L slot
+    // one value: the level-L slot (MD: MPAS-A's wduz(nVertLevels+1) = 0)
+    const double wduzL = MD ? 0.0 : fd(S, F_wduz)[(size_t)e * LP + lpos(LP, L)];
     const int neoe = rec[21];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
@@ -245,6 +255,14 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
     gather2<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k, tv_[AF - 1], tr_phys);
 
+    // MD: the state w at the advCells, for the w reconstruction flux_arr of this edge
+    double wv_[AF];
+    if constexpr (MD) {
+        const double* w_f = fd(S, F_w);
+#pragma unroll
+        for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(w_f, ad_[j], ad_[j + 1], k, wv_[j], wv_[j + 1]);
+        wv_[AF - 1] = colk(w_f, ad_[AF - 1]);
+    }
     // loads of the later sections, also ahead of every store (a store could alias them
     // for the compiler, which would then issue them only after it)
     const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
@@ -280,11 +298,26 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         }
         colk(fw(S, X_F), e) = kl ? flux_arr : 0.0;
     }
+    if constexpr (MD) {  // flux_arr of the w advection at this edge (:1174-1197, every edge)
+        const double ru_edge_w = fzm * ru_e + fzp * lvl_dn<LP>(ru_e, k);
+        const double sg = copysign(1.0, ru_edge_w);
+        double flux_arr = 0.0;
+#pragma unroll
+        for (int j = 0; j < AF; j++) {
+            double scalar_weight = ac_[j] + sg * ac3_[j];
+            flux_arr = add_if(j < na, flux_arr, scalar_weight * wv_[j]);
+        }
+        for (int j = AF; j < na; j++) {
+            double scalar_weight = ac[j] + sg * ac3[j];
+            flux_arr += scalar_weight * colk(fd(S, F_w), ad[j]);
+        }
+        colk(fw(S, X_Fw), e) = (k > 0 && kl) ? flux_arr : 0.0;
+    }
 
     // ---- tend_u (:987-1007)
     double tend_u = -rdzw * (wduz_p - wduz);
     double q = 0.0;
-    if (a.exact_q) {
+    if (a.exact_q && !MD) {
         for (int j = 0; j < neoe; j++) {  // Q10 literal: each term added nVertLevels times
             double ue = colk(u_f, eoe[j]);
             double pve = colk(pv_f, eoe[j]);
@@ -294,7 +327,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
             }
         }
     } else {
-        const double dL = (double)L;  // Q10 value, nVertLevels * term
+        const double dL = MD ? 1.0 : (double)L;  // Q10 value, nVertLevels * term (MD: once)
 #pragma unroll
         for (int j = 0; j < QF; j++) {
             double workpv = 0.5 * (pv + pve_[j]);
@@ -308,8 +341,10 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     tend_u += rho_edge * (q - (ke2 - ke1) * invDc) - u * 0.5 * (hd1 + hd2);
     {  // curvature (:1011-1017, Q12 literal)
         const double cosA = fd(S, X_cosAngleEdge)[e], cosL = fd(S, X_cosLatEdge)[e];
-        tend_u -= (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p)) -
-                  (u * 0.25 * (w1 + w1p + w2 + w2p) * rho_edge * a.inv_r_earth);
+        const double cA = (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p));
+        const double cB = (u * 0.25 * (w1 + w1p + w2 + w2p) * rho_edge * a.inv_r_earth);
+        if (MD) tend_u = tend_u - cA - cB;
+        else tend_u -= cA - cB;
     }
 
     double tue;
@@ -393,7 +428,10 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int *cc1 = fi(S, X_ce_c1) + (size_t)c * 10, *cc2 = fi(S, X_ce_c2) + (size_t)c * 10;
     const double *cdv = fd(S, X_ce_dv) + (size_t)c * 10, *cidc = fd(S, X_ce_idc) + (size_t)c * 10;
     const double* cmsd2 = fd(S, X_ce_msd2) + (size_t)c * 10;
-    const double *rho_edge = fd(S, F_rho_edge), *wc = fd(S, X_wc), *kdiff = fd(S, F_kdiff), *tm = fd(S, F_theta_m);
+    // the w the mixing acts on: dyn_tend's partial w tendency (the reference, Q8), the state
+    // w under the MPAS dynamics
+    const double *rho_edge = fd(S, F_rho_edge), *wc = fd(S, S.physics == 2 ? F_w : X_wc), *kdiff = fd(S, F_kdiff),
+                 *tm = fd(S, F_theta_m);
     const double r_areaCell = fd(S, F_invAreaCell)[c];
     const bool del4 = a.h4 > 0.0;
 
@@ -504,7 +542,7 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
 }
 
 // ------------------------------------------------------------------------ E (cells)
-template <int LP, bool RK0, bool SELF>
+template <int LP, bool RK0, bool SELF, bool MD>
 __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -538,7 +576,14 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     // own columns (gather2: two columns per load instruction; the theta-section loads
     // too, ahead of the w stores that could alias them for the compiler)
     double wc, rw, pp, dpdz, rws, tms, tmv, twe, tte, rho_zz, rt_diab, trp, cqw = 0.0, dw_c = 0.0, dt_c = 0.0;
-    gather2<LP>(fd(S, X_wc), c, fd(S, F_rw), c, k, wc, rw);
+    // wc: the reference's partial w tendency (A); MD: the state w
+    gather2<LP>(fd(S, MD ? F_w : X_wc), c, fd(S, F_rw), c, k, wc, rw);
+    double urz = 0.0, urm = 0.0, Fw_[NF];
+    if constexpr (MD) {
+        gather2<LP>(fd(S, F_uReconstructZonal), c, fd(S, F_uReconstructMeridional), c, k, urz, urm);
+#pragma unroll
+        for (int i = 0; i < NF; i += 2) gather2s<LP>(fd(S, X_Fw), e_[i], e_[i + 1], k, Fw_[i], Fw_[i + 1]);
+    }
     gather2<LP>(fd(S, F_pressure_p), c, fd(S, F_dpdz), c, k, pp, dpdz);
     gather2<LP>(fd(S, F_rw_save), c, tms_f, c, k, rws, tms);
     gather2<LP>(tm, c, fd(S, F_tend_w_euler), c, k, tmv, twe);
@@ -593,7 +638,9 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     tmv = ldz(k <= L, tmv);
     twe = ldz(kl, twe);
     tte = ldz(kl, tte);
-    const double wdwzL = fd(S, F_wdwz)[(size_t)c * LP + lpos(LP, L)], wdtzL = fd(S, F_wdtz)[(size_t)c * LP + lpos(LP, L)];  // level-L slots
+    // level-L slots (MD: MPAS-A's top fluxes are 0)
+    const double wdwzL = MD ? 0.0 : fd(S, F_wdwz)[(size_t)c * LP + lpos(LP, L)];
+    const double wdtzL = MD ? 0.0 : fd(S, F_wdtz)[(size_t)c * LP + lpos(LP, L)];
 
     // ================= W =================
     if (del4 && kl) {  // :1258-1272
@@ -617,14 +664,40 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     const double wdwz_p = lvl_up<LP>(wdwz, k);
     const double pp_m = lvl_dn<LP>(pp, k), dpdz_m = lvl_dn<LP>(dpdz, k);
     double w = wc;
-    if (k > 0 && kl) {  // :1289-1302 (Q14 literal), :1318-1322
-        w *= invA - rdzu * (wdwz_p - wdwz);
-        if (rk0) twe -= cqw * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
-        w += twe;
-    }
-    if (k != L) {  // (padding levels: zeros, PADW)
-        colk(fw(S, F_w), c) = PADW(w);
-        if (rk0) colk(fw(S, F_tend_w_euler), c) = PADW(twe);
+    if constexpr (MD) {  // the horizontal w flux over every edge, then the area scaling
+        double hw = 0.0;
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const double ru_edge_w = fzm * ru_[i] + fzp * lvl_dn<LP>(ru_[i], k);
+            hw = sub_if(i < ne && k > 0 && kl, hw, eocs_[i] * ru_edge_w * Fw_[i]);
+        }
+        for (int i = NF; i < ne; i++) {
+            const double ru_k = ldz(kl, colk(ru, eoc[i])), ru_edge_w = fzm * ru_k + fzp * lvl_dn<LP>(ru_k, k);
+            hw = sub_if(k > 0 && kl, hw, eocs[i] * ru_edge_w * colk(fd(S, X_Fw), eoc[i]));
+        }
+        const double rz_m = lvl_dn<LP>(rho_zz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
+        const double coslat = fd(S, X_cosLatCell)[c];
+        const double aa = fzm * urz + fzp * urz_m, bb = fzm * urm + fzp * urm_m;
+        const double curv = (rho_zz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
+                            2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rho_zz * fzm + rz_m * fzp);
+        w = 0.0;
+        if (k > 0 && kl) {
+            w = hw * invA + curv - rdzu * (wdwz_p - wdwz);
+            if (rk0) twe -= cqw * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
+            w += twe;
+        }
+        colk(fw(S, F_tend_w), c) = PADW(w);
+        if (rk0 && k != L) colk(fw(S, F_tend_w_euler), c) = PADW(twe);
+    } else {
+        if (k > 0 && kl) {  // :1289-1302 (Q14 literal), :1318-1322
+            w *= invA - rdzu * (wdwz_p - wdwz);
+            if (rk0) twe -= cqw * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
+            w += twe;
+        }
+        if (k != L) {  // (padding levels: zeros, PADW)
+            colk(fw(S, F_w), c) = PADW(w);
+            if (rk0) colk(fw(S, F_tend_w_euler), c) = PADW(twe);
+        }
     }
 
     // ================= theta =================
@@ -662,14 +735,22 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     // wdtz (:1406-1420, Q15 literal order); level L read from the never-written field
     const double tms_m = lvl_dn<LP>(tms, k), tm_m = lvl_dn<LP>(tmv, k);
     double wdtz = 0.0;
-    if (k > 0 && k < L - 1) wdtz = ((rws - rw) * (fzm * tms + fzp * tms_m));
-    if (k == 1) wdtz += rw * (fzm * tmv + fzp * tm_m);
-    if (k == L - 1) wdtz = rws * (fzm * tms + fzp * tms_m);
+    if constexpr (MD) {  // MPAS-A: 3rd-order flux of theta_m by rw + the rtheta_pp redefinition term
+        const double tm_m2 = lvl_dn2<LP>(tmv, k), tm_p = lvl_up<LP>(tmv, k);
+        if (k == 1) wdtz = rw * (fzm * tmv + fzp * tm_m) + (rws - rw) * (fzm * tms + fzp * tms_m);
+        if (k > 1 && k < L - 1) wdtz = flux3(tm_m2, tm_m, tmv, tm_p, rw, 0.25) + (rws - rw) * (fzm * tms + fzp * tms_m);
+        if (k == L - 1) wdtz = rws * (fzm * tmv + fzp * tm_m);
+    } else {
+        if (k > 0 && k < L - 1) wdtz = ((rws - rw) * (fzm * tms + fzp * tms_m));
+        if (k == 1) wdtz += rw * (fzm * tmv + fzp * tm_m);
+        if (k == L - 1) wdtz = rws * (fzm * tms + fzp * tms_m);
+    }
     if (k == L) wdtz = wdtzL;
     const double wdtz_p = lvl_up<LP>(wdtz, k);
     if (k == L) return;  // (padding levels: zeros, PADW)
     // :1422-1427, :1477-1479
-    tend_theta *= invA - rdzw * (wdtz_p - wdtz);
+    if (MD) tend_theta = tend_theta * invA - rdzw * (wdtz_p - wdtz);
+    else tend_theta *= invA - rdzw * (wdtz_p - wdtz);
     colk(fw(S, F_tend_rtheta_adv), c) = PADW(tend_theta);
     colk(fw(S, F_rthdynten), c) = PADW(tend_theta / rho_zz);
     tend_theta += rho_zz * rt_diab;
@@ -678,8 +759,8 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
-template <int LP>
-static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& in) {
+template <int LP, bool MD>
+static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs& in) {
     DynK a;
     a.rk_step = in.rk_step;
     a.horiz_mixing = in.horiz_mixing;
@@ -701,14 +782,14 @@ static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& i
     auto kA = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
         if (!nb) return;
-        if (rk0) k_dyn_A<LP, true><<<nb, 256, 0, st>>>(X, a);
-        else k_dyn_A<LP, false><<<nb, 256, 0, st>>>(X, a);
+        if (rk0) k_dyn_A<LP, true, MD><<<nb, 256, 0, st>>>(X, a);
+        else k_dyn_A<LP, false, MD><<<nb, 256, 0, st>>>(X, a);
     };
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
-        if (rk0) k_dyn_B<LP, true><<<nb, 256, 0, st>>>(X, a);
-        else k_dyn_B<LP, false><<<nb, 256, 0, st>>>(X, a);
+        if (rk0) k_dyn_B<LP, true, MD><<<nb, 256, 0, st>>>(X, a);
+        else k_dyn_B<LP, false, MD><<<nb, 256, 0, st>>>(X, a);
     };
     auto kC = [&](const DevState& X) {  // vertex blocks (del4) first, then cell blocks
         const int nv = del4 ? col_blocks<LP>(X, KV) : 0, nb = nv + col_blocks<LP>(X, KC);
@@ -724,35 +805,44 @@ static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& i
         const int nb = col_blocks<LP>(X, KC);
         if (!nb) return;
         if (rk0) {
-            if (X.selfc) k_dyn_E<LP, true, true><<<nb, 256, 0, st>>>(X, a);
-            else k_dyn_E<LP, true, false><<<nb, 256, 0, st>>>(X, a);
+            if (X.selfc) k_dyn_E<LP, true, true, MD><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_E<LP, true, false, MD><<<nb, 256, 0, st>>>(X, a);
         } else {
-            if (X.selfc) k_dyn_E<LP, false, true><<<nb, 256, 0, st>>>(X, a);
-            else k_dyn_E<LP, false, false><<<nb, 256, 0, st>>>(X, a);
+            if (X.selfc) k_dyn_E<LP, false, true, MD><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_E<LP, false, false, MD><<<nb, 256, 0, st>>>(X, a);
         }
     };
     // halo: fields each kernel gathers through an index array / fields it writes
     HALO_RUN(S, st, kA, F_ru, F_u, F_v);
-    HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz, X_wc);
+    HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz);
+    if (!MD) HALO_WROTE(S, X_wc);
     if (rk0) {
         HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p, F_zz, F_dpdz,
                  F_divergence, F_kdiff, F_vorticity);
         HALO_WROTE(S, X_F, F_tend_u, F_tend_u_euler, F_delsq_u);
-        HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, X_wc, F_theta_m);
+        if (MD) HALO_WROTE(S, X_Fw);
+        if (MD) HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, F_w, F_theta_m);
+        else HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, X_wc, F_theta_m);
         HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
                    F_tend_theta_euler);
         if (del4) {
             HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
             HALO_WROTE(S, F_tend_u_euler, F_tend_u);
         }
-        HALO_RUN(S, st, kE, F_ru, X_F, F_delsq_w, F_delsq_theta);
+        HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
     } else {
         HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
         HALO_WROTE(S, X_F, F_tend_u);
-        HALO_RUN(S, st, kE, F_ru, X_F, F_ru_save, F_theta_m_save);
+        if (MD) HALO_WROTE(S, X_Fw);
+        HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);
     }
-    HALO_WROTE(S, F_w, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
+    HALO_WROTE(S, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
+    HALO_WROTE(S, MD ? F_tend_w : F_w);
     return hipGetLastError();
+}
+template <int LP>
+static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& in) {
+    return S.physics == 2 ? dyn_lp_md<LP, true>(S, st, in) : dyn_lp_md<LP, false>(S, st, in);
 }
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& in) {
     MPAS_LP_DISPATCH(S.LP, dyn_lp, S, st, in);

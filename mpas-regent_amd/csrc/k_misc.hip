@@ -22,6 +22,8 @@ __global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
     const double *tm = fd(S, F_theta_m), *rz = fd(S, F_rho_zz);
     double *rws = fw(S, F_rw_save), *rtps = fw(S, F_rtheta_p_save), *rps = fw(S, F_rho_p_save);
     double *w2 = fw(S, F_w_2), *tm2 = fw(S, F_theta_m_2), *rz2 = fw(S, F_rho_zz_2), *rzo = fw(S, F_rho_zz_old_split);
+    double* tms = fw(S, F_theta_m_save);
+    const bool md = S.physics == 2;  // the MPAS dynamics: theta_m_save = theta_m (never written, Q2)
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
         if (plev(S.LP, (int)(i & (size_t)(S.LP - 1))) == S.L) continue;  // (padding copied: zeros, full 64-B sectors)
         rws[i] = rw[i];
@@ -29,6 +31,7 @@ __global__ __launch_bounds__(256) void k_setup_cells(DevState S) {
         rps[i] = rp[i];
         w2[i] = w[i];
         tm2[i] = tm[i];
+        if (md) tms[i] = tm[i];
         double r = rz[i];
         rz2[i] = r;
         rzo[i] = r;
@@ -53,6 +56,7 @@ hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st) {
     k_setup_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
     HALO_WROTE(S, F_ru_save, F_u_2, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2,
                F_rho_zz_old_split);
+    if (S.physics == 2) HALO_WROTE(S, F_theta_m_save);
     return hipGetLastError();
 }
 
@@ -73,9 +77,26 @@ __global__ __launch_bounds__(256) void k_moist(DevState S) {
         }
     }
 }
+// the MPAS dynamics (physics = 2): the edge loop of :491-501 the reference comments out
+// (Q25), cqu = 1 / (1 + qtotal), qtotal = 0.5 (qtot(cell1) + qtot(cell2)) of the qtot the
+// cell loop has just zeroed everywhere (the zero slot is 0 too)
+__global__ __launch_bounds__(256) void k_moist_edges(DevState S) {
+    const size_t n = (size_t)S.nEO * S.LP;
+    double* cqu = fw(S, F_cqu);
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const int k = plev(S.LP, (int)(i & (size_t)(S.LP - 1)));
+        if (k == S.L) continue;
+        const double q1 = 0.0, q2 = 0.0, qtotal = 0.5 * (q1 + q2);
+        cqu[i] = k > S.L ? 0.0 : 1.0 / (1.0 + qtotal);
+    }
+}
 hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
     k_moist<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
     HALO_WROTE(S, F_qtot, F_cqw);
+    if (S.physics == 2) {
+        k_moist_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S);
+        HALO_WROTE(S, F_cqu);
+    }
     return hipGetLastError();
 }
 
@@ -176,7 +197,9 @@ hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts) 
 }
 
 // ---------------------------------------------------------------- set_smlstep
-template <int LP>
+// MD: the MPAS dynamics (physics = 2, ora_mpas_set_smlstep): u_tend is dyn_tend's tend_u
+// and w_tend its tend_w (Q2/Q8), levels 1..L-1 of every cell within the relaxation zone
+template <int LP, bool MD>
 __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -185,13 +208,14 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* sgn = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
-    const double* ut_f = fd(S, F_u_tend);
+    const double* ut_f = fd(S, MD ? F_tend_u : F_u_tend);
+    const int wf = MD ? F_tend_w : F_w;
     const double* zb = fd(S, F_zb_cell);
     const double* zb3 = fd(S, F_zb3_cell);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double zz = col_rd<LP>(fd(S, F_zz), c, k, L);
     const double zz_m = lvl_dn<LP>(zz, k);
-    double w = col_rd<LP>(fd(S, F_w), c, k, L);
+    double w = col_rd<LP>(fd(S, wf), c, k, L);
     int e_[NF];
     double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgn_[NF];
     row_ld(eoc, e_);
@@ -221,16 +245,27 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
         w -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
     }
     w *= (fzm * zz + fzp * zz_m);
-    if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) colk(fw(S, F_w), c) = w;
+    if (MD) {
+        if (k >= 1 && k < L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone) colk(fw(S, wf), c) = w;
+    } else if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) {
+        colk(fw(S, wf), c) = w;
+    }
 }
 template <int LP>
 static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
+    const bool md = S.physics == 2;
     auto run = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
-        if (nb) k_set_smlstep<LP><<<nb, 256, 0, st>>>(X);
+        if (nb && md) k_set_smlstep<LP, true><<<nb, 256, 0, st>>>(X);
+        else if (nb) k_set_smlstep<LP, false><<<nb, 256, 0, st>>>(X);
     };
-    HALO_RUN(S, st, run, F_u_tend);
-    HALO_WROTE(S, F_w);
+    if (md) {
+        HALO_RUN(S, st, run, F_tend_u);
+        HALO_WROTE(S, F_tend_w);
+    } else {
+        HALO_RUN(S, st, run, F_u_tend);
+        HALO_WROTE(S, F_w);
+    }
     return hipGetLastError();
 }
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st); }
@@ -335,7 +370,9 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
         wwAvgS[i] = s;
         if (substep == split) {
             wwAvg[i] = s * inv_split;
-            rho_zz[i] = fd(S, F_rho_zz_old_split)[i];
+            // MPAS-A resets rho_zz of the OLD time level (rho_zz_1); the port has one time
+            // level, so the MPAS dynamics (physics = 2) keeps the new rho_zz
+            if (S.physics != 2) rho_zz[i] = fd(S, F_rho_zz_old_split)[i];
         }
     }
 }

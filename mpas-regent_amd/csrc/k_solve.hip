@@ -12,7 +12,10 @@
 
 namespace mpas {
 
-template <int LP, int EPW>
+// MD: the MPAS dynamics (physics = 2, ora_mpas_solve_diagnostics): divergence += s * u (Q9),
+// h = rho_zz and rho_edge = h_edge (Q2: MPAS-A passes diag%rho_edge as h_edge), v over
+// every edgesOnEdge entry (Q23)
+template <int LP, int EPW, bool MD>
 __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int hollingsworth_part) {
     const int L = S.L;
     const double* u = fd(S, F_u);
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         for (int i = 0; i < NF; i++) {
             const double uu = u_[j][i];
             double s = sgn_[j][i] * dv_[j][i];
-            div = add_if(i < ne[j], div, s + uu);
+            div = add_if(i < ne[j], div, MD ? s * uu : s + uu);
             // ke_edge(iEdge,k) exactly as the edge loop (:352) writes it; the zero slot
             // row of ke_edge is never written, and its recomputation is 0*0*0 as well
             double efac = dc_[j][i] * dv_[j][i];
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
             int iEdge = eoc[i];
             double uu = colk(u, iEdge);
             double s = sgn[i] * dvEdge[iEdge];
-            div += s + uu;
+            div += MD ? s * uu : s + uu;
             double efac = dcEdge[iEdge] * dvEdge[iEdge];
             double kee = (iEdge < S.nEdges) ? efac * (uu * uu) : 0.0;
             ke += 0.25 * kee;
@@ -137,14 +140,14 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
     colk(fw(S, F_ke), c) = ke;
 }
 
-template <int LP, bool RECON_V>
+template <int LP, bool RECON_V, bool MD>
 __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
     ColMap<LP> m(S, KE);
     const int L = S.L, e = m.ent, k = m.k;
     if (e >= S.nEO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
     const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
     const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
-    const double *h = fd(S, F_h), *u = fd(S, F_u), *pvv = fd(S, F_pv_vertex);
+    const double *h = fd(S, MD ? F_rho_zz : F_h), *u = fd(S, F_u), *pvv = fd(S, F_pv_vertex);
     // every load before the first store (the stores could alias them for the compiler)
     double h1, h2, uu, pv1, pv2;
     gather2s<LP>(h, coe[0], coe[1], k, h1, h2);
@@ -158,38 +161,45 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
         row_ld(eoe, ee_);
         row_ld(wts, wts_);
         static_assert(QF == 10, "pairs below");
+        if (MD) {
 #pragma unroll
-        for (int i = 1; i < QF - 1; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
-        gather2s<LP>(u, ee_[QF - 1], e, k, ue[QF - 1], uu);
+            for (int i = 0; i < QF; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
+            uu = colk(u, e);
+        } else {
+#pragma unroll
+            for (int i = 1; i < QF - 1; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
+            gather2s<LP>(u, ee_[QF - 1], e, k, ue[QF - 1], uu);
+        }
     } else {
         uu = colk(u, e);
     }
     if (k == L) return;  // (padding levels k > L: zeros, PADW)
     colk(fw(S, F_h_edge), e) = PADW(0.5 * (h1 + h2));
+    if (MD) colk(fw(S, F_rho_edge), e) = PADW(0.5 * (h1 + h2));
     const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
     colk(fw(S, F_ke_edge), e) = PADW(efac * (uu * uu));
     if (RECON_V) {  // Q23: the sum starts at i = 1
         double v = 0;
 #pragma unroll
-        for (int i = 1; i < QF; i++) v = add_if(i < neoe, v, wts_[i] * ue[i]);
+        for (int i = MD ? 0 : 1; i < QF; i++) v = add_if(i < neoe, v, wts_[i] * ue[i]);
         for (int i = QF; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
         colk(fw(S, F_v), e) = PADW(v);
     }
     colk(fw(S, F_pv_edge), e) = PADW(0.5 * (pv1 + pv2));
 }
 
-template <int LP>
-static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
+template <int LP, bool MD>
+static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
     auto kvc = [&](const DevState& X) {  // vertex blocks, then cell blocks
         if (X.epw == 4) {
             const int nv = col_blocks_n<LP, 4>(X, KV), nb = nv + col_blocks_n<LP, 4>(X, KC);
-            if (nb) k_solve_vc<LP, 4><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+            if (nb) k_solve_vc<LP, 4, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
         } else if (X.epw == 2) {
             const int nv = col_blocks_n<LP, 2>(X, KV), nb = nv + col_blocks_n<LP, 2>(X, KC);
-            if (nb) k_solve_vc<LP, 2><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+            if (nb) k_solve_vc<LP, 2, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
         } else {
             const int nv = col_blocks_n<LP, 1>(X, KV), nb = nv + col_blocks_n<LP, 1>(X, KC);
-            if (nb) k_solve_vc<LP, 1><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+            if (nb) k_solve_vc<LP, 1, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
         }
     };
     auto kh = [&](const DevState& X) {
@@ -199,8 +209,8 @@ static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth,
     auto ke = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
-        if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false><<<nb, 256, 0, st>>>(X);
-        else k_solve_e<LP, true><<<nb, 256, 0, st>>>(X);
+        if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false, MD><<<nb, 256, 0, st>>>(X);
+        else k_solve_e<LP, true, MD><<<nb, 256, 0, st>>>(X);
     };
     HALO_RUN(S, st, kvc, F_u);
     HALO_WROTE(S, F_vorticity, F_pv_vertex, F_ke_vertex, F_divergence, F_ke);
@@ -208,9 +218,19 @@ static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth,
         HALO_RUN(S, st, kh, F_ke_vertex);
         HALO_WROTE(S, F_ke);
     }
-    HALO_RUN(S, st, ke, F_h, F_u, F_pv_vertex);
-    HALO_WROTE(S, F_h_edge, F_ke_edge, F_v, F_pv_edge);
+    if (MD) {
+        HALO_RUN(S, st, ke, F_rho_zz, F_u, F_pv_vertex);
+        HALO_WROTE(S, F_h_edge, F_rho_edge, F_ke_edge, F_v, F_pv_edge);
+    } else {
+        HALO_RUN(S, st, ke, F_h, F_u, F_pv_vertex);
+        HALO_WROTE(S, F_h_edge, F_ke_edge, F_v, F_pv_edge);
+    }
     return hipGetLastError();
+}
+template <int LP>
+static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
+    return S.physics == 2 ? solve_lp_md<LP, true>(S, st, hollingsworth, rk_step)
+                          : solve_lp_md<LP, false>(S, st, hollingsworth, rk_step);
 }
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step) {
     MPAS_LP_DISPATCH(S.LP, solve_lp, S, st, hollingsworth, rk_step);

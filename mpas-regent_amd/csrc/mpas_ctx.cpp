@@ -45,6 +45,7 @@ const FieldInfo kFields[X_COUNT] = {
     {"wfl", K_C2F, 2, D_M, 0, 0},
     {"wc", K_C3, 1, D_M, 0, 0},
     {"F", K_E3, 1, D_M, 0, 0},
+    {"Fw", K_E3, 1, D_M, 0, 0},
     {"Ah", K_E3, 8, D_M, 0, 0},
     {"Rp", K_C3V, 8, D_M, 0, 0},
     {"Rm", K_C3V, 8, D_M, 0, 0},
@@ -310,6 +311,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     }
     if (c->transport)  // after the last stage's recover: ruAvg / wwAvg / rho_zz of the step
         run_task(c, "atm_advance_scalars_mono", [&] { return launch_advance_scalars_mono(S, st, dt); });
+    if (S.physics == 2)  // the MPAS dynamics: cell-centre winds for the next step's curvature
+        run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });  // (:487, commented)
     run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
     // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }
@@ -442,7 +445,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "vcmix") == 0) {
             c->S.vcmix = value ? 1 : 0;
         } else if (name && std::strcmp(name, "physics") == 0) {
-            if (value != 0 && value != 1) throw Fail{MPAS_EINVAL, "physics must be 0 (reference) or 1 (MPAS vertical solver)"};
+            if (value < 0 || value > 2)
+                throw Fail{MPAS_EINVAL, "physics must be 0 (reference), 1 (MPAS vertical solver) or 2 (MPAS dynamics)"};
             c->S.physics = (int)value;
             if (!value) c->transport = 0;
         } else if (name && std::strcmp(name, "trorder") == 0) {

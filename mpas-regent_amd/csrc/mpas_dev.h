@@ -67,6 +67,8 @@ enum FieldId {
                 // the U section still reads the pre-zeroing w (:1013)
     X_F,        // flux_arr of the theta advection (:1333-1340) per edge and level: it
                 // depends only on the edge, so it is formed once per edge, not per cell
+    X_Fw,       // the same for the w advection of the MPAS dynamics (physics = 2: every
+                // edge's flux_arr over the state w, :1174-1205 without Q13)
     // monotonic scalar transport (k_transport.hip), one column per (entity, scalar)
     X_Ah,       // antidiffusive edge flux                                      E3 x 8
     X_Rp,       // R+ (fraction of the incoming antidiffusive flux allowed)     C3V x 8
@@ -93,7 +95,9 @@ struct DevState {
     int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
     int vcmix;  // 1: the vertex and cell blocks of mixed grids interleaved in proportion (vc_block)
     int tro;      // transport slot order (k_transport.hip tr_slot): 0 entity-major, 1 pair-major
-    int physics;  // 0: the reference's vertical solver (quirks Q16-Q21), 1: the MPAS form (option "physics")
+    int physics;  // option "physics": 0 the reference's semantics; 1 the MPAS vertical solver
+                  // (Q16-Q21, Q24, Q5, Q7); 2 also the MPAS dynamics (dyn_tend, solve_diagnostics,
+                  // set_smlstep, setup, moist, finish in MPAS-A's forms: mpas_oracle.c ora_mpas_*)
     int xcd;  // block order: 0 dispatcher, 1 one contiguous eighth per XCD, G > 1 runs of G
               // blocks per XCD in windows of 8G (default 64)
     int selfc;  // 1 when every cell is one of the two cellsOnEdge of each of its first

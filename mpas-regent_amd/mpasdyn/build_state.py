@@ -249,12 +249,15 @@ def geometry(m, st):
 MESH_FIELDS = tuple(f.name for f in FIELDS if f.dist == "M" or f.kind == "ZV")
 
 
-def build_state(m, nVertLevels, variant="ref", seed=20211015, oracle_fill=None, vertical=True, mesh_only=False):
+def build_state(m, nVertLevels, variant="ref", seed=20211015, oracle_fill=None, vertical=True, mesh_only=False,
+                extra_names=()):
     """Return a HostState for mesh m.  ``oracle_fill(state, seed, include_mesh)`` fills the
     synthetic fields on the host (tests pass the oracle's generator); None leaves them 0
     (the benchmark fills them on the device).  mesh_only: allocate only the mesh and
-    vertical-grid fields (MESH_FIELDS), for device-filled benchmark states."""
-    st = HostState(m.nCells, m.nEdges, m.nVertices, nVertLevels, names=MESH_FIELDS if mesh_only else None)
+    vertical-grid fields (MESH_FIELDS), for device-filled benchmark states, plus
+    `extra_names` (e.g. the fields an initial state writes)."""
+    names = (MESH_FIELDS + tuple(extra_names)) if mesh_only else None
+    st = HostState(m.nCells, m.nEdges, m.nVertices, nVertLevels, names=names)
     nC, nE, nV, L = m.nCells, m.nEdges, m.nVertices, nVertLevels
     R = SPHERE_RADIUS
     connectivity(m, st)
@@ -294,6 +297,55 @@ def build_state(m, nVertLevels, variant="ref", seed=20211015, oracle_fill=None, 
         st["defc_a"][:nC] = np.where(np.arange(10)[None, :] < m.nEdgesOnCell[:, None], 0.1, 0.0)
         st["defc_b"][:nC] = np.where(np.arange(10)[None, :] < m.nEdgesOnCell[:, None], 0.05, 0.0)
     return st
+
+
+def mpas_mesh_coefficients(m, st):
+    """The mesh coefficients of MPAS-A's init that the reference never computes (Q2), for
+    the MPAS dynamics (option physics = 2) on a 0-based mesh:
+
+    * defc_a / defc_b (Smagorinsky deformation weights, MPAS-A init's
+      atm_initialize_deformation_weights): with theta the angle of an edge normal to
+      the local east of the CELL (the 3-D normal from angleEdge at the edge, seen in the
+      cell's east/north frame) and s = edgesOnCell_sign,
+      d_diag = u_x - v_y = sum s dv (cos 2theta u - sin 2theta v) / area,
+      d_off  = u_y + v_x = sum s dv (sin 2theta u + cos 2theta v) / area
+      (divergence theorem with u = u_n cos - v_t sin, v = u_n sin + v_t cos), so
+      defc_a = s dv cos(2 theta) / area, defc_b = s dv sin(2 theta) / area;
+    * coeffs_reconstruct (cell-centre velocity from the normal components, read by
+      mpas_reconstruct_2d, dynamics_tasks.rg:1894-1948): the least-squares tangent
+      vector U minimising sum_i (U . n_i - u_i)^2 over the cell's edges, in the local
+      (east, north) basis, mapped to Cartesian (x, y, z) -- the role MPAS-A's RBF
+      reconstruction plays (a regularised variant of the same fit)."""
+    nC, nE = m.nCells, m.nEdges
+    ne = np.asarray(m.nEdgesOnCell)
+    eoc = np.asarray(st["edgesOnCell"][:nC], dtype=np.int64)
+    on = np.arange(10)[None, :] < ne[:, None]
+    e = np.where(on, eoc, 0)
+
+    def frame(lat, lon):  # local east and north unit vectors (Cartesian)
+        east = np.stack([-np.sin(lon), np.cos(lon), np.zeros_like(lon)], axis=-1)
+        north = np.stack([-np.sin(lat) * np.cos(lon), -np.sin(lat) * np.sin(lon), np.cos(lat)], axis=-1)
+        return east, north
+    # each edge normal in 3-D from angleEdge at the edge, then its angle in the frame of
+    # the cell centre (near the poles the local east rotates between edge and cell)
+    ee, en = frame(np.asarray(m.latEdge), np.asarray(m.lonEdge))
+    th_e = st["angleEdge"][:nE, 0]
+    n3 = np.cos(th_e)[:, None] * ee + np.sin(th_e)[:, None] * en  # (nE, 3)
+    lat, lon = np.asarray(m.latCell), np.asarray(m.lonCell)
+    east, north = frame(lat, lon)  # (nC, 3)
+    nx = np.einsum("cid,cd->ci", n3[e], east)
+    ny = np.einsum("cid,cd->ci", n3[e], north)
+    th = np.arctan2(ny, nx)  # (nC, 10)
+    dv = st["dvEdge"][:nE, 0][e]
+    sg = st["edgesOnCell_sign"][:nC]
+    invA = st["invAreaCell"][:nC, 0][:, None]
+    st["defc_a"][:nC] = np.where(on, sg * dv * np.cos(2.0 * th) * invA, 0.0)
+    st["defc_b"][:nC] = np.where(on, sg * dv * np.sin(2.0 * th) * invA, 0.0)
+    n = np.stack([np.cos(th), np.sin(th)], axis=2) * on[:, :, None]  # (nC, 10, 2)
+    ntn = np.einsum("cid,cie->cde", n, n)
+    coef = np.einsum("cde,cie->cdi", np.linalg.inv(ntn), n)  # (nC, 2, 10): east, north weights
+    xyz = coef[:, 0, :, None] * east[:, None, :] + coef[:, 1, :, None] * north[:, None, :]  # (nC, 10, 3)
+    st["coeffs_reconstruct"][:nC] = np.where(on[:, :, None], xyz, 0.0).reshape(nC, 30)
 
 
 def adv_coef_compression_connectivity_only(m, st):

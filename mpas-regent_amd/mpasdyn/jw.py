@@ -15,7 +15,8 @@ Host-side, one-time (like the other precompute of build_state.py); the hot path 
 from this state.  Fields written: the vertical grid (rdzw, rdzu, fzm, fzp, cf1..cf3), zgrid,
 zz, zxu, dss, pressure_base, rho_base, rtheta_base, exner_base, exner, pressure_p,
 rho_p, rho_zz, theta_m, rtheta_p, surface_pressure, u, ru, v, rw, w, zb_cell, zb3_cell,
-rho, theta, fVertex, cqu (1: dry)."""
+rho, theta, fVertex, cqu (1: dry), and the mesh coefficients defc_a, defc_b,
+coeffs_reconstruct (build_state.mpas_mesh_coefficients)."""
 import numpy as np
 
 from .build_state import OMEGA, SPHERE_RADIUS
@@ -63,9 +64,12 @@ def _jw_temperature(eta, phi):
         + (1.6 * c ** 3 * (s ** 2 + 2.0 / 3.0) - np.pi / 4.0) * SPHERE_RADIUS * OMEGA)
 
 
-def init_atm_case_jw(m, st):
+def init_atm_case_jw(m, st, perturb=False):
     """Fill the JW state into HostState st (built by build_state(m, L, "physical") on a
-    0-based mesh m).  Returns st."""
+    0-based mesh m).  perturb: add the test case's zonal-wind perturbation (1 m/s Gaussian
+    of radius a/10 at 20E 40N, Jablonowski & Williamson 2006; MPAS-A's
+    init_atm_case_jw with config_init_case = 2) -- the reference's own branch is dead
+    (u_pert = 0, :552-555).  Returns st."""
     nC, nE, nV, L = m.nCells, m.nEdges, m.nVertices, st.L
     if L < 3:
         raise ValueError("the JW state needs nVertLevels >= 3 (cf1..cf3 use three levels)")
@@ -101,20 +105,31 @@ def init_atm_case_jw(m, st):
     ex_b = (pb / P0) ** (RGAS / CP)
     rb = pb / (RGAS * T0B * zz)
     tb = T0B / ex_b
-    pp = np.zeros_like(pb)
-    rr = np.zeros_like(pb)
     dzw, dzu, fzm, fzp = g["dzw"], g["dzu"], g["fzm"], g["fzp"]
-    for _ in range(10):
-        eta = (pb + pp) / P0
-        tt = _jw_temperature(eta, phi)
-        for _ in range(25):
-            rr = (pp / (RGAS * zz) - rb * (tt - T0B)) / tt
-            ppi = np.empty_like(pp)
-            ppi[:, 0] = P0 - 0.5 * dzw[0] * GRAVITY * (1.25 * (rr[:, 0] + rb[:, 0]) - 0.25 * (rr[:, 1] + rb[:, 1]))
-            ppi[:, 0] -= pb[:, 0]
-            for k in range(L - 1):
-                ppi[:, k + 1] = ppi[:, k] - dzu[k + 1] * GRAVITY * (rr[:, k] * fzp[k + 1] + rr[:, k + 1] * fzm[k + 1])
-            pp = 0.2 * ppi + 0.8 * pp
+    # the iteration runs level-major (contiguous level rows: the k loop is the slow axis),
+    # over chunks of columns small enough to stay in cache (it is column-independent)
+    # the level recurrence ppi(k+1) = ppi(k) - t(k) is np.subtract.accumulate over levels
+    # (the same sequential roundings as the level loop)
+    pp, rr, tt = np.zeros_like(pb), np.zeros_like(pb), np.zeros_like(pb)
+    cdz = (dzu[1:L] * GRAVITY)[:, None]
+    fzp1, fzm1 = fzp[1:L][:, None], fzm[1:L][:, None]
+    CH = 16384
+    for c0 in range(0, nC, CH):
+        sl = slice(c0, min(c0 + CH, nC))
+        pbT, rbT, zzT = np.ascontiguousarray(pb[sl].T), np.ascontiguousarray(rb[sl].T), np.ascontiguousarray(zz[sl].T)
+        ppT = np.zeros_like(pbT)
+        rrT = np.zeros_like(pbT)
+        acc = np.empty_like(ppT)
+        for _ in range(10):
+            ttT = np.ascontiguousarray(_jw_temperature(((pbT + ppT) / P0).T, phi[sl]).T)
+            for _ in range(25):
+                rrT = (ppT / (RGAS * zzT) - rbT * (ttT - T0B)) / ttT
+                acc[0] = P0 - 0.5 * dzw[0] * GRAVITY * (1.25 * (rrT[0] + rbT[0]) - 0.25 * (rrT[1] + rbT[1]))
+                acc[0] -= pbT[0]
+                acc[1:] = cdz * (rrT[:-1] * fzp1 + rrT[1:] * fzm1)
+                ppi = np.subtract.accumulate(acc, axis=0)
+                ppT = 0.2 * ppi + 0.8 * ppT
+        pp[sl], rr[sl], tt[sl] = ppT.T, rrT.T, ttT.T
     exner = ((pb + pp) / P0) ** (RGAS / CP)
     theta_m = tt / exner
     rho_zz = rb + rr
@@ -138,6 +153,12 @@ def init_atm_case_jw(m, st):
     ptot = pb + pp
     ev = (0.5 * (ptot[c1] + ptot[c2]) / P0 - 0.252) * np.pi / 2.0
     u = U0 * flux[:, None] * np.cos(ev) ** 1.5
+    if perturb:
+        lat_e, lon_e = np.asarray(m.latEdge), np.asarray(m.lonEdge)
+        lat_c, lon_c = 2.0 * np.pi / 9.0, np.pi / 9.0
+        r = np.arccos(np.clip(np.sin(lat_c) * np.sin(lat_e) + np.cos(lat_c) * np.cos(lat_e) * np.cos(lon_e - lon_c),
+                              -1.0, 1.0))
+        u = u + (1.0 * np.exp(-(r * 10.0) ** 2) * np.cos(np.asarray(m.angleEdge)))[:, None]
     st["u"][:nE, :L] = u
     st["ru"][:nE, :L] = 0.5 * (rho_zz[c1] + rho_zz[c2]) * u
     st["fVertex"][:nV, 0] = 2.0 * OMEGA * np.sin(np.asarray(m.latVertex))
@@ -183,11 +204,26 @@ def init_atm_case_jw(m, st):
     st["rho"][:nC, :L] = rho_zz * zz
     st["theta"][:nC, :L] = theta_m
     st["cqu"][:nE, :L] = 1.0
+    # the mesh coefficients MPAS-A's init computes and the reference never writes (Q2):
+    # Smagorinsky deformation weights and the cell-centre velocity reconstruction
+    from .build_state import mpas_mesh_coefficients
+    mpas_mesh_coefficients(m, st)
     return st
 
 
-def jw_state(m0, L):
-    """build_state(physical) + init_atm_case_jw for a 0-based mesh m0"""
+# the 3-D fields init_atm_case_jw writes (the rest of the state stays 0)
+JW_FIELDS = ("zgrid", "zz", "zxu", "dss", "pressure_base", "rho_base", "rtheta_base", "exner_base", "exner",
+             "pressure_p", "rho_p", "rho_zz", "theta_m", "rtheta_p", "surface_pressure", "u", "ru", "v", "rw", "w",
+             "zb_cell", "zb3_cell", "rho", "theta", "cqu", "coeffs_reconstruct")
+
+
+def jw_state(m0, L, perturb=False, subset=False, extra_names=()):
+    """build_state(physical) + init_atm_case_jw for a 0-based mesh m0.  subset: a HostState
+    with only the mesh fields, JW_FIELDS and `extra_names` (large meshes; the others are the
+    zeros a fresh context holds)"""
     from .build_state import build_state
-    st = build_state(m0, L, "physical", vertical=False)
-    return init_atm_case_jw(m0, st)
+    if subset:
+        st = build_state(m0, L, "physical", vertical=False, mesh_only=True, extra_names=JW_FIELDS + tuple(extra_names))
+    else:
+        st = build_state(m0, L, "physical", vertical=False)
+    return init_atm_case_jw(m0, st, perturb=perturb)

@@ -333,9 +333,8 @@ void ora_atm_rk_integration_setup(ora_state* S) {
  * horiz_mixing: 0 = "2d_smagorinsky", 1 = "2d_fixed", other = neither.
  * The v_mom/v_theta_eddy_visc2 branches (:1094-1146, :1304-1315, :1430-1475) are dead
  * code under constants.rg:47-48 (both 0.0) and are not restated.                    */
-void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int horiz_mixing,
-                                   double config_mpas_cam_coef, int config_mix_full,
-                                   int config_rayleigh_damp_u) {
+static void dyn_tend_impl(ora_state* S, int rk_step, double dt, int horiz_mixing, double config_mpas_cam_coef,
+                          int config_mix_full, int config_rayleigh_damp_u, int mpas) {
     (void)config_mix_full;
     const int L = S->L, nC = S->nCells, nE = S->nEdges, nV = S->nVertices;
     double prandtl_inv = 1.0 / prandtl;
@@ -408,8 +407,12 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
 #pragma omp parallel for schedule(static)
         for (long c = 0; c < nC; c++)
             for (int k = 0; k < L; k++) {
-                CW(tend_rho, c, k) = -CW(h_divergence, c, k) -
-                                     rdzw[k] * (rc(S, rw, c, k + 1) - CW(rw, c, k) + CW(D(tend_rho_physics), c, k));
+                if (mpas) /* MPAS-A: the physics tendency outside the vertical flux divergence */
+                    CW(tend_rho, c, k) = -CW(h_divergence, c, k) - rdzw[k] * (rc(S, rw, c, k + 1) - CW(rw, c, k)) +
+                                         CW(D(tend_rho_physics), c, k);
+                else
+                    CW(tend_rho, c, k) = -CW(h_divergence, c, k) -
+                                         rdzw[k] * (rc(S, rw, c, k + 1) - CW(rw, c, k) + CW(D(tend_rho_physics), c, k));
                 CW(dpdz, c, k) = -gravity * (CW(D(rho_base), c, k) * (CW(D(qtot), c, k)) +
                                              CW(D(rho_p_save), c, k) * (1.0 + CW(D(qtot), c, k)));
             }
@@ -444,22 +447,29 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
         int cell1 = ie2(S, cellsOnEdge, e, 2, 0), cell2 = ie2(S, cellsOnEdge, e, 2, 1);
         int neoe = ie2(S, I(nEdgesOnEdge), e, 1, 0);
         for (int k = 0; k < L; k++) {
-            CW(tend_u, e, k) = -rdzw[k] * (re(S, wduz, e, k + 1) - CW(wduz, e, k));
+            /* (mpas: wduz(nVertLevels) = 0, MPAS-A's top boundary; the reference reads the
+             * never-written level-L slot) */
+            const double wduz_p = (mpas && k + 1 == L) ? 0.0 : re(S, wduz, e, k + 1);
+            CW(tend_u, e, k) = -rdzw[k] * (wduz_p - CW(wduz, e, k));
             CW(q, e, k) = 0.0;
             for (int j = 0; j < neoe; j++) { /* Q10: each term accumulated nVertLevels times */
                 int eoe = ie2(S, I(edgesOnEdge), e, 20, j);
-                for (int kk = 0; kk < L; kk++) {
+                for (int kk = 0; kk < (mpas ? 1 : L); kk++) { /* (mpas: once) */
                     double workpv = 0.5 * (CW(pv_edge, e, k) + re(S, pv_edge, eoe, k));
                     CW(q, e, k) += re2(S, D(weightsOnEdge), e, 20, j) * re(S, u, eoe, k) * workpv;
                 }
             }
             CW(tend_u, e, k) += CW(rho_edge, e, k) * (CW(q, e, k) - (rc(S, ke, cell2, k) - rc(S, ke, cell1, k)) * re2(S, invDcEdge, e, 1, 0)) -
                                 CW(u, e, k) * 0.5 * (rc(S, h_divergence, cell1, k) + rc(S, h_divergence, cell2, k));
-            /* Q12: -= (A) - (B), literal */
-            CW(tend_u, e, k) -= (2.0 * omega_c * cos(re2(S, cosA, e, 1, 0)) * cos(re2(S, latE, e, 1, 0)) * CW(rho_edge, e, k) * 0.25 *
-                                 (rc(S, w, cell1, k) + rc(S, w, cell1, k + 1) + rc(S, w, cell2, k) + rc(S, w, cell2, k + 1))) -
-                                (CW(u, e, k) * 0.25 * (rc(S, w, cell1, k) + rc(S, w, cell1, k + 1) + rc(S, w, cell2, k) + rc(S, w, cell2, k + 1)) *
-                                 CW(rho_edge, e, k) * inv_r_earth);
+            /* Q12: -= (A) - (B), literal; mpas: tend_u - A - B */
+            const double cA = (2.0 * omega_c * cos(re2(S, cosA, e, 1, 0)) * cos(re2(S, latE, e, 1, 0)) * CW(rho_edge, e, k) * 0.25 *
+                               (rc(S, w, cell1, k) + rc(S, w, cell1, k + 1) + rc(S, w, cell2, k) + rc(S, w, cell2, k + 1)));
+            const double cB = (CW(u, e, k) * 0.25 * (rc(S, w, cell1, k) + rc(S, w, cell1, k + 1) + rc(S, w, cell2, k) + rc(S, w, cell2, k + 1)) *
+                               CW(rho_edge, e, k) * inv_r_earth);
+            if (mpas)
+                CW(tend_u, e, k) = CW(tend_u, e, k) - cA - cB;
+            else
+                CW(tend_u, e, k) -= cA - cB;
         }
     }
 
@@ -533,10 +543,15 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
     for (long e = 0; e < nE; e++) /* :1161-1163 */
         for (int k = 0; k < L; k++) CW(tend_u, e, k) += CW(tend_u_euler, e, k) + CW(D(tend_ru_physics), e, k);
 
-    /* -------- W section -------- */
+    /* -------- W section --------
+     * tw: where the w tendency accumulates (the state w in the reference, Q8; tend_w in
+     * mpas mode); wr: the w the tendency is computed from (the reference reads its own
+     * partial tendency there, Q8/Q13; mpas mode the state w)                          */
+    double* tw = mpas ? D(tend_w) : w;
+    double* wr = mpas ? w : tw;
 #pragma omp parallel for schedule(static)
     for (long c = 0; c < nC; c++) /* :1170-1172 */
-        for (int k = 0; k < L; k++) CW(w, c, k) = 0.0;
+        for (int k = 0; k < (mpas ? L + 1 : L); k++) CW(tw, c, k) = 0.0;
     double *ru_edge_w = D(ru_edge_w), *flux_arr = D(flux_arr);
     double *adv_coefs = D(adv_coefs), *adv_coefs_3rd = D(adv_coefs_3rd);
     int32_t *nAdv = I(nAdvCellsForEdge), *advCells = I(advCellsForEdge);
@@ -554,24 +569,28 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
                     if (k > 0) {
                         double scalar_weight = re2(S, adv_coefs, iEdge, 15, j) +
                                                copysign(1.0, CW(ru_edge_w, c, k)) * re2(S, adv_coefs_3rd, iEdge, 15, j);
-                        CW(flux_arr, c, k) += scalar_weight * rc(S, w, iAdvCell, k);
+                        CW(flux_arr, c, k) += scalar_weight * rc(S, wr, iAdvCell, k);
                     }
                 }
+                /* mpas: the edge's flux enters before the next edge overwrites flux_arr */
+                if (mpas && k > 0) CW(tw, c, k) -= rc2(S, eocs, c, 10, i) * CW(ru_edge_w, c, k) * CW(flux_arr, c, k);
             }
         }
     }
+    if (!mpas) {
 #pragma omp parallel for schedule(static)
-    for (long c = 0; c < nC; c++) { /* :1199-1205 */
-        int ne = ic2(S, nEdgesOnCell, c, 1, 0);
-        for (int k = 0; k < L; k++)
-            for (int i = 0; i < ne; i++)
-                if (k > 0) CW(w, c, k) -= rc2(S, eocs, c, 10, i) * CW(ru_edge_w, c, k) * CW(flux_arr, c, k);
+        for (long c = 0; c < nC; c++) { /* :1199-1205 */
+            int ne = ic2(S, nEdgesOnCell, c, 1, 0);
+            for (int k = 0; k < L; k++)
+                for (int i = 0; i < ne; i++)
+                    if (k > 0) CW(w, c, k) -= rc2(S, eocs, c, 10, i) * CW(ru_edge_w, c, k) * CW(flux_arr, c, k);
+        }
     }
     double *rho_zz = D(rho_zz), *uRZ = D(uReconstructZonal), *uRM = D(uReconstructMeridional);
 #pragma omp parallel for schedule(static)
-    for (long c = 0; c < nC; c++) { /* :1208-1218 */
+    for (long c = 0; c < nC; c++) { /* :1208-1218 (mpas: added after the area scaling below) */
         double coslat = cos(rc2(S, D(lat), c, 1, 0));
-        for (int k = 1; k < L; k++) {
+        for (int k = 1; k < (mpas ? 1 : L); k++) {
             double a = fzm[k] * CW(uRZ, c, k) + fzp[k] * CW(uRZ, c, k - 1);
             double b = fzm[k] * CW(uRM, c, k) + fzp[k] * CW(uRM, c, k - 1);
             CW(w, c, k) += (CW(rho_zz, c, k) * fzm[k] + CW(rho_zz, c, k - 1) * fzp[k]) * ((a * a) + (b * b)) / r_earth +
@@ -595,7 +614,7 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
                     int cell1 = ie2(S, cellsOnEdge, iEdge, 2, 0), cell2 = ie2(S, cellsOnEdge, iEdge, 2, 1);
                     if (k > 0) {
                         double w_turb_flux = edge_sign * (re(S, rho_edge, iEdge, k) + re(S, rho_edge, iEdge, k - 1)) *
-                                             (rc(S, w, cell2, k) - rc(S, w, cell1, k));
+                                             (rc(S, wr, cell2, k) - rc(S, wr, cell1, k));
                         CW(delsq_w, c, k) += w_turb_flux;
                         w_turb_flux *= re2(S, msd2, iEdge, 1, 0) * 0.25 *
                                        (rc(S, kdiff, cell1, k) + rc(S, kdiff, cell2, k) + rc(S, kdiff, cell1, k - 1) + rc(S, kdiff, cell2, k - 1));
@@ -626,18 +645,30 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
         for (int k = 0; k < L; k++) { /* :1277-1287 */
             CW(wdwz, c, k) = 0.0;
             if (k == 1 || k == L - 1)
-                CW(wdwz, c, k) = 0.25 * (CW(rw, c, k) + CW(rw, c, k - 1)) * (CW(w, c, k) + CW(w, c, k - 1));
+                CW(wdwz, c, k) = 0.25 * (CW(rw, c, k) + CW(rw, c, k - 1)) * (CW(wr, c, k) + CW(wr, c, k - 1));
             if (k > 1 && k < L - 1)
-                CW(wdwz, c, k) = flux3(CW(w, c, k - 2), CW(w, c, k - 1), CW(w, c, k), rc(S, w, c, k + 1),
+                CW(wdwz, c, k) = flux3(CW(wr, c, k - 2), CW(wr, c, k - 1), CW(wr, c, k), rc(S, wr, c, k + 1),
                                        0.5 * (CW(rw, c, k) + CW(rw, c, k - 1)), 1.0);
         }
+        const double coslat = cos(rc2(S, D(lat), c, 1, 0));
         for (int k = 0; k < L; k++) { /* :1289-1302 (Q14 literal) */
-            if (k > 0) CW(w, c, k) *= rc2(S, invAreaCell, c, 1, 0) - rdzu[k] * (rc(S, wdwz, c, k + 1) - CW(wdwz, c, k));
+            /* mpas: wdwz(nVertLevels) = 0; tend_w = hflux invAreaCell + curvature - d(wdwz)/dz */
+            const double wdwz_p = (mpas && k + 1 == L) ? 0.0 : rc(S, wdwz, c, k + 1);
+            if (k > 0 && mpas) {
+                double a = fzm[k] * CW(uRZ, c, k) + fzp[k] * CW(uRZ, c, k - 1);
+                double b = fzm[k] * CW(uRM, c, k) + fzp[k] * CW(uRM, c, k - 1);
+                double curv = (CW(rho_zz, c, k) * fzm[k] + CW(rho_zz, c, k - 1) * fzp[k]) * ((a * a) + (b * b)) / r_earth +
+                              2.0 * omega_c * coslat * (fzm[k] * CW(uRZ, c, k) + fzp[k] * CW(uRZ, c, k - 1)) *
+                                  (CW(rho_zz, c, k) * fzm[k] + CW(rho_zz, c, k - 1) * fzp[k]);
+                CW(tw, c, k) = CW(tw, c, k) * rc2(S, invAreaCell, c, 1, 0) + curv - rdzu[k] * (wdwz_p - CW(wdwz, c, k));
+            } else if (k > 0) {
+                CW(w, c, k) *= rc2(S, invAreaCell, c, 1, 0) - rdzu[k] * (wdwz_p - CW(wdwz, c, k));
+            }
             if (rk_step == 0 && k > 0)
                 CW(tend_w_euler, c, k) -= CW(cqw, c, k) * (rdzu[k] * (CW(pressure_p, c, k) - CW(pressure_p, c, k - 1)) -
                                                            (fzm[k] * CW(dpdz, c, k) + fzp[k] * CW(dpdz, c, k - 1)));
         }
-        for (int k = 1; k < L; k++) CW(w, c, k) += CW(tend_w_euler, c, k); /* :1318-1322 */
+        for (int k = 1; k < L; k++) CW(tw, c, k) += CW(tend_w_euler, c, k); /* :1318-1322 */
     }
 
     /* -------- theta section -------- */
@@ -718,13 +749,29 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
     for (long c = 0; c < nC; c++) {
         for (int k = 0; k < L; k++) { /* :1406-1420 (Q15 literal order) */
             CW(wdtz, c, k) = 0.0;
+            if (mpas) { /* MPAS-A: 3rd-order flux of theta_m by rw plus the rtheta_pp redefinition term */
+                if (k == 1)
+                    CW(wdtz, c, k) = CW(rw, c, k) * (fzm[k] * CW(theta_m, c, k) + fzp[k] * CW(theta_m, c, k - 1)) +
+                                     (CW(rw_save, c, k) - CW(rw, c, k)) * (fzm[k] * CW(tms, c, k) + fzp[k] * CW(tms, c, k - 1));
+                if (k > 1 && k < L - 1)
+                    CW(wdtz, c, k) = flux3(CW(theta_m, c, k - 2), CW(theta_m, c, k - 1), CW(theta_m, c, k),
+                                           CW(theta_m, c, k + 1), CW(rw, c, k), 0.25) +
+                                     (CW(rw_save, c, k) - CW(rw, c, k)) * (fzm[k] * CW(tms, c, k) + fzp[k] * CW(tms, c, k - 1));
+                if (k == L - 1)
+                    CW(wdtz, c, k) = CW(rw_save, c, k) * (fzm[k] * CW(theta_m, c, k) + fzp[k] * CW(theta_m, c, k - 1));
+                continue;
+            }
             if (k > 0 && k < L - 1)
                 CW(wdtz, c, k) = ((CW(rw_save, c, k) - CW(rw, c, k)) * (fzm[k] * CW(tms, c, k) + fzp[k] * CW(tms, c, k - 1)));
             if (k == 1) CW(wdtz, c, k) += CW(rw, c, k) * (fzm[k] * CW(theta_m, c, k) + fzp[k] * CW(theta_m, c, k - 1));
             if (k == L - 1) CW(wdtz, c, k) = CW(rw_save, c, k) * (fzm[k] * CW(tms, c, k) + fzp[k] * rc(S, tms, c, k - 1));
         }
         for (int k = 0; k < L; k++) { /* :1422-1427 */
-            CW(tend_theta, c, k) *= rc2(S, invAreaCell, c, 1, 0) - rdzw[k] * (rc(S, wdtz, c, k + 1) - CW(wdtz, c, k));
+            const double wdtz_p = (mpas && k + 1 == L) ? 0.0 : rc(S, wdtz, c, k + 1);
+            if (mpas)
+                CW(tend_theta, c, k) = CW(tend_theta, c, k) * rc2(S, invAreaCell, c, 1, 0) - rdzw[k] * (wdtz_p - CW(wdtz, c, k));
+            else
+                CW(tend_theta, c, k) *= rc2(S, invAreaCell, c, 1, 0) - rdzw[k] * (wdtz_p - CW(wdtz, c, k));
             CW(D(tend_rtheta_adv), c, k) = CW(tend_theta, c, k);
             CW(D(rthdynten), c, k) = CW(tend_theta, c, k) / CW(rho_zz, c, k);
             CW(tend_theta, c, k) += CW(rho_zz, c, k) * CW(D(rt_diabatic_tend), c, k);
@@ -732,6 +779,11 @@ void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int hor
         for (int k = 0; k < L; k++) /* :1477-1479 */
             CW(tend_theta, c, k) += CW(tend_theta_euler, c, k) + CW(D(tend_rtheta_physics), c, k);
     }
+}
+
+void ora_atm_compute_dyn_tend_work(ora_state* S, int rk_step, double dt, int horiz_mixing, double config_mpas_cam_coef,
+                                   int config_mix_full, int config_rayleigh_damp_u) {
+    dyn_tend_impl(S, rk_step, dt, horiz_mixing, config_mpas_cam_coef, config_mix_full, config_rayleigh_damp_u, 0);
 }
 
 /* ===================== atm_set_smlstep_pert_variables_work, dynamics_tasks.rg:1503-1528
@@ -1245,8 +1297,11 @@ void ora_mpas_vert_imp_coefs(ora_state* S, double dts) {
     }
 }
 
-void ora_mpas_acoustic_step(ora_state* S, double dts, int small_step) {
+/* dyn = 0: physics 1 (dyn_tend's w tendency is in the state w, Q8); dyn = 1: physics 2,
+ * the MPAS dynamics (tend_w; the implicit Rayleigh term stays on the state w)        */
+static void mpas_acoustic(ora_state* S, double dts, int small_step, int dyn) {
     const int L = S->L, nC = S->nCells, nE = S->nEdges;
+    double* tw = dyn ? D(tend_w) : D(w);
     const double epssm = config_epssm, rcv = rgas / (CP - rgas), c2 = CP * rcv;
     const double resm = (1.0 - epssm) / (1.0 + epssm);
     double *rtheta_pp_old = D(rtheta_pp_old), *rtheta_pp = D(rtheta_pp), *rho_pp = D(rho_pp);
@@ -1290,7 +1345,7 @@ void ora_mpas_acoustic_step(ora_state* S, double dts, int small_step) {
             for (int k = 0; k < L; k++) {
                 CW(rho_pp, c, k) = CW(rho_pp, c, k) + dts * CW(D(tend_rho), c, k);
                 CW(rtheta_pp, c, k) = CW(rtheta_pp, c, k) + dts * CW(D(tend_theta), c, k);
-                CW(rw_p, c, k) = CW(rw_p, c, k) + dts * CW(w, c, k);
+                CW(rw_p, c, k) = CW(rw_p, c, k) + dts * CW(tw, c, k);
                 CW(wwAvg, c, k) = CW(wwAvg, c, k) + 0.5 * (1.0 + epssm) * CW(rw_p, c, k);
             }
             continue;
@@ -1319,7 +1374,7 @@ void ora_mpas_acoustic_step(ora_state* S, double dts, int small_step) {
         }
         for (int k = 1; k < L; k++) CW(wwAvg, c, k) = CW(wwAvg, c, k) + 0.5 * (1.0 - epssm) * rwp0[k];
         for (int k = 1; k < L; k++)
-            CW(rw_p, c, k) = rwp0[k] + dts * CW(w, c, k) -
+            CW(rw_p, c, k) = rwp0[k] + dts * CW(tw, c, k) -
                              CW(D(cofwz), c, k) * ((CW(zz, c, k) * ts[k] - CW(zz, c, k - 1) * ts[k - 1]) +
                                                    resm * (CW(zz, c, k) * rtp0[k] - CW(zz, c, k - 1) * rtp0[k - 1])) -
                              CW(D(cofwr), c, k) * ((rs[k] + rs[k - 1]) + resm * (rpp0[k] + rpp0[k - 1])) +
@@ -1343,6 +1398,8 @@ void ora_mpas_acoustic_step(ora_state* S, double dts, int small_step) {
         }
     }
 }
+void ora_mpas_acoustic_step(ora_state* S, double dts, int small_step) { mpas_acoustic(S, dts, small_step, 0); }
+void ora_mpas2_acoustic_step(ora_state* S, double dts, int small_step) { mpas_acoustic(S, dts, small_step, 1); }
 
 /* atm_recover_large_step_variables_work (:1766-1872) in the MPAS form: ru = ru_save + ru_p
  * and flux2 = fzm ru(k) + fzp ru(k-1) (Q24), exner = (zz rgas/p0 (rtheta_p + rtheta_base))^rcv,
@@ -1412,11 +1469,149 @@ void ora_mpas_recover(ora_state* S, int ns, int rk_step, double dt) {
     }
 }
 
+/* ===================== the MPAS dynamics (option physics = 2)
+ * Every remaining quirk of the RK3 path fixed as MPAS-A (MPAS-Model v7
+ * mpas_atm_time_integration.F, not vendored) defines it, on top of the vertical solver
+ * above (physics = 1):
+ *   setup   (:747-778)  theta_m_save = theta_m (read by dyn_tend rk > 0, never written: Q2)
+ *   moist   (:460-502)  cqu = 1/(1 + qtotal of the edge) (the commented edge loop, Q25)
+ *   dyn_tend (:814-1480) tend_rho with the physics term outside the flux divergence; the
+ *           top wduz/wdwz/wdtz = 0; q summed once (Q10); curvature -A - B (Q12); the w
+ *           tendency in its own array tend_w computed from the state w (Q8), the
+ *           horizontal w flux accumulated over every edge (Q13), tend_w = flux
+ *           invAreaCell + curvature - d(wdwz)/dz (Q14; the curvature is not area-scaled),
+ *           wdtz = 3rd-order flux of theta_m by rw + the rtheta_pp term (Q15)
+ *           (dyn_tend_impl with mpas = 1)
+ *   set_smlstep (:1503-1528) u_tend = tend_u, w_tend = tend_w (Q2/Q8), levels 1..L-1
+ *   acoustic tend_rw = tend_w (mpas_acoustic, dyn = 1)
+ *   solve_diagnostics (:328-454) h = rho_zz, rho_edge = h_edge (the MPAS-A caller passes
+ *           diag%rho_edge as h_edge; Q2); divergence += sign dvEdge u (Q9); v over every
+ *           edgesOnEdge entry (Q23)
+ *   srk3    mpas_reconstruct_2d after the RK loop (rk_timestep.rg:487, commented); the
+ *           substep finish keeps rho_zz (MPAS-A resets rho_zz of the OLD time level,
+ *           :2001-2004 writes the only one the port has)                             */
+void ora_mpas_rk_integration_setup(ora_state* S) {
+    ora_atm_rk_integration_setup(S);
+    const int L = S->L;
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < S->nCells; c++)
+        for (int k = 0; k < L; k++) CW(D(theta_m_save), c, k) = CW(D(theta_m), c, k);
+}
+
+void ora_mpas_moist_coefficients(ora_state* S) {
+    ora_atm_compute_moist_coefficients(S);
+    const int L = S->L;
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < S->nEdges; e++) {
+        int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        for (int k = 0; k < L; k++) {
+            double qtotal = 0.5 * (rc(S, D(qtot), cell1, k) + rc(S, D(qtot), cell2, k));
+            CW(D(cqu), e, k) = 1.0 / (1.0 + qtotal);
+        }
+    }
+}
+
+void ora_mpas_dyn_tend(ora_state* S, int rk_step, double dt, int horiz_mixing, double config_mpas_cam_coef,
+                       int config_mix_full, int config_rayleigh_damp_u) {
+    dyn_tend_impl(S, rk_step, dt, horiz_mixing, config_mpas_cam_coef, config_mix_full, config_rayleigh_damp_u, 1);
+}
+
+void ora_mpas_set_smlstep(ora_state* S) {
+    const int L = S->L, nC = S->nCells;
+    double *tw = D(tend_w), *zz = D(zz), *tu = D(tend_u), *fzm = D(fzm), *fzp = D(fzp);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        if (ic2(S, I(bdyMaskCell), c, 1, 0) > nRelaxZone) continue;
+        int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int i = 0; i < ne; i++) {
+            int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+            for (int k = 1; k < L; k++) {
+                double flux = rc2(S, D(edgesOnCell_sign), c, 10, i) * (fzm[k] * re(S, tu, iEdge, k) + fzp[k] * re(S, tu, iEdge, k - 1));
+                CW(tw, c, k) = CW(tw, c, k) - (rc3v(S, D(zb_cell), c, k, i) + copysign(1.0, re(S, tu, iEdge, k)) * rc3v(S, D(zb3_cell), c, k, i)) * flux;
+            }
+        }
+        for (int k = 1; k < L; k++) CW(tw, c, k) = (fzm[k] * CW(zz, c, k) + fzp[k] * CW(zz, c, k - 1)) * CW(tw, c, k);
+    }
+}
+
+void ora_mpas_solve_diagnostics(ora_state* S, int hollingsworth, int rk_step) {
+    const int L = S->L, nC = S->nCells, nE = S->nEdges;
+    double *u = D(u), *rho_zz = D(rho_zz), *h_edge = D(h_edge), *rho_edge = D(rho_edge);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) { /* h = rho_zz; rho_edge is MPAS-A's h_edge */
+        int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        for (int k = 0; k < L; k++) {
+            CW(h_edge, e, k) = 0.5 * (rc(S, rho_zz, cell1, k) + rc(S, rho_zz, cell2, k));
+            CW(rho_edge, e, k) = CW(h_edge, e, k);
+        }
+    }
+    /* the reference's diagnostics; then the fixed divergence (Q9) and v (Q23) */
+    double* h = D(h);
+    S->f[F_h] = rho_zz; /* (the h the reference reads is rho_zz: h_edge as above) */
+    ora_atm_compute_solve_diagnostics(S, hollingsworth, -3); /* -3: no v here */
+    S->f[F_h] = h;
+    double* div = D(divergence);
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        for (int k = 0; k < L; k++) {
+            CW(div, c, k) = 0.0;
+            for (int i = 0; i < ne; i++) {
+                int iEdge = ic2(S, I(edgesOnCell), c, 10, i);
+                double s = rc2(S, D(edgesOnCellSign), c, 10, i) * re2(S, D(dvEdge), iEdge, 1, 0);
+                CW(div, c, k) += s * re(S, u, iEdge, k);
+            }
+            CW(div, c, k) *= rc2(S, D(invAreaCell), c, 1, 0);
+        }
+    }
+    if (rk_step == -1 || rk_step == 2) {
+        double* vv = D(v);
+#pragma omp parallel for schedule(static)
+        for (long e = 0; e < nE; e++) {
+            int neoe = ie2(S, I(nEdgesOnEdge), e, 1, 0);
+            for (int k = 0; k < L; k++) {
+                CW(vv, e, k) = 0;
+                for (int i = 0; i < neoe; i++) {
+                    int eoe = ie2(S, I(edgesOnEdge_ECP), e, 20, i);
+                    CW(vv, e, k) += re2(S, D(weightsOnEdge), e, 20, i) * re(S, u, eoe, k);
+                }
+            }
+        }
+    }
+}
+
+void ora_mpas_substep_finish(ora_state* S, int dynamics_substep, int dynamics_split) {
+    const int L = S->L;
+    double* keep = (double*)malloc(sizeof(double) * (size_t)(S->nCells + 1) * LV);
+    memcpy(keep, D(rho_zz), sizeof(double) * (size_t)(S->nCells + 1) * LV);
+    ora_atm_rk_dynamics_substep_finish(S, dynamics_substep, dynamics_split);
+    memcpy(D(rho_zz), keep, sizeof(double) * (size_t)(S->nCells + 1) * LV);
+    free(keep);
+    (void)L;
+}
+
+/* surface pressure (MPAS-A's diagnostic, the formula init_atm_case_jw uses,
+ * init_atm_cases.rg:519-520): hydrostatic extrapolation of the lowest two levels */
+void ora_mpas_surface_pressure(ora_state* S) {
+    const int nC = S->nCells;
+    const double dz0 = 1.0 / D(rdzw)[0];
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++)
+        CW(D(surface_pressure), c, 0) =
+            0.5 * dz0 * gravity * (1.25 * (CW(D(rho_zz), c, 0) * (1.0 + CW(D(qtot), c, 0))) -
+                                   0.25 * (CW(D(rho_zz), c, 1) * (1.0 + CW(D(qtot), c, 1)))) +
+            CW(D(pressure_p), c, 0) + CW(D(pressure_base), c, 0);
+}
+
 void ora_mpas_advance_scalars_mono(ora_state* S, double dt);
 
 /* transport != 0: the monotonic scalar transport over the step (scalars_old = scalars
  * at the start, ora_mpas_advance_scalars_mono after the last stage's recover) */
-void ora_mpas_srk3_ex(ora_state* S, double dt, int schedule, int transport) {
+void ora_mpas_srk3_dyn(ora_state* S, double dt, int schedule, int transport, int physics);
+void ora_mpas_srk3_ex(ora_state* S, double dt, int schedule, int transport) { ora_mpas_srk3_dyn(S, dt, schedule, transport, 1); }
+/* physics 1: the vertical solver only; physics 2: the MPAS dynamics */
+void ora_mpas_srk3_dyn(ora_state* S, double dt, int schedule, int transport, int physics) {
+    const int md = physics >= 2;
     if (transport) memcpy(D(scalars_old), D(scalars), sizeof(double) * (size_t)(S->nCells + 1) * LV * NSC);
     int number_of_sub_steps = 2;
     double rk_sub_timestep[3] = {dt / 3, dt / number_of_sub_steps, dt / number_of_sub_steps};
@@ -1424,23 +1619,39 @@ void ora_mpas_srk3_ex(ora_state* S, double dt, int schedule, int transport) {
     number_sub_steps[0] = (number_of_sub_steps / 2 > 1) ? number_of_sub_steps / 2 : 1;
     number_sub_steps[1] = number_sub_steps[0];
     number_sub_steps[2] = number_of_sub_steps;
-    ora_atm_rk_integration_setup(S);
-    ora_atm_compute_moist_coefficients(S);
+    if (md) {
+        ora_mpas_rk_integration_setup(S);
+        ora_mpas_moist_coefficients(S);
+    } else {
+        ora_atm_rk_integration_setup(S);
+        ora_atm_compute_moist_coefficients(S);
+    }
     ora_mpas_vert_imp_coefs(S, rk_sub_timestep[0]);
     for (int rk_step = 0; rk_step < 3; rk_step++) {
         if (rk_step == 1) ora_mpas_vert_imp_coefs(S, rk_sub_timestep[rk_step]);
         int dyn_rk = schedule == 0 ? (int)rk_sub_timestep[rk_step] : rk_step;
-        ora_atm_compute_dyn_tend_work(S, dyn_rk, dt, 0, 0.0, 0, 0);
-        ora_atm_set_smlstep_pert_variables_work(S);
+        if (md) {
+            ora_mpas_dyn_tend(S, dyn_rk, dt, 0, 0.0, 0, 0);
+            ora_mpas_set_smlstep(S);
+        } else {
+            ora_atm_compute_dyn_tend_work(S, dyn_rk, dt, 0, 0.0, 0, 0);
+            ora_atm_set_smlstep_pert_variables_work(S);
+        }
         for (int small_step = 0; small_step < number_sub_steps[rk_step]; small_step++) { /* Q5 */
-            ora_mpas_acoustic_step(S, rk_sub_timestep[rk_step], small_step);
+            mpas_acoustic(S, rk_sub_timestep[rk_step], small_step, md);
             ora_atm_divergence_damping_3d(S, rk_sub_timestep[rk_step]);
         }
         ora_mpas_recover(S, number_sub_steps[rk_step], rk_step, dt); /* rk_timestep.rg:460 (Q7) */
-        ora_atm_compute_solve_diagnostics(S, 0, rk_step);
+        if (md) ora_mpas_solve_diagnostics(S, 0, rk_step);
+        else ora_atm_compute_solve_diagnostics(S, 0, rk_step);
     }
     if (transport) ora_mpas_advance_scalars_mono(S, dt);
-    ora_atm_rk_dynamics_substep_finish(S, 1, 1);
+    if (md) {
+        ora_mpas_reconstruct_2d(S, 0, 1); /* rk_timestep.rg:487 (commented in the reference) */
+        ora_mpas_substep_finish(S, 1, 1);
+    } else {
+        ora_atm_rk_dynamics_substep_finish(S, 1, 1);
+    }
 }
 void ora_mpas_srk3(ora_state* S, double dt, int schedule) { ora_mpas_srk3_ex(S, dt, schedule, 0); }
 

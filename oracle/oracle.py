@@ -63,6 +63,15 @@ def load():
             "ora_atm_init_coupled_diagnostics": (None, [p]),
             "ora_mpas_recover": (None, [p, i32, i32, dbl]),
             "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
+            "ora_mpas_srk3_dyn": (None, [p, dbl, i32, i32, i32]),
+            "ora_mpas_rk_integration_setup": (None, [p]),
+            "ora_mpas_moist_coefficients": (None, [p]),
+            "ora_mpas_dyn_tend": (None, [p, i32, dbl, i32, dbl, i32, i32]),
+            "ora_mpas_set_smlstep": (None, [p]),
+            "ora_mpas2_acoustic_step": (None, [p, dbl, i32]),
+            "ora_mpas_solve_diagnostics": (None, [p, i32, i32]),
+            "ora_mpas_substep_finish": (None, [p, i32, i32]),
+            "ora_mpas_surface_pressure": (None, [p]),
         }
         for n, (res, args) in sig.items():
             fn = getattr(L, n)
@@ -137,8 +146,37 @@ class Oracle:
     def mpas_recover(self, ns, rk_step, dt):
         self.lib.ora_mpas_recover(self.p, ns, rk_step, dt)
 
-    def mpas_srk3(self, dt, schedule=1, transport=False):
-        self.lib.ora_mpas_srk3_ex(self.p, dt, schedule, int(bool(transport)))
+    def mpas_srk3(self, dt, schedule=1, transport=False, physics=1):
+        """physics 1: the MPAS vertical solver; physics 2: the MPAS dynamics (every quirk fixed)"""
+        self.lib.ora_mpas_srk3_dyn(self.p, dt, schedule, int(bool(transport)), int(physics))
+
+    # the MPAS dynamics (physics = 2), task by task
+    def mpas_rk_integration_setup(self):
+        self.lib.ora_mpas_rk_integration_setup(self.p)
+
+    def mpas_moist_coefficients(self):
+        self.lib.ora_mpas_moist_coefficients(self.p)
+
+    def mpas_dyn_tend(self, rk_step, dt, config_horiz_mixing="2d_smagorinsky", config_mpas_cam_coef=0.0,
+                      config_mix_full=False, config_rayleigh_damp_u=False):
+        hm = config_horiz_mixing if isinstance(config_horiz_mixing, int) else HORIZ.get(config_horiz_mixing, 2)
+        self.lib.ora_mpas_dyn_tend(self.p, rk_step, dt, hm, config_mpas_cam_coef, int(config_mix_full),
+                                   int(config_rayleigh_damp_u))
+
+    def mpas_set_smlstep(self):
+        self.lib.ora_mpas_set_smlstep(self.p)
+
+    def mpas2_acoustic_step(self, dts, small_step):
+        self.lib.ora_mpas2_acoustic_step(self.p, dts, small_step)
+
+    def mpas_solve_diagnostics(self, hollingsworth, rk_step):
+        self.lib.ora_mpas_solve_diagnostics(self.p, int(hollingsworth), rk_step)
+
+    def mpas_substep_finish(self, dynamics_substep=1, dynamics_split=1):
+        self.lib.ora_mpas_substep_finish(self.p, dynamics_substep, dynamics_split)
+
+    def mpas_surface_pressure(self):
+        self.lib.ora_mpas_surface_pressure(self.p)
 
     def atm_compute_damping_coefs(self, config_zd=22000.0, config_xnutr=0.2):
         self.lib.ora_atm_compute_damping_coefs(self.p, config_zd, config_xnutr)

@@ -32,8 +32,11 @@ def test_inputs_pinned(x1_2562, golden, L, variant):
     """the seeded generator + init restatements reproduce the committed inputs bit for bit"""
     st = make_state(x1_2562, L, variant)
     g = golden[f"L{L}_{variant}"]["inputs"]
+    appended = {"tend_w"}  # registry fields appended after the golden was made (physics = 2)
+    assert set(g) == {f.name for f in FIELDS} - appended
     for f in FIELDS:
-        _check(digest(st[f.name]), g[f.name], f"{f.name} input")
+        if f.name not in appended:
+            _check(digest(st[f.name]), g[f.name], f"{f.name} input")
 
 
 @pytest.mark.parametrize("L,variant", [(5, "ref"), (5, "random"), (56, "random")])
