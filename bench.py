@@ -138,7 +138,7 @@ def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False, budget_
 
     def step():
         if physics:
-            o.mpas_srk3(dt, 1, transport=transport)
+            o.mpas_srk3(dt, 1, transport=transport, physics=int(physics))
         else:
             o.atm_srk3(dt, 1)
 
@@ -151,7 +151,7 @@ def cpu_baseline(ncells, L, dt, threads, physics=False, transport=False, budget_
         step()
         times.append(time.perf_counter() - t1)
     t = statistics.median(times)
-    what = "MPAS-solver " if physics else ""
+    what = {0: "", 1: "MPAS-solver ", 2: "MPAS-dynamics "}[int(physics)]
     what += "RK3 steps with scalar transport" if transport else "RK3 steps"
     return {"value": round(ncells / t / 1e6, 6), "unit": "Mcell-columns/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model(), "omp_num_threads": threads, "nproc": os.cpu_count(),
@@ -216,7 +216,7 @@ def measure_traffic(args):
              "--ncells", str(args.ncells), "--levels", str(args.levels), "--exact", str(args.exact)]
     child += [f"--option={o}" for o in args.option]
     if args.physics:
-        child.append("--physics")
+        child.append(f"--physics={args.physics}")
     if args.transport:
         child.append("--transport")
     res = {}
@@ -280,6 +280,10 @@ def task_table(rep, work_dims, n_prof, physics):
         kw = dict(kw_of.get(name, {}))
         if physics and task == "atm_advance_acoustic_step_work":
             kw["physics"] = 1  # the acoustic task's MPAS form also updates ru_p / ruAvg
+        if physics == 2 and task in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
+                                     "atm_compute_dyn_tend_work", "atm_set_smlstep_pert_variables_work",
+                                     "atm_compute_solve_diagnostics"):
+            kw["physics"] = 2  # the MPAS dynamics' read/write sets
         b = roofline.b_alg(task, work_dims, **kw)
         avg = ms / calls
         n = calls / n_prof
@@ -322,13 +326,14 @@ def main():
     ap.add_argument("--replicas", action="store_true", help="N > 1: full-mesh replicas instead of a decomposition")
     ap.add_argument("--decompose", action="store_true",
                     help="run the decomposed (RCCL halo) path also at N = 1 (a 1-part decomposition)")
-    ap.add_argument("--physics", action="store_true",
-                    help="the MPAS vertical solver (option physics = 1: 4 acoustic substeps + recover per step)")
+    ap.add_argument("--physics", type=int, nargs="?", const=1, default=0, choices=[0, 1, 2],
+                    help="1: the MPAS vertical solver (4 acoustic substeps + recover per step); 2: also the MPAS "
+                         "dynamics (every quirk fixed)")
     ap.add_argument("--transport", action="store_true",
                     help="physics = 1 plus the monotonic transport of the 8 scalars in every step")
     args = ap.parse_args()
-    if args.transport:
-        args.physics = True
+    if args.transport and not args.physics:
+        args.physics = 1
     if args.pmc_child:
         return pmc_child(args)
 
@@ -481,13 +486,15 @@ def main():
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
            "scaling": "strong" if decomposed else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": f"x1.{ncells} x {L} levels, atm_srk3 (3 dyn_tend rk 0/1/2, " +
-                                  ("4 acoustic substeps + recover (MPAS vertical solver)" if args.physics
-                                   else "7 acoustic substeps") +
+                                  ({1: "4 acoustic substeps + recover (MPAS vertical solver)",
+                                    2: "4 acoustic substeps + recover, MPAS dynamics (physics 2)"}.get(args.physics,
+                                                                                     "7 acoustic substeps")) +
                                   (", monotonic transport of 8 scalars" if args.transport else "") + ")",
                       "nCells": ncells, "nEdges": m.nEdges, "nVertices": m.nVertices, "nVertLevels": L,
                       "dt": dt, "parallelism": (f"decomposed{world}" if decomposed else
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
-                      "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport)},
+                      "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
+                      "graph": ctx.get_option("graph") if not decomposed else 0},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}
     if halo_info:

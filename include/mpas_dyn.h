@@ -57,7 +57,11 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * or 4 entities per column slot in div_damping / solve_diagnostics; "vcmix" = 1 (default)
  * interleaves the vertex and cell blocks of the mixed grids; "overlap" = 1 (default)
  * computes interior entities beside the halo exchange of a decomposed mesh; "self" = 0
- * disables the SELF gathers.  All but "exact" and "physics" change only speed, never results.
+ * disables the SELF gathers; "graph" = 1 (default) makes mpas_atm_srk3 capture its step once
+ * per (dt, schedule) as a HIP graph and replay it (any option change or mesh upload
+ * re-captures; per-task timing and decomposed contexts run the launches directly; read-only
+ * "graph_captures" / "graph_launches" count them).  All but "exact" and "physics" change
+ * only speed, never results.
  * "physics" = 1 selects the MPAS vertical solver: vert_imp with Q16/Q17
  * fixed, the acoustic step with the ru_p update (Q18), the MPAS statement order (Q19/Q20)
  * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), recover_large_step

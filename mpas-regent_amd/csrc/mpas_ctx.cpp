@@ -84,6 +84,17 @@ struct mpas_ctx {
     int* gid_dev[3] = {nullptr, nullptr, nullptr};
     void* sum_scratch = nullptr;  // summarize_timestep partials (allocated on first use)
     double* sum_out = nullptr;
+    // option "graph": mpas_atm_srk3 captured once per (dt, schedule) as a HIP graph and
+    // replayed (one hipGraphLaunch per step instead of ~60 kernel launches); invalidated
+    // by any option change or mesh upload; not used while per-task timing is on or on a
+    // decomposed context (the halo bookkeeping is host-side per launch)
+    int graph_on = 1;
+    bool graph_valid = false;
+    double graph_dt = 0.0;
+    int graph_schedule = -1;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    int64_t graph_captures = 0, graph_launches = 0;
 };
 
 namespace {
@@ -317,6 +328,52 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }
 
+void graph_drop(mpas_ctx* c) {
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    c->graph_exec = nullptr;
+    c->graph = nullptr;
+    c->graph_valid = false;
+}
+
+void prepare_now(mpas_ctx* c) {
+    if (c->dirty) {
+        hipcheck(launch_prepare(c->S, c->stream), "prepare");
+        c->self_ok = c->S.selfc;
+        c->S.selfc = c->self_ok && c->self_on;
+        c->dirty = false;
+    }
+}
+
+// one atm_srk3 step: replayed from a captured HIP graph when possible
+void srk3_step(mpas_ctx* c, double dt, int schedule) {
+    if (!c->graph_on || c->timing || c->halo) {
+        srk3(c, dt, schedule);
+        return;
+    }
+    prepare_now(c);  // (synchronous: never inside a capture)
+    if (!(c->graph_valid && c->graph_dt == dt && c->graph_schedule == schedule)) {
+        graph_drop(c);
+        hipcheck(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+        try {
+            srk3(c, dt, schedule);
+        } catch (...) {
+            hipGraph_t g = nullptr;
+            (void)hipStreamEndCapture(c->stream, &g);
+            if (g) (void)hipGraphDestroy(g);
+            throw;
+        }
+        hipcheck(hipStreamEndCapture(c->stream, &c->graph), "hipStreamEndCapture");
+        hipcheck(hipGraphInstantiate(&c->graph_exec, c->graph, nullptr, nullptr, 0), "hipGraphInstantiate");
+        c->graph_valid = true;
+        c->graph_dt = dt;
+        c->graph_schedule = schedule;
+        c->graph_captures++;
+    }
+    hipcheck(hipGraphLaunch(c->graph_exec, c->stream), "hipGraphLaunch");
+    c->graph_launches++;
+}
+
 }  // namespace
 
 extern "C" {
@@ -409,6 +466,7 @@ int mpas_ctx_destroy(mpas_ctx* c) {
         (void)hipEventDestroy(t.e1);
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
+    graph_drop(c);
     c->halo.reset();
     c->loopgrp.reset();
     for (auto p : c->gid_dev)
@@ -437,7 +495,9 @@ int mpas_get_stream(mpas_ctx* c, void** stream) {
 
 int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
     return guarded(c, [&] {
+        graph_drop(c);  // every option is baked into a captured step
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
+        else if (name && std::strcmp(name, "graph") == 0) c->graph_on = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
             if (value != 1 && value != 2 && value != 4) throw Fail{MPAS_EINVAL, "epw must be 1, 2 or 4"};
@@ -476,6 +536,9 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
+        else if (name && std::strcmp(name, "graph") == 0) *value = c->graph_on;
+        else if (name && std::strcmp(name, "graph_captures") == 0) *value = c->graph_captures;
+        else if (name && std::strcmp(name, "graph_launches") == 0) *value = c->graph_launches;
         else if (name && std::strcmp(name, "selfc") == 0) {
             if (c->dirty) {  // decide now (needs the mesh uploaded)
                 hipcheck(hipSetDevice(c->device), "hipSetDevice");
@@ -533,6 +596,7 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
         }
         hipcheck(hipMemcpy(c->S.f[f], buf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
         c->dirty = true;
+        graph_drop(c);
         if (c->halo) c->halo->stale[f] = 0;  // uploaded ghosts are the global values
         // derived mesh arrays: cos()/sin() on the host with the same libm as the oracle
         struct { int src, dst; double (*fn)(double); } der[] = {
@@ -619,6 +683,7 @@ int* dev_ints(const int32_t* h, int n) {
 
 int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32_t nVerticesOwned) {
     return guarded(c, [&] {
+        graph_drop(c);
         if (nCellsOwned < 0 || nCellsOwned > c->S.nCells || nEdgesOwned < 0 || nEdgesOwned > c->S.nEdges ||
             nVerticesOwned < 0 || nVerticesOwned > c->S.nVertices)
             throw Fail{MPAS_EINVAL, "mpas_halo_owned: owned counts exceed the local counts"};
@@ -631,6 +696,7 @@ int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32
 
 int mpas_halo_interior(mpas_ctx* c, int32_t nCI, int32_t nEI, int32_t nVI) {
     return guarded(c, [&] {
+        graph_drop(c);
         if (nCI < 0 || nCI > c->S.nCO || nEI < 0 || nEI > c->S.nEO || nVI < 0 || nVI > c->S.nVO)
             throw Fail{MPAS_EINVAL, "mpas_halo_interior: interior counts exceed the owned counts"};
         hipcheck(hipSetDevice(c->device), "hipSetDevice");
@@ -835,7 +901,7 @@ int mpas_summarize_timestep(mpas_ctx* c, int detailed, int global_vel, int globa
 int mpas_atm_srk3(mpas_ctx* c, double dt, int schedule) {
     return guarded(c, [&] {
         hipcheck(hipSetDevice(c->device), "hipSetDevice");
-        srk3(c, dt, schedule);
+        srk3_step(c, dt, schedule);
     });
 }
 int mpas_atm_timestep(mpas_ctx* c, double dt) { return mpas_atm_srk3(c, dt, 0); }

@@ -15,12 +15,13 @@ roofline.achieved divides by the measured launch time.
 
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0):
+    md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "atm_rk_integration_setup":
         return (["rho_p", "rho_zz", "rtheta_p", "rw", "theta_m", "w", "ru", "u"],
                 ["rho_p_save", "rho_zz_2", "rho_zz_old_split", "rtheta_p_save", "rw_save", "theta_m_2", "w_2",
-                 "ru_save", "u_2"])
+                 "ru_save", "u_2"] + (["theta_m_save"] if md else []))
     if task == "atm_compute_moist_coefficients":
-        return [], ["qtot", "cqw"]
+        return [], ["qtot", "cqw"] + (["cqu"] if md else [])
     if task == "atm_compute_vert_imp_coefs":
         return (["cqw", "exner", "exner_base", "qtot", "rho_base", "rtheta_base", "rtheta_p", "theta_m", "zz",
                  "gamma_tri"],
@@ -45,8 +46,14 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0):
                      "tend_theta_euler", "pv_edge", "rho_edge", "ru", "ru_save", "tend_ru_physics", "u",
                      "tend_u_euler"]
             writes = ["h_divergence", "w", "tend_theta", "tend_rtheta_adv", "rthdynten", "tend_u"]
+        if md:  # the w tendency goes to tend_w; the curvature reads the reconstructed winds
+            writes = [("tend_w" if x == "w" else x) for x in writes]
+            reads += ["uReconstructZonal", "uReconstructMeridional", "w"]
         return reads + mesh, writes
     if task == "atm_set_smlstep_pert_variables_work":
+        if md:
+            return (["zz", "tend_w", "zb_cell", "zb3_cell", "tend_u", "bdyMaskCell", "nEdgesOnCell", "edgesOnCell",
+                     "edgesOnCell_sign"], ["tend_w"])
         return (["zz", "w", "zb_cell", "zb3_cell", "u_tend", "cprMask", "bdyMaskCell", "nEdgesOnCell",
                  "edgesOnCell", "edgesOnCell_sign"], ["w"])
     if task == "atm_advance_acoustic_step_work":
@@ -69,7 +76,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0):
         writes = ["h_edge", "ke_edge", "pv_edge", "divergence", "ke", "vorticity", "pv_vertex"]
         if reconstruct_v:
             writes.append("v")
-        return (["h", "u", "cellsOnEdge", "dcEdge", "dvEdge", "edgesOnEdge_ECP", "nEdgesOnEdge", "verticesOnEdge",
+        if md:
+            writes.append("rho_edge")
+        return (["rho_zz" if md else "h", "u", "cellsOnEdge", "dcEdge", "dvEdge", "edgesOnEdge_ECP", "nEdgesOnEdge", "verticesOnEdge",
                  "weightsOnEdge", "edgesOnCell", "edgesOnCellSign", "invAreaCell", "nEdgesOnCell", "edgesOnVertex",
                  "edgesOnVertexSign", "fVertex", "invAreaTriangle"], writes)
     if task == "atm_recover_large_step_variables_work":  # (:1766-1872; rk_step 2 adds the exner part)
@@ -89,6 +98,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0):
                  "invAreaCell"], ["scalars"])
     if task == "scalars_save":  # srk3 with transport: scalars_old = scalars
         return ["scalars"], ["scalars_old"]
+    if task == "mpas_reconstruct_2d":
+        return (["u", "coeffs_reconstruct", "edgesOnCell", "nEdgesOnCell", "lat", "lon"],
+                ["uReconstructX", "uReconstructY", "uReconstructZ", "uReconstructZonal", "uReconstructMeridional"])
     raise KeyError(task)
 
 
@@ -129,18 +141,23 @@ def step_schedule(schedule=1, physics=0, transport=0):
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport"""
     if physics:
-        out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
+        p = {"physics": physics}
+        out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
                ("atm_compute_vert_imp_coefs", {}, 2)]
         if schedule == 1:
-            out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
-        out += [("atm_set_smlstep_pert_variables_work", {}, 3),
+            out += [("atm_compute_dyn_tend_work", {"rk_step": 0, **p}, 1),
+                    ("atm_compute_dyn_tend_work", {"rk_step": 1, **p}, 2)]
+        out += [("atm_set_smlstep_pert_variables_work", p, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "physics": 1}, 1),
                 ("atm_divergence_damping_3d", {}, 4),
                 ("atm_recover_large_step_variables_work", {"rk_step": 0}, 2),
                 ("atm_recover_large_step_variables_work", {"rk_step": 2}, 1),
-                ("atm_compute_solve_diagnostics", {}, 2), ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
+                ("atm_compute_solve_diagnostics", p, 2),
+                ("atm_compute_solve_diagnostics", {"reconstruct_v": True, **p}, 1),
                 ("atm_rk_dynamics_substep_finish", {}, 1)]
+        if physics == 2:
+            out.append(("mpas_reconstruct_2d", {}, 1))
         if transport:
             out += [("scalars_save", {}, 1), ("atm_advance_scalars_mono", {}, 1)]
         return out
