@@ -140,6 +140,15 @@ int mpas_reconstruct_2d(mpas_ctx* ctx, int includeHalos, int on_a_sphere);
  *       pressure = pressure_base + pressure_p on levels 0..nVertLevels-1 (theta is in the
  *       task's write set but its statement is commented out in the reference: unchanged) */
 int mpas_atm_compute_output_diagnostics(mpas_ctx* ctx);
+/* init_atm_case_jw (vertical_init/init_atm_cases.rg:366-432), host side, no context: the
+ * per-column hydrostatic iteration of the JW initial state (10 temperature x 25 pressure
+ * passes) for nCells columns of nVertLevels levels, arrays [cell][level] row-major:
+ * latCell[nCells]; pb, rb, zz (base pressure, base density, zz) in; dzw, dzu, fzm, fzp the
+ * vertical grid (length nVertLevels+1); pressure_p, rho_p, temperature out.  Split over
+ * nthreads host threads (<= 0: all).  mpasdyn/jw.py calls it for the large meshes. */
+int mpas_jw_hydrostatic(int32_t nCells, int32_t nVertLevels, const double* latCell, const double* pb,
+                        const double* rb, const double* zz, const double* dzw, const double* dzu, const double* fzm,
+                        const double* fzp, double* pressure_p, double* rho_p, double* temperature, int32_t nthreads);
 /* One-time tasks of atm_core_init (atm_core.rg:22-42) that run on the device:
  * :274 atm_compute_damping_coefs(config_zd, config_xnutr, cr) (atm_core.rg:41, defaults
  *       22000.0 and 0.2): dss of the upper damping layer */

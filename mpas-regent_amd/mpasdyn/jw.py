@@ -64,6 +64,55 @@ def _jw_temperature(eta, phi):
         + (1.6 * c ** 3 * (s ** 2 + 2.0 / 3.0) - np.pi / 4.0) * SPHERE_RADIUS * OMEGA)
 
 
+def _hydrostatic(phi, pb, rb, zz, g, L):
+    """:366-432 the hydrostatic iteration per column -> (pressure_p, rho_p, temperature):
+    libmpasdyn's host threads (mpas_jw_hydrostatic, the same arithmetic in the same order)
+    when the library is built, else the NumPy statement below"""
+    try:
+        from . import lib
+        so = lib.load()
+    except Exception:  # noqa: BLE001 -- host-side init only: NumPy computes the same values
+        so = None
+    nC = pb.shape[0]
+    pb, rb, zz = (np.ascontiguousarray(x, dtype=np.float64) for x in (pb, rb, zz))
+    if so is not None and nC > 0:
+        import ctypes
+        import os
+        pp, rr, tt = np.empty_like(pb), np.empty_like(pb), np.empty_like(pb)
+        vec = [np.ascontiguousarray(g[n], dtype=np.float64) for n in ("dzw", "dzu", "fzm", "fzp")]
+        lat = np.ascontiguousarray(phi, dtype=np.float64)
+        ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        rc = so.mpas_jw_hydrostatic(nC, L, ptr(lat), ptr(pb), ptr(rb), ptr(zz), *[ptr(v) for v in vec], ptr(pp),
+                                    ptr(rr), ptr(tt), min(16, os.cpu_count() or 1))
+        if rc != 0:
+            raise RuntimeError(f"mpas_jw_hydrostatic failed ({rc})")
+        return pp, rr, tt
+    dzw, dzu, fzm, fzp = g["dzw"], g["dzu"], g["fzm"], g["fzp"]
+    # level-major rows (the k loop is the slow axis), chunks of columns that stay in cache;
+    # the recurrence ppi(k+1) = ppi(k) - t(k) is np.subtract.accumulate (sequential roundings)
+    pp, rr, tt = np.zeros_like(pb), np.zeros_like(pb), np.zeros_like(pb)
+    cdz = (dzu[1:L] * GRAVITY)[:, None]
+    fzp1, fzm1 = fzp[1:L][:, None], fzm[1:L][:, None]
+    CH = 16384
+    for c0 in range(0, nC, CH):
+        sl = slice(c0, min(c0 + CH, nC))
+        pbT, rbT, zzT = np.ascontiguousarray(pb[sl].T), np.ascontiguousarray(rb[sl].T), np.ascontiguousarray(zz[sl].T)
+        ppT = np.zeros_like(pbT)
+        rrT = np.zeros_like(pbT)
+        acc = np.empty_like(ppT)
+        for _ in range(10):
+            ttT = np.ascontiguousarray(_jw_temperature(((pbT + ppT) / P0).T, phi[sl]).T)
+            for _ in range(25):
+                rrT = (ppT / (RGAS * zzT) - rbT * (ttT - T0B)) / ttT
+                acc[0] = P0 - 0.5 * dzw[0] * GRAVITY * (1.25 * (rrT[0] + rbT[0]) - 0.25 * (rrT[1] + rbT[1]))
+                acc[0] -= pbT[0]
+                acc[1:] = cdz * (rrT[:-1] * fzp1 + rrT[1:] * fzm1)
+                ppi = np.subtract.accumulate(acc, axis=0)
+                ppT = 0.2 * ppi + 0.8 * ppT
+        pp[sl], rr[sl], tt[sl] = ppT.T, rrT.T, ttT.T
+    return pp, rr, tt
+
+
 def init_atm_case_jw(m, st, perturb=False):
     """Fill the JW state into HostState st (built by build_state(m, L, "physical") on a
     0-based mesh m).  perturb: add the test case's zonal-wind perturbation (1 m/s Gaussian
@@ -105,31 +154,8 @@ def init_atm_case_jw(m, st, perturb=False):
     ex_b = (pb / P0) ** (RGAS / CP)
     rb = pb / (RGAS * T0B * zz)
     tb = T0B / ex_b
+    pp, rr, tt = _hydrostatic(phi, pb, rb, zz, g, L)
     dzw, dzu, fzm, fzp = g["dzw"], g["dzu"], g["fzm"], g["fzp"]
-    # the iteration runs level-major (contiguous level rows: the k loop is the slow axis),
-    # over chunks of columns small enough to stay in cache (it is column-independent)
-    # the level recurrence ppi(k+1) = ppi(k) - t(k) is np.subtract.accumulate over levels
-    # (the same sequential roundings as the level loop)
-    pp, rr, tt = np.zeros_like(pb), np.zeros_like(pb), np.zeros_like(pb)
-    cdz = (dzu[1:L] * GRAVITY)[:, None]
-    fzp1, fzm1 = fzp[1:L][:, None], fzm[1:L][:, None]
-    CH = 16384
-    for c0 in range(0, nC, CH):
-        sl = slice(c0, min(c0 + CH, nC))
-        pbT, rbT, zzT = np.ascontiguousarray(pb[sl].T), np.ascontiguousarray(rb[sl].T), np.ascontiguousarray(zz[sl].T)
-        ppT = np.zeros_like(pbT)
-        rrT = np.zeros_like(pbT)
-        acc = np.empty_like(ppT)
-        for _ in range(10):
-            ttT = np.ascontiguousarray(_jw_temperature(((pbT + ppT) / P0).T, phi[sl]).T)
-            for _ in range(25):
-                rrT = (ppT / (RGAS * zzT) - rbT * (ttT - T0B)) / ttT
-                acc[0] = P0 - 0.5 * dzw[0] * GRAVITY * (1.25 * (rrT[0] + rbT[0]) - 0.25 * (rrT[1] + rbT[1]))
-                acc[0] -= pbT[0]
-                acc[1:] = cdz * (rrT[:-1] * fzp1 + rrT[1:] * fzm1)
-                ppi = np.subtract.accumulate(acc, axis=0)
-                ppT = 0.2 * ppi + 0.8 * ppT
-        pp[sl], rr[sl], tt[sl] = ppT.T, rrT.T, ttT.T
     exner = ((pb + pp) / P0) ** (RGAS / CP)
     theta_m = tt / exner
     rho_zz = rb + rr
@@ -197,7 +223,7 @@ def init_atm_case_jw(m, st, perturb=False):
     woe = st["weightsOnEdge"][:nE]
     neoe = st["nEdgesOnEdge"][:nE, 0]
     v = np.zeros((nE, L + 1))
-    for i in range(eoe.shape[1]):
+    for i in range(int(neoe.max()) if nE else 0):
         on = i < neoe
         v += np.where(on[:, None], woe[:, i, None] * st["u"][np.where(on, eoe[:, i], 0)], 0.0)
     st["v"][:nE] = v

@@ -28,7 +28,7 @@ EXPORTS = [
     "mpas_atm_compute_damping_coefs", "mpas_atm_init_coupled_diagnostics", "mpas_atm_core_init",
     "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
     "mpas_halo_owned", "mpas_halo_interior", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
-    "mpas_halo_loopback", "mpas_halo_stats",
+    "mpas_halo_loopback", "mpas_halo_stats", "mpas_jw_hydrostatic",
 ]
 KIND_ID = {"cell": 0, "edge": 1, "vertex": 2}
 
@@ -103,6 +103,7 @@ def load():
         "mpas_halo_rccl": (i32, [vp, i32, i32, vp]),
         "mpas_halo_loopback": (i32, [ctypes.POINTER(vp), i32]),
         "mpas_halo_stats": (i32, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
+        "mpas_jw_hydrostatic": (i32, [i32, i32] + [vp] * 11 + [i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

@@ -5,10 +5,10 @@ config 2  x1.2562 x 56                 tests/test_gpu_parity.py (per task and pe
 config 3  x1.40962 x 56, full RK3     one atm_srk3 step vs the oracle (below)
 headline  x1.163842 x 56 (config 4's   one atm_srk3 step vs the oracle (below); the
           mesh; 8 GPUs split it)        8-subdomain split: tests/test_gpu_fullsize.py
-config 5  x1.655362 x 56 + moist       MPAS-solver step with the transport: 8-subdomain
-          transport, 8 GPUs            loopback split = single context, bit for bit; the
-                                        transport task at full size conserves
-                                        sum(rho s volume) and creates no new extrema
+config 5  x1.655362 x 56 + moist       MPAS-dynamics step with the transport from the JW
+          transport, 8 GPUs            state: 8-subdomain loopback split = single context,
+                                        bit for bit; the transport task at full size
+                                        conserves sum(rho s volume), no new extrema
 
 The bench workload is used as is: the mesh with its one-time precompute from the host,
 the 3-D state filled on the device by the seeded generator (bench.upload_inputs).  For
@@ -86,26 +86,46 @@ def test_srk3_step_vs_oracle(ncells):
 
 
 CHECK5 = ["u", "w", "theta_m", "rho_zz", "rho_p", "rtheta_p", "exner", "pressure_p", "ru", "rw", "ruAvg", "wwAvg",
-          "tend_u", "tend_theta", "pv_edge", "divergence", "ke", "vorticity", "scalars"]
+          "tend_u", "tend_w", "tend_theta", "pv_edge", "divergence", "ke", "vorticity", "scalars", "surface_pressure"]
 
 
 def test_config5_transport_step_decomposed_equals_single():
-    """config 5 on one GPU: x1.655362 x 56, MPAS vertical solver + monotonic transport of
-    the 8 scalars inside atm_srk3 (mpas-mode ids), split into the 8 subdomains of the
-    8-GPU run with the halo moved by the loopback transport (overlap on): bit-identical
-    to the undecomposed context, exact and benchmark paths"""
-    bench, m, st, dt = _workload(655362, zero_based=True)
-    opts = {"physics": 1, "transport": 1}
+    """config 5 on one GPU: x1.655362 x 56, the MPAS dynamics (physics = 2, which includes
+    the vertical solver of physics = 1) with the monotonic transport of 8 scalars inside
+    atm_srk3, from the perturbed JW state (a balanced atmosphere: every value finite), split
+    into the 8 subdomains of the 8-GPU run with the halo moved by the loopback transport
+    (overlap on): bit-identical to the undecomposed context, exact and benchmark paths"""
+    from mpasdyn import jw
+    from mpasdyn import mesh as M
+    m = M.zero_based(M.icosahedral(8))
+    st = jw.jw_state(m, L, perturb=True, subset=True, extra_names=("scalars",))
+    nC = m.nCells
+    st["scalars"][:nC, :L] = 0.02 * np.random.default_rng(5).random((nC, L, 8))
+    dt = 720.0 * 2.0 ** (4 - 8)  # 45 s (SURVEY §8.5)
+    opts = {"physics": 2, "transport": 1}
     n = 8
     d = decomp.Decomposition(st, n)
+    locs = [d.local_state(r) for r in range(n)]
+
+    def step(c):
+        T.atm_compute_solve_diagnostics(c, False, -1)  # MPAS-A's initial diagnostics
+        T.mpas_reconstruct_2d(c, False, True)
+        T.atm_srk3(c, dt, 1)
+        T.atm_compute_output_diagnostics(c)
     for exact in (1, 0):
-        ref = _gpu_step(bench, m, st, dt, exact, opts, names=CHECK5)
-        # (the synthetic state is not a balanced atmosphere: the MPAS solver's pow/exner
-        # turn most columns NaN within the step; compare_states demands the same NaN mask
-        # and equal values elsewhere, so the comparison covers the NaN pattern and every
-        # finite value -- the balanced JW state is decomposed in test_gpu_mpas_dynamics)
-        assert np.isfinite(ref["scalars"][:-1]).any() and np.isfinite(ref["tend_u"][:-1]).any()
-        locs = [d.local_state(r) for r in range(n)]
+        ref = HostState(m.nCells, m.nEdges, m.nVertices, L, names=CHECK5)
+        with lib.Context(m.nCells, m.nEdges, m.nVertices, L) as ctx:
+            ctx.set_option("exact", exact)
+            for k, v in opts.items():
+                ctx.set_option(k, v)
+            ctx.upload(st)
+            step(ctx)
+            ctx.sync()
+            ctx.download(ref)
+        for name in CHECK5:
+            assert np.isfinite(ref[name][:-1]).all(), name
+        sp = ref["surface_pressure"][:nC, 0]
+        assert np.abs(sp - 1.0e5).max() < 500.0  # one 45-s step of the (perturbed) JW state
         ctxs = [lib.Context(*d.n_local(r), L) for r in range(n)]
         outs = [HostState(*d.n_local(r), L, names=CHECK5) for r in range(n)]
         try:
@@ -114,13 +134,13 @@ def test_config5_transport_step_decomposed_equals_single():
                 for k, v in opts.items():
                     c.set_option(k, v)
                 lib.setup_subdomain(c, d, r)
-                bench.upload_inputs(c, locs[r])
+                c.upload(locs[r])
             lib.halo_loopback(ctxs)
             errs = [None] * n
 
             def drive(r):
                 try:
-                    T.atm_srk3(ctxs[r], dt, 1)
+                    step(ctxs[r])
                     ctxs[r].sync()
                 except Exception as e:  # noqa: BLE001 -- reported below
                     errs[r] = e
@@ -143,7 +163,7 @@ def test_config5_transport_step_decomposed_equals_single():
             got.arrays[name][-1] = ref.arrays[name][-1]  # the zero slot is not downloaded by rank
         bad = compare_states(got, ref, rtol=0.0, fields=CHECK5)
         assert not bad, f"exact={exact}: {bad[:6]}"
-        del ref, got, outs, locs
+        del ref, got, outs
 
 
 TRANSPORT_IN = ["ruAvg", "wwAvg", "rho_zz_old_split", "rho_zz", "scalars_old", "scalars"]
