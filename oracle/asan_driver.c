@@ -105,6 +105,19 @@ int main(int argc, char** argv) {
     ora_atm_srk3(&S, dt, 0);
     ora_atm_srk3(&S, dt, 1);
     ora_mpas_srk3_ex(&S, dt, 1, 1);
+    /* the MPAS dynamics (option physics = 2) */
+    ora_mpas_solve_diagnostics(&S, 0, -1);
+    ora_mpas_solve_diagnostics(&S, 0, 2);
+    ora_mpas_rk_integration_setup(&S);
+    ora_mpas_moist_coefficients(&S);
+    ora_mpas_dyn_tend(&S, 0, dt, 0, 0.0, 0, 1);
+    ora_mpas_dyn_tend(&S, 1, dt, 2, 0.5, 0, 0);
+    ora_mpas_set_smlstep(&S);
+    ora_mpas2_acoustic_step(&S, dt / 3, 0);
+    ora_mpas2_acoustic_step(&S, dt / 3, 1);
+    ora_mpas_substep_finish(&S, 1, 1);
+    ora_mpas_surface_pressure(&S);
+    ora_mpas_srk3_dyn(&S, dt, 1, 1, 2);
     for (int f = 0; f < F_COUNT; f++) free(S.f[f]);
     printf("asan_driver: every oracle task ran clean (nCells %d, L %d)\n", nC, L);
     return 0;
