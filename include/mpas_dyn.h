@@ -78,7 +78,12 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * "transport" = 1 (needs "physics" >= 1) makes mpas_atm_srk3 copy scalars
  * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
  * recover, before atm_rk_dynamics_substep_finish.  Default 0.  "trorder" = 1 (speed only)
- * orders the transport's column slots pair-major instead of entity-major. */
+ * orders the transport's column slots pair-major instead of entity-major.  "trtile" = 1
+ * (speed only, default 0) runs the transport as two tiled kernels with the scalars of
+ * compact cell tiles in LDS and no edge scratch, when every cell has at most 6 edges with
+ * at most 9 advCells each (bit-identical; measured slower); "trtcells" and
+ * "trtclo" bound a tile's cells (default 16) and LDS columns (default 96); read-only
+ * "trtile_active" / "trtile_count" report whether tiles are built and how many. */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
 /* reads every option above ("self", default 1: when every cell is
  * among the cellsOnEdge of its own edges -- mpas-mode ids -- the cell kernels gather

@@ -351,6 +351,272 @@ __global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
     }
 }
 
+// ---------------------------------------------------------------- tiled transport
+// Opt-in (option "trtile"; measured 2x slower than the three kernels above at x1.163842:
+// the traffic halves but A is computed four times per edge).
+// Two kernels and no edge scratch: a block is one (tile,
+// scalar) pair (TrTiles, mpas_dev.h).  It loads the scalars_old columns of its tile's
+// closure into LDS, then each cell of the tile forms the antidiffusive flux A of each of
+// its edges from LDS with k_tr_edge's expression -- the edge's A is computed by both of its
+// cells instead of stored once and gathered twice --, and
+//   k_trt_bounds  su, the bounds and R+ / R- (k_tr_bounds' expressions; R+ / R- stored)
+//   k_trt_update  su again, each A limited with R+ / R- of the edge's cells (gathered),
+//                 the new scalars (k_tr_update's expressions)
+// The same operations on the same values as the three kernels above: bit-identical.  Used
+// when every owned cell has at most NF edges and each of them at most AF advCells.
+struct TrtK {
+    const int *tptr, *tcell, *cptr, *ccell;
+    const int* slot;
+    int t0;
+};
+constexpr int TRT_THREADS = 1024;
+constexpr int TRT_WAVES = 8;  // min waves per SIMD (VGPR cap 64): two 16-wave blocks per CU, one tile cell per wave
+
+// this lane's column slot of the block (wave-uniform at LP = 64: SGPR)
+template <int LP>
+__device__ __forceinline__ int trt_slot() {
+    int s = (int)(threadIdx.x / LP);
+    if constexpr (LP == 64) s = __builtin_amdgcn_readfirstlane(s);
+    return s;
+}
+
+// level k of column col (64-bit column index: the x8 fields of the largest meshes exceed
+// 4 GiB) of field f
+template <int LP>
+__device__ __forceinline__ double& at64(const double* f, size_t col, int k) {
+    return *(double*)(f + col * LP + lpos(LP, k));
+}
+
+// A load the compiler may take through the scalar unit: the constant address space
+// declares the data read-only for the kernel's lifetime (mesh rows and the tile tables,
+// which no kernel writes).  With a wave-uniform address it is an s_load; through a
+// generic pointer the kernels' stores between cells would make every row entry a vector
+// load of its own (the compiler cannot prove they do not alias).
+#define MPAS_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ T ldc(const T* p) {
+    return *(const MPAS_CONST T*)(uintptr_t)p;
+}
+
+// The mesh data of one tile cell (LP = 64: every index is wave-uniform, so all of it
+// comes through the scalar unit).
+template <int LP>
+struct TrtCell {
+    int c, ne;
+    const int* row;
+    size_t r;
+    const DevState* S;
+
+    __device__ __forceinline__ void load(const DevState& S_, const TrtK& T, int qi, int k) {
+        (void)k;
+        S = &S_;
+        if constexpr (LP == 64) qi = __builtin_amdgcn_readfirstlane(qi);
+        c = ldc(T.tcell + qi);
+        ne = ldc(fi(*S, F_nEdgesOnCell) + c);
+        row = T.slot + (size_t)qi * TRT_ROW;
+        r = (size_t)c * 10;
+    }
+    __device__ __forceinline__ int slot(int idx) const { return ldc(row + idx); }
+    __device__ __forceinline__ int e(int i) const { return ldc(fi(*S, F_edgesOnCell) + r + i); }
+    __device__ __forceinline__ int s1(int i) const { return ldc(fi(*S, X_ce_s1) + r + i); }
+    __device__ __forceinline__ int oth(int i) const { return ldc(fi(*S, X_ce_oth) + r + i); }
+    __device__ __forceinline__ int c1(int i) const { return ldc(fi(*S, X_ce_c1) + r + i); }
+    __device__ __forceinline__ int c2(int i) const { return ldc(fi(*S, X_ce_c2) + r + i); }
+    __device__ __forceinline__ double dv(int i) const { return ldc(fd(*S, X_ce_dv) + r + i); }
+    __device__ __forceinline__ int na(int i) const { return ldc(fi(*S, F_nAdvCellsForEdge) + e(i)); }
+    __device__ __forceinline__ double ac(int i, int j) const { return ldc(fd(*S, F_adv_coefs) + (size_t)e(i) * 15 + j); }
+    __device__ __forceinline__ double ac3(int i, int j) const {
+        return ldc(fd(*S, F_adv_coefs_3rd) + (size_t)e(i) * 15 + j);
+    }
+};
+
+// the closure columns of scalar sc of the tile into LDS (column i at lds[i * LP], level
+// order); two columns per 16-B lane load at LP = 64 (ld2)
+template <int LP>
+__device__ __forceinline__ void trt_load(const DevState& S, const TrtK& T, int tile, int sc, double* lds) {
+    constexpr int NS = TRT_THREADS / LP, U = 4;
+    const int k = (int)(threadIdx.x % LP), slot = trt_slot<LP>();
+    const int cb = T.cptr[tile], n = T.cptr[tile + 1] - cb;
+    const double* so = fd(S, F_scalars_old);
+    for (int i0 = 2 * slot; i0 < n; i0 += 2 * U * NS) {
+        double a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + 2 * u * NS;
+            const int ca = T.ccell[cb + (i < n ? i : 0)], cbb = T.ccell[cb + (i + 1 < n ? i + 1 : 0)];
+            ld2<LP>(so, col8(ca, sc), col8(cbb, sc), k, a[u], b[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + 2 * u * NS;
+            if (i < n) lds[i * LP + k] = a[u];
+            if (i + 1 < n) lds[(i + 1) * LP + k] = b[u];
+        }
+    }
+    __syncthreads();
+}
+
+// edge slot i of one tile cell: the mass flux u, the scalar at cellsOnEdge(0/1) (x1, x2)
+// and the antidiffusive flux A (k_tr_edge: high-order - upwind, PADW as stored in X_Ah)
+template <int LP>
+__device__ __forceinline__ double trt_flux(const double* lds, const TrtCell<LP>& t, int i, double u, int k, int L,
+                                           double& x1, double& x2) {
+    const int b = 1 + i * (2 + AF), na = t.na(i);
+    x1 = lds[t.slot(b) * LP + k];
+    x2 = lds[t.slot(b + 1) * LP + k];
+    const double sgn = copysign(1.0, u);
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < AF; j++) {
+        const double wgt = t.ac(i, j) + sgn * t.ac3(i, j);
+        acc = add_if(j < na, acc, wgt * lds[t.slot(b + 2 + j) * LP + k]);
+    }
+    const double lo = t.dv(i) * (fmax(u, 0.0) * x1 + fmin(u, 0.0) * x2);
+    return PADW(u * acc - lo);
+}
+
+// The edge slots of a cell run as a loop (not unrolled: the scalar registers of one slot's
+// coefficients and LDS columns, ~40, would otherwise be live for all six at once and
+// spill); the global loads of slot i + 1 are issued before slot i is computed.
+template <int LP>
+__global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_bounds(DevState S, TrtK T, double dt) {
+    extern __shared__ double lds[];
+    const int v = xcd_block(S.xcd), tile = T.t0 + v / NSC, sc = v % NSC;
+    trt_load<LP>(S, T, tile, sc, lds);
+    constexpr int NS = TRT_THREADS / LP;
+    const int L = S.L, k = (int)(threadIdx.x % LP), slot = trt_slot<LP>();
+    const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    const double* ru = fd(S, F_ruAvg);
+    const int tb = T.tptr[tile], nt = T.tptr[tile + 1] - tb;
+    for (int q = slot; q < nt; q += NS) {
+        TrtCell<LP> t;
+        t.load(S, T, tb + q, k);
+        const int c = t.c;
+        const double invA = fd(S, F_invAreaCell)[c];
+        const double w = colk(fd(S, F_wwAvg), c), r_o = colk(fd(S, F_rho_zz_old_split), c),
+                     r_n = colk(fd(S, F_rho_zz), c);
+        const double s = lds[t.slot(0) * LP + k];
+        TrAcc r;
+        r.smax = r.smin = s;
+        // slots past nEdgesOnCell change nothing in k_tr_bounds (every update is masked)
+        const int ne = t.ne < NF ? t.ne : NF;
+        double un = colk(ru, t.e(0));
+#pragma unroll 1
+        for (int i = 0; i < ne; i++) {
+            const double u = un;
+            if (i + 1 < ne) un = colk(ru, t.e(i + 1));
+            double x1, x2;
+            const double A = trt_flux<LP>(lds, t, i, u, k, L, x1, x2);
+            tr_bound_slot(true, t.s1(i), t.dv(i), u, x1, x2, A, r);
+        }
+        double Rp, Rm, su;
+        tr_bound_fin<LP>(r, s, w, r_o, r_n, invA, rdzw, fzm, fzp, dt, k, L, Rp, Rm, su);
+        at64<LP>(fw(S, X_Rp), col8(c, sc), k) = Rp;
+        at64<LP>(fw(S, X_Rm), col8(c, sc), k) = Rm;
+    }
+}
+
+// R+ and R- of the two cells of edge slot i: p1/m1 at cellsOnEdge(0), p2/m2 at (1)
+template <int LP, bool SELF>
+__device__ __forceinline__ void trt_r(const double* Rp, const double* Rm, const TrtCell<LP>& t, int i, int sc,
+                                      double rp, double rm, int k, double& p1, double& m1, double& p2, double& m2) {
+    if constexpr (SELF) {  // the cell is one of the two: gather only the other
+        const size_t co = col8(t.oth(i), sc);
+        const double qo = at64<LP>(Rp, co, k), no = at64<LP>(Rm, co, k);
+        const bool f = t.s1(i);
+        p1 = f ? rp : qo, m1 = f ? rm : no, p2 = f ? qo : rp, m2 = f ? no : rm;
+    } else {
+        const size_t c1 = col8(t.c1(i), sc), c2 = col8(t.c2(i), sc);
+        p1 = at64<LP>(Rp, c1, k), m1 = at64<LP>(Rm, c1, k);
+        p2 = at64<LP>(Rp, c2, k), m2 = at64<LP>(Rm, c2, k);
+    }
+}
+
+template <int LP, bool SELF>
+__global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_update(DevState S, TrtK T, double dt) {
+    extern __shared__ double lds[];
+    const int v = xcd_block(S.xcd), tile = T.t0 + v / NSC, sc = v % NSC;
+    trt_load<LP>(S, T, tile, sc, lds);
+    constexpr int NS = TRT_THREADS / LP;
+    const int L = S.L, k = (int)(threadIdx.x % LP), slot = trt_slot<LP>();
+    const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    const double *Rp = fd(S, X_Rp), *Rm = fd(S, X_Rm), *ru = fd(S, F_ruAvg);
+    const int tb = T.tptr[tile], nt = T.tptr[tile + 1] - tb;
+    for (int q = slot; q < nt; q += NS) {
+        TrtCell<LP> t;
+        t.load(S, T, tb + q, k);
+        const int c = t.c;
+        const double invA = fd(S, F_invAreaCell)[c];
+        const double w = colk(fd(S, F_wwAvg), c), r_o = colk(fd(S, F_rho_zz_old_split), c),
+                     r_n = colk(fd(S, F_rho_zz), c);
+        const size_t cc = col8(c, sc);
+        const double rp = at64<LP>(Rp, cc, k), rm = at64<LP>(Rm, cc, k);
+        const double s = lds[t.slot(0) * LP + k];
+        // su as k_tr_bounds forms it (tr_bound_slot's upwind sum, tr_bound_fin's update),
+        // and the limited antidiffusive sum of k_tr_update (masked slots add nothing)
+        const int ne = t.ne < NF ? t.ne : NF;
+        double hlo = 0.0, hc = 0.0;
+        double un = colk(ru, t.e(0)), p1n, m1n, p2n, m2n;
+        trt_r<LP, SELF>(Rp, Rm, t, 0, sc, rp, rm, k, p1n, m1n, p2n, m2n);
+#pragma unroll 1
+        for (int i = 0; i < ne; i++) {
+            const double u = un, p1 = p1n, m1 = m1n, p2 = p2n, m2 = m2n;
+            if (i + 1 < ne) {
+                un = colk(ru, t.e(i + 1));
+                trt_r<LP, SELF>(Rp, Rm, t, i + 1, sc, rp, rm, k, p1n, m1n, p2n, m2n);
+            }
+            double x1, x2;
+            const double A = trt_flux<LP>(lds, t, i, u, k, L, x1, x2);
+            const double sg = t.s1(i) ? 1.0 : -1.0;
+            const double lo = t.dv(i) * (fmax(u, 0.0) * x1 + fmin(u, 0.0) * x2);
+            hlo = hlo + sg * lo;
+            hc = hc + sg * tr_limited(A, m1, p2, p1, m2);
+        }
+        double lob, Ab;
+        tr_vflux<LP>(s, w, k, L, fzm, fzp, lob, Ab);
+        const double lot = lvl_up<LP>(lob, k);
+        const double su = (s * r_o - dt * (hlo * invA + (lot - lob) * rdzw)) / r_n;
+        const double sn = tr_update_fin<LP>(hc, s, w, su, rp, rm, r_n, invA, rdzw, fzm, fzp, dt, k, L);
+        if (k < L) at64<LP>(fw(S, F_scalars), cc, k) = sn;
+    }
+}
+
+template <int LP>
+static hipError_t transport_tiled(const DevState& S, hipStream_t st, double dt) {
+    const TrTiles& TT = *S.trt;
+    // the tiles of a launch range: all owned cells, or (halo overlap) the interior or the
+    // boundary ones -- trt_build never puts interior and boundary cells in one tile
+    auto range = [&](const DevState& X, int& t0, int& t1) {
+        const int lo = X.lo[KC], hi = X.nCO;
+        t0 = t1 = 0;
+        if (lo >= hi) return true;
+        if (lo == 0 && hi == TT.nco) t1 = TT.ntiles;
+        else if (lo == 0 && hi == TT.nint) t1 = TT.nt_int;
+        else if (lo == TT.nint && hi == TT.nco) t0 = TT.nt_int, t1 = TT.ntiles;
+        else return false;
+        return true;
+    };
+    auto args = [&](int t0) { return TrtK{TT.tptr, TT.tcell, TT.cptr, TT.ccell, TT.slot, t0}; };
+    const size_t shm = (size_t)TT.maxclo * LP * sizeof(double);
+    hipError_t bad = hipSuccess;
+    auto k1 = [&](const DevState& X) {
+        int t0, t1;
+        if (!range(X, t0, t1)) bad = hipErrorInvalidValue;
+        else if (t1 > t0) k_trt_bounds<LP><<<(t1 - t0) * NSC, TRT_THREADS, shm, st>>>(X, args(t0), dt);
+    };
+    HALO_RUN(S, st, k1, F_scalars_old, F_ruAvg);
+    HALO_WROTE(S, X_Rp, X_Rm);
+    auto k2 = [&](const DevState& X) {
+        int t0, t1;
+        if (!range(X, t0, t1)) bad = hipErrorInvalidValue;
+        else if (t1 > t0 && X.selfc) k_trt_update<LP, true><<<(t1 - t0) * NSC, TRT_THREADS, shm, st>>>(X, args(t0), dt);
+        else if (t1 > t0) k_trt_update<LP, false><<<(t1 - t0) * NSC, TRT_THREADS, shm, st>>>(X, args(t0), dt);
+    };
+    HALO_RUN(S, st, k2, F_scalars_old, F_ruAvg, X_Rp, X_Rm);
+    HALO_WROTE(S, F_scalars);
+    return bad != hipSuccess ? bad : hipGetLastError();
+}
+
 template <int LP>
 static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
     constexpr int COLS = 256 / LP;  // column slots per block; a slot = one entity, two scalars
@@ -385,6 +651,7 @@ static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
     return hipGetLastError();
 }
 hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt) {
+    if (S.trt) MPAS_LP_DISPATCH(S.LP, transport_tiled, S, st, dt);
     MPAS_LP_DISPATCH(S.LP, transport_lp, S, st, dt);
 }
 

@@ -5,6 +5,7 @@
 
 #include <memory>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -95,6 +96,13 @@ struct mpas_ctx {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     int64_t graph_captures = 0, graph_launches = 0;
+    // option "trtile": the tiled transport (k_transport.hip) when the mesh allows it; the
+    // tiles are rebuilt after a mesh upload or a change of the owned / interior cells.
+    // Off by default: measured 2x slower than the three kernels
+    int trtile = 0;
+    int trt_cells = TRT_CELLS, trt_clo = 96;  // options "trtcells", "trtclo": tile size limits (speed only)
+    bool trt_dirty = true;
+    TrTiles trt;
 };
 
 namespace {
@@ -259,6 +267,136 @@ int guarded(mpas_ctx* c, Fn&& fn) {
     }
 }
 
+// ---- tiled transport: the cell tiles (TrTiles, mpas_dev.h) ----
+void trt_free(mpas_ctx* c) {
+    TrTiles& T = c->trt;
+    for (void* p : {(void*)T.tptr, (void*)T.tcell, (void*)T.cptr, (void*)T.ccell, (void*)T.slot})
+        if (p) (void)hipFree(p);
+    T = TrTiles{};
+    c->S.trt = nullptr;
+}
+template <class V>
+V* dev_copy(const std::vector<V>& h) {
+    V* d = nullptr;
+    hipcheck(hipMalloc(&d, sizeof(V) * (h.empty() ? 1 : h.size())), "hipMalloc");
+    if (!h.empty()) hipcheck(hipMemcpy(d, h.data(), sizeof(V) * h.size(), hipMemcpyHostToDevice), "hipMemcpy H2D");
+    return d;
+}
+template <class V>
+std::vector<V> dev_read(const void* d, size_t n) {
+    std::vector<V> h(n);
+    hipcheck(hipMemcpy(h.data(), d, sizeof(V) * n, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+    return h;
+}
+
+// Compact tiles of at most TRT_CELLS owned cells, grown breadth-first over the cells'
+// edge neighbours from the lowest unassigned cell id, within the interior and within the
+// boundary cells of a decomposed mesh (a launch range is one or both classes), and closed
+// before the closure -- the cells whose scalars_old the tile's kernels read, as the ids
+// on the device resolve -- would exceed trt_clo LDS columns (default 96: 48 KB at LP = 64,
+// three blocks per CU).  Not built (the three-kernel path runs) when an owned cell has more
+// than NF edges or one of its edges more than AF advCells.
+void trt_build(mpas_ctx* c) {
+    trt_free(c);
+    c->trt_dirty = false;
+    if (!c->trtile) return;
+    hipcheck(hipSetDevice(c->device), "hipSetDevice");
+    const DevState& S = c->S;
+    const int nC = S.nCells, nE = S.nEdges, nCO = S.nCO;
+    const int nint = (c->halo && c->halo->interior) ? c->halo->nint[0] : nCO;
+    const auto nEoC = dev_read<int>(S.f[F_nEdgesOnCell], (size_t)nC + 1);
+    const auto eoc = dev_read<int>(S.f[F_edgesOnCell], ((size_t)nC + 1) * 10);
+    const auto coe = dev_read<int>(S.f[F_cellsOnEdge], ((size_t)nE + 1) * 2);
+    const auto adv = dev_read<int>(S.f[F_advCellsForEdge], ((size_t)nE + 1) * 15);
+    const auto nadv = dev_read<int>(S.f[F_nAdvCellsForEdge], (size_t)nE + 1);
+    auto nedges = [&](int x) { return nEoC[x] > 0 ? nEoC[x] : 0; };
+    for (int x = 0; x < nCO; x++) {
+        if (nEoC[x] > NF) return;
+        for (int i = 0; i < nedges(x); i++)
+            if (nadv[eoc[(size_t)x * 10 + i]] > AF) return;
+    }
+    // the columns cell x's kernels read: x, both cells of each edge, the edge's advCells
+    auto need = [&](int x, auto&& f) {
+        f(x);
+        for (int i = 0; i < nedges(x); i++) {
+            const size_t e = (size_t)eoc[(size_t)x * 10 + i];
+            f(coe[e * 2]);
+            f(coe[e * 2 + 1]);
+            for (int j = 0; j < nadv[e]; j++) f(adv[e * 15 + j]);
+        }
+    };
+    std::vector<int> mark((size_t)nC + 1, -1), seen((size_t)nC + 1, -1), inq((size_t)nC + 1, -1);
+    std::vector<char> assigned((size_t)nC + 1, 0);
+    std::vector<int> tptr{0}, tcell, cptr{0}, ccell, queue, cells, clo;
+    std::vector<int> slot;
+    int stamp = 0, maxclo = 0, nt_int = 0;
+    for (int cls = 0; cls < 2; cls++) {
+        const int lo = cls ? nint : 0, hi = cls ? nCO : nint;
+        for (int seed = lo; seed < hi; seed++) {
+            if (assigned[seed]) continue;
+            const int tid = (int)tptr.size();
+            cells.clear();
+            clo.clear();
+            queue.assign(1, seed);
+            inq[seed] = tid;
+            for (size_t qh = 0; qh < queue.size() && (int)cells.size() < c->trt_cells; qh++) {
+                const int x = queue[qh];
+                int add = 0;
+                stamp++;
+                need(x, [&](int y) {
+                    if (mark[y] < 0 && seen[y] != stamp) seen[y] = stamp, add++;
+                });
+                if (!cells.empty() && (int)clo.size() + add > c->trt_clo) continue;
+                cells.push_back(x);
+                assigned[x] = 1;
+                need(x, [&](int y) {
+                    if (mark[y] < 0) mark[y] = (int)clo.size(), clo.push_back(y);
+                });
+                for (int i = 0; i < nedges(x); i++) {
+                    const size_t e = (size_t)eoc[(size_t)x * 10 + i];
+                    for (int side = 0; side < 2; side++) {
+                        const int y = coe[e * 2 + side];
+                        if (y >= lo && y < hi && !assigned[y] && inq[y] != tid) inq[y] = tid, queue.push_back(y);
+                    }
+                }
+            }
+            for (int x : cells) {  // the LDS rows
+                int row[TRT_ROW] = {};
+                row[0] = mark[x];
+                for (int i = 0; i < nedges(x); i++) {
+                    const size_t e = (size_t)eoc[(size_t)x * 10 + i];
+                    int* ri = row + 1 + i * (2 + AF);
+                    ri[0] = mark[coe[e * 2]];
+                    ri[1] = mark[coe[e * 2 + 1]];
+                    for (int j = 0; j < nadv[e]; j++) ri[2 + j] = mark[adv[e * 15 + j]];
+                }
+                slot.insert(slot.end(), row, row + TRT_ROW);
+                tcell.push_back(x);
+            }
+            for (int y : clo) mark[y] = -1, ccell.push_back(y);
+            maxclo = std::max(maxclo, (int)clo.size());
+            tptr.push_back((int)tcell.size());
+            cptr.push_back((int)ccell.size());
+        }
+        if (cls == 0) nt_int = (int)tptr.size() - 1;
+    }
+    TrTiles& T = c->trt;
+    T.ntiles = (int)tptr.size() - 1;
+    T.nt_int = nt_int;
+    T.nco = nCO;
+    T.nint = nint;
+    T.maxclo = maxclo;
+    T.tptr = dev_copy(tptr);
+    T.tcell = dev_copy(tcell);
+    T.cptr = dev_copy(cptr);
+    T.ccell = dev_copy(ccell);
+    T.slot = dev_copy(slot);
+    c->S.trt = &c->trt;
+}
+void trt_ensure(mpas_ctx* c) {
+    if (c->trt_dirty) trt_build(c);
+}
+
 // timing keys: one Regent task, split where its read/write set (B_alg) differs by argument
 // (bench.py aggregates the variants per task)
 const char* acoustic_name(int small_step) {
@@ -321,7 +459,10 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
     }
     if (c->transport)  // after the last stage's recover: ruAvg / wwAvg / rho_zz of the step
-        run_task(c, "atm_advance_scalars_mono", [&] { return launch_advance_scalars_mono(S, st, dt); });
+        run_task(c, "atm_advance_scalars_mono", [&] {
+            trt_ensure(c);  // (built before a capture by prepare_now)
+            return launch_advance_scalars_mono(S, st, dt);
+        });
     if (S.physics == 2)  // the MPAS dynamics: cell-centre winds for the next step's curvature
         run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });  // (:487, commented)
     run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
@@ -343,6 +484,7 @@ void prepare_now(mpas_ctx* c) {
         c->S.selfc = c->self_ok && c->self_on;
         c->dirty = false;
     }
+    if (c->transport) trt_ensure(c);
 }
 
 // one atm_srk3 step: replayed from a captured HIP graph when possible
@@ -467,6 +609,7 @@ int mpas_ctx_destroy(mpas_ctx* c) {
     }
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     graph_drop(c);
+    trt_free(c);
     c->halo.reset();
     c->loopgrp.reset();
     for (auto p : c->gid_dev)
@@ -511,6 +654,17 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             if (!value) c->transport = 0;
         } else if (name && std::strcmp(name, "trorder") == 0) {
             c->S.tro = value ? 1 : 0;
+        } else if (name && std::strcmp(name, "trtile") == 0) {
+            c->trtile = value ? 1 : 0;
+            c->trt_dirty = true;
+        } else if (name && std::strcmp(name, "trtcells") == 0) {
+            if (value < 1 || value > 256) throw Fail{MPAS_EINVAL, "trtcells must be 1..256"};
+            c->trt_cells = (int)value;
+            c->trt_dirty = true;
+        } else if (name && std::strcmp(name, "trtclo") == 0) {
+            if (value < 1 + NF * (2 + AF) || value > 120) throw Fail{MPAS_EINVAL, "trtclo must be 67..120 (LDS columns)"};
+            c->trt_clo = (int)value;
+            c->trt_dirty = true;
         } else if (name && std::strcmp(name, "transport") == 0) {
             if (value && !c->S.physics) throw Fail{MPAS_EINVAL, "transport needs physics = 1 (it reads the recovered ruAvg, wwAvg, rho_zz)"};
             c->transport = value ? 1 : 0;
@@ -534,6 +688,16 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "physics") == 0) *value = c->S.physics;
         else if (name && std::strcmp(name, "transport") == 0) *value = c->transport;
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
+        else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
+        else if (name && std::strcmp(name, "trtcells") == 0) *value = c->trt_cells;
+        else if (name && std::strcmp(name, "trtclo") == 0) *value = c->trt_clo;
+        else if (name && std::strcmp(name, "trtile_active") == 0) {  // tiles built for this mesh
+            trt_ensure(c);
+            *value = c->S.trt ? 1 : 0;
+        } else if (name && std::strcmp(name, "trtile_count") == 0) {
+            trt_ensure(c);
+            *value = c->trt.ntiles;
+        }
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "graph") == 0) *value = c->graph_on;
@@ -596,6 +760,7 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
         }
         hipcheck(hipMemcpy(c->S.f[f], buf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
         c->dirty = true;
+        c->trt_dirty = true;
         graph_drop(c);
         if (c->halo) c->halo->stale[f] = 0;  // uploaded ghosts are the global values
         // derived mesh arrays: cos()/sin() on the host with the same libm as the oracle
@@ -691,6 +856,7 @@ int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32
         c->S.nEO = nEdgesOwned;
         c->S.nVO = nVerticesOwned;
         c->dirty = true;
+        c->trt_dirty = true;
     });
 }
 
@@ -706,6 +872,7 @@ int mpas_halo_interior(mpas_ctx* c, int32_t nCI, int32_t nEI, int32_t nVI) {
         h->nint[2] = nVI;
         h->interior = true;
         h->overlap = c->overlap;
+        c->trt_dirty = true;
         if (!h->comm) {  // the halo stream, at the device's highest priority
             int least = 0, greatest = 0;
             hipcheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
@@ -872,7 +1039,12 @@ int mpas_atm_core_init(mpas_ctx* c) {
 }
 int mpas_atm_advance_scalars_mono(mpas_ctx* c, double dt) {
     if (!c) return MPAS_EINVAL;
-    MPAS_TASK("atm_advance_scalars_mono", launch_advance_scalars_mono(c->S, c->stream, dt));
+    return guarded(c, [&] {
+        run_task(c, "atm_advance_scalars_mono", [&] {
+            trt_ensure(c);
+            return launch_advance_scalars_mono(c->S, c->stream, dt);
+        });
+    });
 }
 int mpas_atm_compute_output_diagnostics(mpas_ctx* c) {
     MPAS_TASK("atm_compute_output_diagnostics", launch_output_diagnostics(c->S, c->stream));

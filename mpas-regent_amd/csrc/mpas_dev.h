@@ -85,6 +85,7 @@ struct FieldInfo {
 extern const FieldInfo kFields[X_COUNT];
 
 struct Halo;  // mpas_halo.h
+struct TrTiles;  // below: the cell tiles of the tiled transport
 
 struct DevState {
     int nCells, nEdges, nVertices, L, LP;  // local entity counts (= the zero-slot ids)
@@ -106,6 +107,7 @@ struct DevState {
                 // itself (SELF path); 0 (e.g. the literal 1-based "ref" ids) gathers both
     void* f[X_COUNT];
     Halo* halo;  // host-side halo exchanger of a decomposed mesh, nullptr otherwise
+    const TrTiles* trt;  // host-side: the tiles of the tiled transport, nullptr = the three-kernel path
     const int* gid[3];  // device global ids of the local cells/edges/vertices (decomposed
                         // meshes: the synthetic fill hashes them), nullptr = identity
 };
@@ -263,6 +265,25 @@ constexpr int NF = 6;   // edgesOnCell
 constexpr int QF = 10;  // edgesOnEdge
 constexpr int AF = 9;   // advCellsForEdge (the reference's list holds at most 9, :175)
 static_assert(NF % 2 == 0 && QF % 2 == 0, "the gathers go in pairs (gather2)");
+
+// Tiled transport (k_transport.hip, option "trtile"): the owned cells grouped into compact
+// tiles of at most TRT_CELLS cells (breadth-first growth on the host, mpas_ctx.cpp
+// trt_build); a tile's CLOSURE is every cell its kernels read scalars_old at -- the cells
+// themselves, both cells of each of their edges and the advCellsForEdge of those edges --
+// loaded into LDS once per (tile, scalar).  Per tile cell one row of TRT_ROW LDS slots:
+// the cell, then per edge slot i < NF: cellsOnEdge(0), cellsOnEdge(1), advCells(0..AF-1).
+constexpr int TRT_CELLS = 16;
+constexpr int TRT_ROW = 1 + NF * (2 + AF);
+struct TrTiles {
+    int ntiles = 0, nt_int = 0;  // tiles; the first nt_int hold interior cells only
+    int nco = 0, nint = 0;       // the owned / interior cell counts the tiles were built for
+    int maxclo = 0;              // largest closure (LDS columns per block)
+    int* tptr = nullptr;         // ntiles + 1: first cell of each tile in tcell
+    int* tcell = nullptr;        // the tiles' cells
+    int* cptr = nullptr;         // ntiles + 1: first closure cell of each tile in ccell
+    int* ccell = nullptr;        // closure cells, in LDS column order
+    int* slot = nullptr;          // TRT_ROW LDS columns per tile cell (tcell order)
+};
 
 // value of x held by level k-1 of the same column (0.0 at k == 0: level -1 reads 0)
 template <int LP>

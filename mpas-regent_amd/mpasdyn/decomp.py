@@ -13,7 +13,7 @@ the connectivity).  Here each rank owns
 and holds as ghosts every entity its owned entities reach through an index array of
 the path.  The closure is taken over exactly the index arrays the kernels follow
 (ID_ARRAYS, plus cellsOnEdge(edgesOnCell), which k_prepare composes for the cell
-kernels), so one hop from an owned entity never leaves the local set.  Every kernel
+kernels, and advCellsForEdge(edgesOnCell), which the tiled transport follows), so one hop from an owned entity never leaves the local set.  Every kernel
 computes owned entities only; a field a kernel gathers is made fresh on the ghosts by
 the device-side halo exchange right before it (csrc/mpas_halo.h; lazily, only after
 some kernel wrote it).  This keeps the ref-mode ids (raw 1-based offsets, which
@@ -81,6 +81,11 @@ class Decomposition:
         coe = np.vstack([self.ids["cellsOnEdge"], np.full((1, 2), nC)])
         eoc = self.ids["edgesOnCell"]
         self.cell_cells = np.concatenate([coe[eoc, 0], coe[eoc, 1]], axis=1)  # k_prepare's composition
+        # the tiled transport's composition (k_transport.hip k_trt_*: a cell forms the
+        # antidiffusive flux of each of its edges): advCellsForEdge(edgesOnCell), used entries
+        self._adv = np.vstack([self.ids["advCellsForEdge"], np.full((1, self.ids["advCellsForEdge"].shape[1]), nC)])
+        self._nadv = np.concatenate([np.asarray(st["nAdvCellsForEdge"][:nE, 0], dtype=np.int64), [0]])
+        self._nec = np.asarray(st["nEdgesOnCell"][:nC, 0], dtype=np.int64)
         self.owned, self.local, self.g2l, self.n_int = [], [], [], []
         for r in range(self.nparts):
             own = {k: np.flatnonzero(self.part[k] == r) for k in KINDS}
@@ -89,6 +94,8 @@ class Decomposition:
                 src = BY_NAME[f].entity
                 need[t].append(self.ids[f][own[src]].ravel())
             need["cell"].append(self.cell_cells[own["cell"]].ravel())
+            ca, cm = self.cell_adv(own["cell"])
+            need["cell"].append(ca[cm])
             # interior first: an owned entity is interior when every id its index arrays
             # (and k_prepare's composed cell ids) reach in their used entries is owned or
             # the zero slot -- its kernels use no ghost value, so they run while a halo
@@ -106,6 +113,7 @@ class Decomposition:
                 bnd[src] |= (~isown[t][self.ids[f][own[src]]] & use).any(axis=1)
             use = np.tile(active_mask(st, "edgesOnCell", own["cell"]), 2)
             bnd["cell"] |= (~isown["cell"][self.cell_cells[own["cell"]]] & use).any(axis=1)
+            bnd["cell"] |= (~isown["cell"][ca] & cm).any(axis=1)
             nint = {}
             for k in KINDS:
                 nint[k] = int(np.count_nonzero(~bnd[k]))
@@ -123,6 +131,16 @@ class Decomposition:
             self.local.append(loc)
             self.g2l.append(g2l)
             self.n_int.append(nint)
+
+    def cell_adv(self, cells):
+        """advCellsForEdge of the edges of `cells` (len, 10 * W) and the mask of the used
+        entries (edge slot below nEdgesOnCell, entry below nAdvCellsForEdge)"""
+        eoc = self.ids["edgesOnCell"][cells]
+        W = self._adv.shape[1]
+        ids = self._adv[eoc].reshape(len(cells), -1)
+        used = (np.arange(eoc.shape[1])[None, :] < self._nec[cells][:, None])[:, :, None]
+        used = used & (np.arange(W)[None, None, :] < self._nadv[eoc][:, :, None])
+        return ids, used.reshape(len(cells), -1)
 
     # ------------------------------------------------------------------ per rank
     def n_owned(self, r):
@@ -211,7 +229,8 @@ class Decomposition:
                 tg = self.ids[f][own[BY_NAME[f].entity]].ravel()
                 tg = tg[tg < self.n[t]]
                 bad += int(np.sum(self.g2l[r][t][tg] >= len(self.local[r][t])))
-            tg = self.cell_cells[own["cell"]].ravel()
-            tg = tg[tg < self.n["cell"]]
-            bad += int(np.sum(self.g2l[r]["cell"][tg] >= len(self.local[r]["cell"])))
+            ca, cm = self.cell_adv(own["cell"])
+            for tg in (self.cell_cells[own["cell"]].ravel(), ca[cm]):
+                tg = tg[tg < self.n["cell"]]
+                bad += int(np.sum(self.g2l[r]["cell"][tg] >= len(self.local[r]["cell"])))
         return bad

@@ -147,3 +147,26 @@ def test_srk3_transport_decomposed(x1_2562, L):
         got, _ = run_decomposed(st, 3, fn, exact)
         bad = compare_states(got, ref, rtol=0.0)
         assert not bad, f"exact={exact}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("L", [5, 56])
+def test_tiled_equals_three_kernel(x1_2562, L):
+    """option trtile (default on: the two tiled kernels, k_trt_*) against trtile = 0 (the
+    three kernels with the edge scratch): bit for bit; the tiles are active on the x1 mesh"""
+    st, _ = transport_state(x1_2562, L, DT)
+    outs = {}
+    for tile in (0, 1):
+        got = st.copy()
+        with lib.Context(*st.dims()) as ctx:
+            ctx.set_option("physics", 1)
+            ctx.set_option("trtile", tile)
+            ctx.upload(st)
+            assert ctx.get_option("trtile_active") == tile
+            if tile:
+                assert 0 < ctx.get_option("trtile_count") <= st.nCells
+            T.atm_advance_scalars_mono(ctx, DT)
+            ctx.sync()
+            ctx.download(got)
+        outs[tile] = got
+    bad = compare_states(outs[1], outs[0], rtol=0.0)
+    assert not bad, bad[:6]
