@@ -161,12 +161,31 @@ int mpas_atm_compute_damping_coefs(mpas_ctx* ctx, double config_zd, double confi
 /* :651 atm_init_coupled_diagnostics(cr, er, vert_r) (atm_core.rg:31): rho_zz /= zz, ru, rw,
  *       rho_p, rtheta_base, rtheta_p, exner, exner_base, pressure_p, pressure_base */
 int mpas_atm_init_coupled_diagnostics(mpas_ctx* ctx);
-/* atm_core.rg:22 atm_core_init: the device part in the reference's order --
- *       init_coupled_diagnostics, solve_diagnostics(hollingsworth = false, rk_step = -1),
- *       mpas_reconstruct_2d(false, true), compute_damping_coefs(config_zd = 22000,
- *       config_xnutr = 0.2; constants.rg:103-104).  atm_compute_signs, atm_adv_coef_compression,
- *       atm_couple_coef_3rd_order and atm_compute_mesh_scaling are mesh preparation the
- *       caller uploads (host side, mpasdyn/build_state.py); physics_init is a stub. */
+/* The mesh tasks of atm_core_init (k_mesh.hip; ids compared as uploaded, the bounds the
+ * reference leaves undefined as oracle/mpas_oracle.c states them; a decomposed context
+ * computes its owned entities, its ghosts keep the uploaded values):
+ * :46  atm_compute_signs(cr, er, vr) (atm_core.rg:22): edgesOnVertexSign, edgesOnCellSign,
+ *       kiteForCell, and zb_cell / zb3_cell copied from the never-written er.zb / zb3 (0.0) */
+int mpas_atm_compute_signs(mpas_ctx* ctx);
+/* :133 atm_adv_coef_compression(cr, er) (atm_core.rg:24): advCellsForEdge,
+ *       nAdvCellsForEdge (the index of the list's last cell, :184), adv_coefs and
+ *       adv_coefs_3rd from cellsOnCell, dcEdge, dvEdge and deriv_two (never initialised by
+ *       the reference, Q2: upload zeros for its semantics) */
+int mpas_atm_adv_coef_compression(mpas_ctx* ctx);
+/* :303 atm_couple_coef_3rd_order(config_coef_3rd_order, cr, er) (atm_core.rg:27, 0.25):
+ *       adv_coefs_3rd and zb3_cell (level 0) scaled */
+int mpas_atm_couple_coef_3rd_order(mpas_ctx* ctx, double config_coef_3rd_order);
+/* :595 atm_compute_mesh_scaling(cr, cpr, csr, cgr, er, config_h_ScaleWithMesh)
+ *       (atm_core.rg:39, true): meshScalingDel2 / Del4 from meshDensity (the regional
+ *       relaxation factors it also writes are read by no task of the path) */
+int mpas_atm_compute_mesh_scaling(mpas_ctx* ctx, int config_h_ScaleWithMesh);
+/* atm_core.rg:22 atm_core_init: every task in the reference's order -- compute_signs,
+ *       adv_coef_compression, couple_coef_3rd_order(0.25), init_coupled_diagnostics,
+ *       solve_diagnostics(hollingsworth = false, rk_step = -1), mpas_reconstruct_2d(false,
+ *       true), compute_mesh_scaling(true), compute_damping_coefs(config_zd = 22000,
+ *       config_xnutr = 0.2; constants.rg:103-104).  physics_init is a stub (OUT OF SCOPE).
+ *       Needs the raw mesh uploaded: connectivity (incl. cellsOnCell, cellsOnVertex),
+ *       dcEdge, dvEdge, deriv_two, meshDensity. */
 int mpas_atm_core_init(mpas_ctx* ctx);
 /* Monotonic scalar transport.  Replaces no reference entry point: the
  *       reference has none (Q26 -- scalars:double[8], data_structures.rg:36, is declared and

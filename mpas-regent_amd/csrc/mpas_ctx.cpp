@@ -146,7 +146,7 @@ size_t dev_bytes(const mpas_ctx* c, int f) {
 int id_target(int f) {
     switch (f) {
         case F_edgesOnCell: case F_edgesOnEdge: case F_edgesOnEdge_ECP: case F_edgesOnVertex: return K_E3;
-        case F_cellsOnEdge: case F_advCellsForEdge: return K_C3;
+        case F_cellsOnEdge: case F_advCellsForEdge: case F_cellsOnCell: case F_cellsOnVertex: return K_C3;
         case F_verticesOnEdge: case F_verticesOnCell: return K_V3;
         default: return -1;
     }
@@ -1023,17 +1023,41 @@ int mpas_atm_compute_damping_coefs(mpas_ctx* c, double config_zd, double config_
 int mpas_atm_init_coupled_diagnostics(mpas_ctx* c) {
     MPAS_TASK("atm_init_coupled_diagnostics", launch_init_coupled_diagnostics(c->S, c->stream));
 }
+// the mesh tasks of atm_core_init (k_mesh.hip); the adv lists feed k_prepare's edge
+// records and the transport tiles, so they are re-derived before the next task
+int mpas_atm_compute_signs(mpas_ctx* c) { MPAS_TASK("atm_compute_signs", launch_compute_signs(c->S, c->stream)); }
+int mpas_atm_adv_coef_compression(mpas_ctx* c) {
+    return guarded(c, [&] {
+        run_task(c, "atm_adv_coef_compression", [&] { return launch_adv_coef_compression(c->S, c->stream); });
+        c->dirty = true;
+        c->trt_dirty = true;
+        graph_drop(c);
+    });
+}
+int mpas_atm_couple_coef_3rd_order(mpas_ctx* c, double config_coef_3rd_order) {
+    MPAS_TASK("atm_couple_coef_3rd_order", launch_couple_coef_3rd_order(c->S, c->stream, config_coef_3rd_order));
+}
+int mpas_atm_compute_mesh_scaling(mpas_ctx* c, int config_h_ScaleWithMesh) {
+    MPAS_TASK("atm_compute_mesh_scaling", launch_mesh_scaling(c->S, c->stream, config_h_ScaleWithMesh));
+}
 int mpas_atm_core_init(mpas_ctx* c) {
-    // atm_core.rg:22-42 in order; the mesh tasks (atm_compute_signs, atm_adv_coef_compression,
-    // atm_couple_coef_3rd_order, atm_compute_mesh_scaling) are host-side preparation whose
-    // outputs the caller uploads (mpasdyn/build_state.py); physics_init is a stub
+    // atm_core.rg:22-42 in order (physics_init is a stub, OUT OF SCOPE; the namelist values
+    // config_coef_3rd_order = 0.25, config_h_ScaleWithMesh = true, config_zd = 22000,
+    // config_xnutr = 0.2)
     return guarded(c, [&] {
         hipcheck(hipSetDevice(c->device), "hipSetDevice");
         const DevState& S = c->S;
         hipStream_t st = c->stream;
+        run_task(c, "atm_compute_signs", [&] { return launch_compute_signs(S, st); });
+        run_task(c, "atm_adv_coef_compression", [&] { return launch_adv_coef_compression(S, st); });
+        c->dirty = true;  // (k_prepare re-derives the edge records before the next task)
+        c->trt_dirty = true;
+        graph_drop(c);
+        run_task(c, "atm_couple_coef_3rd_order", [&] { return launch_couple_coef_3rd_order(S, st, 0.25); });
         run_task(c, "atm_init_coupled_diagnostics", [&] { return launch_init_coupled_diagnostics(S, st); });
         run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, -1); });
         run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });
+        run_task(c, "atm_compute_mesh_scaling", [&] { return launch_mesh_scaling(S, st, 1); });
         run_task(c, "atm_compute_damping_coefs", [&] { return launch_damping_coefs(S, st, 22000.0, 0.2); });
     });
 }

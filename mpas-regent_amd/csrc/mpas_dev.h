@@ -176,6 +176,10 @@ hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sph
 hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
 hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt);
 hipError_t launch_damping_coefs(const DevState& S, hipStream_t st, double zd, double xnutr);
+hipError_t launch_compute_signs(const DevState& S, hipStream_t st);
+hipError_t launch_adv_coef_compression(const DevState& S, hipStream_t st);
+hipError_t launch_couple_coef_3rd_order(const DevState& S, hipStream_t st, double coef);
+hipError_t launch_mesh_scaling(const DevState& S, hipStream_t st, int config_h_ScaleWithMesh);
 hipError_t launch_init_coupled_diagnostics(const DevState& S, hipStream_t st);
 size_t summarize_scratch_bytes();
 hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, double* out);

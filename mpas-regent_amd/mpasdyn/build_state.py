@@ -227,6 +227,8 @@ def connectivity(m, st):
     st["edgesOnEdge_ECP"][:nE] = m.edgesOnEdge  # mesh_loading.rg:275
     st["nEdgesOnEdge"][:nE, 0] = m.nEdgesOnEdge
     st["edgesOnVertex"][:nV] = m.edgesOnVertex
+    st["cellsOnCell"][:nC] = m.cellsOnCell  # read by atm_adv_coef_compression (:133)
+    st["cellsOnVertex"][:nV] = m.cellsOnVertex  # read by atm_compute_signs (:46)
     st["weightsOnEdge"][:nE] = m.weightsOnEdge
     st["kiteAreasOnVertex"][:nV] = m.kiteAreasOnVertex  # (init scales [vertexDegree] only: OOB, no effect)
     md = getattr(m, "meshDensity", None)

@@ -34,13 +34,14 @@ KINDS = ("cell", "edge", "vertex")
 # integer fields holding entity ids -> the entity kind they refer to
 # (mirrors id_target() in csrc/mpas_ctx.cpp: these are clamped to [0, n] on upload)
 ID_ARRAYS = {"edgesOnCell": "edge", "edgesOnEdge": "edge", "edgesOnEdge_ECP": "edge", "edgesOnVertex": "edge",
-             "cellsOnEdge": "cell", "advCellsForEdge": "cell", "verticesOnEdge": "vertex", "verticesOnCell": "vertex"}
+             "cellsOnEdge": "cell", "advCellsForEdge": "cell", "verticesOnEdge": "vertex", "verticesOnCell": "vertex",
+             "cellsOnCell": "cell", "cellsOnVertex": "cell"}
 
 
 # list lengths of the variable-length index arrays: entries past them are padding the
 # kernels may load (unconditionally, ahead of the accumulation) but never use
 COUNTS = {"edgesOnCell": "nEdgesOnCell", "verticesOnCell": "nEdgesOnCell", "edgesOnEdge": "nEdgesOnEdge",
-          "edgesOnEdge_ECP": "nEdgesOnEdge", "advCellsForEdge": "nAdvCellsForEdge"}
+          "edgesOnEdge_ECP": "nEdgesOnEdge", "advCellsForEdge": "nAdvCellsForEdge", "cellsOnCell": "nEdgesOnCell"}
 
 
 def active_mask(st, f, rows):

@@ -26,6 +26,8 @@ EXPORTS = [
     "mpas_atm_recover_large_step_variables_work", "mpas_reconstruct_2d", "mpas_summarize_timestep",
     "mpas_atm_compute_output_diagnostics", "mpas_atm_advance_scalars_mono",
     "mpas_atm_compute_damping_coefs", "mpas_atm_init_coupled_diagnostics", "mpas_atm_core_init",
+    "mpas_atm_compute_signs", "mpas_atm_adv_coef_compression", "mpas_atm_couple_coef_3rd_order",
+    "mpas_atm_compute_mesh_scaling",
     "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
     "mpas_halo_owned", "mpas_halo_interior", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
     "mpas_halo_loopback", "mpas_halo_stats", "mpas_jw_hydrostatic",
@@ -89,6 +91,10 @@ def load():
         "mpas_atm_compute_damping_coefs": (i32, [vp, dbl, dbl]),
         "mpas_atm_init_coupled_diagnostics": (i32, [vp]),
         "mpas_atm_core_init": (i32, [vp]),
+        "mpas_atm_compute_signs": (i32, [vp]),
+        "mpas_atm_adv_coef_compression": (i32, [vp]),
+        "mpas_atm_couple_coef_3rd_order": (i32, [vp, dbl]),
+        "mpas_atm_compute_mesh_scaling": (i32, [vp, i32]),
         "mpas_summarize_timestep": (i32, [vp, i32, i32, i32, ctypes.POINTER(dbl)]),
         "mpas_timing_enable": (i32, [vp, i32]),
         "mpas_timing_reset": (i32, [vp]),

@@ -132,7 +132,8 @@ def renumber(m):
 
 # the state's integer fields that hold entity ids, and the kind they refer to
 ID_FIELDS = {"edgesOnCell": "edge", "verticesOnCell": "vertex", "cellsOnEdge": "cell", "verticesOnEdge": "vertex",
-             "edgesOnEdge": "edge", "edgesOnEdge_ECP": "edge", "advCellsForEdge": "cell", "edgesOnVertex": "edge"}
+             "edgesOnEdge": "edge", "edgesOnEdge_ECP": "edge", "advCellsForEdge": "cell", "edgesOnVertex": "edge",
+             "cellsOnCell": "cell", "cellsOnVertex": "cell"}
 
 
 def permute_state(st, perms):

@@ -105,8 +105,30 @@ def atm_init_coupled_diagnostics(ctx):
     ctx._check(ctx.lib.mpas_atm_init_coupled_diagnostics(ctx.h), "atm_init_coupled_diagnostics")
 
 
+def atm_compute_signs(ctx):
+    """dynamics_tasks.rg:46 (atm_core_init, atm_core.rg:22)"""
+    ctx._check(ctx.lib.mpas_atm_compute_signs(ctx.h), "atm_compute_signs")
+
+
+def atm_adv_coef_compression(ctx):
+    """dynamics_tasks.rg:133 (atm_core_init, atm_core.rg:24)"""
+    ctx._check(ctx.lib.mpas_atm_adv_coef_compression(ctx.h), "atm_adv_coef_compression")
+
+
+def atm_couple_coef_3rd_order(ctx, config_coef_3rd_order=0.25):
+    """dynamics_tasks.rg:303 (atm_core_init, atm_core.rg:27; namelist 0.25)"""
+    ctx._check(ctx.lib.mpas_atm_couple_coef_3rd_order(ctx.h, float(config_coef_3rd_order)),
+               "atm_couple_coef_3rd_order")
+
+
+def atm_compute_mesh_scaling(ctx, config_h_ScaleWithMesh=True):
+    """dynamics_tasks.rg:595 (atm_core_init, atm_core.rg:39)"""
+    ctx._check(ctx.lib.mpas_atm_compute_mesh_scaling(ctx.h, int(bool(config_h_ScaleWithMesh))),
+               "atm_compute_mesh_scaling")
+
+
 def atm_core_init(ctx):
-    """atm_core.rg:22: the device tasks of atm_core_init (the mesh preparation is uploaded)"""
+    """atm_core.rg:22: every task of atm_core_init in order, on the device"""
     ctx._check(ctx.lib.mpas_atm_core_init(ctx.h), "atm_core_init")
 
 

@@ -19,7 +19,7 @@
 static int id_kind(int f, int* hi) {
     switch (f) {
         case F_edgesOnCell: case F_edgesOnEdge: case F_edgesOnEdge_ECP: case F_edgesOnVertex: return 1;
-        case F_cellsOnEdge: case F_advCellsForEdge: return 0;
+        case F_cellsOnEdge: case F_advCellsForEdge: case F_cellsOnCell: case F_cellsOnVertex: return 0;
         case F_verticesOnEdge: case F_verticesOnCell: return 2;
         case F_nEdgesOnCell: *hi = 10; return -1;
         case F_nEdgesOnEdge: *hi = 20; return -1;
@@ -96,6 +96,10 @@ int main(int argc, char** argv) {
     ora_atm_compute_output_diagnostics(&S);
     ora_summarize_timestep(&S, 1, 1, out);
     ora_atm_compute_damping_coefs(&S, 22000.0, 0.2);
+    ora_atm_compute_signs(&S);
+    ora_atm_adv_coef_compression(&S);
+    ora_atm_couple_coef_3rd_order(&S, 0.25);
+    ora_atm_compute_mesh_scaling(&S, 1);
     ora_atm_init_coupled_diagnostics(&S);
     ora_mpas_vert_imp_coefs(&S, dt / 2);
     ora_mpas_acoustic_step(&S, dt / 2, 0);

@@ -1215,6 +1215,170 @@ void ora_atm_compute_damping_coefs(ora_state* S, double config_zd, double config
         }
 }
 
+/* ---- the mesh tasks of atm_core_init (atm_core.rg:22-39) ----
+ * Ids are compared as the arrays hold them (raw); reads through an id follow the Q1
+ * policy (ic2/ie2/iv2: outside [0, n] reads 0).  Out-of-range list writes the reference
+ * leaves undefined are bounded: the cell list of atm_adv_coef_compression is capped at
+ * maxEdges - 1 in both of its loops (the reference caps only the second, :175) and
+ * deriv_two(iCell * FIFTEEN + s) past the array's 30 entries reads 0.0. */
+#define MAXEDGES 10
+#define VERTEXDEGREE 3
+
+/* atm_compute_signs, dynamics_tasks.rg:46-130.  zb_cell / zb3_cell copy er.zb / er.zb3,
+ * which no task writes (Q2): 0.0.  kiteForCell keeps its value when no cellsOnVertex(j),
+ * j = 1..vertexDegree-1, matches (the loop breaks only on a match). */
+void ora_atm_compute_signs(ora_state* S) {
+    const int nC = S->nCells, nE = S->nEdges, nV = S->nVertices, L = S->L;
+    int32_t *eov = I(edgesOnVertex), *eoc = I(edgesOnCell), *voc = I(verticesOnCell), *kite = I(kiteForCell);
+    double *eovs = D(edgesOnVertexSign), *eocs = D(edgesOnCellSign), *zb = D(zb_cell), *zb3 = D(zb3_cell);
+#pragma omp parallel for schedule(static)
+    for (long v = 0; v < nV; v++)
+        for (int i = 0; i < VERTEXDEGREE; i++) {
+            const int e = eov[v * VERTEXDEGREE + i];
+            if (e <= nE) eovs[v * VERTEXDEGREE + i] = (v == ie2(S, I(verticesOnEdge), e, 2, 1)) ? 1.0 : -1.0;
+            else eovs[v * VERTEXDEGREE + i] = 0.0;
+        }
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++) {
+        int ne = ic2(S, I(nEdgesOnCell), c, 1, 0);
+        if (ne > MAXEDGES) ne = MAXEDGES;
+        for (int i = 0; i < ne; i++) {
+            const int e = eoc[c * MAXEDGES + i];
+            if (e <= nE) eocs[c * MAXEDGES + i] = (c == ie2(S, I(cellsOnEdge), e, 2, 0)) ? 1.0 : -1.0;
+            else eocs[c * MAXEDGES + i] = 0.0;
+        }
+        for (int k = 0; k <= L; k++)
+            for (int i = 0; i < ne; i++)
+                if (eoc[c * MAXEDGES + i] <= nE) {
+                    zb[(c * LV + k) * MAXEDGES + i] = 0.0;
+                    zb3[(c * LV + k) * MAXEDGES + i] = 0.0;
+                }
+        for (int i = 0; i < ne; i++) {
+            const int iVtx = voc[c * MAXEDGES + i];
+            if (iVtx <= nV) {
+                for (int j = 1; j < VERTEXDEGREE; j++)
+                    if (c == iv2(S, I(cellsOnVertex), iVtx, VERTEXDEGREE, j)) {
+                        kite[c * MAXEDGES + i] = j;
+                        break;
+                    }
+            } else {
+                kite[c * MAXEDGES + i] = 1;
+            }
+        }
+    }
+}
+
+/* atm_adv_coef_compression, dynamics_tasks.rg:133-269 (nAdvCellsForEdge = n is the index
+ * of the list's last cell, so the coefficient loops over j < n never see it; pow(dc, 2)
+ * as dc * dc) */
+void ora_atm_adv_coef_compression(ora_state* S) {
+    const int nC = S->nCells, nE = S->nEdges;
+    int32_t *nadv = I(nAdvCellsForEdge), *advc = I(advCellsForEdge);
+    double *ac = D(adv_coefs), *ac3 = D(adv_coefs_3rd), *d2 = D(deriv_two);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        nadv[e] = 0;
+        const int cell1 = ie2(S, I(cellsOnEdge), e, 2, 0), cell2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+        if (!(cell1 <= nC || cell2 <= nC)) continue;
+        int cl[MAXEDGES];
+        cl[0] = cell1;
+        cl[1] = cell2;
+        int n = 1;
+        const int ne1 = ic2(S, I(nEdgesOnCell), cell1, 1, 0), ne2 = ic2(S, I(nEdgesOnCell), cell2, 1, 0);
+        for (int i = 0; i < ne1; i++) {
+            const int cc = ic2(S, I(cellsOnCell), cell1, MAXEDGES, i);
+            if (cc != cell2 && n < MAXEDGES - 1) cl[++n] = cc;
+        }
+        for (int ic = 0; ic < ne2; ic++) {
+            const int cc = ic2(S, I(cellsOnCell), cell2, MAXEDGES, ic);
+            int add = 1;
+            for (int i = 0; i < n; i++)
+                if (cl[i] == cc) add = 0;
+            if (add && n < MAXEDGES - 1) cl[++n] = cc;
+        }
+        nadv[e] = n;
+        for (int i = 0; i < n; i++) advc[e * 15 + i] = cl[i];
+        double* a = ac + e * 15;
+        double* a3 = ac3 + e * 15;
+        for (int j = 0; j < 15; j++) a[j] = a3[j] = 0.0;
+        const double* dt2 = d2 + e * 30;
+#define D2(idx) ((idx) < 30 ? dt2[(idx)] : 0.0)
+        int j_in = 0;
+        for (int j = 0; j < n; j++)
+            if (cl[j] == cell1) j_in = j;
+        a[j_in] += dt2[0];
+        a3[j_in] += dt2[0];
+        for (int ic = 0; ic < ne1; ic++) {
+            j_in = 0;
+            for (int j = 0; j < n; j++)
+                if (cl[j] == ic2(S, I(cellsOnCell), cell1, MAXEDGES, ic)) j_in = j;
+            a[j_in] += D2(ic * 15 + 0);
+            a3[j_in] += D2(ic * 15 + 0);
+        }
+        j_in = 0;
+        for (int j = 0; j < n; j++)
+            if (cl[j] == cell2) j_in = j;
+        a[j_in] += dt2[1];
+        a3[j_in] += dt2[1];
+        for (int ic = 0; ic < ne2; ic++) {
+            j_in = 0;
+            for (int j = 0; j < n; j++)
+                if (cl[j] == ic2(S, I(cellsOnCell), cell2, MAXEDGES, ic)) j_in = j;
+            a[j_in] += D2(ic * 15 + 1);
+            a3[j_in] += D2(ic * 15 + 1);
+        }
+#undef D2
+        const double dc = re2(S, D(dcEdge), e, 1, 0), dv = re2(S, D(dvEdge), e, 1, 0);
+        for (int j = 0; j < n; j++) {
+            a[j] = -1.0 * (dc * dc) * a[j] / 12;
+            a3[j] = -1.0 * (dc * dc) * a3[j] / 12;
+        }
+        j_in = 0;
+        for (int j = 0; j < n; j++)
+            if (cl[j] == cell1) j_in = j;
+        a[j_in] += 0.5;
+        j_in = 0;
+        for (int j = 0; j < n; j++)
+            if (cl[j] == cell2) j_in = j;
+        a[j_in] += 0.5;
+        for (int j = 0; j < n; j++) {
+            a[j] *= dv;
+            a3[j] *= dv;
+        }
+    }
+}
+
+/* atm_couple_coef_3rd_order, dynamics_tasks.rg:303-325 (zb3_cell at level 0 only) */
+void ora_atm_couple_coef_3rd_order(ora_state* S, double config_coef_3rd_order) {
+    const int nC = S->nCells, nE = S->nEdges;
+    double *ac3 = D(adv_coefs_3rd), *zb3 = D(zb3_cell);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++)
+        for (int i = 0; i < 15; i++) ac3[e * 15 + i] *= config_coef_3rd_order;
+#pragma omp parallel for schedule(static)
+    for (long c = 0; c < nC; c++)
+        for (int j = 0; j < MAXEDGES; j++) zb3[(c * LV + 0) * MAXEDGES + j] *= config_coef_3rd_order;
+}
+
+/* atm_compute_mesh_scaling, dynamics_tasks.rg:595-646: the del2 / del4 scaling of each
+ * edge (cellOne / cellTwo = the cells of cellsOnEdge(0/1), data_structures.rg:486-487).
+ * The regional-relaxation factors it also writes are read by no task of the path. */
+void ora_atm_compute_mesh_scaling(ora_state* S, int config_h_ScaleWithMesh) {
+    const int nE = S->nEdges;
+    double *d2 = D(meshScalingDel2), *d4 = D(meshScalingDel4), *md = D(meshDensity);
+#pragma omp parallel for schedule(static)
+    for (long e = 0; e < nE; e++) {
+        d2[e] = 1.0;
+        d4[e] = 1.0;
+        if (config_h_ScaleWithMesh) {
+            const int c1 = ie2(S, I(cellsOnEdge), e, 2, 0), c2 = ie2(S, I(cellsOnEdge), e, 2, 1);
+            const double avg = (rc2(S, md, c1, 1, 0) + rc2(S, md, c2, 1, 0)) / 2.0;
+            d2[e] = 1.0 / pow(avg, 0.25);
+            d4[e] = 1.0 / pow(avg, 0.75);
+        }
+    }
+}
+
 /* atm_init_coupled_diagnostics, dynamics_tasks.rg:651-726: rho_zz /= zz, ru from u, rw
  * from w and the slope flux of ru, then rho_p, rtheta_base/_p, exner(_base), pressure */
 void ora_atm_init_coupled_diagnostics(ora_state* S) {

@@ -60,6 +60,10 @@ def load():
             "ora_mpas_srk3_ex": (None, [p, dbl, i32, i32]),
             "ora_mpas_advance_scalars_mono": (None, [p, dbl]),
             "ora_atm_compute_damping_coefs": (None, [p, dbl, dbl]),
+            "ora_atm_compute_signs": (None, [p]),
+            "ora_atm_adv_coef_compression": (None, [p]),
+            "ora_atm_couple_coef_3rd_order": (None, [p, dbl]),
+            "ora_atm_compute_mesh_scaling": (None, [p, i32]),
             "ora_atm_init_coupled_diagnostics": (None, [p]),
             "ora_mpas_recover": (None, [p, i32, i32, dbl]),
             "ora_summarize_timestep": (None, [p, i32, i32, ctypes.POINTER(ctypes.c_double)]),
@@ -184,11 +188,31 @@ class Oracle:
     def atm_init_coupled_diagnostics(self):
         self.lib.ora_atm_init_coupled_diagnostics(self.p)
 
+    def atm_compute_signs(self):
+        """dynamics_tasks.rg:46-130"""
+        self.lib.ora_atm_compute_signs(self.p)
+
+    def atm_adv_coef_compression(self):
+        """dynamics_tasks.rg:133-269"""
+        self.lib.ora_atm_adv_coef_compression(self.p)
+
+    def atm_couple_coef_3rd_order(self, config_coef_3rd_order=0.25):
+        """dynamics_tasks.rg:303-325"""
+        self.lib.ora_atm_couple_coef_3rd_order(self.p, config_coef_3rd_order)
+
+    def atm_compute_mesh_scaling(self, config_h_ScaleWithMesh=True):
+        """dynamics_tasks.rg:595-646"""
+        self.lib.ora_atm_compute_mesh_scaling(self.p, int(bool(config_h_ScaleWithMesh)))
+
     def atm_core_init(self):
-        """atm_core.rg:22-42, the state tasks in order (mesh preparation: build_state)"""
+        """atm_core.rg:22-42: every task in order (physics_init is a stub, OUT OF SCOPE)"""
+        self.atm_compute_signs()
+        self.atm_adv_coef_compression()
+        self.atm_couple_coef_3rd_order(0.25)
         self.atm_init_coupled_diagnostics()
         self.atm_compute_solve_diagnostics(0, -1)
         self.mpas_reconstruct_2d(False, True)
+        self.atm_compute_mesh_scaling(True)
         self.atm_compute_damping_coefs(22000.0, 0.2)
 
     def mpas_advance_scalars_mono(self, dt):

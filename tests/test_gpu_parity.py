@@ -378,6 +378,33 @@ def test_init_tasks(x1_2562, L, variant, task):
         assert np.any(ref["dss"][:st.nCells] > 0)
 
 
+MESH_TASKS = {
+    "signs": (lambda o: o.atm_compute_signs(), lambda c: T.atm_compute_signs(c), set()),
+    "adv_coef": (lambda o: o.atm_adv_coef_compression(), lambda c: T.atm_adv_coef_compression(c), set()),
+    "couple": (lambda o: o.atm_couple_coef_3rd_order(0.25), lambda c: T.atm_couple_coef_3rd_order(c, 0.25), set()),
+    "mesh_scaling": (lambda o: o.atm_compute_mesh_scaling(True), lambda c: T.atm_compute_mesh_scaling(c, True),
+                     {"meshScalingDel2", "meshScalingDel4"}),
+}
+
+
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
+@pytest.mark.parametrize("task", list(MESH_TASKS))
+def test_mesh_tasks(x1_2562, variant, task):
+    """the mesh tasks of atm_core_init (dynamics_tasks.rg:46, :133, :303, :595) on the
+    device: value-identical to the oracle (mesh scaling: pow of the device vs glibc,
+    RTOL_POW); deriv_two (never initialised by the reference) random so that every
+    coefficient term is exercised, kiteForCell pre-set (kept where no vertex matches)"""
+    ofn, gfn, tf = MESH_TASKS[task]
+    st = base_state(x1_2562, 5, variant).copy()
+    nE = st.nEdges
+    st["deriv_two"][:nE] = np.random.default_rng(7).standard_normal((nE, 30))
+    st["kiteForCell"][:st.nCells] = 7
+    ref = run_oracle(st, ofn)
+    got = run_gpu(st, gfn, exact=1)
+    bad = compare_states(got, ref, rtol=RTOL_POW, tol_fields=tf or None) if tf else compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
 @pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
 def test_atm_core_init(x1_2562, variant):
     """mpas_atm_core_init = the device tasks of atm_core_init in the reference's order"""
@@ -386,6 +413,6 @@ def test_atm_core_init(x1_2562, variant):
     ref = run_oracle(st, lambda o: o.atm_core_init())
     got = run_gpu(st, lambda c: T.atm_core_init(c), exact=1)
     tf = {"dss", "exner", "exner_base", "pressure_p", "pressure_base", "uReconstructX", "uReconstructY",
-          "uReconstructZ", "uReconstructZonal", "uReconstructMeridional"}
+          "uReconstructZ", "uReconstructZonal", "uReconstructMeridional", "meshScalingDel2", "meshScalingDel4"}
     bad = compare_states(got, ref, rtol=RTOL_POW, tol_fields=tf)
     assert not bad, bad[:6]
