@@ -152,6 +152,16 @@ int id_target(int f) {
     }
 }
 
+// width of the id rows a count field gives the length of (0: not a count)
+int count_width(int f) {
+    switch (f) {
+        case F_nEdgesOnCell: return 10;      // edgesOnCell, verticesOnCell, cellsOnCell, edgesOnCell_sign, ...
+        case F_nEdgesOnEdge: return 20;      // edgesOnEdge, weightsOnEdge
+        case F_nAdvCellsForEdge: return 15;  // advCellsForEdge, adv_coefs(_3rd)
+        default: return 0;
+    }
+}
+
 int task_index(mpas_ctx* c, const char* name) {
     for (size_t i = 0; i < c->task_names.size(); i++)
         if (c->task_names[i] == name) return (int)i;
@@ -747,10 +757,17 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
             int32_t* d = (int32_t*)buf.data();
             int tgt = id_target(f);
             int lim = tgt < 0 ? 0 : entity_count(c, tgt);
+            // list lengths: the kernels index rows of this width with them (tail loops past
+            // the unrolled entries), so a longer list would read past the row -- refused
+            const int width = count_width(f);
             for (int e = 0; e < n; e++)
                 for (int i = 0; i < W; i++) {
                     int32_t v = *(const int32_t*)(h + e * se + i * sc);
                     if (tgt >= 0 && (v < 0 || v > lim)) v = lim;  // Q1 zero slot
+                    if (width > 0 && v > width)
+                        throw Fail{MPAS_EINVAL, std::string("mpas_upload: ") + fi.name + " " + std::to_string(v) +
+                                                    " at entity " + std::to_string(e) + " exceeds its list width " +
+                                                    std::to_string(width)};
                     d[(size_t)e * W + i] = v;
                 }
         } else {

@@ -416,3 +416,16 @@ def test_atm_core_init(x1_2562, variant):
           "uReconstructZ", "uReconstructZonal", "uReconstructMeridional", "meshScalingDel2", "meshScalingDel4"}
     bad = compare_states(got, ref, rtol=RTOL_POW, tol_fields=tf)
     assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("field,width", [("nEdgesOnCell", 10), ("nEdgesOnEdge", 20), ("nAdvCellsForEdge", 15)])
+def test_upload_rejects_overlong_lists(x1_2562, field, width):
+    """a list length past its row width (the kernels' tail loops would read past the row)
+    is refused at the boundary; the row width itself is accepted"""
+    st = base_state(x1_2562, 5, "mpas0").copy()
+    with lib.Context(*st.dims()) as ctx:
+        st[field][3, 0] = width
+        ctx.upload(st, names=[field])
+        st[field][3, 0] = width + 1
+        with pytest.raises(lib.MpasError, match="exceeds its list width"):
+            ctx.upload(st, names=[field])
