@@ -584,8 +584,9 @@ __global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_update(DevState 
 template <int LP>
 static hipError_t transport_tiled(const DevState& S, hipStream_t st, double dt) {
     const TrTiles& TT = *S.trt;
-    // the tiles of a launch range: all owned cells, or (halo overlap) the interior or the
-    // boundary ones -- trt_build never puts interior and boundary cells in one tile
+    // the tiles of a launch range: all owned cells, or (halo overlap) those of the interior
+    // launch (interior cells reading owned columns only) or of the boundary launch (the
+    // rest) -- trt_build's launch classes; every owned cell is in exactly one tile
     auto range = [&](const DevState& X, int& t0, int& t1) {
         const int lo = X.lo[KC], hi = X.nCO;
         t0 = t1 = 0;

@@ -300,8 +300,8 @@ std::vector<V> dev_read(const void* d, size_t n) {
 }
 
 // Compact tiles of at most TRT_CELLS owned cells, grown breadth-first over the cells'
-// edge neighbours from the lowest unassigned cell id, within the interior and within the
-// boundary cells of a decomposed mesh (a launch range is one or both classes), and closed
+// edge neighbours from the lowest unassigned cell id, within one launch class of a
+// decomposed mesh (below), and closed
 // before the closure -- the cells whose scalars_old the tile's kernels read, as the ids
 // on the device resolve -- would exceed trt_clo LDS columns (default 96: 48 KB at LP = 64,
 // three blocks per CU).  Not built (the three-kernel path runs) when an owned cell has more
@@ -340,10 +340,20 @@ void trt_build(mpas_ctx* c) {
     std::vector<int> tptr{0}, tcell, cptr{0}, ccell, queue, cells, clo;
     std::vector<int> slot;
     int stamp = 0, maxclo = 0, nt_int = 0;
+    // launch classes: 0 = interior cells whose every column is owned (or the zero slot),
+    // run beside a halo exchange; 1 = the rest (boundary cells, and interior cells that
+    // reach a ghost through advCellsForEdge(edgesOnCell), which the halo's interior
+    // classification does not follow), run after it
+    std::vector<char> cls_of((size_t)nC + 1, 1);
+    for (int x = 0; x < nint; x++) {
+        bool own = true;
+        need(x, [&](int y) { own = own && (y < nCO || y == nC); });
+        cls_of[x] = own ? 0 : 1;
+    }
     for (int cls = 0; cls < 2; cls++) {
-        const int lo = cls ? nint : 0, hi = cls ? nCO : nint;
+        const int lo = 0, hi = nCO;
         for (int seed = lo; seed < hi; seed++) {
-            if (assigned[seed]) continue;
+            if (assigned[seed] || cls_of[seed] != cls) continue;
             const int tid = (int)tptr.size();
             cells.clear();
             clo.clear();
@@ -366,7 +376,8 @@ void trt_build(mpas_ctx* c) {
                     const size_t e = (size_t)eoc[(size_t)x * 10 + i];
                     for (int side = 0; side < 2; side++) {
                         const int y = coe[e * 2 + side];
-                        if (y >= lo && y < hi && !assigned[y] && inq[y] != tid) inq[y] = tid, queue.push_back(y);
+                        if (y >= lo && y < hi && cls_of[y] == cls && !assigned[y] && inq[y] != tid)
+                            inq[y] = tid, queue.push_back(y);
                     }
                 }
             }

@@ -114,7 +114,9 @@ class Decomposition:
                 bnd[src] |= (~isown[t][self.ids[f][own[src]]] & use).any(axis=1)
             use = np.tile(active_mask(st, "edgesOnCell", own["cell"]), 2)
             bnd["cell"] |= (~isown["cell"][self.cell_cells[own["cell"]]] & use).any(axis=1)
-            bnd["cell"] |= (~isown["cell"][ca] & cm).any(axis=1)
+            # (the advCellsForEdge(edgesOnCell) composition makes ghosts but not boundary
+            # cells: the tiled transport moves its interior cells that reach a ghost through
+            # it into its boundary launch itself, mpas_ctx.cpp trt_build)
             nint = {}
             for k in KINDS:
                 nint[k] = int(np.count_nonzero(~bnd[k]))

@@ -123,12 +123,14 @@ def _with(opts, fn):
 
 @pytest.mark.parametrize("nparts", [2, 3])
 @pytest.mark.parametrize("overlap", [1, 0])
-def test_transport_decomposed_equals_single(x1_2562, nparts, overlap):
+@pytest.mark.parametrize("trtile", [0, 1])
+def test_transport_decomposed_equals_single(x1_2562, nparts, overlap, trtile):
     """N subdomains (loopback halo: the x8 fields move as 8 columns per entity) give the
-    single-context result bit for bit"""
+    single-context result bit for bit, with the three kernels and with the tiles (whose
+    interior launch takes only the cells reading owned columns)"""
     from test_gpu_decomp import run_decomposed, run_single
     st, _ = transport_state(x1_2562, 56, DT)
-    fn = _with({"physics": 1}, lambda c: T.atm_advance_scalars_mono(c, DT))
+    fn = _with({"physics": 1, "trtile": trtile}, lambda c: T.atm_advance_scalars_mono(c, DT))
     ref = run_single(st, fn, 1)
     got, stats = run_decomposed(st, nparts, fn, 1, overlap=overlap)
     bad = compare_states(got, ref, rtol=0.0)
@@ -151,7 +153,7 @@ def test_srk3_transport_decomposed(x1_2562, L):
 
 @pytest.mark.parametrize("L", [5, 56])
 def test_tiled_equals_three_kernel(x1_2562, L):
-    """option trtile (default on: the two tiled kernels, k_trt_*) against trtile = 0 (the
+    """option trtile = 1 (opt-in: the two tiled kernels, k_trt_*) against trtile = 0 (the
     three kernels with the edge scratch): bit for bit; the tiles are active on the x1 mesh"""
     st, _ = transport_state(x1_2562, L, DT)
     outs = {}
