@@ -102,7 +102,11 @@ int mpas_field_width(int field_id);
  * byte offset e*stride_entity + k*stride_level + i*stride_comp of host (levels 0..L,
  * entities 0..n-1; components only for array fields).  Element type: double for fp64
  * fields, int32 for integer fields, uint8 for masks.  Entity-id fields are clamped
- * on upload so that any id outside [0, n] resolves to the zero slot n. */
+ * on upload so that any id outside [0, n] resolves to the zero slot n; a list
+ * length (nEdgesOnCell, nEdgesOnEdge, nAdvCellsForEdge) past its row width is refused.
+ * The view may be device memory (a Legion instance in framebuffer memory, a torch tensor;
+ * hipPointerGetAttributes decides): 3-D fields then move device to device with a strided
+ * copy kernel, never through the host (non-negative strides); 2-D fields are staged. */
 int mpas_upload(mpas_ctx* ctx, int field_id, const void* host, int64_t stride_entity, int64_t stride_level,
                 int64_t stride_comp);
 int mpas_download(mpas_ctx* ctx, int field_id, void* host, int64_t stride_entity, int64_t stride_level,

@@ -506,3 +506,33 @@ hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t see
 }
 
 }  // namespace mpas
+
+namespace mpas {
+// ---------------------------------------------------------------- device-resident views
+// mpas_upload / mpas_download of a 3-D field from / to a strided view in device memory
+// (a Legion instance in framebuffer memory, a torch tensor): element (entity e, level k,
+// component i) at byte offset e*se + k*sl + i*sc of the view, to / from the LP-padded
+// column layout; one thread per element, the levels of a column on consecutive threads.
+// Only levels 0..L of entities 0..n-1 move (padding and the zero slot keep their zeros).
+template <class T>
+__global__ __launch_bounds__(256) void k_view_copy(T* dev, char* view, int n, int W, int L, int LP, int64_t se,
+                                                  int64_t sl, int64_t sc, int to_dev) {
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t per = (size_t)W * (L + 1);
+    if (t >= (size_t)n * per) return;
+    const int e = (int)(t / per), r = (int)(t % per), i = r / (L + 1), k = r % (L + 1);
+    T* d = dev + ((size_t)e * W + i) * LP + lpos(LP, k);
+    T* v = (T*)(view + (int64_t)e * se + (int64_t)k * sl + (int64_t)i * sc);
+    if (to_dev) *d = *v;
+    else *v = *d;
+}
+hipError_t launch_view_copy(void* dev, void* view, int elem, int n, int W, int L, int LP, int64_t se, int64_t sl,
+                            int64_t sc, int to_dev, hipStream_t st) {
+    const size_t total = (size_t)n * W * (L + 1);
+    if (!total) return hipSuccess;
+    const int nb = (int)((total + 255) / 256);
+    if (elem == 8) k_view_copy<double><<<nb, 256, 0, st>>>((double*)dev, (char*)view, n, W, L, LP, se, sl, sc, to_dev);
+    else k_view_copy<uint8_t><<<nb, 256, 0, st>>>((uint8_t*)dev, (char*)view, n, W, L, LP, se, sl, sc, to_dev);
+    return hipGetLastError();
+}
+}  // namespace mpas

@@ -152,6 +152,24 @@ int id_target(int f) {
     }
 }
 
+// true when p is device memory (a device-resident view: Legion framebuffer instance,
+// torch tensor); host, pinned-host and unregistered pointers are host views
+bool is_device_ptr(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // unregistered host memory reports an error: clear it
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+// bytes a strided view of n entities x W components x levels 0..Lv spans (non-negative strides)
+size_t view_span(int n, int W, int Lv, int64_t se, int64_t sl, int64_t sc, size_t elem) {
+    if (n <= 0) return 0;
+    if (se < 0 || sl < 0 || sc < 0) throw Fail{MPAS_EINVAL, "device views need non-negative strides"};
+    return (size_t)((int64_t)(n - 1) * se + (int64_t)Lv * sl + (int64_t)(W - 1) * sc) + elem;
+}
+bool is_3d(int kind) { return kind == K_C3 || kind == K_E3 || kind == K_V3 || kind == K_C3V || kind == K_C3B; }
+
 // width of the id rows a count field gives the length of (0: not a count)
 int count_width(int f) {
     switch (f) {
@@ -745,6 +763,25 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
         const FieldInfo& fi = kFields[f];
         const int n = entity_count(c, fi.kind), L = c->S.L, LP = c->S.LP, W = fi.width;
         const char* h = (const char*)host;
+        std::vector<char> staged;  // a device view of a 2-D field / ZV: staged through the host
+        if (is_device_ptr(host)) {
+            if (is_3d(fi.kind)) {  // device to device, no host round trip
+                hipcheck(launch_view_copy(c->S.f[f], (void*)host, fi.kind == K_C3B ? 1 : 8, n, W, L, LP, se, sl, sc, 1,
+                                          c->stream),
+                         "upload view");
+                hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+                c->dirty = true;
+                c->trt_dirty = true;
+                graph_drop(c);
+                if (c->halo) c->halo->stale[f] = 0;
+                return;
+            }
+            const size_t span = fi.kind == K_ZV ? (size_t)(L * sl + 8)
+                                                : view_span(n, W, 0, se, 0, sc, elem_size(fi.kind));
+            staged.resize(span);
+            hipcheck(hipMemcpy(staged.data(), host, span, hipMemcpyDeviceToHost), "hipMemcpy D2H (view)");
+            h = staged.data();
+        }
         size_t bytes = dev_bytes(c, f);
         std::vector<char> buf(bytes, 0);
         if (fi.kind == K_C3 || fi.kind == K_E3 || fi.kind == K_V3) {
@@ -813,6 +850,23 @@ int mpas_download(mpas_ctx* c, int f, void* host, int64_t se, int64_t sl, int64_
         hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
         const FieldInfo& fi = kFields[f];
         const int n = entity_count(c, fi.kind), L = c->S.L, LP = c->S.LP, W = fi.width;
+        void* dview = nullptr;  // a device view of a 2-D field / ZV: staged through the host
+        std::vector<char> staged;
+        if (is_device_ptr(host)) {
+            if (is_3d(fi.kind)) {
+                hipcheck(launch_view_copy(c->S.f[f], host, fi.kind == K_C3B ? 1 : 8, n, W, L, LP, se, sl, sc, 0,
+                                          c->stream),
+                         "download view");
+                hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+                return;
+            }
+            const size_t span = fi.kind == K_ZV ? (size_t)(L * sl + 8)
+                                                : view_span(n, W, 0, se, 0, sc, elem_size(fi.kind));
+            staged.resize(span);
+            hipcheck(hipMemcpy(staged.data(), host, span, hipMemcpyDeviceToHost), "hipMemcpy D2H (view)");
+            dview = host;
+            host = staged.data();
+        }
         size_t bytes = dev_bytes(c, f);
         std::vector<char> buf(bytes);
         hipcheck(hipMemcpy(buf.data(), c->S.f[f], bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
@@ -843,6 +897,9 @@ int mpas_download(mpas_ctx* c, int f, void* host, int64_t se, int64_t sl, int64_
             for (int e = 0; e < n; e++)
                 for (int i = 0; i < W; i++) *(double*)(h + e * se + i * sc) = d[(size_t)e * W + i];
         }
+        if (dview)  // the staged image back into the device view (the bytes between its
+                    // elements came from it, so they are unchanged)
+            hipcheck(hipMemcpy(dview, staged.data(), staged.size(), hipMemcpyHostToDevice), "hipMemcpy H2D (view)");
     });
 }
 

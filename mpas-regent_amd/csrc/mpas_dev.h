@@ -177,6 +177,9 @@ hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
 hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt);
 hipError_t launch_damping_coefs(const DevState& S, hipStream_t st, double zd, double xnutr);
 hipError_t launch_compute_signs(const DevState& S, hipStream_t st);
+// strided device view <-> LP-padded 3-D field (elem 8: fp64, 1: uint8 masks)
+hipError_t launch_view_copy(void* dev, void* view, int elem, int n, int W, int L, int LP, int64_t se, int64_t sl,
+                            int64_t sc, int to_dev, hipStream_t st);
 hipError_t launch_adv_coef_compression(const DevState& S, hipStream_t st);
 hipError_t launch_couple_coef_3rd_order(const DevState& S, hipStream_t st, double coef);
 hipError_t launch_mesh_scaling(const DevState& S, hipStream_t st, int config_h_ScaleWithMesh);
