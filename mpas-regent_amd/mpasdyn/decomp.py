@@ -38,6 +38,12 @@ ID_ARRAYS = {"edgesOnCell": "edge", "edgesOnEdge": "edge", "edgesOnEdge_ECP": "e
              "cellsOnCell": "cell", "cellsOnVertex": "cell"}
 
 
+# index arrays only the one-time mesh tasks of atm_core_init follow (k_mesh.hip: owned
+# entities, no halo exchange beside them): part of the ghost closure, not of the
+# interior / boundary split
+INIT_ONLY = {"cellsOnCell", "cellsOnVertex"}
+
+
 # list lengths of the variable-length index arrays: entries past them are padding the
 # kernels may load (unconditionally, ahead of the accumulation) but never use
 COUNTS = {"edgesOnCell": "nEdgesOnCell", "verticesOnCell": "nEdgesOnCell", "edgesOnEdge": "nEdgesOnEdge",
@@ -109,6 +115,8 @@ class Decomposition:
                 isown[k] = m
             bnd = {k: np.zeros(len(own[k]), dtype=bool) for k in KINDS}
             for f, t in ID_ARRAYS.items():
+                if f in INIT_ONLY:  # read by the one-time mesh tasks only, never overlapped
+                    continue
                 src = BY_NAME[f].entity
                 use = active_mask(st, f, own[src])
                 bnd[src] |= (~isown[t][self.ids[f][own[src]]] & use).any(axis=1)
