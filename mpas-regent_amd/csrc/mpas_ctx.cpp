@@ -101,6 +101,8 @@ struct mpas_ctx {
     // Off by default: measured 2x slower than the three kernels
     int trtile = 0;
     int trt_cells = TRT_CELLS, trt_clo = 96;  // options "trtcells", "trtclo": tile size limits (speed only)
+    int trt_ghosts = 0;  // option "trtile_ghosts": a decomposed mesh's ghosts close over
+                         // advCellsForEdge(edgesOnCell) (decomp.Decomposition(tiled_transport))
     bool trt_dirty = true;
     TrTiles trt;
 };
@@ -328,6 +330,7 @@ void trt_build(mpas_ctx* c) {
     trt_free(c);
     c->trt_dirty = false;
     if (!c->trtile) return;
+    if (c->halo && !c->trt_ghosts) return;  // the tiles would read ghosts the local mesh lacks
     hipcheck(hipSetDevice(c->device), "hipSetDevice");
     const DevState& S = c->S;
     const int nC = S.nCells, nE = S.nEdges, nCO = S.nCO;
@@ -696,6 +699,9 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "trtile") == 0) {
             c->trtile = value ? 1 : 0;
             c->trt_dirty = true;
+        } else if (name && std::strcmp(name, "trtile_ghosts") == 0) {
+            c->trt_ghosts = value ? 1 : 0;
+            c->trt_dirty = true;
         } else if (name && std::strcmp(name, "trtcells") == 0) {
             if (value < 1 || value > 256) throw Fail{MPAS_EINVAL, "trtcells must be 1..256"};
             c->trt_cells = (int)value;
@@ -729,6 +735,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
         else if (name && std::strcmp(name, "trtcells") == 0) *value = c->trt_cells;
+        else if (name && std::strcmp(name, "trtile_ghosts") == 0) *value = c->trt_ghosts;
         else if (name && std::strcmp(name, "trtclo") == 0) *value = c->trt_clo;
         else if (name && std::strcmp(name, "trtile_active") == 0) {  // tiles built for this mesh
             trt_ensure(c);

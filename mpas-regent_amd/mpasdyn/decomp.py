@@ -13,7 +13,7 @@ the connectivity).  Here each rank owns
 and holds as ghosts every entity its owned entities reach through an index array of
 the path.  The closure is taken over exactly the index arrays the kernels follow
 (ID_ARRAYS, plus cellsOnEdge(edgesOnCell), which k_prepare composes for the cell
-kernels, and advCellsForEdge(edgesOnCell), which the tiled transport follows), so one hop from an owned entity never leaves the local set.  Every kernel
+kernels, and -- with tiled_transport -- advCellsForEdge(edgesOnCell)), so one hop from an owned entity never leaves the local set.  Every kernel
 computes owned entities only; a field a kernel gathers is made fresh on the ghosts by
 the device-side halo exchange right before it (csrc/mpas_halo.h; lazily, only after
 some kernel wrote it).  This keeps the ref-mode ids (raw 1-based offsets, which
@@ -72,8 +72,13 @@ def _blocks(n, nparts):
 class Decomposition:
     """Partition of a global HostState into `nparts` local subdomains."""
 
-    def __init__(self, st, nparts, cell_part=None):
+    def __init__(self, st, nparts, cell_part=None, tiled_transport=False):
+        """tiled_transport: also close the ghosts over advCellsForEdge(edgesOnCell), which
+        the opt-in tiled transport (option trtile) follows -- the second cell ring across
+        the boundary (x1.163842 / 8: 11 % instead of 5 % ghost cells, every exchange of a
+        cell field moving that many more columns), so it is off unless asked for"""
         self.st, self.nparts = st, int(nparts)
+        self.tiled_transport = bool(tiled_transport)
         self.n = {"cell": st.nCells, "edge": st.nEdges, "vertex": st.nVertices}
         nC, nE, nV = st.nCells, st.nEdges, st.nVertices
         cpart = _blocks(nC, nparts) if cell_part is None else np.asarray(cell_part, dtype=np.int32)
@@ -101,8 +106,9 @@ class Decomposition:
                 src = BY_NAME[f].entity
                 need[t].append(self.ids[f][own[src]].ravel())
             need["cell"].append(self.cell_cells[own["cell"]].ravel())
-            ca, cm = self.cell_adv(own["cell"])
-            need["cell"].append(ca[cm])
+            if self.tiled_transport:
+                ca, cm = self.cell_adv(own["cell"])
+                need["cell"].append(ca[cm])
             # interior first: an owned entity is interior when every id its index arrays
             # (and k_prepare's composed cell ids) reach in their used entries is owned or
             # the zero slot -- its kernels use no ghost value, so they run while a halo
@@ -241,7 +247,8 @@ class Decomposition:
                 tg = tg[tg < self.n[t]]
                 bad += int(np.sum(self.g2l[r][t][tg] >= len(self.local[r][t])))
             ca, cm = self.cell_adv(own["cell"])
-            for tg in (self.cell_cells[own["cell"]].ravel(), ca[cm]):
+            extra = (ca[cm],) if self.tiled_transport else ()
+            for tg in (self.cell_cells[own["cell"]].ravel(),) + extra:
                 tg = tg[tg < self.n["cell"]]
                 bad += int(np.sum(self.g2l[r]["cell"][tg] >= len(self.local[r]["cell"])))
         return bad

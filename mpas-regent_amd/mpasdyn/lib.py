@@ -219,6 +219,8 @@ def setup_subdomain(ctx, dec, r):
     L = ctx.lib
     ctx._check(L.mpas_halo_owned(ctx.h, *dec.n_owned(r)), "mpas_halo_owned")
     ctx._check(L.mpas_halo_interior(ctx.h, *dec.n_interior(r)), "mpas_halo_interior")
+    # whether the ghosts close over advCellsForEdge(edgesOnCell): the tiled transport needs it
+    ctx.set_option("trtile_ghosts", int(getattr(dec, "tiled_transport", False)))
     for kind, g in dec.global_ids(r).items():
         g = np.ascontiguousarray(g, dtype=np.int32)
         ctx._check(L.mpas_set_global_ids(ctx.h, KIND_ID[kind], g.ctypes.data, len(g)), "mpas_set_global_ids")

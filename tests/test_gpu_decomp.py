@@ -40,8 +40,8 @@ def run_single(st, fn, exact):
     return got
 
 
-def run_decomposed(st, nparts, fn, exact, cell_part=None, overlap=1):
-    d = decomp.Decomposition(st, nparts, cell_part=cell_part)
+def run_decomposed(st, nparts, fn, exact, cell_part=None, overlap=1, tiled_transport=False):
+    d = decomp.Decomposition(st, nparts, cell_part=cell_part, tiled_transport=tiled_transport)
     locs = [d.local_state(r) for r in range(nparts)]
     ctxs = [lib.Context(*d.n_local(r), st.L) for r in range(nparts)]
     try:

@@ -189,3 +189,27 @@ def test_decomposed_equals_single(x1_2562, nparts):
         got, stats = run_decomposed(st, nparts, fn, exact)
         bad = compare_states(got, ref, rtol=0.0)
         assert not bad, f"exact={exact}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("L", [1, 2, 63])
+@pytest.mark.parametrize("physics", [1, 2])
+def test_srk3_level_extremes(x1_2562, L, physics):
+    """the MPAS forms (physics 1: the vertical solver, 2: also the dynamics) with the
+    transport at nVertLevels 1, 2 (degenerate vertical stencils and tridiagonal systems)
+    and 63 (LP = 64, level L in the last lane): a whole RK3 step against the oracle, exact
+    (pow fields RTOL_POW) and fast (RTOL_STEP)"""
+    st = state(x1_2562, L, "mpas0")
+    ref = run_oracle(st, lambda o: o.mpas_srk3(720.0, 1, transport=True, physics=physics))
+    for exact, tol, tf in ((1, RTOL_POW, POW_FIELDS), (0, RTOL_STEP, None)):
+        got = st.copy()
+        with lib.Context(*st.dims()) as ctx:
+            ctx.set_option("exact", exact)
+            ctx.set_option("physics", physics)
+            ctx.set_option("transport", 1)
+            ctx.upload(st)
+            T.atm_srk3(ctx, 720.0, 1)
+            ctx.sync()
+            ctx.download(got)
+        got["rho_zz"][st.nCells] = ref["rho_zz"][st.nCells]  # recover's "garbage cell" (zero slot)
+        bad = compare_states(got, ref, rtol=tol, tol_fields=tf)
+        assert not bad, f"L={L} physics={physics} exact={exact}: {bad[:6]}"

@@ -130,9 +130,13 @@ def test_transport_decomposed_equals_single(x1_2562, nparts, overlap, trtile):
     interior launch takes only the cells reading owned columns)"""
     from test_gpu_decomp import run_decomposed, run_single
     st, _ = transport_state(x1_2562, 56, DT)
-    fn = _with({"physics": 1, "trtile": trtile}, lambda c: T.atm_advance_scalars_mono(c, DT))
+    def step(c):
+        if c.get_option("trtile_ghosts"):  # a decomposed context: the tiles must be in use
+            assert c.get_option("trtile_active") == trtile
+        T.atm_advance_scalars_mono(c, DT)
+    fn = _with({"physics": 1, "trtile": trtile}, step)
     ref = run_single(st, fn, 1)
-    got, stats = run_decomposed(st, nparts, fn, 1, overlap=overlap)
+    got, stats = run_decomposed(st, nparts, fn, 1, overlap=overlap, tiled_transport=bool(trtile))
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
     assert all(s[0] > 0 for s in stats)
