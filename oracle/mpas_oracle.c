@@ -644,8 +644,8 @@ static void dyn_tend_impl(ora_state* S, int rk_step, double dt, int horiz_mixing
     for (long c = 0; c < nC; c++) {
         for (int k = 0; k < L; k++) { /* :1277-1287 */
             CW(wdwz, c, k) = 0.0;
-            if (k == 1 || k == L - 1)
-                CW(wdwz, c, k) = 0.25 * (CW(rw, c, k) + CW(rw, c, k - 1)) * (CW(wr, c, k) + CW(wr, c, k - 1));
+            if (k == 1 || k == L - 1)  /* (nVertLevels = 1: level -1 reads 0, the level policy) */
+                CW(wdwz, c, k) = 0.25 * (CW(rw, c, k) + rc(S, rw, c, k - 1)) * (CW(wr, c, k) + rc(S, wr, c, k - 1));
             if (k > 1 && k < L - 1)
                 CW(wdwz, c, k) = flux3(CW(wr, c, k - 2), CW(wr, c, k - 1), CW(wr, c, k), rc(S, wr, c, k + 1),
                                        0.5 * (CW(rw, c, k) + CW(rw, c, k - 1)), 1.0);
@@ -757,8 +757,8 @@ static void dyn_tend_impl(ora_state* S, int rk_step, double dt, int horiz_mixing
                     CW(wdtz, c, k) = flux3(CW(theta_m, c, k - 2), CW(theta_m, c, k - 1), CW(theta_m, c, k),
                                            CW(theta_m, c, k + 1), CW(rw, c, k), 0.25) +
                                      (CW(rw_save, c, k) - CW(rw, c, k)) * (fzm[k] * CW(tms, c, k) + fzp[k] * CW(tms, c, k - 1));
-                if (k == L - 1)
-                    CW(wdtz, c, k) = CW(rw_save, c, k) * (fzm[k] * CW(theta_m, c, k) + fzp[k] * CW(theta_m, c, k - 1));
+                if (k == L - 1)  /* (nVertLevels = 1: level k - 1 = -1 reads 0, the level policy) */
+                    CW(wdtz, c, k) = CW(rw_save, c, k) * (fzm[k] * CW(theta_m, c, k) + fzp[k] * rc(S, theta_m, c, k - 1));
                 continue;
             }
             if (k > 0 && k < L - 1)
