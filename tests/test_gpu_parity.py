@@ -100,7 +100,7 @@ def run_oracle(st, fn):
     return ref
 
 
-@pytest.mark.parametrize("L", [5, 56])
+@pytest.mark.parametrize("L", [1, 2, 5, 56, 63])
 @pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
 @pytest.mark.parametrize("task", TASKS, ids=[t[0] for t in TASKS])
 def test_task_exact(x1_2562, L, variant, task):
