@@ -236,6 +236,11 @@ int mpas_halo_owned(mpas_ctx* ctx, int32_t nCellsOwned, int32_t nEdgesOwned, int
  * then computes them while the exchange runs on the context's halo stream, and the
  * remaining (boundary) owned entities after it (SURVEY §8.6 overlap; option "overlap") */
 int mpas_halo_interior(mpas_ctx* ctx, int32_t nCellsInterior, int32_t nEdgesInterior, int32_t nVerticesInterior);
+/* local edges [0, nEdgesRing1) are the owned edges and then the ghost edges of owned cells
+ * (mpasdyn/decomp.py numbers those first among the ghosts): in the reference semantics
+ * atm_divergence_damping_3d also updates them (option "ring1", default 1), so the acoustic
+ * step's ru_p gathers need no halo exchange.  Every rank must make the same call. */
+int mpas_halo_edge_ring(mpas_ctx* ctx, int32_t nEdgesRing1);
 /* kind 0 cells, 1 edges, 2 vertices: columns this rank sends to / receives from `peer`,
  * as local ids, in the order the peer receives / sends them */
 int mpas_halo_plan(mpas_ctx* ctx, int kind, int peer, const int32_t* send_ids, int32_t nsend,

@@ -338,7 +338,7 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
 #undef MPAS_ACOUSTIC_M
 #undef MPAS_ACOUSTIC
     };
-    HALO_RUN(S, st, run, F_ru_p, F_theta_m);
+    HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m);  // (ru_p at the edges of owned cells only)
     HALO_WROTE(S, F_rtheta_pp_old, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
     return hipGetLastError();
 }

@@ -813,7 +813,10 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         }
     };
     // halo: fields each kernel gathers through an index array / fields it writes
-    HALO_RUN(S, st, kA, F_ru, F_u, F_v);
+    // (u and v only for the Smagorinsky deformation of rk_step 0: a gather declared but not
+    // made would cost an exchange whenever v is stale)
+    if (rk0 && a.horiz_mixing == 0) HALO_RUN(S, st, kA, F_ru, F_u, F_v);
+    else HALO_RUN(S, st, kA, F_ru);
     HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz);
     if (!MD) HALO_WROTE(S, X_wc);
     if (rk0) {

@@ -328,6 +328,22 @@ static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts, int 
         else MPAS_DIVDAMP(1);
 #undef MPAS_DIVDAMP
     };
+    // ring-1 redundancy (reference semantics, where only this task writes ru_p): the launch
+    // that may read ghosts (all owned edges, or the boundary ones) also updates the ghost
+    // edges of owned cells from the freshly exchanged cell values, exactly as their owners
+    // do, so the acoustic step's gathers of ru_p need no exchange (7 per RK3 step fewer)
+    const bool r1 = S.halo && S.ring1 && S.nERing >= S.nEO && S.physics == 0;
+    auto run1 = [&](const DevState& X) {
+        DevState Y = X;
+        if (X.nEO == S.nEO) Y.nEO = S.nERing;
+        run(Y);
+    };
+    if (r1) {
+        if (old_zero) HALO_RUN(S, st, run1, F_rtheta_pp, F_theta_m);
+        else HALO_RUN(S, st, run1, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
+        S.halo->wrote_ring1({F_ru_p});
+        return hipGetLastError();
+    }
     if (old_zero) HALO_RUN(S, st, run, F_rtheta_pp, F_theta_m);
     else HALO_RUN(S, st, run, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
     HALO_WROTE(S, F_ru_p);
@@ -380,8 +396,13 @@ hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep,
     double inv = 1.0 / (double)split;
     k_finish_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S, substep, split, inv);
     k_finish_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S, substep, split, inv);
-    HALO_WROTE(S, F_ru_save, F_u, F_ruAvg, F_ruAvg_split, F_wwAvg, F_wwAvg_split, F_rho_zz, F_rw_save,
-               F_rtheta_p_save, F_rho_p_save, F_w, F_theta_m);
+    // what the kernels write for these arguments (a field declared written but untouched
+    // would cost every later gather of it a halo exchange): with substep = split = 1, as
+    // atm_srk3 calls it, only the averages and (physics != 2) rho_zz
+    if (substep < split)
+        HALO_WROTE(S, F_ru_save, F_u, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w, F_theta_m, F_rho_zz);
+    HALO_WROTE(S, F_ruAvg, F_ruAvg_split, F_wwAvg, F_wwAvg_split);
+    if (substep == split && S.physics != 2) HALO_WROTE(S, F_rho_zz);
     return hipGetLastError();
 }
 

@@ -610,6 +610,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.epw = 2;  // tools/kbench.py: div_damp -3 %, solve_diagnostics -4 % vs 1
         c->S.vcmix = 1;
         c->S.physics = 0;
+        c->S.ring1 = 1;
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         // Field f starts (f % 16) * stagger bytes into its allocation (env MPAS_ALLOC_STAGGER,
@@ -696,6 +697,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             if (!value) c->transport = 0;
         } else if (name && std::strcmp(name, "trorder") == 0) {
             c->S.tro = value ? 1 : 0;
+        } else if (name && std::strcmp(name, "ring1") == 0) {
+            c->S.ring1 = value ? 1 : 0;
         } else if (name && std::strcmp(name, "trtile") == 0) {
             c->trtile = value ? 1 : 0;
             c->trt_dirty = true;
@@ -734,6 +737,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "transport") == 0) *value = c->transport;
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
+        else if (name && std::strcmp(name, "ring1") == 0) *value = c->S.ring1;
         else if (name && std::strcmp(name, "trtcells") == 0) *value = c->trt_cells;
         else if (name && std::strcmp(name, "trtile_ghosts") == 0) *value = c->trt_ghosts;
         else if (name && std::strcmp(name, "trtclo") == 0) *value = c->trt_clo;
@@ -949,6 +953,15 @@ int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32
         c->S.nVO = nVerticesOwned;
         c->dirty = true;
         c->trt_dirty = true;
+    });
+}
+
+int mpas_halo_edge_ring(mpas_ctx* c, int32_t nEdgesRing1) {
+    return guarded(c, [&] {
+        graph_drop(c);
+        if (nEdgesRing1 < c->S.nEO || nEdgesRing1 > c->S.nEdges)
+            throw Fail{MPAS_EINVAL, "mpas_halo_edge_ring: needs owned edges <= count <= local edges"};
+        c->S.nERing = nEdgesRing1;
     });
 }
 

@@ -96,6 +96,10 @@ struct DevState {
     int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
     int vcmix;  // 1: the vertex and cell blocks of mixed grids interleaved in proportion (vc_block)
     int tro;      // transport slot order (k_transport.hip tr_slot): 0 entity-major, 1 pair-major
+    int nERing;   // decomposed mesh: local edges [0, nERing) are owned or ring-1 ghosts (edges of
+                  // owned cells, numbered first among the ghost edges); 0 = not set
+    int ring1;    // option "ring1": div_damping also computes the ring-1 ghost edges (reference
+                  // semantics), so ru_p needs no exchange before the acoustic step (speed only)
     int physics;  // option "physics": 0 the reference's semantics; 1 the MPAS vertical solver
                   // (Q16-Q21, Q24, Q5, Q7); 2 also the MPAS dynamics (dyn_tend, solve_diagnostics,
                   // set_smlstep, setup, moist, finish in MPAS-A's forms: mpas_oracle.c ora_mpas_*)

@@ -50,7 +50,10 @@ struct RcclComm;   // RCCL transport
 struct Halo {
     int nranks = 1, rank = 0;
     std::vector<HaloPeer> peers[3];
-    std::vector<uint8_t> stale;  // per field id
+    // per field id: 0 fresh on every ghost, 1 stale, 2 fresh on the ring-1 ghost edges only
+    // (the ghost edges of owned cells, local edges [nEO, nERing): written there by a launcher
+    // that computes them too, wrote_ring1)
+    std::vector<uint8_t> stale;
     // per-peer packed buffers: [cell fields][edge fields][vertex fields] columns of LP doubles
     double* sendbuf = nullptr;
     double* recvbuf = nullptr;
@@ -73,12 +76,17 @@ struct Halo {
     // make every field in `gathers` that is stale fresh on the ghosts
     hipError_t before(const DevState& S, hipStream_t st, std::initializer_list<int> gathers);
     void wrote(std::initializer_list<int> fields);
+    // the fields were written on the owned entities and, identically to their owners, on the
+    // ring-1 ghost edges: those stay fresh if they were (0 or 2 -> 2), else stale
+    void wrote_ring1(std::initializer_list<int> fields);
     hipError_t exchange(const DevState& S, hipStream_t st, const std::vector<int>& fields);
     // launch `fn` (a kernel launch over the entities of the DevState it is given) with the
     // stale fields of `gathers` exchanged first: interior / exchange / boundary when the
     // overlap is on, else exchange then one launch over every owned entity
+    // `ring1`: fields of `gathers` the kernel reads on ring-1 ghost edges only (edges of
+    // owned cells), for which stale state 2 counts as fresh
     hipError_t launch(const DevState& S, hipStream_t st, std::initializer_list<int> gathers,
-                      const std::function<void(const DevState&)>& fn);
+                      const std::function<void(const DevState&)>& fn, std::initializer_list<int> ring1 = {});
 };
 
 // launchers: without a decomposition HALO_RUN is one call of FN over the owned entities
@@ -94,6 +102,16 @@ struct Halo {
 #define HALO_WROTE(S, ...)                          \
     do {                                            \
         if ((S).halo) (S).halo->wrote({__VA_ARGS__}); \
+    } while (0)
+// HALO_RUN whose gathers of field R1 touch ring-1 ghost edges only (edges of owned cells)
+#define HALO_RUN_R1(S, st, FN, R1, ...)                                                    \
+    do {                                                                                   \
+        if ((S).halo) {                                                                    \
+            hipError_t he_ = (S).halo->launch((S), (st), {__VA_ARGS__}, (FN), {R1});        \
+            if (he_ != hipSuccess) return he_;                                             \
+        } else {                                                                           \
+            (FN)(S);                                                                       \
+        }                                                                                  \
     } while (0)
 
 // loopback group (one per process, N shards)

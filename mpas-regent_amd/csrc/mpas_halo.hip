@@ -2,6 +2,9 @@
 // bookkeeping, RCCL and loopback transports.
 #include "mpas_halo.h"
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <dlfcn.h>
 
 #include <chrono>
@@ -89,6 +92,14 @@ hipError_t Halo::reserve(int LP) {
     return hipSuccess;
 }
 
+void Halo::wrote_ring1(std::initializer_list<int> fields) {
+    std::vector<uint8_t> was;
+    for (int f : fields) was.push_back(stale[f]);
+    wrote(fields);  // (the overlap race check)
+    size_t i = 0;
+    for (int f : fields) stale[f] = was[i++] == 1 ? 1 : 2;
+}
+
 void Halo::wrote(std::initializer_list<int> fields) {
     // Overlap safety: the interior launch of the kernel that just ran executed beside the
     // pack of `overlapped`.  If that kernel writes one of those fields, the pack may read
@@ -117,10 +128,13 @@ hipError_t Halo::before(const DevState& S, hipStream_t st, std::initializer_list
 }
 
 hipError_t Halo::launch(const DevState& S, hipStream_t st, std::initializer_list<int> gathers,
-                        const std::function<void(const DevState&)>& fn) {
+                        const std::function<void(const DevState&)>& fn, std::initializer_list<int> ring1) {
     std::vector<int> need;
-    for (int f : gathers)
-        if (stale[f]) need.push_back(f);
+    for (int f : gathers) {
+        bool r1 = false;
+        for (int g : ring1) r1 = r1 || g == f;
+        if (stale[f] == 1 || (stale[f] == 2 && !r1)) need.push_back(f);
+    }
     hipError_t e;
     overlapped.clear();
     if (need.empty()) {
@@ -361,6 +375,15 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
     }
     exchanges++;
     fields_moved += (int64_t)fields.size();
+    static const bool log = [] {  // MPAS_HALO_LOG=1: one stderr line per exchange (rank 0)
+        const char* v = std::getenv("MPAS_HALO_LOG");
+        return v && *v && *v != '0';
+    }();
+    if (log && rank == 0) {
+        std::string names;
+        for (int f : fields) names += std::string(" ") + kFields[f].name;
+        fprintf(stderr, "halo exchange %lld:%s\n", (long long)exchanges, names.c_str());
+    }
     hipError_t e;
     if (loop) {
         // reuse of our send buffer: every peer's copies of the previous exchange are done

@@ -20,10 +20,11 @@ some kernel wrote it).  This keeps the ref-mode ids (raw 1-based offsets, which
 scramble neighbourhoods) exact: no geometric ring assumption anywhere.
 
 Local numbering: owned entities first -- the interior ones (reaching no ghost through any
-index array) before the boundary ones, each in global order -- then ghosts (global
-order), then the zero slot at index n_local.  Index arrays are mapped to local ids; ids that
-resolve to the global zero slot, or to an entity outside the local set (only ghost
-entities' own connectivity can), map to the local zero slot.
+index array) before the boundary ones, each in global order -- then ghosts (global order;
+for edges the ghost edges of owned cells first), then the zero slot at index n_local.
+Index arrays are mapped to local ids; ids that resolve to the global zero slot, or to an
+entity outside the local set (only ghost entities' own connectivity can), map to the local
+zero slot.
 """
 import numpy as np
 
@@ -98,7 +99,7 @@ class Decomposition:
         self._adv = np.vstack([self.ids["advCellsForEdge"], np.full((1, self.ids["advCellsForEdge"].shape[1]), nC)])
         self._nadv = np.concatenate([np.asarray(st["nAdvCellsForEdge"][:nE, 0], dtype=np.int64), [0]])
         self._nec = np.asarray(st["nEdgesOnCell"][:nC, 0], dtype=np.int64)
-        self.owned, self.local, self.g2l, self.n_int = [], [], [], []
+        self.owned, self.local, self.g2l, self.n_int, self.n_ring1 = [], [], [], [], []
         for r in range(self.nparts):
             own = {k: np.flatnonzero(self.part[k] == r) for k in KINDS}
             need = {k: [own[k]] for k in KINDS}
@@ -135,11 +136,19 @@ class Decomposition:
             for k in KINDS:
                 nint[k] = int(np.count_nonzero(~bnd[k]))
                 own[k] = np.concatenate([own[k][~bnd[k]], own[k][bnd[k]]])
+            # the ghost edges of owned cells (used entries of edgesOnCell) come first among
+            # the ghost edges: the launchers that also compute them (ring-1 redundancy,
+            # mpas_halo_edge_ring) take one contiguous range
+            e1 = self.ids["edgesOnCell"][own["cell"]][active_mask(st, "edgesOnCell", own["cell"])]
             loc, g2l = {}, {}
             for k in KINDS:
                 allk = np.unique(np.concatenate(need[k]))
                 allk = allk[allk < self.n[k]]  # the zero slot is not an entity
                 ghosts = np.setdiff1d(allk, own[k])
+                if k == "edge":
+                    first = np.isin(ghosts, e1)
+                    ghosts = np.concatenate([ghosts[first], ghosts[~first]])
+                    self.n_ring1.append(len(own[k]) + int(first.sum()))
                 loc[k] = np.concatenate([own[k], ghosts]).astype(np.int64)
                 m = np.full(self.n[k] + 1, len(loc[k]), dtype=np.int64)  # default: local zero slot
                 m[loc[k]] = np.arange(len(loc[k]))
@@ -162,6 +171,10 @@ class Decomposition:
     # ------------------------------------------------------------------ per rank
     def n_owned(self, r):
         return tuple(len(self.owned[r][k]) for k in KINDS)
+
+    def n_edge_ring1(self, r):
+        """owned edges plus the ghost edges of owned cells, numbered in that order"""
+        return self.n_ring1[r]
 
     def n_interior(self, r):
         """owned entities of rank r whose stencils reach no ghost (numbered first)"""
@@ -194,9 +207,9 @@ class Decomposition:
 
     def plan(self, r):
         """halo plan of rank r: {kind: [(peer, send_local_ids, recv_local_ids), ...]}.
-        recv ids are rank r's ghosts owned by `peer`; send ids are rank r's owned
-        entities that are ghosts of `peer`; both in global order, so the k-th sent
-        column is the k-th received one on the other side."""
+        recv ids are rank r's ghosts owned by `peer`, in r's ghost order; send ids are rank
+        r's owned entities that are ghosts of `peer`, in the peer's ghost order -- so the
+        k-th sent column is the k-th received one on the other side."""
         out = {}
         for k in KINDS:
             own_r = self.owned[r][k]
