@@ -236,11 +236,14 @@ int mpas_halo_owned(mpas_ctx* ctx, int32_t nCellsOwned, int32_t nEdgesOwned, int
  * then computes them while the exchange runs on the context's halo stream, and the
  * remaining (boundary) owned entities after it (SURVEY §8.6 overlap; option "overlap") */
 int mpas_halo_interior(mpas_ctx* ctx, int32_t nCellsInterior, int32_t nEdgesInterior, int32_t nVerticesInterior);
-/* local edges [0, nEdgesRing1) are the owned edges and then the ghost edges of owned cells
- * (mpasdyn/decomp.py numbers those first among the ghosts): in the reference semantics
- * atm_divergence_damping_3d also updates them (option "ring1", default 1), so the acoustic
- * step's ru_p gathers need no halo exchange.  Every rank must make the same call. */
-int mpas_halo_edge_ring(mpas_ctx* ctx, int32_t nEdgesRing1);
+/* ring-1 ghosts (mpasdyn/decomp.py numbers them first among the ghosts): local edges
+ * [0, nEdgesRing1) are the owned edges and the ghost edges of owned cells, local vertices
+ * [0, nVerticesRing1) the owned vertices and the ghost vertices of owned edges.  With
+ * option "ring1" (default 1) atm_divergence_damping_3d (reference semantics) also updates
+ * those edges and atm_compute_solve_diagnostics those vertices, from inputs fresh there,
+ * so the acoustic step's ru_p and the edge kernels' vorticity / pv_vertex gathers need no
+ * halo exchange.  Every rank must make the same call. */
+int mpas_halo_ring1(mpas_ctx* ctx, int32_t nEdgesRing1, int32_t nVerticesRing1);
 /* kind 0 cells, 1 edges, 2 vertices: columns this rank sends to / receives from `peer`,
  * as local ids, in the order the peer receives / sends them */
 int mpas_halo_plan(mpas_ctx* ctx, int kind, int peer, const int32_t* send_ids, int32_t nsend,

@@ -820,8 +820,8 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz);
     if (!MD) HALO_WROTE(S, X_wc);
     if (rk0) {
-        HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p, F_zz, F_dpdz,
-                 F_divergence, F_kdiff, F_vorticity);
+        HALO_RUN_R1(S, st, kB, F_vorticity, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p,
+                    F_zz, F_dpdz, F_divergence, F_kdiff, F_vorticity);  // (vorticity at vertices of owned edges)
         HALO_WROTE(S, X_F, F_tend_u, F_tend_u_euler, F_delsq_u);
         if (MD) HALO_WROTE(S, X_Fw);
         if (MD) HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, F_w, F_theta_m);

@@ -212,17 +212,32 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
         if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false, MD><<<nb, 256, 0, st>>>(X);
         else k_solve_e<LP, true, MD><<<nb, 256, 0, st>>>(X);
     };
-    HALO_RUN(S, st, kvc, F_u);
-    HALO_WROTE(S, F_vorticity, F_pv_vertex, F_ke_vertex, F_divergence, F_ke);
+    // ring-1 redundancy (option ring1): the launch that runs after u is fresh on the ghosts
+    // also computes the ghost vertices of owned edges (their edges are local, decomp.py),
+    // exactly as their owners do; the edge kernels gather vorticity / pv_vertex there only
+    const bool r1 = S.halo && S.ring1 && S.nVRing >= S.nVO;
+    auto kvc1 = [&](const DevState& X) {
+        DevState Y = X;
+        if (X.nVO == S.nVO) Y.nVO = S.nVRing;
+        kvc(Y);
+    };
+    if (r1) {
+        HALO_RUN(S, st, kvc1, F_u);
+        S.halo->wrote_ring1({F_vorticity, F_pv_vertex});
+        HALO_WROTE(S, F_ke_vertex, F_divergence, F_ke);
+    } else {
+        HALO_RUN(S, st, kvc, F_u);
+        HALO_WROTE(S, F_vorticity, F_pv_vertex, F_ke_vertex, F_divergence, F_ke);
+    }
     if (hollingsworth) {
         HALO_RUN(S, st, kh, F_ke_vertex);
         HALO_WROTE(S, F_ke);
     }
     if (MD) {
-        HALO_RUN(S, st, ke, F_rho_zz, F_u, F_pv_vertex);
+        HALO_RUN_R1(S, st, ke, F_pv_vertex, F_rho_zz, F_u, F_pv_vertex);
         HALO_WROTE(S, F_h_edge, F_rho_edge, F_ke_edge, F_v, F_pv_edge);
     } else {
-        HALO_RUN(S, st, ke, F_h, F_u, F_pv_vertex);
+        HALO_RUN_R1(S, st, ke, F_pv_vertex, F_h, F_u, F_pv_vertex);
         HALO_WROTE(S, F_h_edge, F_ke_edge, F_v, F_pv_edge);
     }
     return hipGetLastError();

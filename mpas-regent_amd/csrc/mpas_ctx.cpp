@@ -956,12 +956,14 @@ int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32
     });
 }
 
-int mpas_halo_edge_ring(mpas_ctx* c, int32_t nEdgesRing1) {
+int mpas_halo_ring1(mpas_ctx* c, int32_t nEdgesRing1, int32_t nVerticesRing1) {
     return guarded(c, [&] {
         graph_drop(c);
-        if (nEdgesRing1 < c->S.nEO || nEdgesRing1 > c->S.nEdges)
-            throw Fail{MPAS_EINVAL, "mpas_halo_edge_ring: needs owned edges <= count <= local edges"};
+        if (nEdgesRing1 < c->S.nEO || nEdgesRing1 > c->S.nEdges || nVerticesRing1 < c->S.nVO ||
+            nVerticesRing1 > c->S.nVertices)
+            throw Fail{MPAS_EINVAL, "mpas_halo_ring1: needs owned <= count <= local, edges and vertices"};
         c->S.nERing = nEdgesRing1;
+        c->S.nVRing = nVerticesRing1;
     });
 }
 

@@ -98,8 +98,10 @@ struct DevState {
     int tro;      // transport slot order (k_transport.hip tr_slot): 0 entity-major, 1 pair-major
     int nERing;   // decomposed mesh: local edges [0, nERing) are owned or ring-1 ghosts (edges of
                   // owned cells, numbered first among the ghost edges); 0 = not set
-    int ring1;    // option "ring1": div_damping also computes the ring-1 ghost edges (reference
-                  // semantics), so ru_p needs no exchange before the acoustic step (speed only)
+    int nVRing;   // local vertices [0, nVRing) are owned or ring-1 ghosts (vertices of owned edges)
+    int ring1;    // option "ring1": the launchers that can also compute the ring-1 ghosts do
+                  // (div_damping: ru_p, reference semantics; solve_diagnostics: vorticity and
+                  // pv_vertex), so their gathers need no exchange (speed only, same bits)
     int physics;  // option "physics": 0 the reference's semantics; 1 the MPAS vertical solver
                   // (Q16-Q21, Q24, Q5, Q7); 2 also the MPAS dynamics (dyn_tend, solve_diagnostics,
                   // set_smlstep, setup, moist, finish in MPAS-A's forms: mpas_oracle.c ora_mpas_*)

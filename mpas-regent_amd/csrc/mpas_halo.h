@@ -50,9 +50,9 @@ struct RcclComm;   // RCCL transport
 struct Halo {
     int nranks = 1, rank = 0;
     std::vector<HaloPeer> peers[3];
-    // per field id: 0 fresh on every ghost, 1 stale, 2 fresh on the ring-1 ghost edges only
-    // (the ghost edges of owned cells, local edges [nEO, nERing): written there by a launcher
-    // that computes them too, wrote_ring1)
+    // per field id: 0 fresh on every ghost, 1 stale, 2 fresh on the ring-1 ghosts of its
+    // kind only (edges of owned cells [nEO, nERing), vertices of owned edges [nVO, nVRing)):
+    // written there by a launcher that computes them too, wrote_ring1
     std::vector<uint8_t> stale;
     // per-peer packed buffers: [cell fields][edge fields][vertex fields] columns of LP doubles
     double* sendbuf = nullptr;
@@ -103,7 +103,8 @@ struct Halo {
     do {                                            \
         if ((S).halo) (S).halo->wrote({__VA_ARGS__}); \
     } while (0)
-// HALO_RUN whose gathers of field R1 touch ring-1 ghost edges only (edges of owned cells)
+// HALO_RUN whose gathers of field R1 touch its ring-1 ghosts only (edges of owned cells,
+// vertices of owned edges)
 #define HALO_RUN_R1(S, st, FN, R1, ...)                                                    \
     do {                                                                                   \
         if ((S).halo) {                                                                    \

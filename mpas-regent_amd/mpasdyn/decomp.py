@@ -99,7 +99,7 @@ class Decomposition:
         self._adv = np.vstack([self.ids["advCellsForEdge"], np.full((1, self.ids["advCellsForEdge"].shape[1]), nC)])
         self._nadv = np.concatenate([np.asarray(st["nAdvCellsForEdge"][:nE, 0], dtype=np.int64), [0]])
         self._nec = np.asarray(st["nEdgesOnCell"][:nC, 0], dtype=np.int64)
-        self.owned, self.local, self.g2l, self.n_int, self.n_ring1 = [], [], [], [], []
+        self.owned, self.local, self.g2l, self.n_int, self.n_ring1_ = [], [], [], [], []
         for r in range(self.nparts):
             own = {k: np.flatnonzero(self.part[k] == r) for k in KINDS}
             need = {k: [own[k]] for k in KINDS}
@@ -107,6 +107,10 @@ class Decomposition:
                 src = BY_NAME[f].entity
                 need[t].append(self.ids[f][own[src]].ravel())
             need["cell"].append(self.cell_cells[own["cell"]].ravel())
+            # the edges of the vertices of owned edges: solve_diagnostics' ring-1 vertices
+            v1 = self.ids["verticesOnEdge"][own["edge"]].ravel()
+            v1 = v1[v1 < self.n["vertex"]]
+            need["edge"].append(self.ids["edgesOnVertex"][v1].ravel())
             if self.tiled_transport:
                 ca, cm = self.cell_adv(own["cell"])
                 need["cell"].append(ca[cm])
@@ -136,23 +140,26 @@ class Decomposition:
             for k in KINDS:
                 nint[k] = int(np.count_nonzero(~bnd[k]))
                 own[k] = np.concatenate([own[k][~bnd[k]], own[k][bnd[k]]])
-            # the ghost edges of owned cells (used entries of edgesOnCell) come first among
-            # the ghost edges: the launchers that also compute them (ring-1 redundancy,
-            # mpas_halo_edge_ring) take one contiguous range
-            e1 = self.ids["edgesOnCell"][own["cell"]][active_mask(st, "edgesOnCell", own["cell"])]
+            # ring-1 ghosts first among the ghosts: the edges of owned cells (used entries of
+            # edgesOnCell) and the vertices of owned edges -- the launchers that also compute
+            # them (mpas_halo_ring1) take one contiguous range
+            first_of = {"edge": self.ids["edgesOnCell"][own["cell"]][active_mask(st, "edgesOnCell", own["cell"])],
+                        "vertex": self.ids["verticesOnEdge"][own["edge"]].ravel()}
+            ring1 = {}
             loc, g2l = {}, {}
             for k in KINDS:
                 allk = np.unique(np.concatenate(need[k]))
                 allk = allk[allk < self.n[k]]  # the zero slot is not an entity
                 ghosts = np.setdiff1d(allk, own[k])
-                if k == "edge":
-                    first = np.isin(ghosts, e1)
+                if k in first_of:
+                    first = np.isin(ghosts, first_of[k])
                     ghosts = np.concatenate([ghosts[first], ghosts[~first]])
-                    self.n_ring1.append(len(own[k]) + int(first.sum()))
+                    ring1[k] = len(own[k]) + int(first.sum())
                 loc[k] = np.concatenate([own[k], ghosts]).astype(np.int64)
                 m = np.full(self.n[k] + 1, len(loc[k]), dtype=np.int64)  # default: local zero slot
                 m[loc[k]] = np.arange(len(loc[k]))
                 g2l[k] = m
+            self.n_ring1_.append((ring1["edge"], ring1["vertex"]))
             self.owned.append(own)
             self.local.append(loc)
             self.g2l.append(g2l)
@@ -172,9 +179,10 @@ class Decomposition:
     def n_owned(self, r):
         return tuple(len(self.owned[r][k]) for k in KINDS)
 
-    def n_edge_ring1(self, r):
-        """owned edges plus the ghost edges of owned cells, numbered in that order"""
-        return self.n_ring1[r]
+    def n_ring1(self, r):
+        """(owned edges + the ghost edges of owned cells, owned vertices + the ghost vertices
+        of owned edges): each numbered in that order"""
+        return self.n_ring1_[r]
 
     def n_interior(self, r):
         """owned entities of rank r whose stencils reach no ghost (numbered first)"""

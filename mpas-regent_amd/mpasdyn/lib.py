@@ -26,7 +26,7 @@ EXPORTS = [
     "mpas_atm_recover_large_step_variables_work", "mpas_reconstruct_2d", "mpas_summarize_timestep",
     "mpas_atm_compute_output_diagnostics", "mpas_atm_advance_scalars_mono",
     "mpas_atm_compute_damping_coefs", "mpas_atm_init_coupled_diagnostics", "mpas_atm_core_init",
-    "mpas_halo_edge_ring", "mpas_atm_compute_signs", "mpas_atm_adv_coef_compression", "mpas_atm_couple_coef_3rd_order",
+    "mpas_halo_ring1", "mpas_atm_compute_signs", "mpas_atm_adv_coef_compression", "mpas_atm_couple_coef_3rd_order",
     "mpas_atm_compute_mesh_scaling",
     "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
     "mpas_halo_owned", "mpas_halo_interior", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
@@ -92,7 +92,7 @@ def load():
         "mpas_atm_init_coupled_diagnostics": (i32, [vp]),
         "mpas_atm_core_init": (i32, [vp]),
         "mpas_atm_compute_signs": (i32, [vp]),
-        "mpas_halo_edge_ring": (i32, [vp, i32]),
+        "mpas_halo_ring1": (i32, [vp, i32, i32]),
         "mpas_atm_adv_coef_compression": (i32, [vp]),
         "mpas_atm_couple_coef_3rd_order": (i32, [vp, dbl]),
         "mpas_atm_compute_mesh_scaling": (i32, [vp, i32]),
@@ -220,7 +220,7 @@ def setup_subdomain(ctx, dec, r):
     L = ctx.lib
     ctx._check(L.mpas_halo_owned(ctx.h, *dec.n_owned(r)), "mpas_halo_owned")
     ctx._check(L.mpas_halo_interior(ctx.h, *dec.n_interior(r)), "mpas_halo_interior")
-    ctx._check(L.mpas_halo_edge_ring(ctx.h, dec.n_edge_ring1(r)), "mpas_halo_edge_ring")
+    ctx._check(L.mpas_halo_ring1(ctx.h, *dec.n_ring1(r)), "mpas_halo_ring1")
     # whether the ghosts close over advCellsForEdge(edgesOnCell): the tiled transport needs it
     ctx.set_option("trtile_ghosts", int(getattr(dec, "tiled_transport", False)))
     for kind, g in dec.global_ids(r).items():

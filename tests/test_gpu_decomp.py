@@ -190,10 +190,12 @@ def test_ragged_partition(x1_2562):
     assert not bad, bad[:6]
 
 
-def test_ring1_div_damping_saves_exchanges(x1_2562):
-    """option ring1 (default 1, reference semantics): atm_divergence_damping_3d also updates
-    the ghost edges of owned cells, so the acoustic step's ru_p gathers need no exchange --
-    one exchange fewer per acoustic substep after the first, the same bits as ring1 = 0"""
+def test_ring1_redundancy_saves_exchanges(x1_2562):
+    """option ring1 (default 1): atm_divergence_damping_3d (reference semantics) also updates
+    the ghost edges of owned cells and solve_diagnostics the ghost vertices of owned edges,
+    so the acoustic step's ru_p gathers and solve's pv_vertex gathers need no exchange -- one
+    exchange fewer per acoustic substep after the first and per solve_diagnostics, the same
+    bits as ring1 = 0"""
     st = state(x1_2562, 56, "random")
     out = {}
     for r1 in (1, 0):
@@ -205,4 +207,4 @@ def test_ring1_div_damping_saves_exchanges(x1_2562):
     bad = compare_states(out[1][0], out[0][0], rtol=0.0)
     assert not bad, bad[:6]
     for s1, s0 in zip(out[1][1], out[0][1]):  # (the first substep's ru_p is fresh from the upload)
-        assert s0[0] - s1[0] == 6, (s0, s1)
+        assert s0[0] - s1[0] == 6 + 3, (s0, s1)
