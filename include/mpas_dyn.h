@@ -32,6 +32,12 @@ extern "C" {
 #define MPAS_ERCCL (-3)
 #define MPAS_ENOMEM (-4)
 #define MPAS_ENOTSUP (-5)
+/* bounds-checked build only (libmpasdyn_bounds.so, `make -C mpas-regent_amd/csrc bounds`):
+ * a kernel of the call accessed a field outside its rows; the message names the field.
+ * Option "bounds" (read-only) is 1 in that build; "bounds_units" (read-only) packs the
+ * translation units whose kernels check (high 32 bits) and those registered (low);
+ * "bounds_probe" = n makes it read field u n columns past its end (the check's own test). */
+#define MPAS_EBOUNDS (-6)
 
 typedef struct mpas_ctx mpas_ctx;
 

@@ -556,4 +556,23 @@ hipError_t launch_view_copy(void* dev, void* view, int elem, int n, int W, int L
     else k_view_copy<uint8_t><<<nb, 256, 0, st>>>((uint8_t*)dev, (char*)view, n, W, L, LP, se, sl, sc, to_dev);
     return hipGetLastError();
 }
+#if MPAS_BOUNDS
+// bounds-checked build: read field u `col` columns past its last row (the zero slot) --
+// the check must report it (tests/test_gpu_bounds.py)
+template <int LP>
+__global__ __launch_bounds__(256) void k_bounds_probe(DevState S, int col) {
+    const int k = (int)(threadIdx.x % LP);
+    const double x = colk(fd(S, F_u), S.nEdges + col);
+    if (x == 12345.678) colk(fw(S, F_tend_u), 0) = x;  // (keeps the load)
+}
+template <int LP>
+static hipError_t bounds_probe_lp(const DevState& S, hipStream_t st, int col) {
+    k_bounds_probe<LP><<<1, LP, 0, st>>>(S, col);
+    return hipGetLastError();
+}
+hipError_t launch_bounds_probe(const DevState& S, hipStream_t st, int col) {
+    MPAS_LP_DISPATCH(S.LP, bounds_probe_lp, S, st, col);
+}
+#endif
+
 }  // namespace mpas

@@ -11,6 +11,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <map>
+#include <mutex>
 #include <new>
 #include <string>
 #include <vector>
@@ -52,6 +54,15 @@ const FieldInfo kFields[X_COUNT] = {
     {"Rm", K_C3V, 8, D_M, 0, 0},
     {"su", K_C3V, 8, D_M, 0, 0},
 };
+// translation units with kernels, registered at load time (mpas_dev.h, bounds-checked build)
+static std::vector<void* (*)()>& bounds_tus() {
+    static std::vector<void* (*)()> v;
+    return v;
+}
+int bounds_register_tu(void* (*symbol)()) {
+    bounds_tus().push_back(symbol);
+    return 0;
+}
 }  // namespace mpas
 
 using namespace mpas;
@@ -276,11 +287,113 @@ void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
     }
 }
 
+// ---- bounds-checked build (mpas_dev.h MPAS_BOUNDS): the field table the kernels check
+// against, and the check after every C-ABI call (which then synchronises the context)
+#if MPAS_BOUNDS
+struct BoundsReg {
+    std::mutex mu;
+    std::map<unsigned long long, std::pair<unsigned long long, std::string>> fields;  // lo -> (hi, name)
+    BoundsTab* dev = nullptr;
+};
+BoundsReg& bounds_reg() {
+    static BoundsReg r;
+    return r;
+}
+// upload the sorted field ranges (every live context) and point each unit's table at them
+void bounds_publish() {
+    BoundsReg& r = bounds_reg();
+    std::lock_guard<std::mutex> lk(r.mu);
+    if (r.fields.size() > (size_t)kBoundsMax) throw Fail{MPAS_ENOMEM, "bounds table full"};
+    hipcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    if (!r.dev) {
+        hipcheck(hipMalloc(&r.dev, sizeof(BoundsTab)), "hipMalloc");
+        hipcheck(hipMemset(r.dev, 0, sizeof(BoundsTab)), "hipMemset");
+        for (auto sym : bounds_tus()) {
+            void* p = sym();
+            if (!p) throw Fail{MPAS_EHIP, "bounds table symbol not found"};
+            hipcheck(hipMemcpy(p, &r.dev, sizeof(r.dev), hipMemcpyHostToDevice), "hipMemcpy bounds");
+        }
+    }
+    std::vector<unsigned long long> lo, hi;
+    for (auto& kv : r.fields) lo.push_back(kv.first), hi.push_back(kv.second.first);
+    const int n = (int)lo.size();
+    if (n) {
+        hipcheck(hipMemcpy(r.dev->lo, lo.data(), n * sizeof(lo[0]), hipMemcpyHostToDevice), "hipMemcpy bounds");
+        hipcheck(hipMemcpy(r.dev->hi, hi.data(), n * sizeof(hi[0]), hipMemcpyHostToDevice), "hipMemcpy bounds");
+    }
+    hipcheck(hipMemcpy(&r.dev->n, &n, sizeof(n), hipMemcpyHostToDevice), "hipMemcpy bounds");
+}
+void bounds_add(mpas_ctx* c) {
+    {
+        BoundsReg& r = bounds_reg();
+        std::lock_guard<std::mutex> lk(r.mu);
+        for (int f = 0; f < X_COUNT; f++) {
+            const unsigned long long lo = (unsigned long long)c->S.f[f];
+            r.fields[lo] = {lo + dev_bytes(c, f), kFields[f].name};
+        }
+    }
+    bounds_publish();
+}
+void bounds_remove(mpas_ctx* c) {
+    {
+        BoundsReg& r = bounds_reg();
+        std::lock_guard<std::mutex> lk(r.mu);
+        for (int f = 0; f < X_COUNT; f++)
+            if (c->S.f[f]) r.fields.erase((unsigned long long)c->S.f[f]);
+    }
+    try {
+        bounds_publish();
+    } catch (const Fail&) {
+    }
+}
+// translation units whose table pointer is set (read back from each unit's symbol)
+int bounds_units() {
+    BoundsReg& r = bounds_reg();
+    int n = 0;
+    for (auto sym : bounds_tus()) {
+        void* p = sym();
+        BoundsTab* t = nullptr;
+        if (p && hipMemcpy(&t, p, sizeof(t), hipMemcpyDeviceToHost) == hipSuccess && t && t == r.dev) n++;
+    }
+    return n;
+}
+void bounds_check(mpas_ctx* c) {
+    BoundsReg& r = bounds_reg();
+    if (!r.dev || !c->stream) return;
+    hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    unsigned int count = 0;
+    hipcheck(hipMemcpy(&count, &r.dev->count, sizeof(count), hipMemcpyDeviceToHost), "hipMemcpy bounds");
+    if (!count) return;
+    unsigned long long addr = 0, flo = 0, where = 0;
+    hipcheck(hipMemcpy(&addr, &r.dev->addr, sizeof(addr), hipMemcpyDeviceToHost), "hipMemcpy bounds");
+    hipcheck(hipMemcpy(&flo, &r.dev->field_lo, sizeof(flo), hipMemcpyDeviceToHost), "hipMemcpy bounds");
+    hipcheck(hipMemcpy(&where, &r.dev->where, sizeof(where), hipMemcpyDeviceToHost), "hipMemcpy bounds");
+    const unsigned int zero = 0;
+    hipcheck(hipMemcpy(&r.dev->count, &zero, sizeof(zero), hipMemcpyHostToDevice), "hipMemcpy bounds");
+    std::string name = "?";
+    unsigned long long fhi = 0;
+    {
+        std::lock_guard<std::mutex> lk(r.mu);
+        auto it = r.fields.find(flo);
+        if (it != r.fields.end()) name = it->second.second, fhi = it->second.first;
+    }
+    char msg[256];
+    snprintf(msg, sizeof msg, "%u access(es) outside their field; first: field %s, byte %lld of %llu (block %llu thread %llu)",
+             count, name.c_str(), (long long)(addr - flo), fhi - flo, where >> 32, where & 0xffffffffull);
+    throw Fail{MPAS_EBOUNDS, msg};
+}
+#else
+void bounds_add(mpas_ctx*) {}
+void bounds_remove(mpas_ctx*) {}
+void bounds_check(mpas_ctx*) {}
+#endif
+
 template <class Fn>
 int guarded(mpas_ctx* c, Fn&& fn) {
     if (!c) return MPAS_EINVAL;
     try {
         fn();
+        if (MPAS_BOUNDS) bounds_check(c);
         return MPAS_OK;
     } catch (const Fail& f) {
         c->err = f.msg;
@@ -629,6 +742,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
             c->S.f[f] = (char*)p + off;
         }
         hipcheck(hipDeviceSynchronize(), "hipDeviceSynchronize");
+        bounds_add(c);
     });
     if (rc != MPAS_OK) {
         g_create_err = c->err;
@@ -644,6 +758,7 @@ int mpas_ctx_destroy(mpas_ctx* c) {
     if (!c) return MPAS_EINVAL;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->raw[0]) bounds_remove(c);
     for (int f = 0; f < X_COUNT; f++)
         if (c->raw[f]) (void)hipFree(c->raw[f]);
     for (auto& t : c->pending) {
@@ -722,6 +837,13 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "self") == 0) {
             c->self_on = value ? 1 : 0;
             c->S.selfc = c->self_ok && c->self_on;
+        } else if (name && std::strcmp(name, "bounds_probe") == 0) {  // bounds-checked build only
+#if MPAS_BOUNDS
+            hipcheck(hipSetDevice(c->device), "hipSetDevice");
+            hipcheck(launch_bounds_probe(c->S, c->stream, (int)value), "bounds_probe");
+#else
+            throw Fail{MPAS_ENOTSUP, "bounds_probe needs the bounds-checked build (libmpasdyn_bounds.so)"};
+#endif
         } else throw Fail{MPAS_EINVAL, std::string("unknown option ") + (name ? name : "(null)")};
     });
 }
@@ -753,6 +875,12 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "graph") == 0) *value = c->graph_on;
         else if (name && std::strcmp(name, "graph_captures") == 0) *value = c->graph_captures;
         else if (name && std::strcmp(name, "graph_launches") == 0) *value = c->graph_launches;
+        else if (name && std::strcmp(name, "bounds") == 0) *value = MPAS_BOUNDS;  // the bounds-checked build
+#if MPAS_BOUNDS
+        else if (name && std::strcmp(name, "bounds_units") == 0) {  // kernel units checking / registered
+            *value = ((int64_t)bounds_units() << 32) | (int64_t)bounds_tus().size();
+        }
+#endif
         else if (name && std::strcmp(name, "selfc") == 0) {
             if (c->dirty) {  // decide now (needs the mesh uploaded)
                 hipcheck(hipSetDevice(c->device), "hipSetDevice");

@@ -191,6 +191,26 @@ hipError_t launch_couple_coef_3rd_order(const DevState& S, hipStream_t st, doubl
 hipError_t launch_mesh_scaling(const DevState& S, hipStream_t st, int config_h_ScaleWithMesh);
 hipError_t launch_init_coupled_diagnostics(const DevState& S, hipStream_t st);
 size_t summarize_scratch_bytes();
+
+// ---- bounds-checked build (MPAS_BOUNDS, below) ----
+#ifndef MPAS_BOUNDS
+#define MPAS_BOUNDS 0
+#endif
+constexpr int kBoundsMax = 4096;  // fields of all live contexts
+struct BoundsTab {
+    unsigned long long lo[kBoundsMax], hi[kBoundsMax];  // sorted field ranges [lo, hi)
+    int n;
+    unsigned int count;           // accesses outside their field since the last check
+    unsigned long long addr;      // the first one: its address,
+    unsigned long long field_lo;  // the start of the field it was checked against,
+    unsigned long long where;     // blockIdx << 32 | threadIdx
+};
+// host: every translation unit with kernels registers the address of its table pointer
+int bounds_register_tu(void* (*symbol)());
+#if MPAS_BOUNDS
+// reads `col` columns past the end of field u (tests: the check must catch it)
+hipError_t launch_bounds_probe(const DevState& S, hipStream_t st, int col);
+#endif
 hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, double* out);
 
 // ---- device helpers ----
@@ -328,6 +348,46 @@ __device__ __forceinline__ MPAS_GLOBAL T* sgpr_ptr(T* p) {
     return (MPAS_GLOBAL T*)(((uint64_t)hi << 32) | lo);
 }
 
+#if MPAS_BOUNDS
+// Bounds-checked build (-DMPAS_BOUNDS=1, `make -C csrc bounds` -> libmpasdyn_bounds.so,
+// selected with env MPAS_LIB).  Every column access (colk, gather2, gather2s,
+// col_rd) is checked against the field its base pointer starts, every mesh-row load
+// (row_ld) against the field it falls in, through a sorted table of the [begin, end) of
+// every field of every live context (mpas_ctx.cpp bounds_publish).  An access outside
+// reads / writes a sink instead and is recorded; the C-ABI call that ran the kernel then
+// fails with MPAS_EBOUNDS, naming the field.  Each translation unit has its own copy of
+// the table pointer, registered with the host at load time.
+static __device__ BoundsTab* g_bounds;
+static __device__ double g_bounds_sink[64];  // (covers the widest row_ld)
+static void* bounds_symbol_() {
+    void* p = nullptr;
+    return hipGetSymbolAddress(&p, HIP_SYMBOL(g_bounds)) == hipSuccess ? p : nullptr;
+}
+static const int g_bounds_registered_ = bounds_register_tu(&bounds_symbol_);
+__device__ __noinline__ static inline void* bounds_chk(const void* base, const void* p, unsigned bytes) {
+    BoundsTab* t = g_bounds;
+    if (!t) return (void*)p;
+    const unsigned long long b = (unsigned long long)base, a = (unsigned long long)p;
+    int lo = 0, hi = t->n - 1, hit = -1;
+    while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        if (t->lo[mid] <= b) hit = mid, lo = mid + 1;
+        else hi = mid - 1;
+    }
+    if (hit < 0 || b >= t->hi[hit]) return (void*)p;  // not inside a field: not checked
+    if (a >= t->lo[hit] && a + bytes <= t->hi[hit]) return (void*)p;
+    if (atomicAdd(&t->count, 1u) == 0u) {
+        t->addr = a;
+        t->field_lo = t->lo[hit];
+        t->where = ((unsigned long long)blockIdx.x << 32) | threadIdx.x;
+    }
+    return g_bounds_sink;
+}
+#define MPAS_CHK(base, p, bytes) bounds_chk((base), (p), (bytes))
+#else
+#define MPAS_CHK(base, p, bytes) (p)
+#endif
+
 // Level k of column ent of field f, addressed as the field's base (wave-uniform, SGPRs)
 // plus a 32-bit byte offset in a VGPR: loads compile to the saddr + voffset form, every
 // field gathered at the same neighbour shares one offset register, and only one SGPR
@@ -339,10 +399,15 @@ __device__ __forceinline__ uint32_t col_off(int ent, int k) {
 }
 template <class T>
 __device__ __forceinline__ T& at_off(T* f, uint32_t off) {
+#if MPAS_BOUNDS
+    return *(T*)bounds_chk(f, (const char*)f + off, sizeof(T));
+#else
     return *(T*)((MPAS_GLOBAL char*)(f) + off);
+#endif
 }
 // level k of column ent of field pointer f (needs LP and k in scope)
 #define colk(f, ent) at_off((f), col_off<LP>((ent), k))
+
 
 // Two gathered columns, a = level k of column ia of field fa, b = level k of column ib
 // of field fb (any fields, any entities).  At LP = 64 one 16-B load per lane (lanes 0-31
@@ -367,7 +432,7 @@ __device__ __forceinline__ void gather2(const double* fa, int ia, const double* 
     if constexpr (LP == 64) {
         const bool hi = k >= 32;
         const char* base = hi ? (const char*)fb + (size_t)(uint32_t)ib * 512 : (const char*)fa + (size_t)(uint32_t)ia * 512;
-        const double2 t = *(const double2*)(base + (k & 31) * 16);
+        const double2 t = *(const double2*)MPAS_CHK(hi ? fb : fa, base + (k & 31) * 16, 16);
         double x = t.x, y = t.y;
         swap_halves(x, y);
         a = x;
@@ -465,6 +530,9 @@ __device__ __forceinline__ double sub_if(bool c, double acc, double t) { return 
 // allocated at its full width, so the entries past the list's length are in bounds)
 template <int N, class T>
 __device__ __forceinline__ void row_ld(const T* p, T (&r)[N]) {
+#if MPAS_BOUNDS
+    p = (const T*)(MPAS_CHK(p, p, N * sizeof(T)) == (const void*)p ? p : (const T*)g_bounds_sink);
+#endif
 #pragma unroll
     for (int i = 0; i < N; i++) r[i] = p[i];
 }

@@ -56,3 +56,14 @@ def test_library_is_gfx950_only():
     assert b"gfx950" in blob
     for other in (b"gfx942", b"gfx90a", b"gfx1100"):
         assert other not in blob
+
+
+def test_bounds_build_exports_the_same_abi():
+    """the bounds-checked build is a drop-in of the product library"""
+    path = os.path.join(os.path.dirname(lib.LIB_PATH), "libmpasdyn_bounds.so")
+    if not os.path.exists(path):
+        pytest.skip("libmpasdyn_bounds.so not built (__graft_entry__.build() builds it)")
+    L = ctypes.CDLL(path)
+    for name in header_functions():
+        assert hasattr(L, name), name
+    assert b"gfx950" in open(path, "rb").read()
