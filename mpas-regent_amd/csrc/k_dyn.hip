@@ -34,6 +34,8 @@
 #include "mpas_dev.h"
 #include "mpas_halo.h"
 
+#include <type_traits>
+
 namespace mpas {
 
 __device__ __forceinline__ double dmin_(double a, double b) { return a < b ? a : b; }
@@ -194,7 +196,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 }
 
 // ------------------------------------------------------------------------ B (edges)
-template <int LP, bool RK0, bool MD>
+template <int LP, bool RK0, bool MD, bool HF>
 __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
@@ -271,7 +273,17 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     gather2s<LP>(hd_f, cell1, cell2, k, hd1, hd2);
     // (the rk0-only loads stay in their section: hoisted they cost more in occupancy,
     // 138 VGPRs, than the second memory round trip)
-    const double tue_in = rk0 ? 0.0 : colk(fd(S, F_tend_u_euler), e);
+    // HF (fast path): E's per-edge theta flux H formed here (rk > 0: with the
+    // perturbation flux, which needs ru_save at the edge and theta_m_save at its cells)
+    double tue_in = 0.0, rus_e = 0.0, ts1 = 0.0, ts2 = 0.0;
+    if constexpr (!RK0) {
+        if constexpr (HF) {
+            gather2<LP>(fd(S, F_tend_u_euler), e, fd(S, F_ru_save), e, k, tue_in, rus_e);
+            gather2s<LP>(fd(S, F_theta_m_save), cell1, cell2, k, ts1, ts2);
+        } else {
+            tue_in = colk(fd(S, F_tend_u_euler), e);
+        }
+    }
 
     const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
     const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
@@ -296,7 +308,13 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
             double scalar_weight = ac[j] + sg * ac3[j];
             flux_arr += scalar_weight * colk(tm_f, ad[j]);
         }
-        colk(fw(S, X_F), e) = kl ? flux_arr : 0.0;
+        if constexpr (HF) {  // H = ru F (+ dvEdge (ru_save - ru) theta_m_save at the edge, rk > 0)
+            double h = ru_e * flux_arr;
+            if constexpr (!RK0) h += fd(S, F_dvEdge)[e] * ((rus_e - ru_e) * 0.5 * (ts2 + ts1));
+            colk(fw(S, X_F), e) = kl ? h : 0.0;
+        } else {
+            colk(fw(S, X_F), e) = kl ? flux_arr : 0.0;
+        }
     }
     if constexpr (MD) {  // flux_arr of the w advection at this edge (:1174-1197, every edge)
         const double ru_edge_w = fzm * ru_e + fzp * lvl_dn<LP>(ru_e, k);
@@ -542,7 +560,7 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
 }
 
 // ------------------------------------------------------------------------ E (cells)
-template <int LP, bool RK0, bool SELF, bool MD>
+template <int LP, bool RK0, bool SELF, bool MD, bool HF>
 __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -584,7 +602,8 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
 #pragma unroll
         for (int i = 0; i < NF; i += 2) gather2s<LP>(fd(S, X_Fw), e_[i], e_[i + 1], k, Fw_[i], Fw_[i + 1]);
     }
-    gather2<LP>(fd(S, F_pressure_p), c, fd(S, F_dpdz), c, k, pp, dpdz);
+    if (rk0) gather2<LP>(fd(S, F_pressure_p), c, fd(S, F_dpdz), c, k, pp, dpdz);
+    else pp = dpdz = 0.0;
     gather2<LP>(fd(S, F_rw_save), c, tms_f, c, k, rws, tms);
     gather2<LP>(tm, c, fd(S, F_tend_w_euler), c, k, tmv, twe);
     gather2<LP>(fd(S, F_tend_theta_euler), c, fd(S, F_rho_zz), c, k, tte, rho_zz);
@@ -595,18 +614,20 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
         if (SELF) dt_c = colk(dth, c);
     }
     const double ts_c = tms;  // (SELF, rk > 0: theta_m_save at the cell itself)
+    // HF: F holds B's per-edge flux H (ru F + the rk > 0 perturbation flux): ru, ru_save
+    // and the theta_m_save pairs are not gathered here
 #pragma unroll
     for (int i = 0; i < NF; i += 2) {
-        gather2s<LP>(ru, e_[i], e_[i + 1], k, ru_[i], ru_[i + 1]);
+        if (!HF) gather2s<LP>(ru, e_[i], e_[i + 1], k, ru_[i], ru_[i + 1]);
         gather2s<LP>(Ff, e_[i], e_[i + 1], k, F_[i], F_[i + 1]);
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ru_[i] = ldz(kl, ru_[i]);
+        ru_[i] = HF ? 0.0 : ldz(kl, ru_[i]);
         F_[i] = ldz(kl, F_[i]);
         rus_[i] = ts1_[i] = ts2_[i] = dw1_[i] = dw2_[i] = dt1_[i] = dt2_[i] = 0.0;
     }
-    if (!rk0) {
+    if (!rk0 && !HF) {
 #pragma unroll
         for (int i = 0; i < NF; i += 2) {
             gather2s<LP>(rus, e_[i], e_[i + 1], k, rus_[i], rus_[i + 1]);
@@ -702,7 +723,11 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
 
     // ================= theta =================
     double tend_theta = 0.0;  // :1328-1344
-    if (kl) {
+    if (kl && HF) {  // the same sums over B's per-edge H (fast path: reassociated)
+#pragma unroll
+        for (int i = 0; i < NF; i++) tend_theta = sub_if(i < ne, tend_theta, eocs_[i] * F_[i]);
+        for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(Ff, eoc[i]);
+    } else if (kl) {
 #pragma unroll
         for (int i = 0; i < NF; i++) tend_theta = sub_if(i < ne, tend_theta, eocs_[i] * ru_[i] * F_[i]);
         for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(ru, eoc[i]) * colk(Ff, eoc[i]);
@@ -719,6 +744,8 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
                 tend_theta -= flux;
             }
         }
+    }
+    if (kl) {
         if (del4) {  // :1384-1400
             double r_areaCell = a.h4 * a.prandtl_inv * invA;
 #pragma unroll
@@ -777,6 +804,9 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
     a.prandtl_inv = 1.0 / kPrandtl;
     const bool rk0 = a.rk_step == 0, del4 = rk0 && a.h4 > 0.0;
+    // HF: the fast path's theta flux per edge formed in B (E sums eocs H; reassociated, so
+    // exact mode keeps the reference's per-cell order)
+    const bool hf = !MD && !a.exact_q;
     // kernel launches over the entities of a DevState range (HALO_RUN: interior /
     // boundary halves around a halo exchange, or all owned entities)
     auto kA = [&](const DevState& X) {
@@ -788,8 +818,16 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
-        if (rk0) k_dyn_B<LP, true, MD><<<nb, 256, 0, st>>>(X, a);
-        else k_dyn_B<LP, false, MD><<<nb, 256, 0, st>>>(X, a);
+        if constexpr (MD) {
+            if (rk0) k_dyn_B<LP, true, MD, false><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_B<LP, false, MD, false><<<nb, 256, 0, st>>>(X, a);
+        } else if (hf) {
+            if (rk0) k_dyn_B<LP, true, MD, true><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_B<LP, false, MD, true><<<nb, 256, 0, st>>>(X, a);
+        } else {
+            if (rk0) k_dyn_B<LP, true, MD, false><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_B<LP, false, MD, false><<<nb, 256, 0, st>>>(X, a);
+        }
     };
     auto kC = [&](const DevState& X) {  // vertex blocks (del4) first, then cell blocks
         const int nv = del4 ? col_blocks<LP>(X, KV) : 0, nb = nv + col_blocks<LP>(X, KC);
@@ -804,13 +842,19 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     auto kE = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
         if (!nb) return;
-        if (rk0) {
-            if (X.selfc) k_dyn_E<LP, true, true, MD><<<nb, 256, 0, st>>>(X, a);
-            else k_dyn_E<LP, true, false, MD><<<nb, 256, 0, st>>>(X, a);
-        } else {
-            if (X.selfc) k_dyn_E<LP, false, true, MD><<<nb, 256, 0, st>>>(X, a);
-            else k_dyn_E<LP, false, false, MD><<<nb, 256, 0, st>>>(X, a);
-        }
+        auto go = [&](auto hfc) {
+            constexpr bool H = decltype(hfc)::value;
+            if (rk0) {
+                if (X.selfc) k_dyn_E<LP, true, true, MD, H><<<nb, 256, 0, st>>>(X, a);
+                else k_dyn_E<LP, true, false, MD, H><<<nb, 256, 0, st>>>(X, a);
+            } else {
+                if (X.selfc) k_dyn_E<LP, false, true, MD, H><<<nb, 256, 0, st>>>(X, a);
+                else k_dyn_E<LP, false, false, MD, H><<<nb, 256, 0, st>>>(X, a);
+            }
+        };
+        if constexpr (MD) go(std::false_type{});
+        else if (hf) go(std::true_type{});
+        else go(std::false_type{});
     };
     // halo: fields each kernel gathers through an index array / fields it writes
     // (u and v only for the Smagorinsky deformation of rk_step 0: a gather declared but not
@@ -832,12 +876,15 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
             HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
             HALO_WROTE(S, F_tend_u_euler, F_tend_u);
         }
-        HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
+        if (hf) HALO_RUN(S, st, kE, X_F, F_delsq_w, F_delsq_theta);
+        else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
     } else {
-        HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
+        if (hf) HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_theta_m_save);
+        else HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
         HALO_WROTE(S, X_F, F_tend_u);
         if (MD) HALO_WROTE(S, X_Fw);
-        HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);
+        if (hf) HALO_RUN(S, st, kE, X_F);
+        else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);
     }
     HALO_WROTE(S, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
     HALO_WROTE(S, MD ? F_tend_w : F_w);
