@@ -51,9 +51,67 @@ static int stream_grid(size_t n) {
     size_t g = (n + 255) / 256;
     return (int)(g < 8192 ? (g ? g : 1) : 8192);
 }
+
+// LP = 64 streaming form: one 16-B position pair per thread (positions 2j, 2j+1 of a
+// column = levels j and j+32, mpas_dev.h lpos), every copy of the task in ONE launch
+// (blockIdx.y = copy).  The never-written level-L slot sits in pair lpos(L) >> 1 of each
+// column: that pair stores only its other element.
+struct Pair64 {
+    int pair, el;  // pair index within the column holding level L, and L's element in it
+    __host__ __device__ Pair64(int L) : pair(lpos(64, L) >> 1), el(lpos(64, L) & 1) {}
+};
+__device__ __forceinline__ void st64(double* d, size_t i, double2 v, Pair64 q) {
+    if ((int)(i & 31) != q.pair) *(double2*)(d + 2 * i) = v;
+    else d[2 * i + (1 - q.el)] = q.el ? v.x : v.y;
+}
+struct CopyList {
+    const double* src[8];
+    double* dst[8];
+    double* dst2[8];  // optional second destination of the same source (nullptr: none)
+    size_t npair[8];
+};
+__global__ __launch_bounds__(256) void k_copy64(CopyList cl, Pair64 q) {
+    const int j = blockIdx.y;
+    const double2* s = (const double2*)cl.src[j];
+    double *d = cl.dst[j], *d2 = cl.dst2[j];
+    const size_t n = cl.npair[j];
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        const double2 v = s[i];
+        st64(d, i, v, q);
+        if (d2) st64(d2, i, v, q);
+    }
+}
+static void copy64(const DevState& S, hipStream_t st, const CopyList& cl, int ncopy) {
+    size_t nmax = 0;
+    for (int j = 0; j < ncopy; j++) nmax = cl.npair[j] > nmax ? cl.npair[j] : nmax;
+    const int gx = (int)((stream_grid(nmax) + 3) / 4);
+    if (nmax) k_copy64<<<dim3(gx, ncopy), 256, 0, st>>>(cl, Pair64(S.L));
+}
+
 hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st) {
-    k_setup_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S);
-    k_setup_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
+    if (S.LP == 64) {
+        CopyList cl{};
+        int n = 0;
+        const size_t ne = (size_t)S.nEO * 32, nc = (size_t)S.nCO * 32;
+        auto add = [&](int from, int to, int to2, size_t np) {
+            cl.src[n] = (const double*)S.f[from];
+            cl.dst[n] = (double*)S.f[to];
+            cl.dst2[n] = to2 >= 0 ? (double*)S.f[to2] : nullptr;
+            cl.npair[n++] = np;
+        };
+        add(F_ru, F_ru_save, -1, ne);
+        add(F_u, F_u_2, -1, ne);
+        add(F_rw, F_rw_save, -1, nc);
+        add(F_rtheta_p, F_rtheta_p_save, -1, nc);
+        add(F_rho_p, F_rho_p_save, -1, nc);
+        add(F_w, F_w_2, -1, nc);
+        add(F_theta_m, F_theta_m_2, S.physics == 2 ? F_theta_m_save : -1, nc);
+        add(F_rho_zz, F_rho_zz_2, F_rho_zz_old_split, nc);
+        copy64(S, st, cl, n);
+    } else {
+        k_setup_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S);
+        k_setup_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S);
+    }
     HALO_WROTE(S, F_ru_save, F_u_2, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2,
                F_rho_zz_old_split);
     if (S.physics == 2) HALO_WROTE(S, F_theta_m_save);
@@ -392,10 +450,50 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
         }
     }
 }
+// LP = 64 form of both finish kernels in one launch (blockIdx.y: 0 edges, 1 cells), 16-B
+// position pairs.  With substep = split = 1 (atm_srk3) the average is s * 1.0 = s: its
+// store back is skipped (the same bits)
+__global__ __launch_bounds__(256) void k_finish64(DevState S, int substep, int split, double inv_split, Pair64 q) {
+    const bool cells = blockIdx.y == 1;
+    const size_t n = (size_t)(cells ? S.nCO : S.nEO) * 32;
+    double *avg = fw(S, cells ? F_wwAvg : F_ruAvg), *avgS = fw(S, cells ? F_wwAvg_split : F_ruAvg_split);
+    const bool restore = substep < split, last = substep == split, same = substep == 1 && inv_split == 1.0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        auto cp = [&](int from, int to) { st64(fw(S, to), i, ((const double2*)fd(S, from))[i], q); };
+        if (restore) {
+            if (cells) {
+                cp(F_rw, F_rw_save);
+                cp(F_rtheta_p, F_rtheta_p_save);
+                cp(F_rho_p, F_rho_p_save);
+                cp(F_w_2, F_w);
+                cp(F_theta_m_2, F_theta_m);
+                cp(F_rho_zz_2, F_rho_zz);
+            } else {
+                cp(F_ru, F_ru_save);
+                cp(F_u_2, F_u);
+            }
+        }
+        const double2 a = ((const double2*)avg)[i];
+        double2 sv = a;
+        if (substep != 1) {
+            const double2 b = ((const double2*)avgS)[i];
+            sv = make_double2(a.x + b.x, a.y + b.y);
+        }
+        st64(avgS, i, sv, q);
+        if (last && !same) st64(avg, i, make_double2(sv.x * inv_split, sv.y * inv_split), q);
+        if (cells && last && S.physics != 2) cp(F_rho_zz_old_split, F_rho_zz);
+    }
+}
+
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split) {
     double inv = 1.0 / (double)split;
-    k_finish_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S, substep, split, inv);
-    k_finish_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    if (S.LP == 64) {
+        const int gx = (stream_grid((size_t)S.nEO * 32) + 3) / 4;
+        k_finish64<<<dim3(gx, 2), 256, 0, st>>>(S, substep, split, inv, Pair64(S.L));
+    } else {
+        k_finish_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S, substep, split, inv);
+        k_finish_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S, substep, split, inv);
+    }
     // what the kernels write for these arguments (a field declared written but untouched
     // would cost every later gather of it a halo exchange): with substep = split = 1, as
     // atm_srk3 calls it, only the averages and (physics != 2) rho_zz
