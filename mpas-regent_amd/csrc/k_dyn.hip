@@ -296,6 +296,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // Every lane goes on (gather2 below needs all of them); level L is not stored, the
     // padding levels get 0.0 (PADW), the scratch F is stored whole.
 
+    double Hv = 0.0, dsq = 0.0;  // HF: the values of the paired stores at the end
     {  // flux_arr of this edge
         const double sg = copysign(1.0, ru_e);
         double flux_arr = 0.0;
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         if constexpr (HF) {  // H = ru F (+ dvEdge (ru_save - ru) theta_m_save at the edge, rk > 0)
             double h = ru_e * flux_arr;
             if constexpr (!RK0) h += fd(S, F_dvEdge)[e] * ((rus_e - ru_e) * 0.5 * (ts2 + ts1));
-            colk(fw(S, X_F), e) = kl ? h : 0.0;
+            Hv = kl ? h : 0.0;  // (stored with tend_u / delsq_u below: paired stores)
         } else {
             colk(fw(S, X_F), e) = kl ? flux_arr : 0.0;
         }
@@ -386,7 +387,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         double u_diffusion = (dv2 - dv1) * r_dc - (vo2 - vo1) * r_dv;
         double delsq_u = 0.0;
         delsq_u += u_diffusion;
-        if (k != L) colk(fw(S, F_delsq_u), e) = PADW(delsq_u);
+        if (HF) dsq = PADW(delsq_u);
+        else if (k != L) colk(fw(S, F_delsq_u), e) = PADW(delsq_u);
         double kdiffu = 0.5 * (kf1 + kf2);
         tue += rho_edge * kdiffu * u_diffusion * fd(S, F_meshScalingDel2)[e];
     } else {
@@ -395,6 +397,20 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // ---- Rayleigh damping (:1152-1159)
     if (a.rayleigh && k > L - kRayleighLevels + 1)
         tend_u -= rho_edge * u * (((double)k - (double)(L - kRayleighLevels)) * a.rayleigh_inv);
+    if constexpr (HF) {  // every lane stores (paired 16-B stores); level L keeps its value
+        double* Fo = fw(S, X_F);
+        double* tuo = fw(S, F_tend_u);
+        double* tueo = fw(S, F_tend_u_euler);
+        if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
+            put2<LP>(Fo, e, fw(S, F_delsq_u), e, k, L, Hv, dsq, true, false);
+            put2<LP>(tueo, e, tuo, e, k, L, PADW(tue), PADW(tend_u), false, false);
+        } else {
+            tend_u += tue + tr_phys;  // :1161-1163 (rk > 0: tue is the tend_u_euler read)
+            put2<LP>(Fo, e, tuo, e, k, L, Hv, PADW(tend_u), true, false);
+            if (rk0) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, L, PADW(tue), dsq, false, false);
+        }
+        return;
+    }
     if (k == L) return;
     if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
         colk(fw(S, F_tend_u_euler), e) = PADW(tue);
@@ -715,7 +731,7 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
             if (rk0) twe -= cqw * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
             w += twe;
         }
-        if (k != L) {  // (padding levels: zeros, PADW)
+        if (!HF && k != L) {  // (padding levels: zeros, PADW; HF: paired stores at the end)
             colk(fw(S, F_w), c) = PADW(w);
             if (rk0) colk(fw(S, F_tend_w_euler), c) = PADW(twe);
         }
@@ -774,6 +790,16 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     }
     if (k == L) wdtz = wdtzL;
     const double wdtz_p = lvl_up<LP>(wdtz, k);
+    if constexpr (HF) {  // every lane stores (paired 16-B stores); level L keeps its value
+        tend_theta *= invA - rdzw * (wdtz_p - wdtz);  // :1422-1427, :1477-1479
+        const double rth = tend_theta / rho_zz;
+        put2<LP>(fw(S, F_w), c, fw(S, F_tend_rtheta_adv), c, k, L, PADW(w), PADW(tend_theta), false, false);
+        tend_theta += rho_zz * rt_diab;
+        tend_theta += tte + trp;
+        put2<LP>(fw(S, F_rthdynten), c, fw(S, F_tend_theta), c, k, L, PADW(rth), PADW(tend_theta), false, false);
+        if (rk0) put2<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k, L, PADW(twe), PADW(tte), false, false);
+        return;
+    }
     if (k == L) return;  // (padding levels: zeros, PADW)
     // :1422-1427, :1477-1479
     if (MD) tend_theta = tend_theta * invA - rdzw * (wdtz_p - wdtz);
