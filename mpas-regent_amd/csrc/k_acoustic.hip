@@ -192,12 +192,10 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
             ww = ww + 0.5 * (1.0 + epssm) * r;
         }
         const double r_p = lvl_up<LP>(r, k);
-        if (k != L) {
-            colk(rpp_f, c) = PADW(rs - cofrz * (r_p - r));
-            colk(rtp_f, c) = PADW(ts - rdzw * (coftz_p * r_p - coftz * r));
-        }
-        colk(rwp_f, c) = PADW(r);
-        colk(ww_f, c) = PADW(ww);
+        // (paired 16-B stores, every lane; level L of rho_pp / rtheta_pp keeps its value)
+        put2<LP>(rpp_f, c, rtp_f, c, k, PADW(rs - cofrz * (r_p - r)), PADW(ts - rdzw * (coftz_p * r_p - coftz * r)),
+                 k != L, k != L);
+        put2<LP>(rwp_f, c, ww_f, c, k, PADW(r), PADW(ww), true, true);
         return;
     }
 
@@ -268,12 +266,10 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         x = (k == 0) ? rwold : H;
     }
     if (k < L && k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
-    if (k != L) {
-        colk(rpp_f, c) = PADW(rs - cofrz * (rwp_p - x));
-        colk(rtp_f, c) = PADW(ts - rdzw * (coftz_p * rwp_p - coftz * x));
-    }
-    colk(rwp_f, c) = PADW((k < L) ? x : rwp);
-    colk(ww_f, c) = PADW(ww);
+    // (paired 16-B stores, every lane; level L of rho_pp / rtheta_pp keeps its value)
+    put2<LP>(rpp_f, c, rtp_f, c, k, PADW(rs - cofrz * (rwp_p - x)), PADW(ts - rdzw * (coftz_p * rwp_p - coftz * x)),
+             k != L, k != L);
+    put2<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww), true, true);
 }
 
 // :1581-1613 restored (Q18, MPAS vertical solver only): ru_p and ruAvg of every owned

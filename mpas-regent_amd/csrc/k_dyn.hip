@@ -150,14 +150,14 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         hd += edge_sign * col_rd<LP>(ru, eoc[i], k, L);
     }
     hd *= fd(S, F_invAreaCell)[c];
-    if (k != L) colk(fw(S, F_h_divergence), c) = PADW(hd);
+    if (MD && k != L) colk(fw(S, F_h_divergence), c) = PADW(hd);  // (else paired with wc below)
 
     // ---- tend_rho, dpdz (:942-951)
     const double rw_p1 = lvl_up<LP>(rw, k);
-    if (rk0 && k != L) {
-        colk(fw(S, F_tend_rho), c) = PADW(MD ? -hd - rdzw * (rw_p1 - rw) + trp : -hd - rdzw * (rw_p1 - rw + trp));
-        colk(fw(S, F_dpdz), c) = PADW(-kGravity * (rb * (qt) + rps * (1.0 + qt)));
-    }
+    if (rk0)  // (paired 16-B store, every lane)
+        put2<LP>(fw(S, F_tend_rho), c, fw(S, F_dpdz), c, k,
+                 PADW(MD ? -hd - rdzw * (rw_p1 - rw) + trp : -hd - rdzw * (rw_p1 - rw + trp)),
+                 PADW(-kGravity * (rb * (qt) + rps * (1.0 + qt))), k != L, k != L);
 
     // ---- w: zeroing (:1170), horizontal advection (:1174-1205, Q13), curvature (:1208-1218)
     // After the zeroing every w(cell, k<L) read by flux_arr is exactly 0.0 (the zero
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
         wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
               2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
     }
-    colk(fw(S, X_wc), c) = k < L ? wc : 0.0;
+    put2<LP>(fw(S, F_h_divergence), c, fw(S, X_wc), c, k, PADW(hd), k < L ? wc : 0.0, k != L, true);
 }
 
 // ------------------------------------------------------------------------ B (edges)
@@ -402,12 +402,12 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         double* tuo = fw(S, F_tend_u);
         double* tueo = fw(S, F_tend_u_euler);
         if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
-            put2<LP>(Fo, e, fw(S, F_delsq_u), e, k, L, Hv, dsq, true, false);
-            put2<LP>(tueo, e, tuo, e, k, L, PADW(tue), PADW(tend_u), false, false);
+            put2<LP>(Fo, e, fw(S, F_delsq_u), e, k, Hv, dsq, true, k != L);
+            put2<LP>(tueo, e, tuo, e, k, PADW(tue), PADW(tend_u), k != L, k != L);
         } else {
             tend_u += tue + tr_phys;  // :1161-1163 (rk > 0: tue is the tend_u_euler read)
-            put2<LP>(Fo, e, tuo, e, k, L, Hv, PADW(tend_u), true, false);
-            if (rk0) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, L, PADW(tue), dsq, false, false);
+            put2<LP>(Fo, e, tuo, e, k, Hv, PADW(tend_u), true, k != L);
+            if (rk0) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, PADW(tue), dsq, k != L, k != L);
         }
         return;
     }
@@ -541,12 +541,10 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
         edge_terms(kl, eocs[i], cdv[i], cidc[i], cmsd2[i], re_k, re_m, kd1, kd2, kd1m, kd2m, ldz(kl, colk(wc, c1)),
                    ldz(kl, colk(wc, c2)), ldz(kl, colk(tm, c1)), ldz(kl, colk(tm, c2)), ldz(kl && del4, colk(dsu, e)));
     }
-    if (k == L) return;  // (padding levels: zeros, PADW)
-    if (del4) colk(fw(S, F_delsq_divergence), c) = PADW(dsd);
-    colk(fw(S, F_delsq_w), c) = PADW(delsq_w);
-    colk(fw(S, F_tend_w_euler), c) = PADW(twe);
-    colk(fw(S, F_delsq_theta), c) = PADW(delsq_theta);
-    colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
+    // (padding levels: zeros, PADW; level L keeps its value; paired 16-B stores, every lane)
+    if (del4 && k != L) colk(fw(S, F_delsq_divergence), c) = PADW(dsd);
+    put2<LP>(fw(S, F_delsq_w), c, fw(S, F_tend_w_euler), c, k, PADW(delsq_w), PADW(twe), k != L, k != L);
+    put2<LP>(fw(S, F_delsq_theta), c, fw(S, F_tend_theta_euler), c, k, PADW(delsq_theta), PADW(tte), k != L, k != L);
 }
 
 // ------------------------------------------------------------------------ D (rk0, del4)
@@ -567,12 +565,11 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
     gather2s<LP>(dd, cell1, cell2, k, dd1, dd2);
     gather2s<LP>(dvv, vertex1, vertex2, k, dv1, dv2);
     gather2<LP>(fd(S, F_tend_u), e, fd(S, F_tend_ru_physics), e, k, tend_u, trp);
-    if (k == L) return;  // (padding levels: zeros, PADW)
     double u_diffusion = re * ((dd2 - dd1) * r_dc - (dv2 - dv1) * r_dv);
     tue -= u_diffusion;
-    colk(fw(S, F_tend_u_euler), e) = PADW(tue);
     tend_u += tue + trp;
-    colk(fw(S, F_tend_u), e) = PADW(tend_u);
+    // (padding levels: zeros, PADW; level L keeps its value; one paired 16-B store, every lane)
+    put2<LP>(fw(S, F_tend_u_euler), e, fw(S, F_tend_u), e, k, PADW(tue), PADW(tend_u), k != L, k != L);
 }
 
 // ------------------------------------------------------------------------ E (cells)
@@ -793,11 +790,11 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     if constexpr (HF) {  // every lane stores (paired 16-B stores); level L keeps its value
         tend_theta *= invA - rdzw * (wdtz_p - wdtz);  // :1422-1427, :1477-1479
         const double rth = tend_theta / rho_zz;
-        put2<LP>(fw(S, F_w), c, fw(S, F_tend_rtheta_adv), c, k, L, PADW(w), PADW(tend_theta), false, false);
+        put2<LP>(fw(S, F_w), c, fw(S, F_tend_rtheta_adv), c, k, PADW(w), PADW(tend_theta), k != L, k != L);
         tend_theta += rho_zz * rt_diab;
         tend_theta += tte + trp;
-        put2<LP>(fw(S, F_rthdynten), c, fw(S, F_tend_theta), c, k, L, PADW(rth), PADW(tend_theta), false, false);
-        if (rk0) put2<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k, L, PADW(twe), PADW(tte), false, false);
+        put2<LP>(fw(S, F_rthdynten), c, fw(S, F_tend_theta), c, k, PADW(rth), PADW(tend_theta), k != L, k != L);
+        if (rk0) put2<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k, PADW(twe), PADW(tte), k != L, k != L);
         return;
     }
     if (k == L) return;  // (padding levels: zeros, PADW)

@@ -172,11 +172,13 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
     const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
     const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
     const double rdzw_m = k > 0 ? rdzw_a[k - 1] : 0.0;
-    const double zz = colk(fd(S, F_zz), c), exner = colk(fd(S, F_exner), c), tm = colk(fd(S, F_theta_m), c);
-    const double cqw = colk(fd(S, F_cqw), c), qtot = colk(fd(S, F_qtot), c);
-    const double rb = colk(fd(S, F_rho_base), c), rtb = colk(fd(S, F_rtheta_base), c), rtp = colk(fd(S, F_rtheta_p), c);
-    const double exb = colk(fd(S, F_exner_base), c);
-    const double gamma_old = colk(fd(S, F_gamma_tri), c);
+    // (gather2: two own columns per 16-B load instruction)
+    double zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old;
+    gather2<LP>(fd(S, F_zz), c, fd(S, F_exner), c, k, zz, exner);
+    gather2<LP>(fd(S, F_theta_m), c, fd(S, F_cqw), c, k, tm, cqw);
+    gather2<LP>(fd(S, F_qtot), c, fd(S, F_rho_base), c, k, qtot, rb);
+    gather2<LP>(fd(S, F_rtheta_base), c, fd(S, F_rtheta_p), c, k, rtb, rtp);
+    gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
     const double coftz_old = colk(fd(S, F_coftz), c);  // level L keeps its (never written) value
     const double zz_m = lvl_dn<LP>(zz, k), exner_m = lvl_dn<LP>(exner, k), tm_m = lvl_dn<LP>(tm, k);
 
@@ -220,24 +222,16 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
         gamma = cc * alpha;               // :587-591
     }
 
-    const bool pad = k > L;  // padding levels: zeros (full 64-B sectors; see PADW)
-    if (k < L || pad) {
-        double* o;
-        colk(fw(S, F_coftz), c) = PADW(coftz);
-        colk(fw(S, F_cofwt), c) = PADW(cofwt);
-        if (k == 0) {
-            colk(fw(S, F_gamma_tri), c) = 0.0;
-        } else {
-            colk(fw(S, F_cofwr), c) = PADW(cofwr);
-            colk(fw(S, F_cofwz), c) = PADW(cofwz);
-            o = fw(S, F_a_tri); colk(o, c) = PADW(a);
-            o = fw(S, F_b_tri); colk(o, c) = PADW(b);
-            o = fw(S, F_c_tri); colk(o, c) = PADW(cc);
-            o = fw(S, F_alpha_tri); colk(o, c) = PADW(alpha);
-            o = fw(S, F_gamma_tri); colk(o, c) = PADW(gamma);
-        }
-        if (c == 0 && !pad) fw(S, F_cofrz)[k] = cofrz;
-    }
+    // written: every level but L (padding levels: zeros, full 64-B sectors; see PADW); the
+    // tridiagonal coefficients not at level 0 either, gamma_tri 0.0 there.  Paired 16-B
+    // stores (put2: every lane takes part)
+    const bool w_all = k != L, w_1 = k != L && k != 0;
+    put2<LP>(fw(S, F_coftz), c, fw(S, F_cofwt), c, k, PADW(coftz), PADW(cofwt), w_all, w_all);
+    put2<LP>(fw(S, F_cofwr), c, fw(S, F_cofwz), c, k, PADW(cofwr), PADW(cofwz), w_1, w_1);
+    put2<LP>(fw(S, F_a_tri), c, fw(S, F_b_tri), c, k, PADW(a), PADW(b), w_1, w_1);
+    put2<LP>(fw(S, F_c_tri), c, fw(S, F_alpha_tri), c, k, PADW(cc), PADW(alpha), w_1, w_1);
+    if (w_all) colk(fw(S, F_gamma_tri), c) = k == 0 ? 0.0 : PADW(gamma);
+    if (c == 0 && k < L) fw(S, F_cofrz)[k] = cofrz;
 }
 template <int LP>
 static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
@@ -271,9 +265,9 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     const double* zb = fd(S, F_zb_cell);
     const double* zb3 = fd(S, F_zb3_cell);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
-    const double zz = col_rd<LP>(fd(S, F_zz), c, k, L);
+    double zz, w;
+    col_rd2<LP>(fd(S, F_zz), fd(S, wf), c, k, L, zz, w);
     const double zz_m = lvl_dn<LP>(zz, k);
-    double w = col_rd<LP>(fd(S, wf), c, k, L);
     int e_[NF];
     double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgn_[NF];
     row_ld(eoc, e_);
@@ -283,9 +277,7 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         ut_[i] = ldz(k <= L, ut_[i]);
-        size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
-        zb_[i] = zb[q];
-        zb3_[i] = zb3[q];
+        gather2<LP>(zb, c * 10 + i, zb3, c * 10 + i, k, zb_[i], zb3_[i]);  // (one 16-B load)
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);

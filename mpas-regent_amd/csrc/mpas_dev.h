@@ -464,26 +464,26 @@ __device__ __forceinline__ void cell_pair(const double* f, int c1, int c2, int o
 // The inverse of gather2: lane k holds level k of column ia of fa (value a) and of column
 // ib of fb (value b); at LP = 64 one 16-B store per lane writes both (lanes 0-31 the level
 // pair of ia, lanes 32-63 that of ib, after the same permlane32 swap), so every lane of the
-// wavefront must take part.  Level L (the slot the reference never writes) is stored only
-// for a column marked whole (wa / wb); the caller applies PADW to the padding levels.
+// wavefront must take part.  oka / okb: whether level k of each column is written (a level
+// the reference never writes -- level L, or level 0 of some fields -- keeps its value);
+// the caller applies PADW to the padding levels.
 template <int LP>
-__device__ __forceinline__ void put2(double* fa, int ia, double* fb, int ib, int k, int L, double a, double b, bool wa,
-                                     bool wb) {
+__device__ __forceinline__ void put2(double* fa, int ia, double* fb, int ib, int k, double a, double b, bool oka,
+                                     bool okb) {
     if constexpr (LP == 64) {
         double x = a, y = b;
         swap_halves(x, y);
+        const auto f = __builtin_amdgcn_permlane32_swap((unsigned)oka, (unsigned)okb, false, false);
+        const bool sx = f[0] != 0, sy = f[1] != 0;  // this lane's two elements (levels k & 31, +32)
         const bool hi = k >= 32;
-        const int lx = k & 31, ly = lx + 32;  // the levels of this lane's two elements
-        const bool whole = hi ? wb : wa;
-        const bool sx = whole || lx != L, sy = whole || ly != L;
         char* base = hi ? (char*)fb + (size_t)(uint32_t)ib * 512 : (char*)fa + (size_t)(uint32_t)ia * 512;
-        double* q = (double*)MPAS_CHK(hi ? fb : fa, base + lx * 16, 16);
+        double* q = (double*)MPAS_CHK(hi ? fb : fa, base + (k & 31) * 16, 16);
         if (sx && sy) *(double2*)q = make_double2(x, y);
         else if (sx) q[0] = x;
-        else q[1] = y;
+        else if (sy) q[1] = y;
     } else {
-        if (wa || k != L) colk(fa, ia) = a;
-        if (wb || k != L) colk(fb, ib) = b;
+        if (oka) colk(fa, ia) = a;
+        if (okb) colk(fb, ib) = b;
     }
 }
 

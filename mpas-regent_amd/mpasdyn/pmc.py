@@ -16,7 +16,7 @@ from collections import defaultdict
 
 # kernel -> timing key of the task it belongs to (first regex that matches)
 KERNEL_TASK = [
-    (r"k_setup_(cells|edges)", "atm_rk_integration_setup"),
+    (r"k_setup_(cells|edges)|k_copy64", "atm_rk_integration_setup"),
     (r"k_moist", "atm_compute_moist_coefficients"),
     (r"k_vert_imp", "atm_compute_vert_imp_coefs"),
     (r"k_dyn_[ABE]<\d+, true", "atm_compute_dyn_tend_work[rk0]"),
@@ -26,7 +26,7 @@ KERNEL_TASK = [
     (r"k_acoustic", "atm_advance_acoustic_step_work"),
     (r"k_div_damp", "atm_divergence_damping_3d"),
     (r"k_solve_", "atm_compute_solve_diagnostics"),
-    (r"k_finish_", "atm_rk_dynamics_substep_finish"),
+    (r"k_finish_|k_finish64", "atm_rk_dynamics_substep_finish"),
     (r"k_recover_", "atm_recover_large_step_variables_work"),
     (r"k_tr_", "atm_advance_scalars_mono"),
 ]
@@ -72,8 +72,10 @@ def read_trace(d):
 
 def write_factor(write, nCells, nEdges, L):
     """WRITE_SIZE KiB -> bytes factor, measured on the copy kernels of the setup task
-    (setup_cells writes 7 cell fields, setup_edges 2 edge fields, levels 0..L-1)"""
-    payload = {"k_setup_cells": 7 * nCells * 8 * L, "k_setup_edges": 2 * nEdges * 8 * L}
+    (setup_cells writes 7 cell fields, setup_edges 2 edge fields, levels 0..L-1; at LP 64
+    one k_copy64 launch writes both)"""
+    payload = {"k_setup_cells": 7 * nCells * 8 * L, "k_setup_edges": 2 * nEdges * 8 * L,
+               "k_copy64": (7 * nCells + 2 * nEdges) * 8 * L}
     f = [payload[k] / (write[k][0] / write[k][1] * 1024.0) for k in payload if k in write and write[k][0] > 0]
     return sum(f) / len(f) if f else None
 

@@ -65,7 +65,7 @@ def main():
     steps = None
     if a.trace:
         tr = read_trace(a.trace)
-        steps = tr.get("k_setup_cells", (None,))[0]
+        steps = tr.get("k_setup_cells", tr.get("k_copy64", (None,)))[0]
         for k, (calls, t) in tr.items():
             out["kernels"][k] = {"calls": calls, "avg_us": round(t / calls * 1e6, 2)}
             task = task_of(k)
@@ -74,11 +74,11 @@ def main():
                 tasks[task]["time_s"] += t
     fetch, nf = read_counter(a.fetch, "FETCH_SIZE") if a.fetch else ({}, {})
     write, nw = read_counter(a.write, "WRITE_SIZE") if a.write else ({}, {})
-    pmc_steps = nf.get("k_setup_cells") or nw.get("k_setup_cells")
+    pmc_steps = nf.get("k_setup_cells") or nw.get("k_setup_cells") or nf.get("k_copy64") or nw.get("k_copy64")
     # calibration on the copies: setup_cells reads 6 cell fields and writes 7 (rho_zz
     # twice), setup_edges reads and writes 2 edge fields
-    lines = {"k_setup_cells": 6 * nC * 4 * 128, "k_setup_edges": 2 * nE * 4 * 128}
-    payload = {"k_setup_cells": 7 * nC * 8 * L, "k_setup_edges": 2 * nE * 8 * L}
+    lines = {"k_setup_cells": 6 * nC * 4 * 128, "k_setup_edges": 2 * nE * 4 * 128, "k_copy64": (6 * nC + 2 * nE) * 4 * 128}
+    payload = {"k_setup_cells": 7 * nC * 8 * L, "k_setup_edges": 2 * nE * 8 * L, "k_copy64": (7 * nC + 2 * nE) * 8 * L}
     ff = [lines[k] / (fetch[k] / nf[k] * 1024.0) for k in lines if fetch.get(k)]
     wf = [payload[k] / (write[k] / nw[k] * 1024.0) for k in payload if write.get(k)]
     out["fetch_factor_doc"] = 2.0
