@@ -330,7 +330,8 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
             double scalar_weight = ac[j] + sg * ac3[j];
             flux_arr += scalar_weight * colk(fd(S, F_w), ad[j]);
         }
-        colk(fw(S, X_Fw), e) = (k > 0 && kl) ? flux_arr : 0.0;
+        // HF: the edge's whole horizontal w flux Hw = ru_edge_w flux_arr (E sums eocs Hw)
+        colk(fw(S, X_Fw), e) = (k > 0 && kl) ? (HF ? ru_edge_w * flux_arr : flux_arr) : 0.0;
     }
 
     // ---- tend_u (:987-1007)
@@ -700,14 +701,20 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     double w = wc;
     if constexpr (MD) {  // the horizontal w flux over every edge, then the area scaling
         double hw = 0.0;
+        if constexpr (HF) {  // B's per-edge Hw (fast path: reassociated)
 #pragma unroll
-        for (int i = 0; i < NF; i++) {
-            const double ru_edge_w = fzm * ru_[i] + fzp * lvl_dn<LP>(ru_[i], k);
-            hw = sub_if(i < ne && k > 0 && kl, hw, eocs_[i] * ru_edge_w * Fw_[i]);
-        }
-        for (int i = NF; i < ne; i++) {
-            const double ru_k = ldz(kl, colk(ru, eoc[i])), ru_edge_w = fzm * ru_k + fzp * lvl_dn<LP>(ru_k, k);
-            hw = sub_if(k > 0 && kl, hw, eocs[i] * ru_edge_w * colk(fd(S, X_Fw), eoc[i]));
+            for (int i = 0; i < NF; i++) hw = sub_if(i < ne && k > 0 && kl, hw, eocs_[i] * Fw_[i]);
+            for (int i = NF; i < ne; i++) hw = sub_if(k > 0 && kl, hw, eocs[i] * colk(fd(S, X_Fw), eoc[i]));
+        } else {
+#pragma unroll
+            for (int i = 0; i < NF; i++) {
+                const double ru_edge_w = fzm * ru_[i] + fzp * lvl_dn<LP>(ru_[i], k);
+                hw = sub_if(i < ne && k > 0 && kl, hw, eocs_[i] * ru_edge_w * Fw_[i]);
+            }
+            for (int i = NF; i < ne; i++) {
+                const double ru_k = ldz(kl, colk(ru, eoc[i])), ru_edge_w = fzm * ru_k + fzp * lvl_dn<LP>(ru_k, k);
+                hw = sub_if(k > 0 && kl, hw, eocs[i] * ru_edge_w * colk(fd(S, X_Fw), eoc[i]));
+            }
         }
         const double rz_m = lvl_dn<LP>(rho_zz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
         const double coslat = fd(S, X_cosLatCell)[c];
@@ -788,13 +795,17 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     if (k == L) wdtz = wdtzL;
     const double wdtz_p = lvl_up<LP>(wdtz, k);
     if constexpr (HF) {  // every lane stores (paired 16-B stores); level L keeps its value
-        tend_theta *= invA - rdzw * (wdtz_p - wdtz);  // :1422-1427, :1477-1479
+        // :1422-1427, :1477-1479 (MD: the MPAS-A form, Q14; its w stores are made above)
+        if (MD) tend_theta = tend_theta * invA - rdzw * (wdtz_p - wdtz);
+        else tend_theta *= invA - rdzw * (wdtz_p - wdtz);
         const double rth = tend_theta / rho_zz;
-        put2<LP>(fw(S, F_w), c, fw(S, F_tend_rtheta_adv), c, k, PADW(w), PADW(tend_theta), k != L, k != L);
+        if (MD && k != L) colk(fw(S, F_tend_rtheta_adv), c) = PADW(tend_theta);
+        if (!MD) put2<LP>(fw(S, F_w), c, fw(S, F_tend_rtheta_adv), c, k, PADW(w), PADW(tend_theta), k != L, k != L);
         tend_theta += rho_zz * rt_diab;
         tend_theta += tte + trp;
         put2<LP>(fw(S, F_rthdynten), c, fw(S, F_tend_theta), c, k, PADW(rth), PADW(tend_theta), k != L, k != L);
-        if (rk0) put2<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k, PADW(twe), PADW(tte), k != L, k != L);
+        if (rk0 && MD && k != L) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
+        if (rk0 && !MD) put2<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k, PADW(twe), PADW(tte), k != L, k != L);
         return;
     }
     if (k == L) return;  // (padding levels: zeros, PADW)
@@ -829,7 +840,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     const bool rk0 = a.rk_step == 0, del4 = rk0 && a.h4 > 0.0;
     // HF: the fast path's theta flux per edge formed in B (E sums eocs H; reassociated, so
     // exact mode keeps the reference's per-cell order)
-    const bool hf = !MD && !a.exact_q;
+    const bool hf = !a.exact_q;
     // kernel launches over the entities of a DevState range (HALO_RUN: interior /
     // boundary halves around a halo exchange, or all owned entities)
     auto kA = [&](const DevState& X) {
@@ -841,10 +852,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
-        if constexpr (MD) {
-            if (rk0) k_dyn_B<LP, true, MD, false><<<nb, 256, 0, st>>>(X, a);
-            else k_dyn_B<LP, false, MD, false><<<nb, 256, 0, st>>>(X, a);
-        } else if (hf) {
+        if (hf) {
             if (rk0) k_dyn_B<LP, true, MD, true><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_B<LP, false, MD, true><<<nb, 256, 0, st>>>(X, a);
         } else {
@@ -875,8 +883,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 else k_dyn_E<LP, false, false, MD, H><<<nb, 256, 0, st>>>(X, a);
             }
         };
-        if constexpr (MD) go(std::false_type{});
-        else if (hf) go(std::true_type{});
+        if (hf) go(std::true_type{});
         else go(std::false_type{});
     };
     // halo: fields each kernel gathers through an index array / fields it writes
@@ -899,14 +906,14 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
             HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
             HALO_WROTE(S, F_tend_u_euler, F_tend_u);
         }
-        if (hf) HALO_RUN(S, st, kE, X_F, F_delsq_w, F_delsq_theta);
+        if (hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta);  // (X_Fw: MD only written)
         else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
     } else {
         if (hf) HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_theta_m_save);
         else HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
         HALO_WROTE(S, X_F, F_tend_u);
         if (MD) HALO_WROTE(S, X_Fw);
-        if (hf) HALO_RUN(S, st, kE, X_F);
+        if (hf) HALO_RUN(S, st, kE, X_F, X_Fw);
         else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);
     }
     HALO_WROTE(S, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
