@@ -236,7 +236,7 @@ def measure_traffic(args):
         shutil.rmtree(tmp, ignore_errors=True)
     m_cells = args.ncells
     m_edges = 3 * (m_cells - 2)
-    wfac = pmc.write_factor(res["WRITE_SIZE"], m_cells, m_edges, args.levels)
+    wfac = pmc.write_factor(res["WRITE_SIZE"], m_cells, m_edges, args.levels, int(args.physics or 0))
     if wfac is None:
         return None, "WRITE_SIZE calibration kernels missing"
     by = pmc.bytes_per_step(res["FETCH_SIZE"], res["WRITE_SIZE"], 1, wfac)

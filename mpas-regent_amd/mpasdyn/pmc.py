@@ -70,12 +70,14 @@ def read_trace(d):
     return out
 
 
-def write_factor(write, nCells, nEdges, L):
+def write_factor(write, nCells, nEdges, L, physics=0):
     """WRITE_SIZE KiB -> bytes factor, measured on the copy kernels of the setup task
-    (setup_cells writes 7 cell fields, setup_edges 2 edge fields, levels 0..L-1; at LP 64
-    one k_copy64 launch writes both)"""
-    payload = {"k_setup_cells": 7 * nCells * 8 * L, "k_setup_edges": 2 * nEdges * 8 * L,
-               "k_copy64": (7 * nCells + 2 * nEdges) * 8 * L}
+    (setup_cells writes 7 cell fields -- 8 under the MPAS dynamics, which also saves
+    theta_m --, setup_edges 2 edge fields, levels 0..L-1; at LP 64 one k_copy64 launch
+    writes both)"""
+    nc = 8 if physics == 2 else 7
+    payload = {"k_setup_cells": nc * nCells * 8 * L, "k_setup_edges": 2 * nEdges * 8 * L,
+               "k_copy64": (nc * nCells + 2 * nEdges) * 8 * L}
     f = [payload[k] / (write[k][0] / write[k][1] * 1024.0) for k in payload if k in write and write[k][0] > 0]
     return sum(f) / len(f) if f else None
 
