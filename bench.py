@@ -58,10 +58,15 @@ NORTH_STAR = "atm_compute_dyn_tend_work"
 
 
 class Hip:
-    """the few HIP runtime calls the timing needs (events on the library's stream)"""
+    """the few HIP runtime calls the timing needs (events on the library's stream, device
+    synchronisation).  Bound after libmpasdyn is loaded, by its soname: the dynamic loader
+    then returns the HIP runtime the library already runs on (its RUNPATH's), never a
+    second one (INTEGRATION.md "One HIP runtime per process")."""
 
     def __init__(self):
-        self.h = ctypes.CDLL("libamdhip64.so")
+        from mpasdyn import lib
+        lib.load()
+        self.h = ctypes.CDLL("libamdhip64.so.7")
         self.h.hipEventCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
         self.h.hipEventRecord.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         self.h.hipEventSynchronize.argtypes = [ctypes.c_void_p]
@@ -74,6 +79,9 @@ class Hip:
 
     def record(self, e, stream):
         assert self.h.hipEventRecord(e, ctypes.c_void_p(stream)) == 0
+
+    def device_sync(self):
+        assert self.h.hipDeviceSynchronize() == 0
 
     def elapsed_ms(self, e0, e1):
         assert self.h.hipEventSynchronize(e1) == 0
@@ -173,11 +181,11 @@ def free_port():
 def spawn_ranks(n, argv):
     """start N rank processes of this script (no GPU touched here); rank 0 inherits
     stdout (the JSON line), the others write theirs to stderr.  Returns the exit code."""
-    port = free_port()
+    port, rdzv = free_port(), free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MPAS_RDZV_PORT=str(rdzv))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
                                       stdout=None if r == 0 else sys.stderr))
     rc = 0
@@ -348,9 +356,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    from mpasdyn.rendezvous import Rendezvous
     if args.dry_run:
+        # the launch environment plus one round of the host rendezvous (unique-id
+        # broadcast, max, barrier) -- with no GPU call and no torch
+        rv = Rendezvous(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1")) if world > 1 else None
+        uid = rv.bcast(b"uid-from-rank-0" if rank == 0 else None) if rv else b""
+        mx = rv.allreduce_max(float(rank)) if rv else 0.0
+        if rv:
+            rv.barrier()
+            rv.close()
         print(json.dumps({"rank": rank, "local_rank": local_rank, "world_size": world, "gpus": args.gpus,
-                          "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}"}),
+                          "master": f"{os.environ.get('MASTER_ADDR', '')}:{os.environ.get('MASTER_PORT', '')}",
+                          "bcast": uid.decode(), "max_rank": mx, "torch_loaded": "torch" in sys.modules}),
               flush=True)
         return 0
 
@@ -365,12 +383,9 @@ def main():
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    import torch
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", init_method="env://")
+    # ranks meet over a plain TCP rendezvous (mpasdyn/rendezvous.py): no torch in this
+    # process, so the one HIP runtime is the library's
+    rv = Rendezvous(rank, world, os.environ.get("MASTER_ADDR", "127.0.0.1")) if world > 1 else None
     from mpasdyn import lib, roofline
     from mpasdyn import tasks as T
 
@@ -386,12 +401,10 @@ def main():
         dims = (*dec.n_local(rank), L)
         ctx = lib.Context(*dims, device=local_rank)
         lib.setup_subdomain(ctx, dec, rank)
-        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(lib.rccl_unique_id()), dtype=torch.uint8))
-        if dist is not None:
-            dist.broadcast(uid, 0)
-        lib.halo_rccl(ctx, world, rank, uid.cpu().numpy().tobytes())
+        uid = lib.rccl_unique_id() if rank == 0 else None
+        if rv is not None:
+            uid = rv.bcast(uid)
+        lib.halo_rccl(ctx, world, rank, uid)
         overlap = int(os.environ.get("MPAS_OVERLAP", "1"))
         ctx.set_option("overlap", overlap)
         own = dec.n_owned(rank)
@@ -421,27 +434,31 @@ def main():
     ctx.sync()
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if rv is not None:
+            rv.barrier()
 
-    e0, e1 = hip.event(), hip.event()
+    # K timed steps, bracketed by barrier + device synchronisation on both sides; one HIP
+    # event between consecutive steps on the task stream gives the per-step device times
+    # (the median step), the wall clock the whole region
+    evs = [hip.event() for _ in range(args.steps + 1)]
     barrier()
-    torch.cuda.synchronize()
+    hip.device_sync()
     t0 = time.perf_counter()
-    hip.record(e0, stream)
-    for _ in range(args.steps):
+    hip.record(evs[0], stream)
+    for i in range(args.steps):
         T.atm_srk3(ctx, dt, 1)
-    hip.record(e1, stream)
+        hip.record(evs[i + 1], stream)
     ctx.sync()
-    torch.cuda.synchronize()
+    hip.device_sync()
     barrier()
     t_wall = time.perf_counter() - t0
-    ev_ms = hip.elapsed_ms(e0, e1)
-    ms_step = max(t_wall * 1000.0, ev_ms) / args.steps
-    if dist is not None:
-        t = torch.tensor([ms_step], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        ms_step = float(t.item())
+    step_ms = [hip.elapsed_ms(evs[i], evs[i + 1]) for i in range(args.steps)]
+    ms_median = statistics.median(step_ms)
+    ms_mean = max(t_wall * 1000.0, sum(step_ms)) / args.steps
+    if rv is not None:  # the slowest rank sets the job's step time
+        ms_median = rv.allreduce_max(ms_median)
+        ms_mean = rv.allreduce_max(ms_mean)
+    ms_step = ms_median
 
     # per-task device times (HIP events bracketing every task on the task stream)
     ctx.timing(True)
@@ -483,7 +500,10 @@ def main():
         halo_info["exchanges_per_step"] = round(ex / (args.warmup + args.steps + n_prof), 2)
         halo_info["fields_per_step"] = round(fl / (args.warmup + args.steps + n_prof), 2)
     out = {"metric": METRIC, "value": round(value, 3), "unit": "Mcell-columns/s", "n_gpus": world,
-           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 4),
+           "ms_per_step_stat": f"median of {args.steps} per-step HIP-event times on the task stream, max over ranks "
+                               f"(SURVEY §8.5)", "ms_per_step_mean": round(ms_mean, 4),
+           "ms_per_step_min_max": [round(min(step_ms), 4), round(max(step_ms), 4)], "higher_is_better": True,
            "scaling": "strong" if decomposed else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
            "config": {"workload": f"x1.{ncells} x {L} levels, atm_srk3 (3 dyn_tend rk 0/1/2, " +
                                   ({1: "4 acoustic substeps + recover (MPAS vertical solver)",
@@ -500,16 +520,23 @@ def main():
     if halo_info:
         out["halo"] = halo_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count())))
+        # all the host cores this process may use: the OMP_NUM_THREADS pin when the
+        # environment sets one (the GPU box pins 16, its CPU share per GPU), else nproc
+        pin = os.environ.get("OMP_NUM_THREADS")
+        threads = int(pin) if pin else (len(os.sched_getaffinity(0)) or os.cpu_count())
+        if not pin:
+            os.environ["OMP_NUM_THREADS"] = str(threads)
         out["cpu_baseline"] = cpu_baseline(ncells, L, dt, threads, args.physics, args.transport, args.cpu_budget)
+        out["cpu_baseline"]["threads_from"] = "OMP_NUM_THREADS (environment pin)" if pin else "sched_getaffinity"
     elif rank == 0:
         out["cpu_baseline"] = None
+    if rv is not None:
+        rv.barrier()
     ctx.close()
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
+    if rv is not None:
+        rv.close()
     return 0
 
 

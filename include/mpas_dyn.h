@@ -178,7 +178,9 @@ int mpas_atm_init_coupled_diagnostics(mpas_ctx* ctx);
  * reference leaves undefined as oracle/mpas_oracle.c states them; a decomposed context
  * computes its owned entities, its ghosts keep the uploaded values):
  * :46  atm_compute_signs(cr, er, vr) (atm_core.rg:22): edgesOnVertexSign, edgesOnCellSign,
- *       kiteForCell, and zb_cell / zb3_cell copied from the never-written er.zb / zb3 (0.0) */
+ *       kiteForCell; zb_cell / zb3_cell (:88-110, the copy of er.zb / zb3 that
+ *       init_atm_case_jw writes) stay as uploaded: the state keeps no er.zb, the host that
+ *       builds the initial state uploads the copy (mpasdyn/jw.py) */
 int mpas_atm_compute_signs(mpas_ctx* ctx);
 /* :133 atm_adv_coef_compression(cr, er) (atm_core.rg:24): advCellsForEdge,
  *       nAdvCellsForEdge (the index of the list's last cell, :184), adv_coefs and

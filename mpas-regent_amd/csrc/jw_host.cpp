@@ -6,6 +6,8 @@
 // jw.py's, in its evaluation order.
 #include <cmath>
 #include <cstdint>
+#include <new>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -61,21 +63,36 @@ extern "C" int mpas_jw_hydrostatic(int32_t nCells, int32_t nVertLevels, const do
                                    const double* rb, const double* zz, const double* dzw, const double* dzu,
                                    const double* fzm, const double* fzp, double* pressure_p, double* rho_p,
                                    double* temperature, int32_t nthreads) {
-    if (nCells < 0 || nVertLevels < 3 || !latCell || !pb || !rb || !zz || !dzw || !dzu || !fzm || !fzp ||
+    if (nCells < 0 || nVertLevels < 2 || !latCell || !pb || !rb || !zz || !dzw || !dzu || !fzm || !fzp ||
         !pressure_p || !rho_p || !temperature)
         return MPAS_EINVAL;
     int nt = nthreads > 0 ? nthreads : (int)std::thread::hardware_concurrency();
     if (nt < 1) nt = 1;
     if (nt > 64) nt = 64;
     if (nt > nCells) nt = nCells > 0 ? nCells : 1;
-    std::vector<std::thread> th;
-    const int per = (nCells + nt - 1) / nt;
-    for (int i = 0; i < nt; i++) {
-        const int c0 = i * per, c1 = std::min(nCells, c0 + per);
-        if (c0 >= c1) break;
-        th.emplace_back(columns, c0, c1, (int)nVertLevels, latCell, pb, rb, zz, dzw, dzu, fzm, fzp, pressure_p, rho_p,
+    // (the recurrence reads levels 0 and 1: nVertLevels >= 2.)  No exception crosses the C
+    // ABI: a thread that cannot be started leaves its columns to this thread, and an
+    // allocation failure is reported as MPAS_ENOMEM.
+    try {
+        std::vector<std::thread> th;
+        th.reserve(nt);  // (emplace_back never reallocates past started threads)
+        const int per = (nCells + nt - 1) / nt;
+        for (int i = 0; i < nt; i++) {
+            const int c0 = i * per, c1 = std::min(nCells, c0 + per);
+            if (c0 >= c1) break;
+            try {
+                th.emplace_back(columns, c0, c1, (int)nVertLevels, latCell, pb, rb, zz, dzw, dzu, fzm, fzp, pressure_p,
+                                rho_p, temperature);
+            } catch (const std::system_error&) {
+                columns(c0, c1, (int)nVertLevels, latCell, pb, rb, zz, dzw, dzu, fzm, fzp, pressure_p, rho_p,
                         temperature);
+            }
+        }
+        for (auto& t : th) t.join();
+    } catch (const std::bad_alloc&) {
+        return MPAS_ENOMEM;
+    } catch (...) {
+        return MPAS_EINVAL;
     }
-    for (auto& t : th) t.join();
     return MPAS_OK;
 }

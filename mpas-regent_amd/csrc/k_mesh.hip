@@ -39,7 +39,7 @@ __global__ __launch_bounds__(256) void k_signs_cells(DevState S) {
     if (c >= S.nCO) return;
     const int *eoc = fi(S, F_edgesOnCell), *coe = fi(S, F_cellsOnEdge), *voc = fi(S, F_verticesOnCell),
               *cov = fi(S, F_cellsOnVertex);
-    double *sgn = fw(S, F_edgesOnCellSign), *zb = fw(S, F_zb_cell), *zb3 = fw(S, F_zb3_cell);
+    double* sgn = fw(S, F_edgesOnCellSign);
     int* kite = (int*)S.f[F_kiteForCell];
     int ne = fi(S, F_nEdgesOnCell)[c];
     if (ne > kMaxEdges) ne = kMaxEdges;
@@ -48,15 +48,10 @@ __global__ __launch_bounds__(256) void k_signs_cells(DevState S) {
         const int e = eoc[r + i];
         sgn[r + i] = e <= S.nEdges ? (c == coe[(size_t)e * 2] ? 1.0 : -1.0) : 0.0;
     }
-    // :89-112: zb_cell / zb3_cell copy er.zb / er.zb3 of the cell's edge at every level
-    // 0..nVertLevels; no task writes er.zb (Q2), so the copy is 0.0
-    for (int i = 0; i < ne; i++)
-        if (eoc[r + i] <= S.nEdges)
-            for (int k = 0; k <= S.L; k++) {
-                const size_t p = (r + i) * LP + lpos(LP, k);
-                zb[p] = 0.0;
-                zb3[p] = 0.0;
-            }
+    // :88-110: zb_cell / zb3_cell = er.zb / er.zb3 of the cell's edge (component 0 or 1 by
+    // the cell's side), written by init_atm_case_jw (init_atm_cases.rg:657-660).  The port
+    // keeps no er.zb: the host that builds the initial state does that copy when it
+    // uploads zb_cell / zb3_cell (mpasdyn/jw.py), so the device task leaves them as uploaded
     for (int i = 0; i < ne; i++) {  // :115-128 (no match: the value stays)
         const int iVtx = voc[r + i];
         if (iVtx <= S.nVertices) {
@@ -76,7 +71,6 @@ static hipError_t signs_lp(const DevState& S, hipStream_t st) {
     const int nv = S.nVO - S.lo[KV], nc = S.nCO - S.lo[KC];
     if (nv > 0) k_signs_vertices<<<(nv + 255) / 256, 256, 0, st>>>(S);
     if (nc > 0) k_signs_cells<LP><<<(nc + 255) / 256, 256, 0, st>>>(S);
-    HALO_WROTE(S, F_zb_cell, F_zb3_cell);
     return hipGetLastError();
 }
 hipError_t launch_compute_signs(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, signs_lp, S, st); }

@@ -385,7 +385,7 @@ static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts, int 
     const bool r1 = S.halo && S.ring1 && S.nERing >= S.nEO && S.physics == 0;
     auto run1 = [&](const DevState& X) {
         DevState Y = X;
-        if (X.nEO == S.nEO) Y.nEO = S.nERing;
+        if (!X.interior) Y.nEO = S.nERing;  // the launch after the exchange (whole or boundary)
         run(Y);
     };
     if (r1) {

@@ -218,7 +218,7 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
     const bool r1 = S.halo && S.ring1 && S.nVRing >= S.nVO;
     auto kvc1 = [&](const DevState& X) {
         DevState Y = X;
-        if (X.nVO == S.nVO) Y.nVO = S.nVRing;
+        if (!X.interior) Y.nVO = S.nVRing;  // the launch after the exchange (whole or boundary)
         kvc(Y);
     };
     if (r1) {

@@ -93,6 +93,8 @@ struct DevState {
                         // grid (= the counts above unless the mesh is decomposed)
     int lo[3];          // first cell / edge / vertex of a launch: kernels compute entities
                         // [lo, nXO); 0 except for the boundary launch of a halo overlap
+    int interior;  // 1 on the interior launch of a halo overlap (Halo::launch: ghosts not
+                   // yet fresh), 0 on a whole-range or boundary launch
     int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
     int vcmix;  // 1: the vertex and cell blocks of mixed grids interleaved in proportion (vc_block)
     int tro;      // transport slot order (k_transport.hip tr_slot): 0 entity-major, 1 pair-major

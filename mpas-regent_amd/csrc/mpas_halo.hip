@@ -156,6 +156,7 @@ hipError_t Halo::launch(const DevState& S, hipStream_t st, std::initializer_list
     in.nCO = nint[0];
     in.nEO = nint[1];
     in.nVO = nint[2];
+    in.interior = 1;
     fn(in);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(comm, ev_ready, 0)) != hipSuccess) return e;

@@ -61,7 +61,7 @@ def compute_signs(m, st):
     valid = i < m.nEdgesOnCell[:, None]
     s = np.where(eoc <= nE, np.where(np.arange(nC)[:, None] == coe[np.minimum(eoc, nE), 0], 1.0, -1.0), 0.0)
     st["edgesOnCellSign"][:nC] = np.where(valid, s, 0.0)
-    # zb_cell / zb3_cell copy er.zb/zb3, which are never written (Q2): zero
+    # zb_cell / zb3_cell (:88-110) copy er.zb / zb3 of the initial state: left as built
     cov = np.zeros((nV + 1, 3), np.int64)
     cov[:nV] = m.cellsOnVertex
     voc = m.verticesOnCell.astype(np.int64)

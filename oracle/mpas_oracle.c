@@ -1224,13 +1224,14 @@ void ora_atm_compute_damping_coefs(ora_state* S, double config_zd, double config
 #define MAXEDGES 10
 #define VERTEXDEGREE 3
 
-/* atm_compute_signs, dynamics_tasks.rg:46-130.  zb_cell / zb3_cell copy er.zb / er.zb3,
- * which no task writes (Q2): 0.0.  kiteForCell keeps its value when no cellsOnVertex(j),
+/* atm_compute_signs, dynamics_tasks.rg:46-130.  zb_cell / zb3_cell copy er.zb / er.zb3
+ * (:88-110), which init_atm_case_jw writes (init_atm_cases.rg:657-660); the state keeps no
+ * er.zb, the host that builds the initial state uploads the copy, so they stay as given.  kiteForCell keeps its value when no cellsOnVertex(j),
  * j = 1..vertexDegree-1, matches (the loop breaks only on a match). */
 void ora_atm_compute_signs(ora_state* S) {
     const int nC = S->nCells, nE = S->nEdges, nV = S->nVertices, L = S->L;
     int32_t *eov = I(edgesOnVertex), *eoc = I(edgesOnCell), *voc = I(verticesOnCell), *kite = I(kiteForCell);
-    double *eovs = D(edgesOnVertexSign), *eocs = D(edgesOnCellSign), *zb = D(zb_cell), *zb3 = D(zb3_cell);
+    double *eovs = D(edgesOnVertexSign), *eocs = D(edgesOnCellSign);
 #pragma omp parallel for schedule(static)
     for (long v = 0; v < nV; v++)
         for (int i = 0; i < VERTEXDEGREE; i++) {
@@ -1247,12 +1248,6 @@ void ora_atm_compute_signs(ora_state* S) {
             if (e <= nE) eocs[c * MAXEDGES + i] = (c == ie2(S, I(cellsOnEdge), e, 2, 0)) ? 1.0 : -1.0;
             else eocs[c * MAXEDGES + i] = 0.0;
         }
-        for (int k = 0; k <= L; k++)
-            for (int i = 0; i < ne; i++)
-                if (eoc[c * MAXEDGES + i] <= nE) {
-                    zb[(c * LV + k) * MAXEDGES + i] = 0.0;
-                    zb3[(c * LV + k) * MAXEDGES + i] = 0.0;
-                }
         for (int i = 0; i < ne; i++) {
             const int iVtx = voc[c * MAXEDGES + i];
             if (iVtx <= nV) {

@@ -74,3 +74,49 @@ def test_task_table_aggregates_variants():
     assert abs(ac["b_alg_GB_per_step"] - (3 * a0 + 4 * a1) / 1e9) < 1e-3
     # the task with the most device time per step is dyn_tend, not the 7-launch acoustic task
     assert max(t, key=lambda k: t[k]["ms_per_step"]) == "atm_compute_dyn_tend_work"
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_rendezvous_without_torch(n):
+    """--dry-run runs one round of the host rendezvous (mpasdyn/rendezvous.py): rank 0's
+    unique-id bytes reach every rank, the max over ranks is world - 1 everywhere, and no
+    rank imported torch (the bench's process holds one HIP runtime, the library's)"""
+    p = _run(["--gpus", str(n), "--dry-run"])
+    assert p.returncode == 0, p.stderr
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.strip()]
+    lines += [json.loads(x) for x in p.stderr.splitlines() if x.startswith("{")]
+    assert len(lines) == n
+    assert all(d["bcast"] == "uid-from-rank-0" and d["max_rank"] == n - 1 for d in lines)
+    assert not any(d["torch_loaded"] for d in lines)
+
+
+def test_single_rank_dry_run_without_torch():
+    p = _run(["--dry-run"])
+    assert p.returncode == 0 and json.loads(p.stdout.strip())["torch_loaded"] is False
+
+
+def test_rendezvous_in_threads():
+    """the rendezvous' collectives at world 4, ranks as threads of one process"""
+    import threading
+    from mpasdyn.rendezvous import Rendezvous
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = {}
+
+    def rank(r):
+        rv = Rendezvous(r, 4, "127.0.0.1", port, timeout=30)
+        b = rv.bcast(b"\x01\x02" * 64 if r == 0 else None)
+        m = rv.allreduce_max(10.0 * r - r * r)  # max at r = 3 (21), not at the last rank
+        rv.barrier()
+        rv.close()
+        out[r] = (b, m)
+    th = [threading.Thread(target=rank, args=(r,)) for r in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(60)
+    assert sorted(out) == [0, 1, 2, 3]
+    assert all(b == b"\x01\x02" * 64 and m == 21.0 for b, m in out.values())

@@ -208,3 +208,23 @@ def test_ring1_redundancy_saves_exchanges(x1_2562):
     assert not bad, bad[:6]
     for s1, s0 in zip(out[1][1], out[0][1]):  # (the first substep's ru_p is fresh from the upload)
         assert s0[0] - s1[0] == 6 + 3, (s0, s1)
+
+
+def test_ring1_rank_without_boundary_edges(x1_2562):
+    """a rank that owns no edge (one cell none of whose edges has it as cellsOnEdge(0);
+    mpas-mode ids): its interior edge range equals its owned one (both empty) while it has
+    ring-1 ghost edges.  Only the launch after the exchange may extend the damping over the
+    ring-1 edges -- extending the interior launch too applied the increment twice"""
+    st = state(x1_2562, 5, "mpas0")
+    coe = st["cellsOnEdge"][:st.nEdges]
+    owners = np.zeros(st.nCells, dtype=np.int64)
+    np.add.at(owners, coe[:, 0], 1)
+    lone = int(np.nonzero(owners == 0)[0][0])
+    part = np.zeros(st.nCells, dtype=np.int32)
+    part[lone] = 1
+    d = decomp.Decomposition(st, 2, cell_part=part)
+    assert d.n_owned(1)[1] == 0 and d.n_interior(1)[1] == 0 and d.n_ring1(1)[0] > 0
+    ref = run_single(st, lambda c: T.atm_srk3(c, 720.0, 1), 1)
+    got, _ = run_decomposed(st, 2, lambda c: T.atm_srk3(c, 720.0, 1), 1, cell_part=part, overlap=1)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]

@@ -47,3 +47,28 @@ def test_driver_end_to_end(x1_2562, tmp_path):
     assert np.array_equal(u, st["u"][:st.nEdges, 0])  # level 0 (the jet peaks aloft)
     assert 34.0 < np.abs(st["u"][:st.nEdges, :26]).max() <= 35.0  # u unchanged by the steps (Q7)
     assert np.allclose(rho, st["rho_zz"][:st.nCells, 0] * st["zz"][:st.nCells, 0], rtol=1e-15)
+
+
+def test_core_init_keeps_jw_terrain_coefficients(x1_2562):
+    """main.rg:57-61 order: the JW state (with its terrain-slope zb_cell / zb3_cell, the copy
+    of er.zb that init_atm_case_jw writes, init_atm_cases.rg:657-660) is uploaded, then
+    atm_core_init runs: atm_compute_signs must not erase zb_cell, and only
+    atm_couple_coef_3rd_order scales zb3_cell at level 0 (:319-323)"""
+    st = jw.jw_state(M.zero_based(x1_2562), 26)
+    nC = st.nCells
+    assert np.abs(st["zb_cell"][:nC]).max() > 0.0
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.upload(st)
+        T.atm_compute_signs(ctx)
+        ctx.sync()
+        ctx.download(got, names=["zb_cell", "zb3_cell"])
+        assert np.array_equal(got["zb_cell"], st["zb_cell"]) and np.array_equal(got["zb3_cell"], st["zb3_cell"])
+        T.atm_core_init(ctx)
+        ctx.sync()
+        ctx.download(got, names=["zb_cell", "zb3_cell"])
+    assert np.array_equal(got["zb_cell"], st["zb_cell"])
+    assert np.array_equal(got["zb3_cell"][:, 1:], st["zb3_cell"][:, 1:])
+    ref = st.copy()
+    O.Oracle(ref).atm_couple_coef_3rd_order(0.25)
+    assert np.array_equal(got["zb3_cell"][:nC, 0], ref["zb3_cell"][:nC, 0])

@@ -49,7 +49,9 @@ def test_mesh_tasks_match_build_state(x1_2562, ids):
 def test_mesh_tasks_quirks(x1_2562):
     """the literal list construction: nAdvCellsForEdge = n is the index of the last cell
     (:184), so that cell is never weighted; deriv_two (never initialised, Q2) feeds the
-    3rd/4th-order weights when given; zb_cell / zb3_cell copy the never-written er.zb (0)"""
+    3rd/4th-order weights when given; zb_cell / zb3_cell (the copy of er.zb that
+    init_atm_case_jw writes, init_atm_cases.rg:657-660, done by the host that uploads them)
+    stay as given -- only couple_coef_3rd_order scales zb3_cell at level 0"""
     m, st = _state(x1_2562, "zero_based")
     nE, nC = st.nEdges, st.nCells
     st["deriv_two"][:nE] = np.random.default_rng(3).standard_normal((nE, 30))
@@ -67,9 +69,7 @@ def test_mesh_tasks_quirks(x1_2562):
     # only entries 0..n-1 are stored (:185-187): the list's last cell is dropped
     assert (st["advCellsForEdge"][np.arange(nE), n] == 0).all()
     ne = st["nEdgesOnCell"][:nC, 0]
-    zb = st["zb_cell"][:nC]  # (nC, L+1, 10): 0 where i < nEdgesOnCell, 1 elsewhere
-    used = np.arange(10)[None, None, :] < ne[:, None, None]
-    assert (zb[np.broadcast_to(used, zb.shape)] == 0.0).all() and (zb[~np.broadcast_to(used, zb.shape)] == 1.0).all()
+    assert (st["zb_cell"][:nC] == 1.0).all()  # as uploaded
     # couple_coef_3rd_order scales zb3_cell at level 0 only (:319-323)
-    assert (st["zb3_cell"][:nC, 1:][~np.broadcast_to(used, zb.shape)[:, 1:]] == 1.0).all()
-    assert (st["zb3_cell"][:nC, 0][~used[:, 0]] == 0.25).all()
+    assert (st["zb3_cell"][:nC, 1:] == 1.0).all()
+    assert (st["zb3_cell"][:nC, 0] == 0.25).all()

@@ -57,3 +57,25 @@ def test_needs_zero_based_mesh(x1_2562):
     st = bs.build_state(x1_2562, 5, "physical", vertical=False)
     with pytest.raises(ValueError):
         jw.init_atm_case_jw(x1_2562, st)
+
+
+@pytest.mark.parametrize("L", [2, 3, 26])
+def test_hydrostatic_library_matches_numpy(L, monkeypatch):
+    """mpas_jw_hydrostatic (host threads in libmpasdyn) and the NumPy statement agree down to
+    2 levels (the recurrence reads levels 0 and 1).  Tolerance 1e-14 relative:
+    NumPy's vectorised pow/sin may differ from glibc's in the last ulp."""
+    from mpasdyn import lib
+    rng = np.random.default_rng(7)
+    nC = 97
+    g = jw.vertical_grid(max(L, 3))
+    g = {k: (v[:L + 1] if isinstance(v, np.ndarray) else v) for k, v in g.items()}
+    phi = rng.uniform(-1.5, 1.5, nC)
+    pb = -np.sort(-rng.uniform(3e4, 1e5, (nC, L)), axis=1)  # eta in (0.3, 1], decreasing upward
+    rb = rng.uniform(0.3, 1.2, (nC, L))
+    zz = rng.uniform(0.9, 1.1, (nC, L))
+    got = jw._hydrostatic(phi, pb, rb, zz, g, L)
+    monkeypatch.setattr(lib, "load", lambda: (_ for _ in ()).throw(OSError("numpy path")))
+    want = jw._hydrostatic(phi, pb, rb, zz, g, L)
+    for a, b in zip(got, want):
+        assert np.isfinite(b).all()
+        assert np.abs(a - b).max() <= 1e-14 * np.abs(b).max()
