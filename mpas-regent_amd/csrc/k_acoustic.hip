@@ -17,6 +17,8 @@
 #include "mpas_dev.h"
 #include "mpas_halo.h"
 
+#include <type_traits>
+
 namespace mpas {
 
 // FIRST: small_step == 0, where rho_pp, rtheta_pp, rw_p and wwAvg start from 0 (:1615-1636):
@@ -29,10 +31,44 @@ namespace mpas {
 // linear recurrences: an affine prefix scan over the wavefront, upward then downward
 // (EXACT: level by level in the reference's order).  The ru_p update (Q18) runs before,
 // in k_acoustic_ru.
-template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV>
-__global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm) {
-    ColMap<LP> m(S, KC);
-    const int L = S.L, k = m.k, c = m.ent;
+//
+// MODE (reference semantics, no halo, option "fusedamp"; launch_acoustic): 0 plain; 1 also
+// stores this substep's div = -(rtheta_pp - rtheta_pp_old) (:1755) per cell in X_dvA; 2
+// also applies the PREVIOUS substep's atm_divergence_damping_3d (:1742-1762, coefficient
+// coef_prev, its div in X_dvB) to every ru_p it reads -- the same expression on the same
+// values as the damping kernel, so the same bits -- and writes the damped ru_p of the
+// edges this cell owns (X_eown; the lowest (cell, slot) listing an edge) to X_rupB, all
+// levels (level L copied, padding 0); the edges no cell lists are written by ncb.. extra
+// blocks (X_orph).  The damping launch between two substeps disappears: its ru_p
+// read-modify-write and its cell gathers (theta_m is gathered here anyway).
+template <int LP>
+__device__ __forceinline__ double damp_edge(double rup, double d1, double d2, double t1, double t2, double spec,
+                                            double coef, bool on) {
+    return on ? rup + coef * (d2 - d1) * (1.0 - spec) / (t1 + t2) : rup;  // (:1757-1759 order)
+}
+
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE>
+__global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm,
+                                                 double coefp, int ncb) {
+    static_assert(!(MPASV && MODE), "the deferred damping is the reference semantics' (physics 0)");
+    const int L = S.L, k = (int)(threadIdx.x % LP);
+    int blk = (int)blockIdx.x;
+    if constexpr (MODE == 2) {
+        if (blk >= ncb) {  // an edge no cell lists: the damping alone, into the new buffer
+            const int j = col_of<LP>(blk - ncb);
+            if (j >= S.n_orph) return;
+            const int e = fi(S, X_orph)[j];
+            const int c1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], c2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+            const double *dvi = fd(S, X_dvB), *tmf = fd(S, F_theta_m);
+            const double ru = colk(fd(S, F_ru_p), e), d1 = colk(dvi, c1), d2 = colk(dvi, c2);
+            const double t1 = colk(tmf, c1), t2 = colk(tmf, c2);
+            const bool on = k < L && !(fi(S, F_isShared)[c1] && fi(S, F_isShared)[c2]);
+            colk(fw(S, X_rupB), e) = PADW(damp_edge<LP>(ru, d1, d2, t1, t2, fd(S, F_specZoneMaskEdge)[e], coefp, on));
+            return;
+        }
+    }
+    blk = xcd_block_n(S.xcd, blk, MODE == 2 ? ncb : (int)gridDim.x);
+    const int c = col_of<LP>(blk) + S.lo[KC];
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + lpos(LP, k);
     double* rtp_f = fw(S, F_rtheta_pp);
@@ -70,6 +106,26 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         gather2s<LP>(ru_p, e_[i], e_[i + 1], k, rup_[i], rup_[i + 1]);
         cell_pair2<LP, SELF>(tm_f, c1_, c2_, o_, s1_, tm, i, k, t1_[i], t2_[i], t1_[i + 1], t2_[i + 1]);
     }
+    int own = 0;
+    if constexpr (MODE == 2) {  // the previous substep's damping on this cell's edges
+        const double* dvi = fd(S, X_dvB);
+        const int* sh = fi(S, F_isShared);
+        const double* spz = fd(S, F_specZoneMaskEdge);
+        own = fi(S, X_eown)[c];
+        const double dv_c = SELF ? colk(dvi, c) : 0.0;
+        double d1_[NF], d2_[NF];
+#pragma unroll
+        for (int i = 0; i < NF; i += 2)
+            cell_pair2<LP, SELF>(dvi, c1_, c2_, o_, s1_, dv_c, i, k, d1_[i], d2_[i], d1_[i + 1], d2_[i + 1]);
+        double* rup_out = fw(S, X_rupB);
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const int x1 = SELF ? (s1_[i] ? c : o_[i]) : c1_[i], x2 = SELF ? (s1_[i] ? o_[i] : c) : c2_[i];
+            const bool on = kl && e_[i] < S.nEdges && !(sh[x1] && sh[x2]);
+            rup_[i] = damp_edge<LP>(rup_[i], d1_[i], d2_[i], t1_[i], t2_[i], spz[e_[i]], coefp, on);
+            if ((own >> i) & 1) colk(rup_out, e_[i]) = PADW(rup_[i]);  // (level L: the value read)
+        }
+    }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         rup_[i] = ldz(kl, rup_[i]);
@@ -92,7 +148,12 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
 
     // :1615-1636
-    if (k != L) colk(fw(S, F_rtheta_pp_old), c) = PADW((small_step == 0) ? 0 : rtp);  // (PADW: mpas_dev.h)
+    const double rtpo = (small_step == 0) ? 0 : rtp;
+    if (k != L) colk(fw(S, F_rtheta_pp_old), c) = PADW(rtpo);  // (PADW: mpas_dev.h)
+    // MODE 1/2: this substep's div (:1755) for the damping applied by the next substep
+    auto store_div = [&](double rtp_new) {
+        if constexpr (MODE != 0) colk(fw(S, X_dvA), c) = kl ? -(rtp_new - rtpo) : 0.0;
+    };
     if (small_step == 0) {
         ww = 0;
         rwp = 0;
@@ -115,6 +176,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         }
         colk(rwp_f, c) = PADW(rwp);
         colk(ww_f, c) = PADW(ww);
+        store_div(rtp);
         return;
     }
 
@@ -127,7 +189,15 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         ts = sub_if(i < ne && kl, ts, flux * 0.5 * (t2_[i] + t1_[i]));
     }
     for (int i = NF; i < ne; i++) {
-        double flux = sgn[i] * dts * cdv[i] * ldz(kl, colk(ru_p, eoc[i])) * invA;
+        double rpe = colk(ru_p, eoc[i]);
+        if constexpr (MODE == 2) {
+            const int e = eoc[i], x1 = cc1[i], x2 = cc2[i];
+            const bool on = kl && e < S.nEdges && !(fi(S, F_isShared)[x1] && fi(S, F_isShared)[x2]);
+            rpe = damp_edge<LP>(rpe, colk(fd(S, X_dvB), x1), colk(fd(S, X_dvB), x2), colk(tm_f, x1), colk(tm_f, x2),
+                                fd(S, F_specZoneMaskEdge)[e], coefp, on);
+            if ((own >> i) & 1) colk(fw(S, X_rupB), e) = PADW(rpe);
+        }
+        double flux = sgn[i] * dts * cdv[i] * ldz(kl, rpe) * invA;
         rs = sub_if(kl, rs, flux);
         ts = sub_if(kl, ts, flux * 0.5 * (ldz(kl, colk(tm_f, cc2[i])) + ldz(kl, colk(tm_f, cc1[i]))));
     }
@@ -267,9 +337,10 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     }
     if (k < L && k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
     // (paired 16-B stores, every lane; level L of rho_pp / rtheta_pp keeps its value)
-    put2<LP>(rpp_f, c, rtp_f, c, k, PADW(rs - cofrz * (rwp_p - x)), PADW(ts - rdzw * (coftz_p * rwp_p - coftz * x)),
-             k != L, k != L);
+    const double rtp_new = ts - rdzw * (coftz_p * rwp_p - coftz * x);
+    put2<LP>(rpp_f, c, rtp_f, c, k, PADW(rs - cofrz * (rwp_p - x)), PADW(rtp_new), k != L, k != L);
     put2<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww), true, true);
+    store_div(rtp_new);
 }
 
 // :1581-1613 restored (Q18, MPAS vertical solver only): ru_p and ruAvg of every owned
@@ -306,9 +377,11 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
 }
 
 template <int LP>
-static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {
+static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
+                              double coef_prev) {
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
+    if (mode && (S.physics || S.halo)) return hipErrorInvalidValue;  // (srk3 never asks: reference semantics only)
     if (S.physics) {  // Q18: the edges first
         const double rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
         auto ru = [&](const DevState& X) {
@@ -319,27 +392,42 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
         HALO_WROTE(S, F_ru_p, F_ruAvg);
     }
     auto run = [&](const DevState& X) {
-        const int grid = col_blocks<LP>(X, KC);
-        if (!grid) return;
-#define MPAS_ACOUSTIC(E, SF, F, M) k_acoustic<LP, E, SF, F, M><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm)
-#define MPAS_ACOUSTIC_M(E, SF, F) (X.physics ? MPAS_ACOUSTIC(E, SF, F, true) : MPAS_ACOUSTIC(E, SF, F, false))
+        const int ncb = col_blocks<LP>(X, KC);
+        if (!ncb) return;
+        const int grid = ncb + (mode == 2 ? (S.n_orph + 256 / LP - 1) / (256 / LP) : 0);
         const bool first = small_step == 0;
-        if (exact) {
-            if (X.selfc) first ? MPAS_ACOUSTIC_M(true, true, true) : MPAS_ACOUSTIC_M(true, true, false);
-            else first ? MPAS_ACOUSTIC_M(true, false, true) : MPAS_ACOUSTIC_M(true, false, false);
-        } else {
-            if (X.selfc) first ? MPAS_ACOUSTIC_M(false, true, true) : MPAS_ACOUSTIC_M(false, true, false);
-            else first ? MPAS_ACOUSTIC_M(false, false, true) : MPAS_ACOUSTIC_M(false, false, false);
-        }
-#undef MPAS_ACOUSTIC_M
-#undef MPAS_ACOUSTIC
+        auto go = [&](auto ex, auto sf, auto md) {
+            constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
+            constexpr int M = decltype(md)::value;
+            if constexpr (M == 0) {
+                if (X.physics) {
+                    if (first) k_acoustic<LP, E, SF, true, true, 0><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
+                    else k_acoustic<LP, E, SF, false, true, 0><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
+                    return;
+                }
+            }
+            if (first) k_acoustic<LP, E, SF, true, false, M><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
+            else k_acoustic<LP, E, SF, false, false, M><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
+        };
+        auto go_m = [&](auto ex, auto sf) {
+            if (mode == 1) go(ex, sf, std::integral_constant<int, 1>{});
+            else if (mode == 2) go(ex, sf, std::integral_constant<int, 2>{});
+            else go(ex, sf, std::integral_constant<int, 0>{});
+        };
+        auto go_s = [&](auto ex) {
+            if (X.selfc) go_m(ex, std::true_type{});
+            else go_m(ex, std::false_type{});
+        };
+        if (exact) go_s(std::true_type{});
+        else go_s(std::false_type{});
     };
     HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m);  // (ru_p at the edges of owned cells only)
     HALO_WROTE(S, F_rtheta_pp_old, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
     return hipGetLastError();
 }
-hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact) {
-    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact);
+hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
+                           double coef_prev) {
+    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev);
 }
 
 }  // namespace mpas

@@ -324,7 +324,9 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPA
 // OLD0: rtheta_pp_old is known to be 0.0 (srk3, right after the first acoustic substep
 // of a stage, which sets it so on every cell, :1615-1618): its columns are not read, and
 // -(r - 0.0) is the same value as the literal expression gives
-template <int LP, int EPW, bool OLD0>
+// DIVB (option fusedamp, the step's last damping): the cells' div = -(rtheta_pp -
+// rtheta_pp_old) comes from the acoustic step's X_dvB (the same subtraction, made there)
+template <int LP, int EPW, bool OLD0, bool DIVB = false>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
     ColMapN<LP, EPW> m(S, KE);
     const int L = S.L, k = m.k;
@@ -347,25 +349,44 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
     for (int i = 0; i < EPW; i++) {
         sh1[i] = sh[c1[i]];
         sh2[i] = sh[c2[i]];
-        gather2s<LP>(rtp, c1[i], c2[i], k, r1[i], r2[i]);
-        if (OLD0) ro1[i] = ro2[i] = 0.0;
-        else gather2s<LP>(rtpo, c1[i], c2[i], k, ro1[i], ro2[i]);
+        if (DIVB) {
+            gather2s<LP>(fd(S, X_dvB), c1[i], c2[i], k, r1[i], r2[i]);
+            ro1[i] = ro2[i] = 0.0;
+        } else {
+            gather2s<LP>(rtp, c1[i], c2[i], k, r1[i], r2[i]);
+            if (OLD0) ro1[i] = ro2[i] = 0.0;
+            else gather2s<LP>(rtpo, c1[i], c2[i], k, ro1[i], ro2[i]);
+        }
         gather2s<LP>(tm, c1[i], c2[i], k, t1[i], t2[i]);
     }
 #pragma unroll
     for (int i = 0; i < EPW; i++) {
         const int e = m.base + i;
         if (e >= S.nEO || k >= L || (sh1[i] && sh2[i])) continue;
-        double divCell1 = -(r1[i] - ro1[i]);
-        double divCell2 = -(r2[i] - ro2[i]);
+        double divCell1 = DIVB ? r1[i] : -(r1[i] - ro1[i]);
+        double divCell2 = DIVB ? r2[i] : -(r2[i] - ro2[i]);
         colk(rup, e) = ru[i] + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec[i]) / (t1[i] + t2[i]);
     }
 }
-template <int LP>
-static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts, int old_zero) {
+double divdamp_coef(double dts) {  // :1736-1738
     double smdiv = kSmdiv;
     double rdts = 1.0 / dts;
-    double coef_divdamp = 2.0 * smdiv * kLenDisp * rdts;
+    return 2.0 * smdiv * kLenDisp * rdts;
+}
+template <int LP>
+static hipError_t divdamp_div_lp(const DevState& S, hipStream_t st, double dts) {
+    if (S.halo || S.physics) return hipErrorInvalidValue;  // (the fused path's; srk3 never asks otherwise)
+    const double coef_divdamp = divdamp_coef(dts);
+    const int nb = col_blocks_n<LP, 2>(S, KE);
+    if (nb) k_div_damp<LP, 2, false, true><<<nb, 256, 0, st>>>(S, coef_divdamp);
+    return hipGetLastError();
+}
+hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts) {
+    MPAS_LP_DISPATCH(S.LP, divdamp_div_lp, S, st, dts);
+}
+template <int LP>
+static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts, int old_zero) {
+    double coef_divdamp = divdamp_coef(dts);
     auto run = [&](const DevState& X) {
 #define MPAS_DIVDAMP(EPW)                                                                    \
     do {                                                                                     \
@@ -558,22 +579,60 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
         }
     }
 }
+// edge ownership of the deferred damping (k_acoustic MODE 2): the lowest cell * 16 + slot
+// listing each edge (slots < nEdgesOnCell, owned cells), the owning slots per cell as a
+// bit mask, and the edges no cell lists; the div buffers' zero-slot rows hold the div the
+// damping computes there, -(0.0 - 0.0) = -0.0
+__global__ __launch_bounds__(256) void k_own_init(DevState S) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t <= (size_t)S.nEdges; t += stride)
+        ((int*)S.f[X_eowner])[t] = 0x7fffffff;
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t <= (size_t)S.nCells; t += stride)
+        ((int*)S.f[X_eown])[t] = 0;
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.LP; t += stride) {
+        fw(S, X_dvA)[(size_t)S.nCells * S.LP + t] = -0.0;
+        fw(S, X_dvB)[(size_t)S.nCells * S.LP + t] = -0.0;
+    }
+}
+__global__ __launch_bounds__(256) void k_own_min(DevState S) {
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.nCO * 10; t += (size_t)gridDim.x * 256) {
+        const int c = (int)(t / 10), i = (int)(t % 10), e = fi(S, F_edgesOnCell)[t];
+        if (i < fi(S, F_nEdgesOnCell)[c] && e >= 0 && e < S.nEdges) atomicMin((int*)S.f[X_eowner] + e, c * 16 + i);
+    }
+}
+__global__ __launch_bounds__(256) void k_own_bits(DevState S, int* norph) {
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.nCO * 10; t += (size_t)gridDim.x * 256) {
+        const int c = (int)(t / 10), i = (int)(t % 10), e = fi(S, F_edgesOnCell)[t];
+        if (i < fi(S, F_nEdgesOnCell)[c] && e >= 0 && e < S.nEdges && fi(S, X_eowner)[e] == c * 16 + i)
+            atomicOr((int*)S.f[X_eown] + c, 1 << i);
+    }
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.nEO; t += (size_t)gridDim.x * 256)
+        if (fi(S, X_eowner)[t] == 0x7fffffff) ((int*)S.f[X_orph])[atomicAdd(norph, 1)] = (int)t;
+}
+
 // derived mesh arrays; decides S.selfc (synchronous: runs once after each mesh upload)
 hipError_t launch_prepare(DevState& S, hipStream_t st) {
-    int* flag = nullptr;
-    hipError_t e = hipMalloc(&flag, sizeof(int));
+    int* flag = nullptr;  // [0] selfc, [1] orphan edges
+    hipError_t e = hipMalloc(&flag, 2 * sizeof(int));
     if (e != hipSuccess) return e;
-    const int one = 1;
-    int host = 0;
-    e = hipMemcpyAsync(flag, &one, sizeof(int), hipMemcpyHostToDevice, st);
+    const int init[2] = {1, 0};
+    int host[2] = {0, 0};
+    e = hipMemcpyAsync(flag, init, sizeof(init), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         k_prepare<<<stream_grid((size_t)S.nCells * 10), 256, 0, st>>>(S, flag);
+        const int g = stream_grid((size_t)S.nCells * 10 > (size_t)S.nEdges ? (size_t)S.nCells * 10 : (size_t)S.nEdges + 1);
+        k_own_init<<<g, 256, 0, st>>>(S);
+        k_own_min<<<g, 256, 0, st>>>(S);
+        k_own_bits<<<g, 256, 0, st>>>(S, flag + 1);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = hipMemcpyAsync(&host, flag, sizeof(int), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(host, flag, sizeof(host), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(flag);
-    if (e == hipSuccess) S.selfc = host;
+    if (e == hipSuccess) {
+        S.selfc = host[0];
+        S.n_orph = host[1];
+    }
     return e;
 }
 

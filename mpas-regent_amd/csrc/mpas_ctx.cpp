@@ -49,6 +49,12 @@ const FieldInfo kFields[X_COUNT] = {
     {"wc", K_C3, 1, D_M, 0, 0},
     {"F", K_E3, 1, D_M, 0, 0},
     {"Fw", K_E3, 1, D_M, 0, 0},
+    {"dvA", K_C3, 1, D_M, 0, 0},
+    {"dvB", K_C3, 1, D_M, 0, 0},
+    {"rupB", K_E3, 1, D_M, 0, 0},
+    {"eown", K_C2I, 1, D_M, 0, 0},
+    {"eowner", K_E2I, 1, D_M, 0, 0},
+    {"orph", K_E2I, 1, D_M, 0, 0},
     {"Ah", K_E3, 8, D_M, 0, 0},
     {"Rp", K_C3V, 8, D_M, 0, 0},
     {"Rm", K_C3V, 8, D_M, 0, 0},
@@ -83,6 +89,8 @@ struct mpas_ctx {
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     int overlap = 1;   // option "overlap": halo exchanges beside interior compute
+    int fusedamp = 1;  // option "fusedamp": atm_srk3 applies each divergence damping inside the next
+                       // acoustic launch (reference semantics, undecomposed; same bits)
     void* raw[X_COUNT] = {};  // the allocations behind S.f (S.f[f] = raw[f] + stagger)
     bool timing = false;
     bool dirty = true;  // derived mesh arrays need k_prepare
@@ -554,9 +562,40 @@ void trt_ensure(mpas_ctx* c) {
 
 // timing keys: one Regent task, split where its read/write set (B_alg) differs by argument
 // (bench.py aggregates the variants per task)
-const char* acoustic_name(int small_step) {
+const char* acoustic_name(int small_step, bool damp = false) {
+    if (damp)  // (option fusedamp: the previous substep's damping applied by this launch)
+        return small_step == 0 ? "atm_advance_acoustic_step_work[ss0+damp]" : "atm_advance_acoustic_step_work[ss>0+damp]";
     return small_step == 0 ? "atm_advance_acoustic_step_work[ss0]" : "atm_advance_acoustic_step_work[ss>0]";
 }
+
+// the buffer pairs of the deferred damping (k_acoustic MODE 2), swapped by atm_srk3 after
+// each launch; restored on exit (the ru_p pair by a copy if a step ended on the second
+// buffer, which the reference schedule's even number of fused launches never does)
+struct FuseBuffers {
+    mpas_ctx* c;
+    void *rup, *rupB, *dvA, *dvB;
+    explicit FuseBuffers(mpas_ctx* c_) : c(c_) {
+        rup = c->S.f[F_ru_p];
+        rupB = c->S.f[X_rupB];
+        dvA = c->S.f[X_dvA];
+        dvB = c->S.f[X_dvB];
+    }
+    void swap_rup() { std::swap(c->S.f[F_ru_p], c->S.f[X_rupB]); }
+    void swap_dv() { std::swap(c->S.f[X_dvA], c->S.f[X_dvB]); }
+    void finish() {
+        if (c->S.f[F_ru_p] != rup)
+            hipcheck(hipMemcpyAsync(rup, c->S.f[F_ru_p], dev_bytes(c, F_ru_p), hipMemcpyDeviceToDevice, c->stream),
+                     "hipMemcpyAsync ru_p");
+        restore();
+    }
+    void restore() {
+        c->S.f[F_ru_p] = rup;
+        c->S.f[X_rupB] = rupB;
+        c->S.f[X_dvA] = dvA;
+        c->S.f[X_dvB] = dvB;
+    }
+    ~FuseBuffers() { restore(); }
+};
 const char* recover_name(int rk_step) {
     return rk_step == 2 ? "atm_recover_large_step_variables_work[rk2]" : "atm_recover_large_step_variables_work[rk<2]";
 }
@@ -587,6 +626,15 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
     run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
     run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
+    // option fusedamp (reference semantics, undecomposed): each damping but the step's last
+    // is applied by the next acoustic launch (k_acoustic MODE 2), the last from the div
+    // the acoustic step stored (launch_div_damping_div); the same bits as the separate task
+    const bool fuse = c->fusedamp && S.physics == 0 && !c->halo;
+    FuseBuffers fb(c);
+    int n_acoustic = 0, done_acoustic = 0;
+    for (int r = 0; r < 3; r++) n_acoustic += number_sub_steps[r] + (S.physics ? 0 : 1);
+    bool pending = false;
+    double coef_prev = 0.0;
     for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
         if (rk_step == 1)
             run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
@@ -603,10 +651,24 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
         const int n_small = number_sub_steps[rk_step] + (S.physics ? 0 : 1);  // Q5 (the MPAS form: n)
         for (int small_step = 0; small_step < n_small; small_step++) {
-            run_task(c, acoustic_name(small_step),
-                     [&] { return launch_acoustic(S, st, rk_sub_timestep[rk_step], small_step, c->exact); });
-            run_task(c, "atm_divergence_damping_3d",
-                     [&] { return launch_div_damping(S, st, rk_sub_timestep[rk_step], small_step == 0); });
+            const double dts = rk_sub_timestep[rk_step];
+            if (fuse) {
+                const int mode = pending ? 2 : 1;
+                run_task(c, acoustic_name(small_step, pending),
+                         [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev); });
+                if (mode == 2) fb.swap_rup();
+                fb.swap_dv();  // this substep's div is read next from X_dvB
+                if (++done_acoustic == n_acoustic) {
+                    run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping_div(S, st, dts); });
+                    pending = false;
+                } else {
+                    pending = true;
+                    coef_prev = divdamp_coef(dts);
+                }
+                continue;
+            }
+            run_task(c, acoustic_name(small_step), [&] { return launch_acoustic(S, st, dts, small_step, c->exact); });
+            run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, dts, small_step == 0); });
         }
         if (S.physics)  // rk_timestep.rg:460, commented out in the reference (Q7)
             run_task(c, recover_name(rk_step),
@@ -621,6 +683,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     if (S.physics == 2)  // the MPAS dynamics: cell-centre winds for the next step's curvature
         run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });  // (:487, commented)
     run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
+    fb.finish();
     // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }
 
@@ -799,6 +862,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         graph_drop(c);  // every option is baked into a captured step
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
         else if (name && std::strcmp(name, "graph") == 0) c->graph_on = value ? 1 : 0;
+        else if (name && std::strcmp(name, "fusedamp") == 0) c->fusedamp = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
             if (value != 1 && value != 2 && value != 4) throw Fail{MPAS_EINVAL, "epw must be 1, 2 or 4"};
@@ -871,6 +935,12 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
             *value = c->trt.ntiles;
         }
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
+        else if (name && std::strcmp(name, "fusedamp") == 0) *value = c->fusedamp;
+        else if (name && std::strcmp(name, "fusedamp_active") == 0) *value = c->fusedamp && c->S.physics == 0 && !c->halo;
+        else if (name && std::strcmp(name, "orphan_edges") == 0) {  // edges no cell lists (k_prepare)
+            prepare_now(c);
+            *value = c->S.n_orph;
+        }
         else if (name && std::strcmp(name, "self") == 0) *value = c->self_on;
         else if (name && std::strcmp(name, "graph") == 0) *value = c->graph_on;
         else if (name && std::strcmp(name, "graph_captures") == 0) *value = c->graph_captures;

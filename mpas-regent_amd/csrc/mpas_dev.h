@@ -69,6 +69,14 @@ enum FieldId {
                 // depends only on the edge, so it is formed once per edge, not per cell
     X_Fw,       // the same for the w advection of the MPAS dynamics (physics = 2: every
                 // edge's flux_arr over the state w, :1174-1205 without Q13)
+    // deferred divergence damping (option "fusedamp", k_acoustic.hip MODE 2): the damping
+    // of an acoustic substep is applied by the next acoustic substep as it reads ru_p
+    X_dvA,      // div = -(rtheta_pp - rtheta_pp_old) of the substep (:1755), per cell    C3
+    X_dvB,      //   (two buffers: a fused launch reads one and writes the other)        C3
+    X_rupB,     // the second ru_p buffer (a fused launch writes the damped ru_p there)  E3
+    X_eown,     // per cell: bit i set when this cell's slot i writes its edge's ru_p    C2I
+    X_eowner,   // per edge: the lowest cell * 16 + slot listing it (prepare scratch)    E2I
+    X_orph,     // the edges no cell lists (written by the fused launch's extra blocks)  E2I
     // monotonic scalar transport (k_transport.hip), one column per (entity, scalar)
     X_Ah,       // antidiffusive edge flux                                      E3 x 8
     X_Rp,       // R+ (fraction of the incoming antidiffusive flux allowed)     C3V x 8
@@ -93,6 +101,7 @@ struct DevState {
                         // grid (= the counts above unless the mesh is decomposed)
     int lo[3];          // first cell / edge / vertex of a launch: kernels compute entities
                         // [lo, nXO); 0 except for the boundary launch of a halo overlap
+    int n_orph;    // edges in X_orph (k_prepare)
     int interior;  // 1 on the interior launch of a halo overlap (Halo::launch: ghosts not
                    // yet fresh), 0 on a whole-range or boundary launch
     int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
@@ -172,9 +181,18 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st);
 hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts);
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
-hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact);
+// mode (reference semantics, no halo; atm_srk3 with option "fusedamp"): 0 plain, 1 also
+// writes div of this substep (X_dvA), 2 also applies the previous substep's damping
+// (coefficient coef_prev, its div in X_dvB) to the ru_p it reads and writes the damped
+// ru_p to X_rupB; the caller swaps the buffer pairs after the launch
+hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode = 0,
+                           double coef_prev = 0.0);
 // old_zero: only from srk3, right after a stage's first acoustic substep (k_div_damp OLD0)
 hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts, int old_zero = 0);
+// the damping from the div buffer X_dvB (fusedamp: the step's last substep), ru_p in place
+hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts);
+// coef_divdamp of atm_divergence_damping_3d (:1736-1738) for dts
+double divdamp_coef(double dts);
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step);
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
@@ -226,8 +244,7 @@ hipError_t launch_summarize(const DevState& S, hipStream_t st, void* scratch, do
 //   on == G > 1: within every window of 8G consecutive blocks each XCD owns G contiguous
 //   blocks (all XCDs stay inside one Infinity-Cache window, each L2 sees a compact
 //   sub-range); blocks past the last whole window keep the dispatcher order.
-__device__ __forceinline__ int xcd_block(int on) {
-    const int b = (int)blockIdx.x, nb = (int)gridDim.x;
+__device__ __forceinline__ int xcd_block_n(int on, int b, int nb) {
     if (on <= 0) return b;
     if (on == 1) {
         const int q = nb >> 3, r = nb & 7, x = b & 7, pos = b >> 3;
@@ -238,6 +255,8 @@ __device__ __forceinline__ int xcd_block(int on) {
     const int w = b / W, r = b - w * W;
     return w * W + (r & 7) * on + (r >> 3);
 }
+// the remap over the whole grid
+__device__ __forceinline__ int xcd_block(int on) { return xcd_block_n(on, (int)blockIdx.x, (int)gridDim.x); }
 
 // Mixed vertex + cell grids (dyn_tend C, solve_diagnostics): nVB vertex blocks and
 // nb - nVB cell blocks.  With S.vcmix they are interleaved in proportion -- block b is a

@@ -14,7 +14,7 @@ roofline.achieved divides by the measured launch time.
 """
 
 # name -> (reads, writes); each a list of field names of the registry
-def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0):
+def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "atm_rk_integration_setup":
         return (["rho_p", "rho_zz", "rtheta_p", "rw", "theta_m", "w", "ru", "u"],
@@ -68,6 +68,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0):
             if small_step != 0:
                 reads += ["ru_p", "ruAvg", "exner", "cqu", "zxu", "invDcEdge"]
             writes += ["ru_p", "ruAvg"]
+        if damp:  # option fusedamp: the previous substep's atm_divergence_damping_3d applied here
+            reads += ["rtheta_pp", "rtheta_pp_old", "isShared", "specZoneMaskEdge"]
+            writes += ["ru_p"]
         return reads, writes
     if task == "atm_divergence_damping_3d":
         return (["rtheta_pp", "rtheta_pp_old", "theta_m", "ru_p", "cellsOnEdge", "isShared", "specZoneMaskEdge"],
@@ -136,10 +139,12 @@ def b_alg(task, dims, **kw):
     return sum(fb(x) for x in set(reads)) + sum(fb(x) for x in set(writes))
 
 
-def step_schedule(schedule=1, physics=0, transport=0):
+def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
-    recover after each stage; transport = 1 adds the scalar save and the transport"""
+    recover after each stage; transport = 1 adds the scalar save and the transport;
+    fusedamp (reference semantics): six of the seven dampings run inside the next acoustic
+    launch"""
     if physics:
         p = {"physics": physics}
         out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
@@ -165,14 +170,22 @@ def step_schedule(schedule=1, physics=0, transport=0):
            ("atm_compute_vert_imp_coefs", {}, 2)]
     if schedule == 1:
         out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
-    out += [("atm_set_smlstep_pert_variables_work", {}, 3),
-            ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
-            ("atm_advance_acoustic_step_work", {"small_step": 1}, 4),
-            ("atm_divergence_damping_3d", {}, 7),
+    if fusedamp:
+        out += [("atm_set_smlstep_pert_variables_work", {}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 0}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True}, 2),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 4),
+                ("atm_divergence_damping_3d", {}, 1)]
+    else:
+        out += [("atm_set_smlstep_pert_variables_work", {}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1}, 4),
+                ("atm_divergence_damping_3d", {}, 7)]
+    out += [
             ("atm_compute_solve_diagnostics", {}, 2), ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
             ("atm_rk_dynamics_substep_finish", {}, 1)]
     return out
 
 
-def b_alg_step(dims, schedule=1, physics=0, transport=0):
-    return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport))
+def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False):
+    return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp))

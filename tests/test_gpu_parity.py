@@ -428,3 +428,56 @@ def test_upload_rejects_overlong_lists(x1_2562, field, width):
         st[field][3, 0] = width + 1
         with pytest.raises(lib.MpasError, match="exceeds its list width"):
             ctx.upload(st, names=[field])
+
+
+# ---- option fusedamp: the damping inside the next acoustic launch ------------------------
+def _two_steps_gpu(st, fusedamp, exact, graph=1):
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.set_option("exact", exact)
+        ctx.set_option("fusedamp", fusedamp)
+        ctx.set_option("graph", graph)
+        ctx.upload(st)
+        assert ctx.get_option("fusedamp_active") == fusedamp
+        T.atm_srk3(ctx, 720.0, 0)
+        T.atm_srk3(ctx, 360.0, 1)
+        T.atm_srk3(ctx, 360.0, 1)  # (graph replay of the second capture)
+        ctx.sync()
+        ctx.download(got)
+        orph = ctx.get_option("orphan_edges")
+    return got, orph
+
+
+@pytest.mark.parametrize("L", [1, 2, 5, 56, 63])
+@pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
+def test_fusedamp_bit_identical(x1_2562, L, variant):
+    """atm_srk3 with six of its seven dampings applied inside the next acoustic launch
+    (k_acoustic MODE 2: the same expression on the same values) is value-identical to the
+    separate atm_divergence_damping_3d launches and to the oracle, in exact mode and on the
+    fast path; raw 1-based ids leave edge 0 listed by no cell (an orphan, written by the
+    launch's extra blocks)"""
+    st = base_state(x1_2562, L, variant)
+    ref = run_oracle(st, lambda o: (o.atm_srk3(720.0, 0), o.atm_srk3(360.0, 1), o.atm_srk3(360.0, 1)))
+    got1, orph = _two_steps_gpu(st, 1, 1)
+    bad = compare_states(got1, ref, rtol=0.0)
+    assert not bad, f"fusedamp exact vs oracle: {bad[:6]}"
+    if variant == "ref":
+        assert orph >= 1
+    if variant == "mpas0":
+        assert orph == 0
+    for graph in (1, 0):
+        a, _ = _two_steps_gpu(st, 1, 0, graph)
+        b, _ = _two_steps_gpu(st, 0, 0, graph)
+        bad = compare_states(a, b, rtol=0.0)
+        assert not bad, f"fusedamp fast path vs separate damping (graph={graph}): {bad[:6]}"
+
+
+def test_fusedamp_dt_zero(x1_2562):
+    """dt = 0 (main.rg:66, j = 0): the deferred coefficient is inf; the NaN / inf pattern of
+    ru_p is the separate damping's"""
+    st = base_state(x1_2562, 5, "ref")
+    ref = run_oracle(st, lambda o: o.atm_srk3(0.0, 0))
+    got = run_gpu(st, lambda c: T.atm_timestep(c, 0.0), exact=1)
+    assert not np.isfinite(ref["ru_p"]).all()
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
