@@ -266,6 +266,11 @@ int mpas_rccl_unique_id(void* id128);
 /* (after every mpas_halo_plan call of the context: the transports size their buffers) */
 int mpas_halo_rccl(mpas_ctx* ctx, int nranks, int rank, const void* id128);
 int mpas_halo_loopback(mpas_ctx** ctxs, int n);
+/* stub transport (measurement only): every exchange packs the send columns of each peer,
+ * stands in for the wire with one device copy of the received bytes out of the send
+ * buffer, and unpacks -- one rank's whole launch sequence on one GPU, everything but the
+ * wire time; the ghosts do NOT receive their neighbours' values */
+int mpas_halo_stub(mpas_ctx* ctx);
 /* halo exchanges made so far and fields moved by them */
 int mpas_halo_stats(mpas_ctx* ctx, int64_t* exchanges, int64_t* fields);
 

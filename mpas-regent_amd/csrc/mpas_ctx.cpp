@@ -115,6 +115,14 @@ struct mpas_ctx {
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
     int64_t graph_captures = 0, graph_launches = 0;
+    // decomposed contexts (option "graph_halo"; RCCL and stub transports -- the loopback's
+    // host barriers cannot be captured): the halo bookkeeping is host-side and evolves
+    // identically every step once its state at the step's start repeats, so the step is
+    // captured then, with the state at its start (graph_stale0) as part of the key, and a
+    // replay sets the host state to the one the captured step ended in (graph_stale1)
+    int graph_halo = 0;
+    std::vector<uint8_t> graph_stale0, graph_stale1, prev_stale0;
+    int64_t graph_exch = 0, graph_fields = 0;
     // option "trtile": the tiled transport (k_transport.hip) when the mesh allows it; the
     // tiles are rebuilt after a mesh upload or a change of the owned / interior cells.
     // Off by default: measured 2x slower than the three kernels
@@ -707,13 +715,37 @@ void prepare_now(mpas_ctx* c) {
 
 // one atm_srk3 step: replayed from a captured HIP graph when possible
 void srk3_step(mpas_ctx* c, double dt, int schedule) {
-    if (!c->graph_on || c->timing || c->halo) {
+    Halo* h = c->halo.get();
+    const bool halo_graph = h && c->graph_halo && (h->rccl || h->stub) && !h->loop;
+    if (!c->graph_on || c->timing || (h && !halo_graph)) {
         srk3(c, dt, schedule);
         return;
     }
     prepare_now(c);  // (synchronous: never inside a capture)
+    if (h) {
+        if (c->graph_valid && c->graph_dt == dt && c->graph_schedule == schedule && h->stale == c->graph_stale0) {
+            hipcheck(hipGraphLaunch(c->graph_exec, c->stream), "hipGraphLaunch");
+            c->graph_launches++;
+            h->stale = c->graph_stale1;  // the bookkeeping the captured step made
+            h->exchanges += c->graph_exch;
+            h->fields_moved += c->graph_fields;
+            return;
+        }
+        if (h->stale != c->prev_stale0) {  // not yet in the steady state: one more eager step
+            c->prev_stale0 = h->stale;
+            srk3(c, dt, schedule);
+            return;
+        }
+    }
     if (!(c->graph_valid && c->graph_dt == dt && c->graph_schedule == schedule)) {
         graph_drop(c);
+        std::vector<uint8_t> stale0;
+        int64_t ex0 = 0, fl0 = 0;
+        if (h) {
+            stale0 = h->stale;
+            ex0 = h->exchanges;
+            fl0 = h->fields_moved;
+        }
         hipcheck(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
         try {
             srk3(c, dt, schedule);
@@ -721,6 +753,11 @@ void srk3_step(mpas_ctx* c, double dt, int schedule) {
             hipGraph_t g = nullptr;
             (void)hipStreamEndCapture(c->stream, &g);
             if (g) (void)hipGraphDestroy(g);
+            if (h) {  // nothing ran: the bookkeeping goes back to the step's start
+                h->stale = stale0;
+                h->exchanges = ex0;
+                h->fields_moved = fl0;
+            }
             throw;
         }
         hipcheck(hipStreamEndCapture(c->stream, &c->graph), "hipStreamEndCapture");
@@ -729,6 +766,12 @@ void srk3_step(mpas_ctx* c, double dt, int schedule) {
         c->graph_dt = dt;
         c->graph_schedule = schedule;
         c->graph_captures++;
+        if (h) {
+            c->graph_stale0 = stale0;
+            c->graph_stale1 = h->stale;
+            c->graph_exch = h->exchanges - ex0;
+            c->graph_fields = h->fields_moved - fl0;
+        }
     }
     hipcheck(hipGraphLaunch(c->graph_exec, c->stream), "hipGraphLaunch");
     c->graph_launches++;
@@ -863,6 +906,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
         else if (name && std::strcmp(name, "graph") == 0) c->graph_on = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp") == 0) c->fusedamp = value ? 1 : 0;
+        else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
             if (value != 1 && value != 2 && value != 4) throw Fail{MPAS_EINVAL, "epw must be 1, 2 or 4"};
@@ -936,6 +980,13 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         }
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "fusedamp") == 0) *value = c->fusedamp;
+        else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
+        else if (name && std::strcmp(name, "halo_state") == 0) {  // hash of the halo bookkeeping (debug)
+            uint64_t hsh = 1469598103934665603ull;
+            if (c->halo)
+                for (uint8_t v : c->halo->stale) hsh = (hsh ^ v) * 1099511628211ull;
+            *value = (int64_t)(hsh >> 1);
+        }
         else if (name && std::strcmp(name, "fusedamp_active") == 0) *value = c->fusedamp && c->S.physics == 0 && !c->halo;
         else if (name && std::strcmp(name, "orphan_edges") == 0) {  // edges no cell lists (k_prepare)
             prepare_now(c);
@@ -1208,6 +1259,10 @@ int mpas_halo_plan(mpas_ctx* c, int kind, int peer, const int32_t* send_ids, int
         p.d_send = dev_ints(send_ids, nsend);
         p.d_recv = dev_ints(recv_ids, nrecv);
         h->peers[kind].push_back(p);
+        for (auto& kv : h->tabs)  // the pack / unpack tables follow the plan
+            if (kv.second.dev) (void)hipFree(kv.second.dev);
+        h->tabs.clear();
+        graph_drop(c);
     });
 }
 
@@ -1268,6 +1323,17 @@ int mpas_halo_rccl(mpas_ctx* c, int nranks, int rank, const void* id128) {
         hipcheck(h->reserve(c->S.LP), "halo buffers");
         std::string err;
         if (rccl_init(h, nranks, rank, id128, err) != 0) throw Fail{MPAS_ERCCL, err};
+    });
+}
+
+int mpas_halo_stub(mpas_ctx* c) {
+    return guarded(c, [&] {
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        Halo* h = halo_of(c);
+        if (h->rccl || h->loop) throw Fail{MPAS_EINVAL, "mpas_halo_stub: the context already has a transport"};
+        hipcheck(h->reserve(c->S.LP), "halo buffers");
+        h->stub = true;
+        graph_drop(c);
     });
 }
 

@@ -27,6 +27,8 @@
 #include <cstdint>
 #include <functional>
 #include <initializer_list>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -45,6 +47,13 @@ struct HaloPeer {
 };
 
 struct LoopGroup;  // loopback transport shared by the contexts of one process
+struct HaloSeg;    // one segment of a pack / unpack (mpas_halo.hip)
+struct HaloCopyTab {  // the device segment table of one direction of one exchange signature
+    HaloSeg* dev = nullptr;
+    int nseg = 0;
+    long ncol = 0;  // buffer columns covered
+    std::shared_ptr<std::vector<HaloSeg>> host;
+};
 struct RcclComm;   // RCCL transport
 
 struct Halo {
@@ -60,6 +69,7 @@ struct Halo {
     size_t cap = 0;  // doubles per buffer
     LoopGroup* loop = nullptr;
     RcclComm* rccl = nullptr;
+    bool stub = false;  // mpas_halo_stub: pack, a device copy for the wire, unpack
     std::string err;
     int64_t exchanges = 0, fields_moved = 0;
     // overlap of the exchange with interior compute
@@ -70,6 +80,7 @@ struct Halo {
     int overlap = 1;           // option "overlap"
     std::vector<int> overlapped;  // fields exchanged beside the last interior launch
     std::string race;             // set by wrote() when a kernel wrote one of them
+    std::map<std::vector<int>, HaloCopyTab> tabs;  // pack / unpack tables per exchange signature
 
     ~Halo();
     hipError_t reserve(int LP);  // size the packed buffers for the largest exchange

@@ -7,6 +7,7 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 
@@ -15,29 +16,34 @@
 namespace mpas {
 
 // ------------------------------------------------------------------ pack / unpack
-constexpr int kMaxSeg = 128;
-struct SegList {
-    double* f[kMaxSeg];      // field base (LP doubles per column)
-    const int* ids[kMaxSeg];  // local entity ids
-    int W[kMaxSeg], comp[kMaxSeg];  // columns per entity and the one this segment moves
-                                    // (x8 transport fields: column = entity * W + comp)
-    long start[kMaxSeg + 1];  // first packed column of each segment
-    int nseg, LP;
+// One launch per direction and exchange, over the columns of every peer region: the
+// segments (field component x peer's id list, contiguous in the buffer) are a device
+// table built once per exchange signature (the fields moved) and cached -- a step repeats
+// the same ~10 signatures -- and each wavefront copies whole columns, finding its
+// segment by a wave-uniform binary search over the segment starts.
+struct HaloSeg {
+    double* f;        // field base (LP doubles per column)
+    const int* ids;   // local entity ids
+    long start;       // first buffer column of the segment
+    int W, comp;      // columns per entity and the one this segment moves (x8 fields)
 };
 
-// one thread per packed double: column j of the buffer <-> column ids[j - start] of f
 template <bool PACK>
-__global__ __launch_bounds__(256) void k_halo_copy(SegList sl, double* buf) {
-    const long t = (long)blockIdx.x * 256 + threadIdx.x;
-    const long col = t / sl.LP;
-    const int k = (int)(t % sl.LP);
-    if (col >= sl.start[sl.nseg]) return;
-    int s = 0;
-    while (col >= sl.start[s + 1]) s++;
-    const long j = col - sl.start[s];
-    double* f = sl.f[s] + ((size_t)sl.ids[s][j] * sl.W[s] + sl.comp[s]) * sl.LP + k;
-    if (PACK) buf[t] = *f;
-    else *f = buf[t];
+__global__ __launch_bounds__(256) void k_halo_copy(const HaloSeg* seg, int nseg, long ncol, int LP, double* buf) {
+    const long col = (long)blockIdx.x * (256 / LP) + threadIdx.x / LP;
+    const int k = (int)(threadIdx.x % LP);
+    if (col >= ncol) return;
+    int lo = 0, hi = nseg - 1;  // the last segment starting at or before col
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (seg[mid].start <= col) lo = mid;
+        else hi = mid - 1;
+    }
+    const HaloSeg& g = seg[lo];
+    double* f = g.f + ((size_t)g.ids[col - g.start] * g.W + g.comp) * LP + k;
+    double* b = buf + (size_t)col * LP + k;
+    if (PACK) *b = *f;
+    else *f = *b;
 }
 
 static int kind_of_field(int f) {
@@ -57,6 +63,8 @@ Halo::~Halo() {
         }
     if (sendbuf) (void)hipFree(sendbuf);
     if (recvbuf) (void)hipFree(recvbuf);
+    for (auto& kv : tabs)
+        if (kv.second.dev) (void)hipFree(kv.second.dev);
     if (rccl) rccl_free(rccl);
     if (comm) {
         (void)hipStreamSynchronize(comm);
@@ -317,16 +325,18 @@ static void plan_regions(const Halo& h, const std::vector<int>& fields, std::vec
     }
 }
 
-static hipError_t run_copy(const DevState& S, hipStream_t st, const Halo& h, const std::vector<Region>& reg,
-                           const std::vector<int> (&byk)[3], bool pack) {
-    SegList sl{};
-    sl.LP = S.LP;
-    sl.nseg = 0;
-    long col = 0;
+// the segment table of one direction of an exchange (cached per signature)
+static const HaloCopyTab* copy_table(const DevState& S, Halo& h, const std::vector<Region>& reg,
+                                     const std::vector<int> (&byk)[3], const std::vector<int>& fields, bool pack,
+                                     hipStream_t st, hipError_t& e) {
+    std::vector<int> key(fields);
+    key.push_back(pack ? 1 : 0);
+    auto it = h.tabs.find(key);
+    if (it != h.tabs.end()) return &it->second;
+    HaloCopyTab t;
+    std::vector<HaloSeg> segs;
     for (const auto& r : reg) {
-        long c0 = pack ? r.soff : r.roff;
-        col = 0;
-        sl.nseg = 0;
+        long col = pack ? r.soff : r.roff;
         for (int k = 0; k < 3; k++) {
             const HaloPeer* p = nullptr;
             for (const auto& x : h.peers[k])
@@ -336,27 +346,39 @@ static hipError_t run_copy(const DevState& S, hipStream_t st, const Halo& h, con
             if (n == 0) continue;
             for (int f : byk[k])
                 for (int comp = 0; comp < kFields[f].width; comp++) {
-                    if (sl.nseg == kMaxSeg) {
-                        const_cast<Halo&>(h).err = "too many halo segments";
-                        return hipErrorInvalidValue;
-                    }
-                    sl.f[sl.nseg] = (double*)S.f[f];
-                    sl.ids[sl.nseg] = pack ? p->d_send : p->d_recv;
-                    sl.W[sl.nseg] = kFields[f].width;
-                    sl.comp[sl.nseg] = comp;
-                    sl.start[sl.nseg] = col;
+                    segs.push_back({(double*)S.f[f], pack ? p->d_send : p->d_recv, col, kFields[f].width, comp});
                     col += n;
-                    sl.nseg++;
                 }
         }
-        if (sl.nseg == 0) continue;
-        sl.start[sl.nseg] = col;
-        const long tot = col * (long)S.LP;
-        double* buf = (pack ? h.sendbuf : h.recvbuf) + c0 * S.LP;
-        const unsigned grid = (unsigned)((tot + 255) / 256);
-        if (pack) k_halo_copy<true><<<grid, 256, 0, st>>>(sl, buf);
-        else k_halo_copy<false><<<grid, 256, 0, st>>>(sl, buf);
+        t.ncol = std::max(t.ncol, col);
     }
+    t.nseg = (int)segs.size();
+    t.host = std::make_shared<std::vector<HaloSeg>>(segs);
+    e = hipSuccess;
+    if (t.nseg) {
+        if ((e = hipMalloc(&t.dev, sizeof(HaloSeg) * segs.size())) != hipSuccess) return nullptr;
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(st, &cs);
+        if (cs == hipStreamCaptureStatusNone)
+            e = hipMemcpy(t.dev, t.host->data(), sizeof(HaloSeg) * segs.size(), hipMemcpyHostToDevice);
+        else  // (inside a capture: a copy node; the host table stays alive in the cache)
+            e = hipMemcpyAsync(t.dev, t.host->data(), sizeof(HaloSeg) * segs.size(), hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return nullptr;
+    }
+    return &(h.tabs[key] = t);
+}
+
+static hipError_t run_copy(const DevState& S, hipStream_t st, Halo& h, const std::vector<Region>& reg,
+                           const std::vector<int> (&byk)[3], const std::vector<int>& fields, bool pack) {
+    hipError_t e = hipSuccess;
+    const HaloCopyTab* t = copy_table(S, h, reg, byk, fields, pack, st, e);
+    if (!t) return e;
+    if (!t->nseg || !t->ncol) return hipSuccess;
+    const int cpb = 256 / S.LP;
+    const unsigned grid = (unsigned)((t->ncol + cpb - 1) / cpb);
+    double* buf = pack ? h.sendbuf : h.recvbuf;
+    if (pack) k_halo_copy<true><<<grid, 256, 0, st>>>(t->dev, t->nseg, t->ncol, S.LP, buf);
+    else k_halo_copy<false><<<grid, 256, 0, st>>>(t->dev, t->nseg, t->ncol, S.LP, buf);
     return hipGetLastError();
 }
 
@@ -391,7 +413,7 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
         for (int s = 0; s < loop->n; s++)
             if (s != rank && (e = hipStreamWaitEvent(st, loop->copied[s], 0)) != hipSuccess) return e;
     }
-    if ((e = run_copy(S, st, *this, reg, byk, true)) != hipSuccess) return e;
+    if ((e = run_copy(S, st, *this, reg, byk, fields, true)) != hipSuccess) return e;
     if (rccl) {
         std::string dummy;
         RcclApi* a = rccl_api(dummy);
@@ -405,6 +427,10 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
             err = std::string("RCCL halo exchange: ") + (a->GetErrorString ? a->GetErrorString(r ? r : r2) : "error");
             return hipErrorUnknown;
         }
+    } else if (stub) {  // the received bytes land from the send buffer (no peer)
+        const size_t n = (size_t)std::min(stot, rtot) * S.LP;
+        if (n && (e = hipMemcpyAsync(recvbuf, sendbuf, n * sizeof(double), hipMemcpyDeviceToDevice, st)) != hipSuccess)
+            return e;
     } else if (loop) {
         if ((e = hipEventRecord(loop->packed[rank], st)) != hipSuccess) return e;
         if (!loop->barrier(120.0)) {
@@ -436,7 +462,7 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
             return hipErrorUnknown;
         }
     }
-    return run_copy(S, st, *this, reg, byk, false);
+    return run_copy(S, st, *this, reg, byk, fields, false);
 }
 
 }  // namespace mpas

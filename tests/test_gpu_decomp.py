@@ -228,3 +228,29 @@ def test_ring1_rank_without_boundary_edges(x1_2562):
     got, _ = run_decomposed(st, 2, lambda c: T.atm_srk3(c, 720.0, 1), 1, cell_part=part, overlap=1)
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
+
+
+def test_stub_transport_graph_replay(x1_2562):
+    """a decomposed context on the stub transport (tools/rank_sim.py: one rank's launch
+    sequence on one GPU) with option graph_halo: the step is captured once the halo
+    bookkeeping at its start repeats, and the replays leave the same bits and the same
+    exchange counts as eager steps (the ghosts hold stub values, identical in both runs)"""
+    st = state(x1_2562, 56, "random")
+    d = decomp.Decomposition(st, 4)
+    out = {}
+    for graph in (1, 0):
+        loc = d.local_state(1)
+        with lib.Context(*d.n_local(1), st.L) as ctx:
+            lib.setup_subdomain(ctx, d, 1)
+            lib.halo_stub(ctx)
+            ctx.set_option("graph_halo", graph)
+            ctx.upload(loc)
+            for _ in range(8):
+                T.atm_srk3(ctx, 720.0, 1)
+            ctx.sync()
+            ctx.download(loc)
+            out[graph] = (loc, lib.halo_stats(ctx), ctx.get_option("graph_captures"), ctx.get_option("graph_launches"))
+    bad = compare_states(out[1][0], out[0][0], rtol=0.0)
+    assert not bad, bad[:6]
+    assert out[1][1] == out[0][1]
+    assert out[1][2] == 1 and out[1][3] >= 3 and out[0][2] == 0
