@@ -163,23 +163,16 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 // b_tri with cofwt(k-1) (Q16) and the LU recurrence alpha(k) = 1 / (b(k) - a(k) gamma(k-1)),
 // gamma(k) = c(k) alpha(k) from gamma(0) = 0 within the call (Q17), level by level
 // (a nonlinear recurrence: lane k waits for lane k-1's gamma, broadcast by a shuffle)
+// one column of atm_compute_vert_imp_coefs from its loaded inputs (k_vert_imp, and the
+// stage-0 fusion with the setup copies and the moist coefficients, k_setup_vi)
 template <int LP, bool MPASV>
-__global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
-    ColMap<LP> m(S, KC);
-    const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCO) return;
-    const size_t p = (size_t)c * LP + lpos(LP, k);
+__device__ __forceinline__ void vi_column(const DevState& S, int c, int k, double zz, double exner, double tm, double cqw,
+                                          double qtot, double rb, double rtb, double rtp, double exb, double gamma_old,
+                                          double coftz_old, double dtseps, double rcv, double c2) {
+    const int L = S.L;
     const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
     const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
     const double rdzw_m = k > 0 ? rdzw_a[k - 1] : 0.0;
-    // (gather2: two own columns per 16-B load instruction)
-    double zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old;
-    gather2<LP>(fd(S, F_zz), c, fd(S, F_exner), c, k, zz, exner);
-    gather2<LP>(fd(S, F_theta_m), c, fd(S, F_cqw), c, k, tm, cqw);
-    gather2<LP>(fd(S, F_qtot), c, fd(S, F_rho_base), c, k, qtot, rb);
-    gather2<LP>(fd(S, F_rtheta_base), c, fd(S, F_rtheta_p), c, k, rtb, rtp);
-    gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
-    const double coftz_old = colk(fd(S, F_coftz), c);  // level L keeps its (never written) value
     const double zz_m = lvl_dn<LP>(zz, k), exner_m = lvl_dn<LP>(exner, k), tm_m = lvl_dn<LP>(tm, k);
 
     // :550-564
@@ -233,6 +226,81 @@ __global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, dou
     if (w_all) colk(fw(S, F_gamma_tri), c) = k == 0 ? 0.0 : PADW(gamma);
     if (c == 0 && k < L) fw(S, F_cofrz)[k] = cofrz;
 }
+
+template <int LP, bool MPASV>
+__global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
+    ColMap<LP> m(S, KC);
+    const int k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    // (gather2: two own columns per 16-B load instruction)
+    double zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old;
+    gather2<LP>(fd(S, F_zz), c, fd(S, F_exner), c, k, zz, exner);
+    gather2<LP>(fd(S, F_theta_m), c, fd(S, F_cqw), c, k, tm, cqw);
+    gather2<LP>(fd(S, F_qtot), c, fd(S, F_rho_base), c, k, qtot, rb);
+    gather2<LP>(fd(S, F_rtheta_base), c, fd(S, F_rtheta_p), c, k, rtb, rtp);
+    gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
+    const double coftz_old = colk(fd(S, F_coftz), c);  // level L keeps its (never written) value
+    vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2);
+}
+
+// Stage 0 of atm_srk3 in one launch (option "fusesetup", reference semantics): the copies
+// of atm_rk_integration_setup (:747-778), atm_compute_moist_coefficients (:460-502) and
+// the first atm_compute_vert_imp_coefs (:513-592) -- all column-local, run in this order
+// by one wavefront per cell column: vert_imp takes theta_m and rtheta_p from the copy's
+// loads and qtot / cqw as moist has just set them, so those four columns are read once.
+// Edge blocks (ncb..) copy ru and u.  The same values as the three launches.
+template <int LP>
+__global__ __launch_bounds__(256) void k_setup_vi(DevState S, int ncb, double dtseps, double rcv, double c2) {
+    const int L = S.L, k = (int)(threadIdx.x % LP);
+    int blk = (int)blockIdx.x;
+    if (blk >= ncb) {  // :767-771 ru_save = ru, u_2 = u (every level but L)
+        const int e = col_of<LP>(xcd_block_n(S.xcd, blk - ncb, (int)gridDim.x - ncb)) + S.lo[KE];
+        if (e >= S.nEO) return;
+        double ru, u;
+        gather2<LP>(fd(S, F_ru), e, fd(S, F_u), e, k, ru, u);
+        put2<LP>(fw(S, F_ru_save), e, fw(S, F_u_2), e, k, PADW(ru), PADW(u), k != L, k != L);
+        return;
+    }
+    const int c = col_of<LP>(xcd_block_n(S.xcd, blk, ncb)) + S.lo[KC];
+    if (c >= S.nCO) return;
+    double rw, rtp, rp, w, tm, rz, zz, exner, rb, rtb, exb, gamma_old;
+    gather2<LP>(fd(S, F_rw), c, fd(S, F_rtheta_p), c, k, rw, rtp);
+    gather2<LP>(fd(S, F_rho_p), c, fd(S, F_w), c, k, rp, w);
+    gather2<LP>(fd(S, F_theta_m), c, fd(S, F_rho_zz), c, k, tm, rz);
+    gather2<LP>(fd(S, F_zz), c, fd(S, F_exner), c, k, zz, exner);
+    gather2<LP>(fd(S, F_rho_base), c, fd(S, F_rtheta_base), c, k, rb, rtb);
+    gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
+    const double coftz_old = colk(fd(S, F_coftz), c);
+    // :773-777 the save copies (every level but L; padding levels carry zeros either way)
+    const bool cp = k != L;
+    put2<LP>(fw(S, F_rw_save), c, fw(S, F_rtheta_p_save), c, k, PADW(rw), PADW(rtp), cp, cp);
+    put2<LP>(fw(S, F_rho_p_save), c, fw(S, F_w_2), c, k, PADW(rp), PADW(w), cp, cp);
+    put2<LP>(fw(S, F_theta_m_2), c, fw(S, F_rho_zz_2), c, k, PADW(tm), PADW(rz), cp, cp);
+    if (cp) colk(fw(S, F_rho_zz_old_split), c) = PADW(rz);
+    // :473-489 (k_moist's expressions): qtot = 0; cqw(k > 0) from the two zeroed qtot
+    const double q_k = 0.0, q_km1 = 0.0, qtotal = 0.5 * (q_k + q_km1);
+    const double cqw = k > L ? 0.0 : 1.0 / (1.0 + qtotal), qtot = 0.0;
+    put2<LP>(fw(S, F_qtot), c, fw(S, F_cqw), c, k, qtot, cqw, cp, cp && k > 0);
+    // (cqw is used at 0 < k < L only, qtot at k < L: the values just written)
+    vi_column<LP, false>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2);
+}
+template <int LP>
+static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts) {
+    if (S.physics) return hipErrorInvalidValue;  // (srk3 asks in the reference semantics only)
+    double dtseps = .5 * dts * (1.0 + kEpssm);
+    double rcv = kRgas / (kCp - kRgas);
+    double c2 = kCp * rcv;
+    const int ncb = col_blocks<LP>(S, KC), neb = col_blocks<LP>(S, KE);
+    if (ncb + neb) k_setup_vi<LP><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2);
+    HALO_WROTE(S, F_ru_save, F_u_2, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2,
+               F_rho_zz_old_split, F_qtot, F_cqw);
+    HALO_WROTE(S, F_coftz, F_cofwt, F_gamma_tri, F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri);
+    return hipGetLastError();
+}
+hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts) {
+    MPAS_LP_DISPATCH(S.LP, setup_vi_lp, S, st, dts);
+}
+
 template <int LP>
 static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
     double dtseps = .5 * dts * (1.0 + kEpssm);

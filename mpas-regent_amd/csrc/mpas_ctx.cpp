@@ -89,6 +89,7 @@ struct mpas_ctx {
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     int overlap = 1;   // option "overlap": halo exchanges beside interior compute
+    int fusesetup = 1;  // option "fusesetup": stage 0's setup, moist and vert_imp in one launch (same values)
     int fusedamp = 1;  // option "fusedamp": atm_srk3 applies each divergence damping inside the next
                        // acoustic launch (reference semantics, undecomposed; same bits)
     void* raw[X_COUNT] = {};  // the allocations behind S.f (S.f[f] = raw[f] + stagger)
@@ -631,9 +632,14 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             return e;
         });
     }
-    run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
-    run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
-    run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
+    if (c->fusesetup && S.physics == 0) {  // :404-417 as one column-local launch (same values)
+        run_task(c, "atm_rk_integration_setup[+moist+vert_imp]",
+                 [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0]); });
+    } else {
+        run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
+        run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
+        run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
+    }
     // option fusedamp (reference semantics, undecomposed): each damping but the step's last
     // is applied by the next acoustic launch (k_acoustic MODE 2), the last from the div
     // the acoustic step stored (launch_div_damping_div); the same bits as the separate task
@@ -906,6 +912,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         if (name && std::strcmp(name, "exact") == 0) c->exact = value ? 1 : 0;
         else if (name && std::strcmp(name, "graph") == 0) c->graph_on = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp") == 0) c->fusedamp = value ? 1 : 0;
+        else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
         else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
@@ -980,6 +987,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         }
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "fusedamp") == 0) *value = c->fusedamp;
+        else if (name && std::strcmp(name, "fusesetup") == 0) *value = c->fusesetup;
         else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
         else if (name && std::strcmp(name, "halo_state") == 0) {  // hash of the halo bookkeeping (debug)
             uint64_t hsh = 1469598103934665603ull;

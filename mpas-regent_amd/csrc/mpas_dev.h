@@ -179,6 +179,8 @@ inline int col_blocks_n(const DevState& S, int kind) {
 hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st);
 hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st);
 hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts);
+// setup + moist + vert_imp(dts) in one launch (option "fusesetup", reference semantics)
+hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts);
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
 // mode (reference semantics, no halo; atm_srk3 with option "fusedamp"): 0 plain, 1 also

@@ -14,8 +14,14 @@ roofline.achieved divides by the measured launch time.
 """
 
 # name -> (reads, writes); each a list of field names of the registry
-def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False):
+def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
+    if task == "atm_rk_integration_setup" and fused:  # option fusesetup: + moist + vert_imp, one launch
+        parts = [_sets(t) for t in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
+                                    "atm_compute_vert_imp_coefs")]
+        writes = sorted(set(w for _, ws in parts for w in ws))
+        reads = sorted(set(r for rs, _ in parts for r in rs) - set(writes) | {"gamma_tri"})
+        return reads, writes
     if task == "atm_rk_integration_setup":
         return (["rho_p", "rho_zz", "rtheta_p", "rw", "theta_m", "w", "ru", "u"],
                 ["rho_p_save", "rho_zz_2", "rho_zz_old_split", "rtheta_p_save", "rw_save", "theta_m_2", "w_2",
@@ -139,7 +145,7 @@ def b_alg(task, dims, **kw):
     return sum(fb(x) for x in set(reads)) + sum(fb(x) for x in set(writes))
 
 
-def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False):
+def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -166,8 +172,11 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False):
         if transport:
             out += [("scalars_save", {}, 1), ("atm_advance_scalars_mono", {}, 1)]
         return out
-    out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
-           ("atm_compute_vert_imp_coefs", {}, 2)]
+    if fusesetup:
+        out = [("atm_rk_integration_setup", {"fused": True}, 1), ("atm_compute_vert_imp_coefs", {}, 1)]
+    else:
+        out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
+               ("atm_compute_vert_imp_coefs", {}, 2)]
     if schedule == 1:
         out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
     if fusedamp:
@@ -187,5 +196,6 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False):
     return out
 
 
-def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False):
-    return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp))
+def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False):
+    return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
+                                                                        fusesetup))

@@ -431,11 +431,12 @@ def test_upload_rejects_overlong_lists(x1_2562, field, width):
 
 
 # ---- option fusedamp: the damping inside the next acoustic launch ------------------------
-def _two_steps_gpu(st, fusedamp, exact, graph=1):
+def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None):
     got = st.copy()
     with lib.Context(*st.dims()) as ctx:
         ctx.set_option("exact", exact)
         ctx.set_option("fusedamp", fusedamp)
+        ctx.set_option("fusesetup", fusedamp if fusesetup is None else fusesetup)
         ctx.set_option("graph", graph)
         ctx.upload(st)
         assert ctx.get_option("fusedamp_active") == fusedamp
@@ -452,10 +453,10 @@ def _two_steps_gpu(st, fusedamp, exact, graph=1):
 @pytest.mark.parametrize("variant", ["random", "ref", "mpas0"])
 def test_fusedamp_bit_identical(x1_2562, L, variant):
     """atm_srk3 with six of its seven dampings applied inside the next acoustic launch
-    (k_acoustic MODE 2: the same expression on the same values) is value-identical to the
-    separate atm_divergence_damping_3d launches and to the oracle, in exact mode and on the
-    fast path; raw 1-based ids leave edge 0 listed by no cell (an orphan, written by the
-    launch's extra blocks)"""
+    (k_acoustic MODE 2: the same expression on the same values) and stage 0's setup, moist
+    and vert_imp in one launch (k_setup_vi) is value-identical to the separate launches and
+    to the oracle, in exact mode and on the fast path; raw 1-based ids leave edge 0 listed
+    by no cell (an orphan, written by the launch's extra blocks)"""
     st = base_state(x1_2562, L, variant)
     ref = run_oracle(st, lambda o: (o.atm_srk3(720.0, 0), o.atm_srk3(360.0, 1), o.atm_srk3(360.0, 1)))
     got1, orph = _two_steps_gpu(st, 1, 1)
@@ -470,6 +471,9 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
         b, _ = _two_steps_gpu(st, 0, 0, graph)
         bad = compare_states(a, b, rtol=0.0)
         assert not bad, f"fusedamp fast path vs separate damping (graph={graph}): {bad[:6]}"
+    c, _ = _two_steps_gpu(st, 0, 0, 1, fusesetup=1)
+    bad = compare_states(c, b, rtol=0.0)
+    assert not bad, f"fusesetup alone vs separate launches: {bad[:6]}"
 
 
 def test_fusedamp_dt_zero(x1_2562):

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-3 profile: kernel trace + stats of the headline bench, small-mesh lines
+set -e
+OUT=${1:-gpurun_out/r03p}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o kt --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --traffic off > "$OUT/trace.log" 2>&1
+for n in 2562 40962; do
+  timeout -k 10 200 python3 bench.py --ncells $n --steps 50 --warmup 5 --no-cpu-baseline --traffic off > "$OUT/bench_x1.${n}.json" 2>> "$OUT/bench.err"
+done
+timeout -k 10 300 python3 bench.py --transport --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_transport.json" 2>> "$OUT/bench.err"
