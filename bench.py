@@ -282,6 +282,8 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_advance_acoustic_step_work[ss>0]": {"small_step": 1},
              "atm_advance_acoustic_step_work[ss0+damp]": {"small_step": 0, "damp": True},
              "atm_rk_integration_setup[+moist+vert_imp]": {"fused": True},
+             "atm_advance_acoustic_step_work[ss0+sml]": {"small_step": 0, "sml": True},
+             "atm_advance_acoustic_step_work[ss0+sml+damp]": {"small_step": 0, "damp": True, "sml": True},
              "atm_advance_acoustic_step_work[ss>0+damp]": {"small_step": 1, "damp": True},
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
              "atm_recover_large_step_variables_work[rk2]": {"rk_step": 2}}
@@ -496,7 +498,8 @@ def main():
                     "rk_step 0 and rk_step > 0 launches); frac = achieved / peak"}
     fused = bool(ctx.get_option("fusedamp_active"))
     fsetup = bool(ctx.get_option("fusesetup")) and not args.physics
-    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup)
+    fsml = fused and bool(ctx.get_option("fusesml"))
+    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -519,7 +522,8 @@ def main():
                       "dt": dt, "parallelism": (f"decomposed{world}" if decomposed else
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
-                      "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup)},
+                      "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup),
+                      "fusesml": int(fsml), "tmedge": int(fused and bool(ctx.get_option("tmedge")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}
     if halo_info:

@@ -41,16 +41,22 @@ namespace mpas {
 // levels (level L copied, padding 0); the edges no cell lists are written by ncb.. extra
 // blocks (X_orph).  The damping launch between two substeps disappears: its ru_p
 // read-modify-write and its cell gathers (theta_m is gathered here anyway).
+// t12 = theta_m(cell1) + theta_m(cell2) (the same value as t2 + t1: X_tme)
 template <int LP>
-__device__ __forceinline__ double damp_edge(double rup, double d1, double d2, double t1, double t2, double spec,
-                                            double coef, bool on) {
-    return on ? rup + coef * (d2 - d1) * (1.0 - spec) / (t1 + t2) : rup;  // (:1757-1759 order)
+__device__ __forceinline__ double damp_edge(double rup, double d1, double d2, double t12, double spec, double coef,
+                                            bool on) {
+    return on ? rup + coef * (d2 - d1) * (1.0 - spec) / t12 : rup;  // (:1757-1759 order)
 }
 
-template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE>
+// TME (atm_srk3, option "tmedge"): theta_m(cell2) + theta_m(cell1) of each edge comes from
+// X_tme, which the stage's dyn_tend edge kernel formed (theta_m is not written in between):
+// one gathered column per edge instead of two -- the same sums
+// SML (atm_srk3, option "fusesml"; a stage's first substep): the stage's set_smlstep first
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm,
                                                  double coefp, int ncb) {
     static_assert(!(MPASV && MODE), "the deferred damping is the reference semantics' (physics 0)");
+    static_assert(!SML || (FIRST && !MPASV), "set_smlstep precedes a stage's first substep (reference semantics)");
     const int L = S.L, k = (int)(threadIdx.x % LP);
     int blk = (int)blockIdx.x;
     if constexpr (MODE == 2) {
@@ -61,9 +67,9 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
             const int c1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], c2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
             const double *dvi = fd(S, X_dvB), *tmf = fd(S, F_theta_m);
             const double ru = colk(fd(S, F_ru_p), e), d1 = colk(dvi, c1), d2 = colk(dvi, c2);
-            const double t1 = colk(tmf, c1), t2 = colk(tmf, c2);
+            const double t12 = TME ? colk(fd(S, X_tme), e) : colk(tmf, c1) + colk(tmf, c2);
             const bool on = k < L && !(fi(S, F_isShared)[c1] && fi(S, F_isShared)[c2]);
-            colk(fw(S, X_rupB), e) = PADW(damp_edge<LP>(ru, d1, d2, t1, t2, fd(S, F_specZoneMaskEdge)[e], coefp, on));
+            colk(fw(S, X_rupB), e) = PADW(damp_edge<LP>(ru, d1, d2, t12, fd(S, F_specZoneMaskEdge)[e], coefp, on));
             return;
         }
     }
@@ -87,7 +93,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     const double *ru_p = fd(S, F_ru_p), *tm_f = fd(S, F_theta_m);
     const int *coth = fi(S, X_ce_oth) + (size_t)c * 10, *cs1 = fi(S, X_ce_s1) + (size_t)c * 10;
     int e_[NF], c1_[NF], c2_[NF], o_[NF], s1_[NF];
-    double sgn_[NF], cdv_[NF], rup_[NF], t1_[NF], t2_[NF];
+    double sgn_[NF], cdv_[NF], rup_[NF], t1_[NF], t2_[NF], ts_[NF];  // ts_: theta_m(cell2) + theta_m(cell1)
     const int ne = SELF ? cell_rec<true>(S, c, e_, o_, s1_) : cell_rec<false>(S, c, e_, c1_, c2_);
     row_ld(sgn, sgn_);
     row_ld(cdv, cdv_);
@@ -104,7 +110,13 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
 #pragma unroll
     for (int i = 0; i < NF; i += 2) {
         gather2s<LP>(ru_p, e_[i], e_[i + 1], k, rup_[i], rup_[i + 1]);
-        cell_pair2<LP, SELF>(tm_f, c1_, c2_, o_, s1_, tm, i, k, t1_[i], t2_[i], t1_[i + 1], t2_[i + 1]);
+        if constexpr (TME) {
+            gather2s<LP>(fd(S, X_tme), e_[i], e_[i + 1], k, ts_[i], ts_[i + 1]);
+        } else {
+            cell_pair2<LP, SELF>(tm_f, c1_, c2_, o_, s1_, tm, i, k, t1_[i], t2_[i], t1_[i + 1], t2_[i + 1]);
+            ts_[i] = t2_[i] + t1_[i];
+            ts_[i + 1] = t2_[i + 1] + t1_[i + 1];
+        }
     }
     int own = 0;
     if constexpr (MODE == 2) {  // the previous substep's damping on this cell's edges
@@ -122,21 +134,60 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
         for (int i = 0; i < NF; i++) {
             const int x1 = SELF ? (s1_[i] ? c : o_[i]) : c1_[i], x2 = SELF ? (s1_[i] ? o_[i] : c) : c2_[i];
             const bool on = kl && e_[i] < S.nEdges && !(sh[x1] && sh[x2]);
-            rup_[i] = damp_edge<LP>(rup_[i], d1_[i], d2_[i], t1_[i], t2_[i], spz[e_[i]], coefp, on);
+            rup_[i] = damp_edge<LP>(rup_[i], d1_[i], d2_[i], ts_[i], spz[e_[i]], coefp, on);
             if ((own >> i) & 1) colk(rup_out, e_[i]) = PADW(rup_[i]);  // (level L: the value read)
         }
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         rup_[i] = ldz(kl, rup_[i]);
-        t1_[i] = ldz(kl, t1_[i]);
-        t2_[i] = ldz(kl, t2_[i]);
+        ts_[i] = ldz(kl, ts_[i]);
     }
     col_rd2<LP>(fd(S, F_w), fd(S, F_coftz), c, k, L, w, coftz);
+    col_rd2<LP>(fd(S, F_zz), fd(S, F_rho_zz), c, k, L, zz, rz);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    if constexpr (SML) {
+        // the stage's atm_set_smlstep_pert_variables_work (:1503-1528, k_set_smlstep's
+        // expressions) on this column, just before the substep reads w: the points of cpr
+        // (cprMask) within the relaxation zone get w -= sum of the slope fluxes of u_tend,
+        // w *= the zz average; the acoustic step then works on that w
+        const double* ut_f = fd(S, F_u_tend);
+        const double *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
+        const double* sgnc = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+        double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgs_[NF];
+        row_ld(sgnc, sgs_);
+#pragma unroll
+        for (int i = 0; i < NF; i += 2) gather2s<LP>(ut_f, e_[i], e_[i + 1], k, ut_[i], ut_[i + 1]);
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            ut_[i] = ldz(k <= L, ut_[i]);
+            gather2<LP>(zb, c * 10 + i, zb3, c * 10 + i, k, zb_[i], zb3_[i]);  // (one 16-B load)
+        }
+#pragma unroll
+        for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
+        double wn = w;
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            double flux = sgs_[i] * (fzm * ut_[i] + fzp * utm_[i]);
+            wn = sub_if(i < ne, wn, (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux);
+        }
+        for (int i = NF; i < ne; i++) {
+            int iEdge = eoc[i];
+            double ut = col_rd<LP>(ut_f, iEdge, k, L);
+            double ut_m = lvl_dn<LP>(ut, k);
+            double flux = sgnc[i] * (fzm * ut + fzp * ut_m);
+            size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
+            wn -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+        }
+        wn *= (fzm * zz + fzp * lvl_dn<LP>(zz, k));
+        if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) {
+            colk(fw(S, F_w), c) = wn;
+            w = wn;
+        }
+    }
     // the w tendency: the state w in the reference and under physics = 1 (Q8), tend_w under
     // the MPAS dynamics (physics = 2); the implicit Rayleigh term reads the state w
     const double tw = (MPASV && S.physics == 2) ? col_rd<LP>(fd(S, F_tend_w), c, k, L) : w;
-    col_rd2<LP>(fd(S, F_zz), fd(S, F_rho_zz), c, k, L, zz, rz);
     col_rd2<LP>(fd(S, F_cofwt), fd(S, F_cofwz), c, k, L, cofwt, cofwz);
     col_rd2<LP>(fd(S, F_cofwr), fd(S, F_a_tri), c, k, L, cofwr, a_tri);
     col_rd2<LP>(fd(S, F_alpha_tri), fd(S, F_rw_save), c, k, L, alpha, rws);
@@ -145,7 +196,6 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     if constexpr (MPASV) col_rd2<LP>(fd(S, F_gamma_tri), fd(S, F_tend_theta), c, k, L, gam, tend_th);
     const double tt = MPASV ? tend_th : tm;  // tend_rt: the reference reads theta_m (Q8)
     const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
-    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
 
     // :1615-1636
     const double rtpo = (small_step == 0) ? 0 : rtp;
@@ -186,14 +236,14 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     for (int i = 0; i < NF; i++) {
         double flux = sgn_[i] * dts * cdv_[i] * rup_[i] * invA;
         rs = sub_if(i < ne && kl, rs, flux);
-        ts = sub_if(i < ne && kl, ts, flux * 0.5 * (t2_[i] + t1_[i]));
+        ts = sub_if(i < ne && kl, ts, flux * 0.5 * ts_[i]);
     }
     for (int i = NF; i < ne; i++) {
         double rpe = colk(ru_p, eoc[i]);
         if constexpr (MODE == 2) {
             const int e = eoc[i], x1 = cc1[i], x2 = cc2[i];
             const bool on = kl && e < S.nEdges && !(fi(S, F_isShared)[x1] && fi(S, F_isShared)[x2]);
-            rpe = damp_edge<LP>(rpe, colk(fd(S, X_dvB), x1), colk(fd(S, X_dvB), x2), colk(tm_f, x1), colk(tm_f, x2),
+            rpe = damp_edge<LP>(rpe, colk(fd(S, X_dvB), x1), colk(fd(S, X_dvB), x2), colk(tm_f, x1) + colk(tm_f, x2),
                                 fd(S, F_specZoneMaskEdge)[e], coefp, on);
             if ((own >> i) & 1) colk(fw(S, X_rupB), e) = PADW(rpe);
         }
@@ -378,7 +428,9 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
 
 template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                              double coef_prev) {
+                              double coef_prev, int tme, int sml) {
+    if ((tme || sml) && (S.physics || S.halo)) return hipErrorInvalidValue;  // (atm_srk3 only, reference semantics)
+    if (sml && (small_step != 0 || mode == 0)) return hipErrorInvalidValue;
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
     if (mode && (S.physics || S.halo)) return hipErrorInvalidValue;  // (srk3 never asks: reference semantics only)
@@ -399,15 +451,26 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
         auto go = [&](auto ex, auto sf, auto md) {
             constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
             constexpr int M = decltype(md)::value;
+#define MPAS_AC(FI, MP, MM, TM, SM) \
+    k_acoustic<LP, E, SF, FI, MP, MM, TM, SM><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb)
             if constexpr (M == 0) {
                 if (X.physics) {
-                    if (first) k_acoustic<LP, E, SF, true, true, 0><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
-                    else k_acoustic<LP, E, SF, false, true, 0><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
+                    if (first) MPAS_AC(true, true, 0, false, false);
+                    else MPAS_AC(false, true, 0, false, false);
                     return;
                 }
+                if (tme) first ? MPAS_AC(true, false, 0, true, false) : MPAS_AC(false, false, 0, true, false);
+                else first ? MPAS_AC(true, false, 0, false, false) : MPAS_AC(false, false, 0, false, false);
+            } else {
+                if (first) {
+                    if (tme) sml ? MPAS_AC(true, false, M, true, true) : MPAS_AC(true, false, M, true, false);
+                    else sml ? MPAS_AC(true, false, M, false, true) : MPAS_AC(true, false, M, false, false);
+                } else {
+                    if (tme) MPAS_AC(false, false, M, true, false);
+                    else MPAS_AC(false, false, M, false, false);
+                }
             }
-            if (first) k_acoustic<LP, E, SF, true, false, M><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
-            else k_acoustic<LP, E, SF, false, false, M><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb);
+#undef MPAS_AC
         };
         auto go_m = [&](auto ex, auto sf) {
             if (mode == 1) go(ex, sf, std::integral_constant<int, 1>{});
@@ -426,8 +489,8 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                           double coef_prev) {
-    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev);
+                           double coef_prev, int tme, int sml) {
+    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml);
 }
 
 }  // namespace mpas

@@ -49,7 +49,7 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 }
 
 struct DynK {
-    int rk_step, horiz_mixing, rayleigh, exact_q;
+    int rk_step, horiz_mixing, rayleigh, exact_q, tme;
     double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
 };
 
@@ -398,6 +398,17 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     // ---- Rayleigh damping (:1152-1159)
     if (a.rayleigh && k > L - kRayleighLevels + 1)
         tend_u -= rho_edge * u * (((double)k - (double)(L - kRayleighLevels)) * a.rayleigh_inv);
+    if (a.tme) {  // X_tme for the stage's acoustic substeps: theta_m(cell2) + theta_m(cell1)
+        double t2pt1;
+        if (na >= 2 && ad_[0] == cell1 && ad_[1] == cell2) {  // (the adv list starts with the two cells)
+            t2pt1 = tv_[1] + tv_[0];
+        } else {
+            double t1, t2;
+            gather2s<LP>(tm_f, cell1, cell2, k, t1, t2);
+            t2pt1 = t2 + t1;
+        }
+        if (k != L) colk(fw(S, X_tme), e) = PADW(t2pt1);
+    }
     if constexpr (HF) {  // every lane stores (paired 16-B stores); level L keeps its value
         double* Fo = fw(S, X_F);
         double* tuo = fw(S, F_tend_u);
@@ -827,6 +838,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     a.horiz_mixing = in.horiz_mixing;
     a.rayleigh = in.rayleigh_damp_u;
     a.exact_q = in.exact_q;
+    a.tme = in.tme && !S.halo;
     const double invDt = 1.0 / in.dt;
     const double c_s = kSmagCoef;
     a.cs_l2 = (c_s * kLenDisp) * (c_s * kLenDisp);

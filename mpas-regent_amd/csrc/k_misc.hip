@@ -394,7 +394,7 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPA
 // -(r - 0.0) is the same value as the literal expression gives
 // DIVB (option fusedamp, the step's last damping): the cells' div = -(rtheta_pp -
 // rtheta_pp_old) comes from the acoustic step's X_dvB (the same subtraction, made there)
-template <int LP, int EPW, bool OLD0, bool DIVB = false>
+template <int LP, int EPW, bool OLD0, bool DIVB = false, bool TME = false>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
     ColMapN<LP, EPW> m(S, KE);
     const int L = S.L, k = m.k;
@@ -425,7 +425,12 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
             if (OLD0) ro1[i] = ro2[i] = 0.0;
             else gather2s<LP>(rtpo, c1[i], c2[i], k, ro1[i], ro2[i]);
         }
-        gather2s<LP>(tm, c1[i], c2[i], k, t1[i], t2[i]);
+        if (TME) {  // theta_m(cell2) + theta_m(cell1) from X_tme (atm_srk3, option tmedge)
+            t1[i] = colk(fd(S, X_tme), min(m.base + i, S.nEO - 1));
+            t2[i] = 0.0;
+        } else {
+            gather2s<LP>(tm, c1[i], c2[i], k, t1[i], t2[i]);
+        }
     }
 #pragma unroll
     for (int i = 0; i < EPW; i++) {
@@ -433,7 +438,7 @@ __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdam
         if (e >= S.nEO || k >= L || (sh1[i] && sh2[i])) continue;
         double divCell1 = DIVB ? r1[i] : -(r1[i] - ro1[i]);
         double divCell2 = DIVB ? r2[i] : -(r2[i] - ro2[i]);
-        colk(rup, e) = ru[i] + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec[i]) / (t1[i] + t2[i]);
+        colk(rup, e) = ru[i] + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec[i]) / (TME ? t1[i] : t1[i] + t2[i]);
     }
 }
 double divdamp_coef(double dts) {  // :1736-1738
@@ -442,15 +447,16 @@ double divdamp_coef(double dts) {  // :1736-1738
     return 2.0 * smdiv * kLenDisp * rdts;
 }
 template <int LP>
-static hipError_t divdamp_div_lp(const DevState& S, hipStream_t st, double dts) {
+static hipError_t divdamp_div_lp(const DevState& S, hipStream_t st, double dts, int tme) {
     if (S.halo || S.physics) return hipErrorInvalidValue;  // (the fused path's; srk3 never asks otherwise)
     const double coef_divdamp = divdamp_coef(dts);
     const int nb = col_blocks_n<LP, 2>(S, KE);
-    if (nb) k_div_damp<LP, 2, false, true><<<nb, 256, 0, st>>>(S, coef_divdamp);
+    if (nb && tme) k_div_damp<LP, 2, false, true, true><<<nb, 256, 0, st>>>(S, coef_divdamp);
+    else if (nb) k_div_damp<LP, 2, false, true><<<nb, 256, 0, st>>>(S, coef_divdamp);
     return hipGetLastError();
 }
-hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts) {
-    MPAS_LP_DISPATCH(S.LP, divdamp_div_lp, S, st, dts);
+hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts, int tme) {
+    MPAS_LP_DISPATCH(S.LP, divdamp_div_lp, S, st, dts, tme);
 }
 template <int LP>
 static hipError_t divdamp_lp(const DevState& S, hipStream_t st, double dts, int old_zero) {

@@ -10,6 +10,8 @@
 #include "mpas_dev.h"
 #include "mpas_halo.h"
 
+#include <type_traits>
+
 namespace mpas {
 
 // MD: the MPAS dynamics (physics = 2, ora_mpas_solve_diagnostics): divergence += s * u (Q9),
@@ -44,7 +46,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
 #pragma unroll
         for (int j = 0; j < EPW; j++) {
             const int v = m.base + j;
-            if (v >= S.nVO || k == L) continue;  // (padding levels: zeros, PADW)
+            if (v >= S.nVO) break;  // (wave-uniform; padding levels: zeros, PADW)
             double vort = 0.0;
 #pragma unroll
             for (int i = 0; i < 3; i++) {
@@ -52,8 +54,9 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
                 vort += s * u_[j][i];
             }
             vort *= iat[j];
-            colk(fw(S, F_vorticity), v) = PADW(vort);
-            colk(fw(S, F_pv_vertex), v) = PADW(fv[j] + vort);
+            // (one paired 16-B store, every lane; level L keeps its value)
+            put2<LP>(fw(S, F_vorticity), v, fw(S, F_pv_vertex), v, k, PADW(vort), PADW(fv[j] + vort), k != L, k != L);
+            if (k == L) continue;
             if (hollingsworth_part) {
                 double r = 0.25 * iat[j];
                 double kes[3];
@@ -89,7 +92,7 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
 #pragma unroll
     for (int j = 0; j < EPW; j++) {
         const int c = c0 + j;
-        if (c >= S.nCO || k == L) continue;  // (padding levels: zeros, PADW)
+        if (c >= S.nCO) break;  // (wave-uniform; padding levels: zeros, PADW)
         double div = 0.0, ke = 0.0;
 #pragma unroll
         for (int i = 0; i < NF; i++) {
@@ -115,8 +118,8 @@ __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int holli
         }
         div *= invA[j];
         ke *= invA[j];
-        colk(fw(S, F_divergence), c) = PADW(div);
-        colk(fw(S, F_ke), c) = PADW(ke);
+        // (one paired 16-B store, every lane; level L keeps its value)
+        put2<LP>(fw(S, F_divergence), c, fw(S, F_ke), c, k, PADW(div), PADW(ke), k != L, k != L);
     }
 }
 
@@ -140,52 +143,68 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
     colk(fw(S, F_ke), c) = ke;
 }
 
-template <int LP, bool RECON_V, bool MD>
+// EPW consecutive edges per column slot (option "epw"): the loads of all of them are issued
+// before the first store; the paired 16-B stores write h_edge with ke_edge and pv_edge with
+// v (or alone) -- every lane takes part (put2), level L keeps its value
+template <int LP, bool RECON_V, bool MD, int EPW>
 __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
-    ColMap<LP> m(S, KE);
-    const int L = S.L, e = m.ent, k = m.k;
-    if (e >= S.nEO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
-    const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
-    const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
+    ColMapN<LP, EPW> m(S, KE);
+    const int L = S.L, k = m.k;
     const double *h = fd(S, MD ? F_rho_zz : F_h), *u = fd(S, F_u), *pvv = fd(S, F_pv_vertex);
-    // every load before the first store (the stores could alias them for the compiler)
-    double h1, h2, uu, pv1, pv2;
-    gather2s<LP>(h, coe[0], coe[1], k, h1, h2);
-    gather2s<LP>(pvv, voe[0], voe[1], k, pv1, pv2);
-    const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
-    const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
-    const int neoe = RECON_V ? fi(S, F_nEdgesOnEdge)[e] : 0;
-    int ee_[QF];
-    double ue[QF], wts_[QF];
-    if (RECON_V) {
-        row_ld(eoe, ee_);
-        row_ld(wts, wts_);
-        static_assert(QF == 10, "pairs below");
-        if (MD) {
+    double h1[EPW], h2[EPW], uu[EPW], pv1[EPW], pv2[EPW], vv[EPW];
+    int ee[EPW];
 #pragma unroll
-            for (int i = 0; i < QF; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
-            uu = colk(u, e);
+    for (int j = 0; j < EPW; j++) {
+        const int e = min(m.base + j, S.nEO - 1);
+        ee[j] = e;
+        const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
+        const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
+        gather2s<LP>(h, coe[0], coe[1], k, h1[j], h2[j]);
+        gather2s<LP>(pvv, voe[0], voe[1], k, pv1[j], pv2[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < EPW; j++) {
+        const int e = ee[j];
+        vv[j] = 0.0;
+        if (RECON_V) {
+            const int* eoe = fi(S, F_edgesOnEdge_ECP) + (size_t)e * 20;
+            const double* wts = fd(S, F_weightsOnEdge) + (size_t)e * 20;
+            const int neoe = fi(S, F_nEdgesOnEdge)[e];
+            int ee_[QF];
+            double ue[QF], wts_[QF];
+            row_ld(eoe, ee_);
+            row_ld(wts, wts_);
+            static_assert(QF == 10, "pairs below");
+            if (MD) {
+#pragma unroll
+                for (int i = 0; i < QF; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
+                uu[j] = colk(u, e);
+            } else {
+#pragma unroll
+                for (int i = 1; i < QF - 1; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
+                gather2s<LP>(u, ee_[QF - 1], e, k, ue[QF - 1], uu[j]);
+            }
+            double v = 0;  // Q23: the sum starts at i = 1
+#pragma unroll
+            for (int i = MD ? 0 : 1; i < QF; i++) v = add_if(i < neoe, v, wts_[i] * ue[i]);
+            for (int i = QF; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
+            vv[j] = v;
         } else {
-#pragma unroll
-            for (int i = 1; i < QF - 1; i += 2) gather2s<LP>(u, ee_[i], ee_[i + 1], k, ue[i], ue[i + 1]);
-            gather2s<LP>(u, ee_[QF - 1], e, k, ue[QF - 1], uu);
+            uu[j] = colk(u, e);
         }
-    } else {
-        uu = colk(u, e);
     }
-    if (k == L) return;  // (padding levels k > L: zeros, PADW)
-    colk(fw(S, F_h_edge), e) = PADW(0.5 * (h1 + h2));
-    if (MD) colk(fw(S, F_rho_edge), e) = PADW(0.5 * (h1 + h2));
-    const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
-    colk(fw(S, F_ke_edge), e) = PADW(efac * (uu * uu));
-    if (RECON_V) {  // Q23: the sum starts at i = 1
-        double v = 0;
 #pragma unroll
-        for (int i = MD ? 0 : 1; i < QF; i++) v = add_if(i < neoe, v, wts_[i] * ue[i]);
-        for (int i = QF; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
-        colk(fw(S, F_v), e) = PADW(v);
+    for (int j = 0; j < EPW; j++) {
+        const int e = m.base + j;
+        if (e >= S.nEO) break;  // (wave-uniform)
+        const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
+        const bool w = k != L;  // (padding levels k > L: zeros, PADW)
+        put2<LP>(fw(S, F_h_edge), e, fw(S, F_ke_edge), e, k, PADW(0.5 * (h1[j] + h2[j])), PADW(efac * (uu[j] * uu[j])),
+                 w, w);
+        if (MD && w) colk(fw(S, F_rho_edge), e) = PADW(0.5 * (h1[j] + h2[j]));
+        if (RECON_V) put2<LP>(fw(S, F_v), e, fw(S, F_pv_edge), e, k, PADW(vv[j]), PADW(0.5 * (pv1[j] + pv2[j])), w, w);
+        else if (w) colk(fw(S, F_pv_edge), e) = PADW(0.5 * (pv1[j] + pv2[j]));
     }
-    colk(fw(S, F_pv_edge), e) = PADW(0.5 * (pv1 + pv2));
 }
 
 template <int LP, bool MD>
@@ -207,10 +226,17 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
         if (nb) k_solve_holl<LP><<<nb, 256, 0, st>>>(X);
     };
     auto ke = [&](const DevState& X) {
-        const int nb = col_blocks<LP>(X, KE);
-        if (!nb) return;
-        if (rk_step != -1 && rk_step != 2) k_solve_e<LP, false, MD><<<nb, 256, 0, st>>>(X);
-        else k_solve_e<LP, true, MD><<<nb, 256, 0, st>>>(X);
+        const bool rv = !(rk_step != -1 && rk_step != 2);
+        auto go = [&](auto epw) {
+            constexpr int E = decltype(epw)::value;
+            const int nb = col_blocks_n<LP, E>(X, KE);
+            if (!nb) return;
+            if (rv) k_solve_e<LP, true, MD, E><<<nb, 256, 0, st>>>(X);
+            else k_solve_e<LP, false, MD, E><<<nb, 256, 0, st>>>(X);
+        };
+        if (X.epw == 4) go(std::integral_constant<int, 4>{});
+        else if (X.epw == 2) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 1>{});
     };
     // ring-1 redundancy (option ring1): the launch that runs after u is fresh on the ghosts
     // also computes the ghost vertices of owned edges (their edges are local, decomp.py),

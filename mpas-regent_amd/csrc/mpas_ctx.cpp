@@ -55,6 +55,7 @@ const FieldInfo kFields[X_COUNT] = {
     {"eown", K_C2I, 1, D_M, 0, 0},
     {"eowner", K_E2I, 1, D_M, 0, 0},
     {"orph", K_E2I, 1, D_M, 0, 0},
+    {"tme", K_E3, 1, D_M, 0, 0},
     {"Ah", K_E3, 8, D_M, 0, 0},
     {"Rp", K_C3V, 8, D_M, 0, 0},
     {"Rm", K_C3V, 8, D_M, 0, 0},
@@ -89,6 +90,8 @@ struct mpas_ctx {
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     int overlap = 1;   // option "overlap": halo exchanges beside interior compute
+    int fusesml = 1;    // option "fusesml": each stage's set_smlstep inside its first acoustic launch (with fusedamp)
+    int tmedge = 1;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values)
     int fusesetup = 1;  // option "fusesetup": stage 0's setup, moist and vert_imp in one launch (same values)
     int fusedamp = 1;  // option "fusedamp": atm_srk3 applies each divergence damping inside the next
                        // acoustic launch (reference semantics, undecomposed; same bits)
@@ -571,7 +574,9 @@ void trt_ensure(mpas_ctx* c) {
 
 // timing keys: one Regent task, split where its read/write set (B_alg) differs by argument
 // (bench.py aggregates the variants per task)
-const char* acoustic_name(int small_step, bool damp = false) {
+const char* acoustic_name(int small_step, bool damp = false, bool sml = false) {
+    if (sml)  // (option fusesml: the stage's set_smlstep run by this launch first)
+        return damp ? "atm_advance_acoustic_step_work[ss0+sml+damp]" : "atm_advance_acoustic_step_work[ss0+sml]";
     if (damp)  // (option fusedamp: the previous substep's damping applied by this launch)
         return small_step == 0 ? "atm_advance_acoustic_step_work[ss0+damp]" : "atm_advance_acoustic_step_work[ss>0+damp]";
     return small_step == 0 ? "atm_advance_acoustic_step_work[ss0]" : "atm_advance_acoustic_step_work[ss>0]";
@@ -649,6 +654,10 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     for (int r = 0; r < 3; r++) n_acoustic += number_sub_steps[r] + (S.physics ? 0 : 1);
     bool pending = false;
     double coef_prev = 0.0;
+    // option tmedge (reference semantics, undecomposed): dyn_tend's edge kernel stores
+    // theta_m(cell2) + theta_m(cell1) per edge, which the stage's acoustic substeps and the
+    // damping read instead of gathering theta_m at both cells (theta_m unchanged in between)
+    const int tme = (c->tmedge && S.physics == 0 && !c->halo) ? 1 : 0;
     for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
         if (rk_step == 1)
             run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
@@ -660,20 +669,24 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a.mix_full = 0;
         a.rayleigh_damp_u = 0;
         a.exact_q = c->exact;
+        a.tme = tme;
         run_task(c, a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]",
                  [&] { return launch_dyn_tend(S, st, a); });
-        run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
+        // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
+        const bool sml = fuse && c->fusesml;
+        if (!sml) run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
         const int n_small = number_sub_steps[rk_step] + (S.physics ? 0 : 1);  // Q5 (the MPAS form: n)
         for (int small_step = 0; small_step < n_small; small_step++) {
             const double dts = rk_sub_timestep[rk_step];
             if (fuse) {
                 const int mode = pending ? 2 : 1;
-                run_task(c, acoustic_name(small_step, pending),
-                         [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev); });
+                const int sm = (sml && small_step == 0) ? 1 : 0;
+                run_task(c, acoustic_name(small_step, pending, sm),
+                         [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev, tme, sm); });
                 if (mode == 2) fb.swap_rup();
                 fb.swap_dv();  // this substep's div is read next from X_dvB
                 if (++done_acoustic == n_acoustic) {
-                    run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping_div(S, st, dts); });
+                    run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping_div(S, st, dts, tme); });
                     pending = false;
                 } else {
                     pending = true;
@@ -681,7 +694,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                 }
                 continue;
             }
-            run_task(c, acoustic_name(small_step), [&] { return launch_acoustic(S, st, dts, small_step, c->exact); });
+            run_task(c, acoustic_name(small_step),
+                     [&] { return launch_acoustic(S, st, dts, small_step, c->exact, 0, 0.0, tme); });
             run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, dts, small_step == 0); });
         }
         if (S.physics)  // rk_timestep.rg:460, commented out in the reference (Q7)
@@ -913,6 +927,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "graph") == 0) c->graph_on = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp") == 0) c->fusedamp = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
+        else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
+        else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
         else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
@@ -988,6 +1004,8 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "fusedamp") == 0) *value = c->fusedamp;
         else if (name && std::strcmp(name, "fusesetup") == 0) *value = c->fusesetup;
+        else if (name && std::strcmp(name, "tmedge") == 0) *value = c->tmedge;
+        else if (name && std::strcmp(name, "fusesml") == 0) *value = c->fusesml;
         else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
         else if (name && std::strcmp(name, "halo_state") == 0) {  // hash of the halo bookkeeping (debug)
             uint64_t hsh = 1469598103934665603ull;

@@ -77,6 +77,9 @@ enum FieldId {
     X_eown,     // per cell: bit i set when this cell's slot i writes its edge's ru_p    C2I
     X_eowner,   // per edge: the lowest cell * 16 + slot listing it (prepare scratch)    E2I
     X_orph,     // the edges no cell lists (written by the fused launch's extra blocks)  E2I
+    X_tme,      // theta_m(cellsOnEdge(1)) + theta_m(cellsOnEdge(0)) per edge and level, formed
+                // by dyn_tend's edge kernel (option "tmedge"): theta_m does not change between
+                // a stage's dyn_tend and its acoustic substeps, which read it there   E3
     // monotonic scalar transport (k_transport.hip), one column per (entity, scalar)
     X_Ah,       // antidiffusive edge flux                                      E3 x 8
     X_Rp,       // R+ (fraction of the incoming antidiffusive flux allowed)     C3V x 8
@@ -156,6 +159,7 @@ struct DynTendArgs {
     int mix_full;
     int rayleigh_damp_u;
     int exact_q;       // 1: Q10 literal (each q term added nVertLevels times), 0: nVertLevels*term
+    int tme = 0;       // 1: the edge kernel also stores X_tme (atm_srk3, option "tmedge")
 };
 
 enum EntityKind { KC = 0, KE = 1, KV = 2 };  // DevState::lo index
@@ -187,12 +191,14 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
 // writes div of this substep (X_dvA), 2 also applies the previous substep's damping
 // (coefficient coef_prev, its div in X_dvB) to the ru_p it reads and writes the damped
 // ru_p to X_rupB; the caller swaps the buffer pairs after the launch
+// tme: theta_m at the cells of each edge from X_tme (valid: dyn_tend of this stage wrote it)
+// sml: the stage's set_smlstep first (a stage's first substep, mode 1 / 2; option fusesml)
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode = 0,
-                           double coef_prev = 0.0);
+                           double coef_prev = 0.0, int tme = 0, int sml = 0);
 // old_zero: only from srk3, right after a stage's first acoustic substep (k_div_damp OLD0)
 hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts, int old_zero = 0);
 // the damping from the div buffer X_dvB (fusedamp: the step's last substep), ru_p in place
-hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts);
+hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts, int tme = 0);
 // coef_divdamp of atm_divergence_damping_3d (:1736-1738) for dts
 double divdamp_coef(double dts);
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step);

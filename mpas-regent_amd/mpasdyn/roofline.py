@@ -14,7 +14,7 @@ roofline.achieved divides by the measured launch time.
 """
 
 # name -> (reads, writes); each a list of field names of the registry
-def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False):
+def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "atm_rk_integration_setup" and fused:  # option fusesetup: + moist + vert_imp, one launch
         parts = [_sets(t) for t in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
@@ -77,6 +77,10 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         if damp:  # option fusedamp: the previous substep's atm_divergence_damping_3d applied here
             reads += ["rtheta_pp", "rtheta_pp_old", "isShared", "specZoneMaskEdge"]
             writes += ["ru_p"]
+        if sml:  # option fusesml: the stage's atm_set_smlstep_pert_variables_work first
+            r2, w2 = _sets("atm_set_smlstep_pert_variables_work")
+            reads += r2
+            writes += w2
         return reads, writes
     if task == "atm_divergence_damping_3d":
         return (["rtheta_pp", "rtheta_pp_old", "theta_m", "ru_p", "cellsOnEdge", "isShared", "specZoneMaskEdge"],
@@ -145,7 +149,7 @@ def b_alg(task, dims, **kw):
     return sum(fb(x) for x in set(reads)) + sum(fb(x) for x in set(writes))
 
 
-def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False):
+def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -179,7 +183,12 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                ("atm_compute_vert_imp_coefs", {}, 2)]
     if schedule == 1:
         out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
-    if fusedamp:
+    if fusedamp and fusesml:
+        out += [("atm_advance_acoustic_step_work", {"small_step": 0, "sml": True}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, "sml": True}, 2),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 4),
+                ("atm_divergence_damping_3d", {}, 1)]
+    elif fusedamp:
         out += [("atm_set_smlstep_pert_variables_work", {}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 0}, 1),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True}, 2),
@@ -196,6 +205,6 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     return out
 
 
-def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False):
+def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
-                                                                        fusesetup))
+                                                                        fusesetup, fusesml))
