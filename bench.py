@@ -283,6 +283,9 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_advance_acoustic_step_work[ss0+damp]": {"small_step": 0, "damp": True},
              "atm_rk_integration_setup[+moist+vert_imp]": {"fused": True},
              "atm_advance_acoustic_step_work[ss0+sml]": {"small_step": 0, "sml": True},
+             "atm_compute_solve_diagnostics[vc]": {"part": "vc"}, "atm_compute_solve_diagnostics[e]": {"part": "e"},
+             "hfuse[damp+solve_vc]": {"pair": "damp+solve_vc"}, "hfuse[solve_e+finish]": {"pair": "solve_e+finish"},
+             "hfuse[solve_e+vert_imp]": {"pair": "solve_e+vert_imp"},
              "atm_advance_acoustic_step_work[ss0+sml+damp]": {"small_step": 0, "damp": True, "sml": True},
              "atm_advance_acoustic_step_work[ss>0+damp]": {"small_step": 1, "damp": True},
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
@@ -523,7 +526,8 @@ def main():
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup),
-                      "fusesml": int(fsml), "tmedge": int(fused and bool(ctx.get_option("tmedge")))},
+                      "fusesml": int(fsml), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
+                      "hfuse": int(bool(ctx.get_option("hfuse")) and not args.physics and not decomposed)},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}
     if halo_info:

@@ -561,8 +561,8 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
 
 // ------------------------------------------------------------------------ D (rk0, del4)
 template <int LP>
-__global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
-    ColMap<LP> m(S, KE);
+__device__ __forceinline__ void dyn_D_body(const DevState& S, const DynK& a, Blk bk) {
+    ColMap<LP> m(S, KE, bk);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;  // (k >= L after the gathers: gather2 needs every lane)
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
@@ -585,9 +585,14 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
 }
 
 // ------------------------------------------------------------------------ E (cells)
+template <int LP>
+__global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
+    dyn_D_body<LP>(S, a, this_blk());
+}
+
 template <int LP, bool RK0, bool SELF, bool MD, bool HF>
-__global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
-    ColMap<LP> m(S, KC);
+__device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk bk) {
+    ColMap<LP> m(S, KC, bk);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + lpos(LP, k);
@@ -831,6 +836,18 @@ __global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
+template <int LP, bool RK0, bool SELF, bool MD, bool HF>
+__global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
+    dyn_E_body<LP, RK0, SELF, MD, HF>(S, a, this_blk());
+}
+// D and E of rk_step 0 in one grid (option "hfuse": neither reads what the other writes)
+template <int LP, bool SELF, bool MD, bool HF>
+__global__ __launch_bounds__(256) void k_dyn_DE(DevState S, DynK a, int nb1) {
+    const int b = (int)blockIdx.x;
+    if (b < nb1) dyn_D_body<LP>(S, a, Blk{b, nb1});
+    else dyn_E_body<LP, true, SELF, MD, HF>(S, a, Blk{b - nb1, (int)gridDim.x - nb1});
+}
+
 template <int LP, bool MD>
 static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs& in) {
     DynK a;
@@ -914,12 +931,25 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         else HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, X_wc, F_theta_m);
         HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
                    F_tend_theta_euler);
-        if (del4) {
-            HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
-            HALO_WROTE(S, F_tend_u_euler, F_tend_u);
+        if (del4 && in.hfuse && !S.halo) {  // D beside E, one grid
+            const int nb1 = col_blocks<LP>(S, KE), nb = nb1 + col_blocks<LP>(S, KC);
+            auto go = [&](auto hfc) {
+                constexpr bool H = decltype(hfc)::value;
+                if (S.selfc) k_dyn_DE<LP, true, MD, H><<<nb, 256, 0, st>>>(S, a, nb1);
+                else k_dyn_DE<LP, false, MD, H><<<nb, 256, 0, st>>>(S, a, nb1);
+            };
+            if (nb) {
+                if (hf) go(std::true_type{});
+                else go(std::false_type{});
+            }
+        } else {
+            if (del4) {
+                HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
+                HALO_WROTE(S, F_tend_u_euler, F_tend_u);
+            }
+            if (hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta);  // (X_Fw: MD only written)
+            else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
         }
-        if (hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta);  // (X_Fw: MD only written)
-        else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
     } else {
         if (hf) HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_theta_m_save);
         else HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);

@@ -11,6 +11,7 @@
 // bit-identical to the oracle's.
 #include "mpas_dev.h"
 #include "mpas_halo.h"
+#include "k_cols.h"
 #include "mpas_synth.h"
 
 namespace mpas {
@@ -52,18 +53,6 @@ static int stream_grid(size_t n) {
     return (int)(g < 8192 ? (g ? g : 1) : 8192);
 }
 
-// LP = 64 streaming form: one 16-B position pair per thread (positions 2j, 2j+1 of a
-// column = levels j and j+32, mpas_dev.h lpos), every copy of the task in ONE launch
-// (blockIdx.y = copy).  The never-written level-L slot sits in pair lpos(L) >> 1 of each
-// column: that pair stores only its other element.
-struct Pair64 {
-    int pair, el;  // pair index within the column holding level L, and L's element in it
-    __host__ __device__ Pair64(int L) : pair(lpos(64, L) >> 1), el(lpos(64, L) & 1) {}
-};
-__device__ __forceinline__ void st64(double* d, size_t i, double2 v, Pair64 q) {
-    if ((int)(i & 31) != q.pair) *(double2*)(d + 2 * i) = v;
-    else d[2 * i + (1 - q.el)] = q.el ? v.x : v.y;
-}
 struct CopyList {
     const double* src[8];
     double* dst[8];
@@ -163,86 +152,6 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 // b_tri with cofwt(k-1) (Q16) and the LU recurrence alpha(k) = 1 / (b(k) - a(k) gamma(k-1)),
 // gamma(k) = c(k) alpha(k) from gamma(0) = 0 within the call (Q17), level by level
 // (a nonlinear recurrence: lane k waits for lane k-1's gamma, broadcast by a shuffle)
-// one column of atm_compute_vert_imp_coefs from its loaded inputs (k_vert_imp, and the
-// stage-0 fusion with the setup copies and the moist coefficients, k_setup_vi)
-template <int LP, bool MPASV>
-__device__ __forceinline__ void vi_column(const DevState& S, int c, int k, double zz, double exner, double tm, double cqw,
-                                          double qtot, double rb, double rtb, double rtp, double exb, double gamma_old,
-                                          double coftz_old, double dtseps, double rcv, double c2) {
-    const int L = S.L;
-    const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
-    const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
-    const double rdzw_m = k > 0 ? rdzw_a[k - 1] : 0.0;
-    const double zz_m = lvl_dn<LP>(zz, k), exner_m = lvl_dn<LP>(exner, k), tm_m = lvl_dn<LP>(tm, k);
-
-    // :550-564
-    double cofwr = 0.0, cofwz = 0.0, coftz = coftz_old, cofwt = 0.0;
-    if (k < L) {
-        if (k > 0) cofwr = .5 * dtseps * kGravity * (fzm * zz + fzp * zz_m);
-        coftz = 0.0;
-        if (k > 0) {
-            cofwz = dtseps * c2 * (fzm * zz + fzp * zz_m) * rdzu * cqw * (fzm * exner + fzp * exner_m);
-            coftz = dtseps * (fzm * tm + fzp * tm_m);
-        }
-        double qtotal = qtot;
-        cofwt = .5 * dtseps * rcv * zz * kGravity * rb / (1.0 + qtotal) * exner / ((rtb + rtp) * exb);
-    }
-    const double coftz_m = lvl_dn<LP>(coftz, k), coftz_p = lvl_up<LP>(coftz, k);
-    const double cofwt_m = lvl_dn<LP>(cofwt, k);
-    const double gamma_dn = lvl_dn<LP>(gamma_old, k);  // shuffle outside any branch
-    const double gamma_m = (k == 1) ? 0.0 : gamma_dn;  // Q17: gamma(0) was just zeroed
-    const double cofrz = dtseps * rdzw, cofrz_m = dtseps * rdzw_m;      // :537-539
-
-    // :566-578 (every lane; used at 0 < k < L)
-    const double a = -1.0 * cofwz * coftz_m * rdzw_m * zz_m + cofwr * cofrz_m - cofwt_m * coftz_m * rdzw_m;
-    const double b = MPASV ? 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) -
-                                 coftz * (cofwt * rdzw - cofwt_m * rdzw_m) + cofwr * ((cofrz - cofrz_m))
-                           : 1.0 + cofwz * (coftz * rdzw * zz + coftz * rdzw_m * zz_m) -
-                                 coftz * (cofwt * rdzw - cofwt * rdzw_m) + cofwr * ((cofrz - cofrz_m));  // Q16 literal
-    const double cc = -1.0 * cofwz * coftz_p * rdzw * zz - cofwr * cofrz + cofwt * coftz_p * rdzw;
-    double alpha, gamma;
-    if constexpr (MPASV) {
-        double gp = 0.0;
-        alpha = gamma = 0.0;
-        for (int kk = 1; kk < L; kk++) {
-            const double al = 1.0 / (b - a * gp);
-            alpha = (k == kk) ? al : alpha;
-            gamma = (k == kk) ? cc * al : gamma;
-            gp = __shfl(gamma, kk, LP);
-        }
-    } else {
-        alpha = 1.0 / (b - a * gamma_m);  // :580-585
-        gamma = cc * alpha;               // :587-591
-    }
-
-    // written: every level but L (padding levels: zeros, full 64-B sectors; see PADW); the
-    // tridiagonal coefficients not at level 0 either, gamma_tri 0.0 there.  Paired 16-B
-    // stores (put2: every lane takes part)
-    const bool w_all = k != L, w_1 = k != L && k != 0;
-    put2<LP>(fw(S, F_coftz), c, fw(S, F_cofwt), c, k, PADW(coftz), PADW(cofwt), w_all, w_all);
-    put2<LP>(fw(S, F_cofwr), c, fw(S, F_cofwz), c, k, PADW(cofwr), PADW(cofwz), w_1, w_1);
-    put2<LP>(fw(S, F_a_tri), c, fw(S, F_b_tri), c, k, PADW(a), PADW(b), w_1, w_1);
-    put2<LP>(fw(S, F_c_tri), c, fw(S, F_alpha_tri), c, k, PADW(cc), PADW(alpha), w_1, w_1);
-    if (w_all) colk(fw(S, F_gamma_tri), c) = k == 0 ? 0.0 : PADW(gamma);
-    if (c == 0 && k < L) fw(S, F_cofrz)[k] = cofrz;
-}
-
-template <int LP, bool MPASV>
-__global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
-    ColMap<LP> m(S, KC);
-    const int k = m.k, c = m.ent;
-    if (c >= S.nCO) return;
-    // (gather2: two own columns per 16-B load instruction)
-    double zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old;
-    gather2<LP>(fd(S, F_zz), c, fd(S, F_exner), c, k, zz, exner);
-    gather2<LP>(fd(S, F_theta_m), c, fd(S, F_cqw), c, k, tm, cqw);
-    gather2<LP>(fd(S, F_qtot), c, fd(S, F_rho_base), c, k, qtot, rb);
-    gather2<LP>(fd(S, F_rtheta_base), c, fd(S, F_rtheta_p), c, k, rtb, rtp);
-    gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
-    const double coftz_old = colk(fd(S, F_coftz), c);  // level L keeps its (never written) value
-    vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2);
-}
-
 // Stage 0 of atm_srk3 in one launch (option "fusesetup", reference semantics): the copies
 // of atm_rk_integration_setup (:747-778), atm_compute_moist_coefficients (:460-502) and
 // the first atm_compute_vert_imp_coefs (:513-592) -- all column-local, run in this order
@@ -301,6 +210,10 @@ hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double
     MPAS_LP_DISPATCH(S.LP, setup_vi_lp, S, st, dts);
 }
 
+template <int LP, bool MPASV>
+__global__ __launch_bounds__(256) void k_vert_imp(DevState S, double dtseps, double rcv, double c2) {
+    vert_imp_body<LP, MPASV>(S, dtseps, rcv, c2, this_blk());
+}
 template <int LP>
 static hipError_t vert_imp_lp(const DevState& S, hipStream_t st, double dts) {
     double dtseps = .5 * dts * (1.0 + kEpssm);
@@ -389,57 +302,10 @@ static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st); }
 
 // ---------------------------------------------------------------- divergence damping
-// OLD0: rtheta_pp_old is known to be 0.0 (srk3, right after the first acoustic substep
-// of a stage, which sets it so on every cell, :1615-1618): its columns are not read, and
-// -(r - 0.0) is the same value as the literal expression gives
-// DIVB (option fusedamp, the step's last damping): the cells' div = -(rtheta_pp -
-// rtheta_pp_old) comes from the acoustic step's X_dvB (the same subtraction, made there)
+// (kernel body: k_cols.h divdamp_body)
 template <int LP, int EPW, bool OLD0, bool DIVB = false, bool TME = false>
 __global__ __launch_bounds__(256) void k_div_damp(DevState S, double coef_divdamp) {
-    ColMapN<LP, EPW> m(S, KE);
-    const int L = S.L, k = m.k;
-    const int *coe = fi(S, F_cellsOnEdge), *sh = fi(S, F_isShared);
-    const double *rtp = fd(S, F_rtheta_pp), *rtpo = fd(S, F_rtheta_pp_old), *tm = fd(S, F_theta_m);
-    const double* spz = fd(S, F_specZoneMaskEdge);
-    double* rup = fw(S, F_ru_p);
-    // every load of the EPW edges first (the isShared test only decides the store)
-    int c1[EPW], c2[EPW], sh1[EPW], sh2[EPW];
-    double r1[EPW], ro1[EPW], r2[EPW], ro2[EPW], t1[EPW], t2[EPW], ru[EPW], spec[EPW];
-#pragma unroll
-    for (int i = 0; i < EPW; i++) {
-        const int e = min(m.base + i, S.nEO - 1);
-        c1[i] = coe[(size_t)e * 2];
-        c2[i] = coe[(size_t)e * 2 + 1];
-        spec[i] = spz[e];
-        ru[i] = colk(rup, e);
-    }
-#pragma unroll
-    for (int i = 0; i < EPW; i++) {
-        sh1[i] = sh[c1[i]];
-        sh2[i] = sh[c2[i]];
-        if (DIVB) {
-            gather2s<LP>(fd(S, X_dvB), c1[i], c2[i], k, r1[i], r2[i]);
-            ro1[i] = ro2[i] = 0.0;
-        } else {
-            gather2s<LP>(rtp, c1[i], c2[i], k, r1[i], r2[i]);
-            if (OLD0) ro1[i] = ro2[i] = 0.0;
-            else gather2s<LP>(rtpo, c1[i], c2[i], k, ro1[i], ro2[i]);
-        }
-        if (TME) {  // theta_m(cell2) + theta_m(cell1) from X_tme (atm_srk3, option tmedge)
-            t1[i] = colk(fd(S, X_tme), min(m.base + i, S.nEO - 1));
-            t2[i] = 0.0;
-        } else {
-            gather2s<LP>(tm, c1[i], c2[i], k, t1[i], t2[i]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < EPW; i++) {
-        const int e = m.base + i;
-        if (e >= S.nEO || k >= L || (sh1[i] && sh2[i])) continue;
-        double divCell1 = DIVB ? r1[i] : -(r1[i] - ro1[i]);
-        double divCell2 = DIVB ? r2[i] : -(r2[i] - ro2[i]);
-        colk(rup, e) = ru[i] + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec[i]) / (TME ? t1[i] : t1[i] + t2[i]);
-    }
+    divdamp_body<LP, EPW, OLD0, DIVB, TME>(S, coef_divdamp, this_blk());
 }
 double divdamp_coef(double dts) {  // :1736-1738
     double smdiv = kSmdiv;
@@ -541,35 +407,7 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
 // position pairs.  With substep = split = 1 (atm_srk3) the average is s * 1.0 = s: its
 // store back is skipped (the same bits)
 __global__ __launch_bounds__(256) void k_finish64(DevState S, int substep, int split, double inv_split, Pair64 q) {
-    const bool cells = blockIdx.y == 1;
-    const size_t n = (size_t)(cells ? S.nCO : S.nEO) * 32;
-    double *avg = fw(S, cells ? F_wwAvg : F_ruAvg), *avgS = fw(S, cells ? F_wwAvg_split : F_ruAvg_split);
-    const bool restore = substep < split, last = substep == split, same = substep == 1 && inv_split == 1.0;
-    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-        auto cp = [&](int from, int to) { st64(fw(S, to), i, ((const double2*)fd(S, from))[i], q); };
-        if (restore) {
-            if (cells) {
-                cp(F_rw, F_rw_save);
-                cp(F_rtheta_p, F_rtheta_p_save);
-                cp(F_rho_p, F_rho_p_save);
-                cp(F_w_2, F_w);
-                cp(F_theta_m_2, F_theta_m);
-                cp(F_rho_zz_2, F_rho_zz);
-            } else {
-                cp(F_ru, F_ru_save);
-                cp(F_u_2, F_u);
-            }
-        }
-        const double2 a = ((const double2*)avg)[i];
-        double2 sv = a;
-        if (substep != 1) {
-            const double2 b = ((const double2*)avgS)[i];
-            sv = make_double2(a.x + b.x, a.y + b.y);
-        }
-        st64(avgS, i, sv, q);
-        if (last && !same) st64(avg, i, make_double2(sv.x * inv_split, sv.y * inv_split), q);
-        if (cells && last && S.physics != 2) cp(F_rho_zz_old_split, F_rho_zz);
-    }
+    finish64_body(S, substep, split, inv_split, q, blockIdx.y == 1, (int)blockIdx.x, (int)gridDim.x);
 }
 
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split) {

@@ -90,6 +90,7 @@ struct mpas_ctx {
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     int overlap = 1;   // option "overlap": halo exchanges beside interior compute
+    int hfuse = 1;      // option "hfuse": independent neighbouring kernels share a launch (same values)
     int fusesml = 1;    // option "fusesml": each stage's set_smlstep inside its first acoustic launch (with fusedamp)
     int tmedge = 1;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values)
     int fusesetup = 1;  // option "fusesetup": stage 0's setup, moist and vert_imp in one launch (same values)
@@ -658,8 +659,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // theta_m(cell2) + theta_m(cell1) per edge, which the stage's acoustic substeps and the
     // damping read instead of gathering theta_m at both cells (theta_m unchanged in between)
     const int tme = (c->tmedge && S.physics == 0 && !c->halo) ? 1 : 0;
+    // option hfuse (reference semantics, undecomposed): neighbouring kernels that neither
+    // read what the other writes share a launch (k_solve.hip combined launches, dyn_tend's
+    // rk 0 D beside E); the same values
+    const int hf = (c->hfuse && S.physics == 0 && !c->halo) ? 1 : 0;
+    bool vi_done = false;  // stage 1's vert_imp ran beside stage 0's solve_diagnostics edges
     for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
-        if (rk_step == 1)
+        if (rk_step == 1 && !vi_done)
             run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
         DynTendArgs a{};
         a.rk_step = schedule == 0 ? (int)rk_sub_timestep[rk_step] : rk_step;  // Q4
@@ -670,6 +676,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a.rayleigh_damp_u = 0;
         a.exact_q = c->exact;
         a.tme = tme;
+        a.hfuse = hf;
         run_task(c, a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]",
                  [&] { return launch_dyn_tend(S, st, a); });
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
@@ -686,7 +693,10 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                 if (mode == 2) fb.swap_rup();
                 fb.swap_dv();  // this substep's div is read next from X_dvB
                 if (++done_acoustic == n_acoustic) {
-                    run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping_div(S, st, dts, tme); });
+                    if (hf)  // beside the solve_diagnostics vertex / cell kernel that follows
+                        run_task(c, "hfuse[damp+solve_vc]", [&] { return launch_hf_damp_solve_vc(S, st, dts, tme); });
+                    else
+                        run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping_div(S, st, dts, tme); });
                     pending = false;
                 } else {
                     pending = true;
@@ -701,7 +711,20 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         if (S.physics)  // rk_timestep.rg:460, commented out in the reference (Q7)
             run_task(c, recover_name(rk_step),
                      [&] { return launch_recover_large_step(S, st, number_sub_steps[rk_step], rk_step, dt); });
-        run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
+        if (hf && fuse && rk_step == 2 && S.LP == 64 && !c->transport) {
+            // (the vertex / cell kernel ran beside the last damping) the edge kernel beside
+            // atm_rk_dynamics_substep_finish, which follows below
+            run_task(c, "hfuse[solve_e+finish]", [&] { return launch_hf_solve_e_finish(S, st); });
+        } else if (hf && fuse && rk_step == 2) {
+            run_task(c, "atm_compute_solve_diagnostics[e]", [&] { return launch_solve_diagnostics(S, st, 0, 2, 2); });
+        } else if (hf && rk_step == 0) {  // the edge kernel beside stage 1's vert_imp
+            run_task(c, "atm_compute_solve_diagnostics[vc]", [&] { return launch_solve_diagnostics(S, st, 0, 0, 1); });
+            run_task(c, "hfuse[solve_e+vert_imp]",
+                     [&] { return launch_hf_solve_e_vert_imp(S, st, rk_sub_timestep[1]); });
+            vi_done = true;
+        } else {
+            run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
+        }
     }
     if (c->transport)  // after the last stage's recover: ruAvg / wwAvg / rho_zz of the step
         run_task(c, "atm_advance_scalars_mono", [&] {
@@ -710,7 +733,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         });
     if (S.physics == 2)  // the MPAS dynamics: cell-centre winds for the next step's curvature
         run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });  // (:487, commented)
-    run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
+    if (!(hf && fuse && S.LP == 64 && !c->transport))  // (else it ran beside solve_diagnostics' edges)
+        run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
     fb.finish();
     // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }
@@ -929,6 +953,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
+        else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value ? 1 : 0;
         else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
@@ -1006,6 +1031,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) *value = c->fusesetup;
         else if (name && std::strcmp(name, "tmedge") == 0) *value = c->tmedge;
         else if (name && std::strcmp(name, "fusesml") == 0) *value = c->fusesml;
+        else if (name && std::strcmp(name, "hfuse") == 0) *value = c->hfuse;
         else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
         else if (name && std::strcmp(name, "halo_state") == 0) {  // hash of the halo bookkeeping (debug)
             uint64_t hsh = 1469598103934665603ull;

@@ -160,6 +160,7 @@ struct DynTendArgs {
     int rayleigh_damp_u;
     int exact_q;       // 1: Q10 literal (each q term added nVertLevels times), 0: nVertLevels*term
     int tme = 0;       // 1: the edge kernel also stores X_tme (atm_srk3, option "tmedge")
+    int hfuse = 0;     // 1: rk_step 0's D and E in one grid (atm_srk3, option "hfuse"; undecomposed)
 };
 
 enum EntityKind { KC = 0, KE = 1, KV = 2 };  // DevState::lo index
@@ -201,7 +202,12 @@ hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts, int
 hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts, int tme = 0);
 // coef_divdamp of atm_divergence_damping_3d (:1736-1738) for dts
 double divdamp_coef(double dts);
-hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step);
+// combined launches of independent neighbours (option "hfuse", k_solve.hip)
+hipError_t launch_hf_damp_solve_vc(const DevState& S, hipStream_t st, double dts, int tme);
+hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st);
+hipError_t launch_hf_solve_e_vert_imp(const DevState& S, hipStream_t st, double dts);
+// parts: 1 the vertex / cell kernel, 2 the edge kernel, 3 both (the task)
+hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts = 3);
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
 hipError_t launch_prepare(DevState& S, hipStream_t st);
@@ -266,18 +272,26 @@ __device__ __forceinline__ int xcd_block_n(int on, int b, int nb) {
 // the remap over the whole grid
 __device__ __forceinline__ int xcd_block(int on) { return xcd_block_n(on, (int)blockIdx.x, (int)gridDim.x); }
 
+// The block index and block count a kernel body sees: blockIdx.x / gridDim.x of its own
+// launch, or its sub-range of a combined launch (k_hfuse.h: two independent kernels of the
+// step in one grid, blocks [0, n1) running the first body and [n1, gridDim.x) the second)
+struct Blk {
+    int b, n;
+};
+__device__ __forceinline__ Blk this_blk() { return {(int)blockIdx.x, (int)gridDim.x}; }
+
 // Mixed vertex + cell grids (dyn_tend C, solve_diagnostics): nVB vertex blocks and
 // nb - nVB cell blocks.  With S.vcmix they are interleaved in proportion -- block b is a
 // vertex block iff floor((b+1) nVB / nb) > floor(b nVB / nb) -- so that the vertex and
 // the cell blocks of one region of the Morton-ordered mesh run at the same time and the
 // edge columns both gather are fetched into L2 once; otherwise all vertex blocks come
 // first.  Returns true for a vertex block; idx = its vertex (or cell) block index.
-__device__ __forceinline__ bool vc_block(const DevState& S, int blk, int nVB, int& idx) {
+__device__ __forceinline__ bool vc_block(const DevState& S, int blk, int nVB, int& idx, int nblocks = -1) {
     if (!S.vcmix) {
         idx = blk < nVB ? blk : blk - nVB;
         return blk < nVB;
     }
-    const long long nb = (long long)gridDim.x;
+    const long long nb = nblocks >= 0 ? (long long)nblocks : (long long)gridDim.x;
     const int a = (int)((long long)blk * nVB / nb), a1 = (int)((long long)(blk + 1) * nVB / nb);
     idx = a1 > a ? a : blk - a;
     return a1 > a;
@@ -297,8 +311,8 @@ template <int LP>
 struct ColMap {
     static constexpr int COLS = 256 / LP;
     int blk, ent, k;
-    __device__ __forceinline__ ColMap(const DevState& S, int kind) {
-        blk = xcd_block(S.xcd);
+    __device__ __forceinline__ ColMap(const DevState& S, int kind, Blk bk = this_blk()) {
+        blk = xcd_block_n(S.xcd, bk.b, bk.n);
         ent = col_of<LP>(blk) + S.lo[kind];
         k = (int)(threadIdx.x % LP);
     }
@@ -311,8 +325,8 @@ template <int LP, int EPW>
 struct ColMapN {
     static constexpr int COLS = 256 / LP;
     int blk, base, k;
-    __device__ __forceinline__ ColMapN(const DevState& S, int kind) {
-        blk = xcd_block(S.xcd);
+    __device__ __forceinline__ ColMapN(const DevState& S, int kind, Blk bk = this_blk()) {
+        blk = xcd_block_n(S.xcd, bk.b, bk.n);
         base = col_of<LP>(blk) * EPW + S.lo[kind];
         k = (int)(threadIdx.x % LP);
     }

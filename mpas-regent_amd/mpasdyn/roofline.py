@@ -14,8 +14,18 @@ roofline.achieved divides by the measured launch time.
 """
 
 # name -> (reads, writes); each a list of field names of the registry
-def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False):
+def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
+          part=None, pair=None):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
+    if task == "hfuse":  # option hfuse: two independent kernels of the step in one launch
+        a, b = {"damp+solve_vc": (("atm_divergence_damping_3d", {}), ("atm_compute_solve_diagnostics", {"part": "vc"})),
+                "solve_e+finish": (("atm_compute_solve_diagnostics", {"part": "e", "reconstruct_v": True}),
+                                   ("atm_rk_dynamics_substep_finish", {})),
+                "solve_e+vert_imp": (("atm_compute_solve_diagnostics", {"part": "e"}),
+                                     ("atm_compute_vert_imp_coefs", {}))}[pair]
+        ra, wa = _sets(a[0], **a[1])
+        rb, wb = _sets(b[0], **b[1])
+        return ra + rb, wa + wb
     if task == "atm_rk_integration_setup" and fused:  # option fusesetup: + moist + vert_imp, one launch
         parts = [_sets(t) for t in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
                                     "atm_compute_vert_imp_coefs")]
@@ -85,6 +95,17 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
     if task == "atm_divergence_damping_3d":
         return (["rtheta_pp", "rtheta_pp_old", "theta_m", "ru_p", "cellsOnEdge", "isShared", "specZoneMaskEdge"],
                 ["ru_p"])
+    if task == "atm_compute_solve_diagnostics" and part == "vc":  # its vertex / cell kernel alone
+        return (["u", "dcEdge", "dvEdge", "edgesOnCell", "edgesOnCellSign", "invAreaCell", "nEdgesOnCell",
+                 "edgesOnVertex", "edgesOnVertexSign", "fVertex", "invAreaTriangle"],
+                ["divergence", "ke", "vorticity", "pv_vertex"])
+    if task == "atm_compute_solve_diagnostics" and part == "e":  # its edge kernel alone
+        reads = ["h", "u", "pv_vertex", "cellsOnEdge", "verticesOnEdge", "dcEdge", "dvEdge"]
+        writes = ["h_edge", "ke_edge", "pv_edge"]
+        if reconstruct_v:
+            reads += ["edgesOnEdge_ECP", "nEdgesOnEdge", "weightsOnEdge"]
+            writes.append("v")
+        return reads, writes
     if task == "atm_compute_solve_diagnostics":
         writes = ["h_edge", "ke_edge", "pv_edge", "divergence", "ke", "vorticity", "pv_vertex"]
         if reconstruct_v:

@@ -431,11 +431,12 @@ def test_upload_rejects_overlong_lists(x1_2562, field, width):
 
 
 # ---- option fusedamp: the damping inside the next acoustic launch ------------------------
-def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None, tmedge=None, fusesml=None):
+def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None, tmedge=None, fusesml=None, hfuse=None):
     got = st.copy()
     with lib.Context(*st.dims()) as ctx:
         ctx.set_option("exact", exact)
         ctx.set_option("fusedamp", fusedamp)
+        ctx.set_option("hfuse", fusedamp if hfuse is None else hfuse)
         ctx.set_option("fusesml", fusedamp if fusesml is None else fusesml)
         ctx.set_option("fusesetup", fusedamp if fusesetup is None else fusesetup)
         ctx.set_option("tmedge", fusedamp if tmedge is None else tmedge)
@@ -457,8 +458,9 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
     """atm_srk3 with six of its seven dampings applied inside the next acoustic launch
     (k_acoustic MODE 2: the same expression on the same values), stage 0's setup, moist
     and vert_imp in one launch (k_setup_vi), each stage's set_smlstep inside its first
-    acoustic launch (option fusesml) and theta_m(cell2) + theta_m(cell1) per edge taken
-    from dyn_tend's edge kernel (option tmedge) is value-identical to the separate launches and
+    acoustic launch (option fusesml), theta_m(cell2) + theta_m(cell1) per edge taken
+    from dyn_tend's edge kernel (option tmedge) and independent neighbouring kernels
+    sharing a launch (option hfuse) is value-identical to the separate launches and
     to the oracle, in exact mode and on the fast path; raw 1-based ids leave edge 0 listed
     by no cell (an orphan, written by the launch's extra blocks)"""
     st = base_state(x1_2562, L, variant)
@@ -478,6 +480,10 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
     c, _ = _two_steps_gpu(st, 0, 0, 1, fusesetup=1)
     bad = compare_states(c, b, rtol=0.0)
     assert not bad, f"fusesetup alone vs separate launches: {bad[:6]}"
+    for hf in (0, 1):  # combined launches of independent kernels with and without the damping fusion
+        c, _ = _two_steps_gpu(st, hf, 0, 1, hfuse=1 - hf)
+        bad = compare_states(c, b, rtol=0.0)
+        assert not bad, f"hfuse={1 - hf}, fusedamp={hf} vs separate launches: {bad[:6]}"
     c, _ = _two_steps_gpu(st, 1, 0, 1, fusesml=0)  # set_smlstep as its own launch
     bad = compare_states(c, b, rtol=0.0)
     assert not bad, f"fusesml=0 vs separate launches: {bad[:6]}"
