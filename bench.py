@@ -247,13 +247,14 @@ def measure_traffic(args):
     wfac = pmc.write_factor(res["WRITE_SIZE"], m_cells, m_edges, args.levels, int(args.physics or 0))
     if wfac is None:
         return None, "WRITE_SIZE calibration kernels missing"
-    by = pmc.bytes_per_step(res["FETCH_SIZE"], res["WRITE_SIZE"], 1, wfac)
+    by = pmc.bytes_per_step(pmc.drop_calibration(res["FETCH_SIZE"]), pmc.drop_calibration(res["WRITE_SIZE"]), 1,
+                            wfac)
     return by, (f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes of 1 RK3 step of this workload; "
                 f"fetch x{pmc.FETCH_FACTOR} (gfx950), write x{wfac:.3f} (calibrated on the setup copies)")
 
 
 def pmc_child(args):
-    """the workload rocprofv3 counts: 1 RK3 step after upload, nothing else"""
+    """the workload rocprofv3 counts: 1 RK3 step after upload, then one setup task alone"""
     from mpasdyn import lib
     from mpasdyn import tasks as T
     m, st = build_inputs(args.ncells, args.levels, zero_based=args.physics)
@@ -268,6 +269,9 @@ def pmc_child(args):
     dt = dt_for(args.ncells)
     for _ in range(args.steps):
         T.atm_srk3(ctx, dt, 1)
+    # the WRITE_SIZE calibration: the setup task's pure copies, run alone (the step may
+    # have fused them into another launch); measure_traffic drops this dispatch again
+    T.atm_rk_integration_setup(ctx)
     ctx.sync()
     ctx.close()
 
@@ -527,7 +531,7 @@ def main():
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup),
                       "fusesml": int(fsml), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
-                      "hfuse": int(bool(ctx.get_option("hfuse")) and not args.physics and not decomposed)},
+                      "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}
     if halo_info:

@@ -90,9 +90,13 @@ struct mpas_ctx {
     int self_on = 1;   // option "self": allow the SELF gathers when the mesh permits
     int self_ok = 0;   // k_prepare's verdict on the uploaded mesh
     int overlap = 1;   // option "overlap": halo exchanges beside interior compute
-    int hfuse = 1;      // option "hfuse": independent neighbouring kernels share a launch (same values)
+    // option "hfuse": independent neighbouring kernels share a launch (same values); 2 = on
+    // where the grids do not fill the chip (hfuse_auto_cells), the case it pays in
+    // (x1.2562: -3 %; x1.163842: +0.8 %, the pair runs at the lower occupancy of the two)
+    int hfuse = 2;
     int fusesml = 1;    // option "fusesml": each stage's set_smlstep inside its first acoustic launch (with fusedamp)
-    int tmedge = 1;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values)
+    int tmedge = 0;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values;
+                        // measured slower at both sizes)
     int fusesetup = 1;  // option "fusesetup": stage 0's setup, moist and vert_imp in one launch (same values)
     int fusedamp = 1;  // option "fusedamp": atm_srk3 applies each divergence damping inside the next
                        // acoustic launch (reference semantics, undecomposed; same bits)
@@ -573,6 +577,15 @@ void trt_ensure(mpas_ctx* c) {
     if (c->trt_dirty) trt_build(c);
 }
 
+// option hfuse (reference semantics, undecomposed); 2: only below this many owned cells
+// (a cell kernel then has fewer than ~16 wavefronts per SIMD: the launches do not fill the
+// chip and their fixed cost dominates)
+constexpr int hfuse_auto_cells = 16384;
+bool hfuse_active(const mpas_ctx* c) {
+    if (c->S.physics != 0 || c->halo) return false;
+    return c->hfuse == 1 || (c->hfuse == 2 && c->S.nCO < hfuse_auto_cells);
+}
+
 // timing keys: one Regent task, split where its read/write set (B_alg) differs by argument
 // (bench.py aggregates the variants per task)
 const char* acoustic_name(int small_step, bool damp = false, bool sml = false) {
@@ -662,7 +675,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // option hfuse (reference semantics, undecomposed): neighbouring kernels that neither
     // read what the other writes share a launch (k_solve.hip combined launches, dyn_tend's
     // rk 0 D beside E); the same values
-    const int hf = (c->hfuse && S.physics == 0 && !c->halo) ? 1 : 0;
+    const int hf = hfuse_active(c) ? 1 : 0;
     bool vi_done = false;  // stage 1's vert_imp ran beside stage 0's solve_diagnostics edges
     for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
         if (rk_step == 1 && !vi_done)
@@ -953,7 +966,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
-        else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value ? 1 : 0;
+        else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
@@ -1032,6 +1045,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "tmedge") == 0) *value = c->tmedge;
         else if (name && std::strcmp(name, "fusesml") == 0) *value = c->fusesml;
         else if (name && std::strcmp(name, "hfuse") == 0) *value = c->hfuse;
+        else if (name && std::strcmp(name, "hfuse_active") == 0) *value = hfuse_active(c);
         else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
         else if (name && std::strcmp(name, "halo_state") == 0) {  // hash of the halo bookkeeping (debug)
             uint64_t hsh = 1469598103934665603ull;

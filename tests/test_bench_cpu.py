@@ -76,6 +76,25 @@ def test_task_table_aggregates_variants():
     assert max(t, key=lambda k: t[k]["ms_per_step"]) == "atm_compute_dyn_tend_work"
 
 
+def test_pmc_kernel_map_covers_fused_launches():
+    """every kernel of the fused schedules is attributed (dyn_tend's combined rk 0 D/E
+    launch to dyn_tend), and the standalone setup run that calibrates WRITE_SIZE is
+    removed from the per-step bytes"""
+    from mpasdyn import pmc
+    assert pmc.task_of("k_dyn_DE<64, true>") == "atm_compute_dyn_tend_work[rk0]"
+    assert pmc.task_of("k_dyn_B<64, false, 2>") == "atm_compute_dyn_tend_work[rk>0]"
+    assert pmc.task_of("k_setup_vi<64>") == "atm_rk_integration_setup"
+    assert pmc.task_of("k_hf_e_vi") == "hfuse"
+    assert pmc.task_of("k_acoustic<64, false, true, true, false, 2, true, true>") == "atm_advance_acoustic_step_work"
+    L, nc, ne = 56, 40962, 3 * (40962 - 2)
+    payload = (7 * nc + 2 * ne) * 8 * L
+    w = {"k_copy64": (2 * payload / 1024.0 / 0.875, 2), "k_dyn_DE<64, true>": (100.0, 1)}
+    assert abs(pmc.write_factor(w, nc, ne, L) - 0.875) < 1e-12
+    d = pmc.drop_calibration(w)
+    assert d["k_copy64"] == (payload / 1024.0 / 0.875, 1) and d["k_dyn_DE<64, true>"] == (100.0, 1)
+    assert "k_copy64" not in pmc.drop_calibration({"k_copy64": (5.0, 1)})
+
+
 @pytest.mark.parametrize("n", [2, 3])
 def test_launcher_rendezvous_without_torch(n):
     """--dry-run runs one round of the host rendezvous (mpasdyn/rendezvous.py): rank 0's

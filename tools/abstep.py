@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Whole-step A/B in one process: the benchmark workload built once, interleaved rounds of
-K atm_srk3 steps (HIP graph replay, as bench.py times them) under each option set; per
+K atm_srk3 steps (HIP graph replay, as bench.py times them) under each option set (options a variant does not name at their defaults); per
 variant the median per-step device time over all rounds (HIP events between steps).
 
 usage: python tools/abstep.py [--ncells 163842] [--rounds 6] [--steps 5] --variants "fusesetup=1" "fusesetup=0"
@@ -35,8 +35,14 @@ def main():
     stream = ctx.stream()
     evs = [hip.event() for _ in range(a.steps + 1)]
     res = {v: [] for v in a.variants}
+    # every option a variant names starts from its default in every variant (a variant
+    # lists only what it changes)
+    keys = {kv.split("=")[0] for v in a.variants for kv in v.split(",")}
+    base = {k: ctx.get_option(k) for k in keys}
     for _ in range(a.rounds):
         for v in a.variants:
+            for k, val in base.items():
+                ctx.set_option(k, val)
             for kv in v.split(","):
                 k, val = kv.split("=")
                 ctx.set_option(k, int(val))

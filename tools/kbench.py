@@ -32,8 +32,12 @@ def main():
     dt = bench.dt_for(a.ncells)
     T.atm_srk3(ctx, dt, 1)
     res = {v: {} for v in a.variants}
+    keys = {kv.split("=")[0] for v in a.variants for kv in v.split(",")}
+    base = {k: ctx.get_option(k) for k in keys}  # (a variant lists only what it changes)
     for r in range(a.rounds):
         for v in a.variants:
+            for k, val in base.items():
+                ctx.set_option(k, val)
             for kv in v.split(","):
                 k, val = kv.split("=")
                 ctx.set_option(k, int(val))
