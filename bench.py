@@ -286,6 +286,9 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_advance_acoustic_step_work[ss>0]": {"small_step": 1},
              "atm_advance_acoustic_step_work[ss0+damp]": {"small_step": 0, "damp": True},
              "atm_rk_integration_setup[+moist+vert_imp]": {"fused": True},
+             "atm_rk_integration_setup[cells+moist+vert_imp]": {"fused": True, "copy": True},
+             "atm_compute_dyn_tend_work[rk0+copy]": {"rk_step": 0, "copy": True},
+             "atm_compute_dyn_tend_work[rk>0+copy]": {"rk_step": 1, "copy": True},
              "atm_advance_acoustic_step_work[ss0+sml]": {"small_step": 0, "sml": True},
              "atm_compute_solve_diagnostics[vc]": {"part": "vc"}, "atm_compute_solve_diagnostics[e]": {"part": "e"},
              "hfuse[damp+solve_vc]": {"pair": "damp+solve_vc"}, "hfuse[solve_e+finish]": {"pair": "solve_e+finish"},
@@ -506,7 +509,8 @@ def main():
     fused = bool(ctx.get_option("fusedamp_active"))
     fsetup = bool(ctx.get_option("fusesetup")) and not args.physics
     fsml = fused and bool(ctx.get_option("fusesml"))
-    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml)
+    fcopy = fsetup and bool(ctx.get_option("fusecopy")) and not decomposed
+    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -529,7 +533,7 @@ def main():
                       "dt": dt, "parallelism": (f"decomposed{world}" if decomposed else
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
-                      "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup),
+                      "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy),
                       "fusesml": int(fsml), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),

@@ -68,6 +68,15 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * re-captures; per-task timing and decomposed contexts run the launches directly; read-only
  * "graph_captures" / "graph_launches" count them).  All but "exact" and "physics" change
  * only speed, never results.
+ * Cross-task fusion in mpas_atm_srk3 (reference semantics, undecomposed):
+ * "fusedamp" = 1 (default) applies each divergence damping inside the next acoustic launch
+ * (read-only "fusedamp_active"); "fusesml" = 1 (default, with fusedamp) runs each stage's
+ * set_smlstep inside its first acoustic launch; "fusesetup" = 1 (default) runs setup, moist
+ * and stage 0's vert_imp as one launch; "fusecopy" = 1 (default, with fusesetup) makes
+ * setup's edge copies in stage 0's dyn_tend edge kernel; "tmedge" = 1 (default 0) has
+ * dyn_tend store theta_m(cell1) + theta_m(cell2) per edge for the acoustic substeps;
+ * "hfuse" = 1 puts independent neighbouring kernels in one launch, 2 (default) only below
+ * 16384 owned cells (read-only "hfuse_active").
  * "physics" = 1 selects the MPAS vertical solver: vert_imp with Q16/Q17
  * fixed, the acoustic step with the ru_p update (Q18), the MPAS statement order (Q19/Q20)
  * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), recover_large_step

@@ -49,7 +49,7 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 }
 
 struct DynK {
-    int rk_step, horiz_mixing, rayleigh, exact_q, tme;
+    int rk_step, horiz_mixing, rayleigh, exact_q, tme, cp;
     double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
 };
 
@@ -279,6 +279,7 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     if constexpr (!RK0) {
         if constexpr (HF) {
             gather2<LP>(fd(S, F_tend_u_euler), e, fd(S, F_ru_save), e, k, tue_in, rus_e);
+            if (a.cp) rus_e = ru_e;  // (the copy below is setup's: ru_save = ru, read after it)
             gather2s<LP>(fd(S, F_theta_m_save), cell1, cell2, k, ts1, ts2);
         } else {
             tue_in = colk(fd(S, F_tend_u_euler), e);
@@ -409,6 +410,11 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         }
         if (k != L) colk(fw(S, X_tme), e) = PADW(t2pt1);
     }
+    // a.cp (atm_srk3 stage 0, option "fusecopy"): atm_rk_integration_setup's edge copies
+    // (:758-761, every level but L) from the u and ru columns this kernel has loaded; no
+    // task between setup and here reads ru_save or u_2 (dyn_tend reads ru_save at
+    // rk_step > 0 only, after this kernel), and u / ru are not written in between
+    if (a.cp) put2<LP>(fw(S, F_ru_save), e, fw(S, F_u_2), e, k, PADW(ru_e), PADW(u), k != L, k != L);
     if constexpr (HF) {  // every lane stores (paired 16-B stores); level L keeps its value
         double* Fo = fw(S, X_F);
         double* tuo = fw(S, F_tend_u);
@@ -856,6 +862,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     a.rayleigh = in.rayleigh_damp_u;
     a.exact_q = in.exact_q;
     a.tme = in.tme && !S.halo;
+    a.cp = in.cp && !S.halo;
     const double invDt = 1.0 / in.dt;
     const double c_s = kSmagCoef;
     a.cs_l2 = (c_s * kLenDisp) * (c_s * kLenDisp);
@@ -960,6 +967,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     }
     HALO_WROTE(S, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
     HALO_WROTE(S, MD ? F_tend_w : F_w);
+    if (a.cp) HALO_WROTE(S, F_ru_save, F_u_2);
     return hipGetLastError();
 }
 template <int LP>

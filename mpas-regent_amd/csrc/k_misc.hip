@@ -157,7 +157,8 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 // the first atm_compute_vert_imp_coefs (:513-592) -- all column-local, run in this order
 // by one wavefront per cell column: vert_imp takes theta_m and rtheta_p from the copy's
 // loads and qtot / cqw as moist has just set them, so those four columns are read once.
-// Edge blocks (ncb..) copy ru and u.  The same values as the three launches.
+// Edge blocks (ncb..) copy ru and u (none with option "fusecopy": dyn_tend's edge kernel
+// makes those copies).  The same values as the three launches.
 template <int LP>
 __global__ __launch_bounds__(256) void k_setup_vi(DevState S, int ncb, double dtseps, double rcv, double c2) {
     const int L = S.L, k = (int)(threadIdx.x % LP);
@@ -194,20 +195,21 @@ __global__ __launch_bounds__(256) void k_setup_vi(DevState S, int ncb, double dt
     vi_column<LP, false>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2);
 }
 template <int LP>
-static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts) {
+static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts, bool edges) {
     if (S.physics) return hipErrorInvalidValue;  // (srk3 asks in the reference semantics only)
     double dtseps = .5 * dts * (1.0 + kEpssm);
     double rcv = kRgas / (kCp - kRgas);
     double c2 = kCp * rcv;
-    const int ncb = col_blocks<LP>(S, KC), neb = col_blocks<LP>(S, KE);
+    const int ncb = col_blocks<LP>(S, KC), neb = edges ? col_blocks<LP>(S, KE) : 0;
     if (ncb + neb) k_setup_vi<LP><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2);
-    HALO_WROTE(S, F_ru_save, F_u_2, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2,
-               F_rho_zz_old_split, F_qtot, F_cqw);
+    if (edges) HALO_WROTE(S, F_ru_save, F_u_2);
+    HALO_WROTE(S, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2, F_rho_zz_old_split, F_qtot,
+               F_cqw);
     HALO_WROTE(S, F_coftz, F_cofwt, F_gamma_tri, F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri);
     return hipGetLastError();
 }
-hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts) {
-    MPAS_LP_DISPATCH(S.LP, setup_vi_lp, S, st, dts);
+hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts, bool edges) {
+    MPAS_LP_DISPATCH(S.LP, setup_vi_lp, S, st, dts, edges);
 }
 
 template <int LP, bool MPASV>

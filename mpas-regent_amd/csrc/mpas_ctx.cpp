@@ -97,6 +97,8 @@ struct mpas_ctx {
     int fusesml = 1;    // option "fusesml": each stage's set_smlstep inside its first acoustic launch (with fusedamp)
     int tmedge = 0;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values;
                         // measured slower at both sizes)
+    int fusecopy = 1;   // option "fusecopy" (with fusesetup): setup's edge copies made by stage 0's dyn_tend
+                        // edge kernel from the columns it loads anyway (same values)
     int fusesetup = 1;  // option "fusesetup": stage 0's setup, moist and vert_imp in one launch (same values)
     int fusedamp = 1;  // option "fusedamp": atm_srk3 applies each divergence damping inside the next
                        // acoustic launch (reference semantics, undecomposed; same bits)
@@ -651,9 +653,11 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             return e;
         });
     }
+    // option fusecopy: ru_save / u_2 by stage 0's dyn_tend edge kernel (reads u and ru there)
+    const bool fcopy = c->fusesetup && c->fusecopy && S.physics == 0 && !c->halo;
     if (c->fusesetup && S.physics == 0) {  // :404-417 as one column-local launch (same values)
-        run_task(c, "atm_rk_integration_setup[+moist+vert_imp]",
-                 [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0]); });
+        run_task(c, fcopy ? "atm_rk_integration_setup[cells+moist+vert_imp]" : "atm_rk_integration_setup[+moist+vert_imp]",
+                 [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0], !fcopy); });
     } else {
         run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
         run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
@@ -690,7 +694,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a.exact_q = c->exact;
         a.tme = tme;
         a.hfuse = hf;
-        run_task(c, a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]",
+        a.cp = (fcopy && rk_step == 0) ? 1 : 0;
+        run_task(c, a.cp ? (a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0+copy]" : "atm_compute_dyn_tend_work[rk>0+copy]")
+                         : (a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]"),
                  [&] { return launch_dyn_tend(S, st, a); });
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
         const bool sml = fuse && c->fusesml;
@@ -964,6 +970,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "graph") == 0) c->graph_on = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp") == 0) c->fusedamp = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
+        else if (name && std::strcmp(name, "fusecopy") == 0) c->fusecopy = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
         else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value < 0 ? 0 : value > 2 ? 2 : value;
@@ -1042,6 +1049,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "fusedamp") == 0) *value = c->fusedamp;
         else if (name && std::strcmp(name, "fusesetup") == 0) *value = c->fusesetup;
+        else if (name && std::strcmp(name, "fusecopy") == 0) *value = c->fusecopy;
         else if (name && std::strcmp(name, "tmedge") == 0) *value = c->tmedge;
         else if (name && std::strcmp(name, "fusesml") == 0) *value = c->fusesml;
         else if (name && std::strcmp(name, "hfuse") == 0) *value = c->hfuse;

@@ -161,6 +161,8 @@ struct DynTendArgs {
     int exact_q;       // 1: Q10 literal (each q term added nVertLevels times), 0: nVertLevels*term
     int tme = 0;       // 1: the edge kernel also stores X_tme (atm_srk3, option "tmedge")
     int hfuse = 0;     // 1: rk_step 0's D and E in one grid (atm_srk3, option "hfuse"; undecomposed)
+    int cp = 0;        // 1: the edge kernel also makes setup's ru_save = ru, u_2 = u (atm_srk3 stage 0,
+                       // option "fusecopy"; undecomposed)
 };
 
 enum EntityKind { KC = 0, KE = 1, KV = 2 };  // DevState::lo index
@@ -185,7 +187,7 @@ hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st);
 hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st);
 hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts);
 // setup + moist + vert_imp(dts) in one launch (option "fusesetup", reference semantics)
-hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts);
+hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts, bool edges = true);
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
 // mode (reference semantics, no halo; atm_srk3 with option "fusedamp"): 0 plain, 1 also

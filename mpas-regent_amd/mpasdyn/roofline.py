@@ -15,7 +15,7 @@ roofline.achieved divides by the measured launch time.
 
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
-          part=None, pair=None):
+          part=None, pair=None, copy=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: two independent kernels of the step in one launch
         a, b = {"damp+solve_vc": (("atm_divergence_damping_3d", {}), ("atm_compute_solve_diagnostics", {"part": "vc"})),
@@ -31,6 +31,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                                     "atm_compute_vert_imp_coefs")]
         writes = sorted(set(w for _, ws in parts for w in ws))
         reads = sorted(set(r for rs, _ in parts for r in rs) - set(writes) | {"gamma_tri"})
+        if copy:  # option fusecopy: the edge copies ru_save = ru, u_2 = u moved to dyn_tend
+            reads = [r for r in reads if r not in ("ru", "u")]
+            writes = [w for w in writes if w not in ("ru_save", "u_2")]
         return reads, writes
     if task == "atm_rk_integration_setup":
         return (["rho_p", "rho_zz", "rtheta_p", "rw", "theta_m", "w", "ru", "u"],
@@ -65,6 +68,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         if md:  # the w tendency goes to tend_w; the curvature reads the reconstructed winds
             writes = [("tend_w" if x == "w" else x) for x in writes]
             reads += ["uReconstructZonal", "uReconstructMeridional", "w"]
+        if copy:  # option fusecopy (stage 0): setup's ru_save = ru, u_2 = u (ru, u already read)
+            writes = writes + ["ru_save", "u_2"]
         return reads + mesh, writes
     if task == "atm_set_smlstep_pert_variables_work":
         if md:
@@ -170,12 +175,13 @@ def b_alg(task, dims, **kw):
     return sum(fb(x) for x in set(reads)) + sum(fb(x) for x in set(writes))
 
 
-def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False):
+def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
+                  fusecopy=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
     fusedamp (reference semantics): six of the seven dampings run inside the next acoustic
-    launch"""
+    launch; fusecopy (with fusesetup): setup's edge copies in stage 0's dyn_tend"""
     if physics:
         p = {"physics": physics}
         out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
@@ -197,13 +203,15 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
         if transport:
             out += [("scalars_save", {}, 1), ("atm_advance_scalars_mono", {}, 1)]
         return out
+    copy = bool(fusesetup and fusecopy)
     if fusesetup:
-        out = [("atm_rk_integration_setup", {"fused": True}, 1), ("atm_compute_vert_imp_coefs", {}, 1)]
+        out = [("atm_rk_integration_setup", {"fused": True, "copy": copy}, 1), ("atm_compute_vert_imp_coefs", {}, 1)]
     else:
         out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
                ("atm_compute_vert_imp_coefs", {}, 2)]
     if schedule == 1:
-        out += [("atm_compute_dyn_tend_work", {"rk_step": 0}, 1), ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
+        out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy}, 1),
+                ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
     if fusedamp and fusesml:
         out += [("atm_advance_acoustic_step_work", {"small_step": 0, "sml": True}, 1),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, "sml": True}, 2),
@@ -226,6 +234,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     return out
 
 
-def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False):
+def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
+               fusecopy=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
-                                                                        fusesetup, fusesml))
+                                                                        fusesetup, fusesml, fusecopy))

@@ -139,3 +139,19 @@ def test_rendezvous_in_threads():
         t.join(60)
     assert sorted(out) == [0, 1, 2, 3]
     assert all(b == b"\x01\x02" * 64 and m == 21.0 for b, m in out.values())
+
+
+def test_roofline_fusecopy_moves_the_edge_copies():
+    """option fusecopy: setup's ru_save / u_2 copies counted in stage 0's dyn_tend launch;
+    the step's B_alg loses exactly the second read of ru and u"""
+    from mpasdyn import roofline
+    dims = (163842, 491520, 327680, 56)
+    e3 = 8 * 491520 * 56
+    a = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, False)
+    b = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True)
+    assert a - b == 2 * e3
+    s0 = roofline.b_alg("atm_rk_integration_setup", dims, fused=True)
+    s1 = roofline.b_alg("atm_rk_integration_setup", dims, fused=True, copy=True)
+    d0 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0)
+    d1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True)
+    assert s0 - s1 == 4 * e3 and d1 - d0 == 2 * e3

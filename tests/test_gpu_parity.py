@@ -431,7 +431,8 @@ def test_upload_rejects_overlong_lists(x1_2562, field, width):
 
 
 # ---- option fusedamp: the damping inside the next acoustic launch ------------------------
-def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None, tmedge=None, fusesml=None, hfuse=None):
+def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None, tmedge=None, fusesml=None, hfuse=None,
+                   fusecopy=None):
     got = st.copy()
     with lib.Context(*st.dims()) as ctx:
         ctx.set_option("exact", exact)
@@ -440,6 +441,7 @@ def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None, tmedge=None, fu
         ctx.set_option("fusesml", fusedamp if fusesml is None else fusesml)
         ctx.set_option("fusesetup", fusedamp if fusesetup is None else fusesetup)
         ctx.set_option("tmedge", fusedamp if tmedge is None else tmedge)
+        ctx.set_option("fusecopy", fusedamp if fusecopy is None else fusecopy)
         ctx.set_option("graph", graph)
         ctx.upload(st)
         assert ctx.get_option("fusedamp_active") == fusedamp
@@ -458,7 +460,9 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
     """atm_srk3 with six of its seven dampings applied inside the next acoustic launch
     (k_acoustic MODE 2: the same expression on the same values), stage 0's setup, moist
     and vert_imp in one launch (k_setup_vi), each stage's set_smlstep inside its first
-    acoustic launch (option fusesml), theta_m(cell2) + theta_m(cell1) per edge taken
+    acoustic launch (option fusesml), setup's edge copies made by stage 0's dyn_tend edge
+    kernel (option fusecopy; stage 0 runs rk_step > 0 kernels under schedule 0, which read
+    ru_save), theta_m(cell2) + theta_m(cell1) per edge taken
     from dyn_tend's edge kernel (option tmedge) and independent neighbouring kernels
     sharing a launch (option hfuse) is value-identical to the separate launches and
     to the oracle, in exact mode and on the fast path; raw 1-based ids leave edge 0 listed
@@ -484,6 +488,11 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
         c, _ = _two_steps_gpu(st, hf, 0, 1, hfuse=1 - hf)
         bad = compare_states(c, b, rtol=0.0)
         assert not bad, f"hfuse={1 - hf}, fusedamp={hf} vs separate launches: {bad[:6]}"
+    for fc in (0, 1):  # setup's edge copies in the setup launch / in dyn_tend, exact and fast
+        for ex in (0, 1):
+            c, _ = _two_steps_gpu(st, 1, ex, 1, fusecopy=fc)
+            bad = compare_states(c, b if ex == 0 else ref, rtol=0.0)
+            assert not bad, f"fusecopy={fc}, exact={ex}: {bad[:6]}"
     c, _ = _two_steps_gpu(st, 1, 0, 1, fusesml=0)  # set_smlstep as its own launch
     bad = compare_states(c, b, rtol=0.0)
     assert not bad, f"fusesml=0 vs separate launches: {bad[:6]}"
