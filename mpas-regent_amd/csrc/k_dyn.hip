@@ -235,10 +235,23 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     for (int j = 0; j < QF; j++) ee_[j] = rec[2 + j];
     row_ld(woe, woe_);
     const bool kl = k < L;
+#ifndef MPAS_EXPT_EOE
+#define MPAS_EXPT_EOE QF
+#endif
+#ifndef MPAS_EXPT_ADV
+#define MPAS_EXPT_ADV (AF - 1)
+#endif
+    // (MPAS_EXPT_EOE / MPAS_EXPT_ADV < the list widths: a timing-only experiment build,
+    // tools/gather_cost.sh, that gathers fewer columns and reuses them -- wrong values)
 #pragma unroll
     for (int j = 0; j < QF; j += 2) {
-        gather2s<LP>(u_f, ee_[j], ee_[j + 1], k, ue_[j], ue_[j + 1]);
-        gather2s<LP>(pv_f, ee_[j], ee_[j + 1], k, pve_[j], pve_[j + 1]);
+        if (j < MPAS_EXPT_EOE) {
+            gather2s<LP>(u_f, ee_[j], ee_[j + 1], k, ue_[j], ue_[j + 1]);
+            gather2s<LP>(pv_f, ee_[j], ee_[j + 1], k, pve_[j], pve_[j + 1]);
+        } else {
+            ue_[j] = ue_[j - 2] * 1.0000001, ue_[j + 1] = ue_[j - 1] * 1.0000001;
+            pve_[j] = pve_[j - 2] * 1.0000001, pve_[j + 1] = pve_[j - 1] * 1.0000001;
+        }
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = rec[22];
@@ -254,7 +267,13 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     static_assert(AF == 9, "tv_ pairing below");
     double tr_phys;
 #pragma unroll
-    for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
+    for (int j = 0; j < AF - 1; j += 2) {
+        if (j < MPAS_EXPT_ADV) {
+            gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
+        } else {
+            tv_[j] = tv_[j - 2] * 1.0000001, tv_[j + 1] = tv_[j - 1] * 1.0000001;
+        }
+    }
     gather2<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k, tv_[AF - 1], tr_phys);
 
     // MD: the state w at the advCells, for the w reconstruction flux_arr of this edge

@@ -149,6 +149,113 @@ __global__ __launch_bounds__(256) void k_tr_edge(DevState S) {
     st2<LP>(fw(S, X_Ah), col8(e, p), col8(e, p + 1), k, PADW(u * acca - loa), PADW(u * accb - lob));
 }
 
+// k_tr_edge with the scalars_old columns staged in LDS (option "tredge", opt-in: measured
+// 2-9 % slower over the transport than the direct gathers at 8-16 edges per group, DESIGN.md
+// §7; LP = 64,
+// undecomposed; TrEdgeGroups in mpas_dev.h).  A block is one (group of TRE_GE consecutive
+// edges, scalar pair): its 4 wavefronts first copy the union's column pairs into LDS (one
+// 16-B lane load per cell: ~36 loads for the group's 144 advCell gathers), then each
+// computes every fourth edge of the group from LDS with k_tr_edge's expressions in its
+// order (the same bits).  The gathers were what bounded k_tr_edge (one 1-KB request per
+// advCell and scalar pair, served by the L2); LDS reads cost no memory requests.  An
+// irregular group (union > TRE_U, or an edge with more than AF advCells) gathers directly.
+struct TreK {
+    const int* ucell;
+    const int* ucnt;
+    const unsigned* eslot;
+    int ngroups;
+};
+__global__ __launch_bounds__(256) void k_tr_edge_lds(DevState S, TreK T) {
+    constexpr int LP = 64, NW = 4, NL = (TRE_U + NW - 1) / NW, EW = TRE_GE / NW;
+    static_assert(TRE_GE % NW == 0, "edges per wavefront");
+    __shared__ double2 lds[TRE_U * LP];
+    const int b = xcd_block_n(S.xcd, (int)blockIdx.x, (int)gridDim.x);
+    const int g = b >> 2, p = (b & 3) * 2;
+    if (g >= T.ngroups) return;
+    const int L = S.L, k = (int)(threadIdx.x % LP), w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / LP));
+    const int nu = T.ucnt[g];
+    const double* so = fd(S, F_scalars_old);
+    const int e0 = g * TRE_GE, ne = min(TRE_GE, S.nEO - e0);
+    // this wavefront's edges e0 + w, + NW, ...: their mass flux columns first, so that the
+    // loads overlap the staging (edges past the owned range load edge e0's and store nothing)
+    double u_[EW];
+#pragma unroll
+    for (int i = 0; i < EW; i++) {
+        const int q = w + i * NW;
+        u_[i] = colk(fd(S, F_ruAvg), e0 + (q < ne ? q : 0));
+    }
+    if (nu >= 0) {  // (block-uniform) stage the union: every load first, then the LDS stores
+        const int* uc = T.ucell + (size_t)g * TRE_U;
+        double a_[NL], b_[NL];
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int s = w + i * NW;
+            const int cell = uc[s < TRE_U ? s : 0];
+            ld2<LP>(so, col8(cell, p), col8(cell, p + 1), k, a_[i], b_[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < NL; i++) {
+            const int s = w + i * NW;
+            if (s < nu) lds[s * LP + k] = make_double2(a_[i], b_[i]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < EW; i++) {
+        const int q = w + i * NW;
+        if (q >= ne) break;
+        const int e = e0 + q;
+        const int* rec = fi(S, X_eB) + (size_t)e * 24;  // cellsOnEdge(2) .. advCellsForEdge(9) @12, nAdv @22
+        const int c1 = rec[0], c2 = rec[1], na = rec[22];
+        double ac[AF], ac3[AF];
+        row_ld(fd(S, F_adv_coefs) + (size_t)e * 15, ac);
+        row_ld(fd(S, F_adv_coefs_3rd) + (size_t)e * 15, ac3);
+        const double dv = fd(S, F_dvEdge)[e];
+        const double u = u_[i];
+        double xa[AF], xb[AF], s1a, s1b, s2a, s2b;
+        if (nu >= 0) {
+            unsigned sl[TRE_ROW / 4];
+#pragma unroll
+            for (int j = 0; j < TRE_ROW / 4; j++) sl[j] = T.eslot[(size_t)e * (TRE_ROW / 4) + j];
+            auto slot = [&](int j) { return (int)((sl[j >> 2] >> ((j & 3) * 8)) & 0xffu); };
+#pragma unroll
+            for (int j = 0; j < AF; j++) {
+                const double2 v = lds[slot(j) * LP + k];
+                xa[j] = v.x, xb[j] = v.y;
+            }
+            const double2 v1 = lds[slot(AF) * LP + k], v2 = lds[slot(AF + 1) * LP + k];
+            s1a = v1.x, s1b = v1.y, s2a = v2.x, s2b = v2.y;
+        } else {
+            int adv[AF];
+#pragma unroll
+            for (int j = 0; j < AF; j++) adv[j] = rec[12 + j];
+#pragma unroll
+            for (int j = 0; j < AF; j++) ld2<LP>(so, col8(adv[j], p), col8(adv[j], p + 1), k, xa[j], xb[j]);
+            ld2<LP>(so, col8(c1, p), col8(c1, p + 1), k, s1a, s1b);
+            ld2<LP>(so, col8(c2, p), col8(c2, p + 1), k, s2a, s2b);
+        }
+        const double sgn = copysign(1.0, u);
+        double acca = 0.0, accb = 0.0;
+#pragma unroll
+        for (int j = 0; j < AF; j++) {
+            const double wgt = ac[j] + sgn * ac3[j];
+            acca = add_if(j < na, acca, wgt * xa[j]);
+            accb = add_if(j < na, accb, wgt * xb[j]);
+        }
+        for (int j = AF; j < na; j++) {  // (irregular groups only)
+            const int cj = fi(S, F_advCellsForEdge)[(size_t)e * 15 + j];
+            const double wgt = fd(S, F_adv_coefs)[(size_t)e * 15 + j] + sgn * fd(S, F_adv_coefs_3rd)[(size_t)e * 15 + j];
+            double ya, yb;
+            ld2<LP>(so, col8(cj, p), col8(cj, p + 1), k, ya, yb);
+            acca = acca + wgt * ya;
+            accb = accb + wgt * yb;
+        }
+        const double loa = dv * (fmax(u, 0.0) * s1a + fmin(u, 0.0) * s2a);
+        const double lob = dv * (fmax(u, 0.0) * s1b + fmin(u, 0.0) * s2b);
+        st2<LP>(fw(S, X_Ah), col8(e, p), col8(e, p + 1), k, PADW(u * acca - loa), PADW(u * accb - lob));
+    }
+}
+
 // the first NF edge slots of a cell: edge, cells of the edge, "cell is cellsOnEdge(0)",
 // the other cell, dvEdge (the per-cell copies of k_prepare)
 struct TrSlots {
@@ -630,6 +737,13 @@ static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
     // on two rings for the adv lists, A on the ghost edges of owned cells, R+/R- on the
     // neighbour cells); the x8 fields move as 8 columns per entity (mpas_halo.hip)
     auto ke = [&](const DevState& X) {
+        if constexpr (LP == 64) {
+            if (X.tre && !X.halo && X.lo[KE] == 0 && X.tre->neo == X.nEO) {  // (option "tredge")
+                const TrEdgeGroups& G = *X.tre;
+                if (G.ngroups) k_tr_edge_lds<<<G.ngroups * (NSC / 2), 256, 0, st>>>(X, TreK{G.ucell, G.ucnt, G.eslot, G.ngroups});
+                return;
+            }
+        }
         const int nb = blocks(X, KE);
         if (nb) k_tr_edge<LP><<<nb, 256, 0, st>>>(X);
     };

@@ -143,6 +143,11 @@ struct mpas_ctx {
                          // advCellsForEdge(edgesOnCell) (decomp.Decomposition(tiled_transport))
     bool trt_dirty = true;
     TrTiles trt;
+    // option "tredge" (default 0: measured slower): the transport's edge kernel
+    // with scalars_old staged in LDS per group of consecutive edges (undecomposed contexts;
+    // rebuilt with the tiles)
+    int tredge = 0;
+    TrEdgeGroups tre;
 };
 
 namespace {
@@ -466,9 +471,72 @@ std::vector<V> dev_read(const void* d, size_t n) {
 // on the device resolve -- would exceed trt_clo LDS columns (default 96: 48 KB at LP = 64,
 // three blocks per CU).  Not built (the three-kernel path runs) when an owned cell has more
 // than NF edges or one of its edges more than AF advCells.
+// The edge groups of k_tr_edge_lds (TrEdgeGroups, mpas_dev.h): TRE_GE consecutive owned
+// edges per group; LDS columns in first-use order over the group's edges (advCells, then
+// the two cells of the edge).
+void tre_free(mpas_ctx* c) {
+    TrEdgeGroups& G = c->tre;
+    for (void* p : {(void*)G.ucell, (void*)G.ucnt, (void*)G.eslot})
+        if (p) (void)hipFree(p);
+    G = TrEdgeGroups{};
+    c->S.tre = nullptr;
+}
+void tre_build(mpas_ctx* c) {
+    tre_free(c);
+    if (!c->tredge || c->halo || c->S.LP != 64) return;
+    const DevState& S = c->S;
+    const int nE = S.nEdges, nEO = S.nEO;
+    if (nEO <= 0) return;
+    const auto coe = dev_read<int>(S.f[F_cellsOnEdge], ((size_t)nE + 1) * 2);
+    const auto adv = dev_read<int>(S.f[F_advCellsForEdge], ((size_t)nE + 1) * 15);
+    const auto nadv = dev_read<int>(S.f[F_nAdvCellsForEdge], (size_t)nE + 1);
+    const int ng = (nEO + TRE_GE - 1) / TRE_GE;
+    std::vector<int> ucell((size_t)ng * TRE_U, 0), ucnt(ng, 0);
+    std::vector<unsigned char> eslot((size_t)nEO * TRE_ROW, 0);
+    int nirr = 0;
+    for (int g = 0; g < ng; g++) {
+        std::vector<int> u;
+        bool ok = true;
+        auto slot_of = [&](int cell) {
+            for (size_t i = 0; i < u.size(); i++)
+                if (u[i] == cell) return (int)i;
+            u.push_back(cell);
+            return (int)u.size() - 1;
+        };
+        for (int e = g * TRE_GE; e < std::min(nEO, (g + 1) * TRE_GE) && ok; e++) {
+            const int na = nadv[e];
+            if (na > AF) ok = false;
+            unsigned char* r = &eslot[(size_t)e * TRE_ROW];
+            for (int j = 0; j < AF && ok; j++) r[j] = (unsigned char)slot_of(adv[(size_t)e * 15 + j]);
+            r[AF] = (unsigned char)slot_of(coe[(size_t)e * 2]);
+            r[AF + 1] = (unsigned char)slot_of(coe[(size_t)e * 2 + 1]);
+            if ((int)u.size() > TRE_U) ok = false;
+        }
+        if (!ok) {
+            ucnt[g] = -1;
+            nirr++;
+            continue;
+        }
+        ucnt[g] = (int)u.size();
+        for (int i = 0; i < TRE_U; i++) ucell[(size_t)g * TRE_U + i] = i < (int)u.size() ? u[i] : u[0];
+    }
+    TrEdgeGroups& G = c->tre;
+    G.ngroups = ng;
+    G.neo = nEO;
+    G.nirr = nirr;
+    G.ucell = dev_copy(ucell);
+    G.ucnt = dev_copy(ucnt);
+    std::vector<unsigned> packed(eslot.size() / 4);
+    std::memcpy(packed.data(), eslot.data(), eslot.size());
+    G.eslot = dev_copy(packed);
+    c->S.tre = &c->tre;
+}
+
 void trt_build(mpas_ctx* c) {
     trt_free(c);
+    tre_free(c);
     c->trt_dirty = false;
+    tre_build(c);
     if (!c->trtile) return;
     if (c->halo && !c->trt_ghosts) return;  // the tiles would read ghosts the local mesh lacks
     hipcheck(hipSetDevice(c->device), "hipSetDevice");
@@ -993,6 +1061,9 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "trtile") == 0) {
             c->trtile = value ? 1 : 0;
             c->trt_dirty = true;
+        } else if (name && std::strcmp(name, "tredge") == 0) {
+            c->tredge = value ? 1 : 0;
+            c->trt_dirty = true;
         } else if (name && std::strcmp(name, "trtile_ghosts") == 0) {
             c->trt_ghosts = value ? 1 : 0;
             c->trt_dirty = true;
@@ -1035,6 +1106,14 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "transport") == 0) *value = c->transport;
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
+        else if (name && std::strcmp(name, "tredge") == 0) *value = c->tredge;
+        else if (name && std::strcmp(name, "tredge_active") == 0) {  // edge groups built for this mesh
+            trt_ensure(c);
+            *value = c->S.tre != nullptr;
+        } else if (name && std::strcmp(name, "tredge_irregular") == 0) {
+            trt_ensure(c);
+            *value = c->tre.nirr;
+        }
         else if (name && std::strcmp(name, "ring1") == 0) *value = c->S.ring1;
         else if (name && std::strcmp(name, "trtcells") == 0) *value = c->trt_cells;
         else if (name && std::strcmp(name, "trtile_ghosts") == 0) *value = c->trt_ghosts;

@@ -97,6 +97,7 @@ extern const FieldInfo kFields[X_COUNT];
 
 struct Halo;  // mpas_halo.h
 struct TrTiles;  // below: the cell tiles of the tiled transport
+struct TrEdgeGroups;  // below: the edge groups of the transport's edge kernel
 
 struct DevState {
     int nCells, nEdges, nVertices, L, LP;  // local entity counts (= the zero-slot ids)
@@ -128,6 +129,7 @@ struct DevState {
     void* f[X_COUNT];
     Halo* halo;  // host-side halo exchanger of a decomposed mesh, nullptr otherwise
     const TrTiles* trt;  // host-side: the tiles of the tiled transport, nullptr = the three-kernel path
+    const TrEdgeGroups* tre;  // host-side: the edge groups of k_tr_edge_lds, nullptr = k_tr_edge
     const int* gid[3];  // device global ids of the local cells/edges/vertices (decomposed
                         // meshes: the synthetic fill hashes them), nullptr = identity
 };
@@ -361,6 +363,27 @@ struct TrTiles {
     int* cptr = nullptr;         // ntiles + 1: first closure cell of each tile in ccell
     int* ccell = nullptr;        // closure cells, in LDS column order
     int* slot = nullptr;          // TRT_ROW LDS columns per tile cell (tcell order)
+};
+
+// The transport's edge kernel with its scalars_old columns staged in LDS (k_tr_edge_lds,
+// option "tredge"): the owned edges in groups of TRE_GE consecutive ids (Morton-adjacent);
+// a group's UNION is the distinct cells its edges read scalars_old at (advCellsForEdge
+// and cellsOnEdge), at most TRE_U; a group with a larger union or an edge with more than AF
+// advCells is irregular (ucnt = -1) and gathers directly.  Built on the host (tre_build).
+#ifndef MPAS_TRE_GE
+#define MPAS_TRE_GE 16
+#define MPAS_TRE_U 52
+#endif
+constexpr int TRE_GE = MPAS_TRE_GE;  // edges per group
+constexpr int TRE_U = MPAS_TRE_U;    // LDS columns per group (52 KB at LP = 64 with a scalar pair
+                                     // each: three blocks per CU)
+constexpr int TRE_ROW = 12;  // slot bytes per edge: AF advCells, cellsOnEdge(0), (1), pad
+struct TrEdgeGroups {
+    int ngroups = 0, neo = 0;  // groups; the owned edge count they were built for
+    int nirr = 0;              // irregular groups (reported by option "tredge_irregular")
+    int* ucell = nullptr;      // ngroups * TRE_U: the union's cells (padding: its first cell)
+    int* ucnt = nullptr;       // ngroups: union size, -1 = irregular
+    unsigned* eslot = nullptr; // neo * TRE_ROW / 4: each edge's LDS columns, one byte each
 };
 
 // value of x held by level k-1 of the same column (0.0 at k == 0: level -1 reads 0)

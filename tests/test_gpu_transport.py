@@ -175,3 +175,36 @@ def test_tiled_equals_three_kernel(x1_2562, L):
         outs[tile] = got
     bad = compare_states(outs[1], outs[0], rtol=0.0)
     assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("variant", ["mesh", "random"])
+@pytest.mark.parametrize("L", [56, 63])
+def test_edge_groups_equal_direct(x1_2562, variant, L):
+    """option tredge (opt-in, LP 64): k_tr_edge_lds, the edge kernel with each group's
+    scalars_old columns staged in LDS, against tredge = 0 (k_tr_edge's direct gathers) and
+    the oracle: bit for bit; random ids make irregular groups (too large a union: direct
+    gathers inside the same kernel)"""
+    if variant == "mesh":
+        st, _ = transport_state(x1_2562, L, DT)
+    else:
+        st = make_state(x1_2562, L, "random")
+    ref = st.copy()
+    O.Oracle(ref).mpas_advance_scalars_mono(DT)
+    outs = {}
+    for on in (0, 1):
+        got = st.copy()
+        with lib.Context(*st.dims()) as ctx:
+            ctx.set_option("physics", 1)
+            ctx.set_option("tredge", on)
+            ctx.upload(st)
+            assert ctx.get_option("tredge_active") == on
+            if on and variant == "random":
+                assert ctx.get_option("tredge_irregular") > 0
+            T.atm_advance_scalars_mono(ctx, DT)
+            ctx.sync()
+            ctx.download(got)
+        outs[on] = got
+    bad = compare_states(outs[1], outs[0], rtol=0.0)
+    assert not bad, bad[:6]
+    bad = compare_states(outs[1], ref, rtol=0.0)
+    assert not bad, bad[:6]

@@ -3,7 +3,8 @@
 workload once and runs interleaved rounds of full RK3 steps under each option set,
 reporting the median per-task device time (HIP events on the task stream).
 
-usage: python tools/kbench.py [--ncells 163842] [--levels 56] [--rounds 5] --variants "xcd=1" "xcd=0"
+usage: python tools/kbench.py [--ncells 163842] [--levels 56] [--rounds 5] [--physics N] [--transport]
+       --variants "xcd=1" "xcd=0"
 """
 import argparse
 import json
@@ -25,9 +26,14 @@ def main():
     ap.add_argument("--levels", type=int, default=56)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--variants", nargs="+", default=["xcd=1", "xcd=0"])
+    ap.add_argument("--physics", type=int, default=0)
+    ap.add_argument("--transport", action="store_true", help="physics 1 + the scalar transport (bench --transport)")
     a = ap.parse_args()
-    m, st = bench.build_inputs(a.ncells, a.levels)
+    physics = max(a.physics, 1 if a.transport else 0)
+    m, st = bench.build_inputs(a.ncells, a.levels, zero_based=physics)
     ctx = lib.Context(m.nCells, m.nEdges, m.nVertices, a.levels)
+    ctx.set_option("physics", physics)
+    ctx.set_option("transport", int(a.transport))
     bench.upload_inputs(ctx, st)
     dt = bench.dt_for(a.ncells)
     T.atm_srk3(ctx, dt, 1)
