@@ -98,11 +98,10 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * compact cell tiles in LDS and no edge scratch, when every cell has at most 6 edges with
  * at most 9 advCells each (bit-identical; measured slower); "trtcells" and
  * "trtclo" bound a tile's cells (default 16) and LDS columns (default 96); read-only
- * "trtile_active" / "trtile_count" report whether tiles are built and how many.  On a
+ * "trtile_active" / "trtile_count" report whether tiles are built and how many.
  * "tredge" = 1 (speed only, default 0) stages each group of 16 consecutive edges' scalars_old
  * columns in LDS for the transport's edge kernel (bit-identical; measured slower, DESIGN.md
- * §7; read-only "tredge_active", "tredge_irregular").  On a
- * decomposed context the tiles are built only with "trtile_ghosts" = 1, which declares that
+ * §7; read-only "tredge_active", "tredge_irregular").  On a decomposed context the tiles are built only with "trtile_ghosts" = 1, which declares that
  * the ghosts close over advCellsForEdge(edgesOnCell) (mpasdyn.decomp.Decomposition(...,
  * tiled_transport=True); lib.setup_subdomain sets it). */
 int mpas_set_option(mpas_ctx* ctx, const char* name, int64_t value);
