@@ -293,6 +293,14 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_compute_solve_diagnostics[vc]": {"part": "vc"}, "atm_compute_solve_diagnostics[e]": {"part": "e"},
              "hfuse[damp+solve_vc]": {"pair": "damp+solve_vc"}, "hfuse[solve_e+finish]": {"pair": "solve_e+finish"},
              "hfuse[solve_e+vert_imp]": {"pair": "solve_e+vert_imp"},
+             "hfuse[acoustic+solve_vc]": {"pair": "acoustic+solve_vc"},
+             "hfuse[solve_e+dyn_A]": {"pair": "solve_e+dyn_A"},
+             "hfuse[solve_e+vert_imp+dyn_A]": {"pair": "solve_e+vert_imp+dyn_A"},
+             "atm_compute_dyn_tend_work[rk>0-A]": {"rk_step": 1, "noA": True},
+             "atm_compute_dyn_tend_work[rk0-A]": {"rk_step": 0, "noA": True},
+             "atm_compute_dyn_tend_work[rk0+copy-A]": {"rk_step": 0, "copy": True, "noA": True},
+             "atm_compute_dyn_tend_work[rk>0+copy-A]": {"rk_step": 1, "copy": True, "noA": True},
+             "hfuse[setup+dyn_A]": {"pair": "setup+dyn_A"},
              "atm_advance_acoustic_step_work[ss0+sml+damp]": {"small_step": 0, "damp": True, "sml": True},
              "atm_advance_acoustic_step_work[ss>0+damp]": {"small_step": 1, "damp": True},
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},

@@ -14,6 +14,7 @@
 // to rounding (tests/test_gpu_parity.py states the tolerance).  The EXACT=true
 // variant evaluates the literal expression level by level (lane k-1 -> lane k
 // broadcast) and is bit-identical to the oracle; it is the reference for the scan.
+#include "k_cols.h"
 #include "mpas_dev.h"
 #include "mpas_halo.h"
 
@@ -53,12 +54,12 @@ __device__ __forceinline__ double damp_edge(double rup, double d1, double d2, do
 // one gathered column per edge instead of two -- the same sums
 // SML (atm_srk3, option "fusesml"; a stage's first substep): the stage's set_smlstep first
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>
-__global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm,
-                                                 double coefp, int ncb) {
+__device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int small_step, double epssm, double resm,
+                                              double coefp, int ncb, Blk bk) {
     static_assert(!(MPASV && MODE), "the deferred damping is the reference semantics' (physics 0)");
     static_assert(!SML || (FIRST && !MPASV), "set_smlstep precedes a stage's first substep (reference semantics)");
     const int L = S.L, k = (int)(threadIdx.x % LP);
-    int blk = (int)blockIdx.x;
+    int blk = bk.b;
     if constexpr (MODE == 2) {
         if (blk >= ncb) {  // an edge no cell lists: the damping alone, into the new buffer
             const int j = col_of<LP>(blk - ncb);
@@ -73,7 +74,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
             return;
         }
     }
-    blk = xcd_block_n(S.xcd, blk, MODE == 2 ? ncb : (int)gridDim.x);
+    blk = xcd_block_n(S.xcd, blk, MODE == 2 ? ncb : bk.n);
     const int c = col_of<LP>(blk) + S.lo[KC];
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + lpos(LP, k);
@@ -392,6 +393,24 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     put2<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww), true, true);
     store_div(rtp_new);
 }
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>
+__global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm,
+                                                 double coefp, int ncb) {
+    acoustic_body<LP, EXACT, SELF, FIRST, MPASV, MODE, TME, SML>(S, dts, small_step, epssm, resm, coefp, ncb,
+                                                                this_blk());
+}
+// option "hfuse" (atm_srk3, stages 0 and 1): a stage's last acoustic launch (MODE 2, the
+// damping of the previous substep inside) beside the stage's solve_diagnostics vertex /
+// cell kernel, which reads u only -- nothing the acoustic step reads or writes
+template <int LP, bool EXACT, bool SELF, int EPW>
+__global__ __launch_bounds__(256) void k_hf_ac_vc(DevState S, double dts, int small_step, double epssm, double resm,
+                                                 double coefp, int ncb, int nb1, int nVB) {
+    const int b = (int)blockIdx.x;
+    if (b < nb1)
+        acoustic_body<LP, EXACT, SELF, false, false, 2, false, false>(S, dts, small_step, epssm, resm, coefp, ncb,
+                                                                       Blk{b, nb1});
+    else solve_vc_body<LP, EPW, false>(S, nVB, 0, Blk{b - nb1, (int)gridDim.x - nb1});
+}
 
 // :1581-1613 restored (Q18, MPAS vertical solver only): ru_p and ruAvg of every owned
 // edge, before the cell kernel reads ru_p
@@ -491,6 +510,29 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
                            double coef_prev, int tme, int sml) {
     MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml);
+}
+template <int LP>
+static hipError_t hf_ac_vc_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
+                              double coef_prev) {
+    if (S.physics || S.halo || small_step == 0 || S.epw != 2) return hipErrorInvalidValue;
+    const double epssm = kEpssm, resm = (1.0 - epssm) / (1.0 + epssm);
+    const int ncb = col_blocks<LP>(S, KC);
+    const int nb1 = ncb + (S.n_orph + 256 / LP - 1) / (256 / LP);
+    const int nv = col_blocks_n<LP, 2>(S, KV), nb2 = nv + col_blocks_n<LP, 2>(S, KC);
+    if (!ncb || !nb2) return hipErrorInvalidValue;
+    const int grid = nb1 + nb2;
+    if (exact) {
+        if (S.selfc) k_hf_ac_vc<LP, true, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
+        else k_hf_ac_vc<LP, true, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
+    } else {
+        if (S.selfc) k_hf_ac_vc<LP, false, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
+        else k_hf_ac_vc<LP, false, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
+    }
+    return hipGetLastError();
+}
+hipError_t launch_hf_acoustic_solve_vc(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
+                                       double coef_prev) {
+    MPAS_LP_DISPATCH(S.LP, hf_ac_vc_lp, S, st, dts, small_step, exact, coef_prev);
 }
 
 }  // namespace mpas

@@ -31,6 +31,7 @@
 // Memory-level parallelism: every loop over a connectivity list first issues the
 // loads of the first NF/QF/AF entries unconditionally (padding ids are valid), then
 // accumulates in the reference's order; longer lists finish in a generic tail loop.
+#include "k_cols.h"
 #include "mpas_dev.h"
 #include "mpas_halo.h"
 
@@ -55,9 +56,12 @@ struct DynK {
 
 
 // ------------------------------------------------------------------------ A (cells)
-template <int LP, bool RK0, bool MD>
-__global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
-    ColMap<LP> m(S, KC);
+// SETUP (atm_srk3 stage 0 beside the fused setup launch, option hfuse): rho_p_save and qtot
+// are being written by that launch -- rho_p_save = rho_p and qtot = 0 at every level A
+// stores (k != L) -- so A takes rho_p and 0.0 instead: the same values
+template <int LP, bool RK0, bool MD, bool SETUP = false>
+__device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk bk) {
+    ColMap<LP> m(S, KC, bk);
     const int L = S.L, k = m.k, c = m.ent;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + lpos(LP, k);
@@ -100,9 +104,9 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
     double trp = 0.0, qt = 0.0, rb = 0.0, rps = 0.0;
     if (rk0) {
         trp = colk(fd(S, F_tend_rho_physics), c);
-        qt = colk(fd(S, F_qtot), c);
+        qt = SETUP ? 0.0 : colk(fd(S, F_qtot), c);
         rb = colk(fd(S, F_rho_base), c);
-        rps = colk(fd(S, F_rho_p_save), c);
+        rps = colk(fd(S, SETUP ? F_rho_p : F_rho_p_save), c);
     }
 
     // ---- kdiff (:858-917)
@@ -193,6 +197,10 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
               2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
     }
     put2<LP>(fw(S, F_h_divergence), c, fw(S, X_wc), c, k, PADW(hd), k < L ? wc : 0.0, k != L, true);
+}
+template <int LP, bool RK0, bool MD>
+__global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
+    dyn_A_body<LP, RK0, MD>(S, a, this_blk());
 }
 
 // ------------------------------------------------------------------------ B (edges)
@@ -873,8 +881,7 @@ __global__ __launch_bounds__(256) void k_dyn_DE(DevState S, DynK a, int nb1) {
     else dyn_E_body<LP, true, SELF, MD, HF>(S, a, Blk{b - nb1, (int)gridDim.x - nb1});
 }
 
-template <int LP, bool MD>
-static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs& in) {
+static DynK make_dynk(const DevState& S, const DynTendArgs& in) {
     DynK a;
     a.rk_step = in.rk_step;
     a.horiz_mixing = in.horiz_mixing;
@@ -892,6 +899,12 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     a.inv_r_earth = 1.0 / a.r_earth;
     a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
     a.prandtl_inv = 1.0 / kPrandtl;
+    return a;
+}
+
+template <int LP, bool MD>
+static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs& in) {
+    const DynK a = make_dynk(S, in);
     const bool rk0 = a.rk_step == 0, del4 = rk0 && a.h4 > 0.0;
     // HF: the fast path's theta flux per edge formed in B (E sums eocs H; reassociated, so
     // exact mode keeps the reference's per-cell order)
@@ -944,8 +957,12 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     // halo: fields each kernel gathers through an index array / fields it writes
     // (u and v only for the Smagorinsky deformation of rk_step 0: a gather declared but not
     // made would cost an exchange whenever v is stale)
-    if (rk0 && a.horiz_mixing == 0) HALO_RUN(S, st, kA, F_ru, F_u, F_v);
-    else HALO_RUN(S, st, kA, F_ru);
+    if (in.skipA) {  // (A ran in the previous combined launch, atm_srk3 hfuse; no halo)
+    } else if (rk0 && a.horiz_mixing == 0) {
+        HALO_RUN(S, st, kA, F_ru, F_u, F_v);
+    } else {
+        HALO_RUN(S, st, kA, F_ru);
+    }
     HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz);
     if (!MD) HALO_WROTE(S, X_wc);
     if (rk0) {
@@ -995,6 +1012,71 @@ static hipError_t dyn_lp(const DevState& S, hipStream_t st, const DynTendArgs& i
 }
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& in) {
     MPAS_LP_DISPATCH(S.LP, dyn_lp, S, st, in);
+}
+
+// option "hfuse" (atm_srk3, reference semantics, undecomposed): the next stage's dyn_tend A
+// (cells: h_divergence and the w scratch from ru, rw, rho_zz, uReconstruct*; at rk_step 0
+// also kdiff, tend_rho, dpdz from u, v, qtot, rho_p_save) beside the stage's solve_diagnostics
+// edge kernel (h_edge, ke_edge, pv_edge from h, u, pv_vertex) -- and, after stage 0, beside
+// stage 1's vert_imp too: none of them reads what another writes
+template <int LP, int EPW, bool RK0, bool VI>
+__global__ __launch_bounds__(256) void k_hf_e_A(DevState S, DynK a, int nb1, int nb2, double dtseps, double rcv,
+                                               double c2) {
+    const int b = (int)blockIdx.x;
+    if (b < nb1) {
+        solve_e_body<LP, false, false, EPW>(S, Blk{b, nb1});
+    } else if (VI && b < nb1 + nb2) {
+        vert_imp_body<LP, false>(S, dtseps, rcv, c2, Blk{b - nb1, nb2});
+    } else {
+        const int o = nb1 + (VI ? nb2 : 0);
+        dyn_A_body<LP, RK0, false>(S, a, Blk{b - o, (int)gridDim.x - o});
+    }
+}
+template <int LP>
+static hipError_t hf_e_A_lp(const DevState& S, hipStream_t st, const DynTendArgs& next, int vi, double dts_vi) {
+    if (S.halo || S.physics || S.epw != 2) return hipErrorInvalidValue;
+    const DynK a = make_dynk(S, next);
+    const bool rk0 = a.rk_step == 0;
+    const double dtseps = .5 * dts_vi * (1.0 + kEpssm), rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
+    const int nb1 = col_blocks_n<LP, 2>(S, KE), nb2 = vi ? col_blocks<LP>(S, KC) : 0, nb3 = col_blocks<LP>(S, KC);
+    if (!nb1 || !nb3) return hipErrorInvalidValue;
+    const int grid = nb1 + nb2 + nb3;
+    if (vi) {
+        if (rk0) k_hf_e_A<LP, 2, true, true><<<grid, 256, 0, st>>>(S, a, nb1, nb2, dtseps, rcv, c2);
+        else k_hf_e_A<LP, 2, false, true><<<grid, 256, 0, st>>>(S, a, nb1, nb2, dtseps, rcv, c2);
+    } else {
+        if (rk0) k_hf_e_A<LP, 2, true, false><<<grid, 256, 0, st>>>(S, a, nb1, 0, dtseps, rcv, c2);
+        else k_hf_e_A<LP, 2, false, false><<<grid, 256, 0, st>>>(S, a, nb1, 0, dtseps, rcv, c2);
+    }
+    return hipGetLastError();
+}
+hipError_t launch_hf_solve_e_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& next, int vi, double dts_vi) {
+    MPAS_LP_DISPATCH(S.LP, hf_e_A_lp, S, st, next, vi, dts_vi);
+}
+
+// option "hfuse" (atm_srk3 stage 0, with fusesetup): dyn_tend A beside the setup + moist +
+// vert_imp launch (k_setup_vi's body, k_misc.hip); A reads nothing that launch writes but
+// rho_p_save and qtot, whose values it takes at their source (SETUP above)
+template <int LP, bool RK0>
+__global__ __launch_bounds__(256) void k_hf_setup_A(DevState S, DynK a, int ncb, int nb1, double dtseps, double rcv,
+                                                   double c2) {
+    const int b = (int)blockIdx.x;
+    if (b < nb1) setup_vi_body<LP>(S, ncb, dtseps, rcv, c2, Blk{b, nb1});
+    else dyn_A_body<LP, RK0, false, true>(S, a, Blk{b - nb1, (int)gridDim.x - nb1});
+}
+template <int LP>
+static hipError_t hf_setup_A_lp(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges) {
+    if (S.halo || S.physics) return hipErrorInvalidValue;
+    const DynK a = make_dynk(S, stage0);
+    const double dtseps = .5 * dts * (1.0 + kEpssm), rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
+    const int ncb = col_blocks<LP>(S, KC), nb1 = ncb + (edges ? col_blocks<LP>(S, KE) : 0);
+    if (!ncb) return hipErrorInvalidValue;
+    if (a.rk_step == 0) k_hf_setup_A<LP, true><<<nb1 + ncb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
+    else k_hf_setup_A<LP, false><<<nb1 + ncb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
+    return hipGetLastError();
+}
+hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges) {
+    MPAS_LP_DISPATCH(S.LP, hf_setup_A_lp, S, st, stage0, dts, edges);
 }
 
 }  // namespace mpas

@@ -161,38 +161,7 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 // makes those copies).  The same values as the three launches.
 template <int LP>
 __global__ __launch_bounds__(256) void k_setup_vi(DevState S, int ncb, double dtseps, double rcv, double c2) {
-    const int L = S.L, k = (int)(threadIdx.x % LP);
-    int blk = (int)blockIdx.x;
-    if (blk >= ncb) {  // :767-771 ru_save = ru, u_2 = u (every level but L)
-        const int e = col_of<LP>(xcd_block_n(S.xcd, blk - ncb, (int)gridDim.x - ncb)) + S.lo[KE];
-        if (e >= S.nEO) return;
-        double ru, u;
-        gather2<LP>(fd(S, F_ru), e, fd(S, F_u), e, k, ru, u);
-        put2<LP>(fw(S, F_ru_save), e, fw(S, F_u_2), e, k, PADW(ru), PADW(u), k != L, k != L);
-        return;
-    }
-    const int c = col_of<LP>(xcd_block_n(S.xcd, blk, ncb)) + S.lo[KC];
-    if (c >= S.nCO) return;
-    double rw, rtp, rp, w, tm, rz, zz, exner, rb, rtb, exb, gamma_old;
-    gather2<LP>(fd(S, F_rw), c, fd(S, F_rtheta_p), c, k, rw, rtp);
-    gather2<LP>(fd(S, F_rho_p), c, fd(S, F_w), c, k, rp, w);
-    gather2<LP>(fd(S, F_theta_m), c, fd(S, F_rho_zz), c, k, tm, rz);
-    gather2<LP>(fd(S, F_zz), c, fd(S, F_exner), c, k, zz, exner);
-    gather2<LP>(fd(S, F_rho_base), c, fd(S, F_rtheta_base), c, k, rb, rtb);
-    gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
-    const double coftz_old = colk(fd(S, F_coftz), c);
-    // :773-777 the save copies (every level but L; padding levels carry zeros either way)
-    const bool cp = k != L;
-    put2<LP>(fw(S, F_rw_save), c, fw(S, F_rtheta_p_save), c, k, PADW(rw), PADW(rtp), cp, cp);
-    put2<LP>(fw(S, F_rho_p_save), c, fw(S, F_w_2), c, k, PADW(rp), PADW(w), cp, cp);
-    put2<LP>(fw(S, F_theta_m_2), c, fw(S, F_rho_zz_2), c, k, PADW(tm), PADW(rz), cp, cp);
-    if (cp) colk(fw(S, F_rho_zz_old_split), c) = PADW(rz);
-    // :473-489 (k_moist's expressions): qtot = 0; cqw(k > 0) from the two zeroed qtot
-    const double q_k = 0.0, q_km1 = 0.0, qtotal = 0.5 * (q_k + q_km1);
-    const double cqw = k > L ? 0.0 : 1.0 / (1.0 + qtotal), qtot = 0.0;
-    put2<LP>(fw(S, F_qtot), c, fw(S, F_cqw), c, k, qtot, cqw, cp, cp && k > 0);
-    // (cqw is used at 0 < k < L only, qtot at k < L: the values just written)
-    vi_column<LP, false>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2);
+    setup_vi_body<LP>(S, ncb, dtseps, rcv, c2, this_blk());
 }
 template <int LP>
 static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts, bool edges) {

@@ -723,14 +723,6 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     }
     // option fusecopy: ru_save / u_2 by stage 0's dyn_tend edge kernel (reads u and ru there)
     const bool fcopy = c->fusesetup && c->fusecopy && S.physics == 0 && !c->halo;
-    if (c->fusesetup && S.physics == 0) {  // :404-417 as one column-local launch (same values)
-        run_task(c, fcopy ? "atm_rk_integration_setup[cells+moist+vert_imp]" : "atm_rk_integration_setup[+moist+vert_imp]",
-                 [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0], !fcopy); });
-    } else {
-        run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
-        run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
-        run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
-    }
     // option fusedamp (reference semantics, undecomposed): each damping but the step's last
     // is applied by the next acoustic launch (k_acoustic MODE 2), the last from the div
     // the acoustic step stored (launch_div_damping_div); the same bits as the separate task
@@ -749,11 +741,14 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // rk 0 D beside E); the same values
     const int hf = hfuse_active(c) ? 1 : 0;
     bool vi_done = false;  // stage 1's vert_imp ran beside stage 0's solve_diagnostics edges
-    for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
-        if (rk_step == 1 && !vi_done)
-            run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
+    // hfuse with fusedamp (and the default epw, no tmedge): a stage's last acoustic launch
+    // beside its solve_diagnostics vertex / cell kernel, and the stage's edge kernel beside
+    // the next stage's dyn_tend A (k_acoustic.hip / k_dyn.hip combined launches)
+    const bool hf2 = hf && fuse && !tme && S.epw == 2;
+    bool vc_done = false, a_done = false;
+    auto stage_args = [&](int r) {
         DynTendArgs a{};
-        a.rk_step = schedule == 0 ? (int)rk_sub_timestep[rk_step] : rk_step;  // Q4
+        a.rk_step = schedule == 0 ? (int)rk_sub_timestep[r] : r;  // Q4
         a.dt = dt;
         a.horiz_mixing = 0;  // constants.rg:57 "2d_smagorinsky"
         a.cam_coef = 0.0;
@@ -762,10 +757,34 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a.exact_q = c->exact;
         a.tme = tme;
         a.hfuse = hf;
-        a.cp = (fcopy && rk_step == 0) ? 1 : 0;
-        run_task(c, a.cp ? (a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0+copy]" : "atm_compute_dyn_tend_work[rk>0+copy]")
-                         : (a.rk_step == 0 ? "atm_compute_dyn_tend_work[rk0]" : "atm_compute_dyn_tend_work[rk>0]"),
-                 [&] { return launch_dyn_tend(S, st, a); });
+        a.cp = (fcopy && r == 0) ? 1 : 0;
+        return a;
+    };
+    if (c->fusesetup && S.physics == 0 && hf2) {  // + stage 0's dyn_tend A in the same launch
+        run_task(c, "hfuse[setup+dyn_A]", [&] {
+            return launch_hf_setup_dyn_A(S, st, stage_args(0), rk_sub_timestep[0], fcopy ? 0 : 1);
+        });
+        a_done = true;
+    } else if (c->fusesetup && S.physics == 0) {  // :404-417 as one column-local launch (same values)
+        run_task(c, fcopy ? "atm_rk_integration_setup[cells+moist+vert_imp]" : "atm_rk_integration_setup[+moist+vert_imp]",
+                 [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0], !fcopy); });
+    } else {
+        run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
+        run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
+        run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
+    }
+    for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
+        if (rk_step == 1 && !vi_done)
+            run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
+        DynTendArgs a = stage_args(rk_step);
+        a.skipA = a_done ? 1 : 0;
+        a_done = false;
+        static const char* const dyn_names[2][2][2] = {  // [rk0][copy][skipA]
+            {{"atm_compute_dyn_tend_work[rk>0]", "atm_compute_dyn_tend_work[rk>0-A]"},
+             {"atm_compute_dyn_tend_work[rk>0+copy]", "atm_compute_dyn_tend_work[rk>0+copy-A]"}},
+            {{"atm_compute_dyn_tend_work[rk0]", "atm_compute_dyn_tend_work[rk0-A]"},
+             {"atm_compute_dyn_tend_work[rk0+copy]", "atm_compute_dyn_tend_work[rk0+copy-A]"}}};
+        run_task(c, dyn_names[a.rk_step == 0][a.cp][a.skipA], [&] { return launch_dyn_tend(S, st, a); });
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
         const bool sml = fuse && c->fusesml;
         if (!sml) run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
@@ -775,8 +794,15 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             if (fuse) {
                 const int mode = pending ? 2 : 1;
                 const int sm = (sml && small_step == 0) ? 1 : 0;
-                run_task(c, acoustic_name(small_step, pending, sm),
-                         [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev, tme, sm); });
+                if (hf2 && rk_step < 2 && mode == 2 && small_step > 0 && small_step == n_small - 1) {
+                    run_task(c, "hfuse[acoustic+solve_vc]", [&] {
+                        return launch_hf_acoustic_solve_vc(S, st, dts, small_step, c->exact, coef_prev);
+                    });
+                    vc_done = true;
+                } else {
+                    run_task(c, acoustic_name(small_step, pending, sm),
+                             [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev, tme, sm); });
+                }
                 if (mode == 2) fb.swap_rup();
                 fb.swap_dv();  // this substep's div is read next from X_dvB
                 if (++done_acoustic == n_acoustic) {
@@ -804,6 +830,16 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             run_task(c, "hfuse[solve_e+finish]", [&] { return launch_hf_solve_e_finish(S, st); });
         } else if (hf && fuse && rk_step == 2) {
             run_task(c, "atm_compute_solve_diagnostics[e]", [&] { return launch_solve_diagnostics(S, st, 0, 2, 2); });
+        } else if (hf2 && vc_done && rk_step < 2) {
+            // (the vertex / cell kernel ran beside the last acoustic launch) the edge kernel
+            // beside the next stage's dyn_tend A, and after stage 0 beside stage 1's vert_imp
+            const DynTendArgs nx = stage_args(rk_step + 1);
+            run_task(c, rk_step == 0 ? "hfuse[solve_e+vert_imp+dyn_A]" : "hfuse[solve_e+dyn_A]", [&] {
+                return launch_hf_solve_e_dyn_A(S, st, nx, rk_step == 0 ? 1 : 0, rk_sub_timestep[1]);
+            });
+            if (rk_step == 0) vi_done = true;
+            a_done = true;
+            vc_done = false;
         } else if (hf && rk_step == 0) {  // the edge kernel beside stage 1's vert_imp
             run_task(c, "atm_compute_solve_diagnostics[vc]", [&] { return launch_solve_diagnostics(S, st, 0, 0, 1); });
             run_task(c, "hfuse[solve_e+vert_imp]",

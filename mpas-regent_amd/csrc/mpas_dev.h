@@ -165,6 +165,7 @@ struct DynTendArgs {
     int hfuse = 0;     // 1: rk_step 0's D and E in one grid (atm_srk3, option "hfuse"; undecomposed)
     int cp = 0;        // 1: the edge kernel also makes setup's ru_save = ru, u_2 = u (atm_srk3 stage 0,
                        // option "fusecopy"; undecomposed)
+    int skipA = 0;     // 1: kernel A already ran (launch_hf_solve_e_dyn_A; atm_srk3 hfuse, undecomposed)
 };
 
 enum EntityKind { KC = 0, KE = 1, KV = 2 };  // DevState::lo index
@@ -190,6 +191,14 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st);
 hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts);
 // setup + moist + vert_imp(dts) in one launch (option "fusesetup", reference semantics)
 hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts, bool edges = true);
+// option hfuse (atm_srk3, reference semantics, undecomposed): a stage's last acoustic launch
+// (mode 2) beside its solve_diagnostics vertex / cell kernel; the stage's solve_diagnostics
+// edge kernel beside the next stage's dyn_tend A (and stage 1's vert_imp after stage 0)
+hipError_t launch_hf_acoustic_solve_vc(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
+                                       double coef_prev);
+hipError_t launch_hf_solve_e_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& next, int vi, double dts_vi);
+// ... and stage 0's setup + moist + vert_imp launch (fusesetup) beside stage 0's dyn_tend A
+hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges);
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
 // mode (reference semantics, no halo; atm_srk3 with option "fusedamp"): 0 plain, 1 also

@@ -15,17 +15,27 @@ roofline.achieved divides by the measured launch time.
 
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
-          part=None, pair=None, copy=False):
+          part=None, pair=None, copy=False, noA=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
-    if task == "hfuse":  # option hfuse: two independent kernels of the step in one launch
-        a, b = {"damp+solve_vc": (("atm_divergence_damping_3d", {}), ("atm_compute_solve_diagnostics", {"part": "vc"})),
-                "solve_e+finish": (("atm_compute_solve_diagnostics", {"part": "e", "reconstruct_v": True}),
-                                   ("atm_rk_dynamics_substep_finish", {})),
-                "solve_e+vert_imp": (("atm_compute_solve_diagnostics", {"part": "e"}),
-                                     ("atm_compute_vert_imp_coefs", {}))}[pair]
-        ra, wa = _sets(a[0], **a[1])
-        rb, wb = _sets(b[0], **b[1])
-        return ra + rb, wa + wb
+    if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
+        e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
+            ("atm_compute_dyn_tend_work", {"rk_step": 1, "part": "A"})
+        parts = {"damp+solve_vc": (("atm_divergence_damping_3d", {}), ("atm_compute_solve_diagnostics", {"part": "vc"})),
+                 "solve_e+finish": (("atm_compute_solve_diagnostics", {"part": "e", "reconstruct_v": True}),
+                                    ("atm_rk_dynamics_substep_finish", {})),
+                 "solve_e+vert_imp": (e, vi),
+                 "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}),
+                                       ("atm_compute_solve_diagnostics", {"part": "vc"})),
+                 "solve_e+dyn_A": (e, dA),
+                 "solve_e+vert_imp+dyn_A": (e, vi, dA),
+                 "setup+dyn_A": (("atm_rk_integration_setup", {"fused": True, "copy": True}),
+                                 ("atm_compute_dyn_tend_work", {"rk_step": 0, "part": "A"}))}[pair]
+        rs, ws = [], []
+        for t, kw in parts:
+            r, w = _sets(t, **kw)
+            rs += r
+            ws += w
+        return rs, ws
     if task == "atm_rk_integration_setup" and fused:  # option fusesetup: + moist + vert_imp, one launch
         parts = [_sets(t) for t in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
                                     "atm_compute_vert_imp_coefs")]
@@ -45,6 +55,18 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         return (["cqw", "exner", "exner_base", "qtot", "rho_base", "rtheta_base", "rtheta_p", "theta_m", "zz",
                  "gamma_tri"],
                 ["a_tri", "b_tri", "c_tri", "alpha_tri", "gamma_tri", "coftz", "cofwr", "cofwt", "cofwz"])
+    if task == "atm_compute_dyn_tend_work" and part == "A":  # its first cell kernel alone
+        reads = ["ru", "rw", "rho_zz", "uReconstructZonal", "uReconstructMeridional", "nEdgesOnCell", "edgesOnCell",
+                 "edgesOnCell_sign", "dvEdge", "invAreaCell", "lat"]
+        if rk_step == 0:  # + the Smagorinsky kdiff, tend_rho and dpdz
+            return (reads + ["u", "v", "defc_a", "defc_b", "qtot", "rho_base", "rho_p_save", "tend_rho_physics"],
+                    ["h_divergence", "kdiff", "tend_rho", "dpdz"])
+        return reads, ["h_divergence"]
+    if task == "atm_compute_dyn_tend_work" and noA:  # the rest after A ran in a combined launch
+        r, w = _sets(task, rk_step=rk_step, physics=physics, copy=copy)
+        ra, wa = _sets(task, rk_step=rk_step, part="A")
+        return ([x for x in r if x not in ("uReconstructZonal", "uReconstructMeridional")] + wa,
+                [x for x in w if x not in wa])
     if task == "atm_compute_dyn_tend_work":
         mesh = ["nEdgesOnCell", "edgesOnCell", "edgesOnCell_sign", "invAreaCell", "lat", "cellsOnEdge",
                 "verticesOnEdge", "dvEdge", "invDcEdge", "nEdgesOnEdge", "edgesOnEdge", "weightsOnEdge",

@@ -464,7 +464,9 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
     kernel (option fusecopy; stage 0 runs rk_step > 0 kernels under schedule 0, which read
     ru_save), theta_m(cell2) + theta_m(cell1) per edge taken
     from dyn_tend's edge kernel (option tmedge) and independent neighbouring kernels
-    sharing a launch (option hfuse) is value-identical to the separate launches and
+    sharing a launch (option hfuse; with fusedamp and without tmedge also a stage's last
+    acoustic launch beside its solve_diagnostics vertex / cell kernel and its edge kernel
+    beside the next stage's dyn_tend A) is value-identical to the separate launches and
     to the oracle, in exact mode and on the fast path; raw 1-based ids leave edge 0 listed
     by no cell (an orphan, written by the launch's extra blocks)"""
     st = base_state(x1_2562, L, variant)
@@ -488,6 +490,11 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
         c, _ = _two_steps_gpu(st, hf, 0, 1, hfuse=1 - hf)
         bad = compare_states(c, b, rtol=0.0)
         assert not bad, f"hfuse={1 - hf}, fusedamp={hf} vs separate launches: {bad[:6]}"
+    for ex in (0, 1):  # hfuse with fusedamp and without tmedge: the acoustic + solve_vc and
+        # solve_e + next stage's dyn_tend A (+ vert_imp) combined launches
+        c, _ = _two_steps_gpu(st, 1, ex, 1, tmedge=0, hfuse=1)
+        bad = compare_states(c, b if ex == 0 else ref, rtol=0.0)
+        assert not bad, f"hfuse=1, tmedge=0, exact={ex}: {bad[:6]}"
     for fc in (0, 1):  # setup's edge copies in the setup launch / in dyn_tend, exact and fast
         for ex in (0, 1):
             c, _ = _two_steps_gpu(st, 1, ex, 1, fusecopy=fc)
