@@ -93,7 +93,8 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * "transport" = 1 (needs "physics" >= 1) makes mpas_atm_srk3 copy scalars
  * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
  * recover, before atm_rk_dynamics_substep_finish.  Default 0.  "trorder" = 1 (speed only)
- * orders the transport's column slots pair-major instead of entity-major.  "trtile" = 1
+ * orders the transport's column slots pair-major instead of entity-major; R >= 2 pair-major
+ * within runs of R consecutive entities, one run per XCD.  "trtile" = 1
  * (speed only, default 0) runs the transport as two tiled kernels with the scalars of
  * compact cell tiles in LDS and no edge scratch, when every cell has at most 6 edges with
  * at most 9 advCells each (bit-identical; measured slower); "trtcells" and

@@ -532,7 +532,7 @@ __global__ __launch_bounds__(256) void k_fill(void* dst, int fid, int kind, long
         const long g = gid ? (long)gid[e] : e;  // the global entity id: same value on every rank
         double v = mpas_synth_value(seed, (uint32_t)fid, (uint64_t)g, (uint32_t)k, (uint32_t)i, dist, lo, hi);
         if (kind == K_ZV) d[k] = v;
-        else if (kind == K_C3V) d[((size_t)e * W + i) * LP + lpos(LP, k)] = v;
+        else if (kind == K_C3V) d[vidx(W, LP, e, i, k)] = v;
         else d[(size_t)e * LP + lpos(LP, k)] = v;
     }
 }
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(256) void k_view_copy(T* dev, char* view, int n, in
     const size_t per = (size_t)W * (L + 1);
     if (t >= (size_t)n * per) return;
     const int e = (int)(t / per), r = (int)(t % per), i = r / (L + 1), k = r % (L + 1);
-    T* d = dev + ((size_t)e * W + i) * LP + lpos(LP, k);
+    T* d = dev + vidx(W, LP, e, i, k);
     T* v = (T*)(view + (int64_t)e * se + (int64_t)k * sl + (int64_t)i * sc);
     if (to_dev) *d = *v;
     else *v = *d;

@@ -14,9 +14,10 @@
 //                cell, and R+ / R- (X_su, X_Rp, X_Rm, C3V x 8)
 //   k_tr_update  per cell: every A scaled by min(R- of its source, R+ of its receiver),
 //                s_new = su - dt div(scaled A) / rho_new  (scalars)
-// Column slot = (entity, scalar pair): the 8 scalars of an entity are 8 consecutive
-// columns; a wavefront computes two of them (one 16-B lane load fetches a gathered column
-// pair: the gathers cost per load instruction), and the 4 wavefronts of an
+// Column slot = (entity, scalar pair): the 8 scalars of an entity are stored as 4 pair
+// columns (scalars 2q, 2q+1 of a level in one 16-B element: vidx in mpas_dev.h); a
+// wavefront computes one pair (one 16-B lane load per gathered entity, from a wave-uniform
+// address: the gathers cost per load instruction), and the 4 wavefronts of an
 // entity read the same connectivity, mass fluxes and densities (one HBM fetch, then L2
 // hits).  One wavefront per column pair at 57 levels (LP = 64); the vertical neighbours
 // are lane shuffles.
@@ -40,8 +41,29 @@ __device__ __forceinline__ double tr_flux3(double q_im2, double q_im1, double q_
 // slots: they share its connectivity and mass-flux loads), 1 pair-major (all entities for
 // pair 0, then pair 1, ...: a quarter of the per-entity footprint in L2, so the entities
 // in flight span 4x the mesh and share more neighbour columns)
+// trorder R >= 2: pair-major within runs of R consecutive entities (the run's entities for
+// pair 0, then pair 1, ...), each run on one XCD: the waves in flight on an XCD share a
+// quarter of the per-entity footprint and the run's mesh data stays in its L2 across the
+// four pairs
 template <int LP>
 __device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, int& p) {
+    constexpr int COLS = 256 / LP;
+    if (S.tro >= 2) {
+        const int R = S.tro, per = (NSC / 2) * R;  // slots per run
+        const int slot = col_of<LP>(xcd_block((per + COLS - 1) / COLS));
+        const int n = (kind == KC ? S.nCO : S.nEO) - S.lo[kind];
+        const int run = slot / per, m = min(R, n - run * R);
+        if (m <= 0) {
+            ent = 0x7fffffff;  // past the last run (caller returns)
+            p = 0;
+            return;
+        }
+        const int within = slot - run * per, q = within / m;
+        ent = run * R + (within - q * m) + S.lo[kind];
+        p = q * 2;
+        if (q >= NSC / 2) ent = 0x7fffffff;
+        return;
+    }
     const int slot = col_of<LP>(xcd_block(S.xcd));
     if (S.tro) {
         const int n = (kind == KC ? S.nCO : S.nEO) - S.lo[kind];
@@ -55,36 +77,63 @@ __device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, i
     }
 }
 
-// level k of columns ia and ib of field f (64-bit column ids: the edge scratch exceeds
-// 4 GiB on the largest meshes).  At LP = 64 one 16-B load per lane (lanes 0-31 the level
-// pair k & 31 of column ia, lanes 32-63 that of column ib, the lpos layout) and a
-// permlane32 swap (gather2 of mpas_dev.h); two loads below LP 64.
+// The x8 fields in their pair layout (vidx in mpas_dev.h): scalars p and p + 1 (p even)
+// of entity ent at level k are one 16-B element.  A wavefront (lane = level) loads or
+// stores both with one 16-B access per lane; the column's address is wave-uniform (ent
+// and p are: SGPRs) and the lane's level is the offset -- no permlane exchange, no per-lane
+// column select (64-bit: the edge scratch exceeds 4 GiB on the largest meshes).
+// Only levels 0..L-1 are read or written (the transport never uses level L or the
+// padding): the lanes k >= L neither load (their values are 0) nor store, so the scratch
+// (A, R+, R-, su; never uploaded) packs its pair columns at pitch L instead of LP
+// (undecomposed contexts) -- at 56 levels 7/8 of the bytes of every column access.
+struct Px {
+    int pitch, L;  // pair-column pitch (elements) and live lanes (levels 0..L-1)
+};
 template <int LP>
-__device__ __forceinline__ void ld2(const double* f, size_t ia, size_t ib, int k, double& a, double& b) {
-    if constexpr (LP == 64) {
-        const double2 t = *(const double2*)((const char*)f + (k >= 32 ? ib : ia) * 512 + (size_t)(k & 31) * 16);
-        double x = t.x, y = t.y;
-        swap_halves(x, y);
-        a = x;
-        b = y;
-    } else {
-        a = f[ia * LP + lpos(LP, k)];
-        b = f[ib * LP + lpos(LP, k)];
-    }
-}
-// the inverse: store a (column ia) and b (column ib) at every level of the lane; at
-// LP = 64 one 16-B store per lane (every lane of the wavefront must take part)
+__device__ __forceinline__ Px px_pub(int L) { return Px{LP, L}; }          // scalars_old, scalars
 template <int LP>
-__device__ __forceinline__ void st2(double* f, size_t ia, size_t ib, int k, double a, double b) {
-    if constexpr (LP == 64) {
-        swap_halves(a, b);
-        *(double2*)((char*)f + (k >= 32 ? ib : ia) * 512 + (size_t)(k & 31) * 16) = make_double2(a, b);
-    } else {
-        f[ia * LP + lpos(LP, k)] = a;
-        f[ib * LP + lpos(LP, k)] = b;
-    }
+__device__ __forceinline__ Px px_scr(const DevState& S) {  // X_Ah, X_Rp, X_Rm, X_su
+    // (a decomposed mesh keeps pitch LP: the halo moves an x8 entity as its 8 x LP block)
+    return Px{LP == 64 && !S.halo ? S.L : LP, S.L};
 }
-__device__ __forceinline__ size_t col8(int ent, int i) { return (size_t)ent * NSC + i; }
+template <int LP>
+__device__ __forceinline__ double2* pcol(Px x, const double* f, int ent, int p) {
+    return (double2*)f + ((size_t)(uint32_t)ent * (NSC / 2) + (size_t)(p >> 1)) * (size_t)x.pitch;
+}
+// The lane mask costs no branch: the column is a raw buffer of L 16-B elements (the
+// descriptor's range is the column, built in SGPRs), so a lane k >= L is out of range --
+// its load returns 0 and fetches nothing, its store is dropped.  (Bounds-checked build:
+// the same through a branch and MPAS_CHK.)
+template <int LP>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t prsrc(Px x, const double* f, int ent, int p) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)pcol<LP>(x, f, ent, p), 0, x.L * 16, 0x00020000);
+}
+template <int LP>
+__device__ __forceinline__ void ld2(Px x, const double* f, int ent, int p, int k, double& a, double& b) {
+#if MPAS_BOUNDS
+    double2 t = make_double2(0.0, 0.0);
+    if (k < x.L) t = *(const double2*)MPAS_CHK(f, pcol<LP>(x, f, ent, p) + k, 16);
+#else
+    const double2 t = __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(prsrc<LP>(x, f, ent, p), k * 16, 0, 0));
+#endif
+    a = t.x;
+    b = t.y;
+}
+template <int LP>
+__device__ __forceinline__ void st2(Px x, double* f, int ent, int p, int k, double a, double b) {
+#if MPAS_BOUNDS
+    if (k < x.L) *(double2*)MPAS_CHK(f, pcol<LP>(x, f, ent, p) + k, 16) = make_double2(a, b);
+#else
+    using u4 = __attribute__((ext_vector_type(4))) unsigned;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, make_double2(a, b)), prsrc<LP>(x, f, ent, p), k * 16, 0, 0);
+#endif
+}
+// scalar i of entity ent at level k < L (one 8-B element of the pair layout; the tiled
+// kernels)
+template <int LP>
+__device__ __forceinline__ double& sat(Px x, const double* f, int ent, int i, int k) {
+    return *(double*)MPAS_CHK(f, (double*)(pcol<LP>(x, f, ent, i) + k) + (i & 1), 8);
+}
 
 // interface k of a column: upwind (lo) and antidiffusive (A) vertical flux of the lane's
 // level; no flux through interfaces 0 and L
@@ -104,6 +153,7 @@ __global__ __launch_bounds__(256) void k_tr_edge(DevState S) {
     int e, p;
     tr_slot<LP>(S, KE, e, p);
     const int L = S.L, k = (int)(threadIdx.x % LP);
+    const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
     if (e >= S.nEO) return;
     const int* rec = fi(S, X_eB) + (size_t)e * 24;  // cellsOnEdge(2) .. advCellsForEdge(9) @12, nAdv @22
     const int c1 = rec[0], c2 = rec[1], na = rec[22];
@@ -118,15 +168,15 @@ __global__ __launch_bounds__(256) void k_tr_edge(DevState S) {
     const double u = colk(fd(S, F_ruAvg), e);
     double xa[AF], xb[AF], s1a, s1b, s2a, s2b;
 #pragma unroll
-    for (int j = 0; j < AF; j++) ld2<LP>(so, col8(adv[j], p), col8(adv[j], p + 1), k, xa[j], xb[j]);
+    for (int j = 0; j < AF; j++) ld2<LP>(XP, so, adv[j], p, k, xa[j], xb[j]);
     // the upwind flux's two cells are normally advCellsForEdge(0) and (1) (MPAS's list
     // construction): take their columns from the list; gather them only where they are not
     // (wave-uniform branch, the same column either way)
     if (na >= 2 && adv[0] == c1 && adv[1] == c2) {
         s1a = xa[0], s1b = xb[0], s2a = xa[1], s2b = xb[1];
     } else {
-        ld2<LP>(so, col8(c1, p), col8(c1, p + 1), k, s1a, s1b);
-        ld2<LP>(so, col8(c2, p), col8(c2, p + 1), k, s2a, s2b);
+        ld2<LP>(XP, so, c1, p, k, s1a, s1b);
+        ld2<LP>(XP, so, c2, p, k, s2a, s2b);
     }
     const double sgn = copysign(1.0, u);
     double acca = 0.0, accb = 0.0;
@@ -140,13 +190,13 @@ __global__ __launch_bounds__(256) void k_tr_edge(DevState S) {
         const int cj = fi(S, F_advCellsForEdge)[(size_t)e * 15 + j];
         const double wgt = fd(S, F_adv_coefs)[(size_t)e * 15 + j] + sgn * fd(S, F_adv_coefs_3rd)[(size_t)e * 15 + j];
         double ya, yb;
-        ld2<LP>(so, col8(cj, p), col8(cj, p + 1), k, ya, yb);
+        ld2<LP>(XP, so, cj, p, k, ya, yb);
         acca = acca + wgt * ya;
         accb = accb + wgt * yb;
     }
     const double loa = dv * (fmax(u, 0.0) * s1a + fmin(u, 0.0) * s2a);
     const double lob = dv * (fmax(u, 0.0) * s1b + fmin(u, 0.0) * s2b);
-    st2<LP>(fw(S, X_Ah), col8(e, p), col8(e, p + 1), k, PADW(u * acca - loa), PADW(u * accb - lob));
+    st2<LP>(XS, fw(S, X_Ah), e, p, k, PADW(u * acca - loa), PADW(u * accb - lob));
 }
 
 // k_tr_edge with the scalars_old columns staged in LDS (option "tredge", opt-in: measured
@@ -173,6 +223,7 @@ __global__ __launch_bounds__(256) void k_tr_edge_lds(DevState S, TreK T) {
     const int g = b >> 2, p = (b & 3) * 2;
     if (g >= T.ngroups) return;
     const int L = S.L, k = (int)(threadIdx.x % LP), w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / LP));
+    const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
     const int nu = T.ucnt[g];
     const double* so = fd(S, F_scalars_old);
     const int e0 = g * TRE_GE, ne = min(TRE_GE, S.nEO - e0);
@@ -191,7 +242,7 @@ __global__ __launch_bounds__(256) void k_tr_edge_lds(DevState S, TreK T) {
         for (int i = 0; i < NL; i++) {
             const int s = w + i * NW;
             const int cell = uc[s < TRE_U ? s : 0];
-            ld2<LP>(so, col8(cell, p), col8(cell, p + 1), k, a_[i], b_[i]);
+            ld2<LP>(XP, so, cell, p, k, a_[i], b_[i]);
         }
 #pragma unroll
         for (int i = 0; i < NL; i++) {
@@ -230,9 +281,9 @@ __global__ __launch_bounds__(256) void k_tr_edge_lds(DevState S, TreK T) {
 #pragma unroll
             for (int j = 0; j < AF; j++) adv[j] = rec[12 + j];
 #pragma unroll
-            for (int j = 0; j < AF; j++) ld2<LP>(so, col8(adv[j], p), col8(adv[j], p + 1), k, xa[j], xb[j]);
-            ld2<LP>(so, col8(c1, p), col8(c1, p + 1), k, s1a, s1b);
-            ld2<LP>(so, col8(c2, p), col8(c2, p + 1), k, s2a, s2b);
+            for (int j = 0; j < AF; j++) ld2<LP>(XP, so, adv[j], p, k, xa[j], xb[j]);
+            ld2<LP>(XP, so, c1, p, k, s1a, s1b);
+            ld2<LP>(XP, so, c2, p, k, s2a, s2b);
         }
         const double sgn = copysign(1.0, u);
         double acca = 0.0, accb = 0.0;
@@ -246,13 +297,13 @@ __global__ __launch_bounds__(256) void k_tr_edge_lds(DevState S, TreK T) {
             const int cj = fi(S, F_advCellsForEdge)[(size_t)e * 15 + j];
             const double wgt = fd(S, F_adv_coefs)[(size_t)e * 15 + j] + sgn * fd(S, F_adv_coefs_3rd)[(size_t)e * 15 + j];
             double ya, yb;
-            ld2<LP>(so, col8(cj, p), col8(cj, p + 1), k, ya, yb);
+            ld2<LP>(XP, so, cj, p, k, ya, yb);
             acca = acca + wgt * ya;
             accb = accb + wgt * yb;
         }
         const double loa = dv * (fmax(u, 0.0) * s1a + fmin(u, 0.0) * s2a);
         const double lob = dv * (fmax(u, 0.0) * s1b + fmin(u, 0.0) * s2b);
-        st2<LP>(fw(S, X_Ah), col8(e, p), col8(e, p + 1), k, PADW(u * acca - loa), PADW(u * accb - lob));
+        st2<LP>(XS, fw(S, X_Ah), e, p, k, PADW(u * acca - loa), PADW(u * accb - lob));
     }
 }
 
@@ -319,6 +370,7 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     int c, p;
     tr_slot<LP>(S, KC, c, p);
     const int L = S.L, k = (int)(threadIdx.x % LP);
+    const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
     if (c >= S.nCO) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     TrSlots t;
@@ -328,23 +380,23 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     const double *so = fd(S, F_scalars_old), *ru = fd(S, F_ruAvg);
     const double* Ah = fd(S, X_Ah);
     double sa, sb;
-    ld2<LP>(so, col8(c, p), col8(c, p + 1), k, sa, sb);
+    ld2<LP>(XP, so, c, p, k, sa, sb);
     const double w = colk(fd(S, F_wwAvg), c), r_o = colk(fd(S, F_rho_zz_old_split), c), r_n = colk(fd(S, F_rho_zz), c);
     double u_[NF], x1a[NF], x2a[NF], x1b[NF], x2b[NF], Aa[NF], Ab[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         u_[i] = colk(ru, t.e[i]);
-        ld2<LP>(Ah, col8(t.e[i], p), col8(t.e[i], p + 1), k, Aa[i], Ab[i]);
+        ld2<LP>(XS, Ah, t.e[i], p, k, Aa[i], Ab[i]);
         if constexpr (SELF) {
             double xa, xb;
-            ld2<LP>(so, col8(t.oth[i], p), col8(t.oth[i], p + 1), k, xa, xb);
+            ld2<LP>(XP, so, t.oth[i], p, k, xa, xb);
             x1a[i] = t.s1[i] ? sa : xa;
             x2a[i] = t.s1[i] ? xa : sa;
             x1b[i] = t.s1[i] ? sb : xb;
             x2b[i] = t.s1[i] ? xb : sb;
         } else {
-            ld2<LP>(so, col8(t.c1[i], p), col8(t.c1[i], p + 1), k, x1a[i], x1b[i]);
-            ld2<LP>(so, col8(t.c2[i], p), col8(t.c2[i], p + 1), k, x2a[i], x2b[i]);
+            ld2<LP>(XP, so, t.c1[i], p, k, x1a[i], x1b[i]);
+            ld2<LP>(XP, so, t.c2[i], p, k, x2a[i], x2b[i]);
         }
     }
     TrAcc ra, rb;
@@ -361,9 +413,9 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
         const int s1f = fi(S, X_ce_s1)[r];
         const double dv = fd(S, X_ce_dv)[r], u = colk(ru, e);
         double y1a, y1b, y2a, y2b, Ba, Bb;
-        ld2<LP>(so, col8(c1, p), col8(c1, p + 1), k, y1a, y1b);
-        ld2<LP>(so, col8(c2, p), col8(c2, p + 1), k, y2a, y2b);
-        ld2<LP>(Ah, col8(e, p), col8(e, p + 1), k, Ba, Bb);
+        ld2<LP>(XP, so, c1, p, k, y1a, y1b);
+        ld2<LP>(XP, so, c2, p, k, y2a, y2b);
+        ld2<LP>(XS, Ah, e, p, k, Ba, Bb);
         tr_bound_slot(true, s1f, dv, u, y1a, y2a, Ba, ra);
         tr_bound_slot(true, s1f, dv, u, y1b, y2b, Bb, rb);
     }
@@ -371,9 +423,9 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     tr_bound_fin<LP>(ra, sa, w, r_o, r_n, invA, rdzw, fzm, fzp, dt, k, L, Rpa, Rma, sua);
     tr_bound_fin<LP>(rb, sb, w, r_o, r_n, invA, rdzw, fzm, fzp, dt, k, L, Rpb, Rmb, sub);
     // level L and the padding levels of the scratch are never read
-    st2<LP>(fw(S, X_Rp), col8(c, p), col8(c, p + 1), k, Rpa, Rpb);
-    st2<LP>(fw(S, X_Rm), col8(c, p), col8(c, p + 1), k, Rma, Rmb);
-    st2<LP>(fw(S, X_su), col8(c, p), col8(c, p + 1), k, sua, sub);
+    st2<LP>(XS, fw(S, X_Rp), c, p, k, Rpa, Rpb);
+    st2<LP>(XS, fw(S, X_Rm), c, p, k, Rma, Rmb);
+    st2<LP>(XS, fw(S, X_su), c, p, k, sua, sub);
 }
 
 // the limited update of one scalar
@@ -393,10 +445,15 @@ __device__ __forceinline__ double tr_limited(double A, double m1, double p2, dou
 }
 
 template <int LP, bool SELF>
-__global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
+// (MPAS_TRU_MINW: min waves per SIMD, a timing-build knob; 1 = the compiler's choice)
+#ifndef MPAS_TRU_MINW
+#define MPAS_TRU_MINW 1
+#endif
+__global__ __launch_bounds__(256, MPAS_TRU_MINW) void k_tr_update(DevState S, double dt) {
     int c, p;
     tr_slot<LP>(S, KC, c, p);
     const int L = S.L, k = (int)(threadIdx.x % LP);
+    const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
     if (c >= S.nCO) return;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     TrSlots t;
@@ -404,29 +461,28 @@ __global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
     const double invA = fd(S, F_invAreaCell)[c];
     const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double *Ah = fd(S, X_Ah), *Rp = fd(S, X_Rp), *Rm = fd(S, X_Rm);
-    const size_t ca = col8(c, p), cb = col8(c, p + 1);
     double sa, sb, sua, sub, rpa, rpb, rma, rmb;
-    ld2<LP>(fd(S, F_scalars_old), ca, cb, k, sa, sb);
-    ld2<LP>(fd(S, X_su), ca, cb, k, sua, sub);
-    ld2<LP>(Rp, ca, cb, k, rpa, rpb);
-    ld2<LP>(Rm, ca, cb, k, rma, rmb);
+    ld2<LP>(XP, fd(S, F_scalars_old), c, p, k, sa, sb);
+    ld2<LP>(XS, fd(S, X_su), c, p, k, sua, sub);
+    ld2<LP>(XS, Rp, c, p, k, rpa, rpb);
+    ld2<LP>(XS, Rm, c, p, k, rma, rmb);
     const double w = colk(fd(S, F_wwAvg), c), r_n = colk(fd(S, F_rho_zz), c);
     double Aa[NF], Ab[NF], p1a[NF], p1b[NF], m1a[NF], m1b[NF], p2a[NF], p2b[NF], m2a[NF], m2b[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ld2<LP>(Ah, col8(t.e[i], p), col8(t.e[i], p + 1), k, Aa[i], Ab[i]);
+        ld2<LP>(XS, Ah, t.e[i], p, k, Aa[i], Ab[i]);
         if constexpr (SELF) {  // the cell is one of the two: gather only the other
             double qa, qb, na, nb;
-            ld2<LP>(Rp, col8(t.oth[i], p), col8(t.oth[i], p + 1), k, qa, qb);
-            ld2<LP>(Rm, col8(t.oth[i], p), col8(t.oth[i], p + 1), k, na, nb);
+            ld2<LP>(XS, Rp, t.oth[i], p, k, qa, qb);
+            ld2<LP>(XS, Rm, t.oth[i], p, k, na, nb);
             const bool f = t.s1[i];
             p1a[i] = f ? rpa : qa, p1b[i] = f ? rpb : qb, m1a[i] = f ? rma : na, m1b[i] = f ? rmb : nb;
             p2a[i] = f ? qa : rpa, p2b[i] = f ? qb : rpb, m2a[i] = f ? na : rma, m2b[i] = f ? nb : rmb;
         } else {
-            ld2<LP>(Rp, col8(t.c1[i], p), col8(t.c1[i], p + 1), k, p1a[i], p1b[i]);
-            ld2<LP>(Rm, col8(t.c1[i], p), col8(t.c1[i], p + 1), k, m1a[i], m1b[i]);
-            ld2<LP>(Rp, col8(t.c2[i], p), col8(t.c2[i], p + 1), k, p2a[i], p2b[i]);
-            ld2<LP>(Rm, col8(t.c2[i], p), col8(t.c2[i], p + 1), k, m2a[i], m2b[i]);
+            ld2<LP>(XS, Rp, t.c1[i], p, k, p1a[i], p1b[i]);
+            ld2<LP>(XS, Rm, t.c1[i], p, k, m1a[i], m1b[i]);
+            ld2<LP>(XS, Rp, t.c2[i], p, k, p2a[i], p2b[i]);
+            ld2<LP>(XS, Rm, t.c2[i], p, k, m2a[i], m2b[i]);
         }
     }
     double hca = 0.0, hcb = 0.0;
@@ -441,21 +497,17 @@ __global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
         const int e = fi(S, F_edgesOnCell)[r], c1 = fi(S, X_ce_c1)[r], c2 = fi(S, X_ce_c2)[r];
         const double sg = fi(S, X_ce_s1)[r] ? 1.0 : -1.0;
         double Ba, Bb, q1a, q1b, n1a, n1b, q2a, q2b, n2a, n2b;
-        ld2<LP>(Ah, col8(e, p), col8(e, p + 1), k, Ba, Bb);
-        ld2<LP>(Rp, col8(c1, p), col8(c1, p + 1), k, q1a, q1b);
-        ld2<LP>(Rm, col8(c1, p), col8(c1, p + 1), k, n1a, n1b);
-        ld2<LP>(Rp, col8(c2, p), col8(c2, p + 1), k, q2a, q2b);
-        ld2<LP>(Rm, col8(c2, p), col8(c2, p + 1), k, n2a, n2b);
+        ld2<LP>(XS, Ah, e, p, k, Ba, Bb);
+        ld2<LP>(XS, Rp, c1, p, k, q1a, q1b);
+        ld2<LP>(XS, Rm, c1, p, k, n1a, n1b);
+        ld2<LP>(XS, Rp, c2, p, k, q2a, q2b);
+        ld2<LP>(XS, Rm, c2, p, k, n2a, n2b);
         hca = hca + sg * tr_limited(Ba, n1a, q2a, q1a, n2a);
         hcb = hcb + sg * tr_limited(Bb, n1b, q2b, q1b, n2b);
     }
     const double na = tr_update_fin<LP>(hca, sa, w, sua, rpa, rma, r_n, invA, rdzw, fzm, fzp, dt, k, L);
     const double nb = tr_update_fin<LP>(hcb, sb, w, sub, rpb, rmb, r_n, invA, rdzw, fzm, fzp, dt, k, L);
-    if (k < L) {  // level L of scalars keeps its value (the oracle writes levels 0..L-1)
-        double* sn = fw(S, F_scalars);
-        sn[ca * LP + lpos(LP, k)] = na;
-        sn[cb * LP + lpos(LP, k)] = nb;
-    }
+    if (k < L) st2<LP>(XP, fw(S, F_scalars), c, p, k, na, nb);  // level L keeps its value (the oracle writes 0..L-1)
 }
 
 // ---------------------------------------------------------------- tiled transport
@@ -485,13 +537,6 @@ __device__ __forceinline__ int trt_slot() {
     int s = (int)(threadIdx.x / LP);
     if constexpr (LP == 64) s = __builtin_amdgcn_readfirstlane(s);
     return s;
-}
-
-// level k of column col (64-bit column index: the x8 fields of the largest meshes exceed
-// 4 GiB) of field f
-template <int LP>
-__device__ __forceinline__ double& at64(const double* f, size_t col, int k) {
-    return *(double*)(f + col * LP + lpos(LP, k));
 }
 
 // A load the compiler may take through the scalar unit: the constant address space
@@ -543,6 +588,7 @@ template <int LP>
 __device__ __forceinline__ void trt_load(const DevState& S, const TrtK& T, int tile, int sc, double* lds) {
     constexpr int NS = TRT_THREADS / LP, U = 4;
     const int k = (int)(threadIdx.x % LP), slot = trt_slot<LP>();
+    const Px XP = px_pub<LP>(S.L);
     const int cb = T.cptr[tile], n = T.cptr[tile + 1] - cb;
     const double* so = fd(S, F_scalars_old);
     for (int i0 = 2 * slot; i0 < n; i0 += 2 * U * NS) {
@@ -551,7 +597,7 @@ __device__ __forceinline__ void trt_load(const DevState& S, const TrtK& T, int t
         for (int u = 0; u < U; u++) {
             const int i = i0 + 2 * u * NS;
             const int ca = T.ccell[cb + (i < n ? i : 0)], cbb = T.ccell[cb + (i + 1 < n ? i + 1 : 0)];
-            ld2<LP>(so, col8(ca, sc), col8(cbb, sc), k, a[u], b[u]);
+            a[u] = sat<LP>(XP, so, ca, sc, k), b[u] = sat<LP>(XP, so, cbb, sc, k);
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -592,6 +638,7 @@ __global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_bounds(DevState 
     trt_load<LP>(S, T, tile, sc, lds);
     constexpr int NS = TRT_THREADS / LP;
     const int L = S.L, k = (int)(threadIdx.x % LP), slot = trt_slot<LP>();
+    const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
     const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double* ru = fd(S, F_ruAvg);
     const int tb = T.tptr[tile], nt = T.tptr[tile + 1] - tb;
@@ -618,24 +665,26 @@ __global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_bounds(DevState 
         }
         double Rp, Rm, su;
         tr_bound_fin<LP>(r, s, w, r_o, r_n, invA, rdzw, fzm, fzp, dt, k, L, Rp, Rm, su);
-        at64<LP>(fw(S, X_Rp), col8(c, sc), k) = Rp;
-        at64<LP>(fw(S, X_Rm), col8(c, sc), k) = Rm;
+        if (k < L) {  // (the scratch holds levels 0..L-1 only: px_scr)
+            sat<LP>(XS, fw(S, X_Rp), c, sc, k) = Rp;
+            sat<LP>(XS, fw(S, X_Rm), c, sc, k) = Rm;
+        }
     }
 }
 
 // R+ and R- of the two cells of edge slot i: p1/m1 at cellsOnEdge(0), p2/m2 at (1)
 template <int LP, bool SELF>
-__device__ __forceinline__ void trt_r(const double* Rp, const double* Rm, const TrtCell<LP>& t, int i, int sc,
+__device__ __forceinline__ void trt_r(Px XS, const double* Rp, const double* Rm, const TrtCell<LP>& t, int i, int sc,
                                       double rp, double rm, int k, double& p1, double& m1, double& p2, double& m2) {
     if constexpr (SELF) {  // the cell is one of the two: gather only the other
-        const size_t co = col8(t.oth(i), sc);
-        const double qo = at64<LP>(Rp, co, k), no = at64<LP>(Rm, co, k);
+        const int co = t.oth(i);
+        const double qo = sat<LP>(XS, Rp, co, sc, k), no = sat<LP>(XS, Rm, co, sc, k);
         const bool f = t.s1(i);
         p1 = f ? rp : qo, m1 = f ? rm : no, p2 = f ? qo : rp, m2 = f ? no : rm;
     } else {
-        const size_t c1 = col8(t.c1(i), sc), c2 = col8(t.c2(i), sc);
-        p1 = at64<LP>(Rp, c1, k), m1 = at64<LP>(Rm, c1, k);
-        p2 = at64<LP>(Rp, c2, k), m2 = at64<LP>(Rm, c2, k);
+        const int c1 = t.c1(i), c2 = t.c2(i);
+        p1 = sat<LP>(XS, Rp, c1, sc, k), m1 = sat<LP>(XS, Rm, c1, sc, k);
+        p2 = sat<LP>(XS, Rp, c2, sc, k), m2 = sat<LP>(XS, Rm, c2, sc, k);
     }
 }
 
@@ -646,6 +695,7 @@ __global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_update(DevState 
     trt_load<LP>(S, T, tile, sc, lds);
     constexpr int NS = TRT_THREADS / LP;
     const int L = S.L, k = (int)(threadIdx.x % LP), slot = trt_slot<LP>();
+    const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
     const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double *Rp = fd(S, X_Rp), *Rm = fd(S, X_Rm), *ru = fd(S, F_ruAvg);
     const int tb = T.tptr[tile], nt = T.tptr[tile + 1] - tb;
@@ -656,21 +706,20 @@ __global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_update(DevState 
         const double invA = fd(S, F_invAreaCell)[c];
         const double w = colk(fd(S, F_wwAvg), c), r_o = colk(fd(S, F_rho_zz_old_split), c),
                      r_n = colk(fd(S, F_rho_zz), c);
-        const size_t cc = col8(c, sc);
-        const double rp = at64<LP>(Rp, cc, k), rm = at64<LP>(Rm, cc, k);
+        const double rp = sat<LP>(XS, Rp, c, sc, k), rm = sat<LP>(XS, Rm, c, sc, k);
         const double s = lds[t.slot(0) * LP + k];
         // su as k_tr_bounds forms it (tr_bound_slot's upwind sum, tr_bound_fin's update),
         // and the limited antidiffusive sum of k_tr_update (masked slots add nothing)
         const int ne = t.ne < NF ? t.ne : NF;
         double hlo = 0.0, hc = 0.0;
         double un = colk(ru, t.e(0)), p1n, m1n, p2n, m2n;
-        trt_r<LP, SELF>(Rp, Rm, t, 0, sc, rp, rm, k, p1n, m1n, p2n, m2n);
+        trt_r<LP, SELF>(XS, Rp, Rm, t, 0, sc, rp, rm, k, p1n, m1n, p2n, m2n);
 #pragma unroll 1
         for (int i = 0; i < ne; i++) {
             const double u = un, p1 = p1n, m1 = m1n, p2 = p2n, m2 = m2n;
             if (i + 1 < ne) {
                 un = colk(ru, t.e(i + 1));
-                trt_r<LP, SELF>(Rp, Rm, t, i + 1, sc, rp, rm, k, p1n, m1n, p2n, m2n);
+                trt_r<LP, SELF>(XS, Rp, Rm, t, i + 1, sc, rp, rm, k, p1n, m1n, p2n, m2n);
             }
             double x1, x2;
             const double A = trt_flux<LP>(lds, t, i, u, k, L, x1, x2);
@@ -684,7 +733,7 @@ __global__ __launch_bounds__(TRT_THREADS, TRT_WAVES) void k_trt_update(DevState 
         const double lot = lvl_up<LP>(lob, k);
         const double su = (s * r_o - dt * (hlo * invA + (lot - lob) * rdzw)) / r_n;
         const double sn = tr_update_fin<LP>(hc, s, w, su, rp, rm, r_n, invA, rdzw, fzm, fzp, dt, k, L);
-        if (k < L) at64<LP>(fw(S, F_scalars), cc, k) = sn;
+        if (k < L) sat<LP>(XP, fw(S, F_scalars), c, sc, k) = sn;
     }
 }
 

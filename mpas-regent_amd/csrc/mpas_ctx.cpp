@@ -1091,7 +1091,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             c->S.physics = (int)value;
             if (!value) c->transport = 0;
         } else if (name && std::strcmp(name, "trorder") == 0) {
-            c->S.tro = value ? 1 : 0;
+            if (value < 0 || value > (1 << 20)) throw Fail{MPAS_EINVAL, "trorder must be 0, 1 or a run length >= 2"};
+            c->S.tro = (int)value;
         } else if (name && std::strcmp(name, "ring1") == 0) {
             c->S.ring1 = value ? 1 : 0;
         } else if (name && std::strcmp(name, "trtile") == 0) {
@@ -1242,7 +1243,7 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
             for (int e = 0; e < n; e++)
                 for (int i = 0; i < W; i++)
                     for (int k = 0; k <= L; k++)
-                        d[((size_t)e * W + i) * LP + lpos(LP, k)] = *(const double*)(h + e * se + k * sl + i * sc);
+                        d[vidx(W, LP, e, i, k)] = *(const double*)(h + e * se + k * sl + i * sc);
         } else if (fi.kind == K_C3B) {
             uint8_t* d = (uint8_t*)buf.data();
             for (int e = 0; e < n; e++)
@@ -1329,7 +1330,7 @@ int mpas_download(mpas_ctx* c, int f, void* host, int64_t se, int64_t sl, int64_
             for (int e = 0; e < n; e++)
                 for (int i = 0; i < W; i++)
                     for (int k = 0; k <= L; k++)
-                        *(double*)(h + e * se + k * sl + i * sc) = d[((size_t)e * W + i) * LP + lpos(LP, k)];
+                        *(double*)(h + e * se + k * sl + i * sc) = d[vidx(W, LP, e, i, k)];
         } else if (fi.kind == K_C3B) {
             const uint8_t* d = (const uint8_t*)buf.data();
             for (int e = 0; e < n; e++)

@@ -26,6 +26,18 @@ namespace mpas {
 __host__ __device__ constexpr int lpos(int LP, int k) { return LP == 64 ? (((k & 31) << 1) | (k >> 5)) : k; }
 __host__ __device__ constexpr int plev(int LP, int p) { return LP == 64 ? ((p >> 1) | ((p & 1) << 5)) : p; }  // inverse
 
+// Element (entity e, component i, level k) of a multi-component 3-D field.  The x8 fields
+// (the transport's scalars and its scratch, width kPairW) store an entity's scalars in
+// pairs: scalars 2q and 2q+1 at level k are ONE 16-B element of pair column e * 4 + q, at
+// position k -- a wavefront loads both scalars of its levels with one 16-B load per lane
+// from a wave-uniform base (no lane exchange, no per-lane column select; k_transport.hip).
+// Other widths (zb_cell / zb3_cell) keep one column per component in the lpos order.
+constexpr int kPairW = 8;
+__host__ __device__ constexpr size_t vidx(int W, int LP, size_t e, int i, int k) {
+    return W == kPairW ? ((e * (kPairW / 2) + (size_t)(i >> 1)) * LP + (size_t)k) * 2 + (size_t)(i & 1)
+                       : (e * W + (size_t)i) * LP + (size_t)lpos(LP, k);
+}
+
 enum FieldKind { K_C3, K_C3V, K_E3, K_V3, K_C2F, K_C2I, K_E2F, K_E2I, K_V2F, K_V2I, K_C3B, K_ZV };
 enum FieldDist { D_U = 0, D_Z = 1, D_B = 2, D_M = 3, D_S = 4 };
 

@@ -53,12 +53,14 @@ def test_transport_task(x1_2562, L, const):
 
 
 @pytest.mark.parametrize("L", [5, 56])
-def test_transport_task_pair_major(x1_2562, L):
-    """option trorder = 1 (pair-major slot order: speed only)"""
+@pytest.mark.parametrize("trorder", [1, 7, 256])
+def test_transport_task_pair_major(x1_2562, L, trorder):
+    """option trorder = 1 (pair-major slot order) and R >= 2 (pair-major within runs of R
+    entities, the last run partial at R = 7 and 256): speed only"""
     st, _ = transport_state(x1_2562, L, DT)
     ref = st.copy()
     O.Oracle(ref).mpas_advance_scalars_mono(DT)
-    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT), trorder=1)
+    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT), trorder=trorder)
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
 
