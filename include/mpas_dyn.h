@@ -92,9 +92,11 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * Default 0: the reference's semantics.
  * "transport" = 1 (needs "physics" >= 1) makes mpas_atm_srk3 copy scalars
  * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
- * recover, before atm_rk_dynamics_substep_finish.  Default 0.  "trorder" = 1 (speed only)
- * orders the transport's column slots pair-major instead of entity-major; R >= 2 pair-major
- * within runs of R consecutive entities, one run per XCD.  "trtile" = 1
+ * recover, before atm_rk_dynamics_substep_finish.  Default 0.  "trorder" (speed only)
+ * orders the transport's column slots: 0 entity-major, 1 pair-major, R >= 2 pair-major
+ * within runs of R consecutive entities, one run per XCD (default 64).  "trsu" = 1 (speed only; measured
+ * slower, default 0): the transport's update forms the upwind update su again instead of
+ * storing and reading it.  "trtile" = 1
  * (speed only, default 0) runs the transport as two tiled kernels with the scalars of
  * compact cell tiles in LDS and no edge scratch, when every cell has at most 6 edges with
  * at most 9 advCells each (bit-identical; measured slower); "trtcells" and

@@ -365,7 +365,8 @@ __device__ __forceinline__ void tr_bound_fin(TrAcc& r, double s, double w, doubl
     Rm = pout_t > 0.0 ? fmin(1.0, qout / pout_t) : 0.0;
 }
 
-template <int LP, bool SELF>
+// SU (option "trsu"): su is not stored; k_tr_update forms it again from the same values
+template <int LP, bool SELF, bool SU>
 __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     int c, p;
     tr_slot<LP>(S, KC, c, p);
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     // level L and the padding levels of the scratch are never read
     st2<LP>(XS, fw(S, X_Rp), c, p, k, Rpa, Rpb);
     st2<LP>(XS, fw(S, X_Rm), c, p, k, Rma, Rmb);
-    st2<LP>(XS, fw(S, X_su), c, p, k, sua, sub);
+    if constexpr (!SU) st2<LP>(XS, fw(S, X_su), c, p, k, sua, sub);
 }
 
 // the limited update of one scalar
@@ -444,11 +445,14 @@ __device__ __forceinline__ double tr_limited(double A, double m1, double p2, dou
     return (A >= 0.0 ? fmin(m1, p2) : fmin(p1, m2)) * A;
 }
 
-template <int LP, bool SELF>
 // (MPAS_TRU_MINW: min waves per SIMD, a timing-build knob; 1 = the compiler's choice)
 #ifndef MPAS_TRU_MINW
 #define MPAS_TRU_MINW 1
 #endif
+// SU (option "trsu"): su formed here as k_tr_bounds forms it -- the upwind sum over the
+// cell's edges (tr_bound_slot's order) and tr_bound_fin's expression -- instead of read
+// from X_su: the same values, one scratch array fewer (written once, read once)
+template <int LP, bool SELF, bool SU>
 __global__ __launch_bounds__(256, MPAS_TRU_MINW) void k_tr_update(DevState S, double dt) {
     int c, p;
     tr_slot<LP>(S, KC, c, p);
@@ -461,12 +465,61 @@ __global__ __launch_bounds__(256, MPAS_TRU_MINW) void k_tr_update(DevState S, do
     const double invA = fd(S, F_invAreaCell)[c];
     const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double *Ah = fd(S, X_Ah), *Rp = fd(S, X_Rp), *Rm = fd(S, X_Rm);
-    double sa, sb, sua, sub, rpa, rpb, rma, rmb;
-    ld2<LP>(XP, fd(S, F_scalars_old), c, p, k, sa, sb);
-    ld2<LP>(XS, fd(S, X_su), c, p, k, sua, sub);
+    const double* so = fd(S, F_scalars_old);
+    double sa, sb, sua = 0.0, sub = 0.0, rpa, rpb, rma, rmb;
+    ld2<LP>(XP, so, c, p, k, sa, sb);
+    if constexpr (!SU) ld2<LP>(XS, fd(S, X_su), c, p, k, sua, sub);
     ld2<LP>(XS, Rp, c, p, k, rpa, rpb);
     ld2<LP>(XS, Rm, c, p, k, rma, rmb);
     const double w = colk(fd(S, F_wwAvg), c), r_n = colk(fd(S, F_rho_zz), c);
+    if constexpr (SU) {  // su (k_tr_bounds: tr_bound_slot's upwind sum, tr_bound_fin)
+        const double* ru = fd(S, F_ruAvg);
+        const double r_o = colk(fd(S, F_rho_zz_old_split), c);
+        double u_[NF], x1a[NF], x2a[NF], x1b[NF], x2b[NF];
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            u_[i] = colk(ru, t.e[i]);
+            if constexpr (SELF) {
+                double xa, xb;
+                ld2<LP>(XP, so, t.oth[i], p, k, xa, xb);
+                x1a[i] = t.s1[i] ? sa : xa;
+                x2a[i] = t.s1[i] ? xa : sa;
+                x1b[i] = t.s1[i] ? sb : xb;
+                x2b[i] = t.s1[i] ? xb : sb;
+            } else {
+                ld2<LP>(XP, so, t.c1[i], p, k, x1a[i], x1b[i]);
+                ld2<LP>(XP, so, t.c2[i], p, k, x2a[i], x2b[i]);
+            }
+        }
+        double hla = 0.0, hlb = 0.0;
+        auto up = [](bool on, int s1f, double dv, double u, double x1, double x2, double& hlo) {
+            const double sg = s1f ? 1.0 : -1.0;
+            const double lo = dv * (fmax(u, 0.0) * x1 + fmin(u, 0.0) * x2);
+            hlo = add_if(on, hlo, sg * lo);
+        };
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            up(i < ne, t.s1[i], t.dv[i], u_[i], x1a[i], x2a[i], hla);
+            up(i < ne, t.s1[i], t.dv[i], u_[i], x1b[i], x2b[i], hlb);
+        }
+        for (int i = NF; i < ne; i++) {
+            const size_t r = (size_t)c * 10 + i;
+            const int e = fi(S, F_edgesOnCell)[r], c1 = fi(S, X_ce_c1)[r], c2 = fi(S, X_ce_c2)[r];
+            const int s1f = fi(S, X_ce_s1)[r];
+            const double dv = fd(S, X_ce_dv)[r], u = colk(ru, e);
+            double y1a, y1b, y2a, y2b;
+            ld2<LP>(XP, so, c1, p, k, y1a, y1b);
+            ld2<LP>(XP, so, c2, p, k, y2a, y2b);
+            up(true, s1f, dv, u, y1a, y2a, hla);
+            up(true, s1f, dv, u, y1b, y2b, hlb);
+        }
+        double loa, Aa_, lob, Ab_;
+        tr_vflux<LP>(sa, w, k, L, fzm, fzp, loa, Aa_);
+        tr_vflux<LP>(sb, w, k, L, fzm, fzp, lob, Ab_);
+        const double lota = lvl_up<LP>(loa, k), lotb = lvl_up<LP>(lob, k);
+        sua = (sa * r_o - dt * (hla * invA + (lota - loa) * rdzw)) / r_n;
+        sub = (sb * r_o - dt * (hlb * invA + (lotb - lob) * rdzw)) / r_n;
+    }
     double Aa[NF], Ab[NF], p1a[NF], p1b[NF], m1a[NF], m1b[NF], p2a[NF], p2b[NF], m2a[NF], m2b[NF];
 #pragma unroll
     for (int i = 0; i < NF; i++) {
@@ -800,17 +853,31 @@ static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
     HALO_WROTE(S, X_Ah);
     auto kb = [&](const DevState& X) {
         const int nb = blocks(X, KC);
-        if (nb && X.selfc) k_tr_bounds<LP, true><<<nb, 256, 0, st>>>(X, dt);
-        else if (nb) k_tr_bounds<LP, false><<<nb, 256, 0, st>>>(X, dt);
+        if (!nb) return;
+        if (X.trsu) {
+            if (X.selfc) k_tr_bounds<LP, true, true><<<nb, 256, 0, st>>>(X, dt);
+            else k_tr_bounds<LP, false, true><<<nb, 256, 0, st>>>(X, dt);
+        } else {
+            if (X.selfc) k_tr_bounds<LP, true, false><<<nb, 256, 0, st>>>(X, dt);
+            else k_tr_bounds<LP, false, false><<<nb, 256, 0, st>>>(X, dt);
+        }
     };
     HALO_RUN(S, st, kb, F_scalars_old, F_ruAvg, X_Ah);
-    HALO_WROTE(S, X_Rp, X_Rm, X_su);
+    if (S.trsu) HALO_WROTE(S, X_Rp, X_Rm);
+    else HALO_WROTE(S, X_Rp, X_Rm, X_su);
     auto ku = [&](const DevState& X) {
         const int nb = blocks(X, KC);
-        if (nb && X.selfc) k_tr_update<LP, true><<<nb, 256, 0, st>>>(X, dt);
-        else if (nb) k_tr_update<LP, false><<<nb, 256, 0, st>>>(X, dt);
+        if (!nb) return;
+        if (X.trsu) {
+            if (X.selfc) k_tr_update<LP, true, true><<<nb, 256, 0, st>>>(X, dt);
+            else k_tr_update<LP, false, true><<<nb, 256, 0, st>>>(X, dt);
+        } else {
+            if (X.selfc) k_tr_update<LP, true, false><<<nb, 256, 0, st>>>(X, dt);
+            else k_tr_update<LP, false, false><<<nb, 256, 0, st>>>(X, dt);
+        }
     };
-    HALO_RUN(S, st, ku, X_Ah, X_Rp, X_Rm);
+    if (S.trsu) HALO_RUN(S, st, ku, F_scalars_old, F_ruAvg, X_Ah, X_Rp, X_Rm);
+    else HALO_RUN(S, st, ku, X_Ah, X_Rp, X_Rm);
     HALO_WROTE(S, F_scalars);
     return hipGetLastError();
 }

@@ -998,6 +998,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.physics = 0;
         c->S.ring1 = 1;
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
+        c->S.tro = 64;  // transport: pair-major within runs of 64 entities (profiles/r03/transport_v5: -1 to -3 %)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         // Field f starts (f % 16) * stagger bytes into its allocation (env MPAS_ALLOC_STAGGER,
         // a multiple of 512: whole columns stay aligned; default 2048): equal-sized arrays
@@ -1090,6 +1091,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
                 throw Fail{MPAS_EINVAL, "physics must be 0 (reference), 1 (MPAS vertical solver) or 2 (MPAS dynamics)"};
             c->S.physics = (int)value;
             if (!value) c->transport = 0;
+        } else if (name && std::strcmp(name, "trsu") == 0) {
+            c->S.trsu = value ? 1 : 0;
         } else if (name && std::strcmp(name, "trorder") == 0) {
             if (value < 0 || value > (1 << 20)) throw Fail{MPAS_EINVAL, "trorder must be 0, 1 or a run length >= 2"};
             c->S.tro = (int)value;
@@ -1142,6 +1145,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "physics") == 0) *value = c->S.physics;
         else if (name && std::strcmp(name, "transport") == 0) *value = c->transport;
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
+        else if (name && std::strcmp(name, "trsu") == 0) *value = c->S.trsu;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
         else if (name && std::strcmp(name, "tredge") == 0) *value = c->tredge;
         else if (name && std::strcmp(name, "tredge_active") == 0) {  // edge groups built for this mesh
