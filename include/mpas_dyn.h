@@ -96,7 +96,8 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * orders the transport's column slots: 0 entity-major, 1 pair-major, R >= 2 pair-major
  * within runs of R consecutive entities, one run per XCD (default 64).  "trsu" = 1 (speed only; measured
  * slower, default 0): the transport's update forms the upwind update su again instead of
- * storing and reading it.  "trtile" = 1
+ * storing and reading it.  "trepw" = 2 (speed only; measured within 2 %, default 1): two
+ * edges per wavefront in the transport's edge kernel.  "trtile" = 1
  * (speed only, default 0) runs the transport as two tiled kernels with the scalars of
  * compact cell tiles in LDS and no edge scratch, when every cell has at most 6 edges with
  * at most 9 advCells each (bit-identical; measured slower); "trtcells" and

@@ -45,13 +45,12 @@ __device__ __forceinline__ double tr_flux3(double q_im2, double q_im1, double q_
 // pair 0, then pair 1, ...), each run on one XCD: the waves in flight on an XCD share a
 // quarter of the per-entity footprint and the run's mesh data stays in its L2 across the
 // four pairs
-template <int LP>
-__device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, int& p) {
-    constexpr int COLS = 256 / LP;
+// entity and pair of column slot `slot` (of (nXO - lo) * 4 slots) in the order option
+// "trorder" selects
+__device__ __forceinline__ void tr_map(const DevState& S, int kind, int slot, int& ent, int& p) {
+    const int n = (kind == KC ? S.nCO : S.nEO) - S.lo[kind];
     if (S.tro >= 2) {
         const int R = S.tro, per = (NSC / 2) * R;  // slots per run
-        const int slot = col_of<LP>(xcd_block((per + COLS - 1) / COLS));
-        const int n = (kind == KC ? S.nCO : S.nEO) - S.lo[kind];
         const int run = slot / per, m = min(R, n - run * R);
         if (m <= 0) {
             ent = 0x7fffffff;  // past the last run (caller returns)
@@ -62,11 +61,7 @@ __device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, i
         ent = run * R + (within - q * m) + S.lo[kind];
         p = q * 2;
         if (q >= NSC / 2) ent = 0x7fffffff;
-        return;
-    }
-    const int slot = col_of<LP>(xcd_block(S.xcd));
-    if (S.tro) {
-        const int n = (kind == KC ? S.nCO : S.nEO) - S.lo[kind];
+    } else if (S.tro) {
         const int q = slot / n;
         ent = slot - q * n + S.lo[kind];
         p = q * 2;
@@ -75,6 +70,18 @@ __device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, i
         ent = (slot >> 2) + S.lo[kind];
         p = (slot & 3) * 2;
     }
+}
+// the first of this wavefront's EPW consecutive column slots (a block holds 256 / LP * EPW
+// slots; with trorder R >= 2 one XCD takes each run's blocks)
+template <int LP, int EPW = 1>
+__device__ __forceinline__ int tr_slot0(const DevState& S) {
+    constexpr int SPB = 256 / LP * EPW;  // slots per block
+    const int on = S.tro >= 2 ? ((NSC / 2) * S.tro + SPB - 1) / SPB : S.xcd;
+    return col_of<LP>(xcd_block(on)) * EPW;
+}
+template <int LP>
+__device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, int& p) {
+    tr_map(S, kind, tr_slot0<LP>(S), ent, p);
 }
 
 // The x8 fields in their pair layout (vidx in mpas_dev.h): scalars p and p + 1 (p even)
@@ -146,6 +153,69 @@ __device__ __forceinline__ void tr_vflux(double s, double w, int k, int L, doubl
     const bool in = k >= 1 && k <= L - 1;
     lo = in ? l : 0.0;
     A = in ? hi - l : 0.0;
+}
+
+// EPW consecutive slots per wavefront (option "trepw" = 2: two edges of one pair, every
+// load of both issued before either is computed -- twice the gathers in flight per wave and
+// the record round trip paid once per two edges; the same expressions)
+template <int LP, int EPW>
+__global__ __launch_bounds__(256) void k_tr_edge_n(DevState S) {
+    const int L = S.L, k = (int)(threadIdx.x % LP);
+    const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
+    const int s0 = tr_slot0<LP, EPW>(S);
+    int e_[EPW], p_[EPW];
+#pragma unroll
+    for (int i = 0; i < EPW; i++) tr_map(S, KE, s0 + i, e_[i], p_[i]);
+    if (e_[0] >= S.nEO) return;
+    const double* so = fd(S, F_scalars_old);
+    int na_[EPW], c1_[EPW], c2_[EPW], adv[EPW][AF];
+    double ac[EPW][AF], ac3[EPW][AF], dv_[EPW], u_[EPW], xa[EPW][AF], xb[EPW][AF];
+#pragma unroll
+    for (int i = 0; i < EPW; i++) {
+        const int e = e_[i] < S.nEO ? e_[i] : e_[0];  // (a slot past the end: loads edge e_[0], stores nothing)
+        const int* rec = fi(S, X_eB) + (size_t)e * 24;
+        c1_[i] = rec[0], c2_[i] = rec[1], na_[i] = rec[22];
+#pragma unroll
+        for (int j = 0; j < AF; j++) adv[i][j] = rec[12 + j];
+        row_ld(fd(S, F_adv_coefs) + (size_t)e * 15, ac[i]);
+        row_ld(fd(S, F_adv_coefs_3rd) + (size_t)e * 15, ac3[i]);
+        dv_[i] = fd(S, F_dvEdge)[e];
+        u_[i] = colk(fd(S, F_ruAvg), e);
+#pragma unroll
+        for (int j = 0; j < AF; j++) ld2<LP>(XP, so, adv[i][j], p_[i], k, xa[i][j], xb[i][j]);
+    }
+#pragma unroll
+    for (int i = 0; i < EPW; i++) {
+        if (e_[i] >= S.nEO) break;
+        const int e = e_[i], p = p_[i], na = na_[i], c1 = c1_[i], c2 = c2_[i];
+        const double u = u_[i], dv = dv_[i];
+        double s1a, s1b, s2a, s2b;
+        if (na >= 2 && adv[i][0] == c1 && adv[i][1] == c2) {
+            s1a = xa[i][0], s1b = xb[i][0], s2a = xa[i][1], s2b = xb[i][1];
+        } else {
+            ld2<LP>(XP, so, c1, p, k, s1a, s1b);
+            ld2<LP>(XP, so, c2, p, k, s2a, s2b);
+        }
+        const double sgn = copysign(1.0, u);
+        double acca = 0.0, accb = 0.0;
+#pragma unroll
+        for (int j = 0; j < AF; j++) {
+            const double wgt = ac[i][j] + sgn * ac3[i][j];
+            acca = add_if(j < na, acca, wgt * xa[i][j]);
+            accb = add_if(j < na, accb, wgt * xb[i][j]);
+        }
+        for (int j = AF; j < na; j++) {
+            const int cj = fi(S, F_advCellsForEdge)[(size_t)e * 15 + j];
+            const double wgt = fd(S, F_adv_coefs)[(size_t)e * 15 + j] + sgn * fd(S, F_adv_coefs_3rd)[(size_t)e * 15 + j];
+            double ya, yb;
+            ld2<LP>(XP, so, cj, p, k, ya, yb);
+            acca = acca + wgt * ya;
+            accb = accb + wgt * yb;
+        }
+        const double loa = dv * (fmax(u, 0.0) * s1a + fmin(u, 0.0) * s2a);
+        const double lob = dv * (fmax(u, 0.0) * s1b + fmin(u, 0.0) * s2b);
+        st2<LP>(XS, fw(S, X_Ah), e, p, k, PADW(u * acca - loa), PADW(u * accb - lob));
+    }
 }
 
 template <int LP>
@@ -845,6 +915,12 @@ static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
                 if (G.ngroups) k_tr_edge_lds<<<G.ngroups * (NSC / 2), 256, 0, st>>>(X, TreK{G.ucell, G.ucnt, G.eslot, G.ngroups});
                 return;
             }
+        }
+        if (X.trepw == 2) {  // (option "trepw" = 2)
+            const long n = (long)(X.nEO - X.lo[KE]) * (NSC / 2);
+            const int nb = n > 0 ? (int)((n + 2 * COLS - 1) / (2 * COLS)) : 0;
+            if (nb) k_tr_edge_n<LP, 2><<<nb, 256, 0, st>>>(X);
+            return;
         }
         const int nb = blocks(X, KE);
         if (nb) k_tr_edge<LP><<<nb, 256, 0, st>>>(X);

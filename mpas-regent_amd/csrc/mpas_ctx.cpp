@@ -998,6 +998,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.physics = 0;
         c->S.ring1 = 1;
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
+        c->S.trepw = 1;
         c->S.tro = 64;  // transport: pair-major within runs of 64 entities (profiles/r03/transport_v5: -1 to -3 %)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         // Field f starts (f % 16) * stagger bytes into its allocation (env MPAS_ALLOC_STAGGER,
@@ -1091,6 +1092,9 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
                 throw Fail{MPAS_EINVAL, "physics must be 0 (reference), 1 (MPAS vertical solver) or 2 (MPAS dynamics)"};
             c->S.physics = (int)value;
             if (!value) c->transport = 0;
+        } else if (name && std::strcmp(name, "trepw") == 0) {
+            if (value != 1 && value != 2) throw Fail{MPAS_EINVAL, "trepw must be 1 or 2"};
+            c->S.trepw = (int)value;
         } else if (name && std::strcmp(name, "trsu") == 0) {
             c->S.trsu = value ? 1 : 0;
         } else if (name && std::strcmp(name, "trorder") == 0) {
@@ -1146,6 +1150,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "transport") == 0) *value = c->transport;
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
         else if (name && std::strcmp(name, "trsu") == 0) *value = c->S.trsu;
+        else if (name && std::strcmp(name, "trepw") == 0) *value = c->S.trepw;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
         else if (name && std::strcmp(name, "tredge") == 0) *value = c->tredge;
         else if (name && std::strcmp(name, "tredge_active") == 0) {  // edge groups built for this mesh

@@ -22,7 +22,7 @@ RTOL_POW = 1e-14
 POW_FIELDS = {"exner", "pressure_p"}
 
 
-def gpu(st, fn, exact=1, physics=1, transport=0, trorder=None, trsu=0):
+def gpu(st, fn, exact=1, physics=1, transport=0, trorder=None, trsu=0, trepw=1):
     got = st.copy()
     with lib.Context(*st.dims()) as ctx:
         ctx.set_option("exact", exact)
@@ -31,6 +31,7 @@ def gpu(st, fn, exact=1, physics=1, transport=0, trorder=None, trsu=0):
         if trorder is not None:  # (None: the library default, 64)
             ctx.set_option("trorder", trorder)
         ctx.set_option("trsu", trsu)
+        ctx.set_option("trepw", trepw)
         ctx.upload(st)
         fn(ctx)
         ctx.sync()
@@ -55,15 +56,16 @@ def test_transport_task(x1_2562, L, const):
 
 
 @pytest.mark.parametrize("L", [5, 56])
-@pytest.mark.parametrize("trorder,trsu", [(0, 0), (1, 0), (7, 0), (256, 0), (0, 1), (64, 1)])
-def test_transport_task_pair_major(x1_2562, L, trorder, trsu):
+@pytest.mark.parametrize("trorder,trsu,trepw", [(0, 0, 1), (1, 0, 1), (7, 0, 1), (256, 0, 1), (0, 1, 1), (64, 1, 1),
+                                                (0, 0, 2), (7, 0, 2), (64, 0, 2)])
+def test_transport_task_pair_major(x1_2562, L, trorder, trsu, trepw):
     """option trorder = 0 (entity-major), 1 (pair-major slot order) and R >= 2 (pair-major
     within runs of R entities, the last run partial at R = 7 and 256); option trsu (su formed again by the
     update instead of stored): speed only, the same values"""
     st, _ = transport_state(x1_2562, L, DT)
     ref = st.copy()
     O.Oracle(ref).mpas_advance_scalars_mono(DT)
-    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT), trorder=trorder, trsu=trsu)
+    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT), trorder=trorder, trsu=trsu, trepw=trepw)
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
 
@@ -127,8 +129,8 @@ def _with(opts, fn):
 
 @pytest.mark.parametrize("nparts", [2, 3])
 @pytest.mark.parametrize("overlap", [1, 0])
-@pytest.mark.parametrize("trtile,trsu", [(0, 0), (1, 0), (0, 1)])
-def test_transport_decomposed_equals_single(x1_2562, nparts, overlap, trtile, trsu):
+@pytest.mark.parametrize("trtile,trsu,trepw", [(0, 0, 1), (1, 0, 1), (0, 1, 1), (0, 0, 2)])
+def test_transport_decomposed_equals_single(x1_2562, nparts, overlap, trtile, trsu, trepw):
     """N subdomains (loopback halo: the x8 fields move as 8 columns per entity) give the
     single-context result bit for bit, with the three kernels and with the tiles (whose
     interior launch takes only the cells reading owned columns)"""
@@ -138,7 +140,7 @@ def test_transport_decomposed_equals_single(x1_2562, nparts, overlap, trtile, tr
         if c.get_option("trtile_ghosts"):  # a decomposed context: the tiles must be in use
             assert c.get_option("trtile_active") == trtile
         T.atm_advance_scalars_mono(c, DT)
-    fn = _with({"physics": 1, "trtile": trtile, "trsu": trsu}, step)
+    fn = _with({"physics": 1, "trtile": trtile, "trsu": trsu, "trepw": trepw}, step)
     ref = run_single(st, fn, 1)
     got, stats = run_decomposed(st, nparts, fn, 1, overlap=overlap, tiled_transport=bool(trtile))
     bad = compare_states(got, ref, rtol=0.0)
