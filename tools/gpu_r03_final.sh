@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-3 evidence (v5): the whole GPU suite and smoke, the headline bench line with its
+# kernel trace, the transport and config-5-mesh lines, small meshes
+set -e
+OUT=${1:-gpurun_out/r03v5}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 1000 python3 -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$OUT/smoke.log" 2>&1
+timeout -k 10 400 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o kt --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --traffic off > "$OUT/trace.log" 2>&1
+timeout -k 10 400 python3 bench.py --transport --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_transport.json" 2>> "$OUT/bench.err"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_tr" -o kt --output-format csv -- python3 bench.py --transport --steps 5 --warmup 1 --no-cpu-baseline --traffic off > "$OUT/trace_tr.log" 2>&1
+for n in 2562 40962; do
+  timeout -k 10 200 python3 bench.py --ncells $n --steps 50 --warmup 5 --no-cpu-baseline --traffic off > "$OUT/bench_x1.${n}.json" 2>> "$OUT/bench.err"
+done
+timeout -k 10 600 python3 bench.py --ncells 655362 --transport --steps 5 --warmup 2 --no-cpu-baseline --traffic off > "$OUT/bench_x1.655362_transport.json" 2>> "$OUT/bench.err"
