@@ -205,7 +205,10 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 
 // ------------------------------------------------------------------------ B (edges)
 template <int LP, bool RK0, bool MD, bool HF>
-__global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
+#ifndef MPAS_B_MINW
+#define MPAS_B_MINW 1
+#endif
+__global__ __launch_bounds__(256, MPAS_B_MINW) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
