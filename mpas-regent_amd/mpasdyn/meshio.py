@@ -5,14 +5,15 @@
   reference reads in ``mesh_loading.rg:123-201``, as a ``mesh.Mesh`` with the file's
   1-based ids and its unit-sphere distances (``init_atm_cases.rg:87-111`` scales by the
   sphere radius later, in the state builder).  ``write_grid`` writes the same subset.
-* ``renumber(m)`` -- cells, edges and vertices each sorted along a Morton curve of
+* ``renumber(m)`` -- cells, edges and vertices each sorted along a space-filling curve
+  (cube-face 2-D Hilbert by default, ``order="morton"`` the 3-D Morton key) of
   their (x, y, z) position, connectivity remapped; the order of every connectivity list
   is kept, so in mpas-mode (0-based) ids every per-entity result is unchanged and only
   its position moves.  Neighbour gathers then stay close in HBM, and a contiguous
   partition has few boundary entities (the overlap's interior share).
   (The reference's "ref" mode uses raw 1-based ids as offsets -- SURVEY Q1 -- which a
   renumbering changes; renumber before building a "ref" state only on purpose.)
-* ``partition_sfc(m, nparts)`` -- balanced contiguous blocks of cells along the Morton
+* ``partition_sfc(m, nparts)`` -- balanced contiguous blocks of cells along the same
   curve, the build's partitioner for meshes without a METIS part file;
   ``read_graph_info_part`` / ``write_graph_info_part`` -- the part-file format of
   ``mesh_loading.rg:11-22`` (one 0-based part id per line).
@@ -74,10 +75,15 @@ def write_grid(path, m, variables=GRID_VARS):
             var[:] = a
 
 
-def _morton_order(x, y, z):
+def _curve_order(x, y, z, order="hilbert"):
+    """permutation sorting the points along a space-filling curve (mesh._order_key: "hilbert",
+    2-D Hilbert curves on the cube faces, or "morton", the 3-D Morton key)"""
     p = np.stack([x, y, z], axis=1).astype(np.float64)
-    p = p / max(float(np.abs(p).max()), 1e-300)  # any sphere radius -> [-1, 1]
-    return np.argsort(M._morton_key(p), kind="stable")
+    if order == "hilbert":  # direction only: the cube-face projection needs no radius
+        p = p / np.maximum(np.linalg.norm(p, axis=1), 1e-300)[:, None]
+    else:
+        p = p / max(float(np.abs(p).max()), 1e-300)  # any sphere radius -> [-1, 1]
+    return np.argsort(M._order_key(p, order), kind="stable")
 
 
 def _remap(ids, new_of_old, n):
@@ -98,16 +104,17 @@ _ROWS = {"nCells": ["latCell", "lonCell", "xCell", "yCell", "zCell", "meshDensit
                        "cellsOnVertex", "kiteAreasOnVertex"]}
 
 
-def renumber(m):
+def renumber(m, order="hilbert"):
     """(renumbered Mesh, {"cell": old_of_new, "edge": ..., "vertex": ...}): each entity
-    kind sorted along the Morton curve of its position; a new entity i is old entity
+    kind sorted along a space-filling curve of its position (order "hilbert": 2-D Hilbert
+    curves on the faces of the circumscribed cube; "morton": the 3-D Morton key); a new entity i is old entity
     old_of_new[i].  Row order of every per-entity array and the values of every
     connectivity array follow; the order inside each connectivity list is kept.  m holds
     the file's 1-based ids (read_grid, mesh.icosahedral); convert with mesh.zero_based
     afterwards for mpas mode."""
-    perm = {"nCells": _morton_order(m.xCell, m.yCell, m.zCell),
-            "nEdges": _morton_order(m.xEdge, m.yEdge, m.zEdge),
-            "nVertices": _morton_order(m.xVertex, m.yVertex, m.zVertex)}
+    perm = {"nCells": _curve_order(m.xCell, m.yCell, m.zCell, order),
+            "nEdges": _curve_order(m.xEdge, m.yEdge, m.zEdge, order),
+            "nVertices": _curve_order(m.xVertex, m.yVertex, m.zVertex, order)}
     new_of_old = {}
     for k, p in perm.items():
         inv = np.empty_like(p)
@@ -167,12 +174,12 @@ def permute_state(st, perms):
     return out
 
 
-def partition_sfc(m, nparts):
+def partition_sfc(m, nparts, order="hilbert"):
     """0-based part id per cell: nparts contiguous, balanced (sizes differ by <= 1)
-    blocks of cells along the Morton curve of their positions."""
+    blocks of cells along a space-filling curve of their positions (renumber's orders)."""
     if nparts < 1 or nparts > m.nCells:
         raise ValueError(f"nparts={nparts} for {m.nCells} cells")
-    order = _morton_order(m.xCell, m.yCell, m.zCell)
+    order = _curve_order(m.xCell, m.yCell, m.zCell, order)
     part = np.empty(m.nCells, dtype=np.int32)
     bounds = np.linspace(0, m.nCells, nparts + 1).round().astype(np.int64)
     for p in range(nparts):
@@ -231,25 +238,26 @@ def write_output_plotting(path, m, st):
 
 
 def main(argv=None):
-    """python -m mpasdyn.meshio GRID.nc [--renumber OUT.nc] [--parts N]: read an MPAS grid,
-    optionally write it Morton-renumbered, optionally write OUT's (or GRID's)
+    """python -m mpasdyn.meshio GRID.nc [--renumber OUT.nc] [--parts N] [--order hilbert|morton]: read an MPAS grid,
+    optionally write it renumbered along the curve, optionally write OUT's (or GRID's)
     graph.info.part.N from the SFC partitioner."""
     import argparse
     ap = argparse.ArgumentParser(prog="python -m mpasdyn.meshio")
     ap.add_argument("grid")
     ap.add_argument("--renumber", metavar="OUT.nc")
     ap.add_argument("--parts", type=int, default=0)
+    ap.add_argument("--order", choices=["hilbert", "morton"], default="hilbert")
     a = ap.parse_args(argv)
     m = read_grid(a.grid)
     base = a.grid
     if a.renumber:
-        m, _ = renumber(m)
+        m, _ = renumber(m, a.order)
         write_grid(a.renumber, m)
         base = a.renumber
     if a.parts:
         stem = base[:-3] if base.endswith(".nc") else base
         stem = stem[:-5] if stem.endswith(".grid") else stem
-        write_graph_info_part(f"{stem}.graph.info.part.{a.parts}", partition_sfc(m, a.parts))
+        write_graph_info_part(f"{stem}.graph.info.part.{a.parts}", partition_sfc(m, a.parts, a.order))
     print(f"{a.grid}: nCells={m.nCells} nEdges={m.nEdges} nVertices={m.nVertices}")
 
 

@@ -160,7 +160,7 @@ def test_rccl_transport_single_rank(x1_2562):
 
 @pytest.mark.parametrize("nparts", [2, 4])
 def test_overlap_morton_mesh(nparts):
-    """a Morton-ordered mesh (icosahedral x1.2562, the benchmark's generator): most owned
+    """a curve-ordered mesh (icosahedral x1.2562, the benchmark's generator): most owned
     entities are interior, so the split launches really run the interior beside the
     exchange; results stay bit-identical to the single context over two RK3 steps"""
     from mpasdyn import mesh as M

@@ -14,8 +14,9 @@ def test_fixture_counts(x1_2562):
 
 
 @pytest.mark.parametrize("level", [2, 4, 5])
-def test_icosahedral_topology(level):
-    m = mesh.icosahedral(level)
+@pytest.mark.parametrize("order", ["hilbert", "morton"])
+def test_icosahedral_topology(level, order):
+    m = mesh.icosahedral(level, order=order)
     n = 10 * 4 ** level + 2
     assert (m.nCells, m.nEdges, m.nVertices) == (n, 3 * (n - 2), 2 * (n - 2))
     assert sorted(set(m.nEdgesOnCell.tolist())) == [5, 6]
@@ -49,6 +50,21 @@ def test_icosahedral_geometry(level):
         f = mesh.load_x1_2562()
         for k in ("dcEdge", "dvEdge", "areaCell"):
             assert 0.8 < np.median(getattr(m, k)) / np.median(getattr(f, k)) < 1.25
+
+
+def test_curve_orders_locality():
+    """both numberings keep neighbouring cells close; the cube-face Hilbert curve (the
+    default) more often than the 3-D Morton key"""
+    far = {}
+    for order in ("hilbert", "morton"):
+        m = mesh.icosahedral(5, order=order)
+        c = m.cellsOnEdge - 1
+        d = np.abs(c[:, 0] - c[:, 1])
+        assert np.median(d) <= 8
+        far[order] = (d > 64).mean()
+    assert far["hilbert"] < far["morton"]
+    with pytest.raises(ValueError):
+        mesh.icosahedral(1, order="peano")
 
 
 def test_zero_based_conversion():
