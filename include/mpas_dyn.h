@@ -281,6 +281,12 @@ int mpas_rccl_unique_id(void* id128);
 /* (after every mpas_halo_plan call of the context: the transports size their buffers) */
 int mpas_halo_rccl(mpas_ctx* ctx, int nranks, int rank, const void* id128);
 int mpas_halo_loopback(mpas_ctx** ctxs, int n);
+/* host-staged TCP transport: nranks processes (they may share one device -- RCCL refuses
+ * two ranks on one GPU), rank r listening on host:base_port + r; each exchange copies the
+ * packed regions to the host, swaps them with the peers over the sockets and copies them
+ * back (synchronous; never captured in a graph).  The multi-process test of the same
+ * plan / pack / unpack code the RCCL transport runs (tests/test_gpu_multiproc.py). */
+int mpas_halo_socket(mpas_ctx* ctx, int nranks, int rank, const char* host, int base_port);
 /* stub transport (measurement only): every exchange packs the send columns of each peer,
  * stands in for the wire with one device copy of the received bytes out of the send
  * buffer, and unpacks -- one rank's whole launch sequence on one GPU, everything but the

@@ -1525,11 +1525,25 @@ int mpas_halo_rccl(mpas_ctx* c, int nranks, int rank, const void* id128) {
     });
 }
 
+int mpas_halo_socket(mpas_ctx* c, int nranks, int rank, const char* host, int base_port) {
+    return guarded(c, [&] {
+        if (nranks < 1 || rank < 0 || rank >= nranks || !host || base_port <= 0 || base_port + nranks > 65535)
+            throw Fail{MPAS_EINVAL, "mpas_halo_socket: bad arguments"};
+        hipcheck(hipSetDevice(c->device), "hipSetDevice");
+        Halo* h = halo_of(c);
+        if (h->rccl || h->loop || h->stub || h->sock) throw Fail{MPAS_EINVAL, "mpas_halo_socket: the context already has a transport"};
+        hipcheck(h->reserve(c->S.LP), "halo buffers");
+        std::string err;
+        if (sock_init(h, nranks, rank, host, base_port, err) != 0) throw Fail{MPAS_EINVAL, err};
+        graph_drop(c);
+    });
+}
+
 int mpas_halo_stub(mpas_ctx* c) {
     return guarded(c, [&] {
         hipcheck(hipSetDevice(c->device), "hipSetDevice");
         Halo* h = halo_of(c);
-        if (h->rccl || h->loop) throw Fail{MPAS_EINVAL, "mpas_halo_stub: the context already has a transport"};
+        if (h->rccl || h->loop || h->sock) throw Fail{MPAS_EINVAL, "mpas_halo_stub: the context already has a transport"};
         hipcheck(h->reserve(c->S.LP), "halo buffers");
         h->stub = true;
         graph_drop(c);

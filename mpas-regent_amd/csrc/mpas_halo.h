@@ -19,7 +19,10 @@
 // ncclGroupStart/End, on the task stream; librccl resolved with dlopen, so the process
 // shares the RCCL that torch.distributed loaded) for one process per GPU, or an
 // in-process loopback for N contexts on one device driven by N host threads (hipMemcpy
-// between the contexts' buffers; the single-GPU test of the decomposition).
+// between the contexts' buffers; the single-GPU test of the decomposition), or a
+// host-staged TCP transport for N processes that may share one device (RCCL refuses two
+// ranks on one GPU): the packed regions go device -> host -> socket -> host -> device,
+// synchronously -- the multi-process test of the same pack / plan / unpack code.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -55,6 +58,7 @@ struct HaloCopyTab {  // the device segment table of one direction of one exchan
     std::shared_ptr<std::vector<HaloSeg>> host;
 };
 struct RcclComm;   // RCCL transport
+struct SockComm;   // host-staged TCP transport (multi-process runs without RCCL)
 
 struct Halo {
     int nranks = 1, rank = 0;
@@ -69,6 +73,7 @@ struct Halo {
     size_t cap = 0;  // doubles per buffer
     LoopGroup* loop = nullptr;
     RcclComm* rccl = nullptr;
+    SockComm* sock = nullptr;
     bool stub = false;  // mpas_halo_stub: pack, a device copy for the wire, unpack
     std::string err;
     int64_t exchanges = 0, fields_moved = 0;
@@ -148,5 +153,7 @@ struct LoopGroup {
 int rccl_unique_id(void* out128, std::string& err);
 int rccl_init(Halo* h, int nranks, int rank, const void* id128, std::string& err);
 void rccl_free(RcclComm* c);
+int sock_init(Halo* h, int nranks, int rank, const char* host, int base_port, std::string& err);
+void sock_free(SockComm* c);
 
 }  // namespace mpas

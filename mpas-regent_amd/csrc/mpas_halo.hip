@@ -1,11 +1,17 @@
 // mpas_halo.hip -- halo exchange (see mpas_halo.h): pack/unpack kernels, staleness
-// bookkeeping, RCCL and loopback transports.
+// bookkeeping, RCCL, loopback and host-staged TCP transports.
 #include "mpas_halo.h"
 
 #include <cstdio>
 #include <cstdlib>
 
 #include <dlfcn.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <arpa/inet.h>
+#include <sys/socket.h>
+#include <sys/time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -66,6 +72,7 @@ Halo::~Halo() {
     for (auto& kv : tabs)
         if (kv.second.dev) (void)hipFree(kv.second.dev);
     if (rccl) rccl_free(rccl);
+    if (sock) sock_free(sock);
     if (comm) {
         (void)hipStreamSynchronize(comm);
         (void)hipStreamDestroy(comm);
@@ -265,6 +272,114 @@ int rccl_init(Halo* h, int nranks, int rank, const void* id128, std::string& err
 }
 void rccl_free(RcclComm* c) { delete c; }
 
+// ------------------------------------------------------------------ TCP (host-staged)
+// Rank r listens on base_port + r; for every pair i < j, j connects to i and sends its rank.
+// Each exchange moves, per peer in increasing rank order, an 8-byte byte count and the
+// packed region: the lower rank of a pair sends first, the higher receives first (a
+// total order of pairwise exchanges: no cycle of blocked senders).  Sockets time out after
+// 120 s, so a plan mismatch or a dead peer fails the call instead of hanging it.
+struct SockComm {
+    int nranks = 0, rank = 0;
+    std::vector<int> fd;  // per peer rank (-1: self)
+    std::vector<double> hsend, hrecv;
+    ~SockComm() {
+        for (int f : fd)
+            if (f >= 0) ::close(f);
+    }
+};
+void sock_free(SockComm* c) { delete c; }
+
+static bool sock_all(int fd, void* p, size_t n, bool snd) {
+    char* b = (char*)p;
+    while (n) {
+        const ssize_t k = snd ? ::send(fd, b, n, MSG_NOSIGNAL) : ::recv(fd, b, n, 0);
+        if (k <= 0) return false;
+        b += k;
+        n -= (size_t)k;
+    }
+    return true;
+}
+static void sock_opts(int fd) {
+    timeval tv{120, 0};
+    (void)setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    (void)setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+    int one = 1;
+    (void)setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+}
+
+int sock_init(Halo* h, int nranks, int rank, const char* host, int base_port, std::string& err) {
+    auto* c = new SockComm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->fd.assign(nranks, -1);
+    auto fail = [&](const std::string& m) {
+        err = m;
+        delete c;
+        return -1;
+    };
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    if (inet_pton(AF_INET, host, &a.sin_addr) != 1) return fail(std::string("socket halo: bad host ") + host);
+    const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (ls < 0) return fail("socket halo: socket()");
+    int one = 1;
+    (void)setsockopt(ls, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in me = a;
+    me.sin_port = htons((uint16_t)(base_port + rank));
+    if (::bind(ls, (sockaddr*)&me, sizeof(me)) != 0 || ::listen(ls, nranks) != 0) {
+        ::close(ls);
+        return fail("socket halo: bind/listen on port " + std::to_string(base_port + rank));
+    }
+    // connect to every lower rank (retrying while it starts), then accept the higher ones
+    for (int p = 0; p < rank; p++) {
+        sockaddr_in to = a;
+        to.sin_port = htons((uint16_t)(base_port + p));
+        int fd = -1;
+        for (int t = 0; t < 1200 && fd < 0; t++) {  // up to 120 s
+            fd = ::socket(AF_INET, SOCK_STREAM, 0);
+            if (fd >= 0 && ::connect(fd, (sockaddr*)&to, sizeof(to)) != 0) {
+                ::close(fd);
+                fd = -1;
+                usleep(100000);
+            }
+        }
+        if (fd < 0) {
+            ::close(ls);
+            return fail("socket halo: cannot reach rank " + std::to_string(p));
+        }
+        sock_opts(fd);
+        int32_t me32 = rank;
+        if (!sock_all(fd, &me32, 4, true)) {
+            ::close(fd);
+            ::close(ls);
+            return fail("socket halo: hello to rank " + std::to_string(p));
+        }
+        c->fd[p] = fd;
+    }
+    timeval tv{120, 0};
+    (void)setsockopt(ls, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+    for (int n = rank + 1; n < nranks; n++) {
+        const int fd = ::accept(ls, nullptr, nullptr);
+        int32_t who = -1;
+        if (fd < 0) {
+            ::close(ls);
+            return fail("socket halo: accept timed out");
+        }
+        sock_opts(fd);
+        if (!sock_all(fd, &who, 4, false) || who <= rank || who >= nranks || c->fd[who] >= 0) {
+            ::close(fd);
+            ::close(ls);
+            return fail("socket halo: bad hello");
+        }
+        c->fd[who] = fd;
+    }
+    ::close(ls);
+    h->sock = c;
+    h->nranks = nranks;
+    h->rank = rank;
+    return 0;
+}
+
 // ------------------------------------------------------------------ loopback barrier
 bool LoopGroup::barrier(double timeout_s) {
     std::unique_lock<std::mutex> lk(mu);
@@ -427,6 +542,46 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
             err = std::string("RCCL halo exchange: ") + (a->GetErrorString ? a->GetErrorString(r ? r : r2) : "error");
             return hipErrorUnknown;
         }
+    } else if (sock) {  // host-staged: the packed buffer down, the regions over TCP, back up
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        (void)hipStreamIsCapturing(st, &cs);
+        if (cs != hipStreamCaptureStatusNone) {
+            err = "socket halo transport inside a graph capture";
+            return hipErrorInvalidValue;
+        }
+        SockComm& c = *sock;
+        const size_t sn = (size_t)stot * S.LP, rn = (size_t)rtot * S.LP;
+        if (c.hsend.size() < sn) c.hsend.resize(sn);
+        if (c.hrecv.size() < rn) c.hrecv.resize(rn);
+        if (sn && (e = hipMemcpyAsync(c.hsend.data(), sendbuf, sn * sizeof(double), hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        std::vector<const Region*> order;
+        for (auto& x : reg) order.push_back(&x);
+        std::sort(order.begin(), order.end(), [](const Region* a, const Region* b) { return a->peer < b->peer; });
+        for (const Region* x : order) {
+            const int fd = c.fd[x->peer];
+            const uint64_t nb = (uint64_t)x->scols * S.LP * sizeof(double);
+            const uint64_t want = (uint64_t)x->rcols * S.LP * sizeof(double);
+            uint64_t got = 0;
+            auto snd = [&] {
+                return sock_all(fd, (void*)&nb, 8, true) && sock_all(fd, c.hsend.data() + x->soff * S.LP, nb, true);
+            };
+            auto rcv = [&] {
+                if (!sock_all(fd, &got, 8, false)) return false;
+                if (got != want) return false;
+                return sock_all(fd, c.hrecv.data() + x->roff * S.LP, want, false);
+            };
+            const bool ok = rank < x->peer ? (snd() && rcv()) : (rcv() && snd());
+            if (!ok) {
+                err = "socket halo exchange with rank " + std::to_string(x->peer) +
+                      (got != want ? " (plan mismatch: " + std::to_string(got) + " bytes for " + std::to_string(want) + ")" : "");
+                return hipErrorUnknown;
+            }
+        }
+        if (rn && (e = hipMemcpyAsync(recvbuf, c.hrecv.data(), rn * sizeof(double), hipMemcpyHostToDevice, st)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;  // (hrecv is reused by the next exchange)
     } else if (stub) {  // the received bytes land from the send buffer (no peer)
         const size_t n = (size_t)std::min(stot, rtot) * S.LP;
         if (n && (e = hipMemcpyAsync(recvbuf, sendbuf, n * sizeof(double), hipMemcpyDeviceToDevice, st)) != hipSuccess)

@@ -30,7 +30,7 @@ EXPORTS = [
     "mpas_atm_compute_mesh_scaling",
     "mpas_timing_enable", "mpas_timing_reset", "mpas_timing_count", "mpas_timing_get",
     "mpas_halo_owned", "mpas_halo_interior", "mpas_halo_plan", "mpas_set_global_ids", "mpas_rccl_unique_id", "mpas_halo_rccl",
-    "mpas_halo_loopback", "mpas_halo_stats", "mpas_jw_hydrostatic", "mpas_halo_stub",
+    "mpas_halo_loopback", "mpas_halo_stats", "mpas_jw_hydrostatic", "mpas_halo_stub", "mpas_halo_socket",
 ]
 KIND_ID = {"cell": 0, "edge": 1, "vertex": 2}
 
@@ -111,6 +111,7 @@ def load():
         "mpas_halo_loopback": (i32, [ctypes.POINTER(vp), i32]),
         "mpas_halo_stats": (i32, [vp, ctypes.POINTER(i64), ctypes.POINTER(i64)]),
         "mpas_halo_stub": (i32, [vp]),
+        "mpas_halo_socket": (i32, [vp, i32, i32, ctypes.c_char_p, i32]),
         "mpas_jw_hydrostatic": (i32, [i32, i32] + [vp] * 11 + [i32]),
     }
     for name, (res, args) in sig.items():
@@ -256,6 +257,11 @@ def rccl_unique_id():
 def halo_rccl(ctx, nranks, rank, uid):
     buf = ctypes.create_string_buffer(bytes(uid), 128)
     ctx._check(ctx.lib.mpas_halo_rccl(ctx.h, nranks, rank, buf), "mpas_halo_rccl")
+
+
+def halo_socket(ctx, nranks, rank, host="127.0.0.1", base_port=29600):
+    """the host-staged TCP transport (N processes, possibly on one GPU; mpas_dyn.h)"""
+    ctx._check(ctx.lib.mpas_halo_socket(ctx.h, nranks, rank, host.encode(), base_port), "mpas_halo_socket")
 
 
 def halo_stub(ctx):
