@@ -94,7 +94,8 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * to scalars_old first and run mpas_atm_advance_scalars_mono(dt) after the last stage's
  * recover, before atm_rk_dynamics_substep_finish.  Default 0.  "trorder" (speed only)
  * orders the transport's column slots: 0 entity-major, 1 pair-major, R >= 2 pair-major
- * within runs of R consecutive entities, one run per XCD (default 64).  "trsu" = 1 (speed only; measured
+ * within runs of R consecutive entities, one run per XCD (default 64); "trorder_e" the same
+ * for the transport's edge kernel alone (0, the default: trorder's).  "trsu" = 1 (speed only; measured
  * slower, default 0): the transport's update forms the upwind update su again instead of
  * storing and reading it.  "trepw" = 2 (speed only; measured within 2 %, default 1): two
  * edges per wavefront in the transport's edge kernel.  "trtile" = 1

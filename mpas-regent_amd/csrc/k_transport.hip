@@ -47,10 +47,13 @@ __device__ __forceinline__ double tr_flux3(double q_im2, double q_im1, double q_
 // four pairs
 // entity and pair of column slot `slot` (of (nXO - lo) * 4 slots) in the order option
 // "trorder" selects
+// (the edge kernel's order: option "trorder_e" when set, else "trorder")
+__device__ __forceinline__ int tro_of(const DevState& S, int kind) { return kind == KE && S.troe ? S.troe : S.tro; }
 __device__ __forceinline__ void tr_map(const DevState& S, int kind, int slot, int& ent, int& p) {
     const int n = (kind == KC ? S.nCO : S.nEO) - S.lo[kind];
-    if (S.tro >= 2) {
-        const int R = S.tro, per = (NSC / 2) * R;  // slots per run
+    const int tro = tro_of(S, kind);
+    if (tro >= 2) {
+        const int R = tro, per = (NSC / 2) * R;  // slots per run
         const int run = slot / per, m = min(R, n - run * R);
         if (m <= 0) {
             ent = 0x7fffffff;  // past the last run (caller returns)
@@ -61,7 +64,7 @@ __device__ __forceinline__ void tr_map(const DevState& S, int kind, int slot, in
         ent = run * R + (within - q * m) + S.lo[kind];
         p = q * 2;
         if (q >= NSC / 2) ent = 0x7fffffff;
-    } else if (S.tro) {
+    } else if (tro) {
         const int q = slot / n;
         ent = slot - q * n + S.lo[kind];
         p = q * 2;
@@ -74,14 +77,15 @@ __device__ __forceinline__ void tr_map(const DevState& S, int kind, int slot, in
 // the first of this wavefront's EPW consecutive column slots (a block holds 256 / LP * EPW
 // slots; with trorder R >= 2 one XCD takes each run's blocks)
 template <int LP, int EPW = 1>
-__device__ __forceinline__ int tr_slot0(const DevState& S) {
+__device__ __forceinline__ int tr_slot0(const DevState& S, int kind) {
     constexpr int SPB = 256 / LP * EPW;  // slots per block
-    const int on = S.tro >= 2 ? ((NSC / 2) * S.tro + SPB - 1) / SPB : S.xcd;
+    const int tro = tro_of(S, kind);
+    const int on = tro >= 2 ? ((NSC / 2) * tro + SPB - 1) / SPB : S.xcd;
     return col_of<LP>(xcd_block(on)) * EPW;
 }
 template <int LP>
 __device__ __forceinline__ void tr_slot(const DevState& S, int kind, int& ent, int& p) {
-    tr_map(S, kind, tr_slot0<LP>(S), ent, p);
+    tr_map(S, kind, tr_slot0<LP>(S, kind), ent, p);
 }
 
 // The x8 fields in their pair layout (vidx in mpas_dev.h): scalars p and p + 1 (p even)
@@ -162,7 +166,7 @@ template <int LP, int EPW>
 __global__ __launch_bounds__(256) void k_tr_edge_n(DevState S) {
     const int L = S.L, k = (int)(threadIdx.x % LP);
     const Px XP = px_pub<LP>(L), XS = px_scr<LP>(S);
-    const int s0 = tr_slot0<LP, EPW>(S);
+    const int s0 = tr_slot0<LP, EPW>(S, KE);
     int e_[EPW], p_[EPW];
 #pragma unroll
     for (int i = 0; i < EPW; i++) tr_map(S, KE, s0 + i, e_[i], p_[i]);

@@ -124,6 +124,7 @@ struct DevState {
     int vcmix;  // 1: the vertex and cell blocks of mixed grids interleaved in proportion (vc_block)
     int trsu;     // option "trsu": the transport's update forms su again instead of reading X_su
     int trepw;    // option "trepw": transport edge slots per wavefront (1, 2)
+    int troe;     // option "trorder_e": the transport edge kernel's slot order (0: trorder's)
     int tro;      // transport slot order (k_transport.hip tr_slot): 0 entity-major, 1 pair-major
     int nERing;   // decomposed mesh: local edges [0, nERing) are owned or ring-1 ghosts (edges of
                   // owned cells, numbered first among the ghost edges); 0 = not set

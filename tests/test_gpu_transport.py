@@ -57,7 +57,7 @@ def test_transport_task(x1_2562, L, const):
 
 @pytest.mark.parametrize("L", [5, 56])
 @pytest.mark.parametrize("trorder,trsu,trepw", [(0, 0, 1), (1, 0, 1), (7, 0, 1), (256, 0, 1), (0, 1, 1), (64, 1, 1),
-                                                (0, 0, 2), (7, 0, 2), (64, 0, 2)])
+                                                (0, 0, 2), (7, 0, 2), (64, 0, 2), (-256, 0, 1), (-1, 0, 2)])
 def test_transport_task_pair_major(x1_2562, L, trorder, trsu, trepw):
     """option trorder = 0 (entity-major), 1 (pair-major slot order) and R >= 2 (pair-major
     within runs of R entities, the last run partial at R = 7 and 256); option trsu (su formed again by the
@@ -65,7 +65,13 @@ def test_transport_task_pair_major(x1_2562, L, trorder, trsu, trepw):
     st, _ = transport_state(x1_2562, L, DT)
     ref = st.copy()
     O.Oracle(ref).mpas_advance_scalars_mono(DT)
-    got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT), trorder=trorder, trsu=trsu, trepw=trepw)
+    if trorder < 0:  # option trorder_e (the edge kernel's own order) beside the default trorder
+        def run(c):
+            c.set_option("trorder_e", -trorder)
+            T.atm_advance_scalars_mono(c, DT)
+        got = gpu(st, run, trsu=trsu, trepw=trepw)
+    else:
+        got = gpu(st, lambda c: T.atm_advance_scalars_mono(c, DT), trorder=trorder, trsu=trsu, trepw=trepw)
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
 
