@@ -76,7 +76,9 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * setup's edge copies in stage 0's dyn_tend edge kernel; "tmedge" = 1 (default 0) has
  * dyn_tend store theta_m(cell1) + theta_m(cell2) per edge for the acoustic substeps;
  * "hfuse" = 1 puts independent neighbouring kernels in one launch, 2 (default) only below
- * 16384 owned cells (read-only "hfuse_active").
+ * 16384 owned cells (read-only "hfuse_active"). "fusedamp_halo" = 1 (default 0: measured neutral at
+ * one rank of an 8-way x1.163842 split) applies fusedamp and fusesml on decomposed meshes
+ * too (with "ring1"): the div is exchanged where rtheta_pp was.
  * "physics" = 1 selects the MPAS vertical solver: vert_imp with Q16/Q17
  * fixed, the acoustic step with the ru_p update (Q18), the MPAS statement order (Q19/Q20)
  * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), recover_large_step

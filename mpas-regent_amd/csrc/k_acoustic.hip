@@ -448,11 +448,11 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
 template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
                               double coef_prev, int tme, int sml) {
-    if ((tme || sml) && (S.physics || S.halo)) return hipErrorInvalidValue;  // (atm_srk3 only, reference semantics)
+    if ((tme && (S.physics || S.halo)) || (sml && S.physics)) return hipErrorInvalidValue;  // (atm_srk3, reference semantics)
     if (sml && (small_step != 0 || mode == 0)) return hipErrorInvalidValue;
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
-    if (mode && (S.physics || S.halo)) return hipErrorInvalidValue;  // (srk3 never asks: reference semantics only)
+    if (mode && S.physics) return hipErrorInvalidValue;  // (srk3 never asks: reference semantics only)
     if (S.physics) {  // Q18: the edges first
         const double rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
         auto ru = [&](const DevState& X) {
@@ -503,8 +503,19 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
         if (exact) go_s(std::true_type{});
         else go_s(std::false_type{});
     };
-    HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m);  // (ru_p at the edges of owned cells only)
+    // (ru_p at the edges of owned cells only; MODE 2 also div at their cells -- X_dvB, the
+    // previous substep's; SML u_tend at the edges of owned cells)
+    if (mode == 2 && sml) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, X_dvB, F_u_tend);
+    else if (mode == 2) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, X_dvB);
+    else if (sml) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, F_u_tend);
+    else HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m);
     HALO_WROTE(S, F_rtheta_pp_old, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
+    if (sml) HALO_WROTE(S, F_w);
+    if (mode) HALO_WROTE(S, X_dvA);
+    // MODE 2: the damped ru_p of every edge an owned cell owns (X_eown) -- the owned edges
+    // and, the owned cells coming first in the local numbering, the ghost edges of owned
+    // cells -- from the fresh ru_p and div there: fresh on the ring-1 ghost edges
+    if (mode == 2 && S.halo) S.halo->fresh_ring1({X_rupB});
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,

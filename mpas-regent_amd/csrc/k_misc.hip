@@ -285,11 +285,27 @@ double divdamp_coef(double dts) {  // :1736-1738
 }
 template <int LP>
 static hipError_t divdamp_div_lp(const DevState& S, hipStream_t st, double dts, int tme) {
-    if (S.halo || S.physics) return hipErrorInvalidValue;  // (the fused path's; srk3 never asks otherwise)
+    if (S.physics || (tme && S.halo)) return hipErrorInvalidValue;  // (the fused path's; srk3 never asks otherwise)
     const double coef_divdamp = divdamp_coef(dts);
-    const int nb = col_blocks_n<LP, 2>(S, KE);
-    if (nb && tme) k_div_damp<LP, 2, false, true, true><<<nb, 256, 0, st>>>(S, coef_divdamp);
-    else if (nb) k_div_damp<LP, 2, false, true><<<nb, 256, 0, st>>>(S, coef_divdamp);
+    auto run = [&](const DevState& X) {
+        const int nb = col_blocks_n<LP, 2>(X, KE);
+        if (nb && tme) k_div_damp<LP, 2, false, true, true><<<nb, 256, 0, st>>>(X, coef_divdamp);
+        else if (nb) k_div_damp<LP, 2, false, true><<<nb, 256, 0, st>>>(X, coef_divdamp);
+    };
+    if (!S.halo) {
+        run(S);
+        return hipGetLastError();
+    }
+    // decomposed: div (X_dvB) at the cells of the edges, and the ring-1 redundancy of
+    // divdamp_lp (the launch after the exchange also updates the ghost edges of owned cells)
+    if (!(S.ring1 && S.nERing >= S.nEO)) return hipErrorInvalidValue;
+    auto run1 = [&](const DevState& X) {
+        DevState Y = X;
+        if (!X.interior) Y.nEO = S.nERing;
+        run(Y);
+    };
+    HALO_RUN(S, st, run1, X_dvB, F_theta_m);
+    S.halo->wrote_ring1({F_ru_p});
     return hipGetLastError();
 }
 hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts, int tme) {

@@ -95,6 +95,7 @@ struct mpas_ctx {
     // (x1.2562: -3 %; x1.163842: +0.8 %, the pair runs at the lower occupancy of the two)
     int hfuse = 2;
     int fusesml = 1;    // option "fusesml": each stage's set_smlstep inside its first acoustic launch (with fusedamp)
+    int fusedamp_halo = 0;  // option "fusedamp_halo": fusedamp / fusesml on decomposed meshes too (measured neutral there)
     int tmedge = 0;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values;
                         // measured slower at both sizes)
     int fusecopy = 1;   // option "fusecopy" (with fusesetup): setup's edge copies made by stage 0's dyn_tend
@@ -678,8 +679,15 @@ struct FuseBuffers {
         dvA = c->S.f[X_dvA];
         dvB = c->S.f[X_dvB];
     }
-    void swap_rup() { std::swap(c->S.f[F_ru_p], c->S.f[X_rupB]); }
-    void swap_dv() { std::swap(c->S.f[X_dvA], c->S.f[X_dvB]); }
+    // (a decomposed context's halo keeps the ghost state of each buffer: it moves with it)
+    void swap_rup() {
+        std::swap(c->S.f[F_ru_p], c->S.f[X_rupB]);
+        if (c->halo) std::swap(c->halo->stale[F_ru_p], c->halo->stale[X_rupB]);
+    }
+    void swap_dv() {
+        std::swap(c->S.f[X_dvA], c->S.f[X_dvB]);
+        if (c->halo) std::swap(c->halo->stale[X_dvA], c->halo->stale[X_dvB]);
+    }
     void finish() {
         if (c->S.f[F_ru_p] != rup)
             hipcheck(hipMemcpyAsync(rup, c->S.f[F_ru_p], dev_bytes(c, F_ru_p), hipMemcpyDeviceToDevice, c->stream),
@@ -687,10 +695,14 @@ struct FuseBuffers {
         restore();
     }
     void restore() {
+        const bool moved = c->S.f[X_rupB] != rupB || c->S.f[X_dvA] != dvA;
         c->S.f[F_ru_p] = rup;
         c->S.f[X_rupB] = rupB;
         c->S.f[X_dvA] = dvA;
         c->S.f[X_dvB] = dvB;
+        // (ru_p's state moved with its data, which finish() copied back; the scratch
+        // buffers hold anything)
+        if (c->halo && moved) c->halo->stale[X_rupB] = c->halo->stale[X_dvA] = c->halo->stale[X_dvB] = 1;
     }
     ~FuseBuffers() { restore(); }
 };
@@ -723,10 +735,11 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     }
     // option fusecopy: ru_save / u_2 by stage 0's dyn_tend edge kernel (reads u and ru there)
     const bool fcopy = c->fusesetup && c->fusecopy && S.physics == 0 && !c->halo;
-    // option fusedamp (reference semantics, undecomposed): each damping but the step's last
-    // is applied by the next acoustic launch (k_acoustic MODE 2), the last from the div
-    // the acoustic step stored (launch_div_damping_div); the same bits as the separate task
-    const bool fuse = c->fusedamp && S.physics == 0 && !c->halo;
+    // option fusedamp (reference semantics): each damping but the step's last is applied by
+    // the next acoustic launch (k_acoustic MODE 2), the last from the div the acoustic step
+    // stored (launch_div_damping_div); the same bits as the separate task.  Decomposed (option
+    // fusedamp_halo): the div is exchanged where rtheta_pp was, the ring-1 edges stay fresh
+    const bool fuse = c->fusedamp && S.physics == 0 && (!c->halo || (c->fusedamp_halo && S.ring1 && S.nERing >= S.nEO));
     FuseBuffers fb(c);
     int n_acoustic = 0, done_acoustic = 0;
     for (int r = 0; r < 3; r++) n_acoustic += number_sub_steps[r] + (S.physics ? 0 : 1);
@@ -1079,6 +1092,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusecopy") == 0) c->fusecopy = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
+        else if (name && std::strcmp(name, "fusedamp_halo") == 0) c->fusedamp_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
@@ -1181,6 +1195,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "fusecopy") == 0) *value = c->fusecopy;
         else if (name && std::strcmp(name, "tmedge") == 0) *value = c->tmedge;
         else if (name && std::strcmp(name, "fusesml") == 0) *value = c->fusesml;
+        else if (name && std::strcmp(name, "fusedamp_halo") == 0) *value = c->fusedamp_halo;
         else if (name && std::strcmp(name, "hfuse") == 0) *value = c->hfuse;
         else if (name && std::strcmp(name, "hfuse_active") == 0) *value = hfuse_active(c);
         else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
@@ -1190,7 +1205,9 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
                 for (uint8_t v : c->halo->stale) hsh = (hsh ^ v) * 1099511628211ull;
             *value = (int64_t)(hsh >> 1);
         }
-        else if (name && std::strcmp(name, "fusedamp_active") == 0) *value = c->fusedamp && c->S.physics == 0 && !c->halo;
+        else if (name && std::strcmp(name, "fusedamp_active") == 0)
+            *value = c->fusedamp && c->S.physics == 0 &&
+                     (!c->halo || (c->fusedamp_halo && c->S.ring1 && c->S.nERing >= c->S.nEO));
         else if (name && std::strcmp(name, "orphan_edges") == 0) {  // edges no cell lists (k_prepare)
             prepare_now(c);
             *value = c->S.n_orph;

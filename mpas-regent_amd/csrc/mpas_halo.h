@@ -95,6 +95,10 @@ struct Halo {
     // the fields were written on the owned entities and, identically to their owners, on the
     // ring-1 ghost edges: those stay fresh if they were (0 or 2 -> 2), else stale
     void wrote_ring1(std::initializer_list<int> fields);
+    // the fields were written on the owned entities and on the ring-1 ghosts from inputs the
+    // launch gathered fresh (a buffer a launcher fills anew, e.g. the fused damping's ru_p):
+    // fresh on the ring-1 ghosts whatever they were before (state 2)
+    void fresh_ring1(std::initializer_list<int> fields);
     hipError_t exchange(const DevState& S, hipStream_t st, const std::vector<int>& fields);
     // launch `fn` (a kernel launch over the entities of the DevState it is given) with the
     // stale fields of `gathers` exchanged first: interior / exchange / boundary when the

@@ -115,6 +115,11 @@ void Halo::wrote_ring1(std::initializer_list<int> fields) {
     for (int f : fields) stale[f] = was[i++] == 1 ? 1 : 2;
 }
 
+void Halo::fresh_ring1(std::initializer_list<int> fields) {
+    wrote(fields);  // (the overlap race check)
+    for (int f : fields) stale[f] = 2;
+}
+
 void Halo::wrote(std::initializer_list<int> fields) {
     // Overlap safety: the interior launch of the kernel that just ran executed beside the
     // pack of `overlapped`.  If that kernel writes one of those fields, the pack may read
@@ -446,6 +451,11 @@ static const HaloCopyTab* copy_table(const DevState& S, Halo& h, const std::vect
                                      hipStream_t st, hipError_t& e) {
     std::vector<int> key(fields);
     key.push_back(pack ? 1 : 0);
+    for (int f : fields) {  // (the fields' buffers: atm_srk3's fused damping swaps two pairs of them)
+        const uint64_t a = (uint64_t)(uintptr_t)S.f[f];
+        key.push_back((int)(uint32_t)a);
+        key.push_back((int)(uint32_t)(a >> 32));
+    }
     auto it = h.tabs.find(key);
     if (it != h.tabs.end()) return &it->second;
     HaloCopyTab t;

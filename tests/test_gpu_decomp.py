@@ -201,6 +201,7 @@ def test_ring1_redundancy_saves_exchanges(x1_2562):
     for r1 in (1, 0):
         def fn(c, r1=r1):
             c.set_option("ring1", r1)
+            c.set_option("fusedamp", 0)  # (the separate damping task; fused: test_fusedamp_decomposed)
             T.atm_srk3(c, 720.0, 1)
         got, stats = run_decomposed(st, 3, fn, 0)
         out[r1] = (got, stats)
@@ -208,6 +209,30 @@ def test_ring1_redundancy_saves_exchanges(x1_2562):
     assert not bad, bad[:6]
     for s1, s0 in zip(out[1][1], out[0][1]):  # (the first substep's ru_p is fresh from the upload)
         assert s0[0] - s1[0] == 6 + 3, (s0, s1)
+
+
+@pytest.mark.parametrize("variant,nparts,overlap", [("random", 3, 1), ("ref", 2, 0), ("mpas0", 3, 1)])
+def test_fusedamp_decomposed(x1_2562, variant, nparts, overlap):
+    """options fusedamp / fusesml on a decomposed mesh (option fusedamp_halo): each damping but the
+    step's last applied inside the next acoustic launch, the div exchanged where rtheta_pp
+    was, ru_p fresh on the ring-1 edges without an exchange -- N subdomains equal one context
+    and the separate-task decomposed run bit for bit, with fewer launches"""
+    st = state(x1_2562, 56, variant)
+    runs = {}
+    for fd in (1, 0):
+        def fn(c, fd=fd):
+            c.set_option("fusedamp", fd)
+            c.set_option("fusedamp_halo", 1)
+            assert c.get_option("fusedamp_active") == fd
+            T.atm_srk3(c, 720.0, 1)
+            T.atm_srk3(c, 720.0, 0)
+        runs[fd] = run_decomposed(st, nparts, fn, 0, overlap=overlap)
+    ref = run_single(st, lambda c: (T.atm_srk3(c, 720.0, 1), T.atm_srk3(c, 720.0, 0)), 0)
+    for fd in (1, 0):
+        bad = compare_states(runs[fd][0], ref, rtol=0.0)
+        assert not bad, f"fusedamp={fd}: {bad[:6]}"
+    for s1, s0 in zip(runs[1][1], runs[0][1]):  # the same number of exchanges (div for rtheta_pp)
+        assert s1[0] == s0[0], (s1, s0)
 
 
 def test_ring1_rank_without_boundary_edges(x1_2562):

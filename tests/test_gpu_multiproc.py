@@ -34,7 +34,7 @@ from mpasdyn import decomp, lib
 from mpasdyn import mesh as M
 from mpasdyn import tasks as T
 rank, n, port, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-L, variant, exact, overlap, steps = {L}, {variant!r}, {exact}, {overlap}, {steps}
+L, variant, exact, overlap, steps, fdh = {L}, {variant!r}, {exact}, {overlap}, {steps}, {fdh}
 m = M.load_x1_2562()
 st = make_state(M.zero_based(m) if variant == "mpas0" else m, L, "random" if variant == "mpas0" else variant)
 d = decomp.Decomposition(st, n)
@@ -42,6 +42,7 @@ loc = d.local_state(rank)
 with lib.Context(*d.n_local(rank), st.L) as c:
     c.set_option("exact", exact)
     c.set_option("overlap", overlap)
+    c.set_option("fusedamp_halo", fdh)
     lib.setup_subdomain(c, d, rank)
     c.upload(loc)
     lib.halo_socket(c, n, rank, "127.0.0.1", port)
@@ -75,9 +76,9 @@ def _free_port(n):
     raise RuntimeError("no free port range")
 
 
-def run_processes(st, nparts, tmp_path, L, variant, exact, overlap, steps):
+def run_processes(st, nparts, tmp_path, L, variant, exact, overlap, steps, fdh=0):
     port = _free_port(nparts)
-    code = WORKER.format(repo=REPO, L=L, variant=variant, exact=exact, overlap=overlap, steps=steps)
+    code = WORKER.format(repo=REPO, L=L, variant=variant, exact=exact, overlap=overlap, steps=steps, fdh=fdh)
     outs = [str(tmp_path / f"rank{r}.npz") for r in range(nparts)]
     procs = [subprocess.Popen([sys.executable, "-c", code, str(r), str(nparts), str(port), outs[r]],
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r in range(nparts)]
@@ -116,15 +117,15 @@ def run_single(st, exact, steps):
     return got
 
 
-@pytest.mark.parametrize("nparts,variant,L,exact,overlap", [(2, "random", 56, 1, 1), (3, "mpas0", 5, 0, 1),
-                                                            (3, "ref", 5, 1, 0)])
-def test_srk3_processes_equal_single(x1_2562, tmp_path, nparts, variant, L, exact, overlap):
-    """two RK3 steps (schedules as atm_timestep runs them) in 2 or 3 rank processes"""
+@pytest.mark.parametrize("nparts,variant,L,exact,overlap,fdh", [(2, "random", 56, 1, 1, 0), (3, "mpas0", 5, 0, 1, 0),
+                                                                (3, "ref", 5, 1, 0, 0), (3, "random", 56, 0, 1, 1)])
+def test_srk3_processes_equal_single(x1_2562, tmp_path, nparts, variant, L, exact, overlap, fdh):
+    """two RK3 steps in 2 or 3 rank processes (fdh: option fusedamp_halo)"""
     st = make_state(M.zero_based(x1_2562) if variant == "mpas0" else x1_2562, L,
                     "random" if variant == "mpas0" else variant)
     steps = 2
     ref = run_single(st, exact, steps)
-    got, exchanges = run_processes(st, nparts, tmp_path, L, variant, exact, overlap, steps)
+    got, exchanges = run_processes(st, nparts, tmp_path, L, variant, exact, overlap, steps, fdh)
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
     assert all(e > 0 for e in exchanges) and len(set(exchanges)) == 1  # every rank ran the same exchanges
