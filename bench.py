@@ -83,6 +83,11 @@ class Hip:
     def device_sync(self):
         assert self.h.hipDeviceSynchronize() == 0
 
+    def device_count(self):
+        n = ctypes.c_int(0)
+        assert self.h.hipGetDeviceCount(ctypes.byref(n)) == 0
+        return int(n.value)
+
     def elapsed_ms(self, e0, e1):
         assert self.h.hipEventSynchronize(e1) == 0
         ms = ctypes.c_float()
@@ -176,6 +181,28 @@ def free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+def free_port_range(n):
+    """a base port with n free consecutive ports (the socket halo transport: rank r on base + r)"""
+    for _ in range(50):
+        base = free_port()
+        if base + n >= 65535:
+            continue
+        ok = True
+        for q in range(base, base + n):
+            t = socket.socket()
+            try:
+                t.bind(("127.0.0.1", q))
+            except OSError:
+                ok = False
+            finally:
+                t.close()
+            if not ok:
+                break
+        if ok:
+            return base
+    raise RuntimeError("no free port range")
 
 
 def spawn_ranks(n, argv):
@@ -355,6 +382,9 @@ def main():
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="extra mpas_set_option (A/B runs, e.g. xcd=32)")
     ap.add_argument("--replicas", action="store_true", help="N > 1: full-mesh replicas instead of a decomposition")
+    ap.add_argument("--halo", choices=["rccl", "socket"], default="rccl",
+                    help="socket: the host-staged TCP transport, ranks sharing the visible GPUs -- a rehearsal of "
+                         "the multi-rank flow on one GPU, not a measurement")
     ap.add_argument("--decompose", action="store_true",
                     help="run the decomposed (RCCL halo) path also at N = 1 (a 1-part decomposition)")
     ap.add_argument("--physics", type=int, nargs="?", const=1, default=0, choices=[0, 1, 2],
@@ -422,17 +452,26 @@ def main():
         dec = decomp.Decomposition(st, world)
         lst = dec.local_state(rank)
         dims = (*dec.n_local(rank), L)
-        ctx = lib.Context(*dims, device=local_rank)
+        device = local_rank if args.halo == "rccl" else local_rank % Hip().device_count()
+        ctx = lib.Context(*dims, device=device)
         lib.setup_subdomain(ctx, dec, rank)
-        uid = lib.rccl_unique_id() if rank == 0 else None
-        if rv is not None:
-            uid = rv.bcast(uid)
-        lib.halo_rccl(ctx, world, rank, uid)
+        if args.halo == "socket":  # rank r listens on base + r (rank 0 picks the range)
+            base = str(free_port_range(world)).encode() if rank == 0 else None
+            if rv is not None:
+                base = rv.bcast(base)
+            lib.halo_socket(ctx, world, rank, "127.0.0.1", int(base.decode()))
+        else:
+            uid = lib.rccl_unique_id() if rank == 0 else None
+            if rv is not None:
+                uid = rv.bcast(uid)
+            lib.halo_rccl(ctx, world, rank, uid)
         overlap = int(os.environ.get("MPAS_OVERLAP", "1"))
         ctx.set_option("overlap", overlap)
         own = dec.n_owned(rank)
         nint = dec.n_interior(rank)
-        halo_info = {"partition": f"{world} contiguous Morton blocks of cells", "owned": list(own),
+        halo_info = {"partition": f"{world} contiguous blocks of the curve-ordered cells (cube-face Hilbert)",
+                     "transport": args.halo if args.halo == "rccl" else "socket (host-staged TCP rehearsal, not a measurement)",
+                     "owned": list(own),
                      "ghost_frac": [round(1 - o / n, 4) for o, n in zip(own, dims[:3])],
                      "interior_frac": [round(i / max(o, 1), 4) for i, o in zip(nint, own)],
                      "overlap": overlap}

@@ -114,6 +114,12 @@ def test_single_rank_dry_run_without_torch():
     assert p.returncode == 0 and json.loads(p.stdout.strip())["torch_loaded"] is False
 
 
+def test_free_port_range():
+    import bench
+    base = bench.free_port_range(4)
+    assert 1024 < base < 65535 - 4
+
+
 def test_rendezvous_in_threads():
     """the rendezvous' collectives at world 4, ranks as threads of one process"""
     import threading

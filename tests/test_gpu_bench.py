@@ -40,6 +40,19 @@ def test_bench_line(mode):
 
 
 @pytest.mark.gpu
+def test_bench_multirank_flow_socket():
+    """--gpus 2 --halo socket: bench.py spawns two rank processes that share the one GPU,
+    meet over the TCP rendezvous, split the mesh and exchange halos over the host-staged
+    socket transport -- the multi-rank flow of the driver's N-GPU run (rank spawning,
+    rendezvous, decomposition, max-over-ranks timing, one JSON line), RCCL aside"""
+    d = run_bench("--gpus", "2", "--halo", "socket", "--ncells", "2562")
+    assert KEYS <= set(d)
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["value"] > 0
+    assert d["halo"]["transport"].startswith("socket") and d["halo"]["exchanges_per_step"] > 0
+    assert all(0 < g < 0.5 for g in d["halo"]["ghost_frac"][:1])
+
+
+@pytest.mark.gpu
 def test_bench_line_transport():
     """--transport: the MPAS solver and the scalar transport inside the timed step"""
     d = run_bench("--transport")
