@@ -345,8 +345,8 @@ int sock_init(Halo* h, int nranks, int rank, const char* host, int base_port, st
             if (fd >= 0 && ::connect(fd, (sockaddr*)&to, sizeof(to)) != 0) {
                 ::close(fd);
                 fd = -1;
-                usleep(100000);
             }
+            if (fd < 0) usleep(100000);
         }
         if (fd < 0) {
             ::close(ls);
