@@ -60,7 +60,8 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * evaluate the reference's literal order (bit-identical to the oracle, slower);
  * "xcd" = 0 dispatcher block order, 1 one contiguous eighth of the columns per XCD,
  * G > 1 runs of G blocks per XCD inside windows of 8G (default 64); "epw" = 1, 2 (default)
- * or 4 entities per column slot in div_damping / solve_diagnostics; "vcmix" = 1 (default)
+ * or 4 entities per column slot in div_damping / solve_diagnostics; "cve" = 1, 4 or 8
+ * vertices per wavefront in dyn_tend's delsq_vorticity (default 0: 4); "vcmix" = 1 (default)
  * interleaves the vertex and cell blocks of the mixed grids; "overlap" = 1 (default)
  * computes interior entities beside the halo exchange of a decomposed mesh; "self" = 0
  * disables the SELF gathers; "graph" = 1 (default) makes mpas_atm_srk3 capture its step once

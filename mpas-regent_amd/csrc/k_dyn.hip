@@ -471,33 +471,46 @@ __global__ __launch_bounds__(256, MPAS_B_MINW) void k_dyn_B(DevState S, DynK a) 
 }
 
 // ------------------------------------------------------------------------ C (rk0)
-template <int LP, bool SELF>
+// VE vertices per vertex wave of C (at LP = 64): a vertex is 3 gathers and one store, so a
+// one-vertex wave is latency-bound; the VE vertices issue their gathers together
+// (option "cve", default 4; profiles/r03/c_vertex_epw: C 482 -> 398 us at x1.163842, the
+// step -0.7 %; 8 vertices: C 410 us, the step and x1.2562 no better than 4)
+template <int LP, bool SELF, int VE>
 __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
     ColMap<LP> m(S, KV);
     int bi;
-    if (vc_block(S, m.blk, nVB, bi)) {  // delsq_vorticity (:1052-1060)
-        const int vx = col_of<LP>(bi) + S.lo[KV], k = m.k;
-        if (vx >= S.nVO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
-        const int* eov = fi(S, F_edgesOnVertex) + (size_t)vx * 3;
-        const double* sgn = fd(S, F_edgesOnVertex_sign) + (size_t)vx * 3;
-        const double iat = fd(S, F_invAreaTriangle)[vx];
-        int ev[3];
-        double d[3], sg_[3], dc_[3];
-        row_ld(eov, ev);
-        row_ld(sgn, sg_);
-        row_ld(fd(S, X_ve_dc) + (size_t)vx * 3, dc_);  // dcEdge(edgesOnVertex)
-        gather2s<LP>(dsu, ev[0], ev[1], k, d[0], d[1]);
-        d[2] = colk(dsu, ev[2]);
-        if (k >= L) return;
-        double dsv = 0.0;
+    if (vc_block(S, m.blk, nVB, bi)) {  // VE vertices: delsq_vorticity (:1052-1060)
+        const int v0 = col_of<LP>(bi) * VE + S.lo[KV], k = m.k;
+        if (v0 >= S.nVO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
+        int ev[VE][3];
+        double d[VE][3], sg_[VE][3], dc_[VE][3], iat[VE];
 #pragma unroll
-        for (int i = 0; i < 3; i++) {
-            double edge_sign = iat * dc_[i] * sg_[i];
-            dsv += edge_sign * d[i];
+        for (int j = 0; j < VE; j++) {
+            const int v = min(v0 + j, S.nVO - 1);
+            row_ld(fi(S, F_edgesOnVertex) + (size_t)v * 3, ev[j]);
+            row_ld(fd(S, F_edgesOnVertex_sign) + (size_t)v * 3, sg_[j]);
+            row_ld(fd(S, X_ve_dc) + (size_t)v * 3, dc_[j]);  // dcEdge(edgesOnVertex)
+            iat[j] = fd(S, F_invAreaTriangle)[v];
         }
-        colk(fw(S, F_delsq_vorticity), vx) = dsv;
+#pragma unroll
+        for (int j = 0; j < VE; j++) gather2s<LP>(dsu, ev[j][0], ev[j][1], k, d[j][0], d[j][1]);
+#pragma unroll
+        for (int j = 0; j + 1 < VE; j += 2) gather2s<LP>(dsu, ev[j][2], ev[j + 1][2], k, d[j][2], d[j + 1][2]);
+        if (VE % 2) d[VE - 1][2] = colk(dsu, ev[VE - 1][2]);
+        if (k >= L) return;
+#pragma unroll
+        for (int j = 0; j < VE; j++) {
+            if (v0 + j >= S.nVO) break;  // (wave-uniform)
+            double dsv = 0.0;
+#pragma unroll
+            for (int i = 0; i < 3; i++) {
+                double edge_sign = iat[j] * dc_[j][i] * sg_[j][i];
+                dsv += edge_sign * d[j][i];
+            }
+            colk(fw(S, F_delsq_vorticity), v0 + j) = dsv;
+        }
         return;
     }
     const int c = col_of<LP>(bi) + S.lo[KC];
@@ -932,10 +945,17 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         }
     };
     auto kC = [&](const DevState& X) {  // vertex blocks (del4) first, then cell blocks
-        const int nv = del4 ? col_blocks<LP>(X, KV) : 0, nb = nv + col_blocks<LP>(X, KC);
-        if (!nb) return;
-        if (X.selfc) k_dyn_C<LP, true><<<nb, 256, 0, st>>>(X, a, nv);
-        else k_dyn_C<LP, false><<<nb, 256, 0, st>>>(X, a, nv);
+        auto go = [&](auto ve) {
+            constexpr int VE = LP == 64 ? decltype(ve)::value : 1;
+            const int nv = del4 ? col_blocks_n<LP, VE>(X, KV) : 0, nb = nv + col_blocks<LP>(X, KC);
+            if (!nb) return;
+            if (X.selfc) k_dyn_C<LP, true, VE><<<nb, 256, 0, st>>>(X, a, nv);
+            else k_dyn_C<LP, false, VE><<<nb, 256, 0, st>>>(X, a, nv);
+        };
+        const int ve = X.cve ? X.cve : 4;  // (option "cve")
+        if (ve == 8) go(std::integral_constant<int, 8>{});
+        else if (ve == 4) go(std::integral_constant<int, 4>{});
+        else go(std::integral_constant<int, 1>{});
     };
     auto kD = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);

@@ -1109,6 +1109,9 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "trorder_e") == 0) {
             if (value < 0 || value > (1 << 20)) throw Fail{MPAS_EINVAL, "trorder_e must be 0 (trorder's), 1 or a run length >= 2"};
             c->S.troe = (int)value;
+        } else if (name && std::strcmp(name, "cve") == 0) {
+            if (value != 0 && value != 1 && value != 4 && value != 8) throw Fail{MPAS_EINVAL, "cve must be 0, 1, 4 or 8"};
+            c->S.cve = (int)value;
         } else if (name && std::strcmp(name, "trepw") == 0) {
             if (value != 1 && value != 2) throw Fail{MPAS_EINVAL, "trepw must be 1 or 2"};
             c->S.trepw = (int)value;
@@ -1168,6 +1171,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "trorder") == 0) *value = c->S.tro;
         else if (name && std::strcmp(name, "trsu") == 0) *value = c->S.trsu;
         else if (name && std::strcmp(name, "trepw") == 0) *value = c->S.trepw;
+        else if (name && std::strcmp(name, "cve") == 0) *value = c->S.cve;
         else if (name && std::strcmp(name, "trorder_e") == 0) *value = c->S.troe;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
         else if (name && std::strcmp(name, "tredge") == 0) *value = c->tredge;

@@ -89,6 +89,23 @@ def test_srk3_decomposed_equals_single(x1_2562, variant, nparts, L, overlap):
         assert all(s[0] > 0 for s in stats)  # the halo was exercised
 
 
+@pytest.mark.parametrize("cve", [1, 4, 8])
+def test_dyn_tend_vertex_widths_decomposed(x1_2562, cve):
+    """dyn_tend rk 0 on 3 subdomains (vertex counts not multiples of the wave's vertices:
+    the last vertex wave is partial) with option cve, equal to the single context"""
+    st = state(x1_2562, 56, "random")
+
+    def fn(c):
+        c.set_option("cve", cve)
+        T.atm_compute_dyn_tend_work(c, 0, 720.0)
+    ref = run_single(st, fn, 1)
+    d = decomp.Decomposition(st, 3)
+    assert cve == 1 or any(d.n_owned(r)[2] % (4 * cve) for r in range(3))
+    got, _ = run_decomposed(st, 3, fn, 1)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
 def test_srk3_part_file_16(x1_2562):
     """the reference's own x1.2562.graph.info.part.16 split, 16 subdomains, schedule 0"""
     st = state(x1_2562, 5, "random")

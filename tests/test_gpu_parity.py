@@ -518,3 +518,21 @@ def test_fusedamp_dt_zero(x1_2562):
     assert not np.isfinite(ref["ru_p"]).all()
     bad = compare_states(got, ref, rtol=0.0)
     assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("L", [56, 63])
+@pytest.mark.parametrize("variant", ["random", "mpas0"])
+@pytest.mark.parametrize("cve", [1, 4, 8])
+def test_dyn_tend_vertex_widths(x1_2562, L, variant, cve):
+    """option cve: 1, 4 or 8 vertices per wavefront in dyn_tend's delsq_vorticity, each
+    value-identical to the oracle (rk 0, where the del4 terms run)"""
+    st = base_state(x1_2562, L, variant)
+    ref = run_oracle(st, lambda o: o.atm_compute_dyn_tend_work(0, 720.0))
+
+    def fn(c):
+        c.set_option("cve", cve)
+        assert c.get_option("cve") == cve
+        T.atm_compute_dyn_tend_work(c, 0, 720.0)
+    got = run_gpu(st, fn, exact=1)
+    bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, f"cve={cve}: {bad[:6]}"
