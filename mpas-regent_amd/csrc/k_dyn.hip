@@ -205,10 +205,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 
 // ------------------------------------------------------------------------ B (edges)
 template <int LP, bool RK0, bool MD, bool HF>
-#ifndef MPAS_B_MINW
-#define MPAS_B_MINW 1
-#endif
-__global__ __launch_bounds__(256, MPAS_B_MINW) void k_dyn_B(DevState S, DynK a) {
+__global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -246,23 +243,10 @@ __global__ __launch_bounds__(256, MPAS_B_MINW) void k_dyn_B(DevState S, DynK a) 
     for (int j = 0; j < QF; j++) ee_[j] = rec[2 + j];
     row_ld(woe, woe_);
     const bool kl = k < L;
-#ifndef MPAS_EXPT_EOE
-#define MPAS_EXPT_EOE QF
-#endif
-#ifndef MPAS_EXPT_ADV
-#define MPAS_EXPT_ADV (AF - 1)
-#endif
-    // (MPAS_EXPT_EOE / MPAS_EXPT_ADV < the list widths: a timing-only experiment build,
-    // tools/gather_cost.sh, that gathers fewer columns and reuses them -- wrong values)
 #pragma unroll
     for (int j = 0; j < QF; j += 2) {
-        if (j < MPAS_EXPT_EOE) {
-            gather2s<LP>(u_f, ee_[j], ee_[j + 1], k, ue_[j], ue_[j + 1]);
-            gather2s<LP>(pv_f, ee_[j], ee_[j + 1], k, pve_[j], pve_[j + 1]);
-        } else {
-            ue_[j] = ue_[j - 2] * 1.0000001, ue_[j + 1] = ue_[j - 1] * 1.0000001;
-            pve_[j] = pve_[j - 2] * 1.0000001, pve_[j + 1] = pve_[j - 1] * 1.0000001;
-        }
+        gather2s<LP>(u_f, ee_[j], ee_[j + 1], k, ue_[j], ue_[j + 1]);
+        gather2s<LP>(pv_f, ee_[j], ee_[j + 1], k, pve_[j], pve_[j + 1]);
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = rec[22];
@@ -278,13 +262,7 @@ __global__ __launch_bounds__(256, MPAS_B_MINW) void k_dyn_B(DevState S, DynK a) 
     static_assert(AF == 9, "tv_ pairing below");
     double tr_phys;
 #pragma unroll
-    for (int j = 0; j < AF - 1; j += 2) {
-        if (j < MPAS_EXPT_ADV) {
-            gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
-        } else {
-            tv_[j] = tv_[j - 2] * 1.0000001, tv_[j + 1] = tv_[j - 1] * 1.0000001;
-        }
-    }
+    for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
     gather2<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k, tv_[AF - 1], tr_phys);
 
     // MD: the state w at the advCells, for the w reconstruction flux_arr of this edge

@@ -121,20 +121,27 @@ struct mpas_ctx {
     // by any option change or mesh upload; not used while per-task timing is on or on a
     // decomposed context (the halo bookkeeping is host-side per launch)
     int graph_on = 1;
-    bool graph_valid = false;
-    double graph_dt = 0.0;
-    int graph_schedule = -1;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t graph_exec = nullptr;
-    int64_t graph_captures = 0, graph_launches = 0;
     // decomposed contexts (option "graph_halo"; RCCL and stub transports -- the loopback's
     // host barriers cannot be captured): the halo bookkeeping is host-side and evolves
-    // identically every step once its state at the step's start repeats, so the step is
-    // captured then, with the state at its start (graph_stale0) as part of the key, and a
-    // replay sets the host state to the one the captured step ended in (graph_stale1)
+    // identically every step from a given state at the step's start, so that state is part
+    // of a captured step's key (stale0), and a replay sets the host state to the one the
+    // captured step ended in (stale1).  A few steps are kept, one per start state seen twice
+    // (a standalone task or an upload between steps gives a second one)
+    struct GraphEntry {
+        double dt = 0.0;
+        int schedule = -1;
+        std::vector<uint8_t> stale0, stale1;
+        int64_t exch = 0, fields = 0;
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        uint64_t used = 0;
+    };
+    static constexpr size_t kGraphCache = 4;
+    std::vector<GraphEntry> graphs;
+    uint64_t graph_clock = 0;
+    int64_t graph_captures = 0, graph_launches = 0;
     int graph_halo = 0;
-    std::vector<uint8_t> graph_stale0, graph_stale1, prev_stale0;
-    int64_t graph_exch = 0, graph_fields = 0;
+    std::vector<std::vector<uint8_t>> seen_stale0;  // start states stepped eagerly once
     // option "trtile": the tiled transport (k_transport.hip) when the mesh allows it; the
     // tiles are rebuilt after a mesh upload or a change of the owned / interior cells.
     // Off by default: measured 2x slower than the three kernels
@@ -875,12 +882,16 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }
 
+void graph_free(mpas_ctx::GraphEntry& g) {
+    if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (g.graph) (void)hipGraphDestroy(g.graph);
+    g.exec = nullptr;
+    g.graph = nullptr;
+}
 void graph_drop(mpas_ctx* c) {
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-    if (c->graph) (void)hipGraphDestroy(c->graph);
-    c->graph_exec = nullptr;
-    c->graph = nullptr;
-    c->graph_valid = false;
+    for (auto& g : c->graphs) graph_free(g);
+    c->graphs.clear();
+    c->seen_stale0.clear();
 }
 
 void prepare_now(mpas_ctx* c) {
@@ -902,58 +913,74 @@ void srk3_step(mpas_ctx* c, double dt, int schedule) {
         return;
     }
     prepare_now(c);  // (synchronous: never inside a capture)
-    if (h) {
-        if (c->graph_valid && c->graph_dt == dt && c->graph_schedule == schedule && h->stale == c->graph_stale0) {
-            hipcheck(hipGraphLaunch(c->graph_exec, c->stream), "hipGraphLaunch");
+    static const std::vector<uint8_t> none;
+    const std::vector<uint8_t>& start = h ? h->stale : none;
+    for (auto& g : c->graphs)
+        if (g.dt == dt && g.schedule == schedule && g.stale0 == start) {
+            hipcheck(hipGraphLaunch(g.exec, c->stream), "hipGraphLaunch");
+            g.used = ++c->graph_clock;
             c->graph_launches++;
-            h->stale = c->graph_stale1;  // the bookkeeping the captured step made
-            h->exchanges += c->graph_exch;
-            h->fields_moved += c->graph_fields;
-            return;
-        }
-        if (h->stale != c->prev_stale0) {  // not yet in the steady state: one more eager step
-            c->prev_stale0 = h->stale;
-            srk3(c, dt, schedule);
-            return;
-        }
-    }
-    if (!(c->graph_valid && c->graph_dt == dt && c->graph_schedule == schedule)) {
-        graph_drop(c);
-        std::vector<uint8_t> stale0;
-        int64_t ex0 = 0, fl0 = 0;
-        if (h) {
-            stale0 = h->stale;
-            ex0 = h->exchanges;
-            fl0 = h->fields_moved;
-        }
-        hipcheck(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-        try {
-            srk3(c, dt, schedule);
-        } catch (...) {
-            hipGraph_t g = nullptr;
-            (void)hipStreamEndCapture(c->stream, &g);
-            if (g) (void)hipGraphDestroy(g);
-            if (h) {  // nothing ran: the bookkeeping goes back to the step's start
-                h->stale = stale0;
-                h->exchanges = ex0;
-                h->fields_moved = fl0;
+            if (h) {
+                h->stale = g.stale1;  // the bookkeeping the captured step made
+                h->exchanges += g.exch;
+                h->fields_moved += g.fields;
             }
-            throw;
+            return;
         }
-        hipcheck(hipStreamEndCapture(c->stream, &c->graph), "hipStreamEndCapture");
-        hipcheck(hipGraphInstantiate(&c->graph_exec, c->graph, nullptr, nullptr, 0), "hipGraphInstantiate");
-        c->graph_valid = true;
-        c->graph_dt = dt;
-        c->graph_schedule = schedule;
-        c->graph_captures++;
-        if (h) {
-            c->graph_stale0 = stale0;
-            c->graph_stale1 = h->stale;
-            c->graph_exch = h->exchanges - ex0;
-            c->graph_fields = h->fields_moved - fl0;
-        }
+    if (h && std::find(c->seen_stale0.begin(), c->seen_stale0.end(), h->stale) == c->seen_stale0.end()) {
+        // a start state not seen before (e.g. the first step after an upload): one eager step
+        if (c->seen_stale0.size() >= 16) c->seen_stale0.erase(c->seen_stale0.begin());
+        c->seen_stale0.push_back(h->stale);
+        srk3(c, dt, schedule);
+        return;
     }
-    hipcheck(hipGraphLaunch(c->graph_exec, c->stream), "hipGraphLaunch");
+    mpas_ctx::GraphEntry g;
+    g.dt = dt;
+    g.schedule = schedule;
+    g.stale0 = start;
+    int64_t ex0 = 0, fl0 = 0;
+    if (h) {
+        ex0 = h->exchanges;
+        fl0 = h->fields_moved;
+        h->capture_miss = false;
+    }
+    hipcheck(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    try {
+        srk3(c, dt, schedule);
+    } catch (...) {
+        hipGraph_t gr = nullptr;
+        (void)hipStreamEndCapture(c->stream, &gr);
+        if (gr) (void)hipGraphDestroy(gr);
+        if (h) {  // nothing ran: the bookkeeping goes back to the step's start
+            h->stale = g.stale0;
+            h->exchanges = ex0;
+            h->fields_moved = fl0;
+            if (h->capture_miss) {  // a pack table not built yet (never built inside a capture)
+                h->capture_miss = false;
+                h->err.clear();
+                srk3(c, dt, schedule);  // eagerly: builds it; the next step captures
+                return;
+            }
+        }
+        throw;
+    }
+    hipcheck(hipStreamEndCapture(c->stream, &g.graph), "hipStreamEndCapture");
+    hipcheck(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0), "hipGraphInstantiate");
+    c->graph_captures++;
+    if (h) {
+        g.stale1 = h->stale;
+        g.exch = h->exchanges - ex0;
+        g.fields = h->fields_moved - fl0;
+    }
+    g.used = ++c->graph_clock;
+    if (c->graphs.size() >= mpas_ctx::kGraphCache) {  // the least recently replayed goes
+        auto lru = std::min_element(c->graphs.begin(), c->graphs.end(),
+                                    [](const mpas_ctx::GraphEntry& a, const mpas_ctx::GraphEntry& b) { return a.used < b.used; });
+        graph_free(*lru);
+        c->graphs.erase(lru);
+    }
+    c->graphs.push_back(g);
+    hipcheck(hipGraphLaunch(g.exec, c->stream), "hipGraphLaunch");
     c->graph_launches++;
 }
 

@@ -86,6 +86,10 @@ struct Halo {
     std::vector<int> overlapped;  // fields exchanged beside the last interior launch
     std::string race;             // set by wrote() when a kernel wrote one of them
     std::map<std::vector<int>, HaloCopyTab> tabs;  // pack / unpack tables per exchange signature
+    // set when an exchange inside a stream capture needed a table not built yet: tables are
+    // built and uploaded outside captures only, so that capture fails and the step runs
+    // eagerly (mpas_ctx.cpp srk3_step)
+    bool capture_miss = false;
 
     ~Halo();
     hipError_t reserve(int LP);  // size the packed buffers for the largest exchange

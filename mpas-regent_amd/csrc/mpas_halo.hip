@@ -61,6 +61,8 @@ static int kind_of_field(int f) {
     }
 }
 
+static hipError_t tables_ready(const DevState& S, Halo& h, hipStream_t st, const std::vector<int>& fields);
+
 Halo::~Halo() {
     for (auto& v : peers)
         for (auto& p : v) {
@@ -167,6 +169,8 @@ hipError_t Halo::launch(const DevState& S, hipStream_t st, std::initializer_list
         fn(S);
         return hipGetLastError();
     }
+    // (the pack / unpack tables first: nothing is forked if one cannot be built here)
+    if ((e = tables_ready(S, *this, st, need)) != hipSuccess) return e;
     // the halo stream starts after everything the task stream holds (the stale values
     // were written there); the interior launch reads no ghost and writes no gathered
     // field, so it runs beside the pack / send / recv / unpack
@@ -458,6 +462,14 @@ static const HaloCopyTab* copy_table(const DevState& S, Halo& h, const std::vect
     }
     auto it = h.tabs.find(key);
     if (it != h.tabs.end()) return &it->second;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    (void)hipStreamIsCapturing(st, &cs);
+    if (cs != hipStreamCaptureStatusNone) {  // (no allocation or upload inside a capture)
+        h.capture_miss = true;
+        h.err = "halo pack table built inside a graph capture";
+        e = hipErrorInvalidValue;
+        return nullptr;
+    }
     HaloCopyTab t;
     std::vector<HaloSeg> segs;
     for (const auto& r : reg) {
@@ -482,13 +494,10 @@ static const HaloCopyTab* copy_table(const DevState& S, Halo& h, const std::vect
     e = hipSuccess;
     if (t.nseg) {
         if ((e = hipMalloc(&t.dev, sizeof(HaloSeg) * segs.size())) != hipSuccess) return nullptr;
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        (void)hipStreamIsCapturing(st, &cs);
-        if (cs == hipStreamCaptureStatusNone)
-            e = hipMemcpy(t.dev, t.host->data(), sizeof(HaloSeg) * segs.size(), hipMemcpyHostToDevice);
-        else  // (inside a capture: a copy node; the host table stays alive in the cache)
-            e = hipMemcpyAsync(t.dev, t.host->data(), sizeof(HaloSeg) * segs.size(), hipMemcpyHostToDevice, st);
-        if (e != hipSuccess) return nullptr;
+        if ((e = hipMemcpy(t.dev, t.host->data(), sizeof(HaloSeg) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess) {
+            (void)hipFree(t.dev);
+            return nullptr;
+        }
     }
     return &(h.tabs[key] = t);
 }
@@ -507,7 +516,21 @@ static hipError_t run_copy(const DevState& S, hipStream_t st, Halo& h, const std
     return hipGetLastError();
 }
 
+// both tables of an exchange of `fields` built (outside a capture) or found; inside a capture
+// a missing one fails the call before anything is enqueued (capture_miss)
+static hipError_t tables_ready(const DevState& S, Halo& h, hipStream_t st, const std::vector<int>& fields) {
+    std::vector<Region> reg;
+    std::vector<int> byk[3];
+    plan_regions(h, fields, reg, byk);
+    hipError_t e = hipSuccess;
+    for (bool pack : {true, false})
+        if (!copy_table(S, h, reg, byk, fields, pack, st, e)) return e;
+    return hipSuccess;
+}
+
 hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<int>& fields) {
+    hipError_t e0 = tables_ready(S, *this, st, fields);
+    if (e0 != hipSuccess) return e0;
     std::vector<Region> reg;
     std::vector<int> byk[3];
     plan_regions(*this, fields, reg, byk);
@@ -574,18 +597,22 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
             const uint64_t nb = (uint64_t)x->scols * S.LP * sizeof(double);
             const uint64_t want = (uint64_t)x->rcols * S.LP * sizeof(double);
             uint64_t got = 0;
+            bool header = false;  // the peer's byte count arrived
             auto snd = [&] {
                 return sock_all(fd, (void*)&nb, 8, true) && sock_all(fd, c.hsend.data() + x->soff * S.LP, nb, true);
             };
             auto rcv = [&] {
                 if (!sock_all(fd, &got, 8, false)) return false;
+                header = true;
                 if (got != want) return false;
                 return sock_all(fd, c.hrecv.data() + x->roff * S.LP, want, false);
             };
             const bool ok = rank < x->peer ? (snd() && rcv()) : (rcv() && snd());
-            if (!ok) {
+            if (!ok) {  // a plan mismatch only when the header came and disagrees; else the transport failed
                 err = "socket halo exchange with rank " + std::to_string(x->peer) +
-                      (got != want ? " (plan mismatch: " + std::to_string(got) + " bytes for " + std::to_string(want) + ")" : "");
+                      (header && got != want
+                           ? " (plan mismatch: " + std::to_string(got) + " bytes for " + std::to_string(want) + ")"
+                           : " (transport failure: peer closed, timed out or unreachable)");
                 return hipErrorUnknown;
             }
         }

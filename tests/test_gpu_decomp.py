@@ -296,3 +296,36 @@ def test_stub_transport_graph_replay(x1_2562):
     assert not bad, bad[:6]
     assert out[1][1] == out[0][1]
     assert out[1][2] == 1 and out[1][3] >= 3 and out[0][2] == 0
+
+
+@pytest.mark.parametrize("between", ["solve", "upload", "fusedamp_halo", "schedules"])
+def test_stub_graph_start_states(x1_2562, between):
+    """graph_halo keys a captured step on the halo state at the step's start: a
+    standalone task between steps (solve_diagnostics: it writes fields the step exchanges), an
+    upload between steps, fusedamp_halo with the graph, and alternating schedules (two keys) each give start states other than the
+    steady one; replays leave the same bits and exchange counts as eager steps"""
+    st = state(x1_2562, 56, "random")
+    d = decomp.Decomposition(st, 4)
+    out = {}
+    for graph in (1, 0):
+        loc = d.local_state(1)
+        with lib.Context(*d.n_local(1), st.L) as ctx:
+            lib.setup_subdomain(ctx, d, 1)
+            lib.halo_stub(ctx)
+            ctx.set_option("graph_halo", graph)
+            if between == "fusedamp_halo":
+                ctx.set_option("fusedamp_halo", 1)
+            ctx.upload(loc)
+            for i in range(9):
+                T.atm_srk3(ctx, 720.0, 1 if between != "schedules" or i % 2 else 0)
+                if between == "solve" and i % 3 != 2:  # (two start states alternate with the steady one)
+                    T.atm_compute_solve_diagnostics(ctx, False, 2)
+                if between == "upload" and i == 4:
+                    ctx.upload(loc, names=["u", "theta_m"])
+            ctx.sync()
+            ctx.download(loc)
+            out[graph] = (loc, lib.halo_stats(ctx), ctx.get_option("graph_captures"), ctx.get_option("graph_launches"))
+    bad = compare_states(out[1][0], out[0][0], rtol=0.0)
+    assert not bad, bad[:6]
+    assert out[1][1] == out[0][1]
+    assert out[1][2] >= 1 and out[1][3] >= 2 and out[0][2] == 0
