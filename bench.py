@@ -332,10 +332,21 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_advance_acoustic_step_work[ss>0+damp]": {"small_step": 1, "damp": True},
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
              "atm_recover_large_step_variables_work[rk2]": {"rk_step": 2}}
+    def dyn_kw(name):  # atm_compute_dyn_tend_work[rk0|rk>0 (+copy) (+d4o) (+d4i) (-A)] (mpas_ctx.cpp srk3)
+        tag = name[name.index("[") + 1:-1]
+        kw = {"rk_step": 0 if tag.startswith("rk0") else 1}
+        if "+copy" in tag:
+            kw["copy"] = True
+        if "+d4o" in tag:
+            kw["defer_out"] = True
+        if tag.endswith("-A"):
+            kw["noA"] = True
+        return kw
+
     variants, tasks = {}, {}
     for name, (calls, ms) in rep.items():
         task = name.split("[")[0]
-        kw = dict(kw_of.get(name, {}))
+        kw = dyn_kw(name) if task == NORTH_STAR and "[" in name else dict(kw_of.get(name, {}))
         if physics and task == "atm_advance_acoustic_step_work":
             kw["physics"] = 1  # the acoustic task's MPAS form also updates ru_p / ruAvg
         if physics == 2 and task in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
@@ -557,7 +568,8 @@ def main():
     fsetup = bool(ctx.get_option("fusesetup")) and not args.physics
     fsml = fused and bool(ctx.get_option("fusesml"))
     fcopy = fsetup and bool(ctx.get_option("fusecopy")) and not decomposed
-    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy)
+    d4 = bool(ctx.get_option("defer4")) and not args.physics
+    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -581,7 +593,7 @@ def main():
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy),
-                      "fusesml": int(fsml), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
+                      "fusesml": int(fsml), "defer4": int(d4), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}

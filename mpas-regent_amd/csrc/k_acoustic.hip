@@ -55,7 +55,7 @@ __device__ __forceinline__ double damp_edge(double rup, double d1, double d2, do
 // SML (atm_srk3, option "fusesml"; a stage's first substep): the stage's set_smlstep first
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>
 __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int small_step, double epssm, double resm,
-                                              double coefp, int ncb, Blk bk) {
+                                              double coefp, int ncb, Blk bk, int wold = 1) {
     static_assert(!(MPASV && MODE), "the deferred damping is the reference semantics' (physics 0)");
     static_assert(!SML || (FIRST && !MPASV), "set_smlstep precedes a stage's first substep (reference semantics)");
     const int L = S.L, k = (int)(threadIdx.x % LP);
@@ -200,7 +200,7 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
 
     // :1615-1636
     const double rtpo = (small_step == 0) ? 0 : rtp;
-    if (k != L) colk(fw(S, F_rtheta_pp_old), c) = PADW(rtpo);  // (PADW: mpas_dev.h)
+    if (k != L && (MODE == 0 || wold)) colk(fw(S, F_rtheta_pp_old), c) = PADW(rtpo);  // (PADW: mpas_dev.h)
     // MODE 1/2: this substep's div (:1755) for the damping applied by the next substep
     auto store_div = [&](double rtp_new) {
         if constexpr (MODE != 0) colk(fw(S, X_dvA), c) = kl ? -(rtp_new - rtpo) : 0.0;
@@ -395,20 +395,20 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
 }
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm,
-                                                 double coefp, int ncb) {
+                                                 double coefp, int ncb, int wold) {
     acoustic_body<LP, EXACT, SELF, FIRST, MPASV, MODE, TME, SML>(S, dts, small_step, epssm, resm, coefp, ncb,
-                                                                this_blk());
+                                                                this_blk(), wold);
 }
 // option "hfuse" (atm_srk3, stages 0 and 1): a stage's last acoustic launch (MODE 2, the
 // damping of the previous substep inside) beside the stage's solve_diagnostics vertex /
 // cell kernel, which reads u only -- nothing the acoustic step reads or writes
 template <int LP, bool EXACT, bool SELF, int EPW>
 __global__ __launch_bounds__(256) void k_hf_ac_vc(DevState S, double dts, int small_step, double epssm, double resm,
-                                                 double coefp, int ncb, int nb1, int nVB) {
+                                                 double coefp, int ncb, int nb1, int nVB, int wold) {
     const int b = (int)blockIdx.x;
     if (b < nb1)
         acoustic_body<LP, EXACT, SELF, false, false, 2, false, false>(S, dts, small_step, epssm, resm, coefp, ncb,
-                                                                       Blk{b, nb1});
+                                                                       Blk{b, nb1}, wold);
     else solve_vc_body<LP, EPW, false>(S, nVB, 0, Blk{b - nb1, (int)gridDim.x - nb1});
 }
 
@@ -447,7 +447,7 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
 
 template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                              double coef_prev, int tme, int sml) {
+                              double coef_prev, int tme, int sml, int wold) {
     if ((tme && (S.physics || S.halo)) || (sml && S.physics)) return hipErrorInvalidValue;  // (atm_srk3, reference semantics)
     if (sml && (small_step != 0 || mode == 0)) return hipErrorInvalidValue;
     double epssm = kEpssm;
@@ -471,7 +471,7 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
             constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
             constexpr int M = decltype(md)::value;
 #define MPAS_AC(FI, MP, MM, TM, SM) \
-    k_acoustic<LP, E, SF, FI, MP, MM, TM, SM><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb)
+    k_acoustic<LP, E, SF, FI, MP, MM, TM, SM><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb, wold)
             if constexpr (M == 0) {
                 if (X.physics) {
                     if (first) MPAS_AC(true, true, 0, false, false);
@@ -509,7 +509,8 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     else if (mode == 2) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, X_dvB);
     else if (sml) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, F_u_tend);
     else HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m);
-    HALO_WROTE(S, F_rtheta_pp_old, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
+    if (mode == 0 || wold) HALO_WROTE(S, F_rtheta_pp_old);
+    HALO_WROTE(S, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
     if (sml) HALO_WROTE(S, F_w);
     if (mode) HALO_WROTE(S, X_dvA);
     // MODE 2: the damped ru_p of every edge an owned cell owns (X_eown) -- the owned edges
@@ -519,12 +520,12 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                           double coef_prev, int tme, int sml) {
-    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml);
+                           double coef_prev, int tme, int sml, int wold) {
+    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml, wold);
 }
 template <int LP>
 static hipError_t hf_ac_vc_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
-                              double coef_prev) {
+                              double coef_prev, int wold) {
     if (S.physics || S.halo || small_step == 0 || S.epw != 2) return hipErrorInvalidValue;
     const double epssm = kEpssm, resm = (1.0 - epssm) / (1.0 + epssm);
     const int ncb = col_blocks<LP>(S, KC);
@@ -533,17 +534,17 @@ static hipError_t hf_ac_vc_lp(const DevState& S, hipStream_t st, double dts, int
     if (!ncb || !nb2) return hipErrorInvalidValue;
     const int grid = nb1 + nb2;
     if (exact) {
-        if (S.selfc) k_hf_ac_vc<LP, true, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
-        else k_hf_ac_vc<LP, true, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
+        if (S.selfc) k_hf_ac_vc<LP, true, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
+        else k_hf_ac_vc<LP, true, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
     } else {
-        if (S.selfc) k_hf_ac_vc<LP, false, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
-        else k_hf_ac_vc<LP, false, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv);
+        if (S.selfc) k_hf_ac_vc<LP, false, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
+        else k_hf_ac_vc<LP, false, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
     }
     return hipGetLastError();
 }
 hipError_t launch_hf_acoustic_solve_vc(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
-                                       double coef_prev) {
-    MPAS_LP_DISPATCH(S.LP, hf_ac_vc_lp, S, st, dts, small_step, exact, coef_prev);
+                                       double coef_prev, int wold) {
+    MPAS_LP_DISPATCH(S.LP, hf_ac_vc_lp, S, st, dts, small_step, exact, coef_prev, wold);
 }
 
 }  // namespace mpas

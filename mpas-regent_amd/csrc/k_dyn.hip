@@ -50,8 +50,9 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 }
 
 struct DynK {
-    int rk_step, horiz_mixing, rayleigh, exact_q, tme, cp;
+    int rk_step, horiz_mixing, rayleigh, exact_q, tme, cp, d4o;
     double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
+    double h4d;  // DIN: the h4 of the rk_step 0 call whose del4 of tend_u_euler this call applies
 };
 
 
@@ -154,7 +155,10 @@ __device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk
         hd += edge_sign * col_rd<LP>(ru, eoc[i], k, L);
     }
     hd *= fd(S, F_invAreaCell)[c];
-    if (MD && k != L) colk(fw(S, F_h_divergence), c) = PADW(hd);  // (else paired with wc below)
+    // the w scratch wc (below) is formed here at rk_step 0, where C gathers it; at rk_step > 0
+    // E, its only reader, forms it from the same operands (wc_body), so A reads ru alone
+    constexpr bool WC = !MD && RK0;
+    if (!WC && k != L) colk(fw(S, F_h_divergence), c) = PADW(hd);  // (else paired with wc below)
 
     // ---- tend_rho, dpdz (:942-951)
     const double rw_p1 = lvl_up<LP>(rw, k);
@@ -178,7 +182,7 @@ __device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk
     if (ne > NF) ru_l = col_rd<LP>(ru, eoc[ne - 1], k, L);
     const double ru_lm = lvl_dn<LP>(ru_l, k);
     const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
-    if constexpr (MD) return;  // (the w tendency is formed in E from the state w)
+    if constexpr (!WC) return;  // (MD: the w tendency is formed in E from the state w)
     // (every lane goes on: the scratch wc is stored whole, 0.0 from level L up)
     double w0 = 0.0;
     if (ne > 0 && k > 0) {
@@ -204,7 +208,11 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 }
 
 // ------------------------------------------------------------------------ B (edges)
-template <int LP, bool RK0, bool MD, bool HF>
+// DIN (rk_step > 0, option "defer4"): the previous rk_step 0 call left tend_u_euler without
+// its del4 part (kernel D, skipped there); this kernel applies D's statements to the
+// tend_u_euler it reads -- the same operands in the same order, so the same bits -- and
+// stores the result.  D's tend_u of that call is dead in atm_srk3 (this kernel writes tend_u)
+template <int LP, bool RK0, bool MD, bool HF, bool DIN = false>
 __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
@@ -292,6 +300,17 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         } else {
             tue_in = colk(fd(S, F_tend_u_euler), e);
         }
+    }
+    if constexpr (DIN) {  // kernel D of the rk_step 0 call (:1132-1150), deferred here
+        const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
+        double dd1, dd2, dv1, dv2;
+        gather2s<LP>(fd(S, F_delsq_divergence), cell1, cell2, k, dd1, dd2);
+        gather2s<LP>(fd(S, F_delsq_vorticity), vertex1, vertex2, k, dv1, dv2);
+        const double u_mix_scale = fd(S, F_meshScalingDel4)[e] * a.h4d;
+        const double r_dc = u_mix_scale * kDel4uDivFactor * invDc;
+        const double r_dv = u_mix_scale * dmin_(fd(S, F_invDvEdge)[e], 4 * invDc);
+        const double u_diffusion = rho_edge * ((dd2 - dd1) * r_dc - (dv2 - dv1) * r_dv);
+        tue_in -= u_diffusion;
     }
 
     const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
@@ -428,21 +447,27 @@ __global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
         double* tuo = fw(S, F_tend_u);
         double* tueo = fw(S, F_tend_u_euler);
         if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
-            put2<LP>(Fo, e, fw(S, F_delsq_u), e, k, Hv, dsq, true, k != L);
-            put2<LP>(tueo, e, tuo, e, k, PADW(tue), PADW(tend_u), k != L, k != L);
+            if (a.d4o) {  // (defer4: D runs in the next call's B; this tend_u is dead)
+                put2<LP>(Fo, e, tueo, e, k, Hv, PADW(tue), true, k != L);
+                if (k != L) colk(fw(S, F_delsq_u), e) = dsq;
+            } else {
+                put2<LP>(Fo, e, fw(S, F_delsq_u), e, k, Hv, dsq, true, k != L);
+                put2<LP>(tueo, e, tuo, e, k, PADW(tue), PADW(tend_u), k != L, k != L);
+            }
         } else {
             tend_u += tue + tr_phys;  // :1161-1163 (rk > 0: tue is the tend_u_euler read)
             put2<LP>(Fo, e, tuo, e, k, Hv, PADW(tend_u), true, k != L);
             if (rk0) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, PADW(tue), dsq, k != L, k != L);
+            if (DIN && k != L) colk(tueo, e) = PADW(tue);
         }
         return;
     }
     if (k == L) return;
     if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
         colk(fw(S, F_tend_u_euler), e) = PADW(tue);
-        colk(fw(S, F_tend_u), e) = PADW(tend_u);
+        if (!a.d4o) colk(fw(S, F_tend_u), e) = PADW(tend_u);
     } else {
-        if (rk0) colk(fw(S, F_tend_u_euler), e) = PADW(tue);
+        if (rk0 || DIN) colk(fw(S, F_tend_u_euler), e) = PADW(tue);
         tend_u += tue + tr_phys;  // :1161-1163
         colk(fw(S, F_tend_u), e) = PADW(tend_u);
     }
@@ -651,9 +676,22 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
     // own columns (gather2: two columns per load instruction; the theta-section loads
     // too, ahead of the w stores that could alias them for the compiler)
     double wc, rw, pp, dpdz, rws, tms, tmv, twe, tte, rho_zz, rt_diab, trp, cqw = 0.0, dw_c = 0.0, dt_c = 0.0;
-    // wc: the reference's partial w tendency (A); MD: the state w
-    gather2<LP>(fd(S, MD ? F_w : X_wc), c, fd(S, F_rw), c, k, wc, rw);
-    double urz = 0.0, urm = 0.0, Fw_[NF];
+    // wc: the reference's partial w tendency (A at rk_step 0; WCE: formed below); MD: the state w
+    constexpr bool WCE = !MD && !RK0;
+    double urz = 0.0, urm = 0.0, Fw_[NF], ru_l = 0.0, wfl[2];
+    if constexpr (WCE) {
+        col_rd2<LP>(fd(S, F_uReconstructZonal), fd(S, F_uReconstructMeridional), c, k, L, urz, urm);
+        rw = colk(fd(S, F_rw), c);
+        int el = 0;  // the cell's last edge (Q13: ru_edge_w of the last edge)
+#pragma unroll
+        for (int i = 0; i < NF; i++) el = (i == ne - 1) ? e_[i] : el;
+        if (ne > NF) el = eoc[ne - 1];
+        ru_l = ne > 0 ? col_rd<LP>(ru, el, k, L) : 0.0;
+        row_ld(fd(S, X_wfl) + (size_t)c * 2, wfl);
+        wc = 0.0;
+    } else {
+        gather2<LP>(fd(S, MD ? F_w : X_wc), c, fd(S, F_rw), c, k, wc, rw);
+    }
     if constexpr (MD) {
         gather2<LP>(fd(S, F_uReconstructZonal), c, fd(S, F_uReconstructMeridional), c, k, urz, urm);
 #pragma unroll
@@ -705,6 +743,27 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
             dw2_[i] = ldz(kl && del4, dw2_[i]);
             dt1_[i] = ldz(kl && del4, dt1_[i]);
             dt2_[i] = ldz(kl && del4, dt2_[i]);
+        }
+    }
+    if constexpr (WCE) {  // dyn_A's w section (:1170-1218, Q13), the same operands in the same order
+        const double ru_lm = lvl_dn<LP>(ru_l, k);
+        const double rz = ldz(k <= L, rho_zz);
+        const double rz_m = lvl_dn<LP>(rz, k), urz_m = lvl_dn<LP>(urz, k), urm_m = lvl_dn<LP>(urm, k);
+        double w0 = 0.0;
+        if (ne > 0 && k > 0) {
+            double ru_edge_w = fzm * ru_l + fzp * ru_lm;
+            const double flux_arr = copysign(1.0, ru_edge_w) > 0.0 ? wfl[0] : wfl[1];
+#pragma unroll
+            for (int i = 0; i < NF; i++) w0 = sub_if(i < ne, w0, eocs_[i] * ru_edge_w * flux_arr);
+            for (int i = NF; i < ne; i++) w0 -= eocs[i] * ru_edge_w * flux_arr;
+        }
+        wc = w0;
+        if (k > 0) {
+            const double coslat = fd(S, X_cosLatCell)[c];
+            double aa = fzm * urz + fzp * urz_m;
+            double bb = fzm * urm + fzp * urm_m;
+            wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
+                  2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
         }
     }
     wc = ldz(kl, wc);
@@ -893,6 +952,8 @@ static DynK make_dynk(const DevState& S, const DynTendArgs& in) {
     a.inv_r_earth = 1.0 / a.r_earth;
     a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
     a.prandtl_inv = 1.0 / kPrandtl;
+    a.d4o = (in.defer_out && in.rk_step == 0 && a.h4 > 0.0) ? 1 : 0;
+    a.h4d = (in.defer_in && in.rk_step != 0 && in.horiz_mixing == 0) ? kVisc4_2dsmag * (kLenDisp * kLenDisp * kLenDisp) : 0.0;
     return a;
 }
 
@@ -911,14 +972,17 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         if (rk0) k_dyn_A<LP, true, MD><<<nb, 256, 0, st>>>(X, a);
         else k_dyn_A<LP, false, MD><<<nb, 256, 0, st>>>(X, a);
     };
+    const bool din = !MD && a.h4d > 0.0;  // (defer4: this rk_step > 0 call applies rk_step 0's D)
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
         if (hf) {
             if (rk0) k_dyn_B<LP, true, MD, true><<<nb, 256, 0, st>>>(X, a);
+            else if (din) k_dyn_B<LP, false, MD, true, !MD><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_B<LP, false, MD, true><<<nb, 256, 0, st>>>(X, a);
         } else {
             if (rk0) k_dyn_B<LP, true, MD, false><<<nb, 256, 0, st>>>(X, a);
+            else if (din) k_dyn_B<LP, false, MD, false, !MD><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_B<LP, false, MD, false><<<nb, 256, 0, st>>>(X, a);
         }
     };
@@ -965,7 +1029,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         HALO_RUN(S, st, kA, F_ru);
     }
     HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz);
-    if (!MD) HALO_WROTE(S, X_wc);
+    if (!MD && rk0) HALO_WROTE(S, X_wc);
     if (rk0) {
         HALO_RUN_R1(S, st, kB, F_vorticity, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p,
                     F_zz, F_dpdz, F_divergence, F_kdiff, F_vorticity);  // (vorticity at vertices of owned edges)
@@ -975,7 +1039,8 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         else HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, X_wc, F_theta_m);
         HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
                    F_tend_theta_euler);
-        if (del4 && in.hfuse && !S.halo) {  // D beside E, one grid
+        const bool runD = del4 && !a.d4o;  // (defer4: D runs in the next call's B)
+        if (runD && in.hfuse && !S.halo) {  // D beside E, one grid
             const int nb1 = col_blocks<LP>(S, KE), nb = nb1 + col_blocks<LP>(S, KC);
             auto go = [&](auto hfc) {
                 constexpr bool H = decltype(hfc)::value;
@@ -987,7 +1052,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 else go(std::false_type{});
             }
         } else {
-            if (del4) {
+            if (runD) {
                 HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
                 HALO_WROTE(S, F_tend_u_euler, F_tend_u);
             }
@@ -995,11 +1060,18 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
             else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
         }
     } else {
-        if (hf) HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_theta_m_save);
+        if (din && hf)
+            HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_theta_m_save,
+                     F_delsq_divergence, F_delsq_vorticity);
+        else if (din)
+            HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_delsq_divergence,
+                     F_delsq_vorticity);
+        else if (hf) HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_theta_m_save);
         else HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
         HALO_WROTE(S, X_F, F_tend_u);
+        if (din) HALO_WROTE(S, F_tend_u_euler);
         if (MD) HALO_WROTE(S, X_Fw);
-        if (hf) HALO_RUN(S, st, kE, X_F, X_Fw);
+        if (hf) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw);  // (ru: wc at the cell's last edge, reference semantics)
         else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);
     }
     HALO_WROTE(S, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);

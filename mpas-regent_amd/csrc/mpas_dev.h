@@ -182,6 +182,10 @@ struct DynTendArgs {
     int cp = 0;        // 1: the edge kernel also makes setup's ru_save = ru, u_2 = u (atm_srk3 stage 0,
                        // option "fusecopy"; undecomposed)
     int skipA = 0;     // 1: kernel A already ran (launch_hf_solve_e_dyn_A; atm_srk3 hfuse, undecomposed)
+    // option "defer4" (atm_srk3, reference semantics): rk_step 0's del4 of tend_u_euler (kernel D)
+    // is applied by the next stage's rk_step > 0 edge kernel, which reads tend_u_euler anyway
+    int defer_out = 0;  // 1 (rk_step 0): no D; tend_u_euler left without its del4 part, tend_u not stored
+    int defer_in = 0;   // 1 (rk_step > 0): apply the deferred del4 to tend_u_euler first, store it
 };
 
 enum EntityKind { KC = 0, KE = 1, KV = 2 };  // DevState::lo index
@@ -211,7 +215,7 @@ hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double
 // (mode 2) beside its solve_diagnostics vertex / cell kernel; the stage's solve_diagnostics
 // edge kernel beside the next stage's dyn_tend A (and stage 1's vert_imp after stage 0)
 hipError_t launch_hf_acoustic_solve_vc(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
-                                       double coef_prev);
+                                       double coef_prev, int wold = 1);
 hipError_t launch_hf_solve_e_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& next, int vi, double dts_vi);
 // ... and stage 0's setup + moist + vert_imp launch (fusesetup) beside stage 0's dyn_tend A
 hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges);
@@ -223,8 +227,10 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
 // ru_p to X_rupB; the caller swaps the buffer pairs after the launch
 // tme: theta_m at the cells of each edge from X_tme (valid: dyn_tend of this stage wrote it)
 // sml: the stage's set_smlstep first (a stage's first substep, mode 1 / 2; option fusesml)
+// wold 0 (mode 1 / 2 only): rtheta_pp_old not stored -- atm_srk3's fused damping reads the div
+// this launch stores instead, so only the step's last substep leaves rtheta_pp_old
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode = 0,
-                           double coef_prev = 0.0, int tme = 0, int sml = 0);
+                           double coef_prev = 0.0, int tme = 0, int sml = 0, int wold = 1);
 // old_zero: only from srk3, right after a stage's first acoustic substep (k_div_damp OLD0)
 hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts, int old_zero = 0);
 // the damping from the div buffer X_dvB (fusedamp: the step's last substep), ru_p in place
