@@ -212,8 +212,10 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // its del4 part (kernel D, skipped there); this kernel applies D's statements to the
 // tend_u_euler it reads -- the same operands in the same order, so the same bits -- and
 // stores the result.  D's tend_u of that call is dead in atm_srk3 (this kernel writes tend_u)
+// (DIN: capped at 128 VGPRs, the 4 waves per SIMD of the plain rk_step > 0 kernel; uncapped
+// the compiler takes 132 and 3 waves: +35 %, profiles/r04)
 template <int LP, bool RK0, bool MD, bool HF, bool DIN = false>
-__global__ __launch_bounds__(256) void k_dyn_B(DevState S, DynK a) {
+__global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -922,8 +924,9 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
+// (rk_step > 0, reference semantics: 4 waves per SIMD, as before E formed wc itself)
 template <int LP, bool RK0, bool SELF, bool MD, bool HF>
-__global__ __launch_bounds__(256) void k_dyn_E(DevState S, DynK a) {
+__global__ __launch_bounds__(256, (!RK0 && !MD) ? 4 : 1) void k_dyn_E(DevState S, DynK a) {
     dyn_E_body<LP, RK0, SELF, MD, HF>(S, a, this_blk());
 }
 // D and E of rk_step 0 in one grid (option "hfuse": neither reads what the other writes)
@@ -941,7 +944,7 @@ static DynK make_dynk(const DevState& S, const DynTendArgs& in) {
     a.rayleigh = in.rayleigh_damp_u;
     a.exact_q = in.exact_q;
     a.tme = in.tme && !S.halo;
-    a.cp = in.cp && !S.halo;
+    a.cp = in.cp;  // (decomposed: owned edges, like the setup copy; ru_save / u_2 then stale on ghosts)
     const double invDt = 1.0 / in.dt;
     const double c_s = kSmagCoef;
     a.cs_l2 = (c_s * kLenDisp) * (c_s * kLenDisp);

@@ -95,7 +95,7 @@ struct mpas_ctx {
     // (x1.2562: -3 %; x1.163842: +0.8 %, the pair runs at the lower occupancy of the two)
     int hfuse = 2;
     int fusesml = 1;    // option "fusesml": each stage's set_smlstep inside its first acoustic launch (with fusedamp)
-    int fusedamp_halo = 0;  // option "fusedamp_halo": fusedamp / fusesml on decomposed meshes too (measured neutral there)
+    int fusedamp_halo = 1;  // option "fusedamp_halo": fusedamp / fusesml on decomposed meshes too
     int tmedge = 0;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values;
                         // measured slower at both sizes)
     int fusecopy = 1;   // option "fusecopy" (with fusesetup): setup's edge copies made by stage 0's dyn_tend
@@ -142,7 +142,8 @@ struct mpas_ctx {
     std::vector<GraphEntry> graphs;
     uint64_t graph_clock = 0;
     int64_t graph_captures = 0, graph_launches = 0;
-    int graph_halo = 0;
+    int graph_halo = 1;  // (a capture that fails on a transport falls back to eager steps: graph_fallbacks)
+    int64_t graph_fallbacks = 0;
     std::vector<std::vector<uint8_t>> seen_stale0;  // start states stepped eagerly once
     // option "trtile": the tiled transport (k_transport.hip) when the mesh allows it; the
     // tiles are rebuilt after a mesh upload or a change of the owned / interior cells.
@@ -743,7 +744,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         });
     }
     // option fusecopy: ru_save / u_2 by stage 0's dyn_tend edge kernel (reads u and ru there)
-    const bool fcopy = c->fusesetup && c->fusecopy && S.physics == 0 && !c->halo;
+    const bool fcopy = c->fusesetup && c->fusecopy && S.physics == 0;
     // option fusedamp (reference semantics): each damping but the step's last is applied by
     // the next acoustic launch (k_acoustic MODE 2), the last from the div the acoustic step
     // stored (launch_div_damping_div); the same bits as the separate task.  Decomposed (option
@@ -973,11 +974,35 @@ void srk3_step(mpas_ctx* c, double dt, int schedule) {
                 srk3(c, dt, schedule);  // eagerly: builds it; the next step captures
                 return;
             }
+            // the transport refused the capture (a communicator that cannot be captured):
+            // eager steps from now on, and the step again eagerly (a real error repeats there)
+            (void)hipGetLastError();
+            h->err.clear();
+            c->graph_halo = 0;
+            c->graph_fallbacks++;
+            srk3(c, dt, schedule);
+            return;
         }
         throw;
     }
-    hipcheck(hipStreamEndCapture(c->stream, &g.graph), "hipStreamEndCapture");
-    hipcheck(hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0), "hipGraphInstantiate");
+    {
+        const hipError_t ee = hipStreamEndCapture(c->stream, &g.graph);
+        hipError_t ei = ee;
+        if (ee == hipSuccess) ei = hipGraphInstantiate(&g.exec, g.graph, nullptr, nullptr, 0);
+        if (h && (ee != hipSuccess || ei != hipSuccess)) {  // (as above: nothing ran)
+            graph_free(g);
+            (void)hipGetLastError();
+            h->stale = g.stale0;
+            h->exchanges = ex0;
+            h->fields_moved = fl0;
+            c->graph_halo = 0;
+            c->graph_fallbacks++;
+            srk3(c, dt, schedule);
+            return;
+        }
+        hipcheck(ee, "hipStreamEndCapture");
+        hipcheck(ei, "hipGraphInstantiate");
+    }
     c->graph_captures++;
     if (h) {
         g.stale1 = h->stale;
@@ -1135,6 +1160,11 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusedamp_halo") == 0) c->fusedamp_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
+        else if (name && std::strcmp(name, "stub_latency_us") == 0) {
+            if (!c->halo || !c->halo->stub || value < 0 || value > 100000)
+                throw Fail{MPAS_EINVAL, "stub_latency_us: a stub-transport context and 0..100000 us"};
+            c->halo->stub_latency_us = (int)value;
+        }
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
         else if (name && std::strcmp(name, "epw") == 0) {
             if (value != 1 && value != 2 && value != 4) throw Fail{MPAS_EINVAL, "epw must be 1, 2 or 4"};
@@ -1244,6 +1274,8 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "hfuse") == 0) *value = c->hfuse;
         else if (name && std::strcmp(name, "hfuse_active") == 0) *value = hfuse_active(c);
         else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
+        else if (name && std::strcmp(name, "graph_fallbacks") == 0) *value = c->graph_fallbacks;
+        else if (name && std::strcmp(name, "stub_latency_us") == 0) *value = c->halo ? c->halo->stub_latency_us : 0;
         else if (name && std::strcmp(name, "halo_state") == 0) {  // hash of the halo bookkeeping (debug)
             uint64_t hsh = 1469598103934665603ull;
             if (c->halo)

@@ -75,6 +75,10 @@ struct Halo {
     RcclComm* rccl = nullptr;
     SockComm* sock = nullptr;
     bool stub = false;  // mpas_halo_stub: pack, a device copy for the wire, unpack
+    // option "stub_latency_us": the stub's wire also waits this long on the device (a one-wave
+    // kernel spinning on the wall clock), standing in for a transport's per-exchange latency
+    int stub_latency_us = 0;
+    int wall_khz = 0;  // hipDeviceAttributeWallClockRate
     std::string err;
     int64_t exchanges = 0, fields_moved = 0;
     // overlap of the exchange with interior compute

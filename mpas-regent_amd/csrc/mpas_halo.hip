@@ -52,6 +52,13 @@ __global__ __launch_bounds__(256) void k_halo_copy(const HaloSeg* seg, int nseg,
     else *f = *b;
 }
 
+// the stub transport's modelled wire latency: one wave spins on the device wall clock
+// (bounded: it leaves after `ticks` whatever happens)
+__global__ __launch_bounds__(64) void k_halo_wait(long long ticks) {
+    const long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
 static int kind_of_field(int f) {
     switch (kFields[f].kind) {
         case K_C3: case K_C3V: return HK_CELL;
@@ -623,6 +630,15 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
         const size_t n = (size_t)std::min(stot, rtot) * S.LP;
         if (n && (e = hipMemcpyAsync(recvbuf, sendbuf, n * sizeof(double), hipMemcpyDeviceToDevice, st)) != hipSuccess)
             return e;
+        if (stub_latency_us > 0) {
+            if (!wall_khz) {
+                int dev = 0;
+                (void)hipGetDevice(&dev);
+                if ((e = hipDeviceGetAttribute(&wall_khz, hipDeviceAttributeWallClockRate, dev)) != hipSuccess) return e;
+            }
+            k_halo_wait<<<1, 64, 0, st>>>((long long)stub_latency_us * wall_khz / 1000);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
     } else if (loop) {
         if ((e = hipEventRecord(loop->packed[rank], st)) != hipSuccess) return e;
         if (!loop->barrier(120.0)) {

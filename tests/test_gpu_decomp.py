@@ -329,3 +329,61 @@ def test_stub_graph_start_states(x1_2562, between):
     assert not bad, bad[:6]
     assert out[1][1] == out[0][1]
     assert out[1][2] >= 1 and out[1][3] >= 2 and out[0][2] == 0
+
+
+def test_rccl_graph_capture_single_rank(x1_2562):
+    """graph_halo (default on) with the RCCL transport: a 1-rank communicator's grouped
+    send / recv captured into the step's graph and replayed; bit-identical to eager steps,
+    no fallback to eager (graph_fallbacks), the same exchange counts"""
+    st = state(x1_2562, 56, "random")
+    d = decomp.Decomposition(st, 1)
+    out = {}
+    for graph in (1, 0):
+        got = d.local_state(0)
+        with lib.Context(*d.n_local(0), st.L) as ctx:
+            lib.setup_subdomain(ctx, d, 0)
+            ctx.upload(got)
+            lib.halo_rccl(ctx, 1, 0, lib.rccl_unique_id())
+            assert ctx.get_option("graph_halo") == 1
+            ctx.set_option("graph_halo", graph)
+            for _ in range(5):
+                T.atm_srk3(ctx, 720.0, 1)
+            ctx.sync()
+            ctx.download(got)
+            out[graph] = (got, lib.halo_stats(ctx), ctx.get_option("graph_captures"),
+                          ctx.get_option("graph_fallbacks"))
+    bad = compare_states(out[1][0], out[0][0], rtol=0.0)
+    assert not bad, bad[:6]
+    assert out[1][1] == out[0][1]
+    assert out[1][2] >= 1 and out[1][3] == 0, out[1][2:]
+
+
+def test_stub_latency_option(x1_2562):
+    """option stub_latency_us (tools/rank_sim.py --latency-us): the stub's wire waits on the
+    device; the values are unchanged and the step takes longer by about the waits"""
+    import time
+    st = state(x1_2562, 5, "random")
+    d = decomp.Decomposition(st, 2)
+    res = {}
+    for lat in (0, 2000):
+        loc = d.local_state(0)
+        with lib.Context(*d.n_local(0), st.L) as ctx:
+            lib.setup_subdomain(ctx, d, 0)
+            lib.halo_stub(ctx)
+            ctx.set_option("overlap", 0)
+            ctx.set_option("graph_halo", 0)
+            ctx.set_option("stub_latency_us", lat)
+            assert ctx.get_option("stub_latency_us") == lat
+            ctx.upload(loc)
+            T.atm_srk3(ctx, 720.0, 1)
+            ctx.sync()
+            t = time.perf_counter()
+            T.atm_srk3(ctx, 720.0, 1)
+            ctx.sync()
+            res[lat] = (time.perf_counter() - t, lib.halo_stats(ctx)[0])
+            ctx.download(loc)
+            res[lat] += (loc,)
+    n_ex = res[0][1] / 2
+    assert res[2000][0] - res[0][0] > 0.5 * n_ex * 2e-3, (res[0][:2], res[2000][:2])
+    bad = compare_states(res[2000][2], res[0][2], rtol=0.0)
+    assert not bad, bad[:6]

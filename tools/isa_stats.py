@@ -26,7 +26,7 @@ def stats(src):
         end = s.index(".Lfunc_end", m.end())
         body = s[m.end():end]
         c = lambda p: len(re.findall(p, body))
-        short = re.sub(r"^_ZN4mpas\d+", "", name).split("ILi")[0] + (name.split("ILi64E")[1][:12] if os.environ.get("ISA_FULL") else "")
+        short = re.sub(r"^_ZN4mpas\d+", "", name).split("ILi")[0] + (name.split("ILi64E")[1][:int(os.environ.get("ISA_FULL", "12")) if os.environ.get("ISA_FULL", "").isdigit() else 12] if os.environ.get("ISA_FULL") else "")
         v = int(meta.get(name, 0))
         print("%-14s vgpr %3d vload %3d sload %3d vstore %3d vmcnt0 %3d execz %3d valu %4d addr64 %3d f64 %4d insts %5d" % (
             short, v, c(r"global_load|buffer_load"), c(r"s_load"), c(r"global_store"), c(r"vmcnt\(0\)"),
