@@ -565,8 +565,8 @@ def main():
             "note": "achieved = B_alg per step / device time per step of the task (launch-weighted average of its "
                     "rk_step 0 and rk_step > 0 launches); frac = achieved / peak"}
     fused = bool(ctx.get_option("fusedamp_active"))
-    fsetup = bool(ctx.get_option("fusesetup")) and not args.physics
-    fsml = fused and bool(ctx.get_option("fusesml"))
+    fsetup = bool(ctx.get_option("fusesetup"))
+    fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
     fcopy = fsetup and bool(ctx.get_option("fusecopy")) and not decomposed
     d4 = bool(ctx.get_option("defer4")) and not args.physics
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4)

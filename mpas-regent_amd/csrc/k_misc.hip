@@ -159,18 +159,26 @@ hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st) {
 // loads and qtot / cqw as moist has just set them, so those four columns are read once.
 // Edge blocks (ncb..) copy ru and u (none with option "fusecopy": dyn_tend's edge kernel
 // makes those copies).  The same values as the three launches.
-template <int LP>
-__global__ __launch_bounds__(256) void k_setup_vi(DevState S, int ncb, double dtseps, double rcv, double c2) {
-    setup_vi_body<LP>(S, ncb, dtseps, rcv, c2, this_blk());
+// MPAS vertical solver / dynamics (physics 1 / 2): the same fusion with vert_imp's MPAS form,
+// and under the MPAS dynamics setup's theta_m_save and moist's cqu (edge blocks) too
+template <int LP, bool MPASV = false, bool MD = false>
+__global__ __launch_bounds__(256) void k_setup_vi(DevState S, int ncb, double dtseps, double rcv, double c2, int copies) {
+    setup_vi_body<LP, MPASV, MD>(S, ncb, dtseps, rcv, c2, this_blk(), copies);
 }
 template <int LP>
 static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts, bool edges) {
-    if (S.physics) return hipErrorInvalidValue;  // (srk3 asks in the reference semantics only)
     double dtseps = .5 * dts * (1.0 + kEpssm);
     double rcv = kRgas / (kCp - kRgas);
     double c2 = kCp * rcv;
-    const int ncb = col_blocks<LP>(S, KC), neb = edges ? col_blocks<LP>(S, KE) : 0;
-    if (ncb + neb) k_setup_vi<LP><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2);
+    const bool md = S.physics == 2;
+    const int ncb = col_blocks<LP>(S, KC), neb = (edges || md) ? col_blocks<LP>(S, KE) : 0;
+    const int cp = edges ? 1 : 0;
+    if (ncb + neb) {
+        if (md) k_setup_vi<LP, true, true><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2, cp);
+        else if (S.physics) k_setup_vi<LP, true, false><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2, cp);
+        else k_setup_vi<LP><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2, cp);
+    }
+    if (md) HALO_WROTE(S, F_theta_m_save, F_cqu);
     if (edges) HALO_WROTE(S, F_ru_save, F_u_2);
     HALO_WROTE(S, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2, F_rho_zz_old_split, F_qtot,
                F_cqw);

@@ -796,7 +796,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             return launch_hf_setup_dyn_A(S, st, stage_args(0), rk_sub_timestep[0], fcopy ? 0 : 1);
         });
         a_done = true;
-    } else if (c->fusesetup && S.physics == 0) {  // :404-417 as one column-local launch (same values)
+    } else if (c->fusesetup) {  // :404-417 as one column-local launch (same values; MPAS forms under physics)
         run_task(c, fcopy ? "atm_rk_integration_setup[cells+moist+vert_imp]" : "atm_rk_integration_setup[+moist+vert_imp]",
                  [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0], !fcopy); });
     } else {

@@ -37,8 +37,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             ws += w
         return rs, ws
     if task == "atm_rk_integration_setup" and fused:  # option fusesetup: + moist + vert_imp, one launch
-        parts = [_sets(t) for t in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
-                                    "atm_compute_vert_imp_coefs")]
+        parts = [_sets(t, physics=physics) for t in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
+                                                     "atm_compute_vert_imp_coefs")]
         writes = sorted(set(w for _, ws in parts for w in ws))
         reads = sorted(set(r for rs, _ in parts for r in rs) - set(writes) | {"gamma_tri"})
         if copy:  # option fusecopy: the edge copies ru_save = ru, u_2 = u moved to dyn_tend
@@ -117,7 +117,7 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             reads += ["rtheta_pp", "rtheta_pp_old", "isShared", "specZoneMaskEdge"]
             writes += ["ru_p"]
         if sml:  # option fusesml: the stage's atm_set_smlstep_pert_variables_work first
-            r2, w2 = _sets("atm_set_smlstep_pert_variables_work")
+            r2, w2 = _sets("atm_set_smlstep_pert_variables_work", physics=physics)
             reads += r2
             writes += w2
         return reads, writes
@@ -208,8 +208,11 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     launch; fusecopy (with fusesetup): setup's edge copies in stage 0's dyn_tend"""
     if physics:
         p = {"physics": physics}
-        out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
-               ("atm_compute_vert_imp_coefs", {}, 2)]
+        if fusesetup:  # stage 0's setup + moist + vert_imp in one launch (MPAS forms)
+            out = [("atm_rk_integration_setup", {"fused": True, **p}, 1), ("atm_compute_vert_imp_coefs", {}, 1)]
+        else:
+            out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
+                   ("atm_compute_vert_imp_coefs", {}, 2)]
         if schedule == 1:
             out += [("atm_compute_dyn_tend_work", {"rk_step": 0, **p}, 1),
                     ("atm_compute_dyn_tend_work", {"rk_step": 1, **p}, 2)]

@@ -217,3 +217,30 @@ def test_srk3_level_extremes(x1_2562, L, physics):
             ctx.download(got)
         bad = compare_states(got, ref, rtol=tol, tol_fields=tf, zero_slot_excluded=ZERO_SLOT_WRITTEN)
         assert not bad, f"L={L} physics={physics} exact={exact}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("physics", [1, 2])
+@pytest.mark.parametrize("L", [5, 56])
+def test_mpas_fusesetup_bit_identical(x1_2562, physics, L):
+    """atm_srk3 under the MPAS solver / dynamics with option fusesetup (setup + moist + vert_imp
+    of stage 0 in one launch, with the MPAS forms: vert_imp's LU, theta_m_save and cqu by the
+    edge blocks) equals the separate launches bit for bit, in the exact and the fast path, with
+    the transport under physics 1"""
+    st = state(x1_2562, L, "mpas0")
+    for exact in (1, 0):
+        out = {}
+        for fused in (1, 0):
+            got = st.copy()
+            with lib.Context(*st.dims()) as ctx:
+                ctx.set_option("exact", exact)
+                ctx.set_option("physics", physics)
+                ctx.set_option("transport", 1 if physics == 1 else 0)
+                ctx.set_option("fusesetup", fused)
+                ctx.upload(st)
+                for _ in range(3):
+                    T.atm_srk3(ctx, 720.0, 1)
+                ctx.sync()
+                ctx.download(got)
+            out[fused] = got
+        bad = compare_states(out[1], out[0], rtol=0.0)
+        assert not bad, f"exact={exact}: {bad[:6]}"
