@@ -319,6 +319,8 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_advance_acoustic_step_work[ss0+sml]": {"small_step": 0, "sml": True},
              "atm_compute_solve_diagnostics[vc]": {"part": "vc"}, "atm_compute_solve_diagnostics[e]": {"part": "e"},
              "hfuse[damp+solve_vc]": {"pair": "damp+solve_vc"}, "hfuse[solve_e+finish]": {"pair": "solve_e+finish"},
+             "hfuse[solve_e-v+finish]": {"pair": "solve_e-v+finish"},
+             "atm_compute_solve_diagnostics[e-v]": {"part": "e"}, "atm_compute_solve_diagnostics[-v]": {},
              "hfuse[solve_e+vert_imp]": {"pair": "solve_e+vert_imp"},
              "hfuse[acoustic+solve_vc]": {"pair": "acoustic+solve_vc"},
              "hfuse[solve_e+dyn_A]": {"pair": "solve_e+dyn_A"},
@@ -339,6 +341,8 @@ def task_table(rep, work_dims, n_prof, physics):
             kw["copy"] = True
         if "+d4o" in tag:
             kw["defer_out"] = True
+        if "+v" in tag:
+            kw["store_v"] = True
         if tag.endswith("-A"):
             kw["noA"] = True
         return kw

@@ -66,20 +66,29 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * computes interior entities beside the halo exchange of a decomposed mesh; "self" = 0
  * disables the SELF gathers; "graph" = 1 (default) makes mpas_atm_srk3 capture its step once
  * per (dt, schedule) as a HIP graph and replay it (any option change or mesh upload
- * re-captures; per-task timing and decomposed contexts run the launches directly; read-only
- * "graph_captures" / "graph_launches" count them).  All but "exact" and "physics" change
- * only speed, never results.
- * Cross-task fusion in mpas_atm_srk3 (reference semantics, undecomposed):
+ * re-captures; per-task timing runs the launches directly; read-only "graph_captures" /
+ * "graph_launches" count them).  "graph_halo" = 1 (default) does the same on a decomposed
+ * context with the RCCL or stub transport: a step is captured per halo state at its start
+ * (a start state met twice; up to 4 kept), and a capture the transport refuses falls back to
+ * eager steps (read-only "graph_fallbacks").  "stub_latency_us" (stub transport only) adds a
+ * device-side wait of that many microseconds to every exchange (tools/rank_sim.py).  All but
+ * "exact" and "physics" change only speed, never results.
+ * Cross-task fusion in mpas_atm_srk3 (reference semantics):
  * "fusedamp" = 1 (default) applies each divergence damping inside the next acoustic launch
  * (read-only "fusedamp_active"); "fusesml" = 1 (default, with fusedamp) runs each stage's
  * set_smlstep inside its first acoustic launch; "fusesetup" = 1 (default) runs setup, moist
  * and stage 0's vert_imp as one launch; "fusecopy" = 1 (default, with fusesetup) makes
- * setup's edge copies in stage 0's dyn_tend edge kernel; "tmedge" = 1 (default 0) has
+ * setup's edge copies in stage 0's dyn_tend edge kernel (decomposed contexts too); "defer4" = 1
+ * (default) applies rk_step 0's del4 of tend_u_euler (dyn_tend kernel D) in the next stage's
+ * rk_step > 0 edge kernel; "vdyn" = 1 (default) has the last stage's dyn_tend edge kernel store
+ * solve_diagnostics' v from the u it gathers (when edgesOnEdge_ECP = edgesOnEdge, read-only
+ * "eoe_same"); "tmedge" = 1 (default 0) has
  * dyn_tend store theta_m(cell1) + theta_m(cell2) per edge for the acoustic substeps;
  * "hfuse" = 1 puts independent neighbouring kernels in one launch, 2 (default) only below
- * 16384 owned cells (read-only "hfuse_active"). "fusedamp_halo" = 1 (default 0: measured neutral at
- * one rank of an 8-way x1.163842 split) applies fusedamp and fusesml on decomposed meshes
- * too (with "ring1"): the div is exchanged where rtheta_pp was.
+ * 16384 owned cells, undecomposed (read-only "hfuse_active"). "fusedamp_halo" = 1 (default)
+ * applies fusedamp and fusesml on decomposed meshes too (with "ring1"): the div is exchanged
+ * where rtheta_pp was.  Under "physics" >= 1 "fusesetup" runs setup, moist and stage 0's
+ * vert_imp in their MPAS forms as one launch.
  * "physics" = 1 selects the MPAS vertical solver: vert_imp with Q16/Q17
  * fixed, the acoustic step with the ru_p update (Q18), the MPAS statement order (Q19/Q20)
  * and the tridiagonal back substitution (Q21), tend_rt = tend_theta (Q8), recover_large_step

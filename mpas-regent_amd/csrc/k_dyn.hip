@@ -50,7 +50,7 @@ __device__ __forceinline__ double flux3(double q_im2, double q_im1, double q_i, 
 }
 
 struct DynK {
-    int rk_step, horiz_mixing, rayleigh, exact_q, tme, cp, d4o;
+    int rk_step, horiz_mixing, rayleigh, exact_q, tme, cp, d4o, vB;
     double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
     double h4d;  // DIN: the h4 of the rk_step 0 call whose del4 of tend_u_euler this call applies
 };
@@ -389,6 +389,13 @@ __global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) 
         }
     }
     tend_u += rho_edge * (q - (ke2 - ke1) * invDc) - u * 0.5 * (hd1 + hd2);
+    if (a.vB) {  // solve_diagnostics' v (:429-437; Q23: from i = 1) from the same u columns
+        double vv = 0.0;
+#pragma unroll
+        for (int j = 1; j < QF; j++) vv = add_if(j < neoe, vv, woe_[j] * ue_[j]);
+        for (int j = QF; j < neoe; j++) vv += woe[j] * colk(u_f, eoe[j]);
+        if (k != L) colk(fw(S, F_v), e) = PADW(vv);
+    }
     {  // curvature (:1011-1017, Q12 literal)
         const double cosA = fd(S, X_cosAngleEdge)[e], cosL = fd(S, X_cosLatEdge)[e];
         const double cA = (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p));
@@ -956,6 +963,7 @@ static DynK make_dynk(const DevState& S, const DynTendArgs& in) {
     a.rayleigh_inv = 1.0 / ((double)kRayleighLevels * (kRayleighDays * kSecondsPerDay));
     a.prandtl_inv = 1.0 / kPrandtl;
     a.d4o = (in.defer_out && in.rk_step == 0 && a.h4 > 0.0) ? 1 : 0;
+    a.vB = (in.store_v && S.eoe_same && S.physics != 2) ? 1 : 0;
     a.h4d = (in.defer_in && in.rk_step != 0 && in.horiz_mixing == 0) ? kVisc4_2dsmag * (kLenDisp * kLenDisp * kLenDisp) : 0.0;
     return a;
 }
@@ -1073,6 +1081,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         else HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m);
         HALO_WROTE(S, X_F, F_tend_u);
         if (din) HALO_WROTE(S, F_tend_u_euler);
+        if (a.vB) HALO_WROTE(S, F_v);
         if (MD) HALO_WROTE(S, X_Fw);
         if (hf) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw);  // (ru: wc at the cell's last edge, reference semantics)
         else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);

@@ -442,6 +442,8 @@ __global__ __launch_bounds__(256) void k_prepare(DevState S, int* selfc) {
         else if (j == 22) v = fi(S, F_nAdvCellsForEdge)[e];
         ((int*)S.f[X_eB])[t] = v;
     }
+    for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < (size_t)S.nEO * 20; t += (size_t)gridDim.x * 256)
+        if (fi(S, F_edgesOnEdge)[t] != fi(S, F_edgesOnEdge_ECP)[t]) atomicAnd(selfc + 2, 0);
     for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < n; t += (size_t)gridDim.x * 256) {
         const int e = eoc[t], c = (int)(t / 10), i = (int)(t % 10);
         const int c1 = coe[(size_t)e * 2], c2 = coe[(size_t)e * 2 + 1];
@@ -519,11 +521,11 @@ __global__ __launch_bounds__(256) void k_own_bits(DevState S, int* norph) {
 
 // derived mesh arrays; decides S.selfc (synchronous: runs once after each mesh upload)
 hipError_t launch_prepare(DevState& S, hipStream_t st) {
-    int* flag = nullptr;  // [0] selfc, [1] orphan edges
-    hipError_t e = hipMalloc(&flag, 2 * sizeof(int));
+    int* flag = nullptr;  // [0] selfc, [1] orphan edges, [2] eoe_same
+    hipError_t e = hipMalloc(&flag, 3 * sizeof(int));
     if (e != hipSuccess) return e;
-    const int init[2] = {1, 0};
-    int host[2] = {0, 0};
+    const int init[3] = {1, 0, 1};
+    int host[3] = {0, 0, 0};
     e = hipMemcpyAsync(flag, init, sizeof(init), hipMemcpyHostToDevice, st);
     if (e == hipSuccess) {
         k_prepare<<<stream_grid((size_t)S.nCells * 10), 256, 0, st>>>(S, flag);
@@ -539,6 +541,7 @@ hipError_t launch_prepare(DevState& S, hipStream_t st) {
     if (e == hipSuccess) {
         S.selfc = host[0];
         S.n_orph = host[1];
+        S.eoe_same = host[2];
     }
     return e;
 }

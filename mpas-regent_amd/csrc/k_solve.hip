@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
 }
 
 template <int LP, bool MD>
-static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts) {
+static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts, int no_v) {
     auto kvc = [&](const DevState& X) {  // vertex blocks, then cell blocks
         if (X.epw == 4) {
             const int nv = col_blocks_n<LP, 4>(X, KV), nb = nv + col_blocks_n<LP, 4>(X, KC);
@@ -64,7 +64,7 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
         if (nb) k_solve_holl<LP><<<nb, 256, 0, st>>>(X);
     };
     auto ke = [&](const DevState& X) {
-        const bool rv = !(rk_step != -1 && rk_step != 2);
+        const bool rv = !(rk_step != -1 && rk_step != 2) && !no_v;
         auto go = [&](auto epw) {
             constexpr int E = decltype(epw)::value;
             const int nb = col_blocks_n<LP, E>(X, KE);
@@ -104,17 +104,19 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
         HALO_WROTE(S, F_h_edge, F_rho_edge, F_ke_edge, F_v, F_pv_edge);
     } else {
         HALO_RUN_R1(S, st, ke, F_pv_vertex, F_h, F_u, F_pv_vertex);
-        HALO_WROTE(S, F_h_edge, F_ke_edge, F_v, F_pv_edge);
+        HALO_WROTE(S, F_h_edge, F_ke_edge, F_pv_edge);
+        if (!no_v && (rk_step == -1 || rk_step == 2)) HALO_WROTE(S, F_v);
     }
     return hipGetLastError();
 }
 template <int LP>
-static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts) {
-    return S.physics == 2 ? solve_lp_md<LP, true>(S, st, hollingsworth, rk_step, parts)
-                          : solve_lp_md<LP, false>(S, st, hollingsworth, rk_step, parts);
+static hipError_t solve_lp(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts, int no_v) {
+    return S.physics == 2 ? solve_lp_md<LP, true>(S, st, hollingsworth, rk_step, parts, no_v)
+                          : solve_lp_md<LP, false>(S, st, hollingsworth, rk_step, parts, no_v);
 }
-hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts) {
-    MPAS_LP_DISPATCH(S.LP, solve_lp, S, st, hollingsworth, rk_step, parts);
+hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts,
+                                    int no_v) {
+    MPAS_LP_DISPATCH(S.LP, solve_lp, S, st, hollingsworth, rk_step, parts, no_v);
 }
 
 // ---------------------------------------------------------------- combined launches
@@ -132,12 +134,12 @@ __global__ __launch_bounds__(256) void k_hf_damp_vc(DevState S, double coef, int
     if (b < nb1) divdamp_body<LP, 2, false, true, TME>(S, coef, Blk{b, nb1});
     else solve_vc_body<LP, EPW, false>(S, nVB, 0, Blk{b - nb1, (int)gridDim.x - nb1});
 }
-template <int EPW>
+template <int EPW, bool RV>
 __global__ __launch_bounds__(256) void k_hf_e_finish(DevState S, int nb1, int gx, int substep, int split, double inv,
                                                      Pair64 q) {
     const int b = (int)blockIdx.x;
     if (b < nb1) {
-        solve_e_body<64, true, false, EPW>(S, Blk{b, nb1});
+        solve_e_body<64, RV, false, EPW>(S, Blk{b, nb1});
     } else {
         const int r = b - nb1;
         const bool cells = r >= gx;
@@ -176,14 +178,15 @@ static hipError_t hf_damp_vc_lp(const DevState& S, hipStream_t st, double dts, i
 hipError_t launch_hf_damp_solve_vc(const DevState& S, hipStream_t st, double dts, int tme) {
     MPAS_LP_DISPATCH(S.LP, hf_damp_vc_lp, S, st, dts, tme);
 }
-hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st) {
+hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st, int recon_v) {
     if (!hf_ok(S) || S.LP != 64) return hipErrorInvalidValue;
     const int gx = (stream_grid_((size_t)S.nEO * 32) + 3) / 4;
     hipError_t e = hipSuccess;
     epw_go<64>(S, [&](auto epw) {
         constexpr int E = decltype(epw)::value;
         const int nb1 = col_blocks_n<64, E>(S, KE);
-        k_hf_e_finish<E><<<nb1 + 2 * gx, 256, 0, st>>>(S, nb1, gx, 1, 1, 1.0, Pair64(S.L));
+        if (recon_v) k_hf_e_finish<E, true><<<nb1 + 2 * gx, 256, 0, st>>>(S, nb1, gx, 1, 1, 1.0, Pair64(S.L));
+        else k_hf_e_finish<E, false><<<nb1 + 2 * gx, 256, 0, st>>>(S, nb1, gx, 1, 1, 1.0, Pair64(S.L));
     });
     return e == hipSuccess ? hipGetLastError() : e;
 }

@@ -101,6 +101,8 @@ struct mpas_ctx {
     int fusecopy = 1;   // option "fusecopy" (with fusesetup): setup's edge copies made by stage 0's dyn_tend
                         // edge kernel from the columns it loads anyway (same values)
     int fusesetup = 1;  // option "fusesetup": stage 0's setup, moist and vert_imp in one launch (same values)
+    int vdyn = 1;      // option "vdyn": atm_srk3's stage 2 dyn_tend edge kernel stores solve_diagnostics' v
+                       // (reference semantics, edgesOnEdge_ECP = edgesOnEdge; same values)
     int defer4 = 1;    // option "defer4": atm_srk3 applies rk_step 0's del4 of tend_u_euler (dyn_tend D) in the
                        // next stage's rk_step > 0 edge kernel (reference semantics; same values)
     int fusedamp = 1;  // option "fusedamp": atm_srk3 applies each divergence damping inside the next
@@ -768,7 +770,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // beside its solve_diagnostics vertex / cell kernel, and the stage's edge kernel beside
     // the next stage's dyn_tend A (k_acoustic.hip / k_dyn.hip combined launches)
     const bool hf2 = hf && fuse && !tme && S.epw == 2;
-    bool vc_done = false, a_done = false;
+    bool vc_done = false, a_done = false, vdyn_on = false;
     auto stage_args = [&](int r) {
         DynTendArgs a{};
         a.rk_step = schedule == 0 ? (int)rk_sub_timestep[r] : r;  // Q4
@@ -809,11 +811,16 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
         DynTendArgs a = stage_args(rk_step);
         a.skipA = a_done ? 1 : 0;
+        // option vdyn (reference semantics): the last stage's v (:429-437) is reconstructed by its
+        // dyn_tend edge kernel from the edgesOnEdge u it gathers for q -- u is not written between
+        // that kernel and the stage's solve_diagnostics, which then skips v
+        if (rk_step == 2) vdyn_on = c->vdyn && S.physics == 0 && a.rk_step > 0 && S.eoe_same;
+        a.store_v = (rk_step == 2 && vdyn_on) ? 1 : 0;
         a_done = false;
         // timing key: the variant's read / write set (bench.py parses the tags)
         const std::string dname = std::string("atm_compute_dyn_tend_work[") + (a.rk_step == 0 ? "rk0" : "rk>0") +
                                   (a.cp ? "+copy" : "") + (a.defer_out ? "+d4o" : "") + (a.defer_in ? "+d4i" : "") +
-                                  (a.skipA ? "-A" : "") + "]";
+                                  (a.store_v ? "+v" : "") + (a.skipA ? "-A" : "") + "]";
         run_task(c, dname.c_str(), [&] { return launch_dyn_tend(S, st, a); });
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
         const bool sml = fuse && c->fusesml;
@@ -860,9 +867,11 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         if (hf && fuse && rk_step == 2 && S.LP == 64 && !c->transport) {
             // (the vertex / cell kernel ran beside the last damping) the edge kernel beside
             // atm_rk_dynamics_substep_finish, which follows below
-            run_task(c, "hfuse[solve_e+finish]", [&] { return launch_hf_solve_e_finish(S, st); });
+            run_task(c, vdyn_on ? "hfuse[solve_e-v+finish]" : "hfuse[solve_e+finish]",
+                     [&] { return launch_hf_solve_e_finish(S, st, vdyn_on ? 0 : 1); });
         } else if (hf && fuse && rk_step == 2) {
-            run_task(c, "atm_compute_solve_diagnostics[e]", [&] { return launch_solve_diagnostics(S, st, 0, 2, 2); });
+            run_task(c, vdyn_on ? "atm_compute_solve_diagnostics[e-v]" : "atm_compute_solve_diagnostics[e]",
+                     [&] { return launch_solve_diagnostics(S, st, 0, 2, 2, vdyn_on ? 1 : 0); });
         } else if (hf2 && vc_done && rk_step < 2) {
             // (the vertex / cell kernel ran beside the last acoustic launch) the edge kernel
             // beside the next stage's dyn_tend A, and after stage 0 beside stage 1's vert_imp
@@ -879,7 +888,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                      [&] { return launch_hf_solve_e_vert_imp(S, st, rk_sub_timestep[1]); });
             vi_done = true;
         } else {
-            run_task(c, "atm_compute_solve_diagnostics", [&] { return launch_solve_diagnostics(S, st, 0, rk_step); });
+            const int nv = (rk_step == 2 && vdyn_on) ? 1 : 0;
+            run_task(c, nv ? "atm_compute_solve_diagnostics[-v]" : "atm_compute_solve_diagnostics",
+                     [&] { return launch_solve_diagnostics(S, st, 0, rk_step, 3, nv); });
         }
     }
     if (c->transport)  // after the last stage's recover: ruAvg / wwAvg / rho_zz of the step
@@ -1155,6 +1166,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusecopy") == 0) c->fusecopy = value ? 1 : 0;
         else if (name && std::strcmp(name, "defer4") == 0) c->defer4 = value ? 1 : 0;
+        else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp_halo") == 0) c->fusedamp_halo = value ? 1 : 0;
@@ -1268,6 +1280,11 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) *value = c->fusesetup;
         else if (name && std::strcmp(name, "fusecopy") == 0) *value = c->fusecopy;
         else if (name && std::strcmp(name, "defer4") == 0) *value = c->defer4;
+        else if (name && std::strcmp(name, "vdyn") == 0) *value = c->vdyn;
+        else if (name && std::strcmp(name, "eoe_same") == 0) {
+            prepare_now(c);
+            *value = c->S.eoe_same;
+        }
         else if (name && std::strcmp(name, "tmedge") == 0) *value = c->tmedge;
         else if (name && std::strcmp(name, "fusesml") == 0) *value = c->fusesml;
         else if (name && std::strcmp(name, "fusedamp_halo") == 0) *value = c->fusedamp_halo;

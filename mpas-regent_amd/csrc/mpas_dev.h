@@ -138,6 +138,8 @@ struct DevState {
                   // set_smlstep, setup, moist, finish in MPAS-A's forms: mpas_oracle.c ora_mpas_*)
     int xcd;  // block order: 0 dispatcher, 1 one contiguous eighth per XCD, G > 1 runs of G
               // blocks per XCD in windows of 8G (default 64)
+    int eoe_same;  // 1 when edgesOnEdge_ECP equals edgesOnEdge on the owned edges (k_prepare; as
+                   // mesh_loading.rg:275 sets it): v's and q's gathers are the same columns
     int selfc;  // 1 when every cell is one of the two cellsOnEdge of each of its first
                 // min(nEdgesOnCell, NF) edges (k_prepare): the cell kernels then gather
                 // only the other cell of an edge and use their own column for the cell
@@ -186,6 +188,9 @@ struct DynTendArgs {
     // is applied by the next stage's rk_step > 0 edge kernel, which reads tend_u_euler anyway
     int defer_out = 0;  // 1 (rk_step 0): no D; tend_u_euler left without its del4 part, tend_u not stored
     int defer_in = 0;   // 1 (rk_step > 0): apply the deferred del4 to tend_u_euler first, store it
+    // option "vdyn" (atm_srk3 stage 2, reference semantics): the edge kernel also stores
+    // solve_diagnostics' v (:429-437, Q23) from the edgesOnEdge u it gathers (S.eoe_same)
+    int store_v = 0;
 };
 
 enum EntityKind { KC = 0, KE = 1, KV = 2 };  // DevState::lo index
@@ -239,10 +244,13 @@ hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts,
 double divdamp_coef(double dts);
 // combined launches of independent neighbours (option "hfuse", k_solve.hip)
 hipError_t launch_hf_damp_solve_vc(const DevState& S, hipStream_t st, double dts, int tme);
-hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st);
+hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st, int recon_v = 1);
 hipError_t launch_hf_solve_e_vert_imp(const DevState& S, hipStream_t st, double dts);
 // parts: 1 the vertex / cell kernel, 2 the edge kernel, 3 both (the task)
-hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts = 3);
+// no_v: v (rk_step -1 / 2) is not reconstructed here (atm_srk3 option "vdyn": stage 2's dyn_tend
+// edge kernel has stored it from the same u)
+hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts = 3,
+                                    int no_v = 0);
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
 hipError_t launch_prepare(DevState& S, hipStream_t st);

@@ -15,7 +15,7 @@ roofline.achieved divides by the measured launch time.
 
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
-          part=None, pair=None, copy=False, noA=False, defer_out=False):
+          part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -23,6 +23,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         parts = {"damp+solve_vc": (("atm_divergence_damping_3d", {}), ("atm_compute_solve_diagnostics", {"part": "vc"})),
                  "solve_e+finish": (("atm_compute_solve_diagnostics", {"part": "e", "reconstruct_v": True}),
                                     ("atm_rk_dynamics_substep_finish", {})),
+                 "solve_e-v+finish": (("atm_compute_solve_diagnostics", {"part": "e"}),
+                                      ("atm_rk_dynamics_substep_finish", {})),
                  "solve_e+vert_imp": (e, vi),
                  "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}),
                                        ("atm_compute_solve_diagnostics", {"part": "vc"})),
@@ -63,7 +65,7 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                     ["h_divergence", "kdiff", "tend_rho", "dpdz"])
         return reads, ["h_divergence"]
     if task == "atm_compute_dyn_tend_work" and noA:  # the rest after A ran in a combined launch
-        r, w = _sets(task, rk_step=rk_step, physics=physics, copy=copy, defer_out=defer_out)
+        r, w = _sets(task, rk_step=rk_step, physics=physics, copy=copy, defer_out=defer_out, store_v=store_v)
         ra, wa = _sets(task, rk_step=rk_step, part="A")
         return ([x for x in r if x not in ("uReconstructZonal", "uReconstructMeridional")] + wa,
                 [x for x in w if x not in wa])
@@ -92,6 +94,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             reads += ["uReconstructZonal", "uReconstructMeridional", "w"]
         if copy:  # option fusecopy (stage 0): setup's ru_save = ru, u_2 = u (ru, u already read)
             writes = writes + ["ru_save", "u_2"]
+        if store_v:  # option vdyn (stage 2): solve_diagnostics' v from the gathered edgesOnEdge u
+            writes = writes + ["v"]
         if defer_out and rk_step == 0:  # option defer4: tend_u of this call is dead and not stored
             writes = [x for x in writes if x != "tend_u"]  # (its del4 runs in the next call: no credit taken)
         return reads + mesh, writes

@@ -432,7 +432,7 @@ def test_upload_rejects_overlong_lists(x1_2562, field, width):
 
 # ---- option fusedamp: the damping inside the next acoustic launch ------------------------
 def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None, tmedge=None, fusesml=None, hfuse=None,
-                   fusecopy=None, defer4=None):
+                   fusecopy=None, defer4=None, vdyn=None):
     got = st.copy()
     with lib.Context(*st.dims()) as ctx:
         ctx.set_option("exact", exact)
@@ -443,6 +443,7 @@ def _two_steps_gpu(st, fusedamp, exact, graph=1, fusesetup=None, tmedge=None, fu
         ctx.set_option("tmedge", fusedamp if tmedge is None else tmedge)
         ctx.set_option("fusecopy", fusedamp if fusecopy is None else fusecopy)
         ctx.set_option("defer4", fusedamp if defer4 is None else defer4)
+        ctx.set_option("vdyn", fusedamp if vdyn is None else vdyn)
         ctx.set_option("graph", graph)
         ctx.upload(st)
         assert ctx.get_option("fusedamp_active") == fusedamp
@@ -463,7 +464,8 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
     and vert_imp in one launch (k_setup_vi), each stage's set_smlstep inside its first
     acoustic launch (option fusesml), setup's edge copies made by stage 0's dyn_tend edge
     kernel (option fusecopy; stage 0 runs rk_step > 0 kernels under schedule 0, which read
-    ru_save), rk_step 0's dyn_tend D applied by stage 1's edge kernel (option defer4), theta_m(cell2) + theta_m(cell1) per edge taken
+    ru_save), rk_step 0's dyn_tend D applied by stage 1's edge kernel (option defer4), stage 2's v
+    stored by its dyn_tend edge kernel (option vdyn), theta_m(cell2) + theta_m(cell1) per edge taken
     from dyn_tend's edge kernel (option tmedge) and independent neighbouring kernels
     sharing a launch (option hfuse; with fusedamp and without tmedge also a stage's last
     acoustic launch beside its solve_diagnostics vertex / cell kernel and its edge kernel
@@ -501,6 +503,11 @@ def test_fusedamp_bit_identical(x1_2562, L, variant):
             c, _ = _two_steps_gpu(st, 1, ex, 1, fusecopy=fc)
             bad = compare_states(c, b if ex == 0 else ref, rtol=0.0)
             assert not bad, f"fusecopy={fc}, exact={ex}: {bad[:6]}"
+    for vd in (0, 1):  # stage 2's v by its dyn_tend edge kernel (option vdyn), exact and fast
+        for ex in (0, 1):
+            c, _ = _two_steps_gpu(st, 1 - vd, ex, 1, vdyn=vd)
+            bad = compare_states(c, b if ex == 0 else ref, rtol=0.0)
+            assert not bad, f"vdyn={vd}, exact={ex}: {bad[:6]}"
     for d4 in (0, 1):  # rk_step 0's dyn_tend D in stage 1's edge kernel (option defer4), exact and fast
         for ex in (0, 1):
             c, _ = _two_steps_gpu(st, 1 - d4, ex, 1, defer4=d4)
