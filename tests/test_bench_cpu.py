@@ -161,3 +161,28 @@ def test_roofline_fusecopy_moves_the_edge_copies():
     d0 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0)
     d1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True)
     assert s0 - s1 == 4 * e3 and d1 - d0 == 2 * e3
+
+
+def test_roofline_defer4_and_vdyn_accounting():
+    """option defer4: stage 0's dead tend_u store is taken out of that launch's B_alg (no
+    credit for bytes not moved), the receiving launch gets none for what it adds; option
+    vdyn: stage 2's launch is credited the v it stores; bench.py reads the variant tags"""
+    import bench
+    from mpasdyn import roofline
+    dims = (163842, 491520, 327680, 56)
+    e3 = 8 * 491520 * 56
+    d0 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True)
+    d0o = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True, defer_out=True)
+    assert d0 - d0o == e3
+    d1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1)
+    d1v = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1, store_v=True)
+    assert d1v - d1 == e3
+    a = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, False)
+    b = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, True)
+    assert a - b == e3
+    rep = {"atm_compute_dyn_tend_work[rk0+copy+d4o]": (2, 4.4), "atm_compute_dyn_tend_work[rk>0+d4i]": (2, 2.8),
+           "atm_compute_dyn_tend_work[rk>0+v-A]": (2, 2.2)}
+    t = bench.task_table(rep, dims, 2, physics=False)["atm_compute_dyn_tend_work"]
+    na = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1, store_v=True, noA=True)
+    assert abs(t["b_alg_GB_per_step"] - (d0o + d1 + na) / 1e9) < 1e-3
+    assert set(t["variants"]) == {"[rk0+copy+d4o]", "[rk>0+d4i]", "[rk>0+v-A]"}
