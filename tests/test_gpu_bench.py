@@ -74,7 +74,9 @@ def test_bench_roofline_is_dyn_tend_with_live_traffic():
     d = json.loads(p.stdout.strip())
     r = d["roofline"]
     assert r["kernel"] == "atm_compute_dyn_tend_work" and r["launches_per_step"] == 3
-    assert set(r["variants"]) in ({"[rk0]", "[rk>0]"}, {"[rk0+copy]", "[rk>0]"})  # (option fusecopy)
+    # (options fusecopy, defer4 and vdyn tag the launches whose read / write sets they change)
+    assert set(r["variants"]) == {"[rk0+copy+d4o]", "[rk>0+d4i]", "[rk>0+v]"}
+    assert sum(v["launches_per_step"] for v in r["variants"].values()) == 3
     assert r["traffic"] is not None, r["traffic_source"]
     # measured traffic cannot be below the distinct arrays the task must touch (minus the
     # 2-D mesh rows, which may stay in cache), nor absurdly above
