@@ -53,6 +53,7 @@ struct LoopGroup;  // loopback transport shared by the contexts of one process
 struct HaloSeg;    // one segment of a pack / unpack (mpas_halo.hip)
 struct HaloCopyTab {  // the device segment table of one direction of one exchange signature
     HaloSeg* dev = nullptr;
+    double** addr = nullptr;  // per buffer column: the field column it moves (built once, on the device)
     int nseg = 0;
     long ncol = 0;  // buffer columns covered
     std::shared_ptr<std::vector<HaloSeg>> host;

@@ -34,10 +34,11 @@ struct HaloSeg {
     int W, comp;      // columns per entity and the one this segment moves (x8 fields)
 };
 
-template <bool PACK>
-__global__ __launch_bounds__(256) void k_halo_copy(const HaloSeg* seg, int nseg, long ncol, int LP, double* buf) {
-    const long col = (long)blockIdx.x * (256 / LP) + threadIdx.x / LP;
-    const int k = (int)(threadIdx.x % LP);
+// the column address of every buffer column of a table (once per exchange signature: the
+// segment search and the id lookup -- five or six dependent memory round trips -- leave the
+// per-exchange copies, which then load one address per column)
+__global__ __launch_bounds__(256) void k_halo_addr(const HaloSeg* seg, int nseg, long ncol, int LP, double** addr) {
+    const long col = (long)blockIdx.x * 256 + threadIdx.x;
     if (col >= ncol) return;
     int lo = 0, hi = nseg - 1;  // the last segment starting at or before col
     while (lo < hi) {
@@ -46,7 +47,15 @@ __global__ __launch_bounds__(256) void k_halo_copy(const HaloSeg* seg, int nseg,
         else hi = mid - 1;
     }
     const HaloSeg& g = seg[lo];
-    double* f = g.f + ((size_t)g.ids[col - g.start] * g.W + g.comp) * LP + k;
+    addr[col] = g.f + ((size_t)g.ids[col - g.start] * g.W + g.comp) * LP;
+}
+
+template <bool PACK>
+__global__ __launch_bounds__(256) void k_halo_copy(double* const* addr, long ncol, int LP, double* buf) {
+    const long col = (long)blockIdx.x * (256 / LP) + threadIdx.x / LP;
+    const int k = (int)(threadIdx.x % LP);
+    if (col >= ncol) return;
+    double* f = addr[col] + k;
     double* b = buf + (size_t)col * LP + k;
     if (PACK) *b = *f;
     else *f = *b;
@@ -78,8 +87,10 @@ Halo::~Halo() {
         }
     if (sendbuf) (void)hipFree(sendbuf);
     if (recvbuf) (void)hipFree(recvbuf);
-    for (auto& kv : tabs)
+    for (auto& kv : tabs) {
         if (kv.second.dev) (void)hipFree(kv.second.dev);
+        if (kv.second.addr) (void)hipFree(kv.second.addr);
+    }
     if (rccl) rccl_free(rccl);
     if (sock) sock_free(sock);
     if (comm) {
@@ -501,9 +512,18 @@ static const HaloCopyTab* copy_table(const DevState& S, Halo& h, const std::vect
     e = hipSuccess;
     if (t.nseg) {
         if ((e = hipMalloc(&t.dev, sizeof(HaloSeg) * segs.size())) != hipSuccess) return nullptr;
-        if ((e = hipMemcpy(t.dev, t.host->data(), sizeof(HaloSeg) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess) {
+        if ((e = hipMemcpy(t.dev, t.host->data(), sizeof(HaloSeg) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+            (t.ncol && (e = hipMalloc(&t.addr, sizeof(double*) * t.ncol)) != hipSuccess)) {
             (void)hipFree(t.dev);
             return nullptr;
+        }
+        if (t.ncol) {  // (stream-ordered before every copy that uses the table)
+            k_halo_addr<<<(unsigned)((t.ncol + 255) / 256), 256, 0, st>>>(t.dev, t.nseg, t.ncol, S.LP, t.addr);
+            if ((e = hipGetLastError()) != hipSuccess) {
+                (void)hipFree(t.dev);
+                (void)hipFree(t.addr);
+                return nullptr;
+            }
         }
     }
     return &(h.tabs[key] = t);
@@ -518,8 +538,8 @@ static hipError_t run_copy(const DevState& S, hipStream_t st, Halo& h, const std
     const int cpb = 256 / S.LP;
     const unsigned grid = (unsigned)((t->ncol + cpb - 1) / cpb);
     double* buf = pack ? h.sendbuf : h.recvbuf;
-    if (pack) k_halo_copy<true><<<grid, 256, 0, st>>>(t->dev, t->nseg, t->ncol, S.LP, buf);
-    else k_halo_copy<false><<<grid, 256, 0, st>>>(t->dev, t->nseg, t->ncol, S.LP, buf);
+    if (pack) k_halo_copy<true><<<grid, 256, 0, st>>>(t->addr, t->ncol, S.LP, buf);
+    else k_halo_copy<false><<<grid, 256, 0, st>>>(t->addr, t->ncol, S.LP, buf);
     return hipGetLastError();
 }
 
