@@ -74,13 +74,21 @@ _r04["rk0"][1] = ("B", KERN["r03"]["rk0"][1][1], ["X_F", "tend_u_euler", "delsq_
 _r04["rk1din"] = [k if k[0] != "B" else
                   ("B", k[1] + ["delsq_divergence", "delsq_vorticity"], k[2] + ["tend_u_euler"])
                   for k in KERN["r03"]["rk1"]]
+# (the plain rk_step > 0 launch is stage 2's, whose B also stores v: option vdyn; E forms wc)
+_r04["rk1"] = [("A", ["ru"], ["h_divergence"]) if k[0] == "A" else
+               ("B", k[1], k[2] + ["v"]) if k[0] == "B" else
+               ("E", [f for f in k[1] if f != "X_wc"] + ["ru", "uReconstructZonal", "uReconstructMeridional"], k[2])
+               for k in KERN["r03"]["rk1"]]
+_r04["rk1din"] = [("A", ["ru"], ["h_divergence"]) if k[0] == "A" else
+                  ("E", [f for f in k[1] if f != "X_wc"] + ["ru", "uReconstructZonal", "uReconstructMeridional"], k[2])
+                  if k[0] == "E" else k for k in _r04["rk1din"]]
 KERN["r04"] = _r04
 
 # the kernel names of the rocprofv3 output per launch kind
 PAT = {
     ("rk0", "A"): r"^k_dyn_A<64, true", ("rk0", "B"): r"^k_dyn_B<64, true", ("rk0", "C"): r"^k_dyn_C<64",
     ("rk0", "D"): r"^k_dyn_D<64", ("rk0", "E"): r"^k_dyn_E<64, true",
-    ("rk1", "A"): r"^k_dyn_A<64, false", ("rk1", "B"): r"^k_dyn_B<64, false, false, true>$",
+    ("rk1", "A"): r"^k_dyn_A<64, false", ("rk1", "B"): r"^k_dyn_B<64, false, false, true(, false)?>$",
     ("rk1", "E"): r"^k_dyn_E<64, false",
     ("rk1din", "A"): r"^k_dyn_A<64, false", ("rk1din", "B"): r"^k_dyn_B<64, false, false, true, true>",
     ("rk1din", "E"): r"^k_dyn_E<64, false",
