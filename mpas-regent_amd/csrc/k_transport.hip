@@ -519,15 +519,11 @@ __device__ __forceinline__ double tr_limited(double A, double m1, double p2, dou
     return (A >= 0.0 ? fmin(m1, p2) : fmin(p1, m2)) * A;
 }
 
-// (MPAS_TRU_MINW: min waves per SIMD, a timing-build knob; 1 = the compiler's choice)
-#ifndef MPAS_TRU_MINW
-#define MPAS_TRU_MINW 1
-#endif
 // SU (option "trsu"): su formed here as k_tr_bounds forms it -- the upwind sum over the
 // cell's edges (tr_bound_slot's order) and tr_bound_fin's expression -- instead of read
 // from X_su: the same values, one scratch array fewer (written once, read once)
 template <int LP, bool SELF, bool SU>
-__global__ __launch_bounds__(256, MPAS_TRU_MINW) void k_tr_update(DevState S, double dt) {
+__global__ __launch_bounds__(256) void k_tr_update(DevState S, double dt) {
     int c, p;
     tr_slot<LP>(S, KC, c, p);
     const int L = S.L, k = (int)(threadIdx.x % LP);

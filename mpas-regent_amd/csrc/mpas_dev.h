@@ -409,13 +409,9 @@ struct TrTiles {
 // a group's UNION is the distinct cells its edges read scalars_old at (advCellsForEdge
 // and cellsOnEdge), at most TRE_U; a group with a larger union or an edge with more than AF
 // advCells is irregular (ucnt = -1) and gathers directly.  Built on the host (tre_build).
-#ifndef MPAS_TRE_GE
-#define MPAS_TRE_GE 16
-#define MPAS_TRE_U 52
-#endif
-constexpr int TRE_GE = MPAS_TRE_GE;  // edges per group
-constexpr int TRE_U = MPAS_TRE_U;    // LDS columns per group (52 KB at LP = 64 with a scalar pair
-                                     // each: three blocks per CU)
+constexpr int TRE_GE = 16;  // edges per group
+constexpr int TRE_U = 52;   // LDS columns per group (52 KB at LP = 64 with a scalar pair
+                            // each: three blocks per CU)
 constexpr int TRE_ROW = 12;  // slot bytes per edge: AF advCells, cellsOnEdge(0), (1), pad
 struct TrEdgeGroups {
     int ngroups = 0, neo = 0;  // groups; the owned edge count they were built for
