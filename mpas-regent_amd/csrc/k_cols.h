@@ -34,7 +34,7 @@ __device__ __forceinline__ void st64(double* d, size_t i, double2 v, Pair64 q) {
 template <int LP, bool MPASV>
 __device__ __forceinline__ void vi_column(const DevState& S, int c, int k, double zz, double exner, double tm, double cqw,
                                           double qtot, double rb, double rtb, double rtp, double exb, double gamma_old,
-                                          double coftz_old, double dtseps, double rcv, double c2) {
+                                          double coftz_old, double dtseps, double rcv, double c2, bool live = true) {
     const int L = S.L;
     const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
     const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
@@ -69,15 +69,32 @@ __device__ __forceinline__ void vi_column(const DevState& S, int c, int k, doubl
     double alpha, gamma;
     if constexpr (MPASV) {
         // level by level: a nonlinear recurrence (a prefix scan of its Moebius maps measured
-        // 2-4e-9 off the oracle over a step on the blowing-up random states, beyond RTOL_STEP)
-        double gp = 0.0;
-        alpha = gamma = 0.0;
-        for (int kk = 1; kk < L; kk++) {
-            const double al = 1.0 / (b - a * gp);
-            alpha = (k == kk) ? al : alpha;
-            gamma = (k == kk) ? cc * al : gamma;
-            gp = __shfl(gamma, kk, LP);
+        // 2-4e-9 off the oracle over a step on the blowing-up random states, beyond RTOL_STEP).
+        // The block's columns run it side by side, one lane per column, on their a / b / c
+        // staged in LDS -- the level-by-level expressions, so the same values -- instead of
+        // every lane of a column's wavefront stepping through all L - 1 levels.  Every wave of
+        // the block reaches both barriers (callers clamp a dead column and pass live = false)
+        constexpr int CPB = 256 / LP;
+        __shared__ double s_a[CPB][LP], s_b[CPB][LP], s_c[CPB][LP];
+        const int j = (int)(threadIdx.x / LP);
+        s_a[j][k] = a;
+        s_b[j][k] = b;
+        s_c[j][k] = cc;
+        __syncthreads();
+        if ((int)threadIdx.x < CPB) {
+            const int jj = (int)threadIdx.x;
+            double gp = 0.0;
+            for (int kk = 1; kk < L; kk++) {
+                const double al = 1.0 / (s_b[jj][kk] - s_a[jj][kk] * gp);
+                gp = s_c[jj][kk] * al;
+                s_a[jj][kk] = al;  // (alpha)
+                s_c[jj][kk] = gp;  // (gamma)
+            }
         }
+        __syncthreads();
+        const bool in = k >= 1 && k < L;
+        alpha = in ? s_a[j][k] : 0.0;
+        gamma = in ? s_c[j][k] : 0.0;
     } else {
         alpha = 1.0 / (b - a * gamma_m);  // :580-585
         gamma = cc * alpha;               // :587-591
@@ -86,20 +103,22 @@ __device__ __forceinline__ void vi_column(const DevState& S, int c, int k, doubl
     // written: every level but L (padding levels: zeros, full 64-B sectors; see PADW); the
     // tridiagonal coefficients not at level 0 either, gamma_tri 0.0 there.  Paired 16-B
     // stores (put2: every lane takes part)
-    const bool w_all = k != L, w_1 = k != L && k != 0;
+    const bool w_all = live && k != L, w_1 = w_all && k != 0;
     put2<LP>(fw(S, F_coftz), c, fw(S, F_cofwt), c, k, PADW(coftz), PADW(cofwt), w_all, w_all);
     put2<LP>(fw(S, F_cofwr), c, fw(S, F_cofwz), c, k, PADW(cofwr), PADW(cofwz), w_1, w_1);
     put2<LP>(fw(S, F_a_tri), c, fw(S, F_b_tri), c, k, PADW(a), PADW(b), w_1, w_1);
     put2<LP>(fw(S, F_c_tri), c, fw(S, F_alpha_tri), c, k, PADW(cc), PADW(alpha), w_1, w_1);
     if (w_all) colk(fw(S, F_gamma_tri), c) = k == 0 ? 0.0 : PADW(gamma);
-    if (c == 0 && k < L) fw(S, F_cofrz)[k] = cofrz;
+    if (live && c == 0 && k < L) fw(S, F_cofrz)[k] = cofrz;
 }
 
 template <int LP, bool MPASV>
 __device__ __forceinline__ void vert_imp_body(const DevState& S, double dtseps, double rcv, double c2, Blk bk) {
     ColMap<LP> m(S, KC, bk);
-    const int k = m.k, c = m.ent;
-    if (c >= S.nCO) return;
+    const int k = m.k;
+    const bool live = m.ent < S.nCO;
+    if (!MPASV && !live) return;  // (MPASV: vi_column's barriers need every wave; a dead column
+    const int c = live ? m.ent : S.nCO - 1;  // loads the last one and stores nothing)
     // (gather2: two own columns per 16-B load instruction)
     double zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old;
     gather2<LP>(fd(S, F_zz), c, fd(S, F_exner), c, k, zz, exner);
@@ -108,7 +127,8 @@ __device__ __forceinline__ void vert_imp_body(const DevState& S, double dtseps, 
     gather2<LP>(fd(S, F_rtheta_base), c, fd(S, F_rtheta_p), c, k, rtb, rtp);
     gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
     const double coftz_old = colk(fd(S, F_coftz), c);  // level L keeps its (never written) value
-    vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2);
+    vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2,
+                         live);
 }
 
 
@@ -402,8 +422,10 @@ __device__ __forceinline__ void setup_vi_body(const DevState& S, int ncb, double
         }
         return;
     }
-    const int c = col_of<LP>(xcd_block_n(S.xcd, blk, ncb)) + S.lo[KC];
-    if (c >= S.nCO) return;
+    const int c0 = col_of<LP>(xcd_block_n(S.xcd, blk, ncb)) + S.lo[KC];
+    const bool live = c0 < S.nCO;
+    if (!MPASV && !live) return;  // (MPASV: as vert_imp_body)
+    const int c = live ? c0 : S.nCO - 1;
     double rw, rtp, rp, w, tm, rz, zz, exner, rb, rtb, exb, gamma_old;
     gather2<LP>(fd(S, F_rw), c, fd(S, F_rtheta_p), c, k, rw, rtp);
     gather2<LP>(fd(S, F_rho_p), c, fd(S, F_w), c, k, rp, w);
@@ -413,7 +435,7 @@ __device__ __forceinline__ void setup_vi_body(const DevState& S, int ncb, double
     gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
     const double coftz_old = colk(fd(S, F_coftz), c);
     // :773-777 the save copies (every level but L; padding levels carry zeros either way)
-    const bool cp = k != L;
+    const bool cp = live && k != L;
     put2<LP>(fw(S, F_rw_save), c, fw(S, F_rtheta_p_save), c, k, PADW(rw), PADW(rtp), cp, cp);
     put2<LP>(fw(S, F_rho_p_save), c, fw(S, F_w_2), c, k, PADW(rp), PADW(w), cp, cp);
     put2<LP>(fw(S, F_theta_m_2), c, fw(S, F_rho_zz_2), c, k, PADW(tm), PADW(rz), cp, cp);
@@ -424,6 +446,7 @@ __device__ __forceinline__ void setup_vi_body(const DevState& S, int ncb, double
     const double cqw = k > L ? 0.0 : 1.0 / (1.0 + qtotal), qtot = 0.0;
     put2<LP>(fw(S, F_qtot), c, fw(S, F_cqw), c, k, qtot, cqw, cp, cp && k > 0);
     // (cqw is used at 0 < k < L only, qtot at k < L: the values just written)
-    vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2);
+    vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2,
+                         live);
 }
 }  // namespace mpas

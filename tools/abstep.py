@@ -3,7 +3,8 @@
 K atm_srk3 steps (HIP graph replay, as bench.py times them) under each option set (options a variant does not name at their defaults); per
 variant the median per-step device time over all rounds (HIP events between steps).
 
-usage: python tools/abstep.py [--ncells 163842] [--rounds 6] [--steps 5] --variants "fusesetup=1" "fusesetup=0"
+usage: python tools/abstep.py [--ncells 163842] [--rounds 6] [--steps 5] [--physics N] [--transport]
+       --variants "fusesetup=1" "fusesetup=0"
 """
 import argparse
 import json
@@ -26,9 +27,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--variants", nargs="+", required=True)
+    ap.add_argument("--physics", type=int, default=0, choices=[0, 1, 2])
+    ap.add_argument("--transport", action="store_true", help="physics 1 + the scalar transport (bench --transport)")
     a = ap.parse_args()
-    m, st = bench.build_inputs(a.ncells, a.levels)
+    physics = max(a.physics, 1 if a.transport else 0)
+    m, st = bench.build_inputs(a.ncells, a.levels, zero_based=physics)
     ctx = lib.Context(m.nCells, m.nEdges, m.nVertices, a.levels)
+    ctx.set_option("physics", physics)
+    ctx.set_option("transport", int(a.transport))
     bench.upload_inputs(ctx, st)
     dt = bench.dt_for(a.ncells)
     hip = bench.Hip()
@@ -57,7 +63,7 @@ def main():
             res[v] += [hip.elapsed_ms(evs[i], evs[i + 1]) for i in range(a.steps)]
     out = {v: {"median_ms": round(statistics.median(x), 4), "min_ms": round(min(x), 4), "n": len(x)}
            for v, x in res.items()}
-    out["workload"] = f"x1.{a.ncells} x {a.levels}"
+    out["workload"] = f"x1.{a.ncells} x {a.levels}, physics {physics}, transport {int(a.transport)}"
     print(json.dumps(out), flush=True)
 
 
