@@ -67,10 +67,11 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * disables the SELF gathers; "graph" = 1 (default) makes mpas_atm_srk3 capture its step once
  * per (dt, schedule) as a HIP graph and replay it (any option change or mesh upload
  * re-captures; per-task timing runs the launches directly; read-only "graph_captures" /
- * "graph_launches" count them).  "graph_halo" = 1 (default) does the same on a decomposed
- * context with the RCCL or stub transport: a step is captured per halo state at its start
- * (a start state met twice; up to 4 kept), and a capture the transport refuses falls back to
- * eager steps (read-only "graph_fallbacks").  "stub_latency_us" (stub transport only) adds a
+ * "graph_launches" count them).  "graph_halo" does the same on a decomposed context: 2
+ * (default) with the stub transport, 1 with the RCCL transport too (opt-in: its grouped
+ * send / recv has been captured on a 1-rank communicator only), 0 never; a step is
+ * captured per halo state at its start (a start state met twice; up to 4 kept), and a
+ * capture the transport refuses falls back to eager steps (read-only "graph_fallbacks").  "stub_latency_us" (stub transport only) adds a
  * device-side wait of that many microseconds to every exchange (tools/rank_sim.py).  All but
  * "exact" and "physics" change only speed, never results.
  * Cross-task fusion in mpas_atm_srk3 (reference semantics):

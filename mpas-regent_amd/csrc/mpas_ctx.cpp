@@ -144,7 +144,10 @@ struct mpas_ctx {
     std::vector<GraphEntry> graphs;
     uint64_t graph_clock = 0;
     int64_t graph_captures = 0, graph_launches = 0;
-    int graph_halo = 1;  // (a capture that fails on a transport falls back to eager steps: graph_fallbacks)
+    // 2 (default): the stub transport only; 1: RCCL too (its grouped send / recv captured --
+    // exercised on a 1-rank communicator only, which moves nothing); 0: off.  A capture that
+    // fails on a transport falls back to eager steps (graph_fallbacks)
+    int graph_halo = 2;
     int64_t graph_fallbacks = 0;
     std::vector<std::vector<uint8_t>> seen_stale0;  // start states stepped eagerly once
     // option "trtile": the tiled transport (k_transport.hip) when the mesh allows it; the
@@ -931,7 +934,7 @@ void prepare_now(mpas_ctx* c) {
 // one atm_srk3 step: replayed from a captured HIP graph when possible
 void srk3_step(mpas_ctx* c, double dt, int schedule) {
     Halo* h = c->halo.get();
-    const bool halo_graph = h && c->graph_halo && (h->rccl || h->stub) && !h->loop;
+    const bool halo_graph = h && !h->loop && (h->stub ? c->graph_halo != 0 : (h->rccl && c->graph_halo == 1));
     if (!c->graph_on || c->timing || (h && !halo_graph)) {
         srk3(c, dt, schedule);
         return;
@@ -1171,7 +1174,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp_halo") == 0) c->fusedamp_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value < 0 ? 0 : value > 2 ? 2 : value;
-        else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = value ? 1 : 0;
+        else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = (value == 1 || value == 2) ? value : 0;
         else if (name && std::strcmp(name, "stub_latency_us") == 0) {
             if (!c->halo || !c->halo->stub || value < 0 || value > 100000)
                 throw Fail{MPAS_EINVAL, "stub_latency_us: a stub-transport context and 0..100000 us"};

@@ -285,7 +285,8 @@ def test_stub_transport_graph_replay(x1_2562):
         with lib.Context(*d.n_local(1), st.L) as ctx:
             lib.setup_subdomain(ctx, d, 1)
             lib.halo_stub(ctx)
-            ctx.set_option("graph_halo", graph)
+            assert ctx.get_option("graph_halo") == 2  # (the default: on for the stub)
+            ctx.set_option("graph_halo", 2 if graph else 0)
             ctx.upload(loc)
             for _ in range(8):
                 T.atm_srk3(ctx, 720.0, 1)
@@ -332,9 +333,10 @@ def test_stub_graph_start_states(x1_2562, between):
 
 
 def test_rccl_graph_capture_single_rank(x1_2562):
-    """graph_halo (default on) with the RCCL transport: a 1-rank communicator's grouped
-    send / recv captured into the step's graph and replayed; bit-identical to eager steps,
-    no fallback to eager (graph_fallbacks), the same exchange counts"""
+    """graph_halo = 1 (opt-in for RCCL; the default 2 leaves RCCL steps eager) with the RCCL
+    transport: a 1-rank communicator's grouped send / recv captured into the step's graph and
+    replayed; bit-identical to eager steps, no fallback to eager (graph_fallbacks), the same
+    exchange counts; under the default no step is captured"""
     st = state(x1_2562, 56, "random")
     d = decomp.Decomposition(st, 1)
     out = {}
@@ -344,7 +346,7 @@ def test_rccl_graph_capture_single_rank(x1_2562):
             lib.setup_subdomain(ctx, d, 0)
             ctx.upload(got)
             lib.halo_rccl(ctx, 1, 0, lib.rccl_unique_id())
-            assert ctx.get_option("graph_halo") == 1
+            assert ctx.get_option("graph_halo") == 2
             ctx.set_option("graph_halo", graph)
             for _ in range(5):
                 T.atm_srk3(ctx, 720.0, 1)
@@ -356,6 +358,15 @@ def test_rccl_graph_capture_single_rank(x1_2562):
     assert not bad, bad[:6]
     assert out[1][1] == out[0][1]
     assert out[1][2] >= 1 and out[1][3] == 0, out[1][2:]
+    got = d.local_state(0)
+    with lib.Context(*d.n_local(0), st.L) as ctx:  # the default: RCCL steps run eagerly
+        lib.setup_subdomain(ctx, d, 0)
+        ctx.upload(got)
+        lib.halo_rccl(ctx, 1, 0, lib.rccl_unique_id())
+        for _ in range(3):
+            T.atm_srk3(ctx, 720.0, 1)
+        ctx.sync()
+        assert ctx.get_option("graph_captures") == 0
 
 
 def test_stub_latency_option(x1_2562):
