@@ -226,18 +226,17 @@ __global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) 
     int rec[24];
     row_ld(fi(S, X_eB) + (size_t)e * 24, rec);
     const int cell1 = rec[0], cell2 = rec[1];
-    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
     const double invDc = fd(S, F_invDcEdge)[e];
     const double *u_f = fd(S, F_u), *pv_f = fd(S, F_pv_edge), *tm_f = fd(S, F_theta_m);
     const size_t p1 = (size_t)cell1 * LP + lpos(LP, k), p2 = (size_t)cell2 * LP + lpos(LP, k);
 
-    // ---- issue every independent load of the column first
-    // (gather2: two columns per load instruction)
+    // ---- issue every independent load of the column first (gather2: two columns per load
+    // instruction; the raw halves, swapped after the scheduling barrier below)
     double u, ru_e, rw1, rw2, w1, w2, rho_edge, pv;
-    gather2<LP>(u_f, e, fd(S, F_ru), e, k, u, ru_e);
-    gather2s<LP>(fd(S, F_rw), cell1, cell2, k, rw1, rw2);
-    gather2s<LP>(fd(S, F_w), cell1, cell2, k, w1, w2);
-    gather2<LP>(fd(S, F_rho_edge), e, pv_f, e, k, rho_edge, pv);
+    const double2 g_uru = gather2_ld<LP>(u_f, e, fd(S, F_ru), e, k);
+    const double2 g_rw = gather2s_ld<LP>(fd(S, F_rw), cell1, cell2, k);
+    const double2 g_w = gather2s_ld<LP>(fd(S, F_w), cell1, cell2, k);
+    const double2 g_rp = gather2_ld<LP>(fd(S, F_rho_edge), e, pv_f, e, k);
     // No level masks (ldz) in this kernel: lanes k >= L store nothing (k > L: PADW
     // zeros), so a value used in its own lane needs none, and the vertical shuffles
     // (lvl_up/dn) of u and w bring lanes k <= L only levels <= L -- exactly what the
@@ -253,10 +252,11 @@ __global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) 
     for (int j = 0; j < QF; j++) ee_[j] = rec[2 + j];
     row_ld(woe, woe_);
     const bool kl = k < L;
+    double2 g_ue[QF / 2], g_pve[QF / 2];
 #pragma unroll
     for (int j = 0; j < QF; j += 2) {
-        gather2s<LP>(u_f, ee_[j], ee_[j + 1], k, ue_[j], ue_[j + 1]);
-        gather2s<LP>(pv_f, ee_[j], ee_[j + 1], k, pve_[j], pve_[j + 1]);
+        g_ue[j / 2] = gather2s_ld<LP>(u_f, ee_[j], ee_[j + 1], k);
+        g_pve[j / 2] = gather2s_ld<LP>(pv_f, ee_[j], ee_[j + 1], k);
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = rec[22];
@@ -271,43 +271,77 @@ __global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) 
     row_ld(ac3, ac3_);
     static_assert(AF == 9, "tv_ pairing below");
     double tr_phys;
+    double2 g_tv[AF / 2];
 #pragma unroll
-    for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(tm_f, ad_[j], ad_[j + 1], k, tv_[j], tv_[j + 1]);
-    gather2<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k, tv_[AF - 1], tr_phys);
+    for (int j = 0; j < AF - 1; j += 2) g_tv[j / 2] = gather2s_ld<LP>(tm_f, ad_[j], ad_[j + 1], k);
+    const double2 g_tvl = gather2_ld<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k);
 
     // MD: the state w at the advCells, for the w reconstruction flux_arr of this edge
     double wv_[AF];
+    double2 g_wv[AF / 2];
     if constexpr (MD) {
         const double* w_f = fd(S, F_w);
 #pragma unroll
-        for (int j = 0; j < AF - 1; j += 2) gather2s<LP>(w_f, ad_[j], ad_[j + 1], k, wv_[j], wv_[j + 1]);
+        for (int j = 0; j < AF - 1; j += 2) g_wv[j / 2] = gather2s_ld<LP>(w_f, ad_[j], ad_[j + 1], k);
         wv_[AF - 1] = colk(w_f, ad_[AF - 1]);
     }
     // loads of the later sections, also ahead of every store (a store could alias them
     // for the compiler, which would then issue them only after it)
     const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
     double ke1, ke2, hd1, hd2;
-    gather2s<LP>(ke_f, cell1, cell2, k, ke1, ke2);
-    gather2s<LP>(hd_f, cell1, cell2, k, hd1, hd2);
+    const double2 g_ke = gather2s_ld<LP>(ke_f, cell1, cell2, k);
+    const double2 g_hd = gather2s_ld<LP>(hd_f, cell1, cell2, k);
     // (the rk0-only loads stay in their section: hoisted they cost more in occupancy,
     // 138 VGPRs, than the second memory round trip)
     // HF (fast path): E's per-edge theta flux H formed here (rk > 0: with the
     // perturbation flux, which needs ru_save at the edge and theta_m_save at its cells)
     double tue_in = 0.0, rus_e = 0.0, ts1 = 0.0, ts2 = 0.0;
+    double2 g_tr = make_double2(0.0, 0.0), g_ts = make_double2(0.0, 0.0);
     if constexpr (!RK0) {
         if constexpr (HF) {
-            gather2<LP>(fd(S, F_tend_u_euler), e, fd(S, F_ru_save), e, k, tue_in, rus_e);
-            if (a.cp) rus_e = ru_e;  // (the copy below is setup's: ru_save = ru, read after it)
-            gather2s<LP>(fd(S, F_theta_m_save), cell1, cell2, k, ts1, ts2);
+            g_tr = gather2_ld<LP>(fd(S, F_tend_u_euler), e, fd(S, F_ru_save), e, k);
+            g_ts = gather2s_ld<LP>(fd(S, F_theta_m_save), cell1, cell2, k);
         } else {
             tue_in = colk(fd(S, F_tend_u_euler), e);
         }
     }
-    if constexpr (DIN) {  // kernel D of the rk_step 0 call (:1132-1150), deferred here
+    double2 g_dd = make_double2(0.0, 0.0), g_dv = make_double2(0.0, 0.0);
+    if constexpr (DIN) {
         const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
+        g_dd = gather2s_ld<LP>(fd(S, F_delsq_divergence), cell1, cell2, k);
+        g_dv = gather2s_ld<LP>(fd(S, F_delsq_vorticity), vertex1, vertex2, k);
+    }
+    // every load above in flight before the first swap consumes one (the per-level
+    // coefficients after it: cache hits, no registers held across the batch)
+    __builtin_amdgcn_sched_barrier(0);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
+    g2_fin<LP>(g_uru, u, ru_e);
+    g2_fin<LP>(g_rw, rw1, rw2);
+    g2_fin<LP>(g_w, w1, w2);
+    g2_fin<LP>(g_rp, rho_edge, pv);
+#pragma unroll
+    for (int j = 0; j < QF; j += 2) {
+        g2_fin<LP>(g_ue[j / 2], ue_[j], ue_[j + 1]);
+        g2_fin<LP>(g_pve[j / 2], pve_[j], pve_[j + 1]);
+    }
+#pragma unroll
+    for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_tv[j / 2], tv_[j], tv_[j + 1]);
+    g2_fin<LP>(g_tvl, tv_[AF - 1], tr_phys);
+    if constexpr (MD) {
+#pragma unroll
+        for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_wv[j / 2], wv_[j], wv_[j + 1]);
+    }
+    g2_fin<LP>(g_ke, ke1, ke2);
+    g2_fin<LP>(g_hd, hd1, hd2);
+    if constexpr (!RK0 && HF) {
+        g2_fin<LP>(g_tr, tue_in, rus_e);
+        if (a.cp) rus_e = ru_e;  // (the copy below is setup's: ru_save = ru, read after it)
+        g2_fin<LP>(g_ts, ts1, ts2);
+    }
+    if constexpr (DIN) {  // kernel D of the rk_step 0 call (:1132-1150), deferred here
         double dd1, dd2, dv1, dv2;
-        gather2s<LP>(fd(S, F_delsq_divergence), cell1, cell2, k, dd1, dd2);
-        gather2s<LP>(fd(S, F_delsq_vorticity), vertex1, vertex2, k, dv1, dv2);
+        g2_fin<LP>(g_dd, dd1, dd2);
+        g2_fin<LP>(g_dv, dv1, dv2);
         const double u_mix_scale = fd(S, F_meshScalingDel4)[e] * a.h4d;
         const double r_dc = u_mix_scale * kDel4uDivFactor * invDc;
         const double r_dv = u_mix_scale * dmin_(fd(S, F_invDvEdge)[e], 4 * invDc);

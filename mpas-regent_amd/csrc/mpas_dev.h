@@ -546,6 +546,36 @@ __device__ __forceinline__ void gather2(const double* fa, int ia, const double* 
     }
 }
 
+// gather2 / gather2s in two halves, for a kernel that issues every load of a section before
+// the first swap (the loads, __builtin_amdgcn_sched_barrier, then g2_fin): the compiler
+// otherwise interleaves the first swaps with the loads and waits on each (dyn_tend B)
+template <int LP>
+__device__ __forceinline__ double2 gather2_ld(const double* fa, int ia, const double* fb, int ib, int k) {
+    if constexpr (LP == 64) {
+        const bool hi = k >= 32;
+        const char* base = hi ? (const char*)fb + (size_t)(uint32_t)ib * 512 : (const char*)fa + (size_t)(uint32_t)ia * 512;
+        return *(const double2*)MPAS_CHK(hi ? fb : fa, base + (k & 31) * 16, 16);
+    } else {
+        return make_double2(colk(fa, ia), colk(fb, ib));
+    }
+}
+template <int LP>
+__device__ __forceinline__ double2 gather2s_ld(const double* f, int ia, int ib, int k) {
+    if constexpr (LP == 64) {
+        const uint32_t off = (uint32_t)(k >= 32 ? ib : ia) * 512u + (uint32_t)(k & 31) * 16u;
+        return at_off((const double2*)f, off);
+    } else {
+        return make_double2(colk(f, ia), colk(f, ib));
+    }
+}
+template <int LP>
+__device__ __forceinline__ void g2_fin(double2 t, double& a, double& b) {
+    double x = t.x, y = t.y;
+    if constexpr (LP == 64) swap_halves(x, y);
+    a = x;
+    b = y;
+}
+
 // f at the two cellsOnEdge (x1, x2) of edge slot i of a cell.  SELF (S.selfc): the cell
 // is one of them, so only the other cell `oth` is gathered and `own`, f at the cell
 // itself, stands in for the other (s1: the cell is cellsOnEdge(0)).  Same values either way.
