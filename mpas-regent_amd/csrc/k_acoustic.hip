@@ -69,7 +69,8 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             const double *dvi = fd(S, X_dvB), *tmf = fd(S, F_theta_m);
             const double ru = colk(fd(S, F_ru_p), e), d1 = colk(dvi, c1), d2 = colk(dvi, c2);
             const double t12 = TME ? colk(fd(S, X_tme), e) : colk(tmf, c1) + colk(tmf, c2);
-            const bool on = k < L && !(fi(S, F_isShared)[c1] && fi(S, F_isShared)[c2]);
+            const int sh1 = fi(S, F_isShared)[c1], sh2 = fi(S, F_isShared)[c2];
+            const bool on = (k < L) & !(sh1 & sh2);
             colk(fw(S, X_rupB), e) = PADW(damp_edge<LP>(ru, d1, d2, t12, fd(S, F_specZoneMaskEdge)[e], coefp, on));
             return;
         }
@@ -107,6 +108,9 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         col_rd2<LP>(rwp_f, ww_f, c, k, L, rwp, ww);
     }
     col_rd2<LP>(fd(S, F_theta_m), fd(S, F_tend_rho), c, k, L, tm, tend_rho);
+    // SML: the point's cprMask byte with the column loads (tested after a lane condition it
+    // was loaded under a divergent branch and waited for there)
+    const uint8_t cpr = SML ? ((const uint8_t*)S.f[F_cprMask])[p] : 0;
     static_assert(NF % 2 == 0, "slot pairs");
 #pragma unroll
     for (int i = 0; i < NF; i += 2) {
@@ -131,11 +135,23 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         for (int i = 0; i < NF; i += 2)
             cell_pair2<LP, SELF>(dvi, c1_, c2_, o_, s1_, dv_c, i, k, d1_[i], d2_[i], d1_[i + 1], d2_[i + 1]);
         double* rup_out = fw(S, X_rupB);
+        // the isShared flags of every slot's two cells loaded up front and combined without
+        // short-circuit evaluation: `kl && ... && !(sh[x1] && sh[x2])` put each slot's loads
+        // under a lane-divergent branch with a full wait inside (six round trips per wave)
+        // (specZoneMaskEdge too: sunk into the `on` branch, its load waited there)
+        int sh1_[NF], sh2_[NF];
+        double spz_[NF];
 #pragma unroll
         for (int i = 0; i < NF; i++) {
             const int x1 = SELF ? (s1_[i] ? c : o_[i]) : c1_[i], x2 = SELF ? (s1_[i] ? o_[i] : c) : c2_[i];
-            const bool on = kl && e_[i] < S.nEdges && !(sh[x1] && sh[x2]);
-            rup_[i] = damp_edge<LP>(rup_[i], d1_[i], d2_[i], ts_[i], spz[e_[i]], coefp, on);
+            sh1_[i] = sh[x1];
+            sh2_[i] = sh[x2];
+            spz_[i] = spz[e_[i]];
+        }
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const bool on = kl & (e_[i] < S.nEdges) & !(sh1_[i] & sh2_[i]);
+            rup_[i] = damp_edge<LP>(rup_[i], d1_[i], d2_[i], ts_[i], spz_[i], coefp, on);
             if ((own >> i) & 1) colk(rup_out, e_[i]) = PADW(rup_[i]);  // (level L: the value read)
         }
     }
@@ -181,7 +197,7 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             wn -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
         }
         wn *= (fzm * zz + fzp * lvl_dn<LP>(zz, k));
-        if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) {
+        if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
             colk(fw(S, F_w), c) = wn;
             w = wn;
         }
@@ -243,7 +259,8 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         double rpe = colk(ru_p, eoc[i]);
         if constexpr (MODE == 2) {
             const int e = eoc[i], x1 = cc1[i], x2 = cc2[i];
-            const bool on = kl && e < S.nEdges && !(fi(S, F_isShared)[x1] && fi(S, F_isShared)[x2]);
+            const int sh1 = fi(S, F_isShared)[x1], sh2 = fi(S, F_isShared)[x2];
+            const bool on = kl & (e < S.nEdges) & !(sh1 & sh2);
             rpe = damp_edge<LP>(rpe, colk(fd(S, X_dvB), x1), colk(fd(S, X_dvB), x2), colk(tm_f, x1) + colk(tm_f, x2),
                                 fd(S, F_specZoneMaskEdge)[e], coefp, on);
             if ((own >> i) & 1) colk(fw(S, X_rupB), e) = PADW(rpe);

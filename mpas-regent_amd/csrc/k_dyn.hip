@@ -423,7 +423,9 @@ __global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) 
         }
     }
     tend_u += rho_edge * (q - (ke2 - ke1) * invDc) - u * 0.5 * (hd1 + hd2);
-    if (a.vB) {  // solve_diagnostics' v (:429-437; Q23: from i = 1) from the same u columns
+    // (rk_step > 0 only: at rk_step 0 the store would keep the compiler from issuing the rk0
+    // section's loads below ahead of it)
+    if (!RK0 && a.vB) {  // solve_diagnostics' v (:429-437; Q23: from i = 1) from the same u columns
         double vv = 0.0;
 #pragma unroll
         for (int j = 1; j < QF; j++) vv = add_if(j < neoe, vv, woe_[j] * ue_[j]);

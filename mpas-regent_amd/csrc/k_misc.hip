@@ -227,6 +227,9 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     double zz, w;
     col_rd2<LP>(fd(S, F_zz), fd(S, wf), c, k, L, zz, w);
+    // (the point's cprMask byte loaded with the columns: tested after a lane condition it
+    // was loaded under a divergent branch and waited for there)
+    const uint8_t cpr = MD ? 0 : ((const uint8_t*)S.f[F_cprMask])[p];
     const double zz_m = lvl_dn<LP>(zz, k);
     int e_[NF];
     double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgn_[NF];
@@ -257,7 +260,7 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     w *= (fzm * zz + fzp * zz_m);
     if (MD) {
         if (k >= 1 && k < L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone) colk(fw(S, wf), c) = w;
-    } else if (k <= L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone && ((const uint8_t*)S.f[F_cprMask])[p]) {
+    } else if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
         colk(fw(S, wf), c) = w;
     }
 }
