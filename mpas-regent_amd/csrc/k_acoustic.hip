@@ -146,7 +146,8 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             const int x1 = SELF ? (s1_[i] ? c : o_[i]) : c1_[i], x2 = SELF ? (s1_[i] ? o_[i] : c) : c2_[i];
             sh1_[i] = sh[x1];
             sh2_[i] = sh[x2];
-            spz_[i] = spz[e_[i]];
+            // (the edge's mask: wave-uniform at LP = 64, one column per wave)
+            spz_[i] = LP == 64 ? uniform_d(spz[e_[i]]) : spz[e_[i]];
         }
 #pragma unroll
         for (int i = 0; i < NF; i++) {

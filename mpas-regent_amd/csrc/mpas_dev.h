@@ -451,6 +451,17 @@ __device__ __forceinline__ MPAS_GLOBAL T* sgpr_ptr(T* p) {
     return (MPAS_GLOBAL T*)(((uint64_t)hi << 32) | lo);
 }
 
+// A wave-uniform double made visibly uniform (readfirstlane of both halves; only for values
+// the whole wavefront shares: one column per wave, LP = 64).  The lane
+// reads are convergent, so the compiler cannot sink the load feeding them into a
+// lane-divergent block, where it would be waited for with a full s_waitcnt vmcnt(0)
+__device__ __forceinline__ double uniform_d(double x) {
+    const uint64_t v = __builtin_bit_cast(uint64_t, x);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+
 #if MPAS_BOUNDS
 // Bounds-checked build (-DMPAS_BOUNDS=1, `make -C csrc bounds` -> libmpasdyn_bounds.so,
 // selected with env MPAS_LIB).  Every column access (colk, gather2, gather2s,
