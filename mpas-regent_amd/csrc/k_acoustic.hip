@@ -39,14 +39,38 @@ namespace mpas {
 // coef_prev, its div in X_dvB) to every ru_p it reads -- the same expression on the same
 // values as the damping kernel, so the same bits -- and writes the damped ru_p of the
 // edges this cell owns (X_eown; the lowest (cell, slot) listing an edge) to X_rupB, all
-// levels (level L copied, padding 0); the edges no cell lists are written by ncb.. extra
-// blocks (X_orph).  The damping launch between two substeps disappears: its ru_p
+// levels (level L copied, padding 0); the edges no cell lists are written by blocks of
+// their own (X_orph, acoustic_orph_body).  The damping launch between two substeps disappears: its ru_p
 // read-modify-write and its cell gathers (theta_m is gathered here anyway).
 // t12 = theta_m(cell1) + theta_m(cell2) (the same value as t2 + t1: X_tme)
 template <int LP>
 __device__ __forceinline__ double damp_edge(double rup, double d1, double d2, double t12, double spec, double coef,
                                             bool on) {
     return on ? rup + coef * (d2 - d1) * (1.0 - spec) / t12 : rup;  // (:1757-1759 order)
+}
+
+// MODE 2, the edges no cell lists (X_orph): the damping alone, into the new buffer.  Its own
+// blocks -- a launch of their own (k_acoustic_orph) or the tail of a combined grid: with this
+// store on a path of the cell kernel, the compiler could no longer prove the cell kernel's
+// mesh rows unclobbered and loaded them as vector loads after its first gathers (18 more
+// VGPRs, a second memory round trip)
+template <int LP, bool TME>
+__device__ __forceinline__ void acoustic_orph_body(const DevState& S, double coefp, int ob) {
+    const int L = S.L, k = (int)(threadIdx.x % LP);
+    const int j = col_of<LP>(ob);
+    if (j >= S.n_orph) return;
+    const int e = fi(S, X_orph)[j];
+    const int c1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], c2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
+    const double *dvi = fd(S, X_dvB), *tmf = fd(S, F_theta_m);
+    const double ru = colk(fd(S, F_ru_p), e), d1 = colk(dvi, c1), d2 = colk(dvi, c2);
+    const double t12 = TME ? colk(fd(S, X_tme), e) : colk(tmf, c1) + colk(tmf, c2);
+    const int sh1 = fi(S, F_isShared)[c1], sh2 = fi(S, F_isShared)[c2];
+    const bool on = (k < L) & !(sh1 & sh2);
+    colk(fw(S, X_rupB), e) = PADW(damp_edge<LP>(ru, d1, d2, t12, fd(S, F_specZoneMaskEdge)[e], coefp, on));
+}
+template <int LP, bool TME>
+__global__ __launch_bounds__(256) void k_acoustic_orph(DevState S, double coefp) {
+    acoustic_orph_body<LP, TME>(S, coefp, (int)blockIdx.x);
 }
 
 // TME (atm_srk3, option "tmedge"): theta_m(cell2) + theta_m(cell1) of each edge comes from
@@ -60,22 +84,7 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
     static_assert(!SML || (FIRST && !MPASV), "set_smlstep precedes a stage's first substep (reference semantics)");
     const int L = S.L, k = (int)(threadIdx.x % LP);
     int blk = bk.b;
-    if constexpr (MODE == 2) {
-        if (blk >= ncb) {  // an edge no cell lists: the damping alone, into the new buffer
-            const int j = col_of<LP>(blk - ncb);
-            if (j >= S.n_orph) return;
-            const int e = fi(S, X_orph)[j];
-            const int c1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], c2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
-            const double *dvi = fd(S, X_dvB), *tmf = fd(S, F_theta_m);
-            const double ru = colk(fd(S, F_ru_p), e), d1 = colk(dvi, c1), d2 = colk(dvi, c2);
-            const double t12 = TME ? colk(fd(S, X_tme), e) : colk(tmf, c1) + colk(tmf, c2);
-            const int sh1 = fi(S, F_isShared)[c1], sh2 = fi(S, F_isShared)[c2];
-            const bool on = (k < L) & !(sh1 & sh2);
-            colk(fw(S, X_rupB), e) = PADW(damp_edge<LP>(ru, d1, d2, t12, fd(S, F_specZoneMaskEdge)[e], coefp, on));
-            return;
-        }
-    }
-    blk = xcd_block_n(S.xcd, blk, MODE == 2 ? ncb : bk.n);
+    blk = xcd_block_n(S.xcd, blk, ncb);  // (ncb: the cell blocks, bk.n or fewer)
     const int c = col_of<LP>(blk) + S.lo[KC];
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + lpos(LP, k);
@@ -424,9 +433,10 @@ template <int LP, bool EXACT, bool SELF, int EPW>
 __global__ __launch_bounds__(256) void k_hf_ac_vc(DevState S, double dts, int small_step, double epssm, double resm,
                                                  double coefp, int ncb, int nb1, int nVB, int wold) {
     const int b = (int)blockIdx.x;
-    if (b < nb1)
+    if (b < ncb)
         acoustic_body<LP, EXACT, SELF, false, false, 2, false, false>(S, dts, small_step, epssm, resm, coefp, ncb,
-                                                                       Blk{b, nb1}, wold);
+                                                                       Blk{b, ncb}, wold);
+    else if (b < nb1) acoustic_orph_body<LP, false>(S, coefp, b - ncb);
     else solve_vc_body<LP, EPW, false>(S, nVB, 0, Blk{b - nb1, (int)gridDim.x - nb1});
 }
 
@@ -483,7 +493,7 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     auto run = [&](const DevState& X) {
         const int ncb = col_blocks<LP>(X, KC);
         if (!ncb) return;
-        const int grid = ncb + (mode == 2 ? (S.n_orph + 256 / LP - 1) / (256 / LP) : 0);
+        const int grid = ncb;
         const bool first = small_step == 0;
         auto go = [&](auto ex, auto sf, auto md) {
             constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
@@ -520,6 +530,11 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
         };
         if (exact) go_s(std::true_type{});
         else go_s(std::false_type{});
+        const int nob = (S.n_orph + 256 / LP - 1) / (256 / LP);  // (MODE 2: the edges no cell lists)
+        if (mode == 2 && nob) {
+            if (tme) k_acoustic_orph<LP, true><<<nob, 256, 0, st>>>(X, coef_prev);
+            else k_acoustic_orph<LP, false><<<nob, 256, 0, st>>>(X, coef_prev);
+        }
     };
     // (ru_p at the edges of owned cells only; MODE 2 also div at their cells -- X_dvB, the
     // previous substep's; SML u_tend at the edges of owned cells)
