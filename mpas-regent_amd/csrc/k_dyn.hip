@@ -523,13 +523,16 @@ __global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) 
 // one-vertex wave is latency-bound; the VE vertices issue their gathers together
 // (option "cve", default 4; profiles/r03/c_vertex_epw: C 482 -> 398 us at x1.163842, the
 // step -0.7 %; 8 vertices: C 410 us, the step and x1.2562 no better than 4)
-template <int LP, bool SELF, int VE>
-__global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a, int nVB) {
+// PART (a launch's blocks): 1 the vertex blocks, 2 the cell blocks -- two launches, each
+// with its mesh rows as scalar loads (one grid of both interleaved made the compiler load
+// ~24 of them per wave with vector loads: the other path's stores could clobber them)
+template <int LP, bool SELF, int VE, int PART>
+__global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
     ColMap<LP> m(S, KV);
-    int bi;
-    if (vc_block(S, m.blk, nVB, bi)) {  // VE vertices: delsq_vorticity (:1052-1060)
+    const int bi = m.blk;
+    if constexpr (PART == 1) {  // VE vertices: delsq_vorticity (:1052-1060)
         const int v0 = col_of<LP>(bi) * VE + S.lo[KV], k = m.k;
         if (v0 >= S.nVO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
         int ev[VE][3];
@@ -1033,13 +1036,14 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
             else k_dyn_B<LP, false, MD, false><<<nb, 256, 0, st>>>(X, a);
         }
     };
-    auto kC = [&](const DevState& X) {  // vertex blocks (del4) first, then cell blocks
+    auto kC = [&](const DevState& X) {  // the vertex blocks (del4), then the cell blocks
         auto go = [&](auto ve) {
             constexpr int VE = LP == 64 ? decltype(ve)::value : 1;
-            const int nv = del4 ? col_blocks_n<LP, VE>(X, KV) : 0, nb = nv + col_blocks<LP>(X, KC);
-            if (!nb) return;
-            if (X.selfc) k_dyn_C<LP, true, VE><<<nb, 256, 0, st>>>(X, a, nv);
-            else k_dyn_C<LP, false, VE><<<nb, 256, 0, st>>>(X, a, nv);
+            const int nv = del4 ? col_blocks_n<LP, VE>(X, KV) : 0, nc = col_blocks<LP>(X, KC);
+            if (nv && X.selfc) k_dyn_C<LP, true, VE, 1><<<nv, 256, 0, st>>>(X, a);
+            else if (nv) k_dyn_C<LP, false, VE, 1><<<nv, 256, 0, st>>>(X, a);
+            if (nc && X.selfc) k_dyn_C<LP, true, VE, 2><<<nc, 256, 0, st>>>(X, a);
+            else if (nc) k_dyn_C<LP, false, VE, 2><<<nc, 256, 0, st>>>(X, a);
         };
         const int ve = X.cve ? X.cve : 4;  // (option "cve")
         if (ve == 8) go(std::integral_constant<int, 8>{});

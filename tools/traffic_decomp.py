@@ -143,14 +143,17 @@ def main():
             task_r |= set(f for f in rd if f not in task_w)
             task_w |= set(wr)
             m = [v for kname, v in pmc.items() if re.search(PAT[(lk, name)], kname)]
+            # (every matching kernel summed: C is two launches, its vertex and its cell blocks)
             if not m:
                 meas = None
             else:
-                meas = 1e3 * (2 * m[0]["FETCH_SIZE"] + m[0]["WRITE_SIZE"])  # KB -> B; FETCH x 2 (gfx950)
+                meas = 1e3 * sum(2 * x["FETCH_SIZE"] + x["WRITE_SIZE"] for x in m)  # KB -> B; FETCH x 2 (gfx950)
+            hit = None
+            if m and all("TCC_HIT_sum" in x for x in m):
+                h = sum(x["TCC_HIT_sum"] for x in m)
+                hit = h / (h + sum(x["TCC_MISS_sum"] for x in m))
             per.append({"kernel": name, "compulsory_GB": comp / 1e9, "measured_GB": None if meas is None else meas / 1e9,
-                        "refetch_GB": None if meas is None else (meas - comp) / 1e9,
-                        "l2_hit": None if not m or "TCC_HIT_sum" not in m[0] else
-                        m[0]["TCC_HIT_sum"] / (m[0]["TCC_HIT_sum"] + m[0]["TCC_MISS_sum"])})
+                        "refetch_GB": None if meas is None else (meas - comp) / 1e9, "l2_hit": hit})
             tot_kernel += comp
             meas_tot += meas or 0.0
         scratch = {"X_wc", "X_F"}
