@@ -212,10 +212,12 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // its del4 part (kernel D, skipped there); this kernel applies D's statements to the
 // tend_u_euler it reads -- the same operands in the same order, so the same bits -- and
 // stores the result.  D's tend_u of that call is dead in atm_srk3 (this kernel writes tend_u)
-// (DIN: capped at 128 VGPRs, the 4 waves per SIMD of the plain rk_step > 0 kernel; uncapped
-// the compiler takes 132 and 3 waves: +35 %, profiles/r04)
+// (DIN at LP = 64: capped at 128 VGPRs, the 4 waves per SIMD of the plain rk_step > 0 kernel;
+// uncapped the compiler takes 132 and 3 waves: +35 %, profiles/r04.  At LP < 64 the cap made
+// it spill ~78 VGPRs.  The MPAS dynamics' B (139-147 VGPRs) under the same cap spills 8-32
+// and runs 7-80 % slower: profiles/r04/md_cap_tried)
 template <int LP, bool RK0, bool MD, bool HF, bool DIN = false>
-__global__ __launch_bounds__(256, DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) {
+__global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -970,9 +972,10 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
-// (rk_step > 0, reference semantics: 4 waves per SIMD, as before E formed wc itself)
+// (rk_step > 0, reference semantics, LP = 64: 4 waves per SIMD, as before E formed wc itself;
+// at LP < 64 that cap spilled 10-22 VGPRs)
 template <int LP, bool RK0, bool SELF, bool MD, bool HF>
-__global__ __launch_bounds__(256, (!RK0 && !MD) ? 4 : 1) void k_dyn_E(DevState S, DynK a) {
+__global__ __launch_bounds__(256, LP == 64 && !RK0 && !MD ? 4 : 1) void k_dyn_E(DevState S, DynK a) {
     dyn_E_body<LP, RK0, SELF, MD, HF>(S, a, this_blk());
 }
 // D and E of rk_step 0 in one grid (option "hfuse": neither reads what the other writes)
