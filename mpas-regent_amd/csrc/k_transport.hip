@@ -662,16 +662,7 @@ __device__ __forceinline__ int trt_slot() {
     return s;
 }
 
-// A load the compiler may take through the scalar unit: the constant address space
-// declares the data read-only for the kernel's lifetime (mesh rows and the tile tables,
-// which no kernel writes).  With a wave-uniform address it is an s_load; through a
-// generic pointer the kernels' stores between cells would make every row entry a vector
-// load of its own (the compiler cannot prove they do not alias).
-#define MPAS_CONST __attribute__((address_space(4)))
-template <class T>
-__device__ __forceinline__ T ldc(const T* p) {
-    return *(const MPAS_CONST T*)(uintptr_t)p;
-}
+// (ldc, the constant-address-space load of the mesh rows and the tile tables: mpas_dev.h)
 
 // The mesh data of one tile cell (LP = 64: every index is wave-uniform, so all of it
 // comes through the scalar unit).

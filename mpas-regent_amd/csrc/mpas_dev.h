@@ -696,15 +696,29 @@ __device__ __forceinline__ double ldz(bool keep, double v) { return keep ? v : 0
 __device__ __forceinline__ double add_if(bool c, double acc, double t) { return c ? acc + t : acc; }
 __device__ __forceinline__ double sub_if(bool c, double acc, double t) { return c ? acc - t : acc; }
 
+// A load the compiler may take through the scalar unit: the constant address space
+// declares the data read-only for the kernel's lifetime (mesh rows and the tile tables,
+// which only the one-time preparation kernels write).  With a wave-uniform address it is an s_load; through a
+// generic pointer the kernels' stores between cells would make every row entry a vector
+// load of its own (the compiler cannot prove they do not alias).
+#define MPAS_CONST __attribute__((address_space(4)))
+template <class T>
+__device__ __forceinline__ T ldc(const T* p) {
+    return *(const MPAS_CONST T*)(uintptr_t)p;
+}
+
 // the first N entries of a padded mesh-data row, loaded unconditionally (every row is
-// allocated at its full width, so the entries past the list's length are in bounds)
+// allocated at its full width, so the entries past the list's length are in bounds).
+// Through ldc: every row_ld source is mesh data or a precomputed mesh table, so a
+// wave-uniform row is scalar loads even in a kernel that also stores (a mixed vertex /
+// cell grid, a damping path)
 template <int N, class T>
 __device__ __forceinline__ void row_ld(const T* p, T (&r)[N]) {
 #if MPAS_BOUNDS
     p = (const T*)(MPAS_CHK(p, p, N * sizeof(T)) == (const void*)p ? p : (const T*)g_bounds_sink);
 #endif
 #pragma unroll
-    for (int i = 0; i < N; i++) r[i] = p[i];
+    for (int i = 0; i < N; i++) r[i] = ldc(p + i);
 }
 
 // a cell's first NF edges and their cells from its record (X_cR / X_cRs): one scalar
