@@ -243,8 +243,8 @@ __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int ho
             row_ld(fi(S, F_edgesOnVertex) + (size_t)v * 3, ev[j]);
             row_ld(fd(S, F_edgesOnVertexSign) + (size_t)v * 3, sg_[j]);
             row_ld(fd(S, X_ve_dc) + (size_t)v * 3, dc_[j]);  // dcEdge(edgesOnVertex)
-            iat[j] = fd(S, F_invAreaTriangle)[v];
-            fv[j] = fd(S, F_fVertex)[v];
+            iat[j] = ldc(fd(S, F_invAreaTriangle) + v);
+            fv[j] = ldc(fd(S, F_fVertex) + v);
         }
 #pragma unroll
         for (int j = 0; j < EPW; j++) gather2s<LP>(u, ev[j][0], ev[j][1], k, u_[j][0], u_[j][1]);
@@ -286,8 +286,8 @@ __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int ho
 #pragma unroll
     for (int j = 0; j < EPW; j++) {
         const int c = min(c0 + j, S.nCO - 1);
-        ne[j] = fi(S, F_nEdgesOnCell)[c];
-        invA[j] = fd(S, F_invAreaCell)[c];
+        ne[j] = ldc(fi(S, F_nEdgesOnCell) + c);
+        invA[j] = ldc(fd(S, F_invAreaCell) + c);
         row_ld(fi(S, F_edgesOnCell) + (size_t)c * 10, e_[j]);
         row_ld(fd(S, F_edgesOnCellSign) + (size_t)c * 10, sgn_[j]);
         row_ld(fd(S, X_ce_dv) + (size_t)c * 10, dv_[j]);  // dvEdge(edgesOnCell)
