@@ -350,7 +350,12 @@ def task_table(rep, work_dims, n_prof, physics):
     variants, tasks = {}, {}
     for name, (calls, ms) in rep.items():
         task = name.split("[")[0]
-        kw = dyn_kw(name) if task == NORTH_STAR and "[" in name else dict(kw_of.get(name, {}))
+        if task == NORTH_STAR and "[" in name:
+            kw = dyn_kw(name)
+        elif name.endswith("-old]"):  # a fused acoustic launch that leaves rtheta_pp_old (mpas_ctx.cpp)
+            kw = dict(kw_of.get(name[:-5] + "]", {}), wold=False)
+        else:
+            kw = dict(kw_of.get(name, {}))
         if physics and task == "atm_advance_acoustic_step_work":
             kw["physics"] = 1  # the acoustic task's MPAS form also updates ru_p / ruAvg
         if physics == 2 and task in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
@@ -571,7 +576,7 @@ def main():
     fused = bool(ctx.get_option("fusedamp_active"))
     fsetup = bool(ctx.get_option("fusesetup"))
     fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
-    fcopy = fsetup and bool(ctx.get_option("fusecopy")) and not decomposed
+    fcopy = fsetup and bool(ctx.get_option("fusecopy")) and not args.physics  # (decomposed too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9

@@ -149,6 +149,9 @@ struct mpas_ctx {
     // fails on a transport falls back to eager steps (graph_fallbacks)
     int graph_halo = 2;
     int64_t graph_fallbacks = 0;
+    // set when a transport refused a capture: eager steps from then on (the user's graph_halo
+    // stays as set; a new halo plan or option change clears it)
+    bool graph_refused = false;
     std::vector<std::vector<uint8_t>> seen_stale0;  // start states stepped eagerly once
     // option "trtile": the tiled transport (k_transport.hip) when the mesh allows it; the
     // tiles are rebuilt after a mesh upload or a change of the owned / interior cells.
@@ -674,11 +677,17 @@ bool hfuse_active(const mpas_ctx* c) {
 
 // timing keys: one Regent task, split where its read/write set (B_alg) differs by argument
 // (bench.py aggregates the variants per task)
-const char* acoustic_name(int small_step, bool damp = false, bool sml = false) {
+// (nold: a fused launch that does not store rtheta_pp_old -- every one but the step's last --
+// tagged "-old" so that bench.py credits it no rtheta_pp_old write)
+const char* acoustic_name(int small_step, bool damp = false, bool sml = false, bool nold = false) {
     if (sml)  // (option fusesml: the stage's set_smlstep run by this launch first)
-        return damp ? "atm_advance_acoustic_step_work[ss0+sml+damp]" : "atm_advance_acoustic_step_work[ss0+sml]";
+        return damp ? (nold ? "atm_advance_acoustic_step_work[ss0+sml+damp-old]" : "atm_advance_acoustic_step_work[ss0+sml+damp]")
+                    : (nold ? "atm_advance_acoustic_step_work[ss0+sml-old]" : "atm_advance_acoustic_step_work[ss0+sml]");
     if (damp)  // (option fusedamp: the previous substep's damping applied by this launch)
-        return small_step == 0 ? "atm_advance_acoustic_step_work[ss0+damp]" : "atm_advance_acoustic_step_work[ss>0+damp]";
+        return small_step == 0
+                   ? (nold ? "atm_advance_acoustic_step_work[ss0+damp-old]" : "atm_advance_acoustic_step_work[ss0+damp]")
+                   : (nold ? "atm_advance_acoustic_step_work[ss>0+damp-old]" : "atm_advance_acoustic_step_work[ss>0+damp]");
+    if (nold) return small_step == 0 ? "atm_advance_acoustic_step_work[ss0-old]" : "atm_advance_acoustic_step_work[ss>0-old]";
     return small_step == 0 ? "atm_advance_acoustic_step_work[ss0]" : "atm_advance_acoustic_step_work[ss>0]";
 }
 
@@ -843,7 +852,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                     });
                     vc_done = true;
                 } else {
-                    run_task(c, acoustic_name(small_step, pending, sm),
+                    run_task(c, acoustic_name(small_step, pending, sm, !wold),
                              [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev, tme, sm, wold); });
                 }
                 if (mode == 2) fb.swap_rup();
@@ -934,7 +943,8 @@ void prepare_now(mpas_ctx* c) {
 // one atm_srk3 step: replayed from a captured HIP graph when possible
 void srk3_step(mpas_ctx* c, double dt, int schedule) {
     Halo* h = c->halo.get();
-    const bool halo_graph = h && !h->loop && (h->stub ? c->graph_halo != 0 : (h->rccl && c->graph_halo == 1));
+    const bool halo_graph = h && !h->loop && (h->stub ? c->graph_halo != 0 : (h->rccl && c->graph_halo == 1)) &&
+                            !c->graph_refused;
     if (!c->graph_on || c->timing || (h && !halo_graph)) {
         srk3(c, dt, schedule);
         return;
@@ -982,6 +992,8 @@ void srk3_step(mpas_ctx* c, double dt, int schedule) {
             h->stale = g.stale0;
             h->exchanges = ex0;
             h->fields_moved = fl0;
+            h->overlapped.clear();  // (the aborted step's overlap record and race flag too)
+            h->race.clear();
             if (h->capture_miss) {  // a pack table not built yet (never built inside a capture)
                 h->capture_miss = false;
                 h->err.clear();
@@ -992,7 +1004,7 @@ void srk3_step(mpas_ctx* c, double dt, int schedule) {
             // eager steps from now on, and the step again eagerly (a real error repeats there)
             (void)hipGetLastError();
             h->err.clear();
-            c->graph_halo = 0;
+            c->graph_refused = true;
             c->graph_fallbacks++;
             srk3(c, dt, schedule);
             return;
@@ -1009,7 +1021,9 @@ void srk3_step(mpas_ctx* c, double dt, int schedule) {
             h->stale = g.stale0;
             h->exchanges = ex0;
             h->fields_moved = fl0;
-            c->graph_halo = 0;
+            h->overlapped.clear();
+            h->race.clear();
+            c->graph_refused = true;
             c->graph_fallbacks++;
             srk3(c, dt, schedule);
             return;
@@ -1174,7 +1188,13 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp_halo") == 0) c->fusedamp_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value < 0 ? 0 : value > 2 ? 2 : value;
-        else if (name && std::strcmp(name, "graph_halo") == 0) c->graph_halo = (value == 1 || value == 2) ? value : 0;
+        else if (name && std::strcmp(name, "graph_halo") == 0) {
+            c->graph_halo = (value == 1 || value == 2) ? value : 0;
+            c->graph_refused = false;
+        } else if (name && std::strcmp(name, "stub_refuse_capture") == 0) {
+            if (!c->halo || !c->halo->stub) throw Fail{MPAS_EINVAL, "stub_refuse_capture: a stub-transport context"};
+            c->halo->stub_refuse_capture = value ? 1 : 0;
+        }
         else if (name && std::strcmp(name, "stub_latency_us") == 0) {
             if (!c->halo || !c->halo->stub || value < 0 || value > 100000)
                 throw Fail{MPAS_EINVAL, "stub_latency_us: a stub-transport context and 0..100000 us"};
@@ -1295,6 +1315,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "hfuse_active") == 0) *value = hfuse_active(c);
         else if (name && std::strcmp(name, "graph_halo") == 0) *value = c->graph_halo;
         else if (name && std::strcmp(name, "graph_fallbacks") == 0) *value = c->graph_fallbacks;
+        else if (name && std::strcmp(name, "graph_refused") == 0) *value = c->graph_refused ? 1 : 0;
         else if (name && std::strcmp(name, "stub_latency_us") == 0) *value = c->halo ? c->halo->stub_latency_us : 0;
         else if (name && std::strcmp(name, "halo_state") == 0) {  // hash of the halo bookkeeping (debug)
             uint64_t hsh = 1469598103934665603ull;
@@ -1576,9 +1597,8 @@ int mpas_halo_plan(mpas_ctx* c, int kind, int peer, const int32_t* send_ids, int
         p.d_send = dev_ints(send_ids, nsend);
         p.d_recv = dev_ints(recv_ids, nrecv);
         h->peers[kind].push_back(p);
-        for (auto& kv : h->tabs)  // the pack / unpack tables follow the plan
-            if (kv.second.dev) (void)hipFree(kv.second.dev);
-        h->tabs.clear();
+        h->clear_tabs();  // the pack / unpack tables follow the plan
+        c->graph_refused = false;
         graph_drop(c);
     });
 }

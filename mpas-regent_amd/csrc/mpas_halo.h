@@ -79,6 +79,9 @@ struct Halo {
     // option "stub_latency_us": the stub's wire also waits this long on the device (a one-wave
     // kernel spinning on the wall clock), standing in for a transport's per-exchange latency
     int stub_latency_us = 0;
+    // option "stub_refuse_capture" (test hook): the stub fails an exchange made inside a stream
+    // capture, as a transport that cannot be captured does -- the graph fallback's test
+    int stub_refuse_capture = 0;
     int wall_khz = 0;  // hipDeviceAttributeWallClockRate
     std::string err;
     int64_t exchanges = 0, fields_moved = 0;
@@ -97,6 +100,7 @@ struct Halo {
     bool capture_miss = false;
 
     ~Halo();
+    void clear_tabs();  // free every pack / unpack table (a plan change)
     hipError_t reserve(int LP);  // size the packed buffers for the largest exchange
     // make every field in `gathers` that is stale fresh on the ghosts
     hipError_t before(const DevState& S, hipStream_t st, std::initializer_list<int> gathers);

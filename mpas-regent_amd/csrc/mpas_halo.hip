@@ -79,6 +79,14 @@ static int kind_of_field(int f) {
 
 static hipError_t tables_ready(const DevState& S, Halo& h, hipStream_t st, const std::vector<int>& fields);
 
+void Halo::clear_tabs() {
+    for (auto& kv : tabs) {
+        if (kv.second.dev) (void)hipFree(kv.second.dev);
+        if (kv.second.addr) (void)hipFree(kv.second.addr);
+    }
+    tabs.clear();
+}
+
 Halo::~Halo() {
     for (auto& v : peers)
         for (auto& p : v) {
@@ -87,10 +95,7 @@ Halo::~Halo() {
         }
     if (sendbuf) (void)hipFree(sendbuf);
     if (recvbuf) (void)hipFree(recvbuf);
-    for (auto& kv : tabs) {
-        if (kv.second.dev) (void)hipFree(kv.second.dev);
-        if (kv.second.addr) (void)hipFree(kv.second.addr);
-    }
+    clear_tabs();
     if (rccl) rccl_free(rccl);
     if (sock) sock_free(sock);
     if (comm) {
@@ -202,7 +207,14 @@ hipError_t Halo::launch(const DevState& S, hipStream_t st, std::initializer_list
     fn(in);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(comm, ev_ready, 0)) != hipSuccess) return e;
-    if ((e = exchange(S, comm, need)) != hipSuccess) return e;
+    if ((e = exchange(S, comm, need)) != hipSuccess) {
+        // the halo stream was forked from the task stream: join it back before failing, so
+        // that a stream capture in progress stays joined and can be ended
+        (void)hipEventRecord(ev_done, comm);
+        (void)hipStreamWaitEvent(st, ev_done, 0);
+        overlapped.clear();
+        return e;
+    }
     for (int f : need) stale[f] = 0;
     if ((e = hipEventRecord(ev_done, comm)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(st, ev_done, 0)) != hipSuccess) return e;
@@ -647,6 +659,14 @@ hipError_t Halo::exchange(const DevState& S, hipStream_t st, const std::vector<i
             return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;  // (hrecv is reused by the next exchange)
     } else if (stub) {  // the received bytes land from the send buffer (no peer)
+        if (stub_refuse_capture) {  // test hook: a transport that cannot be captured
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            (void)hipStreamIsCapturing(st, &cs);
+            if (cs != hipStreamCaptureStatusNone) {
+                err = "stub halo transport refuses the capture (option stub_refuse_capture)";
+                return hipErrorInvalidValue;
+            }
+        }
         const size_t n = (size_t)std::min(stot, rtot) * S.LP;
         if (n && (e = hipMemcpyAsync(recvbuf, sendbuf, n * sizeof(double), hipMemcpyDeviceToDevice, st)) != hipSuccess)
             return e;

@@ -15,7 +15,7 @@ roofline.achieved divides by the measured launch time.
 
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
-          part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False):
+          part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -26,7 +26,7 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                  "solve_e-v+finish": (("atm_compute_solve_diagnostics", {"part": "e"}),
                                       ("atm_rk_dynamics_substep_finish", {})),
                  "solve_e+vert_imp": (e, vi),
-                 "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}),
+                 "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}),
                                        ("atm_compute_solve_diagnostics", {"part": "vc"})),
                  "solve_e+dyn_A": (e, dA),
                  "solve_e+vert_imp+dyn_A": (e, vi, dA),
@@ -111,7 +111,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                  "invAreaCell", "cellsOnEdge", "dvEdge", "specZoneMaskCell"]
         if small_step != 0:
             reads += ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
-        writes = ["rtheta_pp_old", "rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+        # (wold False: a fused launch of option fusedamp other than the step's last, which leaves
+        # rtheta_pp_old unwritten -- the fused damping reads the stored div instead)
+        writes = (["rtheta_pp_old"] if wold else []) + ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
         if physics:  # the MPAS form (option physics = 1): the ru_p / ruAvg update of :1581-1613
             reads += ["tend_u", "tend_theta", "c_tri", "gamma_tri", "specZoneMaskEdge"]
             if small_step != 0:
@@ -243,16 +245,19 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     if schedule == 1:
         out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, "defer_out": defer4}, 1),
                 ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
+    # (fusedamp: only the step's last acoustic launch stores rtheta_pp_old, wold)
     if fusedamp and fusesml:
-        out += [("atm_advance_acoustic_step_work", {"small_step": 0, "sml": True}, 1),
-                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, "sml": True}, 2),
-                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 4),
+        out += [("atm_advance_acoustic_step_work", {"small_step": 0, "sml": True, "wold": False}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, "sml": True, "wold": False}, 2),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 1),
                 ("atm_divergence_damping_3d", {}, 1)]
     elif fusedamp:
         out += [("atm_set_smlstep_pert_variables_work", {}, 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 0}, 1),
-                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True}, 2),
-                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 4),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "wold": False}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, "wold": False}, 2),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 1),
                 ("atm_divergence_damping_3d", {}, 1)]
     else:
         out += [("atm_set_smlstep_pert_variables_work", {}, 3),

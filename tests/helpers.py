@@ -122,3 +122,42 @@ def transport_state(mesh, L, dt, seed=SEED, const=None):
         st["scalars_old"][:nC, :L] = const
     vol = 1.0 / (invA[:, None] * rdzw[None, :])
     return st, vol
+
+
+def compare_elementwise(got, ref, rtol, afloor, fields=None, skip=SCRATCH, zero_slot_excluded=()):
+    """Per-element comparison: every finite reference element must hold
+    |got - ref| <= rtol * |ref| + afloor * max|ref of that field|, NaN / inf at the same places,
+    integer fields equal.  Unlike compare_states' normwise rule, an error in a small entry is
+    not hidden behind the field's largest one.  Returns (mismatches, worst) where worst maps
+    each float field to its largest |got - ref| / (|ref| + afloor max|ref|)."""
+    bad, worst = [], {}
+    for f in FIELDS:
+        if f.name in skip or (fields is not None and f.name not in fields):
+            continue
+        a, b = got.arrays[f.name], ref.arrays[f.name]
+        if f.name in zero_slot_excluded:
+            n = got.n_of(f)
+            a, b = a[:n], b[:n]
+        if f.dtype != np.float64:
+            if not np.array_equal(a, b):
+                bad.append((f.name, "int mismatch", None))
+            continue
+        na, nb = np.isnan(a), np.isnan(b)
+        if not np.array_equal(na, nb) or not np.array_equal(np.isinf(a), np.isinf(b)):
+            bad.append((f.name, "non-finite mask differs", None))
+            continue
+        fin = np.isfinite(b)
+        if not fin.any():
+            continue
+        aa, bb = a[fin], b[fin]
+        scale = float(np.max(np.abs(bb)))
+        lim = rtol * np.abs(bb) + afloor * scale
+        d = np.abs(aa - bb)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            r = np.where(lim > 0, d / np.maximum(np.abs(bb) + afloor * scale, 1e-300), np.where(d > 0, np.inf, 0.0))
+        worst[f.name] = float(r.max()) if r.size else 0.0
+        over = d > lim
+        if over.any():
+            i = int(np.argmax(np.where(over, d - lim, -np.inf)))
+            bad.append((f.name, float(aa[i]), float(bb[i]), int(over.sum())))
+    return bad, worst

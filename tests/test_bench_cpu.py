@@ -186,3 +186,28 @@ def test_roofline_defer4_and_vdyn_accounting():
     na = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1, store_v=True, noA=True)
     assert abs(t["b_alg_GB_per_step"] - (d0o + d1 + na) / 1e9) < 1e-3
     assert set(t["variants"]) == {"[rk0+copy+d4o]", "[rk>0+d4i]", "[rk>0+v-A]"}
+
+
+def test_roofline_acoustic_rtheta_pp_old_accounting():
+    """option fusedamp: only the step's last acoustic launch stores rtheta_pp_old (the fused
+    damping reads the stored div), so the other six fused launches are credited no
+    rtheta_pp_old write; the library tags them "-old" and bench.py reads the tag"""
+    import bench
+    from mpasdyn import roofline
+    dims = (163842, 491520, 327680, 56)
+    c3 = 8 * 163842 * 56
+    a = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=1, damp=True)
+    b = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=1, damp=True, wold=False)
+    assert a - b == c3
+    for sml in (True, False):
+        fused = roofline.b_alg_step(dims, 1, 0, 0, True, True, sml, True, True)
+        sched = roofline.step_schedule(1, 0, 0, True, True, sml, True, True)
+        n_ac = sum(n for t, kw, n in sched if t == "atm_advance_acoustic_step_work")
+        n_old = sum(n for t, kw, n in sched if t == "atm_advance_acoustic_step_work" and kw.get("wold", True))
+        assert (n_ac, n_old) == (7, 1)
+        # against the same schedule with every launch credited the write
+        full = sum(roofline.b_alg(t, dims, **{k: v for k, v in kw.items() if k != "wold"}) * n for t, kw, n in sched)
+        assert full - fused == 6 * c3
+    rep = {"atm_advance_acoustic_step_work[ss>0+damp-old]": (3, 1.5), "atm_advance_acoustic_step_work[ss>0+damp]": (1, 0.5)}
+    t = bench.task_table(rep, dims, 1, physics=False)["atm_advance_acoustic_step_work"]
+    assert abs(t["b_alg_GB_per_step"] - (3 * b + a) / 1e9) < 1e-3

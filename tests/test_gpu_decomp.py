@@ -314,8 +314,8 @@ def test_stub_graph_start_states(x1_2562, between):
             lib.setup_subdomain(ctx, d, 1)
             lib.halo_stub(ctx)
             ctx.set_option("graph_halo", graph)
-            if between == "fusedamp_halo":
-                ctx.set_option("fusedamp_halo", 1)
+            if between == "fusedamp_halo":  # (the default is 1: the non-fused decomposed path under replay)
+                ctx.set_option("fusedamp_halo", 0)
             ctx.upload(loc)
             for i in range(9):
                 T.atm_srk3(ctx, 720.0, 1 if between != "schedules" or i % 2 else 0)
@@ -330,6 +330,41 @@ def test_stub_graph_start_states(x1_2562, between):
     assert not bad, bad[:6]
     assert out[1][1] == out[0][1]
     assert out[1][2] >= 1 and out[1][3] >= 2 and out[0][2] == 0
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_stub_capture_refused_falls_back(x1_2562, overlap):
+    """a transport that refuses the capture of a decomposed step (test hook
+    stub_refuse_capture): the capture is abandoned -- with the overlap on, after the halo
+    stream was forked, which must be joined back so that the capture can be ended
+    -- the step runs again eagerly, graph_fallbacks counts it once, the user's graph_halo is
+    kept, no race is left behind, and every step equals the eager run bit for bit"""
+    st = state(x1_2562, 56, "random")
+    d = decomp.Decomposition(st, 4)
+    out = {}
+    for refuse in (1, 0):
+        loc = d.local_state(1)
+        with lib.Context(*d.n_local(1), st.L) as ctx:
+            lib.setup_subdomain(ctx, d, 1)
+            lib.halo_stub(ctx)
+            ctx.set_option("overlap", overlap)
+            ctx.set_option("graph_halo", 2 if refuse else 0)
+            ctx.set_option("stub_refuse_capture", refuse)
+            ctx.upload(loc)
+            for _ in range(5):
+                T.atm_srk3(ctx, 720.0, 1)
+            T.atm_compute_solve_diagnostics(ctx, False, 2)  # (a task after the fallback: no stale race)
+            ctx.sync()
+            ctx.download(loc)
+            out[refuse] = (loc, lib.halo_stats(ctx), ctx.get_option("graph_fallbacks"),
+                           ctx.get_option("graph_captures"), ctx.get_option("graph_halo"),
+                           ctx.get_option("graph_refused"))
+    bad = compare_states(out[1][0], out[0][0], rtol=0.0)
+    assert not bad, bad[:6]
+    assert out[1][1] == out[0][1]
+    assert out[1][2] == 1 and out[1][3] == 0, out[1][2:]
+    assert out[1][4] == 2 and out[1][5] == 1  # (the option as set; the refusal recorded apart)
+    assert out[0][2] == 0
 
 
 def test_rccl_graph_capture_single_rank(x1_2562):
