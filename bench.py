@@ -205,6 +205,54 @@ def free_port_range(n):
     raise RuntimeError("no free port range")
 
 
+class Watchdog:
+    """a bounded wait on a blocking call that cannot time out by itself (ncclCommInitRank, the
+    first exchange of the first step): unless cancelled within `seconds`, the rank prints a
+    named error and exits with status 3 -- the launcher (torchrun, or spawn_ranks) then ends
+    the other ranks, instead of the job hanging until an outer limit kills it"""
+
+    def __init__(self, seconds, what, rank):
+        import threading
+        self.what, self.rank = what, rank
+        self.t = threading.Timer(seconds, self._fire, args=(seconds,))
+        self.t.daemon = True
+        self.t.start()
+
+    def _fire(self, seconds):
+        print(f"bench.py rank {self.rank}: {self.what} did not complete within {seconds:.0f} s "
+              f"(a rank missing or a transport that cannot connect); exiting", file=sys.stderr, flush=True)
+        os._exit(3)
+
+    def cancel(self):
+        self.t.cancel()
+
+
+def dump_rows(path, ctx, st, gids, steps, extra):
+    """tests (--dump): one 64-bit fingerprint per owned row of every fp64 field -- the row's
+    bits (-0.0 as +0.0, every NaN as one NaN) under a fixed linear hash -- with the rows'
+    global ids, so that the owned parts of N ranks can be compared with one context bit for
+    bit without moving the fields themselves (tests/test_gpu_bench.py)"""
+    from mpasdyn.registry import FIELDS
+    from mpasdyn.state import HostState
+    out = {f"gid_{k}": np.asarray(v, dtype=np.int64) for k, v in gids.items()}
+    rng = np.random.default_rng(12345)
+    for f in FIELDS:
+        if f.entity is None or f.dtype != np.float64:
+            continue
+        got = HostState(*st.dims(), names=[f.name])  # (one field at a time: host memory)
+        ctx.download(got)
+        a = np.asarray(got.arrays[f.name])[:len(gids[f.entity])]
+        a = np.where(np.isnan(a), np.nan, a) + 0.0  # (canonical NaN, -0.0 -> +0.0)
+        bits = np.ascontiguousarray(a.reshape(len(a), -1)).view(np.uint64)
+        mult = rng.integers(1, 2**63, size=bits.shape[1], dtype=np.uint64) | np.uint64(1)
+        with np.errstate(over="ignore"):
+            out[f.name] = (bits * mult[None, :]).sum(axis=1, dtype=np.uint64)
+    out["steps"] = np.int64(steps)
+    for k, v in extra.items():
+        out[k] = np.asarray(v)
+    np.savez(path, **out)
+
+
 def spawn_ranks(n, argv):
     """start N rank processes of this script (no GPU touched here); rank 0 inherits
     stdout (the JSON line), the others write theirs to stderr.  Returns the exit code."""
@@ -412,6 +460,10 @@ def main():
                          "dynamics (every quirk fixed)")
     ap.add_argument("--transport", action="store_true",
                     help="physics = 1 plus the monotonic transport of the 8 scalars in every step")
+    ap.add_argument("--dump", metavar="DIR", help=argparse.SUPPRESS)  # (tests: per-row fingerprints, see dump_rows)
+    ap.add_argument("--init-timeout", type=float, default=float(os.environ.get("MPAS_INIT_TIMEOUT", "300")),
+                    help="seconds the communicator set-up and the first (exchanging) step may take before the rank "
+                         "exits non-zero with a named error instead of hanging")
     args = ap.parse_args()
     if args.transport and not args.physics:
         args.physics = 1
@@ -484,7 +536,9 @@ def main():
             uid = lib.rccl_unique_id() if rank == 0 else None
             if rv is not None:
                 uid = rv.bcast(uid)
+            wd = Watchdog(args.init_timeout, "ncclCommInitRank", rank)
             lib.halo_rccl(ctx, world, rank, uid)
+            wd.cancel()
         overlap = int(os.environ.get("MPAS_OVERLAP", "1"))
         ctx.set_option("overlap", overlap)
         own = dec.n_owned(rank)
@@ -511,8 +565,14 @@ def main():
     hip = Hip()
     stream = ctx.stream()
 
-    for _ in range(args.warmup):
+    # (the first step makes the first halo exchanges: bounded like the communicator set-up)
+    wd = Watchdog(args.init_timeout, "the first RK3 step (its halo exchanges)", rank) if decomposed else None
+    for i in range(args.warmup):
         T.atm_srk3(ctx, dt, 1)
+        if i == 0 and wd is not None:
+            ctx.sync()
+            wd.cancel()
+            wd = None
     ctx.sync()
 
     def barrier():
@@ -530,9 +590,24 @@ def main():
     for i in range(args.steps):
         T.atm_srk3(ctx, dt, 1)
         hip.record(evs[i + 1], stream)
+        if wd is not None:  # (no warm-up: the first timed step made the first exchanges)
+            ctx.sync()
+            wd.cancel()
+            wd = None
     ctx.sync()
     hip.device_sync()
     barrier()
+    if args.dump:  # (after the timed steps, before the per-task timing steps)
+        os.makedirs(args.dump, exist_ok=True)
+        if decomposed:
+            gids = {k: dec.owned[rank][k] for k in ("cell", "edge", "vertex")}
+            ex = lib.halo_stats(ctx)[0]
+        else:
+            gids = {"cell": np.arange(m.nCells), "edge": np.arange(m.nEdges), "vertex": np.arange(m.nVertices)}
+            ex = 0
+        dump_rows(os.path.join(args.dump, f"rank{rank}.npz"), ctx, st, gids, args.warmup + args.steps,
+                  {"exchanges": ex, "world": world})
+        barrier()
     t_wall = time.perf_counter() - t0
     step_ms = [hip.elapsed_ms(evs[i], evs[i + 1]) for i in range(args.steps)]
     ms_median = statistics.median(step_ms)

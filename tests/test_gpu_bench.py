@@ -13,9 +13,10 @@ KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
         "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"}
 
 
-def run_bench(*args):
+def run_bench(*args, timeout=110):
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "2", "--warmup", "1",
-                        "--no-cpu-baseline", "--traffic", "off", *args], capture_output=True, text=True, timeout=110, cwd=REPO)
+                        "--no-cpu-baseline", "--traffic", "off", *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=REPO)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, f"stdout must be ONE JSON line, got {len(lines)}: {p.stdout[:500]}"
@@ -81,3 +82,64 @@ def test_bench_roofline_is_dyn_tend_with_live_traffic():
     # measured traffic cannot be below the distinct arrays the task must touch (minus the
     # 2-D mesh rows, which may stay in cache), nor absurdly above
     assert 0.5 * r["b_alg_per_launch_GB"] < r["traffic"] < 10 * r["b_alg_per_launch_GB"]
+
+
+@pytest.mark.gpu
+def test_bench_8rank_headline_socket(tmp_path):
+    """the driver's 8-GPU flow at the headline size, rehearsed on the one
+    GPU -- bench.py --gpus 8 spawns 8 rank processes, each splits x1.163842 x 56 8 ways
+    (the split the 8-GPU run uses), builds its pack / unpack address tables and exchanges
+    halos (host-staged socket transport in RCCL's place).  The owned rows of the 8 ranks,
+    assembled by global id, equal one undecomposed context bit for bit (exact mode; per-row
+    64-bit fingerprints of every fp64 field, bench.py dump_rows), and every rank made the
+    exchanges per step the in-process loopback split makes (x1.2562, 2 parts: the count is
+    the launch sequence's, not the mesh's)"""
+    import numpy as np
+    sys.path.insert(0, REPO)
+    import bench
+    from mpasdyn import decomp, lib
+    from mpasdyn import tasks as T
+    from mpasdyn.registry import FIELDS
+
+    common = ("--steps", "1", "--warmup", "1", "--exact", "1", "--ncells", "163842")
+    d8 = run_bench("--gpus", "8", "--halo", "socket", *common, "--dump", str(tmp_path / "r8"), timeout=150)
+    assert d8["n_gpus"] == 8 and d8["config"]["parallelism"] == "decomposed8" and d8["value"] > 0
+    run_bench(*common, "--dump", str(tmp_path / "r1"), timeout=100)
+    one = np.load(tmp_path / "r1" / "rank0.npz")
+    names = [f.name for f in FIELDS if f.entity is not None and f.dtype == np.float64]
+    seen = {k: np.zeros(len(one[f"gid_{k}"]), dtype=bool) for k in ("cell", "edge", "vertex")}
+    ex = []
+    for r in range(8):
+        part = np.load(tmp_path / "r8" / f"rank{r}.npz")
+        assert int(part["steps"]) == int(one["steps"]) == 2 and int(part["world"]) == 8
+        ex.append(int(part["exchanges"]))
+        for k in seen:
+            seen[k][part[f"gid_{k}"]] = True
+        bad = [n for n in names
+               if not np.array_equal(part[n], one[n][part["gid_" + next(f.entity for f in FIELDS if f.name == n)]])]
+        assert not bad, f"rank {r}: owned rows differ from the single context in {bad[:8]}"
+    assert all(v.all() for v in seen.values())  # (the 8 ranks own every entity)
+    # the exchanges of the same two steps in the in-process loopback split
+    m, st = bench.build_inputs(2562, 56)
+    dec = decomp.Decomposition(st, 2)
+    ctxs = [lib.Context(*dec.n_local(r), 56) for r in range(2)]
+    try:
+        import threading
+        for r, c in enumerate(ctxs):
+            c.set_option("exact", 1)
+            lib.setup_subdomain(c, dec, r)
+            bench.upload_inputs(c, dec.local_state(r))
+        lib.halo_loopback(ctxs)
+        th = [threading.Thread(target=lambda c=c: [T.atm_srk3(c, bench.dt_for(2562), 1) for _ in range(2)])
+              for c in ctxs]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        for c in ctxs:
+            c.sync()
+        loop = lib.halo_stats(ctxs[0])[0]
+    finally:
+        for c in ctxs:
+            c.close()
+    assert ex == [loop] * 8, (ex, loop)

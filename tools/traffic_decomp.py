@@ -164,6 +164,26 @@ def main():
         res[lk] = {"kernels": per, "B_alg_GB": balg / 1e9, "compulsory_GB": task / 1e9,
                    "intermediates_GB": (tot_kernel - task) / 1e9, "refetch_GB": (meas_tot - tot_kernel) / 1e9,
                    "measured_GB": meas_tot / 1e9, "measured_over_B_alg": meas_tot / balg}
+    # per array: which kernel writes it, which read it, and the bytes it
+    # moves beyond its compulsory once -- each kernel touching it moves its stored size (the
+    # distinct bytes, no refetch); a scratch array (X_*) has no compulsory part
+    arrays = {}
+    for lk in kinds:
+        rows = {}
+        for name, rd, wr in KERN[a.layout][lk]:
+            for f in dict.fromkeys(rd + wr):
+                r = rows.setdefault(f, {"writers": [], "readers": [], "GB": col(field_kind(f)) / 1e9})
+                if f in wr:
+                    r["writers"].append(name)
+                if f in rd:
+                    r["readers"].append(name)
+        for f, r in rows.items():
+            touches = len(set(r["writers"]) | set(r["readers"])) + sum(
+                1 for w in set(r["writers"]) if w in r["readers"])  # (read and written by one kernel: twice)
+            r["extra_GB"] = r["GB"] * (touches - (0 if f.startswith("X_") else 1))
+        arrays[lk] = dict(sorted(((f, r) for f, r in rows.items() if r["extra_GB"] > 0),
+                                 key=lambda x: -x[1]["extra_GB"]))
+        res[lk]["arrays"] = arrays[lk]
     print(f"dyn_tend traffic decomposition ({a.layout}), x1.{nC} x {L}, LP {a.lp}, GB per launch")
     for lk, d in res.items():
         print(f"{lk:7s} measured {d['measured_GB']:6.2f} = compulsory {d['compulsory_GB']:5.2f} + intermediates "
@@ -174,6 +194,12 @@ def main():
             rf = "--" if k["refetch_GB"] is None else f"{k['refetch_GB']:5.2f}"
             l2 = "--" if k["l2_hit"] is None else f"{k['l2_hit']:.2f}"
             print(f"    {k['kernel']}: measured {ms}  distinct {k['compulsory_GB']:5.2f}  refetch {rf}  L2 hit {l2}")
+    for lk, rows in arrays.items():
+        print(f"{lk}: arrays moved more than once (extra GB per launch beyond the compulsory once)")
+        for f, r in rows.items():
+            print(f"    {f:22s} {r['extra_GB']:5.3f}  written by {','.join(r['writers']) or '-':6s} "
+                  f"read by {','.join(r['readers'])}")
+        print(f"    sum {sum(r['extra_GB'] for r in rows.values()):.2f}")
     if a.json:
         json.dump(res, open(a.json, "w"), indent=1)
 
