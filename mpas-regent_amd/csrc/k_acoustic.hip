@@ -209,7 +209,10 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         wn *= (fzm * zz + fzp * lvl_dn<LP>(zz, k));
         if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
             colk(fw(S, F_w), c) = wn;
+            if (k == L) keep_put<LP>(S, F_w, KC, c, wn);  // (w's level L changes: its keep tail too)
             w = wn;
+        } else if ((k > L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone)) {
+            colk(fw(S, F_w), c) = 0.0;  // (the padding's content: the column's last line written whole)
         }
     }
     // the w tendency: the state w in the reference and under physics = 1 (Q8), tend_w under
@@ -226,7 +229,8 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
 
     // :1615-1636
     const double rtpo = (small_step == 0) ? 0 : rtp;
-    if (k != L && (MODE == 0 || wold)) colk(fw(S, F_rtheta_pp_old), c) = PADW(rtpo);  // (PADW: mpas_dev.h)
+    // (level L: the kept value, keep tails in mpas_dev.h -- every line of the column whole)
+    if (MODE == 0 || wold) colk(fw(S, F_rtheta_pp_old), c) = KEEPW(rtpo, keepv<LP>(S, F_rtheta_pp_old, KC, c));
     // MODE 1/2: this substep's div (:1755) for the damping applied by the next substep
     auto store_div = [&](double rtp_new) {
         if constexpr (MODE != 0) colk(fw(S, X_dvA), c) = kl ? -(rtp_new - rtpo) : 0.0;
@@ -247,10 +251,8 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             rwp = rwp + dts * tw;
             ww = ww + 0.5 * (1.0 + epssm) * rwp;
         }
-        if (k != L) {
-            colk(rpp_f, c) = PADW(rpp);
-            colk(rtp_f, c) = PADW(rtp);
-        }
+        colk(rpp_f, c) = KEEPW(rpp, keepv<LP>(S, F_rho_pp, KC, c));
+        colk(rtp_f, c) = KEEPW(rtp, keepv<LP>(S, F_rtheta_pp, KC, c));
         colk(rwp_f, c) = PADW(rwp);
         colk(ww_f, c) = PADW(ww);
         store_div(rtp);
@@ -341,9 +343,9 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         }
         const double r_p = lvl_up<LP>(r, k);
         // (paired 16-B stores, every lane; level L of rho_pp / rtheta_pp keeps its value)
-        put2<LP>(rpp_f, c, rtp_f, c, k, PADW(rs - cofrz * (r_p - r)), PADW(ts - rdzw * (coftz_p * r_p - coftz * r)),
-                 k != L, k != L);
-        put2<LP>(rwp_f, c, ww_f, c, k, PADW(r), PADW(ww), true, true);
+        put2f<LP>(rpp_f, c, rtp_f, c, k, KEEPW(rs - cofrz * (r_p - r), keepv<LP>(S, F_rho_pp, KC, c)),
+                 KEEPW(ts - rdzw * (coftz_p * r_p - coftz * r), keepv<LP>(S, F_rtheta_pp, KC, c)));
+        put2f<LP>(rwp_f, c, ww_f, c, k, PADW(r), PADW(ww));
         return;
     }
 
@@ -416,8 +418,9 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
     if (k < L && k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
     // (paired 16-B stores, every lane; level L of rho_pp / rtheta_pp keeps its value)
     const double rtp_new = ts - rdzw * (coftz_p * rwp_p - coftz * x);
-    put2<LP>(rpp_f, c, rtp_f, c, k, PADW(rs - cofrz * (rwp_p - x)), PADW(rtp_new), k != L, k != L);
-    put2<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww), true, true);
+    put2f<LP>(rpp_f, c, rtp_f, c, k, KEEPW(rs - cofrz * (rwp_p - x), keepv<LP>(S, F_rho_pp, KC, c)),
+             KEEPW(rtp_new, keepv<LP>(S, F_rtheta_pp, KC, c)));
+    put2f<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww));
     store_div(rtp_new);
 }
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>

@@ -27,6 +27,15 @@ __device__ __forceinline__ void st64(double* d, size_t i, double2 v, Pair64 q) {
     if ((int)(i & 31) != q.pair) *(double2*)(d + 2 * i) = v;
     else d[2 * i + (1 - q.el)] = q.el ? v.x : v.y;
 }
+// st64 with the level-L element written too, with kl (its kept value: keep tails, mpas_dev.h):
+// every line of the column whole
+__device__ __forceinline__ void st64k(double* d, size_t i, double2 v, Pair64 q, double kl) {
+    if ((int)(i & 31) == q.pair) {
+        if (q.el) v.y = kl;
+        else v.x = kl;
+    }
+    *(double2*)(d + 2 * i) = v;
+}
 
 // ---------------------------------------------------------------- vert_imp
 // one column of atm_compute_vert_imp_coefs from its loaded inputs (k_vert_imp, and the
@@ -103,12 +112,18 @@ __device__ __forceinline__ void vi_column(const DevState& S, int c, int k, doubl
     // written: every level but L (padding levels: zeros, full 64-B sectors; see PADW); the
     // tridiagonal coefficients not at level 0 either, gamma_tri 0.0 there.  Paired 16-B
     // stores (put2: every lane takes part)
-    const bool w_all = live && k != L, w_1 = w_all && k != 0;
-    put2<LP>(fw(S, F_coftz), c, fw(S, F_cofwt), c, k, PADW(coftz), PADW(cofwt), w_all, w_all);
-    put2<LP>(fw(S, F_cofwr), c, fw(S, F_cofwz), c, k, PADW(cofwr), PADW(cofwz), w_1, w_1);
-    put2<LP>(fw(S, F_a_tri), c, fw(S, F_b_tri), c, k, PADW(a), PADW(b), w_1, w_1);
-    put2<LP>(fw(S, F_c_tri), c, fw(S, F_alpha_tri), c, k, PADW(cc), PADW(alpha), w_1, w_1);
-    if (w_all) colk(fw(S, F_gamma_tri), c) = k == 0 ? 0.0 : PADW(gamma);
+    // (the slots the reference leaves -- level L, and level 0 of the tridiagonal coefficients --
+    // written with their kept values: keep tails, mpas_dev.h; every line of a column whole)
+    auto kL = [&](int f) { return keepv<LP>(S, f, KC, c); };
+    auto k0 = [&](int f) { return keepv<LP>(S, f, KC, c, true); };
+    put2<LP>(fw(S, F_coftz), c, fw(S, F_cofwt), c, k, KEEPW(coftz, kL(F_coftz)), KEEPW(cofwt, kL(F_cofwt)), live, live);
+    put2<LP>(fw(S, F_cofwr), c, fw(S, F_cofwz), c, k, KEEPW0(cofwr, k0(F_cofwr), kL(F_cofwr)),
+             KEEPW0(cofwz, k0(F_cofwz), kL(F_cofwz)), live, live);
+    put2<LP>(fw(S, F_a_tri), c, fw(S, F_b_tri), c, k, KEEPW0(a, k0(F_a_tri), kL(F_a_tri)),
+             KEEPW0(b, k0(F_b_tri), kL(F_b_tri)), live, live);
+    put2<LP>(fw(S, F_c_tri), c, fw(S, F_alpha_tri), c, k, KEEPW0(cc, k0(F_c_tri), kL(F_c_tri)),
+             KEEPW0(alpha, k0(F_alpha_tri), kL(F_alpha_tri)), live, live);
+    if (live) colk(fw(S, F_gamma_tri), c) = k == 0 ? 0.0 : KEEPW(gamma, kL(F_gamma_tri));
     if (live && c == 0 && k < L) fw(S, F_cofrz)[k] = cofrz;
 }
 
@@ -193,8 +208,14 @@ __device__ __forceinline__ void finish64_body(const DevState& S, int substep, in
     const size_t n = (size_t)(cells ? S.nCO : S.nEO) * 32;
     double *avg = fw(S, cells ? F_wwAvg : F_ruAvg), *avgS = fw(S, cells ? F_wwAvg_split : F_ruAvg_split);
     const bool restore = substep < split, last = substep == split, same = substep == 1 && inv_split == 1.0;
+    const int kind = cells ? KC : KE;
     for (size_t i = (size_t)b * 256 + threadIdx.x; i < n; i += (size_t)nb * 256) {
-        auto cp = [&](int from, int to) { st64(fw(S, to), i, ((const double2*)fd(S, from))[i], q); };
+        // (level L: the kept value of the destination -- its keep tail, or for the averages the
+        // value just loaded -- so every line of a column is written whole)
+        const int col = (int)(i >> 5);
+        auto cp = [&](int from, int to) {
+            st64k(fw(S, to), i, ((const double2*)fd(S, from))[i], q, keepv<64>(S, to, kind, col));
+        };
         if (restore) {
             if (cells) {
                 cp(F_rw, F_rw_save);
@@ -214,8 +235,8 @@ __device__ __forceinline__ void finish64_body(const DevState& S, int substep, in
             const double2 b = ((const double2*)avgS)[i];
             sv = make_double2(a.x + b.x, a.y + b.y);
         }
-        st64(avgS, i, sv, q);
-        if (last && !same) st64(avg, i, make_double2(sv.x * inv_split, sv.y * inv_split), q);
+        st64k(avgS, i, sv, q, keepv<64>(S, cells ? F_wwAvg_split : F_ruAvg_split, kind, col));
+        if (last && !same) st64k(avg, i, make_double2(sv.x * inv_split, sv.y * inv_split), q, q.el ? a.y : a.x);
         if (cells && last && S.physics != 2) cp(F_rho_zz_old_split, F_rho_zz);
     }
 }
@@ -263,6 +284,7 @@ __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int ho
             }
             vort *= iat[j];
             // (one paired 16-B store, every lane; level L keeps its value)
+            // (level L left unwritten, as the reference: the keep tails cost this kernel 12 %)
             put2<LP>(fw(S, F_vorticity), v, fw(S, F_pv_vertex), v, k, PADW(vort), PADW(fv[j] + vort), k != L, k != L);
             if (k == L) continue;
             if (hollingsworth_part) {
@@ -386,12 +408,15 @@ __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
         const int e = m.base + j;
         if (e >= S.nEO) break;  // (wave-uniform)
         const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
-        const bool w = k != L;  // (padding levels k > L: zeros, PADW)
-        put2<LP>(fw(S, F_h_edge), e, fw(S, F_ke_edge), e, k, PADW(0.5 * (h1[j] + h2[j])), PADW(efac * (uu[j] * uu[j])),
-                 w, w);
-        if (MD && w) colk(fw(S, F_rho_edge), e) = PADW(0.5 * (h1[j] + h2[j]));
-        if (RECON_V) put2<LP>(fw(S, F_v), e, fw(S, F_pv_edge), e, k, PADW(vv[j]), PADW(0.5 * (pv1[j] + pv2[j])), w, w);
-        else if (w) colk(fw(S, F_pv_edge), e) = PADW(0.5 * (pv1[j] + pv2[j]));
+        // (padding levels k > L: zeros; level L: the kept values, keep tails in mpas_dev.h)
+        auto kL = [&](int f) { return keepv<LP>(S, f, KE, e); };
+        put2f<LP>(fw(S, F_h_edge), e, fw(S, F_ke_edge), e, k, KEEPW(0.5 * (h1[j] + h2[j]), kL(F_h_edge)),
+                 KEEPW(efac * (uu[j] * uu[j]), kL(F_ke_edge)));
+        if (MD) colk(fw(S, F_rho_edge), e) = KEEPW(0.5 * (h1[j] + h2[j]), kL(F_rho_edge));
+        if (RECON_V)
+            put2f<LP>(fw(S, F_v), e, fw(S, F_pv_edge), e, k, KEEPW(vv[j], kL(F_v)),
+                     KEEPW(0.5 * (pv1[j] + pv2[j]), kL(F_pv_edge)));
+        else colk(fw(S, F_pv_edge), e) = KEEPW(0.5 * (pv1[j] + pv2[j]), kL(F_pv_edge));
     }
 }
 
@@ -414,11 +439,12 @@ __device__ __forceinline__ void setup_vi_body(const DevState& S, int ncb, double
         if (copies) {
             double ru, u;
             gather2<LP>(fd(S, F_ru), e, fd(S, F_u), e, k, ru, u);
-            put2<LP>(fw(S, F_ru_save), e, fw(S, F_u_2), e, k, PADW(ru), PADW(u), k != L, k != L);
+            put2f<LP>(fw(S, F_ru_save), e, fw(S, F_u_2), e, k, KEEPW(ru, keepv<LP>(S, F_ru_save, KE, e)),
+                     KEEPW(u, keepv<LP>(S, F_u_2, KE, e)));
         }
         if constexpr (MD) {  // :491-501 (Q25 fixed): qtot(cell1) = qtot(cell2) = 0 just written
             const double q1 = 0.0, q2 = 0.0, qtotal = 0.5 * (q1 + q2);
-            if (k != L) colk(fw(S, F_cqu), e) = k > L ? 0.0 : 1.0 / (1.0 + qtotal);
+            colk(fw(S, F_cqu), e) = KEEPW(1.0 / (1.0 + qtotal), keepv<LP>(S, F_cqu, KE, e));
         }
         return;
     }
@@ -435,16 +461,22 @@ __device__ __forceinline__ void setup_vi_body(const DevState& S, int ncb, double
     gather2<LP>(fd(S, F_exner_base), c, fd(S, F_gamma_tri), c, k, exb, gamma_old);
     const double coftz_old = colk(fd(S, F_coftz), c);
     // :773-777 the save copies (every level but L; padding levels carry zeros either way)
-    const bool cp = live && k != L;
-    put2<LP>(fw(S, F_rw_save), c, fw(S, F_rtheta_p_save), c, k, PADW(rw), PADW(rtp), cp, cp);
-    put2<LP>(fw(S, F_rho_p_save), c, fw(S, F_w_2), c, k, PADW(rp), PADW(w), cp, cp);
-    put2<LP>(fw(S, F_theta_m_2), c, fw(S, F_rho_zz_2), c, k, PADW(tm), PADW(rz), cp, cp);
-    if constexpr (MD) put2<LP>(fw(S, F_rho_zz_old_split), c, fw(S, F_theta_m_save), c, k, PADW(rz), PADW(tm), cp, cp);
-    else if (cp) colk(fw(S, F_rho_zz_old_split), c) = PADW(rz);
+    // (level L: the kept values, keep tails in mpas_dev.h -- every line of a column whole)
+    auto kL = [&](int f) { return keepv<LP>(S, f, KC, c); };
+    put2<LP>(fw(S, F_rw_save), c, fw(S, F_rtheta_p_save), c, k, KEEPW(rw, kL(F_rw_save)),
+             KEEPW(rtp, kL(F_rtheta_p_save)), live, live);
+    put2<LP>(fw(S, F_rho_p_save), c, fw(S, F_w_2), c, k, KEEPW(rp, kL(F_rho_p_save)), KEEPW(w, kL(F_w_2)), live, live);
+    put2<LP>(fw(S, F_theta_m_2), c, fw(S, F_rho_zz_2), c, k, KEEPW(tm, kL(F_theta_m_2)), KEEPW(rz, kL(F_rho_zz_2)),
+             live, live);
+    if constexpr (MD)
+        put2<LP>(fw(S, F_rho_zz_old_split), c, fw(S, F_theta_m_save), c, k, KEEPW(rz, kL(F_rho_zz_old_split)),
+                 KEEPW(tm, kL(F_theta_m_save)), live, live);
+    else if (live) colk(fw(S, F_rho_zz_old_split), c) = KEEPW(rz, kL(F_rho_zz_old_split));
     // :473-489 (k_moist's expressions): qtot = 0; cqw(k > 0) from the two zeroed qtot
     const double q_k = 0.0, q_km1 = 0.0, qtotal = 0.5 * (q_k + q_km1);
     const double cqw = k > L ? 0.0 : 1.0 / (1.0 + qtotal), qtot = 0.0;
-    put2<LP>(fw(S, F_qtot), c, fw(S, F_cqw), c, k, qtot, cqw, cp, cp && k > 0);
+    put2<LP>(fw(S, F_qtot), c, fw(S, F_cqw), c, k, KEEPW(qtot, kL(F_qtot)),
+             KEEPW0(cqw, keepv<LP>(S, F_cqw, KC, c, true), kL(F_cqw)), live, live);
     // (cqw is used at 0 < k < L only, qtot at k < L: the values just written)
     vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2,
                          live);

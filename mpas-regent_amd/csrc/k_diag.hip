@@ -22,6 +22,43 @@ struct RecK {
 // rho_zz = 1.0 of :1790-1792 (our zero slot).  MPASV (option physics = 1, oracle
 // ora_mpas_recover): w(0) = 0, w(L) = 0, rw/wwAvg/w of the interior interfaces only,
 // exner = (zz rgas/p0 (rtheta_p + rtheta_base))^rcv
+// the MPAS form of k_recover_cells for one lane, every level stored: levels 1..L-1 the
+// recovered values (:1800-1820 with Q24 fixed), w(0) = w(L) = 0, rw / wwAvg at levels 0 and L
+// the values they hold (wwAvg: just loaded; rw: its keep tails), every other field at level L
+// its keep tail, the padding levels 0.0 (mpas_dev.h keep tails)
+template <int LP>
+__device__ __forceinline__ void recover_cells_mpas(const DevState& S, const RecK& a, int c, int k, double zz,
+                                                   double zz_m, double fzm, double fzp, double rps, double rpp,
+                                                   double rb, double ww, double rws, double rwp, double rtps,
+                                                   double rtpp, double rtb, double rtd, double exb) {
+    const int L = S.L;
+    auto kL = [&](int f) { return keepv<LP>(S, f, KC, c); };
+    const double rho_p = rps + rpp;
+    const double rho_zz = rho_p + rb;
+    double wwAvg = ww;
+    wwAvg *= a.invNs;
+    wwAvg += rws;
+    const double rw = rws + rwp;
+    const double w = rw / (fzm * zz + fzp * zz_m);
+    colk(fw(S, F_rho_p), c) = KEEPW(rho_p, kL(F_rho_p));
+    colk(fw(S, F_rho_zz), c) = KEEPW(rho_zz, kL(F_rho_zz));
+    colk(fw(S, F_wwAvg), c) = (k == 0 || k == L) ? ww : PADW(wwAvg);
+    colk(fw(S, F_rw), c) = KEEPW0(rw, keepv<LP>(S, F_rw, KC, c, true), kL(F_rw));
+    colk(fw(S, F_w), c) = (k == 0 || k >= L) ? 0.0 : w;
+    if (a.rk_step == 2) {
+        const double rtheta_p = rtps + rtpp - a.dt * rho_zz * rtd;
+        colk(fw(S, F_rtheta_p), c) = KEEPW(rtheta_p, kL(F_rtheta_p));
+        colk(fw(S, F_theta_m), c) = KEEPW((rtheta_p + rtb) / rho_zz, kL(F_theta_m));
+        const double exner = pow(zz * a.rgas_p0 * (rtheta_p + rtb), a.rcv);
+        colk(fw(S, F_exner), c) = KEEPW(exner, kL(F_exner));
+        colk(fw(S, F_pressure_p), c) = KEEPW(zz * a.rgas * (exner * rtheta_p + rtb * (exner - exb)), kL(F_pressure_p));
+    } else {
+        const double rtheta_p = rtps + rtpp;
+        colk(fw(S, F_rtheta_p), c) = KEEPW(rtheta_p, kL(F_rtheta_p));
+        colk(fw(S, F_theta_m), c) = KEEPW((rtheta_p + rtb) / rho_zz, kL(F_theta_m));
+    }
+}
+
 template <int LP, bool MPASV>
 __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     ColMap<LP> m(S, KC);
@@ -37,7 +74,12 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     const double rtb = colk(fd(S, F_rtheta_base), c);
     const double rtd = a.rk_step == 2 ? colk(fd(S, F_rt_diabatic_tend), c) : 0.0;
     const double exb = a.rk_step == 2 ? colk(fd(S, F_exner_base), c) : 0.0;
-    if (MPASV && k == L) colk(fw(S, F_w), c) = 0.0;
+    if (MPASV && k == L) keep_put<LP>(S, F_w, KC, c, 0.0);  // (w's level L changes: its keep tail too)
+    if (MPASV) {  // every level of every column written (level L / 0 with their kept values, the
+                  // padding with zeros: keep tails, mpas_dev.h) -- no partially written line
+        recover_cells_mpas<LP>(S, a, c, k, zz, zz_m, fzm, fzp, rps, rpp, rb, ww, rws, rwp, rtps, rtpp, rtb, rtd, exb);
+        return;
+    }
     if (!kl) return;
     const double rho_p = rps + rpp;
     const double rho_zz = rho_p + rb;
@@ -51,6 +93,7 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     if (!MPASV || k > 0) {
         colk(fw(S, F_wwAvg), c) = wwAvg;
         colk(fw(S, F_rw), c) = rw;
+        if (k == 0) keep_put0<LP>(S, F_rw, KC, c, rw);  // (rw's level 0 changes: its keep tail too)
     }
     colk(fw(S, F_w), c) = (MPASV && k == 0) ? 0.0 : w;
     if (a.rk_step == 2) {
@@ -73,7 +116,7 @@ template <int LP, bool MPASV>
 __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
-    if (e >= S.nEO || k >= L) return;
+    if (e >= S.nEO || (!MPASV && k >= L)) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const double* rz = fd(S, F_rho_zz);
     const double rz1 = colk(rz, cell1), rz2 = colk(rz, cell2);
@@ -82,6 +125,13 @@ __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
     ruAvg *= a.invNs;
     ruAvg += rus;
     const double ru = MPASV ? rus + rup : rus * rup;
+    if (MPASV) {  // (every level written: level L with the values it holds -- ruAvg just loaded, ru / u
+                  // their keep tails -- the padding with zeros; mpas_dev.h keep tails)
+        colk(fw(S, F_ruAvg), e) = KEEPW(ruAvg, ra);
+        colk(fw(S, F_ru), e) = KEEPW(ru, keepv<LP>(S, F_ru, KE, e));
+        colk(fw(S, F_u), e) = KEEPW(2 * ru / (rz1 + rz2), keepv<LP>(S, F_u, KE, e));
+        return;
+    }
     colk(fw(S, F_ruAvg), e) = ruAvg;
     colk(fw(S, F_ru), e) = ru;
     colk(fw(S, F_u), e) = 2 * ru / (rz1 + rz2);
@@ -124,6 +174,7 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
     const double cf1 = fd(S, F_cf1)[0], cf2 = fd(S, F_cf2)[0], cf3 = fd(S, F_cf3)[0];
     double rz, w;
     col_rd2<LP>(fd(S, F_rho_zz), fd(S, F_w), c, k, L, rz, w);
+    const double w_in = w;  // (level L: stored back as loaded -- the column's lines written whole)
     const double rz_m = lvl_dn<LP>(rz, k), rz1 = __shfl(rz, 1, LP), rz2 = __shfl(rz, 2, LP);
     // the first NF slots: loads issued unconditionally, in pairs (every lane is active);
     // slots NF..9 (cells with more edges) one at a time under wave-uniform guards
@@ -168,7 +219,7 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
             if (i < ne) w += b_[i];
         w /= (fzm * rz + fzp * rz_m);
     }
-    if (k < L) colk(fw(S, F_w), c) = w;
+    colk(fw(S, F_w), c) = k < L ? w : PADW(w_in);
 }
 
 template <int LP>

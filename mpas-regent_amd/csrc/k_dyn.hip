@@ -74,6 +74,9 @@ __device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk
     const double *u = fd(S, F_u), *v = fd(S, F_v), *ru = fd(S, F_ru);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
     const bool smag = rk0 && a.horiz_mixing == 0;
+    // the kept level-L values of the stored columns (keep tails, mpas_dev.h), issued ahead
+    const double kl_kd = keepv<LP>(S, F_kdiff, KC, c), kl_hd = keepv<LP>(S, F_h_divergence, KC, c);
+    const double kl_tr = keepv<LP>(S, F_tend_rho, KC, c), kl_dp = keepv<LP>(S, F_dpdz, KC, c);
 
     int e_[NF];
     double ru_[NF], u_[NF], v_[NF], eocs_[NF], cdv_[NF], wfl[2];
@@ -140,7 +143,7 @@ __device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk
             int pw = k - (L - 2);
             kd = dmax_(kd, (pw == 0 ? 1.0 : 2.0) * 2.0833 * kLenDisp * a.cam_coef);
         }
-        if (k != L) colk(fw(S, F_kdiff), c) = PADW(kd);
+        colk(fw(S, F_kdiff), c) = KEEPW(kd, kl_kd);
     }
 
     // ---- h_divergence (:924-938)
@@ -158,14 +161,14 @@ __device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk
     // the w scratch wc (below) is formed here at rk_step 0, where C gathers it; at rk_step > 0
     // E, its only reader, forms it from the same operands (wc_body), so A reads ru alone
     constexpr bool WC = !MD && RK0;
-    if (!WC && k != L) colk(fw(S, F_h_divergence), c) = PADW(hd);  // (else paired with wc below)
+    if (!WC) colk(fw(S, F_h_divergence), c) = KEEPW(hd, kl_hd);  // (else paired below)
 
     // ---- tend_rho, dpdz (:942-951)
     const double rw_p1 = lvl_up<LP>(rw, k);
     if (rk0)  // (paired 16-B store, every lane)
-        put2<LP>(fw(S, F_tend_rho), c, fw(S, F_dpdz), c, k,
-                 PADW(MD ? -hd - rdzw * (rw_p1 - rw) + trp : -hd - rdzw * (rw_p1 - rw + trp)),
-                 PADW(-kGravity * (rb * (qt) + rps * (1.0 + qt))), k != L, k != L);
+        put2f<LP>(fw(S, F_tend_rho), c, fw(S, F_dpdz), c, k,
+                 KEEPW(MD ? -hd - rdzw * (rw_p1 - rw) + trp : -hd - rdzw * (rw_p1 - rw + trp), kl_tr),
+                 KEEPW(-kGravity * (rb * (qt) + rps * (1.0 + qt)), kl_dp));
 
     // ---- w: zeroing (:1170), horizontal advection (:1174-1205, Q13), curvature (:1208-1218)
     // After the zeroing every w(cell, k<L) read by flux_arr is exactly 0.0 (the zero
@@ -200,7 +203,7 @@ __device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk
         wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
               2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
     }
-    put2<LP>(fw(S, F_h_divergence), c, fw(S, X_wc), c, k, PADW(hd), k < L ? wc : 0.0, k != L, true);
+    put2f<LP>(fw(S, F_h_divergence), c, fw(S, X_wc), c, k, KEEPW(hd, kl_hd), k < L ? wc : 0.0);
 }
 template <int LP, bool RK0, bool MD>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
@@ -208,6 +211,8 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 }
 
 // ------------------------------------------------------------------------ B (edges)
+// (B's stores leave level L unwritten, as the reference: the keep tails of mpas_dev.h measured
+// no gain on this gather-bound kernel and cost its DIN form 5-9 %, profiles/r05/keep_tails)
 // DIN (rk_step > 0, option "defer4"): the previous rk_step 0 call left tend_u_euler without
 // its del4 part (kernel D, skipped there); this kernel applies D's statements to the
 // tend_u_euler it reads -- the same operands in the same order, so the same bits -- and
@@ -525,6 +530,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
 // one-vertex wave is latency-bound; the VE vertices issue their gathers together
 // (option "cve", default 4; profiles/r03/c_vertex_epw: C 482 -> 398 us at x1.163842, the
 // step -0.7 %; 8 vertices: C 410 us, the step and x1.2562 no better than 4)
+// (C's stores leave level L unwritten: the keep tails cost it 4 %, profiles/r05/keep_tails)
 // PART (a launch's blocks): 1 the vertex blocks, 2 the cell blocks -- two launches, each
 // with its mesh rows as scalar loads (one grid of both interleaved made the compiler load
 // ~24 of them per wave with vector loads: the other path's stores could clobber them)
@@ -670,6 +676,7 @@ __device__ __forceinline__ void dyn_D_body(const DevState& S, const DynK& a, Blk
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
     const double invDc = fd(S, F_invDcEdge)[e];
+    const double kl_tue = keepv<LP>(S, F_tend_u_euler, KE, e), kl_tu = keepv<LP>(S, F_tend_u, KE, e);
     double u_mix_scale = fd(S, F_meshScalingDel4)[e] * a.h4;
     double r_dc = u_mix_scale * kDel4uDivFactor * invDc;
     double r_dv = u_mix_scale * dmin_(fd(S, F_invDvEdge)[e], 4 * invDc);
@@ -683,7 +690,7 @@ __device__ __forceinline__ void dyn_D_body(const DevState& S, const DynK& a, Blk
     tue -= u_diffusion;
     tend_u += tue + trp;
     // (padding levels: zeros, PADW; level L keeps its value; one paired 16-B store, every lane)
-    put2<LP>(fw(S, F_tend_u_euler), e, fw(S, F_tend_u), e, k, PADW(tue), PADW(tend_u), k != L, k != L);
+    put2f<LP>(fw(S, F_tend_u_euler), e, fw(S, F_tend_u), e, k, KEEPW(tue, kl_tue), KEEPW(tend_u, kl_tu));
 }
 
 // ------------------------------------------------------------------------ E (cells)
@@ -708,6 +715,10 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k], rdzu = fd(S, F_rdzu)[k];
     const double invA = fd(S, F_invAreaCell)[c];
     const bool del4 = rk0 && a.h4 > 0.0;
+    // the kept level-L values of the stored columns (keep tails, mpas_dev.h), issued ahead
+    const double kl_tra = keepv<LP>(S, F_tend_rtheta_adv, KC, c), kl_w = keepv<LP>(S, F_w, KC, c);
+    const double kl_rth = keepv<LP>(S, F_rthdynten, KC, c), kl_tt = keepv<LP>(S, F_tend_theta, KC, c);
+    const double kl_twe = keepv<LP>(S, F_tend_w_euler, KC, c), kl_tte = keepv<LP>(S, F_tend_theta_euler, KC, c);
     const double *ru = fd(S, F_ru), *Ff = fd(S, X_F), *rus = fd(S, F_ru_save), *tms_f = fd(S, F_theta_m_save);
     const double *dw = fd(S, F_delsq_w), *dth = fd(S, F_delsq_theta), *tm = fd(S, F_theta_m);
 
@@ -880,7 +891,7 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
             w += twe;
         }
         colk(fw(S, F_tend_w), c) = PADW(w);
-        if (rk0 && k != L) colk(fw(S, F_tend_w_euler), c) = PADW(twe);
+        if (rk0) colk(fw(S, F_tend_w_euler), c) = KEEPW(twe, kl_twe);
     } else {
         if (k > 0 && kl) {  // :1289-1302 (Q14 literal), :1318-1322
             w *= invA - rdzu * (wdwz_p - wdwz);
@@ -951,13 +962,18 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
         if (MD) tend_theta = tend_theta * invA - rdzw * (wdtz_p - wdtz);
         else tend_theta *= invA - rdzw * (wdtz_p - wdtz);
         const double rth = tend_theta / rho_zz;
-        if (MD && k != L) colk(fw(S, F_tend_rtheta_adv), c) = PADW(tend_theta);
-        if (!MD) put2<LP>(fw(S, F_w), c, fw(S, F_tend_rtheta_adv), c, k, PADW(w), PADW(tend_theta), k != L, k != L);
+        // (level L: the kept values, keep tails in mpas_dev.h -- every line written whole)
+        if (MD) colk(fw(S, F_tend_rtheta_adv), c) = KEEPW(tend_theta, kl_tra);
+        if (!MD)
+            put2f<LP>(fw(S, F_w), c, fw(S, F_tend_rtheta_adv), c, k, KEEPW(w, kl_w),
+                     KEEPW(tend_theta, kl_tra));
         tend_theta += rho_zz * rt_diab;
         tend_theta += tte + trp;
-        put2<LP>(fw(S, F_rthdynten), c, fw(S, F_tend_theta), c, k, PADW(rth), PADW(tend_theta), k != L, k != L);
-        if (rk0 && MD && k != L) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
-        if (rk0 && !MD) put2<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k, PADW(twe), PADW(tte), k != L, k != L);
+        put2f<LP>(fw(S, F_rthdynten), c, fw(S, F_tend_theta), c, k, KEEPW(rth, kl_rth), KEEPW(tend_theta, kl_tt));
+        if (rk0 && MD) colk(fw(S, F_tend_theta_euler), c) = KEEPW(tte, kl_tte);
+        if (rk0 && !MD)
+            put2f<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k,
+                     KEEPW(twe, kl_twe), KEEPW(tte, kl_tte));
         return;
     }
     if (k == L) return;  // (padding levels: zeros, PADW)

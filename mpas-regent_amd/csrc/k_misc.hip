@@ -227,6 +227,7 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     double zz, w;
     col_rd2<LP>(fd(S, F_zz), fd(S, wf), c, k, L, zz, w);
+    const double w_in = w;  // (MD: levels 0 and L keep the tend_w just loaded)
     // (the point's cprMask byte loaded with the columns: tested after a lane condition it
     // was loaded under a divergent branch and waited for there)
     const uint8_t cpr = MD ? 0 : ((const uint8_t*)S.f[F_cprMask])[p];
@@ -258,10 +259,13 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
         w -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
     }
     w *= (fzm * zz + fzp * zz_m);
-    if (MD) {
-        if (k >= 1 && k < L && fi(S, F_bdyMaskCell)[c] <= kRelaxZone) colk(fw(S, wf), c) = w;
+    if (MD) {  // (every level written: 0 and L with their loaded values, the padding with zeros)
+        if (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) colk(fw(S, wf), c) = (k >= 1 && k < L) ? w : PADW(w_in);
     } else if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
         colk(fw(S, wf), c) = w;
+        if (k == L) keep_put<LP>(S, F_w, KC, c, w);  // (w's level L changes: its keep tail too)
+    } else if ((k > L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone)) {
+        colk(fw(S, wf), c) = 0.0;  // (the padding's content: the column's last line written whole)
     }
 }
 template <int LP>
@@ -636,5 +640,55 @@ hipError_t launch_bounds_probe(const DevState& S, hipStream_t st, int col) {
     MPAS_LP_DISPATCH(S.LP, bounds_probe_lp, S, st, col);
 }
 #endif
+
+// ---------------------------------------------------------------- keep tails (mpas_dev.h)
+// (plain arguments -- the column base, n, no: a runtime field id / kind into DevState made the
+// compiler index a scratch copy of the struct and select n from it, and that select came out
+// wrong for the third kind, ROCm 7.2 hipcc -O3: vertex tails were read at the cell offset)
+template <int LP>
+__global__ __launch_bounds__(256) void k_keep_refresh(double* f, int n, int L) {
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i > n) return;
+    const double* col = f + (size_t)i * LP;
+    double* t = f + (size_t)(n + 1) * LP;
+    t[i] = col[lpos(LP, L)];
+    t[(size_t)n + 1 + i] = col[lpos(LP, 0)];
+}
+template <int LP>
+__global__ __launch_bounds__(256) void k_keep_check(const double* f, int n, int no, int L, int fid, int lev0, int* flag) {
+    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (i >= no) return;
+    const double a = f[(size_t)i * LP + lpos(LP, lev0 ? 0 : L)];
+    const double b = f[(size_t)(n + 1) * LP + (lev0 ? (size_t)n + 1 : 0) + i];
+    if (__builtin_bit_cast(uint64_t, a) != __builtin_bit_cast(uint64_t, b)) {
+        atomicAdd(flag + 6, 1);
+        atomicMin(flag + 7, i);
+        if (atomicCAS(flag, 0, 2 * fid + lev0 + 1) == 0) {
+            flag[1] = i;  // (the first mismatch found: entity and both values, for the message)
+            ((double*)(flag + 2))[0] = a;
+            ((double*)(flag + 2))[1] = b;
+        }
+    }
+}
+static inline int keep_n(const DevState& S, int kind) { return kind == KC ? S.nCells : kind == KE ? S.nEdges : S.nVertices; }
+template <int LP>
+static hipError_t keep_refresh_lp(const DevState& S, hipStream_t st, int f, int kind) {
+    const int n = keep_n(S, kind);
+    k_keep_refresh<LP><<<(n + 256) / 256, 256, 0, st>>>((double*)S.f[f], n, S.L);
+    return hipGetLastError();
+}
+hipError_t launch_keep_refresh(const DevState& S, hipStream_t st, int f, int kind) {
+    MPAS_LP_DISPATCH(S.LP, keep_refresh_lp, S, st, f, kind);
+}
+template <int LP>
+static hipError_t keep_check_lp(const DevState& S, hipStream_t st, int f, int kind, int lev0, int* flag) {
+    const int no = kind == KC ? S.nCO : kind == KE ? S.nEO : S.nVO;
+    if (no > 0)
+        k_keep_check<LP><<<(no + 255) / 256, 256, 0, st>>>((const double*)S.f[f], keep_n(S, kind), no, S.L, f, lev0, flag);
+    return hipGetLastError();
+}
+hipError_t launch_keep_check(const DevState& S, hipStream_t st, int f, int kind, int lev0, int* flag) {
+    MPAS_LP_DISPATCH(S.LP, keep_check_lp, S, st, f, kind, lev0, flag);
+}
 
 }  // namespace mpas

@@ -149,6 +149,10 @@ struct mpas_ctx {
     // fails on a transport falls back to eager steps (graph_fallbacks)
     int graph_halo = 2;
     int64_t graph_fallbacks = 0;
+    // option "keep_check" (tests): after every task, every keep tail is compared with its
+    // field on the owned entities (mpas_dev.h keep tails); a mismatch fails the task
+    int keep_check = 0;
+    int* keep_flag = nullptr;
     // set when a transport refused a capture: eager steps from then on (the user's graph_halo
     // stays as set; a new halo plan or option change clears it)
     bool graph_refused = false;
@@ -199,13 +203,65 @@ size_t dev_bytes(const mpas_ctx* c, int f) {
     const size_t LP = c->S.LP;
     size_t rows = (size_t)entity_count(c, fi.kind) + 1;
     switch (fi.kind) {
-        case K_C3: case K_E3: case K_V3: return rows * fi.width * LP * 8;
+        // (width-1 fields: + the two keep tails of rows doubles each, mpas_dev.h keep_tail)
+        case K_C3: case K_E3: case K_V3: return rows * fi.width * LP * 8 + (fi.width == 1 ? 2 * rows * 8 : 0);
         case K_C3V: return rows * fi.width * LP * 8;
         case K_C3B: return rows * LP;
         case K_ZV: return LP * 8;
         default: return rows * fi.width * elem_size(fi.kind);
     }
 }
+// Keep tails (mpas_dev.h): the fields a step kernel writes with the kept value of level L
+// (kKeepL) or of level 0 (kKeep0) -- the slots the reference never writes there.  Their
+// tails are set from the field after every write from outside the step kernels
+// (keep_refresh); option "keep_check" compares them with the field after every task.
+const int kKeepL[] = {
+    // dyn_tend (A, D, E; B and C keep the reference's unwritten slots)
+    F_kdiff, F_h_divergence, F_tend_rho, F_dpdz, F_v, F_ru_save, F_u_2, F_tend_u_euler, F_tend_u,
+    F_tend_w_euler, F_tend_theta_euler, F_tend_rtheta_adv, F_w, F_rthdynten, F_tend_theta,
+    // vert_imp
+    F_coftz, F_cofwt, F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri, F_gamma_tri,
+    // solve_diagnostics (its edge kernel)
+    F_h_edge, F_ke_edge, F_rho_edge, F_pv_edge,
+    // setup + moist
+    F_cqu, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2, F_rho_zz_old_split,
+    F_theta_m_save, F_qtot, F_cqw,
+    // acoustic
+    F_rtheta_pp_old, F_rho_pp, F_rtheta_pp,
+    // recover (the MPAS forms)
+    F_rho_p, F_rho_zz, F_rtheta_p, F_theta_m, F_exner, F_pressure_p, F_rw, F_ru, F_u,
+    // substep_finish
+    F_wwAvg_split, F_ruAvg_split};
+const int kKeep0[] = {F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri, F_cqw, F_rw};
+int keep_kind(int f) { return kFields[f].kind == K_C3 ? 0 : kFields[f].kind == K_E3 ? 1 : 2; }  // KC / KE / KV
+
+void keep_refresh_all(mpas_ctx* c) {
+    for (int f : kKeepL) hipcheck(launch_keep_refresh(c->S, c->stream, f, keep_kind(f)), "keep_refresh");
+    for (int f : kKeep0) hipcheck(launch_keep_refresh(c->S, c->stream, f, keep_kind(f)), "keep_refresh");
+}
+void keep_verify(mpas_ctx* c, const char* task) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipcheck(hipStreamIsCapturing(c->stream, &cs), "hipStreamIsCapturing");
+    if (cs != hipStreamCaptureStatusNone) return;  // (a captured step is checked when it runs eagerly)
+    if (!c->keep_flag) hipcheck(hipMalloc(&c->keep_flag, 8 * sizeof(int)), "hipMalloc");
+    hipcheck(hipMemsetAsync(c->keep_flag, 0, 7 * sizeof(int), c->stream), "hipMemsetAsync");
+    hipcheck(hipMemsetAsync(c->keep_flag + 7, 0x7f, sizeof(int), c->stream), "hipMemsetAsync");
+    for (int f : kKeepL) hipcheck(launch_keep_check(c->S, c->stream, f, keep_kind(f), 0, c->keep_flag), "keep_check");
+    for (int f : kKeep0) hipcheck(launch_keep_check(c->S, c->stream, f, keep_kind(f), 1, c->keep_flag), "keep_check");
+    int fl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    hipcheck(hipMemcpyAsync(fl, c->keep_flag, sizeof(fl), hipMemcpyDeviceToHost, c->stream), "hipMemcpyAsync");
+    hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
+    if (fl[0]) {
+        double v[2];
+        std::memcpy(v, fl + 2, sizeof v);
+        throw Fail{MPAS_EINVAL, std::string(task) + ": keep tail of " + kFields[(fl[0] - 1) / 2].name + " (level " +
+                                    ((fl[0] - 1) % 2 ? "0" : "L") + ") differs from the field at entity " +
+                                    std::to_string(fl[1]) + ": field " + std::to_string(v[0]) + ", tail " +
+                                    std::to_string(v[1]) + "; " + std::to_string(fl[6]) +
+                                    " mismatches, the first at entity " + std::to_string(fl[7]) + " (keep_check)"};
+    }
+}
+
 // entity kind an integer field refers to (for the Q1 clamp), -1 if it is not an id
 int id_target(int f) {
     switch (f) {
@@ -331,6 +387,7 @@ void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
         throw Fail{MPAS_EHIP, std::string(name) + ": " + hipGetErrorString(e)};
     }
     if (c->halo && !c->halo->race.empty()) throw Fail{MPAS_EINVAL, std::string(name) + ": " + c->halo->race};
+    if (c->keep_check) keep_verify(c, name);
     if (c->timing) {
         hipcheck(hipEventRecord(e1, c->stream), "hipEventRecord");
         c->pending.push_back({ti, e0, e1});
@@ -380,7 +437,11 @@ void bounds_add(mpas_ctx* c) {
         std::lock_guard<std::mutex> lk(r.mu);
         for (int f = 0; f < X_COUNT; f++) {
             const unsigned long long lo = (unsigned long long)c->S.f[f];
-            r.fields[lo] = {lo + dev_bytes(c, f), kFields[f].name};
+            // (the columns only: the keep tails behind them are reached by keepv / keep_put alone)
+            const FieldInfo& fi = kFields[f];
+            const bool tails = (fi.kind == K_C3 || fi.kind == K_E3 || fi.kind == K_V3) && fi.width == 1;
+            const size_t cols = dev_bytes(c, f) - (tails ? 2 * ((size_t)entity_count(c, fi.kind) + 1) * 8 : 0);
+            r.fields[lo] = {lo + cols, kFields[f].name};
         }
     }
     bounds_publish();
@@ -1153,6 +1214,7 @@ int mpas_ctx_destroy(mpas_ctx* c) {
     for (auto p : c->gid_dev)
         if (p) (void)hipFree(p);
     if (c->sum_scratch) (void)hipFree(c->sum_scratch);
+    if (c->keep_flag) (void)hipFree(c->keep_flag);
     if (c->sum_out) (void)hipFree(c->sum_out);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1201,6 +1263,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             c->halo->stub_latency_us = (int)value;
         }
         else if (name && std::strcmp(name, "xcd") == 0) c->S.xcd = (int)value;
+        else if (name && std::strcmp(name, "keep_check") == 0) c->keep_check = value ? 1 : 0;
         else if (name && std::strcmp(name, "epw") == 0) {
             if (value != 1 && value != 2 && value != 4) throw Fail{MPAS_EINVAL, "epw must be 1, 2 or 4"};
             c->S.epw = (int)value;
@@ -1269,6 +1332,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         if (!value) throw Fail{MPAS_EINVAL, "mpas_get_option: null value"};
         if (name && std::strcmp(name, "exact") == 0) *value = c->exact;
         else if (name && std::strcmp(name, "xcd") == 0) *value = c->S.xcd;
+        else if (name && std::strcmp(name, "keep_check") == 0) *value = c->keep_check;
         else if (name && std::strcmp(name, "epw") == 0) *value = c->S.epw;
         else if (name && std::strcmp(name, "vcmix") == 0) *value = c->S.vcmix;
         else if (name && std::strcmp(name, "physics") == 0) *value = c->S.physics;
@@ -1367,6 +1431,8 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
                 hipcheck(launch_view_copy(c->S.f[f], (void*)host, fi.kind == K_C3B ? 1 : 8, n, W, L, LP, se, sl, sc, 1,
                                           c->stream),
                          "upload view");
+                if (fi.kind != K_C3V && fi.kind != K_C3B && W == 1)
+                    hipcheck(launch_keep_refresh(c->S, c->stream, f, keep_kind(f)), "keep_refresh");
                 hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
                 c->dirty = true;
                 c->trt_dirty = true;
@@ -1386,6 +1452,13 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
             double* d = (double*)buf.data();
             for (int e = 0; e < n; e++)
                 for (int k = 0; k <= L; k++) d[(size_t)e * LP + lpos(LP, k)] = *(const double*)(h + e * se + k * sl);
+            if (W == 1) {  // the keep tails: level L and level 0 of every column (the zero slot's: 0)
+                const size_t rows = (size_t)n + 1;
+                for (int e = 0; e < n; e++) {
+                    d[rows * LP + e] = d[(size_t)e * LP + lpos(LP, L)];
+                    d[rows * LP + rows + e] = d[(size_t)e * LP + lpos(LP, 0)];
+                }
+            }
         } else if (fi.kind == K_C3V) {
             double* d = (double*)buf.data();
             for (int e = 0; e < n; e++)
@@ -1505,6 +1578,7 @@ int mpas_fill_synthetic(mpas_ctx* c, uint64_t seed) {
     return guarded(c, [&] {
         hipcheck(hipSetDevice(c->device), "hipSetDevice");
         hipcheck(launch_fill_synthetic(c->S, c->stream, seed), "fill_synthetic");
+        keep_refresh_all(c);
         hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
         if (c->halo)  // filled from global ids: ghosts hold the global values
             for (auto& v : c->halo->stale) v = 0;
@@ -1739,11 +1813,20 @@ int mpas_reconstruct_2d(mpas_ctx* c, int includeHalos, int on_a_sphere) {
     (void)includeHalos;  // :1909-1912: the range is nCells either way
     MPAS_TASK("mpas_reconstruct_2d", launch_reconstruct_2d(c->S, c->stream, on_a_sphere ? 1 : 0));
 }
+// (the init tasks write state fields at every level from outside the step: the keep tails
+// follow them, mpas_dev.h)
 int mpas_atm_compute_damping_coefs(mpas_ctx* c, double config_zd, double config_xnutr) {
-    MPAS_TASK("atm_compute_damping_coefs", launch_damping_coefs(c->S, c->stream, config_zd, config_xnutr));
+    return guarded(c, [&] {
+        run_task(c, "atm_compute_damping_coefs",
+                 [&] { return launch_damping_coefs(c->S, c->stream, config_zd, config_xnutr); });
+        keep_refresh_all(c);
+    });
 }
 int mpas_atm_init_coupled_diagnostics(mpas_ctx* c) {
-    MPAS_TASK("atm_init_coupled_diagnostics", launch_init_coupled_diagnostics(c->S, c->stream));
+    return guarded(c, [&] {
+        run_task(c, "atm_init_coupled_diagnostics", [&] { return launch_init_coupled_diagnostics(c->S, c->stream); });
+        keep_refresh_all(c);
+    });
 }
 // the mesh tasks of atm_core_init (k_mesh.hip); the adv lists feed k_prepare's edge
 // records and the transport tiles, so they are re-derived before the next task
@@ -1781,6 +1864,7 @@ int mpas_atm_core_init(mpas_ctx* c) {
         run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });
         run_task(c, "atm_compute_mesh_scaling", [&] { return launch_mesh_scaling(S, st, 1); });
         run_task(c, "atm_compute_damping_coefs", [&] { return launch_damping_coefs(S, st, 22000.0, 0.2); });
+        keep_refresh_all(c);  // (the init tasks write the state from outside the step)
     });
 }
 int mpas_atm_advance_scalars_mono(mpas_ctx* c, double dt) {

@@ -253,6 +253,10 @@ hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int holli
                                     int no_v = 0);
 hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
+// keep tails (below): set both tails of field f from the field; compare one tail (level 0 or
+// L) with the field on the owned entities, *flag = 2 f + lev0 + 1 on a mismatch
+hipError_t launch_keep_refresh(const DevState& S, hipStream_t st, int f, int kind);
+hipError_t launch_keep_check(const DevState& S, hipStream_t st, int f, int kind, int lev0, int* flag);
 hipError_t launch_prepare(DevState& S, hipStream_t st);
 hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt);
 hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
@@ -614,6 +618,10 @@ __device__ __forceinline__ void cell_pair(const double* f, int c1, int c2, int o
 template <int LP>
 __device__ __forceinline__ void put2(double* fa, int ia, double* fb, int ib, int k, double a, double b, bool oka,
                                      bool okb) {
+#if MPAS_NOHOLE  // (timing-only experiment build: the never-written slots written too -- wrong values)
+    oka = oka || k <= 63;
+    okb = okb || k <= 63;
+#endif
     if constexpr (LP == 64) {
         double x = a, y = b;
         swap_halves(x, y);
@@ -628,6 +636,23 @@ __device__ __forceinline__ void put2(double* fa, int ia, double* fb, int ib, int
     } else {
         if (oka) colk(fa, ia) = a;
         if (okb) colk(fb, ib) = b;
+    }
+}
+
+// put2 of two whole columns (every level stored: the keep-tail stores, KEEPW): one 16-B store
+// per lane with no mask exchange -- put2's masks, even when all true, cost a permlane of the
+// flags and three divergent store branches (the compiler cannot fold them through the swap)
+template <int LP>
+__device__ __forceinline__ void put2f(double* fa, int ia, double* fb, int ib, int k, double a, double b) {
+    if constexpr (LP == 64) {
+        double x = a, y = b;
+        swap_halves(x, y);
+        const bool hi = k >= 32;
+        char* base = hi ? (char*)fb + (size_t)(uint32_t)ib * 512 : (char*)fa + (size_t)(uint32_t)ia * 512;
+        *(double2*)MPAS_CHK(hi ? fb : fa, base + (k & 31) * 16, 16) = make_double2(x, y);
+    } else {
+        colk(fa, ia) = a;
+        colk(fb, ib) = b;
     }
 }
 
@@ -741,8 +766,46 @@ __device__ __forceinline__ int cell_rec(const DevState& S, int c, int (&e_)[NF],
 // unwritten; with the level-pair layout (lpos) those sit at odd positions spread over the
 // last two 64-B sectors of the column, and every partially written sector costs HBM time.
 // Kernels therefore also write the padding levels, with 0.0 (their content everywhere):
-// `if (k < L || k > L) f = PADW(v)`.  Only level L stays unwritten.
+// `if (k < L || k > L) f = PADW(v)`.
 #define PADW(v) (k > L ? 0.0 : (v))
+
+// Keep tails (round 5).  Level L of the fields the reference never writes there (and level
+// 0 of vert_imp's tridiagonal coefficients) used to stay unwritten: one 8-B hole per column,
+// so the column's last 128-B line was written partially -- measured +9 to +24 % on a write
+// stream (tools/ubench/pitch.py, profiles/r05/pitch_ubench_holes.json) and -4 % over the
+// step when filled (timing-only build, profiles/r05/nohole_ab).  Every width-1 C3 / E3 / V3
+// field's allocation now ends with two tails of n + 1 doubles: the value of level L
+// (keepL) and of level 0 (keep0) of each column.  A kernel that leaves one of those slots
+// writes the tail's value there instead (the value the slot holds: the same bits), so every
+// line of the column is written whole.  The tails are set from the field by
+// mpas_ctx.cpp keep_refresh after every write from outside the step kernels (upload, the
+// synthetic fill, the init tasks, ...), and a kernel that writes level L of a keep field
+// (set_smlstep's w) writes its tail too; option "keep_check" (tests) compares every tail
+// with its field after each task.
+template <int LP>
+__device__ __forceinline__ const double* keep_tail(const DevState& S, int f, int kind, bool lev0) {
+    const int n = kind == KC ? S.nCells : kind == KE ? S.nEdges : S.nVertices;
+    return fd(S, f) + (size_t)(n + 1) * LP + (lev0 ? (size_t)(n + 1) : 0);
+}
+// the kept level-L (lev0: level-0) value of column ent of field f: a scalar load when ent is
+// wave-uniform (the tails change only between launches)
+template <int LP>
+__device__ __forceinline__ double keepv(const DevState& S, int f, int kind, int ent, bool lev0 = false) {
+    return ldc(keep_tail<LP>(S, f, kind, lev0) + ent);
+}
+// a kernel that changes the level-L value of a keep field updates its tail with it
+template <int LP>
+__device__ __forceinline__ void keep_put(const DevState& S, int f, int kind, int ent, double v) {
+    const_cast<double*>(keep_tail<LP>(S, f, kind, false))[ent] = v;
+}
+template <int LP>
+__device__ __forceinline__ void keep_put0(const DevState& S, int f, int kind, int ent, double v) {
+    const_cast<double*>(keep_tail<LP>(S, f, kind, true))[ent] = v;
+}
+// the value a store of level k writes: v where the kernel computes the level, the kept
+// value at level L (and, hold0, at level 0), 0.0 on the padding levels
+#define KEEPW(v, kl_) (k == L ? (kl_) : PADW(v))
+#define KEEPW0(v, k0_, kl_) (k == 0 ? (k0_) : KEEPW(v, kl_))
 
 // column read with the level policy: levels outside 0..L read 0.0
 template <int LP>

@@ -48,19 +48,27 @@ __device__ __forceinline__ void ld2(const double* fa, int ca, const double* fb, 
     swap_halves(a, b);
 }
 
-template <int P>
+// HOLE (P = 64): the level-L slot (level NP - 1 + 32 = L, in pair NP - 1) is not written
+// -- the library's stores of the fields whose level L the reference never writes: that
+// lane stores its 8-B level NP - 1 only, so the column's last line is written partially.
+// HOLE0: level 0 (pair 0) not written either (vert_imp's tridiagonal coefficients)
+template <int P, bool HOLE = false, bool HOLE0 = false>
 __device__ __forceinline__ void st2(double* fa, int ca, double* fb, int cb, int NP, double a, double b) {
     const int l = threadIdx.x & 63, j = l & 31;
     swap_halves(a, b);  // back to the pair layout
     double* base = l < 32 ? fa + (size_t)ca * P : fb + (size_t)cb * P;
-    if (P == 64 || j < NP) {
+    if (HOLE && j == NP - 1) {
+        base[2 * j] = a;
+    } else if (HOLE0 && j == 0) {
+        base[1] = b;
+    } else if (P == 64 || j < NP) {
         *(double2*)(base + 2 * j) = make_double2(a, b);
     } else if (j < 32) {
         base[NP + j] = a;  // (the partner level j+32 > L does not exist)
     }
 }
 
-template <int P, int NIN, int NOUT, bool ALN>
+template <int P, int NIN, int NOUT, bool ALN, bool HOLE = false, bool HOLE0 = false>
 __global__ __launch_bounds__(256) void kstream(const double* const* in, double* const* out, int n, int NP) {
     const int c = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
     if (c >= n) return;
@@ -74,7 +82,7 @@ __global__ __launch_bounds__(256) void kstream(const double* const* in, double* 
         t += 0.5 * v[i];
     }
 #pragma unroll
-    for (int o = 0; o < NOUT; o += 2) st2<P>(out[o], c, out[o + 1], c, NP, s + o, t - o);
+    for (int o = 0; o < NOUT; o += 2) st2<P, HOLE, HOLE0>(out[o], c, out[o + 1], c, NP, s + o, t - o);
 }
 
 template <int P, int NG, bool ALN>
@@ -110,6 +118,12 @@ extern "C" int ub_stream(int P, int nin, const double* const* in, double* const*
     else if (P == 64 && nin == 4) kstream<64, 4, 4, false><<<nb, 256, 0, st>>>(in, out, n, NP);
     else if (P == 58 && nin == 4) kstream<58, 4, 4, false><<<nb, 256, 0, st>>>(in, out, n, NP);
     else if (P == 59 && nin == 4) kstream<58, 4, 4, true><<<nb, 256, 0, st>>>(in, out, n, NP);
+    else if (P == 65 && nin == 12) kstream<64, 12, 2, false, true><<<nb, 256, 0, st>>>(in, out, n, NP);
+    else if (P == 65 && nin == 4) kstream<64, 4, 4, false, true><<<nb, 256, 0, st>>>(in, out, n, NP);
+    else if (P == 66 && nin == 12) kstream<64, 12, 2, false, true, true><<<nb, 256, 0, st>>>(in, out, n, NP);
+    else if (P == 66 && nin == 4) kstream<64, 4, 4, false, true, true><<<nb, 256, 0, st>>>(in, out, n, NP);
+    else if (P == 65 && nin == 10) kstream<64, 10, 10, false, true><<<nb, 256, 0, st>>>(in, out, n, NP);
+    else if (P == 64 && nin == 10) kstream<64, 10, 10, false><<<nb, 256, 0, st>>>(in, out, n, NP);
     else return -1;
     return (int)hipGetLastError();
 }

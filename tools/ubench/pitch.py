@@ -41,8 +41,8 @@ def unpack(f, n, nl, P, NP):
     return f.reshape(-1, P)[:n, lpos(P, np.arange(nl), NP)]
 
 
-def store_pitch(P):  # (59: the P = 58 layout read by the aligned-select kernels)
-    return 58 if P == 59 else P
+def store_pitch(P):  # (59: the P = 58 layout read by the aligned-select kernels; 65 / 66: P = 64 with
+    return 58 if P == 59 else 64 if P in (65, 66) else P  # the level-L hole / + the level-0 hole)
 
 
 def main():
@@ -102,10 +102,10 @@ def main():
     res["gather_values_match"] = bool(ok_g and np.allclose(outs[58][0], s_ref, rtol=1e-12, atol=1e-12))
 
     # stream (12 in / 2 out, and 4 in / 4 out) over cell columns
-    for nin, nout in ((12, 2), (4, 4)):
+    for nin, nout, pvs in ((12, 2, (64, 58, 59, 65, 66)), (4, 4, (64, 58, 59, 65, 66)), (10, 10, (64, 65))):
         xs = [rng.standard_normal((nC, nl)) for _ in range(nin)]
         outs = {}
-        for PV in (64, 58, 59, 64, 58, 59):
+        for PV in pvs + pvs:
             P = store_pitch(PV)
             din = [torch.from_numpy(pack(x, P, NP)).to(dev) for x in xs]
             dout = [torch.zeros((nC + 1) * P, dtype=torch.float64, device=dev) for _ in range(nout)]
@@ -119,7 +119,7 @@ def main():
             res[f"stream{nin}x{nout}_P{PV}_TBs_of_stored_bytes"] = round(byts / t / 1e9, 2)
             res[f"stream{nin}x{nout}_P{PV}_TBs_of_57_levels"] = round((nin + nout) * nC * nl * 8 / t / 1e9, 2)
         res[f"stream{nin}x{nout}_values_match"] = all(np.array_equal(outs[64][i], outs[PV][i])
-                                                      for i in range(nout) for PV in (58, 59))
+                                                      for i in range(nout) for PV in pvs if PV in (58, 59))
     print(json.dumps(res, indent=1))
 
 
