@@ -408,7 +408,7 @@ def task_table(rep, work_dims, n_prof, physics):
             kw["physics"] = 1  # the acoustic task's MPAS form also updates ru_p / ruAvg
         if physics == 2 and task in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
                                      "atm_compute_dyn_tend_work", "atm_set_smlstep_pert_variables_work",
-                                     "atm_compute_solve_diagnostics"):
+                                     "atm_compute_solve_diagnostics", "atm_rk_dynamics_substep_finish"):
             kw["physics"] = 2  # the MPAS dynamics' read/write sets
         b = roofline.b_alg(task, work_dims, **kw)
         avg = ms / calls

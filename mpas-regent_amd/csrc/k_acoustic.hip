@@ -453,6 +453,7 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     double rp, ra, tu, cqu, zxu;
     gather2<LP>(fd(S, F_ru_p), e, fd(S, F_ruAvg), e, k, rp, ra);
+    const double rp0 = rp, ra0 = ra;  // (level L: stored back as loaded -- the column's lines whole)
     gather2<LP>(fd(S, F_tend_u), e, fd(S, F_cqu), e, k, tu, cqu);
     zxu = colk(fd(S, F_zxu), e);
     if (small_step != 0) {  // (uniform)
@@ -471,9 +472,9 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
         rp = dts * tu;
         ra = rp;
     }
-    if (k == L) return;  // (padding levels: zeros, PADW)
-    colk(fw(S, F_ru_p), e) = PADW(rp);
-    colk(fw(S, F_ruAvg), e) = PADW(ra);
+    // (padding levels: zeros, PADW; level L: the values loaded, which the reference leaves)
+    colk(fw(S, F_ru_p), e) = KEEPW(rp, rp0);
+    colk(fw(S, F_ruAvg), e) = KEEPW(ra, ra0);
 }
 
 template <int LP>

@@ -194,10 +194,12 @@ __device__ __forceinline__ void divdamp_body(const DevState& S, double coef_divd
 #pragma unroll
     for (int i = 0; i < EPW; i++) {
         const int e = m.base + i;
-        if (e >= S.nEO || k >= L || (sh1[i] && sh2[i])) continue;
+        if (e >= S.nEO || (sh1[i] && sh2[i])) continue;
         double divCell1 = DIVB ? r1[i] : -(r1[i] - ro1[i]);
         double divCell2 = DIVB ? r2[i] : -(r2[i] - ro2[i]);
-        colk(rup, e) = ru[i] + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec[i]) / (TME ? t1[i] : t1[i] + t2[i]);
+        // (levels >= L: the value loaded, zeros on the padding -- the column's lines written whole)
+        colk(rup, e) = k < L ? ru[i] + coef_divdamp * (divCell2 - divCell1) * (1.0 - spec[i]) / (TME ? t1[i] : t1[i] + t2[i])
+                             : PADW(ru[i]);
     }
 }
 

@@ -391,7 +391,8 @@ __global__ __launch_bounds__(256) void k_reconstruct(DevState S, int on_a_sphere
     for (int i = 0; i < NF; i++) u_[i] = colk(u, e_[i]);
     const double clat = fd(S, X_cosLatCell)[c], slat = fd(S, X_sinLatCell)[c];
     const double clon = fd(S, X_cosLonCell)[c], slon = fd(S, X_sinLonCell)[c];
-    if (k >= L) return;
+    // (every level written: level L with its kept value, the padding with zeros -- keep tails)
+    auto kL = [&](int f) { return keepv<LP>(S, f, KC, c); };
     double X = 0.0, Y = 0.0, Z = 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++) {
@@ -405,15 +406,16 @@ __global__ __launch_bounds__(256) void k_reconstruct(DevState S, int on_a_sphere
         Y += cr[3 * i + 1] * ue;
         Z += cr[3 * i + 2] * ue;
     }
-    colk(fw(S, F_uReconstructX), c) = X;
-    colk(fw(S, F_uReconstructY), c) = Y;
-    colk(fw(S, F_uReconstructZ), c) = Z;
+    colk(fw(S, F_uReconstructX), c) = KEEPW(X, kL(F_uReconstructX));
+    colk(fw(S, F_uReconstructY), c) = KEEPW(Y, kL(F_uReconstructY));
+    colk(fw(S, F_uReconstructZ), c) = KEEPW(Z, kL(F_uReconstructZ));
     if (on_a_sphere) {
-        colk(fw(S, F_uReconstructZonal), c) = -X * slon + Y * clon;
-        colk(fw(S, F_uReconstructMeridional), c) = -(X * clon + Y * slon) * slat + Z * clat;
+        colk(fw(S, F_uReconstructZonal), c) = KEEPW(-X * slon + Y * clon, kL(F_uReconstructZonal));
+        colk(fw(S, F_uReconstructMeridional), c) = KEEPW(-(X * clon + Y * slon) * slat + Z * clat,
+                                                         kL(F_uReconstructMeridional));
     } else {
-        colk(fw(S, F_uReconstructZonal), c) = X;
-        colk(fw(S, F_uReconstructMeridional), c) = Y;
+        colk(fw(S, F_uReconstructZonal), c) = KEEPW(X, kL(F_uReconstructZonal));
+        colk(fw(S, F_uReconstructMeridional), c) = KEEPW(Y, kL(F_uReconstructMeridional));
     }
 }
 template <int LP>

@@ -231,7 +231,9 @@ const int kKeepL[] = {
     // recover (the MPAS forms)
     F_rho_p, F_rho_zz, F_rtheta_p, F_theta_m, F_exner, F_pressure_p, F_rw, F_ru, F_u,
     // substep_finish
-    F_wwAvg_split, F_ruAvg_split};
+    F_wwAvg_split, F_ruAvg_split,
+    // mpas_reconstruct_2d
+    F_uReconstructX, F_uReconstructY, F_uReconstructZ, F_uReconstructZonal, F_uReconstructMeridional};
 const int kKeep0[] = {F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri, F_cqw, F_rw};
 int keep_kind(int f) { return kFields[f].kind == K_C3 ? 0 : kFields[f].kind == K_E3 ? 1 : 2; }  // KC / KE / KV
 

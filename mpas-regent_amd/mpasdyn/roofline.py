@@ -160,7 +160,13 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             writes += ["exner", "pressure_p"]
         return reads, writes
     if task == "atm_rk_dynamics_substep_finish":
-        return (["wwAvg", "rho_zz_old_split", "ruAvg"], ["wwAvg_split", "wwAvg", "rho_zz", "ruAvg_split", "ruAvg"])
+        # (:1951-2007 with dynamics_substep = dynamics_split = 1, as atm_srk3 calls it: the
+        # averages are copied to the *_split fields and divided by 1 -- the kernel stores no
+        # unchanged average (no credit for bytes not moved); rho_zz = rho_zz_old_split in the
+        # reference semantics, kept under the MPAS dynamics)
+        if md:
+            return ["wwAvg", "ruAvg"], ["wwAvg_split", "ruAvg_split"]
+        return ["wwAvg", "rho_zz_old_split", "ruAvg"], ["wwAvg_split", "rho_zz", "ruAvg_split"]
     if task == "atm_advance_scalars_mono":  # k_transport.hip (Q26: MPAS-A's, not the reference's)
         return (["scalars_old", "ruAvg", "wwAvg", "rho_zz_old_split", "rho_zz", "cellsOnEdge", "advCellsForEdge",
                  "nAdvCellsForEdge", "adv_coefs", "adv_coefs_3rd", "dvEdge", "edgesOnCell", "nEdgesOnCell",
@@ -230,7 +236,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                 ("atm_recover_large_step_variables_work", {"rk_step": 2}, 1),
                 ("atm_compute_solve_diagnostics", p, 2),
                 ("atm_compute_solve_diagnostics", {"reconstruct_v": True, **p}, 1),
-                ("atm_rk_dynamics_substep_finish", {}, 1)]
+                ("atm_rk_dynamics_substep_finish", p, 1)]
         if physics == 2:
             out.append(("mpas_reconstruct_2d", {}, 1))
         if transport:
