@@ -415,6 +415,8 @@ def task_table(rep, work_dims, n_prof, physics):
         n = calls / n_prof
         variants[name] = {"launches_per_step": round(n, 3), "avg_ms": round(avg, 4), "b_alg_GB": round(b / 1e9, 4),
                           "GBs": round(b / (avg * 1e-3) / 1e9, 1)}
+        if kw.get("copy") and task == NORTH_STAR:  # the setup copies fusecopy moved in
+            variants[name]["b_alg_GB_excl_fusecopy"] = round(roofline.b_alg(task, work_dims, **dict(kw, copy=False)) / 1e9, 4)
         t = tasks.setdefault(task, {"launches_per_step": 0.0, "ms_per_step": 0.0, "b_alg_GB_per_step": 0.0})
         t["launches_per_step"] += n
         t["ms_per_step"] += n * avg
@@ -431,6 +433,14 @@ def task_table(rep, work_dims, n_prof, physics):
         if vs:
             t["variants"] = vs
     return tasks
+
+
+def frac_excl_copy(t):
+    """the task's B_alg fraction without the bytes of the setup copies (ru_save = ru, u_2 = u) that
+    option fusecopy moved into its rk_step 0 launch"""
+    vs = (t.get("variants") or {}).values()
+    b = sum(v["launches_per_step"] * v.get("b_alg_GB_excl_fusecopy", v["b_alg_GB"]) for v in vs) if vs else t["b_alg_GB_per_step"]
+    return round(b / (t["ms_per_step"] * 1e-3) / HBM_PEAK_GBS, 4)
 
 
 def main():
@@ -645,7 +655,7 @@ def main():
             "traffic_frac": ns.get("hbm_frac_measured"), "traffic_source": traffic_note,
             "b_alg_per_launch_GB": ns["b_alg_GB"], "avg_launch_ms": ns["avg_ms"],
             "launches_per_step": ns["launches_per_step"], "ms_per_step": ns["ms_per_step"],
-            "variants": ns.get("variants"), "dominant_task": dom,
+            "frac_excl_fusecopy": frac_excl_copy(ns), "variants": ns.get("variants"), "dominant_task": dom,
             "note": "achieved = B_alg per step / device time per step of the task (launch-weighted average of its "
                     "rk_step 0 and rk_step > 0 launches); frac = achieved / peak"}
     fused = bool(ctx.get_option("fusedamp_active"))

@@ -429,6 +429,20 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
     acoustic_body<LP, EXACT, SELF, FIRST, MPASV, MODE, TME, SML>(S, dts, small_step, epssm, resm, coefp, ncb,
                                                                 this_blk(), wold);
 }
+// MODE 2 on a small grid (fewer than kTailCells owned cells, where a launch's fixed cost is
+// most of its time): the orphan edges' blocks at the tail of the cell grid, one launch
+// instead of two (on large grids the separate launch keeps the cell path's mesh rows in
+// scalar loads, profiles/r04/orph_split)
+constexpr int kTailCells = 16384;
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool TME, bool SML>
+__global__ __launch_bounds__(256) void k_acoustic_o(DevState S, double dts, int small_step, double epssm, double resm,
+                                                   double coefp, int ncb, int wold) {
+    const int b = (int)blockIdx.x;
+    if (b < ncb)
+        acoustic_body<LP, EXACT, SELF, FIRST, false, 2, TME, SML>(S, dts, small_step, epssm, resm, coefp, ncb,
+                                                                   Blk{b, ncb}, wold);
+    else acoustic_orph_body<LP, TME>(S, coefp, b - ncb);
+}
 // option "hfuse" (atm_srk3, stages 0 and 1): a stage's last acoustic launch (MODE 2, the
 // damping of the previous substep inside) beside the stage's solve_diagnostics vertex /
 // cell kernel, which reads u only -- nothing the acoustic step reads or writes
@@ -444,12 +458,23 @@ __global__ __launch_bounds__(256) void k_hf_ac_vc(DevState S, double dts, int sm
 }
 
 // :1581-1613 restored (Q18, MPAS vertical solver only): ru_p and ruAvg of every owned
-// edge, before the cell kernel reads ru_p
-template <int LP>
+// edge, before the cell kernel reads ru_p.  FIRST (small_step 0): ru_p = dts tend_u and
+// ruAvg = ru_p need tend_u alone -- the old ru_p / ruAvg columns are not read (their level L,
+// stored back as it is, comes by one scalar load each), nor cqu / zxu: 2 of 6 column streams
+template <int LP, bool FIRST>
 __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int small_step, double c2) {
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
+    if constexpr (FIRST) {
+        const size_t pL = (size_t)e * LP + lpos(LP, L);
+        const double rp0 = ldc(fd(S, F_ru_p) + pL), ra0 = ldc(fd(S, F_ruAvg) + pL);
+        const double rp = dts * colk(fd(S, F_tend_u), e);
+        const double ra = rp;
+        colk(fw(S, F_ru_p), e) = KEEPW(rp, rp0);
+        colk(fw(S, F_ruAvg), e) = KEEPW(ra, ra0);
+        return;
+    }
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     double rp, ra, tu, cqu, zxu;
     gather2<LP>(fd(S, F_ru_p), e, fd(S, F_ruAvg), e, k, rp, ra);
@@ -489,16 +514,42 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
         const double rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
         auto ru = [&](const DevState& X) {
             const int nb = col_blocks<LP>(X, KE);
-            if (nb) k_acoustic_ru<LP><<<nb, 256, 0, st>>>(X, dts, small_step, c2);
+            if (nb && small_step == 0) k_acoustic_ru<LP, true><<<nb, 256, 0, st>>>(X, dts, small_step, c2);
+            else if (nb) k_acoustic_ru<LP, false><<<nb, 256, 0, st>>>(X, dts, small_step, c2);
         };
-        HALO_RUN(S, st, ru, F_rtheta_pp, F_zz, F_exner, F_rho_pp);
+        if (small_step == 0) HALO_RUN(S, st, ru);  // (own columns only: no ghost read)
+        else HALO_RUN(S, st, ru, F_rtheta_pp, F_zz, F_exner, F_rho_pp);
         HALO_WROTE(S, F_ru_p, F_ruAvg);
     }
     auto run = [&](const DevState& X) {
         const int ncb = col_blocks<LP>(X, KC);
         if (!ncb) return;
+        const int nob = (S.n_orph + 256 / LP - 1) / (256 / LP);  // (MODE 2: the edges no cell lists)
+        const bool tail = mode == 2 && nob && X.nCO - X.lo[KC] < kTailCells;
         const int grid = ncb;
         const bool first = small_step == 0;
+        if (tail) {  // (one launch: the orphan edges' blocks after the cell blocks)
+            auto go_t = [&](auto ex, auto sf) {
+                constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
+#define MPAS_ACO(FI, TM, SM) \
+    k_acoustic_o<LP, E, SF, FI, TM, SM><<<ncb + nob, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb, wold)
+                if (first) {
+                    if (tme) sml ? MPAS_ACO(true, true, true) : MPAS_ACO(true, true, false);
+                    else sml ? MPAS_ACO(true, false, true) : MPAS_ACO(true, false, false);
+                } else {
+                    if (tme) MPAS_ACO(false, true, false);
+                    else MPAS_ACO(false, false, false);
+                }
+#undef MPAS_ACO
+            };
+            auto go_ts = [&](auto ex) {
+                if (X.selfc) go_t(ex, std::true_type{});
+                else go_t(ex, std::false_type{});
+            };
+            if (exact) go_ts(std::true_type{});
+            else go_ts(std::false_type{});
+            return;
+        }
         auto go = [&](auto ex, auto sf, auto md) {
             constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
             constexpr int M = decltype(md)::value;
@@ -534,7 +585,6 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
         };
         if (exact) go_s(std::true_type{});
         else go_s(std::false_type{});
-        const int nob = (S.n_orph + 256 / LP - 1) / (256 / LP);  // (MODE 2: the edges no cell lists)
         if (mode == 2 && nob) {
             if (tme) k_acoustic_orph<LP, true><<<nob, 256, 0, st>>>(X, coef_prev);
             else k_acoustic_orph<LP, false><<<nob, 256, 0, st>>>(X, coef_prev);

@@ -535,10 +535,10 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
 // with its mesh rows as scalar loads (one grid of both interleaved made the compiler load
 // ~24 of them per wave with vector loads: the other path's stores could clobber them)
 template <int LP, bool SELF, int VE, int PART>
-__global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a) {
+__device__ __forceinline__ void dyn_C_body(const DevState& S, const DynK& a, Blk bk) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
-    ColMap<LP> m(S, KV);
+    ColMap<LP> m(S, KV, bk);
     const int bi = m.blk;
     if constexpr (PART == 1) {  // VE vertices: delsq_vorticity (:1052-1060)
         const int v0 = col_of<LP>(bi) * VE + S.lo[KV], k = m.k;
@@ -665,6 +665,19 @@ __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a) {
     if (del4 && k != L) colk(fw(S, F_delsq_divergence), c) = PADW(dsd);
     put2<LP>(fw(S, F_delsq_w), c, fw(S, F_tend_w_euler), c, k, PADW(delsq_w), PADW(twe), k != L, k != L);
     put2<LP>(fw(S, F_delsq_theta), c, fw(S, F_tend_theta_euler), c, k, PADW(delsq_theta), PADW(tte), k != L, k != L);
+}
+template <int LP, bool SELF, int VE, int PART>
+__global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a) {
+    dyn_C_body<LP, SELF, VE, PART>(S, a, this_blk());
+}
+// both parts in one grid (the vertex blocks first) where a launch's fixed cost is most of
+// its time: grids under kSmallC cell blocks
+constexpr int kSmallC = 4096;
+template <int LP, bool SELF, int VE>
+__global__ __launch_bounds__(256) void k_dyn_C12(DevState S, DynK a, int nv) {
+    const int b = (int)blockIdx.x;
+    if (b < nv) dyn_C_body<LP, SELF, VE, 1>(S, a, Blk{b, nv});
+    else dyn_C_body<LP, SELF, VE, 2>(S, a, Blk{b - nv, (int)gridDim.x - nv});
 }
 
 // ------------------------------------------------------------------------ D (rk0, del4)
@@ -1059,6 +1072,11 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         auto go = [&](auto ve) {
             constexpr int VE = LP == 64 ? decltype(ve)::value : 1;
             const int nv = del4 ? col_blocks_n<LP, VE>(X, KV) : 0, nc = col_blocks<LP>(X, KC);
+            if (nv && nc && nc < kSmallC) {
+                if (X.selfc) k_dyn_C12<LP, true, VE><<<nv + nc, 256, 0, st>>>(X, a, nv);
+                else k_dyn_C12<LP, false, VE><<<nv + nc, 256, 0, st>>>(X, a, nv);
+                return;
+            }
             if (nv && X.selfc) k_dyn_C<LP, true, VE, 1><<<nv, 256, 0, st>>>(X, a);
             else if (nv) k_dyn_C<LP, false, VE, 1><<<nv, 256, 0, st>>>(X, a);
             if (nc && X.selfc) k_dyn_C<LP, true, VE, 2><<<nc, 256, 0, st>>>(X, a);

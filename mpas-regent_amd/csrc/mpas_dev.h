@@ -618,10 +618,6 @@ __device__ __forceinline__ void cell_pair(const double* f, int c1, int c2, int o
 template <int LP>
 __device__ __forceinline__ void put2(double* fa, int ia, double* fb, int ib, int k, double a, double b, bool oka,
                                      bool okb) {
-#if MPAS_NOHOLE  // (timing-only experiment build: the never-written slots written too -- wrong values)
-    oka = oka || k <= 63;
-    okb = okb || k <= 63;
-#endif
     if constexpr (LP == 64) {
         double x = a, y = b;
         swap_halves(x, y);

@@ -21,7 +21,7 @@ KERNEL_TASK = [
     (r"k_moist", "atm_compute_moist_coefficients"),
     (r"k_vert_imp", "atm_compute_vert_imp_coefs"),
     (r"k_dyn_[ABE]<\d+, true", "atm_compute_dyn_tend_work[rk0]"),
-    (r"k_dyn_([CD]|DE)<", "atm_compute_dyn_tend_work[rk0]"),
+    (r"k_dyn_([CD]|DE|C12)<", "atm_compute_dyn_tend_work[rk0]"),
     # option hfuse: launches shared by two tasks (timing keys hfuse[a+b])
     (r"k_hf_", "hfuse"),
     (r"k_dyn_[ABE]<\d+, false", "atm_compute_dyn_tend_work[rk>0]"),

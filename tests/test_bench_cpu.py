@@ -186,6 +186,13 @@ def test_roofline_defer4_and_vdyn_accounting():
     na = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1, store_v=True, noA=True)
     assert abs(t["b_alg_GB_per_step"] - (d0o + d1 + na) / 1e9) < 1e-3
     assert set(t["variants"]) == {"[rk0+copy+d4o]", "[rk>0+d4i]", "[rk>0+v-A]"}
+    # the fraction without the fusecopy bytes: the rk_step 0 launch's
+    # ru_save / u_2 stores out, nothing else
+    d0x = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, defer_out=True)
+    assert d0o - d0x == 2 * e3
+    assert t["variants"]["[rk0+copy+d4o]"]["b_alg_GB_excl_fusecopy"] == round(d0x / 1e9, 4)
+    want = (d0x + d1 + na) / 1e9 / (t["ms_per_step"] * 1e-3) / bench.HBM_PEAK_GBS
+    assert abs(bench.frac_excl_copy(t) - want) < 2e-4
 
 
 def test_roofline_acoustic_rtheta_pp_old_accounting():
