@@ -856,8 +856,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a.rayleigh_damp_u = 0;
         a.exact_q = c->exact;
         a.tme = tme;
-        // (the MPAS dynamics' one combined launch: D beside E, under hfuse = 1 only)
-        a.hfuse = hf || (S.physics == 2 && c->hfuse == 1 && !c->halo);
+        a.hfuse = hf;
         a.cp = (fcopy && r == 0) ? 1 : 0;
         // option defer4: an rk_step 0 stage followed by an rk_step > 0 one leaves its kernel D
         // (tend_u_euler's del4 part; its tend_u is dead: the next stage rewrites it and no task
