@@ -661,7 +661,7 @@ def main():
     fused = bool(ctx.get_option("fusedamp_active"))
     fsetup = bool(ctx.get_option("fusesetup"))
     fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
-    fcopy = fsetup and bool(ctx.get_option("fusecopy")) and not args.physics  # (decomposed too, as srk3 does)
+    fcopy = fsetup and bool(ctx.get_option("fusecopy"))  # (decomposed and MPAS forms too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9

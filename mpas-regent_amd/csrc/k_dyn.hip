@@ -534,14 +534,14 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
 // PART (a launch's blocks): 1 the vertex blocks, 2 the cell blocks -- two launches, each
 // with its mesh rows as scalar loads (one grid of both interleaved made the compiler load
 // ~24 of them per wave with vector loads: the other path's stores could clobber them)
+// bi: the block's index among its part's blocks (after the XCD remap)
 template <int LP, bool SELF, int VE, int PART>
-__device__ __forceinline__ void dyn_C_body(const DevState& S, const DynK& a, Blk bk) {
+__device__ __forceinline__ void dyn_C_body(const DevState& S, const DynK& a, int bi) {
     const int L = S.L;
     const double* dsu = fd(S, F_delsq_u);
-    ColMap<LP> m(S, KV, bk);
-    const int bi = m.blk;
+    const int kk = (int)(threadIdx.x % LP);
     if constexpr (PART == 1) {  // VE vertices: delsq_vorticity (:1052-1060)
-        const int v0 = col_of<LP>(bi) * VE + S.lo[KV], k = m.k;
+        const int v0 = col_of<LP>(bi) * VE + S.lo[KV], k = kk;
         if (v0 >= S.nVO) return;  // (k >= L exits after the gathers: gather2 needs every lane)
         int ev[VE][3];
         double d[VE][3], sg_[VE][3], dc_[VE][3], iat[VE];
@@ -573,7 +573,7 @@ __device__ __forceinline__ void dyn_C_body(const DevState& S, const DynK& a, Blk
         return;
     }
     const int c = col_of<LP>(bi) + S.lo[KC];
-    const int k = m.k;
+    const int k = kk;
     if (c >= S.nCO) return;
     const size_t p = (size_t)c * LP + lpos(LP, k);
     const bool live = k <= L, kl = k < L;
@@ -668,16 +668,15 @@ __device__ __forceinline__ void dyn_C_body(const DevState& S, const DynK& a, Blk
 }
 template <int LP, bool SELF, int VE, int PART>
 __global__ __launch_bounds__(256) void k_dyn_C(DevState S, DynK a) {
-    dyn_C_body<LP, SELF, VE, PART>(S, a, this_blk());
+    dyn_C_body<LP, SELF, VE, PART>(S, a, xcd_block(S.xcd));
 }
-// both parts in one grid (the vertex blocks first) where a launch's fixed cost is most of
-// its time: grids under kSmallC cell blocks
-constexpr int kSmallC = 4096;
+// both parts in one grid, the vertex and the cell blocks interleaved in proportion
+// (vc_block, option vcmix) so that the delsq_u columns both gather are fetched into L2 once
 template <int LP, bool SELF, int VE>
 __global__ __launch_bounds__(256) void k_dyn_C12(DevState S, DynK a, int nv) {
-    const int b = (int)blockIdx.x;
-    if (b < nv) dyn_C_body<LP, SELF, VE, 1>(S, a, Blk{b, nv});
-    else dyn_C_body<LP, SELF, VE, 2>(S, a, Blk{b - nv, (int)gridDim.x - nv});
+    int bi;
+    if (vc_block(S, xcd_block(S.xcd), nv, bi)) dyn_C_body<LP, SELF, VE, 1>(S, a, bi);
+    else dyn_C_body<LP, SELF, VE, 2>(S, a, bi);
 }
 
 // ------------------------------------------------------------------------ D (rk0, del4)
@@ -1072,7 +1071,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         auto go = [&](auto ve) {
             constexpr int VE = LP == 64 ? decltype(ve)::value : 1;
             const int nv = del4 ? col_blocks_n<LP, VE>(X, KV) : 0, nc = col_blocks<LP>(X, KC);
-            if (nv && nc && nc < kSmallC) {
+            if (nv && nc) {
                 if (X.selfc) k_dyn_C12<LP, true, VE><<<nv + nc, 256, 0, st>>>(X, a, nv);
                 else k_dyn_C12<LP, false, VE><<<nv + nc, 256, 0, st>>>(X, a, nv);
                 return;

@@ -820,8 +820,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             return e;
         });
     }
-    // option fusecopy: ru_save / u_2 by stage 0's dyn_tend edge kernel (reads u and ru there)
-    const bool fcopy = c->fusesetup && c->fusecopy && S.physics == 0;
+    // option fusecopy: ru_save / u_2 by stage 0's dyn_tend edge kernel (reads u and ru there;
+    // no task between the setup and that kernel reads ru_save or u_2, in any physics mode)
+    const bool fcopy = c->fusesetup && c->fusecopy;
     // option fusedamp (reference semantics): each damping but the step's last is applied by
     // the next acoustic launch (k_acoustic MODE 2), the last from the div the acoustic step
     // stored (launch_div_damping_div); the same bits as the separate task.  Decomposed (option

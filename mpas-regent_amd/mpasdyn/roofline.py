@@ -218,15 +218,17 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     recover after each stage; transport = 1 adds the scalar save and the transport;
     fusedamp (reference semantics): six of the seven dampings run inside the next acoustic
     launch; fusecopy (with fusesetup): setup's edge copies in stage 0's dyn_tend"""
+    copy = bool(fusesetup and fusecopy)
     if physics:
         p = {"physics": physics}
         if fusesetup:  # stage 0's setup + moist + vert_imp in one launch (MPAS forms)
-            out = [("atm_rk_integration_setup", {"fused": True, **p}, 1), ("atm_compute_vert_imp_coefs", {}, 1)]
+            out = [("atm_rk_integration_setup", {"fused": True, "copy": copy, **p}, 1),
+                   ("atm_compute_vert_imp_coefs", {}, 1)]
         else:
             out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
                    ("atm_compute_vert_imp_coefs", {}, 2)]
         if schedule == 1:
-            out += [("atm_compute_dyn_tend_work", {"rk_step": 0, **p}, 1),
+            out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, **p}, 1),
                     ("atm_compute_dyn_tend_work", {"rk_step": 1, **p}, 2)]
         out += [("atm_set_smlstep_pert_variables_work", p, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 3),
@@ -242,7 +244,6 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
         if transport:
             out += [("scalars_save", {}, 1), ("atm_advance_scalars_mono", {}, 1)]
         return out
-    copy = bool(fusesetup and fusecopy)
     if fusesetup:
         out = [("atm_rk_integration_setup", {"fused": True, "copy": copy}, 1), ("atm_compute_vert_imp_coefs", {}, 1)]
     else:

@@ -161,6 +161,11 @@ def test_roofline_fusecopy_moves_the_edge_copies():
     d0 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0)
     d1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True)
     assert s0 - s1 == 4 * e3 and d1 - d0 == 2 * e3
+    # the MPAS forms (round 5: srk3 applies fusecopy under every physics mode)
+    for physics in (1, 2):
+        a = roofline.b_alg_step(dims, 1, physics, 0, False, True, False, False)
+        b = roofline.b_alg_step(dims, 1, physics, 0, False, True, False, True)
+        assert a - b == 2 * e3
 
 
 def test_roofline_defer4_and_vdyn_accounting():
