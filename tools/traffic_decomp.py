@@ -86,7 +86,7 @@ KERN["r04"] = _r04
 
 # the kernel names of the rocprofv3 output per launch kind
 PAT = {
-    ("rk0", "A"): r"^k_dyn_A<64, true", ("rk0", "B"): r"^k_dyn_B<64, true", ("rk0", "C"): r"^k_dyn_C<64",
+    ("rk0", "A"): r"^k_dyn_A<64, true", ("rk0", "B"): r"^k_dyn_B<64, true", ("rk0", "C"): r"^k_dyn_C(12)?<64",
     ("rk0", "D"): r"^k_dyn_D<64", ("rk0", "E"): r"^k_dyn_E<64, true",
     ("rk1", "A"): r"^k_dyn_A<64, false", ("rk1", "B"): r"^k_dyn_B<64, false, false, true(, false)?>$",
     ("rk1", "E"): r"^k_dyn_E<64, false",
