@@ -79,11 +79,15 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * (read-only "fusedamp_active"); "fusesml" = 1 (default, with fusedamp) runs each stage's
  * set_smlstep inside its first acoustic launch; "fusesetup" = 1 (default) runs setup, moist
  * and stage 0's vert_imp as one launch; "fusecopy" = 1 (default, with fusesetup) makes
- * setup's edge copies in stage 0's dyn_tend edge kernel (decomposed contexts too); "defer4" = 1
+ * setup's edge copies in stage 0's dyn_tend edge kernel (decomposed contexts and every
+ * "physics" mode too); "defer4" = 1
  * (default) applies rk_step 0's del4 of tend_u_euler (dyn_tend kernel D) in the next stage's
  * rk_step > 0 edge kernel; "vdyn" = 1 (default) has the last stage's dyn_tend edge kernel store
  * solve_diagnostics' v from the u it gathers (when edgesOnEdge_ECP = edgesOnEdge, read-only
- * "eoe_same"); "tmedge" = 1 (default 0) has
+ * "eoe_same"); "keep_check" = 1 (default 0; debug, slow) compares every field's keep tail -- the value of
+ * each column's slot the reference never writes, which the kernels store back so that every
+ * column is written as whole lines -- with the field after every task and fails the task
+ * (MPAS_EINVAL, naming the task, the field and the first entity) on a mismatch.  "tmedge" = 1 (default 0) has
  * dyn_tend store theta_m(cell1) + theta_m(cell2) per edge for the acoustic substeps;
  * "hfuse" = 1 puts independent neighbouring kernels in one launch, 2 (default) only below
  * 16384 owned cells, undecomposed (read-only "hfuse_active"). "fusedamp_halo" = 1 (default)
