@@ -84,7 +84,10 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * (default) applies rk_step 0's del4 of tend_u_euler (dyn_tend kernel D) in the next stage's
  * rk_step > 0 edge kernel; "vdyn" = 1 (default) has the last stage's dyn_tend edge kernel store
  * solve_diagnostics' v from the u it gathers (when edgesOnEdge_ECP = edgesOnEdge, read-only
- * "eoe_same"); "keep_check" = 1 (default 0; debug, slow) compares every field's keep tail -- the value of
+ * "eoe_same"); "bsplit" (fast path, speed only) puts dyn_tend's per-edge theta flux (and the MPAS dynamics' w
+ * flux) in an edge kernel of its own beside the edge kernel B: 1 always, 2 (default) under
+ * "physics" = 2 only, where B's registers would otherwise hold it to 3 waves per SIMD, 0 never.
+ * "keep_check" = 1 (default 0; debug, slow) compares every field's keep tail -- the value of
  * each column's slot the reference never writes, which the kernels store back so that every
  * column is written as whole lines -- with the field after every task and fails the task
  * (MPAS_EINVAL, naming the task, the field and the first entity) on a mismatch.  "tmedge" = 1 (default 0) has

@@ -221,8 +221,11 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // uncapped the compiler takes 132 and 3 waves: +35 %, profiles/r04.  At LP < 64 the cap made
 // it spill ~78 VGPRs.  The MPAS dynamics' B (139-147 VGPRs) under the same cap spills 8-32
 // and runs 7-80 % slower: profiles/r04/md_cap_tried)
-template <int LP, bool RK0, bool MD, bool HF, bool DIN = false>
+// NOF (option "bsplit", fast path): the per-edge theta flux H (and the MD w flux) are left to
+// k_dyn_Bf, an edge kernel of their own: this one skips the advCells gathers
+template <int LP, bool RK0, bool MD, bool HF, bool DIN = false, bool NOF = false>
 __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) {
+    static_assert(!NOF || HF, "the split is the fast path's");
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -278,15 +281,18 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     row_ld(ac3, ac3_);
     static_assert(AF == 9, "tv_ pairing below");
     double tr_phys;
-    double2 g_tv[AF / 2];
+    double2 g_tv[AF / 2], g_tvl = make_double2(0.0, 0.0);
+    const double trp_in = NOF ? colk(fd(S, F_tend_ru_physics), e) : 0.0;
+    if constexpr (!NOF) {
 #pragma unroll
-    for (int j = 0; j < AF - 1; j += 2) g_tv[j / 2] = gather2s_ld<LP>(tm_f, ad_[j], ad_[j + 1], k);
-    const double2 g_tvl = gather2_ld<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k);
+        for (int j = 0; j < AF - 1; j += 2) g_tv[j / 2] = gather2s_ld<LP>(tm_f, ad_[j], ad_[j + 1], k);
+        g_tvl = gather2_ld<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k);
+    }
 
     // MD: the state w at the advCells, for the w reconstruction flux_arr of this edge
     double wv_[AF];
     double2 g_wv[AF / 2];
-    if constexpr (MD) {
+    if constexpr (MD && !NOF) {
         const double* w_f = fd(S, F_w);
 #pragma unroll
         for (int j = 0; j < AF - 1; j += 2) g_wv[j / 2] = gather2s_ld<LP>(w_f, ad_[j], ad_[j + 1], k);
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     double tue_in = 0.0, rus_e = 0.0, ts1 = 0.0, ts2 = 0.0;
     double2 g_tr = make_double2(0.0, 0.0), g_ts = make_double2(0.0, 0.0);
     if constexpr (!RK0) {
-        if constexpr (HF) {
+        if constexpr (HF && !NOF) {
             g_tr = gather2_ld<LP>(fd(S, F_tend_u_euler), e, fd(S, F_ru_save), e, k);
             g_ts = gather2s_ld<LP>(fd(S, F_theta_m_save), cell1, cell2, k);
         } else {
@@ -331,16 +337,20 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         g2_fin<LP>(g_ue[j / 2], ue_[j], ue_[j + 1]);
         g2_fin<LP>(g_pve[j / 2], pve_[j], pve_[j + 1]);
     }
+    if constexpr (NOF) {
+        tr_phys = trp_in;
+    } else {
 #pragma unroll
-    for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_tv[j / 2], tv_[j], tv_[j + 1]);
-    g2_fin<LP>(g_tvl, tv_[AF - 1], tr_phys);
-    if constexpr (MD) {
+        for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_tv[j / 2], tv_[j], tv_[j + 1]);
+        g2_fin<LP>(g_tvl, tv_[AF - 1], tr_phys);
+    }
+    if constexpr (MD && !NOF) {
 #pragma unroll
         for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_wv[j / 2], wv_[j], wv_[j + 1]);
     }
     g2_fin<LP>(g_ke, ke1, ke2);
     g2_fin<LP>(g_hd, hd1, hd2);
-    if constexpr (!RK0 && HF) {
+    if constexpr (!RK0 && HF && !NOF) {
         g2_fin<LP>(g_tr, tue_in, rus_e);
         if (a.cp) rus_e = ru_e;  // (the copy below is setup's: ru_save = ru, read after it)
         g2_fin<LP>(g_ts, ts1, ts2);
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     // padding levels get 0.0 (PADW), the scratch F is stored whole.
 
     double Hv = 0.0, dsq = 0.0;  // HF: the values of the paired stores at the end
-    {  // flux_arr of this edge
+    if constexpr (!NOF) {  // flux_arr of this edge
         const double sg = copysign(1.0, ru_e);
         double flux_arr = 0.0;
 #pragma unroll
@@ -388,7 +398,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
             colk(fw(S, X_F), e) = kl ? flux_arr : 0.0;
         }
     }
-    if constexpr (MD) {  // flux_arr of the w advection at this edge (:1174-1197, every edge)
+    if constexpr (MD && !NOF) {  // flux_arr of the w advection at this edge (:1174-1197, every edge)
         const double ru_edge_w = fzm * ru_e + fzp * lvl_dn<LP>(ru_e, k);
         const double sg = copysign(1.0, ru_edge_w);
         double flux_arr = 0.0;
@@ -500,15 +510,24 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         double* tueo = fw(S, F_tend_u_euler);
         if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
             if (a.d4o) {  // (defer4: D runs in the next call's B; this tend_u is dead)
-                put2<LP>(Fo, e, tueo, e, k, Hv, PADW(tue), true, k != L);
-                if (k != L) colk(fw(S, F_delsq_u), e) = dsq;
+                if constexpr (NOF) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, PADW(tue), dsq, k != L, k != L);
+                else put2<LP>(Fo, e, tueo, e, k, Hv, PADW(tue), true, k != L);
+                if (!NOF && k != L) colk(fw(S, F_delsq_u), e) = dsq;
             } else {
-                put2<LP>(Fo, e, fw(S, F_delsq_u), e, k, Hv, dsq, true, k != L);
+                if constexpr (NOF) {
+                    if (k != L) colk(fw(S, F_delsq_u), e) = dsq;
+                } else {
+                    put2<LP>(Fo, e, fw(S, F_delsq_u), e, k, Hv, dsq, true, k != L);
+                }
                 put2<LP>(tueo, e, tuo, e, k, PADW(tue), PADW(tend_u), k != L, k != L);
             }
         } else {
             tend_u += tue + tr_phys;  // :1161-1163 (rk > 0: tue is the tend_u_euler read)
-            put2<LP>(Fo, e, tuo, e, k, Hv, PADW(tend_u), true, k != L);
+            if constexpr (NOF) {
+                if (k != L) colk(tuo, e) = PADW(tend_u);
+            } else {
+                put2<LP>(Fo, e, tuo, e, k, Hv, PADW(tend_u), true, k != L);
+            }
             if (rk0) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, PADW(tue), dsq, k != L, k != L);
             if (DIN && k != L) colk(tueo, e) = PADW(tue);
         }
@@ -522,6 +541,93 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         if (rk0 || DIN) colk(fw(S, F_tend_u_euler), e) = PADW(tue);
         tend_u += tue + tr_phys;  // :1161-1163
         colk(fw(S, F_tend_u), e) = PADW(tend_u);
+    }
+}
+
+// option "bsplit" (fast path): B's per-edge theta flux H = ru F (+ dvEdge (ru_save - ru)
+// theta_m_save at the edge, rk > 0) for E, and under the MPAS dynamics the w flux Hw, as an edge
+// kernel of their own beside k_dyn_B<NOF>: the advCells gathers leave B's registers (the same
+// expressions on the same values: the same bits)
+template <int LP, bool RK0, bool MD>
+__global__ __launch_bounds__(256) void k_dyn_Bf(DevState S, DynK a) {
+    ColMap<LP> m(S, KE);
+    const int L = S.L, k = m.k, e = m.ent;
+    if (e >= S.nEO) return;
+    int rec[24];
+    row_ld(fi(S, X_eB) + (size_t)e * 24, rec);
+    const int cell1 = rec[0], cell2 = rec[1], na = rec[22];
+    const double* tm_f = fd(S, F_theta_m);
+    const int* ad = fi(S, F_advCellsForEdge) + (size_t)e * 15;
+    const double* ac = fd(S, F_adv_coefs) + (size_t)e * 15;
+    const double* ac3 = fd(S, F_adv_coefs_3rd) + (size_t)e * 15;
+    int ad_[AF];
+    double tv_[AF], ac_[AF], ac3_[AF], wv_[AF];
+#pragma unroll
+    for (int j = 0; j < AF; j++) ad_[j] = rec[12 + j];
+    row_ld(ac, ac_);
+    row_ld(ac3, ac3_);
+    const bool kl = k < L;
+    double2 g_tv[AF / 2], g_wv[AF / 2];
+#pragma unroll
+    for (int j = 0; j < AF - 1; j += 2) g_tv[j / 2] = gather2s_ld<LP>(tm_f, ad_[j], ad_[j + 1], k);
+    const double2 g_tvl = gather2_ld<LP>(tm_f, ad_[AF - 1], fd(S, F_ru), e, k);
+    if constexpr (MD) {
+#pragma unroll
+        for (int j = 0; j < AF - 1; j += 2) g_wv[j / 2] = gather2s_ld<LP>(fd(S, F_w), ad_[j], ad_[j + 1], k);
+    }
+    double2 g_ts = make_double2(0.0, 0.0);
+    double rus_e = 0.0;
+    if constexpr (!RK0) {
+        g_ts = gather2s_ld<LP>(fd(S, F_theta_m_save), cell1, cell2, k);
+        rus_e = colk(fd(S, F_ru_save), e);
+    }
+    const double wvl = MD ? colk(fd(S, F_w), ad_[AF - 1]) : 0.0;
+    __builtin_amdgcn_sched_barrier(0);
+    double ru_e;
+#pragma unroll
+    for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_tv[j / 2], tv_[j], tv_[j + 1]);
+    g2_fin<LP>(g_tvl, tv_[AF - 1], ru_e);
+    if constexpr (MD) {
+#pragma unroll
+        for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_wv[j / 2], wv_[j], wv_[j + 1]);
+        wv_[AF - 1] = wvl;
+    }
+    double ts1 = 0.0, ts2 = 0.0;
+    if constexpr (!RK0) {
+        g2_fin<LP>(g_ts, ts1, ts2);
+        if (a.cp) rus_e = ru_e;  // (k_dyn_B's rule: the copy is setup's, ru_save = ru)
+    }
+    {  // k_dyn_B's flux_arr and H, the same expressions
+        const double sg = copysign(1.0, ru_e);
+        double flux_arr = 0.0;
+#pragma unroll
+        for (int j = 0; j < AF; j++) {
+            double scalar_weight = ac_[j] + sg * ac3_[j];
+            flux_arr = add_if(j < na, flux_arr, scalar_weight * tv_[j]);
+        }
+        for (int j = AF; j < na; j++) {
+            double scalar_weight = ac[j] + sg * ac3[j];
+            flux_arr += scalar_weight * colk(tm_f, ad[j]);
+        }
+        double h = ru_e * flux_arr;
+        if constexpr (!RK0) h += fd(S, F_dvEdge)[e] * ((rus_e - ru_e) * 0.5 * (ts2 + ts1));
+        colk(fw(S, X_F), e) = kl ? h : 0.0;
+    }
+    if constexpr (MD) {  // k_dyn_B's w flux, the same expressions
+        const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+        const double ru_edge_w = fzm * ru_e + fzp * lvl_dn<LP>(ru_e, k);
+        const double sg = copysign(1.0, ru_edge_w);
+        double flux_arr = 0.0;
+#pragma unroll
+        for (int j = 0; j < AF; j++) {
+            double scalar_weight = ac_[j] + sg * ac3_[j];
+            flux_arr = add_if(j < na, flux_arr, scalar_weight * wv_[j]);
+        }
+        for (int j = AF; j < na; j++) {
+            double scalar_weight = ac[j] + sg * ac3[j];
+            flux_arr += scalar_weight * colk(fd(S, F_w), ad[j]);
+        }
+        colk(fw(S, X_Fw), e) = (k > 0 && kl) ? ru_edge_w * flux_arr : 0.0;
     }
 }
 
@@ -1057,7 +1163,13 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
-        if (hf) {
+        if (hf && (X.bsplit == 1 || (X.bsplit == 2 && MD))) {  // (option bsplit: the fluxes in k_dyn_Bf first)
+            if (rk0) k_dyn_Bf<LP, true, MD><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_Bf<LP, false, MD><<<nb, 256, 0, st>>>(X, a);
+            if (rk0) k_dyn_B<LP, true, MD, true, false, true><<<nb, 256, 0, st>>>(X, a);
+            else if (din) k_dyn_B<LP, false, MD, true, !MD, true><<<nb, 256, 0, st>>>(X, a);
+            else k_dyn_B<LP, false, MD, true, false, true><<<nb, 256, 0, st>>>(X, a);
+        } else if (hf) {
             if (rk0) k_dyn_B<LP, true, MD, true><<<nb, 256, 0, st>>>(X, a);
             else if (din) k_dyn_B<LP, false, MD, true, !MD><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_B<LP, false, MD, true><<<nb, 256, 0, st>>>(X, a);

@@ -1169,6 +1169,7 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.xcd = 64;  // runs of 64 blocks per XCD (tools/kbench.py: -2.5 % step time vs dispatcher order)
         c->S.trepw = 1;
         c->S.tro = 64;  // transport: pair-major within runs of 64 entities (profiles/r03/transport_v5: -1 to -3 %)
+        c->S.bsplit = 2;  // dyn_tend's flux kernel split off under the MPAS dynamics (profiles/r05/bsplit)
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         // Field f starts (f % 16) * stagger bytes into its allocation (env MPAS_ALLOC_STAGGER,
         // a multiple of 512: whole columns stay aligned; default 2048): equal-sized arrays
@@ -1283,6 +1284,9 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "cve") == 0) {
             if (value != 0 && value != 1 && value != 4 && value != 8) throw Fail{MPAS_EINVAL, "cve must be 0, 1, 4 or 8"};
             c->S.cve = (int)value;
+        } else if (name && std::strcmp(name, "bsplit") == 0) {
+            if (value < 0 || value > 2) throw Fail{MPAS_EINVAL, "bsplit must be 0, 1 or 2"};
+            c->S.bsplit = (int)value;
         } else if (name && std::strcmp(name, "trepw") == 0) {
             if (value != 1 && value != 2) throw Fail{MPAS_EINVAL, "trepw must be 1 or 2"};
             c->S.trepw = (int)value;
@@ -1344,6 +1348,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "trsu") == 0) *value = c->S.trsu;
         else if (name && std::strcmp(name, "trepw") == 0) *value = c->S.trepw;
         else if (name && std::strcmp(name, "cve") == 0) *value = c->S.cve;
+        else if (name && std::strcmp(name, "bsplit") == 0) *value = c->S.bsplit;
         else if (name && std::strcmp(name, "trorder_e") == 0) *value = c->S.troe;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
         else if (name && std::strcmp(name, "tredge") == 0) *value = c->tredge;

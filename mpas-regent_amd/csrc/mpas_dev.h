@@ -123,6 +123,8 @@ struct DevState {
     int epw;  // entities per column slot of the few-gather kernels (div_damp, solve): 1, 2 or 4
     int vcmix;  // 1: the vertex and cell blocks of mixed grids interleaved in proportion (vc_block)
     int cve;  // option "cve": vertices per vertex wave of dyn_tend C at LP = 64 (1, 4, 8; 0: 4)
+    int bsplit;  // option "bsplit": dyn_tend's per-edge theta / w fluxes in an edge kernel of their own
+                 // (fast path): 1 always, 2 under the MPAS dynamics only, 0 never
     int trsu;     // option "trsu": the transport's update forms su again instead of reading X_su
     int trepw;    // option "trepw": transport edge slots per wavefront (1, 2)
     int troe;     // option "trorder_e": the transport edge kernel's slot order (0: trorder's)

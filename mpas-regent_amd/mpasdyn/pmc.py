@@ -20,11 +20,11 @@ KERNEL_TASK = [
     (r"k_setup_(cells|edges|vi)|k_copy64", "atm_rk_integration_setup"),
     (r"k_moist", "atm_compute_moist_coefficients"),
     (r"k_vert_imp", "atm_compute_vert_imp_coefs"),
-    (r"k_dyn_[ABE]<\d+, true", "atm_compute_dyn_tend_work[rk0]"),
+    (r"k_dyn_(Bf|[ABE])<\d+, true", "atm_compute_dyn_tend_work[rk0]"),
     (r"k_dyn_([CD]|DE|C12)<", "atm_compute_dyn_tend_work[rk0]"),
     # option hfuse: launches shared by two tasks (timing keys hfuse[a+b])
     (r"k_hf_", "hfuse"),
-    (r"k_dyn_[ABE]<\d+, false", "atm_compute_dyn_tend_work[rk>0]"),
+    (r"k_dyn_(Bf|[ABE])<\d+, false", "atm_compute_dyn_tend_work[rk>0]"),
     (r"k_set_smlstep", "atm_set_smlstep_pert_variables_work"),
     (r"k_acoustic", "atm_advance_acoustic_step_work"),
     (r"k_div_damp", "atm_divergence_damping_3d"),
