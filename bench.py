@@ -365,6 +365,9 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_compute_dyn_tend_work[rk0+copy]": {"rk_step": 0, "copy": True},
              "atm_compute_dyn_tend_work[rk>0+copy]": {"rk_step": 1, "copy": True},
              "atm_advance_acoustic_step_work[ss0+sml]": {"small_step": 0, "sml": True},
+             "atm_advance_acoustic_step_work[ss0+smlS]": {"small_step": 0, "sml": True, "smls": True},
+             "atm_advance_acoustic_step_work[ss0+smlS+damp]": {"small_step": 0, "damp": True, "sml": True, "smls": True},
+             "atm_set_smlstep_pert_variables_work[flux]": {"part": "flux"},
              "atm_compute_solve_diagnostics[vc]": {"part": "vc"}, "atm_compute_solve_diagnostics[e]": {"part": "e"},
              "hfuse[damp+solve_vc]": {"pair": "damp+solve_vc"}, "hfuse[solve_e+finish]": {"pair": "solve_e+finish"},
              "hfuse[solve_e-v+finish]": {"pair": "solve_e-v+finish"},
@@ -663,7 +666,9 @@ def main():
     fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
     fcopy = fsetup and bool(ctx.get_option("fusecopy"))  # (decomposed and MPAS forms too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
-    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4)
+    smls = fsml and bool(ctx.get_option("smlsum")) and not args.exact
+    b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
+                                 smls)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -686,7 +691,7 @@ def main():
                       "dt": dt, "parallelism": (f"decomposed{world}" if decomposed else
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
-                      "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy),
+                      "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy), "smlsum": int(smls),
                       "fusesml": int(fsml), "defer4": int(d4), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),

@@ -76,12 +76,15 @@ __global__ __launch_bounds__(256) void k_acoustic_orph(DevState S, double coefp)
 // TME (atm_srk3, option "tmedge"): theta_m(cell2) + theta_m(cell1) of each edge comes from
 // X_tme, which the stage's dyn_tend edge kernel formed (theta_m is not written in between):
 // one gathered column per edge instead of two -- the same sums
-// SML (atm_srk3, option "fusesml"; a stage's first substep): the stage's set_smlstep first
-template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>
+// SML (atm_srk3, option "fusesml"; a stage's first substep): the stage's set_smlstep first;
+// 1 from its slope fluxes, 2 (fast path) from their sum per level, X_smlS, formed once per step
+// by k_sml_flux: u_tend, zb_cell and zb3_cell do not change within a step (reference semantics)
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, int SML>
 __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int small_step, double epssm, double resm,
                                               double coefp, int ncb, Blk bk, int wold = 1) {
     static_assert(!(MPASV && MODE), "the deferred damping is the reference semantics' (physics 0)");
     static_assert(!SML || (FIRST && !MPASV), "set_smlstep precedes a stage's first substep (reference semantics)");
+    static_assert(SML != 2 || !EXACT, "the flux sum reassociates: fast path only");
     const int L = S.L, k = (int)(threadIdx.x % LP);
     int blk = bk.b;
     blk = xcd_block_n(S.xcd, blk, ncb);  // (ncb: the cell blocks, bk.n or fewer)
@@ -173,7 +176,17 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
     col_rd2<LP>(fd(S, F_w), fd(S, F_coftz), c, k, L, w, coftz);
     col_rd2<LP>(fd(S, F_zz), fd(S, F_rho_zz), c, k, L, zz, rz);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
-    if constexpr (SML) {
+    if constexpr (SML == 2) {  // (X_smlS: k_sml_flux's sum of the slope fluxes)
+        double wn = w - colk(fd(S, X_smlS), c);
+        wn *= (fzm * zz + fzp * lvl_dn<LP>(zz, k));
+        if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
+            colk(fw(S, F_w), c) = wn;
+            if (k == L) keep_put<LP>(S, F_w, KC, c, wn);  // (w's level L changes: its keep tail too)
+            w = wn;
+        } else if ((k > L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone)) {
+            colk(fw(S, F_w), c) = 0.0;  // (the padding's content: the column's last line written whole)
+        }
+    } else if constexpr (SML == 1) {
         // the stage's atm_set_smlstep_pert_variables_work (:1503-1528, k_set_smlstep's
         // expressions) on this column, just before the substep reads w: the points of cpr
         // (cprMask) within the relaxation zone get w -= sum of the slope fluxes of u_tend,
@@ -192,11 +205,16 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         }
 #pragma unroll
         for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
-        double wn = w;
+        // (exact: the terms subtracted from w one by one, :1512-1521; fast path: summed first
+        // in k_sml_flux's order, then subtracted -- the same bits as SML = 2 and k_set_smlstep's
+        // fast path)
+        double wn = w, sum = 0.0;
 #pragma unroll
         for (int i = 0; i < NF; i++) {
             double flux = sgs_[i] * (fzm * ut_[i] + fzp * utm_[i]);
-            wn = sub_if(i < ne, wn, (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux);
+            const double t = (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux;
+            if constexpr (EXACT) wn = sub_if(i < ne, wn, t);
+            else sum = add_if(i < ne, sum, t);
         }
         for (int i = NF; i < ne; i++) {
             int iEdge = eoc[i];
@@ -204,8 +222,10 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             double ut_m = lvl_dn<LP>(ut, k);
             double flux = sgnc[i] * (fzm * ut + fzp * ut_m);
             size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
-            wn -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+            if constexpr (EXACT) wn -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+            else sum += (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
         }
+        if constexpr (!EXACT) wn = w - sum;
         wn *= (fzm * zz + fzp * lvl_dn<LP>(zz, k));
         if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
             colk(fw(S, F_w), c) = wn;
@@ -423,7 +443,7 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
     put2f<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww));
     store_div(rtp_new);
 }
-template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, bool SML>
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, int SML>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm,
                                                  double coefp, int ncb, int wold) {
     acoustic_body<LP, EXACT, SELF, FIRST, MPASV, MODE, TME, SML>(S, dts, small_step, epssm, resm, coefp, ncb,
@@ -434,7 +454,7 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
 // instead of two (on large grids the separate launch keeps the cell path's mesh rows in
 // scalar loads, profiles/r04/orph_split)
 constexpr int kTailCells = 16384;
-template <int LP, bool EXACT, bool SELF, bool FIRST, bool TME, bool SML>
+template <int LP, bool EXACT, bool SELF, bool FIRST, bool TME, int SML>
 __global__ __launch_bounds__(256) void k_acoustic_o(DevState S, double dts, int small_step, double epssm, double resm,
                                                    double coefp, int ncb, int wold) {
     const int b = (int)blockIdx.x;
@@ -456,6 +476,59 @@ __global__ __launch_bounds__(256) void k_hf_ac_vc(DevState S, double dts, int sm
     else if (b < nb1) acoustic_orph_body<LP, false>(S, coefp, b - ncb);
     else solve_vc_body<LP, EPW, false>(S, nVB, 0, Blk{b - nb1, (int)gridDim.x - nb1});
 }
+
+// X_smlS for SML = 2 (atm_srk3 fast path, reference semantics; once per step): per cell and
+// level k <= L the sum over the cell's edges of set_smlstep's slope-flux terms (k_set_smlstep
+// and acoustic_body SML = 1: the same terms, summed instead of subtracted from w one by one)
+template <int LP>
+__global__ __launch_bounds__(256) void k_sml_flux(DevState S) {
+    ColMap<LP> m(S, KC);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    int e_[NF], c1_[NF], c2_[NF];
+    const int ne = cell_rec<false>(S, c, e_, c1_, c2_);
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgnc = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+    const double *ut_f = fd(S, F_u_tend), *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgs_[NF];
+    row_ld(sgnc, sgs_);
+#pragma unroll
+    for (int i = 0; i < NF; i += 2) gather2s<LP>(ut_f, e_[i], e_[i + 1], k, ut_[i], ut_[i + 1]);
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        ut_[i] = ldz(k <= L, ut_[i]);
+        gather2<LP>(zb, c * 10 + i, zb3, c * 10 + i, k, zb_[i], zb3_[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        double flux = sgs_[i] * (fzm * ut_[i] + fzp * utm_[i]);
+        sum = add_if(i < ne, sum, (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux);
+    }
+    for (int i = NF; i < ne; i++) {
+        int iEdge = eoc[i];
+        double ut = col_rd<LP>(ut_f, iEdge, k, L);
+        double ut_m = lvl_dn<LP>(ut, k);
+        double flux = sgnc[i] * (fzm * ut + fzp * ut_m);
+        size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
+        sum += (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+    }
+    colk(fw(S, X_smlS), c) = k <= L ? sum : 0.0;
+}
+template <int LP>
+static hipError_t sml_flux_lp(const DevState& S, hipStream_t st) {
+    auto run = [&](const DevState& X) {
+        const int nb = col_blocks<LP>(X, KC);
+        if (nb) k_sml_flux<LP><<<nb, 256, 0, st>>>(X);
+    };
+    HALO_RUN_R1(S, st, run, F_u_tend, F_u_tend);  // (u_tend at the edges of owned cells)
+    HALO_WROTE(S, X_smlS);
+    return hipGetLastError();
+}
+hipError_t launch_sml_flux(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, sml_flux_lp, S, st); }
 
 // :1581-1613 restored (Q18, MPAS vertical solver only): ru_p and ruAvg of every owned
 // edge, before the cell kernel reads ru_p.  FIRST (small_step 0): ru_p = dts tend_u and
@@ -534,8 +607,14 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
 #define MPAS_ACO(FI, TM, SM) \
     k_acoustic_o<LP, E, SF, FI, TM, SM><<<ncb + nob, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb, wold)
                 if (first) {
-                    if (tme) sml ? MPAS_ACO(true, true, true) : MPAS_ACO(true, true, false);
-                    else sml ? MPAS_ACO(true, false, true) : MPAS_ACO(true, false, false);
+                    if constexpr (!E) {
+                        if (sml == 2) {
+                            tme ? MPAS_ACO(true, true, 2) : MPAS_ACO(true, false, 2);
+                            return;
+                        }
+                    }
+                    if (tme) sml ? MPAS_ACO(true, true, 1) : MPAS_ACO(true, true, 0);
+                    else sml ? MPAS_ACO(true, false, 1) : MPAS_ACO(true, false, 0);
                 } else {
                     if (tme) MPAS_ACO(false, true, false);
                     else MPAS_ACO(false, false, false);
@@ -565,8 +644,14 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
                 else first ? MPAS_AC(true, false, 0, false, false) : MPAS_AC(false, false, 0, false, false);
             } else {
                 if (first) {
-                    if (tme) sml ? MPAS_AC(true, false, M, true, true) : MPAS_AC(true, false, M, true, false);
-                    else sml ? MPAS_AC(true, false, M, false, true) : MPAS_AC(true, false, M, false, false);
+                    if constexpr (!E) {
+                        if (sml == 2) {
+                            tme ? MPAS_AC(true, false, M, true, 2) : MPAS_AC(true, false, M, false, 2);
+                            return;
+                        }
+                    }
+                    if (tme) sml ? MPAS_AC(true, false, M, true, 1) : MPAS_AC(true, false, M, true, 0);
+                    else sml ? MPAS_AC(true, false, M, false, 1) : MPAS_AC(true, false, M, false, 0);
                 } else {
                     if (tme) MPAS_AC(false, false, M, true, false);
                     else MPAS_AC(false, false, M, false, false);
@@ -592,9 +677,9 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     };
     // (ru_p at the edges of owned cells only; MODE 2 also div at their cells -- X_dvB, the
     // previous substep's; SML u_tend at the edges of owned cells)
-    if (mode == 2 && sml) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, X_dvB, F_u_tend);
+    if (mode == 2 && sml == 1) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, X_dvB, F_u_tend);
     else if (mode == 2) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, X_dvB);
-    else if (sml) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, F_u_tend);
+    else if (sml == 1) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, F_u_tend);
     else HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m);
     if (mode == 0 || wold) HALO_WROTE(S, F_rtheta_pp_old);
     HALO_WROTE(S, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);

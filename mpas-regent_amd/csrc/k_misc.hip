@@ -211,7 +211,9 @@ hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts) 
 // ---------------------------------------------------------------- set_smlstep
 // MD: the MPAS dynamics (physics = 2, ora_mpas_set_smlstep): u_tend is dyn_tend's tend_u
 // and w_tend its tend_w (Q2/Q8), levels 1..L-1 of every cell within the relaxation zone
-template <int LP, bool MD>
+// SUM (reference semantics, fast path): the slope-flux terms summed first, then subtracted from
+// w (k_sml_flux's order: the same bits as atm_srk3's fused set_smlstep); else one by one (:1512-1521)
+template <int LP, bool MD, bool SUM>
 __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
@@ -245,10 +247,13 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
+    double sum = 0.0;
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         double flux = sgn_[i] * (fzm * ut_[i] + fzp * utm_[i]);
-        w = sub_if(i < ne, w, (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux);
+        const double t = (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux;
+        if constexpr (SUM) sum = add_if(i < ne, sum, t);
+        else w = sub_if(i < ne, w, t);
     }
     for (int i = NF; i < ne; i++) {
         int iEdge = eoc[i];
@@ -256,8 +261,10 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
         double ut_m = lvl_dn<LP>(ut, k);
         double flux = sgn[i] * (fzm * ut + fzp * ut_m);
         size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
-        w -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+        if constexpr (SUM) sum += (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+        else w -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
     }
+    if constexpr (SUM) w = w - sum;
     w *= (fzm * zz + fzp * zz_m);
     if (MD) {  // (every level written: 0 and L with their loaded values, the padding with zeros)
         if (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) colk(fw(S, wf), c) = (k >= 1 && k < L) ? w : PADW(w_in);
@@ -269,12 +276,13 @@ __global__ __launch_bounds__(256) void k_set_smlstep(DevState S) {
     }
 }
 template <int LP>
-static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
+static hipError_t smlstep_lp(const DevState& S, hipStream_t st, int exact) {
     const bool md = S.physics == 2;
     auto run = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
-        if (nb && md) k_set_smlstep<LP, true><<<nb, 256, 0, st>>>(X);
-        else if (nb) k_set_smlstep<LP, false><<<nb, 256, 0, st>>>(X);
+        if (nb && md) k_set_smlstep<LP, true, false><<<nb, 256, 0, st>>>(X);
+        else if (nb && !exact) k_set_smlstep<LP, false, true><<<nb, 256, 0, st>>>(X);
+        else if (nb) k_set_smlstep<LP, false, false><<<nb, 256, 0, st>>>(X);
     };
     if (md) {
         HALO_RUN(S, st, run, F_tend_u);
@@ -285,7 +293,9 @@ static hipError_t smlstep_lp(const DevState& S, hipStream_t st) {
     }
     return hipGetLastError();
 }
-hipError_t launch_set_smlstep(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st); }
+hipError_t launch_set_smlstep(const DevState& S, hipStream_t st, int exact) {
+    MPAS_LP_DISPATCH(S.LP, smlstep_lp, S, st, exact);
+}
 
 // ---------------------------------------------------------------- divergence damping
 // (kernel body: k_cols.h divdamp_body)

@@ -56,6 +56,7 @@ const FieldInfo kFields[X_COUNT] = {
     {"eowner", K_E2I, 1, D_M, 0, 0},
     {"orph", K_E2I, 1, D_M, 0, 0},
     {"tme", K_E3, 1, D_M, 0, 0},
+    {"smlS", K_C3, 1, D_M, 0, 0},
     {"Ah", K_E3, 8, D_M, 0, 0},
     {"Rp", K_C3V, 8, D_M, 0, 0},
     {"Rm", K_C3V, 8, D_M, 0, 0},
@@ -95,6 +96,7 @@ struct mpas_ctx {
     // (x1.2562: -3 %; x1.163842: +0.8 %, the pair runs at the lower occupancy of the two)
     int hfuse = 2;
     int fusesml = 1;    // option "fusesml": each stage's set_smlstep inside its first acoustic launch (with fusedamp)
+    int smlsum = 1;     // option "smlsum": its slope-flux sum once per step (fast path, with fusesml)
     int fusedamp_halo = 1;  // option "fusedamp_halo": fusedamp / fusesml on decomposed meshes too
     int tmedge = 0;     // option "tmedge": theta_m edge sums from dyn_tend for the acoustic substeps (same values;
                         // measured slower at both sizes)
@@ -742,7 +744,11 @@ bool hfuse_active(const mpas_ctx* c) {
 // (bench.py aggregates the variants per task)
 // (nold: a fused launch that does not store rtheta_pp_old -- every one but the step's last --
 // tagged "-old" so that bench.py credits it no rtheta_pp_old write)
-const char* acoustic_name(int small_step, bool damp = false, bool sml = false, bool nold = false) {
+// (sml 2: set_smlstep from the step's flux sum X_smlS, "+smlS")
+const char* acoustic_name(int small_step, bool damp = false, int sml = 0, bool nold = false) {
+    if (sml == 2)
+        return damp ? (nold ? "atm_advance_acoustic_step_work[ss0+smlS+damp-old]" : "atm_advance_acoustic_step_work[ss0+smlS+damp]")
+                    : (nold ? "atm_advance_acoustic_step_work[ss0+smlS-old]" : "atm_advance_acoustic_step_work[ss0+smlS]");
     if (sml)  // (option fusesml: the stage's set_smlstep run by this launch first)
         return damp ? (nold ? "atm_advance_acoustic_step_work[ss0+sml+damp-old]" : "atm_advance_acoustic_step_work[ss0+sml+damp]")
                     : (nold ? "atm_advance_acoustic_step_work[ss0+sml-old]" : "atm_advance_acoustic_step_work[ss0+sml]");
@@ -847,6 +853,10 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // the next stage's dyn_tend A (k_acoustic.hip / k_dyn.hip combined launches)
     const bool hf2 = hf && fuse && !tme && S.epw == 2;
     bool vc_done = false, a_done = false, vdyn_on = false;
+    // option smlsum (fast path, with fusesml): the slope-flux sum of set_smlstep formed once per
+    // step (X_smlS); each stage's fused set_smlstep then reads one column instead of u_tend at
+    // the cell's edges and zb_cell / zb3_cell (none of them written within the step)
+    const bool smls = fuse && c->fusesml && c->smlsum && !c->exact && S.physics == 0;
     auto stage_args = [&](int r) {
         DynTendArgs a{};
         a.rk_step = schedule == 0 ? (int)rk_sub_timestep[r] : r;  // Q4
@@ -882,6 +892,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
         run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
     }
+    if (smls) run_task(c, "atm_set_smlstep_pert_variables_work[flux]", [&] { return launch_sml_flux(S, st); });
     for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
         if (rk_step == 1 && !vi_done)
             run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
@@ -900,13 +911,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, dname.c_str(), [&] { return launch_dyn_tend(S, st, a); });
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
         const bool sml = fuse && c->fusesml;
-        if (!sml) run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st); });
+        if (!sml) run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st, c->exact); });
         const int n_small = number_sub_steps[rk_step] + (S.physics ? 0 : 1);  // Q5 (the MPAS form: n)
         for (int small_step = 0; small_step < n_small; small_step++) {
             const double dts = rk_sub_timestep[rk_step];
             if (fuse) {
                 const int mode = pending ? 2 : 1;
-                const int sm = (sml && small_step == 0) ? 1 : 0;
+                const int sm = (sml && small_step == 0) ? (smls ? 2 : 1) : 0;
                 // rtheta_pp_old is read by the separate damping only: the fused one reads the
                 // stored div, so the step's last substep alone leaves it (option fusedamp)
                 const int wold = (done_acoustic + 1 == n_acoustic) ? 1 : 0;
@@ -1252,6 +1263,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
+        else if (name && std::strcmp(name, "smlsum") == 0) c->smlsum = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusedamp_halo") == 0) c->fusedamp_halo = value ? 1 : 0;
         else if (name && std::strcmp(name, "hfuse") == 0) c->hfuse = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (name && std::strcmp(name, "graph_halo") == 0) {
@@ -1382,6 +1394,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         }
         else if (name && std::strcmp(name, "tmedge") == 0) *value = c->tmedge;
         else if (name && std::strcmp(name, "fusesml") == 0) *value = c->fusesml;
+        else if (name && std::strcmp(name, "smlsum") == 0) *value = c->smlsum;
         else if (name && std::strcmp(name, "fusedamp_halo") == 0) *value = c->fusedamp_halo;
         else if (name && std::strcmp(name, "hfuse") == 0) *value = c->hfuse;
         else if (name && std::strcmp(name, "hfuse_active") == 0) *value = hfuse_active(c);
@@ -1797,7 +1810,7 @@ int mpas_atm_compute_dyn_tend_work(mpas_ctx* c, int rk_step, double dt, int hori
               launch_dyn_tend(c->S, c->stream, a));
 }
 int mpas_atm_set_smlstep_pert_variables_work(mpas_ctx* c) {
-    MPAS_TASK("atm_set_smlstep_pert_variables_work", launch_set_smlstep(c->S, c->stream));
+    MPAS_TASK("atm_set_smlstep_pert_variables_work", launch_set_smlstep(c->S, c->stream, c->exact));
 }
 int mpas_atm_advance_acoustic_step_work(mpas_ctx* c, double dts, int small_step) {
     MPAS_TASK(acoustic_name(small_step), launch_acoustic(c->S, c->stream, dts, small_step, c->exact));

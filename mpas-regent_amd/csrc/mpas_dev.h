@@ -92,6 +92,9 @@ enum FieldId {
     X_tme,      // theta_m(cellsOnEdge(1)) + theta_m(cellsOnEdge(0)) per edge and level, formed
                 // by dyn_tend's edge kernel (option "tmedge"): theta_m does not change between
                 // a stage's dyn_tend and its acoustic substeps, which read it there   E3
+    X_smlS,     // set_smlstep's slope flux sum of u_tend per cell and level, formed once per step
+                // (atm_srk3 fast path, reference semantics: u_tend, zb_cell, zb3_cell are not
+                // written by any task of the step) for the stages' fused set_smlstep      C3
     // monotonic scalar transport (k_transport.hip), one column per (entity, scalar)
     X_Ah,       // antidiffusive edge flux                                      E3 x 8
     X_Rp,       // R+ (fraction of the incoming antidiffusive flux allowed)     C3V x 8
@@ -227,17 +230,22 @@ hipError_t launch_hf_solve_e_dyn_A(const DevState& S, hipStream_t st, const DynT
 // ... and stage 0's setup + moist + vert_imp launch (fusesetup) beside stage 0's dyn_tend A
 hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges);
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
-hipError_t launch_set_smlstep(const DevState& S, hipStream_t st);
+// exact = 0 (reference semantics): the slope-flux terms summed, then subtracted (k_sml_flux's order)
+hipError_t launch_set_smlstep(const DevState& S, hipStream_t st, int exact);
 // mode (reference semantics, no halo; atm_srk3 with option "fusedamp"): 0 plain, 1 also
 // writes div of this substep (X_dvA), 2 also applies the previous substep's damping
 // (coefficient coef_prev, its div in X_dvB) to the ru_p it reads and writes the damped
 // ru_p to X_rupB; the caller swaps the buffer pairs after the launch
 // tme: theta_m at the cells of each edge from X_tme (valid: dyn_tend of this stage wrote it)
-// sml: the stage's set_smlstep first (a stage's first substep, mode 1 / 2; option fusesml)
+// sml: the stage's set_smlstep first (a stage's first substep, mode 1 / 2; option fusesml):
+// 1 from its slope fluxes, 2 (exact = 0) from X_smlS, the step's launch_sml_flux
 // wold 0 (mode 1 / 2 only): rtheta_pp_old not stored -- atm_srk3's fused damping reads the div
 // this launch stores instead, so only the step's last substep leaves rtheta_pp_old
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode = 0,
                            double coef_prev = 0.0, int tme = 0, int sml = 0, int wold = 1);
+// X_smlS = the sum of set_smlstep's slope-flux terms per cell and level (atm_srk3 fast path,
+// once per step: u_tend / zb_cell / zb3_cell are not written within a step)
+hipError_t launch_sml_flux(const DevState& S, hipStream_t st);
 // old_zero: only from srk3, right after a stage's first acoustic substep (k_div_damp OLD0)
 hipError_t launch_div_damping(const DevState& S, hipStream_t st, double dts, int old_zero = 0);
 // the damping from the div buffer X_dvB (fusedamp: the step's last substep), ru_p in place

@@ -25,7 +25,7 @@ KERNEL_TASK = [
     # option hfuse: launches shared by two tasks (timing keys hfuse[a+b])
     (r"k_hf_", "hfuse"),
     (r"k_dyn_(Bf|[ABE])<\d+, false", "atm_compute_dyn_tend_work[rk>0]"),
-    (r"k_set_smlstep", "atm_set_smlstep_pert_variables_work"),
+    (r"k_set_smlstep|k_sml_flux", "atm_set_smlstep_pert_variables_work"),
     (r"k_acoustic", "atm_advance_acoustic_step_work"),
     (r"k_div_damp", "atm_divergence_damping_3d"),
     (r"k_solve_", "atm_compute_solve_diagnostics"),

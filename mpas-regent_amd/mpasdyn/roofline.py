@@ -15,7 +15,7 @@ roofline.achieved divides by the measured launch time.
 
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
-          part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True):
+          part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -99,6 +99,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         if defer_out and rk_step == 0:  # option defer4: tend_u of this call is dead and not stored
             writes = [x for x in writes if x != "tend_u"]  # (its del4 runs in the next call: no credit taken)
         return reads + mesh, writes
+    if task == "atm_set_smlstep_pert_variables_work" and part == "flux":
+        # option smlsum (atm_srk3 fast path): the slope-flux sum, once per step (X_smlS, scratch)
+        return ["zb_cell", "zb3_cell", "u_tend", "nEdgesOnCell", "edgesOnCell", "edgesOnCell_sign"], []
     if task == "atm_set_smlstep_pert_variables_work":
         if md:
             return (["zz", "tend_w", "zb_cell", "zb3_cell", "tend_u", "bdyMaskCell", "nEdgesOnCell", "edgesOnCell",
@@ -122,7 +125,10 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         if damp:  # option fusedamp: the previous substep's atm_divergence_damping_3d applied here
             reads += ["rtheta_pp", "rtheta_pp_old", "isShared", "specZoneMaskEdge"]
             writes += ["ru_p"]
-        if sml:  # option fusesml: the stage's atm_set_smlstep_pert_variables_work first
+        if sml and smls:  # option smlsum: set_smlstep from the step's flux sum (X_smlS, scratch)
+            reads += ["zz", "w", "cprMask", "bdyMaskCell"]
+            writes += ["w"]
+        elif sml:  # option fusesml: the stage's atm_set_smlstep_pert_variables_work first
             r2, w2 = _sets("atm_set_smlstep_pert_variables_work", physics=physics)
             reads += r2
             writes += w2
@@ -212,7 +218,7 @@ def b_alg(task, dims, **kw):
 
 
 def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-                  fusecopy=False, defer4=False):
+                  fusecopy=False, defer4=False, smlsum=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -254,8 +260,11 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                 ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
     # (fusedamp: only the step's last acoustic launch stores rtheta_pp_old, wold)
     if fusedamp and fusesml:
-        out += [("atm_advance_acoustic_step_work", {"small_step": 0, "sml": True, "wold": False}, 1),
-                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, "sml": True, "wold": False}, 2),
+        sm = {"sml": True, "smls": bool(smlsum)}
+        if smlsum:  # option smlsum: the slope-flux sum once per step
+            out += [("atm_set_smlstep_pert_variables_work", {"part": "flux"}, 1)]
+        out += [("atm_advance_acoustic_step_work", {"small_step": 0, **sm, "wold": False}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, **sm, "wold": False}, 2),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 1),
                 ("atm_divergence_damping_3d", {}, 1)]
@@ -278,6 +287,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
 
 
 def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-               fusecopy=False, defer4=False):
+               fusecopy=False, defer4=False, smlsum=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
-                                                                        fusesetup, fusesml, fusecopy, defer4))
+                                                                        fusesetup, fusesml, fusecopy, defer4,
+                                                                        smlsum))

@@ -223,3 +223,29 @@ def test_roofline_acoustic_rtheta_pp_old_accounting():
     rep = {"atm_advance_acoustic_step_work[ss>0+damp-old]": (3, 1.5), "atm_advance_acoustic_step_work[ss>0+damp]": (1, 0.5)}
     t = bench.task_table(rep, dims, 1, physics=False)["atm_advance_acoustic_step_work"]
     assert abs(t["b_alg_GB_per_step"] - (3 * b + a) / 1e9) < 1e-3
+
+
+def test_roofline_smlsum_accounting():
+    """option smlsum: set_smlstep's zb_cell / zb3_cell / u_tend / edge-sign reads counted once per
+    step (the flux task) instead of in each of the three fused acoustic launches; the flux task
+    also reads the cell's edge list, which the acoustic launches share; bench.py reads the tags"""
+    import bench
+    from mpasdyn import roofline
+    dims = (163842, 491520, 327680, 56)
+    fb = lambda n: roofline.field_bytes(n, *dims)  # noqa: E731
+    a = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, True, False)
+    b = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, True, True)
+    kw = dict(small_step=0, damp=True, sml=True, wold=False)
+    d_ac = roofline.b_alg("atm_advance_acoustic_step_work", dims, **kw) - \
+        roofline.b_alg("atm_advance_acoustic_step_work", dims, smls=True, **kw)
+    flux = roofline.b_alg("atm_set_smlstep_pert_variables_work", dims, part="flux")
+    assert flux - d_ac == fb("nEdgesOnCell") + fb("edgesOnCell")  # (the acoustic launch reads them anyway)
+    assert d_ac > fb("u_tend") + fb("edgesOnCell_sign")  # (+ the zb_cell / zb3_cell components)
+    assert a - b == 3 * d_ac - flux
+    rep = {"atm_set_smlstep_pert_variables_work[flux]": (1, 0.2),
+           "atm_advance_acoustic_step_work[ss0+smlS+damp-old]": (2, 1.2)}
+    t = bench.task_table(rep, dims, 1, physics=False)
+    assert abs(t["atm_set_smlstep_pert_variables_work"]["b_alg_GB_per_step"]
+               - roofline.b_alg("atm_set_smlstep_pert_variables_work", dims, part="flux") / 1e9) < 1e-3
+    ac = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=0, damp=True, sml=True, smls=True, wold=False)
+    assert abs(t["atm_advance_acoustic_step_work"]["b_alg_GB_per_step"] - 2 * ac / 1e9) < 1e-3
