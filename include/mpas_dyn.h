@@ -56,8 +56,8 @@ const char* mpas_last_error(const mpas_ctx* ctx);
 int mpas_sync(mpas_ctx* ctx);
 /* the HIP stream (hipStream_t) the tasks run on, for callers that time with events */
 int mpas_get_stream(mpas_ctx* ctx, void** stream);
-/* options: "exact" = 1 makes the two reassociated kernels (Q10 q sum, acoustic scan)
- * evaluate the reference's literal order (bit-identical to the oracle, slower);
+/* options: "exact" = 1 makes the reassociated kernels (Q10 q sum, acoustic scan, set_smlstep's
+ * slope-flux sum) evaluate the reference's literal order (bit-identical to the oracle, slower);
  * "xcd" = 0 dispatcher block order, 1 one contiguous eighth of the columns per XCD,
  * G > 1 runs of G blocks per XCD inside windows of 8G (default 64); "epw" = 1, 2 (default)
  * or 4 entities per column slot in div_damping / solve_diagnostics; "cve" = 1, 4 or 8
@@ -77,7 +77,9 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * Cross-task fusion in mpas_atm_srk3 (reference semantics):
  * "fusedamp" = 1 (default) applies each divergence damping inside the next acoustic launch
  * (read-only "fusedamp_active"); "fusesml" = 1 (default, with fusedamp) runs each stage's
- * set_smlstep inside its first acoustic launch; "fusesetup" = 1 (default) runs setup, moist
+ * set_smlstep inside its first acoustic launch; "smlsum" = 1 (default, with fusesml, exact = 0)
+ * forms set_smlstep's slope-flux sum once per step (u_tend, zb_cell and zb3_cell are not written
+ * within a step) and the stages' fused set_smlstep read it; "fusesetup" = 1 (default) runs setup, moist
  * and stage 0's vert_imp as one launch; "fusecopy" = 1 (default, with fusesetup) makes
  * setup's edge copies in stage 0's dyn_tend edge kernel (decomposed contexts and every
  * "physics" mode too); "defer4" = 1
