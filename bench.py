@@ -352,7 +352,7 @@ def pmc_child(args):
 
 
 # ------------------------------------------------------------------ roofline
-def task_table(rep, work_dims, n_prof, physics):
+def task_table(rep, work_dims, n_prof, physics, ddx=False):
     """per timing key (a task, split by the arguments that change its read/write set)
     and aggregated per Regent task: launches and device ms per step, B_alg per step"""
     from mpasdyn import roofline
@@ -381,6 +381,7 @@ def task_table(rep, work_dims, n_prof, physics):
              "atm_compute_dyn_tend_work[rk0+copy-A]": {"rk_step": 0, "copy": True, "noA": True},
              "atm_compute_dyn_tend_work[rk>0+copy-A]": {"rk_step": 1, "copy": True, "noA": True},
              "hfuse[setup+dyn_A]": {"pair": "setup+dyn_A"},
+             "hfuse[setup+dyn_A+sml_flux]": {"pair": "setup+dyn_A+sml_flux"},
              "atm_advance_acoustic_step_work[ss0+sml+damp]": {"small_step": 0, "damp": True, "sml": True},
              "atm_advance_acoustic_step_work[ss>0+damp]": {"small_step": 1, "damp": True},
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
@@ -407,6 +408,8 @@ def task_table(rep, work_dims, n_prof, physics):
             kw = dict(kw_of.get(name[:-5] + "]", {}), wold=False)
         else:
             kw = dict(kw_of.get(name, {}))
+        if ddx and (task == "atm_advance_acoustic_step_work" or name == "hfuse[acoustic+solve_vc]"):
+            kw["ddx"] = True  # (option smlsum: the acoustic launches read rw_save - rw from X_Dd)
         if physics and task == "atm_advance_acoustic_step_work":
             kw["physics"] = 1  # the acoustic task's MPAS form also updates ru_p / ruAvg
         if physics == 2 and task in ("atm_rk_integration_setup", "atm_compute_moist_coefficients",
@@ -639,7 +642,9 @@ def main():
     ctx.sync()
     rep = ctx.timing_report()
     ctx.timing(False)
-    tasks_out = task_table(rep, work_dims, n_prof, args.physics)
+    smls = (bool(ctx.get_option("fusedamp_active")) and bool(ctx.get_option("fusesml")) and
+            bool(ctx.get_option("smlsum")) and not args.exact and not args.physics)
+    tasks_out = task_table(rep, work_dims, n_prof, args.physics, ddx=smls)
     if traffic_by:
         for name, t in tasks_out.items():
             keys = [k for k in traffic_by if k.split("[")[0] == name]
@@ -666,7 +671,6 @@ def main():
     fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
     fcopy = fsetup and bool(ctx.get_option("fusecopy"))  # (decomposed and MPAS forms too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
-    smls = fsml and bool(ctx.get_option("smlsum")) and not args.exact
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
                                  smls)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256) void k_acoustic_orph(DevState S, double coefp)
 // by k_sml_flux: u_tend, zb_cell and zb3_cell do not change within a step (reference semantics)
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, int SML>
 __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int small_step, double epssm, double resm,
-                                              double coefp, int ncb, Blk bk, int wold = 1) {
+                                              double coefp, int ncb, Blk bk, int wold = 1, int ddx = 0) {
     static_assert(!(MPASV && MODE), "the deferred damping is the reference semantics' (physics 0)");
     static_assert(!SML || (FIRST && !MPASV), "set_smlstep precedes a stage's first substep (reference semantics)");
     static_assert(SML != 2 || !EXACT, "the flux sum reassociates: fast path only");
@@ -240,8 +240,17 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
     const double tw = (MPASV && S.physics == 2) ? col_rd<LP>(fd(S, F_tend_w), c, k, L) : w;
     col_rd2<LP>(fd(S, F_cofwt), fd(S, F_cofwz), c, k, L, cofwt, cofwz);
     col_rd2<LP>(fd(S, F_cofwr), fd(S, F_a_tri), c, k, L, cofwr, a_tri);
-    col_rd2<LP>(fd(S, F_alpha_tri), fd(S, F_rw_save), c, k, L, alpha, rws);
-    col_rd2<LP>(fd(S, F_rw), fd(S, F_dss), c, k, L, rw, dss);
+    // (ddx, atm_srk3 with option smlsum: rw_save - rw, the step uses only their difference, from
+    // X_Dd -- formed once per step, the same value: one column read instead of two)
+    double dd;
+    if (!MPASV && ddx) {
+        col_rd2<LP>(fd(S, F_alpha_tri), fd(S, X_Dd), c, k, L, alpha, dd);
+        dss = col_rd<LP>(fd(S, F_dss), c, k, L);
+    } else {
+        col_rd2<LP>(fd(S, F_alpha_tri), fd(S, F_rw_save), c, k, L, alpha, rws);
+        col_rd2<LP>(fd(S, F_rw), fd(S, F_dss), c, k, L, rw, dss);
+        dd = rws - rw;
+    }
     double gam = 0.0, tend_th = 0.0;
     if constexpr (MPASV) col_rd2<LP>(fd(S, F_gamma_tri), fd(S, F_tend_theta), c, k, L, gam, tend_th);
     const double tt = MPASV ? tend_th : tm;  // tend_rt: the reference reads theta_m (Q8)
@@ -357,7 +366,7 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         }
         double r = (k == L) ? rwold : z;
         if (in) {  // implicit Rayleigh damping of w
-            const double d = rws - rw;
+            const double d = dd;
             r = (z + d - dts * dss * (fzm * zz + fzp * zz_m) * (fzm * rz + fzp * rz_m) * w) / (1.0 + dts * dss) - d;
             ww = ww + 0.5 * (1.0 + epssm) * r;
         }
@@ -391,9 +400,9 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
                      cofwr * ((rs + rsm) + resm * (rpp + R)) + cofwt * (ts + resm * rtp) + cofwt_m * (tsm + resm * T);
                 y -= a_tri * X;
                 y *= alpha;
-                y += (rws - rw) - dts * dss * (fzm * zz + fzp * zz_m) * (fzm * rz + fzp * rz_m) * w;
+                y += dd - dts * dss * (fzm * zz + fzp * zz_m) * (fzm * rz + fzp * rz_m) * w;
                 y /= (1.0 + dts * dss);
-                y -= (rws - rw);
+                y -= dd;
                 x = y;
                 rpp_new = rs - cofrz * (rwp_p - x);
                 rtp_new = ts - rdzw * (coftz_p * rwp_p - coftz * x);
@@ -414,7 +423,7 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             const double cT = cofwz * resm * zz_m + cofwt_m * resm;
             const double cR = cofwr * resm;
             const double F = 1.0 + dts * dss;
-            const double Dd = rws - rw;
+            const double Dd = dd;
             const double E = dts * dss * (fzm * zz + fzp * zz_m) * (fzm * rz + fzp * rz_m) * w;
             const double af = alpha / F;
             G = af * (cT * Tcm - cR * Rcm - a_tri);
@@ -445,9 +454,9 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
 }
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, int SML>
 __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int small_step, double epssm, double resm,
-                                                 double coefp, int ncb, int wold) {
+                                                 double coefp, int ncb, int wold, int ddx) {
     acoustic_body<LP, EXACT, SELF, FIRST, MPASV, MODE, TME, SML>(S, dts, small_step, epssm, resm, coefp, ncb,
-                                                                this_blk(), wold);
+                                                                this_blk(), wold, ddx);
 }
 // MODE 2 on a small grid (fewer than kTailCells owned cells, where a launch's fixed cost is
 // most of its time): the orphan edges' blocks at the tail of the cell grid, one launch
@@ -456,11 +465,11 @@ __global__ __launch_bounds__(256) void k_acoustic(DevState S, double dts, int sm
 constexpr int kTailCells = 16384;
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool TME, int SML>
 __global__ __launch_bounds__(256) void k_acoustic_o(DevState S, double dts, int small_step, double epssm, double resm,
-                                                   double coefp, int ncb, int wold) {
+                                                   double coefp, int ncb, int wold, int ddx) {
     const int b = (int)blockIdx.x;
     if (b < ncb)
         acoustic_body<LP, EXACT, SELF, FIRST, false, 2, TME, SML>(S, dts, small_step, epssm, resm, coefp, ncb,
-                                                                   Blk{b, ncb}, wold);
+                                                                   Blk{b, ncb}, wold, ddx);
     else acoustic_orph_body<LP, TME>(S, coefp, b - ncb);
 }
 // option "hfuse" (atm_srk3, stages 0 and 1): a stage's last acoustic launch (MODE 2, the
@@ -468,11 +477,11 @@ __global__ __launch_bounds__(256) void k_acoustic_o(DevState S, double dts, int 
 // cell kernel, which reads u only -- nothing the acoustic step reads or writes
 template <int LP, bool EXACT, bool SELF, int EPW>
 __global__ __launch_bounds__(256) void k_hf_ac_vc(DevState S, double dts, int small_step, double epssm, double resm,
-                                                 double coefp, int ncb, int nb1, int nVB, int wold) {
+                                                 double coefp, int ncb, int nb1, int nVB, int wold, int ddx) {
     const int b = (int)blockIdx.x;
     if (b < ncb)
         acoustic_body<LP, EXACT, SELF, false, false, 2, false, false>(S, dts, small_step, epssm, resm, coefp, ncb,
-                                                                       Blk{b, ncb}, wold);
+                                                                       Blk{b, ncb}, wold, ddx);
     else if (b < nb1) acoustic_orph_body<LP, false>(S, coefp, b - ncb);
     else solve_vc_body<LP, EPW, false>(S, nVB, 0, Blk{b - nb1, (int)gridDim.x - nb1});
 }
@@ -482,41 +491,7 @@ __global__ __launch_bounds__(256) void k_hf_ac_vc(DevState S, double dts, int sm
 // and acoustic_body SML = 1: the same terms, summed instead of subtracted from w one by one)
 template <int LP>
 __global__ __launch_bounds__(256) void k_sml_flux(DevState S) {
-    ColMap<LP> m(S, KC);
-    const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCO) return;
-    int e_[NF], c1_[NF], c2_[NF];
-    const int ne = cell_rec<false>(S, c, e_, c1_, c2_);
-    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
-    const double* sgnc = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
-    const double *ut_f = fd(S, F_u_tend), *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
-    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
-    double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgs_[NF];
-    row_ld(sgnc, sgs_);
-#pragma unroll
-    for (int i = 0; i < NF; i += 2) gather2s<LP>(ut_f, e_[i], e_[i + 1], k, ut_[i], ut_[i + 1]);
-#pragma unroll
-    for (int i = 0; i < NF; i++) {
-        ut_[i] = ldz(k <= L, ut_[i]);
-        gather2<LP>(zb, c * 10 + i, zb3, c * 10 + i, k, zb_[i], zb3_[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
-    double sum = 0.0;
-#pragma unroll
-    for (int i = 0; i < NF; i++) {
-        double flux = sgs_[i] * (fzm * ut_[i] + fzp * utm_[i]);
-        sum = add_if(i < ne, sum, (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux);
-    }
-    for (int i = NF; i < ne; i++) {
-        int iEdge = eoc[i];
-        double ut = col_rd<LP>(ut_f, iEdge, k, L);
-        double ut_m = lvl_dn<LP>(ut, k);
-        double flux = sgnc[i] * (fzm * ut + fzp * ut_m);
-        size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
-        sum += (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
-    }
-    colk(fw(S, X_smlS), c) = k <= L ? sum : 0.0;
+    sml_flux_body<LP>(S, this_blk());
 }
 template <int LP>
 static hipError_t sml_flux_lp(const DevState& S, hipStream_t st) {
@@ -525,7 +500,7 @@ static hipError_t sml_flux_lp(const DevState& S, hipStream_t st) {
         if (nb) k_sml_flux<LP><<<nb, 256, 0, st>>>(X);
     };
     HALO_RUN_R1(S, st, run, F_u_tend, F_u_tend);  // (u_tend at the edges of owned cells)
-    HALO_WROTE(S, X_smlS);
+    HALO_WROTE(S, X_smlS, X_Dd);
     return hipGetLastError();
 }
 hipError_t launch_sml_flux(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH(S.LP, sml_flux_lp, S, st); }
@@ -577,12 +552,13 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
 
 template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                              double coef_prev, int tme, int sml, int wold) {
+                              double coef_prev, int tme, int sml, int wold, int ddx) {
     if ((tme && (S.physics || S.halo)) || (sml && S.physics)) return hipErrorInvalidValue;  // (atm_srk3, reference semantics)
     if (sml && (small_step != 0 || mode == 0)) return hipErrorInvalidValue;
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
     if (mode && S.physics) return hipErrorInvalidValue;  // (srk3 never asks: reference semantics only)
+    if (ddx && S.physics) return hipErrorInvalidValue;   // (X_Dd: atm_srk3's reference semantics only)
     if (S.physics) {  // Q18: the edges first
         const double rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
         auto ru = [&](const DevState& X) {
@@ -605,7 +581,7 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
             auto go_t = [&](auto ex, auto sf) {
                 constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
 #define MPAS_ACO(FI, TM, SM) \
-    k_acoustic_o<LP, E, SF, FI, TM, SM><<<ncb + nob, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb, wold)
+    k_acoustic_o<LP, E, SF, FI, TM, SM><<<ncb + nob, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb, wold, ddx)
                 if (first) {
                     if constexpr (!E) {
                         if (sml == 2) {
@@ -633,7 +609,7 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
             constexpr bool E = decltype(ex)::value, SF = decltype(sf)::value;
             constexpr int M = decltype(md)::value;
 #define MPAS_AC(FI, MP, MM, TM, SM) \
-    k_acoustic<LP, E, SF, FI, MP, MM, TM, SM><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb, wold)
+    k_acoustic<LP, E, SF, FI, MP, MM, TM, SM><<<grid, 256, 0, st>>>(X, dts, small_step, epssm, resm, coef_prev, ncb, wold, ddx)
             if constexpr (M == 0) {
                 if (X.physics) {
                     if (first) MPAS_AC(true, true, 0, false, false);
@@ -692,12 +668,12 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                           double coef_prev, int tme, int sml, int wold) {
-    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml, wold);
+                           double coef_prev, int tme, int sml, int wold, int ddx) {
+    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml, wold, ddx);
 }
 template <int LP>
 static hipError_t hf_ac_vc_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
-                              double coef_prev, int wold) {
+                              double coef_prev, int wold, int ddx) {
     if (S.physics || S.halo || small_step == 0 || S.epw != 2) return hipErrorInvalidValue;
     const double epssm = kEpssm, resm = (1.0 - epssm) / (1.0 + epssm);
     const int ncb = col_blocks<LP>(S, KC);
@@ -706,17 +682,17 @@ static hipError_t hf_ac_vc_lp(const DevState& S, hipStream_t st, double dts, int
     if (!ncb || !nb2) return hipErrorInvalidValue;
     const int grid = nb1 + nb2;
     if (exact) {
-        if (S.selfc) k_hf_ac_vc<LP, true, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
-        else k_hf_ac_vc<LP, true, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
+        if (S.selfc) k_hf_ac_vc<LP, true, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold, ddx);
+        else k_hf_ac_vc<LP, true, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold, ddx);
     } else {
-        if (S.selfc) k_hf_ac_vc<LP, false, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
-        else k_hf_ac_vc<LP, false, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold);
+        if (S.selfc) k_hf_ac_vc<LP, false, true, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold, ddx);
+        else k_hf_ac_vc<LP, false, false, 2><<<grid, 256, 0, st>>>(S, dts, small_step, epssm, resm, coef_prev, ncb, nb1, nv, wold, ddx);
     }
     return hipGetLastError();
 }
 hipError_t launch_hf_acoustic_solve_vc(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
-                                       double coef_prev, int wold) {
-    MPAS_LP_DISPATCH(S.LP, hf_ac_vc_lp, S, st, dts, small_step, exact, coef_prev, wold);
+                                       double coef_prev, int wold, int ddx) {
+    MPAS_LP_DISPATCH(S.LP, hf_ac_vc_lp, S, st, dts, small_step, exact, coef_prev, wold, ddx);
 }
 
 }  // namespace mpas

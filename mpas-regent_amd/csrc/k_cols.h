@@ -423,6 +423,56 @@ __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
 }
 
 
+// ---------------------------------------------------------------- set_smlstep's flux sum
+// X_smlS (atm_srk3 fast path, reference semantics; once per step: k_sml_flux, or a body of
+// stage 0's combined hfuse launch): per cell and level k <= L the sum over the cell's edges of
+// set_smlstep's slope-flux terms, in the order every fast-path set_smlstep adds them; and X_Dd
+// = rw_save - rw for the stages' acoustic launches (the same difference they formed)
+// SETUP: beside the stage-0 setup launch that is writing rw_save = rw (every level but L): rw
+// stands in for rw_save (the same values where the acoustic step reads the difference)
+template <int LP, bool SETUP = false>
+__device__ __forceinline__ void sml_flux_body(const DevState& S, Blk bk) {
+    ColMap<LP> m(S, KC, bk);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    int e_[NF], c1_[NF], c2_[NF];
+    const int ne = cell_rec<false>(S, c, e_, c1_, c2_);
+    const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
+    const double* sgnc = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
+    const double *ut_f = fd(S, F_u_tend), *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
+    const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    double ut_[NF], utm_[NF], zb_[NF], zb3_[NF], sgs_[NF];
+    row_ld(sgnc, sgs_);
+#pragma unroll
+    for (int i = 0; i < NF; i += 2) gather2s<LP>(ut_f, e_[i], e_[i + 1], k, ut_[i], ut_[i + 1]);
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        ut_[i] = ldz(k <= L, ut_[i]);
+        gather2<LP>(zb, c * 10 + i, zb3, c * 10 + i, k, zb_[i], zb3_[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < NF; i++) {
+        double flux = sgs_[i] * (fzm * ut_[i] + fzp * utm_[i]);
+        sum = add_if(i < ne, sum, (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux);
+    }
+    for (int i = NF; i < ne; i++) {
+        int iEdge = eoc[i];
+        double ut = col_rd<LP>(ut_f, iEdge, k, L);
+        double ut_m = lvl_dn<LP>(ut, k);
+        double flux = sgnc[i] * (fzm * ut + fzp * ut_m);
+        size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
+        sum += (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+    }
+    colk(fw(S, X_smlS), c) = k <= L ? sum : 0.0;
+    double rws, rw;
+    if constexpr (SETUP) rws = rw = col_rd<LP>(fd(S, F_rw), c, k, L);
+    else col_rd2<LP>(fd(S, F_rw_save), fd(S, F_rw), c, k, L, rws, rw);
+    colk(fw(S, X_Dd), c) = k <= L ? rws - rw : 0.0;
+}
+
 // ---------------------------------------------------------------- setup + moist + vert_imp
 // Stage 0 of atm_srk3 in one launch (option "fusesetup", reference semantics; k_setup_vi,
 // k_misc.hip, and its combined launch with dyn_tend A, k_dyn.hip): blocks [0, ncb) one cell

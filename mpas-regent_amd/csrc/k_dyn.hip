@@ -1330,26 +1330,36 @@ hipError_t launch_hf_solve_e_dyn_A(const DevState& S, hipStream_t st, const DynT
 // option "hfuse" (atm_srk3 stage 0, with fusesetup): dyn_tend A beside the setup + moist +
 // vert_imp launch (k_setup_vi's body, k_misc.hip); A reads nothing that launch writes but
 // rho_p_save and qtot, whose values it takes at their source (SETUP above)
-template <int LP, bool RK0>
+// (+ option smlsum: set_smlstep's flux sum of the step, X_smlS, in the last ncb blocks -- it
+// reads u_tend / zb_cell / zb3_cell and writes a scratch column neither other body touches)
+template <int LP, bool RK0, bool FLUX>
 __global__ __launch_bounds__(256) void k_hf_setup_A(DevState S, DynK a, int ncb, int nb1, double dtseps, double rcv,
                                                    double c2) {
     const int b = (int)blockIdx.x;
+    const int nA = FLUX ? ((int)gridDim.x - nb1) / 2 : (int)gridDim.x - nb1;
     if (b < nb1) setup_vi_body<LP>(S, ncb, dtseps, rcv, c2, Blk{b, nb1});
-    else dyn_A_body<LP, RK0, false, true>(S, a, Blk{b - nb1, (int)gridDim.x - nb1});
+    else if (!FLUX || b < nb1 + nA) dyn_A_body<LP, RK0, false, true>(S, a, Blk{b - nb1, nA});
+    else sml_flux_body<LP, true>(S, Blk{b - nb1 - nA, nA});
 }
 template <int LP>
-static hipError_t hf_setup_A_lp(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges) {
+static hipError_t hf_setup_A_lp(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges,
+                                int flux) {
     if (S.halo || S.physics) return hipErrorInvalidValue;
     const DynK a = make_dynk(S, stage0);
     const double dtseps = .5 * dts * (1.0 + kEpssm), rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
     const int ncb = col_blocks<LP>(S, KC), nb1 = ncb + (edges ? col_blocks<LP>(S, KE) : 0);
     if (!ncb) return hipErrorInvalidValue;
-    if (a.rk_step == 0) k_hf_setup_A<LP, true><<<nb1 + ncb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
-    else k_hf_setup_A<LP, false><<<nb1 + ncb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
+    const int nb = nb1 + ncb * (flux ? 2 : 1);
+    if (a.rk_step == 0 && flux) k_hf_setup_A<LP, true, true><<<nb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
+    else if (a.rk_step == 0) k_hf_setup_A<LP, true, false><<<nb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
+    else if (flux) k_hf_setup_A<LP, false, true><<<nb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
+    else k_hf_setup_A<LP, false, false><<<nb, 256, 0, st>>>(S, a, ncb, nb1, dtseps, rcv, c2);
+    if (flux) HALO_WROTE(S, X_smlS, X_Dd);
     return hipGetLastError();
 }
-hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges) {
-    MPAS_LP_DISPATCH(S.LP, hf_setup_A_lp, S, st, stage0, dts, edges);
+hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges,
+                                 int flux) {
+    MPAS_LP_DISPATCH(S.LP, hf_setup_A_lp, S, st, stage0, dts, edges, flux);
 }
 
 }  // namespace mpas

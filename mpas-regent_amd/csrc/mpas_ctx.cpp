@@ -57,6 +57,7 @@ const FieldInfo kFields[X_COUNT] = {
     {"orph", K_E2I, 1, D_M, 0, 0},
     {"tme", K_E3, 1, D_M, 0, 0},
     {"smlS", K_C3, 1, D_M, 0, 0},
+    {"Dd", K_C3, 1, D_M, 0, 0},
     {"Ah", K_E3, 8, D_M, 0, 0},
     {"Rp", K_C3V, 8, D_M, 0, 0},
     {"Rm", K_C3V, 8, D_M, 0, 0},
@@ -879,11 +880,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         }
         return a;
     };
+    bool flux_done = false;  // (option smlsum: the step's flux sum, beside setup and A on small grids)
     if (c->fusesetup && S.physics == 0 && hf2) {  // + stage 0's dyn_tend A in the same launch
-        run_task(c, "hfuse[setup+dyn_A]", [&] {
-            return launch_hf_setup_dyn_A(S, st, stage_args(0), rk_sub_timestep[0], fcopy ? 0 : 1);
+        run_task(c, smls ? "hfuse[setup+dyn_A+sml_flux]" : "hfuse[setup+dyn_A]", [&] {
+            return launch_hf_setup_dyn_A(S, st, stage_args(0), rk_sub_timestep[0], fcopy ? 0 : 1, smls ? 1 : 0);
         });
         a_done = true;
+        flux_done = smls;
     } else if (c->fusesetup) {  // :404-417 as one column-local launch (same values; MPAS forms under physics)
         run_task(c, fcopy ? "atm_rk_integration_setup[cells+moist+vert_imp]" : "atm_rk_integration_setup[+moist+vert_imp]",
                  [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0], !fcopy); });
@@ -892,7 +895,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });
         run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[0]); });
     }
-    if (smls) run_task(c, "atm_set_smlstep_pert_variables_work[flux]", [&] { return launch_sml_flux(S, st); });
+    if (smls && !flux_done)
+        run_task(c, "atm_set_smlstep_pert_variables_work[flux]", [&] { return launch_sml_flux(S, st); });
     for (int rk_step = 0; rk_step < 3; rk_step++) {  // :426-477
         if (rk_step == 1 && !vi_done)
             run_task(c, "atm_compute_vert_imp_coefs", [&] { return launch_vert_imp_coefs(S, st, rk_sub_timestep[rk_step]); });
@@ -923,12 +927,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                 const int wold = (done_acoustic + 1 == n_acoustic) ? 1 : 0;
                 if (hf2 && rk_step < 2 && mode == 2 && small_step > 0 && small_step == n_small - 1) {
                     run_task(c, "hfuse[acoustic+solve_vc]", [&] {
-                        return launch_hf_acoustic_solve_vc(S, st, dts, small_step, c->exact, coef_prev, wold);
+                        return launch_hf_acoustic_solve_vc(S, st, dts, small_step, c->exact, coef_prev, wold, smls ? 1 : 0);
                     });
                     vc_done = true;
                 } else {
                     run_task(c, acoustic_name(small_step, pending, sm, !wold),
-                             [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev, tme, sm, wold); });
+                             [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev, tme, sm, wold,
+                                                          smls ? 1 : 0); });
                 }
                 if (mode == 2) fb.swap_rup();
                 fb.swap_dv();  // this substep's div is read next from X_dvB

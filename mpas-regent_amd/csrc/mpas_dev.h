@@ -95,6 +95,9 @@ enum FieldId {
     X_smlS,     // set_smlstep's slope flux sum of u_tend per cell and level, formed once per step
                 // (atm_srk3 fast path, reference semantics: u_tend, zb_cell, zb3_cell are not
                 // written by any task of the step) for the stages' fused set_smlstep      C3
+    X_Dd,       // rw_save - rw per cell and level, formed with X_smlS once per step (neither is
+                // written within a step in the reference semantics): the acoustic step's only use
+                // of the two columns                                                      C3
     // monotonic scalar transport (k_transport.hip), one column per (entity, scalar)
     X_Ah,       // antidiffusive edge flux                                      E3 x 8
     X_Rp,       // R+ (fraction of the incoming antidiffusive flux allowed)     C3V x 8
@@ -225,10 +228,12 @@ hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double
 // (mode 2) beside its solve_diagnostics vertex / cell kernel; the stage's solve_diagnostics
 // edge kernel beside the next stage's dyn_tend A (and stage 1's vert_imp after stage 0)
 hipError_t launch_hf_acoustic_solve_vc(const DevState& S, hipStream_t st, double dts, int small_step, int exact,
-                                       double coef_prev, int wold = 1);
+                                       double coef_prev, int wold = 1, int ddx = 0);
 hipError_t launch_hf_solve_e_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& next, int vi, double dts_vi);
 // ... and stage 0's setup + moist + vert_imp launch (fusesetup) beside stage 0's dyn_tend A
-hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges);
+// flux: also set_smlstep's flux sum of the step (X_smlS; option smlsum)
+hipError_t launch_hf_setup_dyn_A(const DevState& S, hipStream_t st, const DynTendArgs& stage0, double dts, int edges,
+                                 int flux = 0);
 hipError_t launch_dyn_tend(const DevState& S, hipStream_t st, const DynTendArgs& a);
 // exact = 0 (reference semantics): the slope-flux terms summed, then subtracted (k_sml_flux's order)
 hipError_t launch_set_smlstep(const DevState& S, hipStream_t st, int exact);
@@ -241,8 +246,9 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st, int exact);
 // 1 from its slope fluxes, 2 (exact = 0) from X_smlS, the step's launch_sml_flux
 // wold 0 (mode 1 / 2 only): rtheta_pp_old not stored -- atm_srk3's fused damping reads the div
 // this launch stores instead, so only the step's last substep leaves rtheta_pp_old
+// ddx: rw_save - rw from X_Dd (atm_srk3 with option smlsum: launch_sml_flux formed it this step)
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode = 0,
-                           double coef_prev = 0.0, int tme = 0, int sml = 0, int wold = 1);
+                           double coef_prev = 0.0, int tme = 0, int sml = 0, int wold = 1, int ddx = 0);
 // X_smlS = the sum of set_smlstep's slope-flux terms per cell and level (atm_srk3 fast path,
 // once per step: u_tend / zb_cell / zb3_cell are not written within a step)
 hipError_t launch_sml_flux(const DevState& S, hipStream_t st);

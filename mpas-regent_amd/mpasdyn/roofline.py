@@ -15,7 +15,8 @@ roofline.achieved divides by the measured launch time.
 
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
-          part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False):
+          part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
+          ddx=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -26,12 +27,16 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                  "solve_e-v+finish": (("atm_compute_solve_diagnostics", {"part": "e"}),
                                       ("atm_rk_dynamics_substep_finish", {})),
                  "solve_e+vert_imp": (e, vi),
-                 "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}),
+                 "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False,
+                                                                           "ddx": ddx}),
                                        ("atm_compute_solve_diagnostics", {"part": "vc"})),
                  "solve_e+dyn_A": (e, dA),
                  "solve_e+vert_imp+dyn_A": (e, vi, dA),
                  "setup+dyn_A": (("atm_rk_integration_setup", {"fused": True, "copy": True}),
-                                 ("atm_compute_dyn_tend_work", {"rk_step": 0, "part": "A"}))}[pair]
+                                 ("atm_compute_dyn_tend_work", {"rk_step": 0, "part": "A"})),
+                 "setup+dyn_A+sml_flux": (("atm_rk_integration_setup", {"fused": True, "copy": True}),
+                                          ("atm_compute_dyn_tend_work", {"rk_step": 0, "part": "A"}),
+                                          ("atm_set_smlstep_pert_variables_work", {"part": "flux"}))}[pair]
         rs, ws = [], []
         for t, kw in parts:
             r, w = _sets(t, **kw)
@@ -101,7 +106,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         return reads + mesh, writes
     if task == "atm_set_smlstep_pert_variables_work" and part == "flux":
         # option smlsum (atm_srk3 fast path): the slope-flux sum, once per step (X_smlS, scratch)
-        return ["zb_cell", "zb3_cell", "u_tend", "nEdgesOnCell", "edgesOnCell", "edgesOnCell_sign"], []
+        # (+ X_Dd = rw_save - rw for the stages' acoustic launches: rw_save and rw read here once)
+        return ["zb_cell", "zb3_cell", "u_tend", "nEdgesOnCell", "edgesOnCell", "edgesOnCell_sign", "rw_save", "rw"], []
     if task == "atm_set_smlstep_pert_variables_work":
         if md:
             return (["zz", "tend_w", "zb_cell", "zb3_cell", "tend_u", "bdyMaskCell", "nEdgesOnCell", "edgesOnCell",
@@ -114,6 +120,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                  "invAreaCell", "cellsOnEdge", "dvEdge", "specZoneMaskCell"]
         if small_step != 0:
             reads += ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+        if ddx and not physics:  # (atm_srk3 with smlsum: rw_save - rw from the step's X_Dd, scratch)
+            reads = [r for r in reads if r not in ("rw", "rw_save")]
         # (wold False: a fused launch of option fusedamp other than the step's last, which leaves
         # rtheta_pp_old unwritten -- the fused damping reads the stored div instead)
         writes = (["rtheta_pp_old"] if wold else []) + ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
@@ -261,12 +269,13 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     # (fusedamp: only the step's last acoustic launch stores rtheta_pp_old, wold)
     if fusedamp and fusesml:
         sm = {"sml": True, "smls": bool(smlsum)}
+        dd = {"ddx": bool(smlsum)}  # (smlsum: rw_save - rw from the step's X_Dd too)
         if smlsum:  # option smlsum: the slope-flux sum once per step
             out += [("atm_set_smlstep_pert_variables_work", {"part": "flux"}, 1)]
-        out += [("atm_advance_acoustic_step_work", {"small_step": 0, **sm, "wold": False}, 1),
-                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, **sm, "wold": False}, 2),
-                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}, 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 1),
+        out += [("atm_advance_acoustic_step_work", {"small_step": 0, **sm, "wold": False, **dd}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, **sm, "wold": False, **dd}, 2),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False, **dd}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, **dd}, 1),
                 ("atm_divergence_damping_3d", {}, 1)]
     elif fusedamp:
         out += [("atm_set_smlstep_pert_variables_work", {}, 3),

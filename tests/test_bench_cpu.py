@@ -239,13 +239,16 @@ def test_roofline_smlsum_accounting():
     d_ac = roofline.b_alg("atm_advance_acoustic_step_work", dims, **kw) - \
         roofline.b_alg("atm_advance_acoustic_step_work", dims, smls=True, **kw)
     flux = roofline.b_alg("atm_set_smlstep_pert_variables_work", dims, part="flux")
-    assert flux - d_ac == fb("nEdgesOnCell") + fb("edgesOnCell")  # (the acoustic launch reads them anyway)
+    dd = fb("rw") + fb("rw_save")  # (X_Dd = rw_save - rw, formed by the flux task, read by all 7 launches)
+    assert flux - d_ac == fb("nEdgesOnCell") + fb("edgesOnCell") + dd  # (the acoustic launch reads the lists anyway)
     assert d_ac > fb("u_tend") + fb("edgesOnCell_sign")  # (+ the zb_cell / zb3_cell components)
-    assert a - b == 3 * d_ac - flux
+    assert a - b == 3 * d_ac - flux + 7 * dd
     rep = {"atm_set_smlstep_pert_variables_work[flux]": (1, 0.2),
            "atm_advance_acoustic_step_work[ss0+smlS+damp-old]": (2, 1.2)}
-    t = bench.task_table(rep, dims, 1, physics=False)
-    assert abs(t["atm_set_smlstep_pert_variables_work"]["b_alg_GB_per_step"]
-               - roofline.b_alg("atm_set_smlstep_pert_variables_work", dims, part="flux") / 1e9) < 1e-3
-    ac = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=0, damp=True, sml=True, smls=True, wold=False)
+    t = bench.task_table(rep, dims, 1, physics=False, ddx=True)
+    assert abs(t["atm_set_smlstep_pert_variables_work"]["b_alg_GB_per_step"] - flux / 1e9) < 1e-3
+    ac = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=0, damp=True, sml=True, smls=True,
+                        wold=False, ddx=True)
+    assert ac == roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=0, damp=True, sml=True, smls=True,
+                                wold=False) - dd
     assert abs(t["atm_advance_acoustic_step_work"]["b_alg_GB_per_step"] - 2 * ac / 1e9) < 1e-3
