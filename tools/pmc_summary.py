@@ -28,16 +28,19 @@ from collections import defaultdict
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "mpas-regent_amd"))
 from mpasdyn.pmc import read_trace, short, task_of  # noqa: E402,F401  (kernel -> task map shared with bench.py)
 
-# task launches per RK3 step (schedule 1, x1.163842: 7 acoustic substeps)
-LAUNCHES = {"atm_rk_integration_setup": 1, "atm_compute_moist_coefficients": 1, "atm_compute_vert_imp_coefs": 2,
+# task launches per RK3 step (schedule 1, x1.163842, the default fusions: setup + moist + stage
+# 0's vert_imp in one launch, six dampings and the three set_smlstep inside acoustic launches,
+# set_smlstep's flux sum once per step -- 7 acoustic substeps)
+LAUNCHES = {"atm_rk_integration_setup": 1, "atm_compute_moist_coefficients": 1, "atm_compute_vert_imp_coefs": 1,
             "atm_compute_dyn_tend_work[rk0]": 1, "atm_compute_dyn_tend_work[rk>0]": 2,
-            "atm_set_smlstep_pert_variables_work": 3, "atm_advance_acoustic_step_work": 7,
-            "atm_divergence_damping_3d": 7, "atm_compute_solve_diagnostics": 3,
+            "atm_set_smlstep_pert_variables_work": 1, "atm_advance_acoustic_step_work": 7,
+            "atm_divergence_damping_3d": 1, "atm_compute_solve_diagnostics": 3,
             "atm_rk_dynamics_substep_finish": 1}
-# bench.py --physics / --transport (the MPAS vertical solver: 4 acoustic substeps, recover
-# after every stage, the scalar transport once per step)
+# bench.py --physics / --transport (the MPAS vertical solver: 4 acoustic substeps and dampings,
+# set_smlstep per stage, recover after every stage, the scalar transport once per step)
 LAUNCHES_PHYSICS = dict(LAUNCHES, atm_advance_acoustic_step_work=4, atm_divergence_damping_3d=4,
-                        atm_recover_large_step_variables_work=3, atm_advance_scalars_mono=1)
+                        atm_set_smlstep_pert_variables_work=3, atm_recover_large_step_variables_work=3,
+                        atm_advance_scalars_mono=1)
 
 
 def read_counter(d, counter):
@@ -45,6 +48,15 @@ def read_counter(d, counter):
     from mpasdyn.pmc import read_counter as rc
     r = rc(d, counter)
     return {k: v[0] for k, v in r.items()}, {k: v[1] for k, v in r.items()}
+
+
+def once_per_step(d):
+    """the step count of a run: the calls of a kernel that runs once per RK3 step (the separate
+    setup copies of rounds 1-2, the fused setup launch since, or the substep finish)"""
+    for k, v in d.items():
+        if k in ("k_setup_cells", "k_copy64", "k_finish64") or k.startswith(("k_setup_vi<", "k_hf_setup_A<")):
+            return v[0] if isinstance(v, tuple) else v
+    return None
 
 
 def main():
@@ -65,7 +77,7 @@ def main():
     steps = None
     if a.trace:
         tr = read_trace(a.trace)
-        steps = tr.get("k_setup_cells", tr.get("k_copy64", (None,)))[0]
+        steps = once_per_step(tr)
         for k, (calls, t) in tr.items():
             out["kernels"][k] = {"calls": calls, "avg_us": round(t / calls * 1e6, 2)}
             task = task_of(k)
@@ -74,7 +86,7 @@ def main():
                 tasks[task]["time_s"] += t
     fetch, nf = read_counter(a.fetch, "FETCH_SIZE") if a.fetch else ({}, {})
     write, nw = read_counter(a.write, "WRITE_SIZE") if a.write else ({}, {})
-    pmc_steps = nf.get("k_setup_cells") or nw.get("k_setup_cells") or nf.get("k_copy64") or nw.get("k_copy64")
+    pmc_steps = once_per_step(nf) or once_per_step(nw)
     # calibration on the copies: setup_cells reads 6 cell fields and writes 7 (rho_zz
     # twice), setup_edges reads and writes 2 edge fields
     lines = {"k_setup_cells": 6 * nC * 4 * 128, "k_setup_edges": 2 * nE * 4 * 128, "k_copy64": (6 * nC + 2 * nE) * 4 * 128}
