@@ -146,7 +146,6 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
 #pragma unroll
         for (int i = 0; i < NF; i += 2)
             cell_pair2<LP, SELF>(dvi, c1_, c2_, o_, s1_, dv_c, i, k, d1_[i], d2_[i], d1_[i + 1], d2_[i + 1]);
-        double* rup_out = fw(S, X_rupB);
         // the isShared flags of every slot's two cells loaded up front and combined without
         // short-circuit evaluation: `kl && ... && !(sh[x1] && sh[x2])` put each slot's loads
         // under a lane-divergent branch with a full wait inside (six round trips per wave)
@@ -165,27 +164,19 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         for (int i = 0; i < NF; i++) {
             const bool on = kl & (e_[i] < S.nEdges) & !(sh1_[i] & sh2_[i]);
             rup_[i] = damp_edge<LP>(rup_[i], d1_[i], d2_[i], ts_[i], spz_[i], coefp, on);
-            if ((own >> i) & 1) colk(rup_out, e_[i]) = PADW(rup_[i]);  // (level L: the value read)
         }
     }
-#pragma unroll
-    for (int i = 0; i < NF; i++) {
-        rup_[i] = ldz(kl, rup_[i]);
-        ts_[i] = ldz(kl, ts_[i]);
-    }
+    // (rup_ / ts_ at k >= L: unused, the flux sum below selects on kl)
     col_rd2<LP>(fd(S, F_w), fd(S, F_coftz), c, k, L, w, coftz);
     col_rd2<LP>(fd(S, F_zz), fd(S, F_rho_zz), c, k, L, zz, rz);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
+    int wst = 0;  // SML: set_smlstep's w store (1: the new w, 2: the padding's 0.0), made below
     if constexpr (SML == 2) {  // (X_smlS: k_sml_flux's sum of the slope fluxes)
         double wn = w - colk(fd(S, X_smlS), c);
         wn *= (fzm * zz + fzp * lvl_dn<LP>(zz, k));
-        if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
-            colk(fw(S, F_w), c) = wn;
-            if (k == L) keep_put<LP>(S, F_w, KC, c, wn);  // (w's level L changes: its keep tail too)
-            w = wn;
-        } else if ((k > L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone)) {
-            colk(fw(S, F_w), c) = 0.0;  // (the padding's content: the column's last line written whole)
-        }
+        const bool rz_ok = fi(S, F_bdyMaskCell)[c] <= kRelaxZone;
+        wst = ((k <= L) & rz_ok & (cpr != 0)) ? 1 : ((k > L) & rz_ok) ? 2 : 0;
+        if (wst == 1) w = wn;
     } else if constexpr (SML == 1) {
         // the stage's atm_set_smlstep_pert_variables_work (:1503-1528, k_set_smlstep's
         // expressions) on this column, just before the substep reads w: the points of cpr
@@ -227,13 +218,9 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         }
         if constexpr (!EXACT) wn = w - sum;
         wn *= (fzm * zz + fzp * lvl_dn<LP>(zz, k));
-        if ((k <= L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone) & (cpr != 0)) {
-            colk(fw(S, F_w), c) = wn;
-            if (k == L) keep_put<LP>(S, F_w, KC, c, wn);  // (w's level L changes: its keep tail too)
-            w = wn;
-        } else if ((k > L) & (fi(S, F_bdyMaskCell)[c] <= kRelaxZone)) {
-            colk(fw(S, F_w), c) = 0.0;  // (the padding's content: the column's last line written whole)
-        }
+        const bool rz_ok = fi(S, F_bdyMaskCell)[c] <= kRelaxZone;
+        wst = ((k <= L) & rz_ok & (cpr != 0)) ? 1 : ((k > L) & rz_ok) ? 2 : 0;
+        if (wst == 1) w = wn;
     }
     // the w tendency: the state w in the reference and under physics = 1 (Q8), tend_w under
     // the MPAS dynamics (physics = 2); the implicit Rayleigh term reads the state w
@@ -255,6 +242,24 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
     if constexpr (MPASV) col_rd2<LP>(fd(S, F_gamma_tri), fd(S, F_tend_theta), c, k, L, gam, tend_th);
     const double tt = MPASV ? tend_th : tm;  // tend_rt: the reference reads theta_m (Q8)
     const double cofrz = fd(S, F_cofrz)[k], rdzw = fd(S, F_rdzw)[k];
+    // ---- the stores of the values formed above (the previous substep's damped ru_p on the
+    // edges this cell owns, set_smlstep's w), after the column's last load: made where they
+    // were formed, they let no later load move above them (the compiler cannot tell they do not
+    // alias), and the second batch of column loads waited for the first batch's consumers
+    if constexpr (MODE == 2) {
+        double* rup_out = fw(S, X_rupB);
+#pragma unroll
+        for (int i = 0; i < NF; i++)
+            if ((own >> i) & 1) colk(rup_out, e_[i]) = PADW(rup_[i]);  // (level L: the value read)
+    }
+    if constexpr (SML != 0) {
+        if (wst == 1) {
+            colk(fw(S, F_w), c) = w;
+            if (k == L) keep_put<LP>(S, F_w, KC, c, w);  // (w's level L changes: its keep tail too)
+        } else if (wst == 2) {
+            colk(fw(S, F_w), c) = 0.0;  // (the padding's content: the column's last line written whole)
+        }
+    }
 
     // :1615-1636
     const double rtpo = (small_step == 0) ? 0 : rtp;
