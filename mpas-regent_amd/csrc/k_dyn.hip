@@ -450,7 +450,8 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         if (k != L) colk(fw(S, F_v), e) = PADW(vv);
     }
     {  // curvature (:1011-1017, Q12 literal)
-        const double cosA = fd(S, X_cosAngleEdge)[e], cosL = fd(S, X_cosLatEdge)[e];
+        // (ldc: mesh tables no step kernel writes -- not held behind the v store above)
+        const double cosA = ldc(fd(S, X_cosAngleEdge) + e), cosL = ldc(fd(S, X_cosLatEdge) + e);
         const double cA = (2.0 * kOmega * cosA * cosL * rho_edge * 0.25 * (w1 + w1p + w2 + w2p));
         const double cB = (u * 0.25 * (w1 + w1p + w2 + w2p) * rho_edge * a.inv_r_earth);
         if (MD) tend_u = tend_u - cA - cB;
