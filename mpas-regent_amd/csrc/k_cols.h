@@ -205,12 +205,16 @@ __device__ __forceinline__ void divdamp_body(const DevState& S, double coef_divd
 
 // ---------------------------------------------------------------- substep finish
 // cells: the cell part (else the edges); blocks b of nb cover its pairs (grid stride)
-__device__ __forceinline__ void finish64_body(const DevState& S, int substep, int split, double inv_split, Pair64 q,
-                                              bool cells, int b, int nb) {
+// (CELLS a template argument: every keep tail is addressed with a constant entity kind -- a runtime
+// kind select in keep_tail was miscompiled once, mpas_dev.h k_keep_refresh)
+template <bool CELLS>
+__device__ __forceinline__ void finish64_part(const DevState& S, int substep, int split, double inv_split, Pair64 q,
+                                              int b, int nb) {
+    constexpr bool cells = CELLS;
+    constexpr int kind = CELLS ? KC : KE;
     const size_t n = (size_t)(cells ? S.nCO : S.nEO) * 32;
     double *avg = fw(S, cells ? F_wwAvg : F_ruAvg), *avgS = fw(S, cells ? F_wwAvg_split : F_ruAvg_split);
     const bool restore = substep < split, last = substep == split, same = substep == 1 && inv_split == 1.0;
-    const int kind = cells ? KC : KE;
     for (size_t i = (size_t)b * 256 + threadIdx.x; i < n; i += (size_t)nb * 256) {
         // (level L: the kept value of the destination -- its keep tail, or for the averages the
         // value just loaded -- so every line of a column is written whole)
@@ -241,6 +245,11 @@ __device__ __forceinline__ void finish64_body(const DevState& S, int substep, in
         if (last && !same) st64k(avg, i, make_double2(sv.x * inv_split, sv.y * inv_split), q, q.el ? a.y : a.x);
         if (cells && last && S.physics != 2) cp(F_rho_zz_old_split, F_rho_zz);
     }
+}
+__device__ __forceinline__ void finish64_body(const DevState& S, int substep, int split, double inv_split, Pair64 q,
+                                              bool cells, int b, int nb) {
+    if (cells) finish64_part<true>(S, substep, split, inv_split, q, b, nb);
+    else finish64_part<false>(S, substep, split, inv_split, q, b, nb);
 }
 
 
@@ -470,7 +479,9 @@ __device__ __forceinline__ void sml_flux_body(const DevState& S, Blk bk) {
     double rws, rw;
     if constexpr (SETUP) rws = rw = col_rd<LP>(fd(S, F_rw), c, k, L);
     else col_rd2<LP>(fd(S, F_rw_save), fd(S, F_rw), c, k, L, rws, rw);
-    colk(fw(S, X_Dd), c) = k <= L ? rws - rw : 0.0;
+    // (level L: 0.0 in both forms -- the SETUP form's rw stands in for rw_save, which differs there;
+    // the acoustic step reads the interfaces 1..L-1 only: ADVICE r05)
+    colk(fw(S, X_Dd), c) = k < L ? rws - rw : 0.0;
 }
 
 // ---------------------------------------------------------------- setup + moist + vert_imp

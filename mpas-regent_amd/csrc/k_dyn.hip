@@ -222,10 +222,10 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // it spill ~78 VGPRs.  The MPAS dynamics' B (139-147 VGPRs) under the same cap spills 8-32
 // and runs 7-80 % slower: profiles/r04/md_cap_tried)
 // NOF (option "bsplit", fast path): the per-edge theta flux H (and the MD w flux) are left to
-// k_dyn_Bf, an edge kernel of their own: this one skips the advCells gathers
+// k_dyn_Bf, an edge kernel of their own: this one skips the advCells gathers.  Also (option
+// "etile", either path) when the tiled E forms each edge's flux itself: no X_F at all
 template <int LP, bool RK0, bool MD, bool HF, bool DIN = false, bool NOF = false>
 __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) {
-    static_assert(!NOF || HF, "the split is the fast path's");
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         tend_u -= rho_edge * u * (((double)k - (double)(L - kRayleighLevels)) * a.rayleigh_inv);
     if (a.tme) {  // X_tme for the stage's acoustic substeps: theta_m(cell2) + theta_m(cell1)
         double t2pt1;
-        if (na >= 2 && ad_[0] == cell1 && ad_[1] == cell2) {  // (the adv list starts with the two cells)
+        if (!NOF && na >= 2 && ad_[0] == cell1 && ad_[1] == cell2) {  // (the adv list starts with the two cells)
             t2pt1 = tv_[1] + tv_[0];
         } else {
             double t1, t2;
@@ -818,11 +818,19 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
     dyn_D_body<LP>(S, a, this_blk());
 }
 
-template <int LP, bool RK0, bool SELF, bool MD, bool HF>
-__device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk bk) {
-    ColMap<LP> m(S, KC, bk);
-    const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCO) return;
+// TILE (option "etile", k_dyn_Et below): the cell is one of a tile whose theta_m closure sits
+// in LDS (tl.lds, level order, one LP-double column per closure cell; tl.row the cell's
+// TrTiles slot row): the flux of each edge over its advCells (B's flux_arr, and under HF B's H)
+// is formed here from LDS with B's expressions in B's order, instead of gathered from X_F
+struct EtTile {
+    const double* lds;    // the closure's theta_m columns, then the zero column
+    const double* ldsw;   // per tile edge, per advCell j: B's weights ac + ac3, ac - ac3 (0, 0 past nAdv)
+    const unsigned* rec;  // the cell's ETT_REC-byte record (TrTiles::erow)
+};
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false>
+__device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int c, int k, EtTile tl = {}) {
+    static_assert(!TILE || (LP == 64 && !MD), "the tiled E: LP = 64, reference semantics");
+    const int L = S.L;
     const size_t p = (size_t)c * LP + lpos(LP, k);
     constexpr bool rk0 = RK0;
     const bool kl = k < L;
@@ -852,6 +860,24 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
     if (rk0) {
         row_ld(cidc, cidc_);
         row_ld(cmsd4, cmsd4_);
+    }
+    // TILE: E's theta advection sum over the cell's edges (:1328-1360), into tth -- each edge's flux
+    // over its advCells from the tile's LDS columns with B's expressions in B's order (B's flux_arr;
+    // under HF B's H), then summed in E's order.  Its gathers first, then the cell's own columns
+    // below, then the sum (before the w section): one memory round trip for both
+    // (lanes k >= L: unmasked values, their sums are never used -- tend_theta takes tth where k < L)
+    double tth = 0.0;
+    double tru[NF], trus[NF], tt1[NF], tt2[NF];
+    if constexpr (TILE) {
+        const double ts_own = SELF ? colk(tms_f, c) : 0.0;
+#pragma unroll
+        for (int i = 0; i < NF; i += 2) {
+            gather2s<LP>(ru, e_[i], e_[i + 1], k, tru[i], tru[i + 1]);
+            if (!rk0) {
+                gather2s<LP>(rus, e_[i], e_[i + 1], k, trus[i], trus[i + 1]);
+                cell_pair2<LP, SELF>(tms_f, c1_, c2_, o_, s1_, ts_own, i, k, tt1[i], tt2[i], tt1[i + 1], tt2[i + 1]);
+            }
+        }
     }
     // own columns (gather2: two columns per load instruction; the theta-section loads
     // too, ahead of the w stores that could alias them for the compiler)
@@ -891,18 +917,20 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
     const double ts_c = tms;  // (SELF, rk > 0: theta_m_save at the cell itself)
     // HF: F holds B's per-edge flux H (ru F + the rk > 0 perturbation flux): ru, ru_save
     // and the theta_m_save pairs are not gathered here
+    // (TILE: the theta advection sum tth was formed above; no ru, ru_save, theta_m_save or X_F here)
+    constexpr bool GRU = !HF && !TILE;
 #pragma unroll
     for (int i = 0; i < NF; i += 2) {
-        if (!HF) gather2s<LP>(ru, e_[i], e_[i + 1], k, ru_[i], ru_[i + 1]);
-        gather2s<LP>(Ff, e_[i], e_[i + 1], k, F_[i], F_[i + 1]);
+        if (GRU) gather2s<LP>(ru, e_[i], e_[i + 1], k, ru_[i], ru_[i + 1]);
+        if (!TILE) gather2s<LP>(Ff, e_[i], e_[i + 1], k, F_[i], F_[i + 1]);
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
-        ru_[i] = HF ? 0.0 : ldz(kl, ru_[i]);
-        F_[i] = ldz(kl, F_[i]);
+        ru_[i] = GRU ? ldz(kl, ru_[i]) : 0.0;
+        F_[i] = TILE ? 0.0 : ldz(kl, F_[i]);
         rus_[i] = ts1_[i] = ts2_[i] = dw1_[i] = dw2_[i] = dt1_[i] = dt2_[i] = 0.0;
     }
-    if (!rk0 && !HF) {
+    if (!rk0 && GRU) {
 #pragma unroll
         for (int i = 0; i < NF; i += 2) {
             gather2s<LP>(rus, e_[i], e_[i + 1], k, rus_[i], rus_[i + 1]);
@@ -923,6 +951,43 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
             dw2_[i] = ldz(kl && del4, dw2_[i]);
             dt1_[i] = ldz(kl && del4, dt1_[i]);
             dt2_[i] = ldz(kl && del4, dt2_[i]);
+        }
+    }
+    if constexpr (TILE) {
+        // per edge: B's scalar weights (ac + sign ac3: the tile's LDS pair, picked per lane by the sign
+        // of ru) times the advCells' columns from LDS, in B's order; the slots past nAdvCellsForEdge
+        // add 0 * 0 (the zero column), which leaves the sum as B's masked add does (it is never -0)
+        unsigned rw_[ETT_REC / 4];
+        row_ld(tl.rec, rw_);
+        auto byte_at = [&](int b) { return (int)((rw_[b >> 2] >> ((b & 3) * 8)) & 0xffu); };
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const bool pos = copysign(1.0, tru[i]) > 0.0;
+            const double* wr = tl.ldsw + byte_at(i * ETT_EB) * (2 * AF) + (pos ? 0 : 1);
+            double flux_arr = 0.0;
+#pragma unroll
+            for (int j = 0; j < AF; j++) flux_arr = flux_arr + wr[2 * j] * tl.lds[byte_at(i * ETT_EB + 1 + j) * LP + k];
+            if constexpr (HF) {  // B's H: ru F (+ dvEdge (ru_save - ru) theta_m_save at the edge, rk > 0)
+                double h = tru[i] * flux_arr;
+                if constexpr (!RK0) {
+                    const double rus_e = a.cp ? tru[i] : trus[i];
+                    h += cdv_[i] * ((rus_e - tru[i]) * 0.5 * (tt2[i] + tt1[i]));
+                }
+                tth = sub_if(i < ne, tth, eocs_[i] * (kl ? h : 0.0));
+            } else {
+                tth = sub_if(i < ne, tth, eocs_[i] * tru[i] * (kl ? flux_arr : 0.0));
+            }
+            // one edge at a time (the asm ties tth to this point): the scheduler would otherwise hoist
+            // all 54 LDS reads of the cell and spill
+            asm volatile("" : "+v"(tth));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (!HF && !RK0) {  // :1347-1360
+#pragma unroll
+            for (int i = 0; i < NF; i++) {
+                double flux = eocs_[i] * cdv_[i] * (trus[i] - tru[i]) * 0.5 * (tt2[i] + tt1[i]);
+                tth = sub_if(i < ne, tth, flux);
+            }
         }
     }
     if constexpr (WCE) {  // dyn_A's w section (:1170-1218, Q13), the same operands in the same order
@@ -1025,14 +1090,18 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
 
     // ================= theta =================
     double tend_theta = 0.0;  // :1328-1344
-    if (kl && HF) {  // the same sums over B's per-edge H (fast path: reassociated)
+    if (TILE) {  // (formed above)
+        if (kl) tend_theta = tth;
+    } else if (kl && HF) {  // the same sums over B's per-edge H (fast path: reassociated)
 #pragma unroll
         for (int i = 0; i < NF; i++) tend_theta = sub_if(i < ne, tend_theta, eocs_[i] * F_[i]);
-        for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(Ff, eoc[i]);
+        if constexpr (!TILE)
+            for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(Ff, eoc[i]);
     } else if (kl) {
 #pragma unroll
         for (int i = 0; i < NF; i++) tend_theta = sub_if(i < ne, tend_theta, eocs_[i] * ru_[i] * F_[i]);
-        for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(ru, eoc[i]) * colk(Ff, eoc[i]);
+        if constexpr (!TILE)
+            for (int i = NF; i < ne; i++) tend_theta -= eocs[i] * colk(ru, eoc[i]) * colk(Ff, eoc[i]);
         if (!rk0) {  // :1347-1360
 #pragma unroll
             for (int i = 0; i < NF; i++) {
@@ -1107,6 +1176,71 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
+template <int LP, bool RK0, bool SELF, bool MD, bool HF>
+__device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk bk) {
+    ColMap<LP> m(S, KC, bk);
+    if (m.ent >= S.nCO) return;
+    dyn_E_cell<LP, RK0, SELF, MD, HF>(S, a, m.ent, m.k);
+}
+
+// option "etile" (reference semantics, LP = 64): E over the tiles of TrTiles (mpas_dev.h; the
+// cells of a tile compact, its closure every cell the tile's cells read theta_m at).  The block
+// stages the closure's theta_m columns in LDS once -- two columns per 16-B lane load, level
+// order --, then its waves run E for the tile's cells, one cell per wave at a time, each edge's
+// advCells flux formed from LDS (dyn_E_cell TILE): no per-edge scratch X_F, and the ~27 theta_m
+// column gathers per cell of B's flux become the tile's closure, ~4 columns per cell
+struct EtK {
+    const int *tptr, *tcell, *cptr, *ccell, *teptr, *tedge;
+    const unsigned* erow;
+    int maxclo;
+};
+constexpr int ET_THREADS = 512;
+template <bool RK0, bool SELF, bool HF>
+__global__ __launch_bounds__(ET_THREADS, 4) void k_dyn_Et(DevState S, DynK a, EtK T) {
+    constexpr int LP = 64, NW = ET_THREADS / LP, U = 4;
+    extern __shared__ double lds[];
+    double* ldsw = lds + (size_t)(T.maxclo + 1) * LP;
+    const int tile = xcd_block(S.xcd);
+    const int k = (int)(threadIdx.x % LP), w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / LP));
+    const int cb = ldc(T.cptr + tile), n = ldc(T.cptr + tile + 1) - cb;
+    const double* tm = fd(S, F_theta_m);
+    // the closure's theta_m columns, level order (two columns per 16-B lane load), and the zero column
+    for (int i0 = 2 * w; i0 < n; i0 += 2 * NW * U) {
+        double2 g[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + 2 * NW * u;
+            const int ca = ldc(T.ccell + cb + (i < n ? i : 0)), cc = ldc(T.ccell + cb + (i + 1 < n ? i + 1 : 0));
+            g[u] = gather2s_ld<LP>(tm, ca, cc, k);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int i = i0 + 2 * NW * u;
+            double x, y;
+            g2_fin<LP>(g[u], x, y);
+            if (i < n) lds[i * LP + k] = x;
+            if (i + 1 < n) lds[(i + 1) * LP + k] = y;
+        }
+    }
+    if (w == NW - 1) lds[n * LP + k] = 0.0;
+    // B's scalar weights of the tile's edges (ac + s ac3 for s = +1, -1: exact in s, B's values)
+    const int eb = ldc(T.teptr + tile), nte = ldc(T.teptr + tile + 1) - eb;
+    const double *acf = fd(S, F_adv_coefs), *ac3f = fd(S, F_adv_coefs_3rd);
+    for (int t = (int)threadIdx.x; t < nte * AF; t += ET_THREADS) {
+        const int q = t / AF, j = t - q * AF;
+        const int e = T.tedge[eb + q];
+        const bool on = j < fi(S, F_nAdvCellsForEdge)[e];
+        const double ac = acf[(size_t)e * 15 + j], ac3 = ac3f[(size_t)e * 15 + j];
+        *(double2*)(ldsw + 2 * t) = on ? make_double2(ac + 1.0 * ac3, ac + -1.0 * ac3) : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+    const int tb = ldc(T.tptr + tile), nt = ldc(T.tptr + tile + 1) - tb;
+    for (int q = w; q < nt; q += NW) {
+        const int c = ldc(T.tcell + tb + q);
+        dyn_E_cell<LP, RK0, SELF, false, HF, true>(S, a, c, k, EtTile{lds, ldsw, T.erow + (size_t)(tb + q) * (ETT_REC / 4)});
+    }
+}
+
 // (rk_step > 0, reference semantics, LP = 64: 4 waves per SIMD, as before E formed wc itself;
 // at LP < 64 that cap spilled 10-22 VGPRs)
 template <int LP, bool RK0, bool SELF, bool MD, bool HF>
@@ -1161,10 +1295,22 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         else k_dyn_A<LP, false, MD><<<nb, 256, 0, st>>>(X, a);
     };
     const bool din = !MD && a.h4d > 0.0;  // (defer4: this rk_step > 0 call applies rk_step 0's D)
+    // option etile (reference semantics, LP = 64): E over cell tiles forms the fluxes; B none
+    const bool et = !MD && LP == 64 && S.ett != nullptr;
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
-        if (hf && (X.bsplit == 1 || (X.bsplit == 2 && MD))) {  // (option bsplit: the fluxes in k_dyn_Bf first)
+        if (et) {
+            if (hf) {
+                if (rk0) k_dyn_B<LP, true, MD, true, false, true><<<nb, 256, 0, st>>>(X, a);
+                else if (din) k_dyn_B<LP, false, MD, true, !MD, true><<<nb, 256, 0, st>>>(X, a);
+                else k_dyn_B<LP, false, MD, true, false, true><<<nb, 256, 0, st>>>(X, a);
+            } else {
+                if (rk0) k_dyn_B<LP, true, MD, false, false, true><<<nb, 256, 0, st>>>(X, a);
+                else if (din) k_dyn_B<LP, false, MD, false, !MD, true><<<nb, 256, 0, st>>>(X, a);
+                else k_dyn_B<LP, false, MD, false, false, true><<<nb, 256, 0, st>>>(X, a);
+            }
+        } else if (hf && (X.bsplit == 1 || (X.bsplit == 2 && MD))) {  // (option bsplit: the fluxes in k_dyn_Bf first)
             if (rk0) k_dyn_Bf<LP, true, MD><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_Bf<LP, false, MD><<<nb, 256, 0, st>>>(X, a);
             if (rk0) k_dyn_B<LP, true, MD, true, false, true><<<nb, 256, 0, st>>>(X, a);
@@ -1206,6 +1352,23 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     auto kE = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
         if (!nb) return;
+        if constexpr (LP == 64 && !MD) {
+            if (et) {  // (tiles only undecomposed: X is the whole owned range)
+                const TrTiles& TT = *X.ett;
+                const EtK T{TT.tptr, TT.tcell, TT.cptr, TT.ccell, TT.teptr, TT.tedge, TT.erow, TT.maxclo};
+                const size_t shm = ((size_t)(TT.maxclo + 1) * LP + (size_t)TT.maxte * 2 * AF) * sizeof(double);
+                auto go = [&](auto hfc, auto rkc) {
+                    constexpr bool H = decltype(hfc)::value, R = decltype(rkc)::value;
+                    if (X.selfc) k_dyn_Et<R, true, H><<<TT.ntiles, ET_THREADS, shm, st>>>(X, a, T);
+                    else k_dyn_Et<R, false, H><<<TT.ntiles, ET_THREADS, shm, st>>>(X, a, T);
+                };
+                if (hf && rk0) go(std::true_type{}, std::true_type{});
+                else if (hf) go(std::true_type{}, std::false_type{});
+                else if (rk0) go(std::false_type{}, std::true_type{});
+                else go(std::false_type{}, std::false_type{});
+                return;
+            }
+        }
         auto go = [&](auto hfc) {
             constexpr bool H = decltype(hfc)::value;
             if (rk0) {
@@ -1240,7 +1403,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
                    F_tend_theta_euler);
         const bool runD = del4 && !a.d4o;  // (defer4: D runs in the next call's B)
-        if (runD && in.hfuse && !S.halo) {  // D beside E, one grid
+        if (runD && in.hfuse && !S.halo && !et) {  // D beside E, one grid
             const int nb1 = col_blocks<LP>(S, KE), nb = nb1 + col_blocks<LP>(S, KC);
             auto go = [&](auto hfc) {
                 constexpr bool H = decltype(hfc)::value;
@@ -1256,7 +1419,8 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
                 HALO_WROTE(S, F_tend_u_euler, F_tend_u);
             }
-            if (hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta);  // (X_Fw: MD only written)
+            if (et) HALO_RUN(S, st, kE, F_ru, F_theta_m, F_delsq_w, F_delsq_theta);
+            else if (hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta);  // (X_Fw: MD only written)
             else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
         }
     } else {
@@ -1272,7 +1436,8 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         if (din) HALO_WROTE(S, F_tend_u_euler);
         if (a.vB) HALO_WROTE(S, F_v);
         if (MD) HALO_WROTE(S, X_Fw);
-        if (hf) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw);  // (ru: wc at the cell's last edge, reference semantics)
+        if (et) HALO_RUN(S, st, kE, F_ru, F_ru_save, F_theta_m, F_theta_m_save);
+        else if (hf) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw);  // (ru: wc at the cell's last edge, reference semantics)
         else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);
     }
     HALO_WROTE(S, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);

@@ -157,7 +157,7 @@ struct mpas_ctx {
     int keep_check = 0;
     int* keep_flag = nullptr;
     // set when a transport refused a capture: eager steps from then on (the user's graph_halo
-    // stays as set; a new halo plan or option change clears it)
+    // stays as set; a new halo plan or a graph_halo option change clears it)
     bool graph_refused = false;
     std::vector<std::vector<uint8_t>> seen_stale0;  // start states stepped eagerly once
     // option "trtile": the tiled transport (k_transport.hip) when the mesh allows it; the
@@ -174,9 +174,19 @@ struct mpas_ctx {
     // rebuilt with the tiles)
     int tredge = 0;
     TrEdgeGroups tre;
+    // option "etile" (default 1): dyn_tend's cell kernel E over compact tiles of cells, the tile's
+    // theta_m closure staged in LDS, each edge's advCells flux formed there (k_dyn_Et) -- the edge
+    // kernel then forms no flux and the per-edge scratch X_F goes (reference semantics, LP = 64,
+    // undecomposed; the same bits either way).  Options "etcells" / "etclo": tile size limits
+    int etile = 0;
+    int ett_cells = 8, ett_clo = 96;
+    bool ett_dirty = true;
+    TrTiles ett;
 };
 
 namespace {
+
+void ett_ensure(mpas_ctx* c);
 
 struct Fail {
     int code;
@@ -385,6 +395,7 @@ void run_task(mpas_ctx* c, const char* name, Fn&& fn) {
         c->S.selfc = c->self_ok && c->self_on;
         c->dirty = false;
     }
+    ett_ensure(c);  // (built before a capture by prepare_now)
     hipError_t e = fn();
     if (e != hipSuccess) {
         if (c->halo && !c->halo->err.empty())
@@ -528,11 +539,9 @@ int guarded(mpas_ctx* c, Fn&& fn) {
 }
 
 // ---- tiled transport: the cell tiles (TrTiles, mpas_dev.h) ----
+void tiles_free(TrTiles& T);
 void trt_free(mpas_ctx* c) {
-    TrTiles& T = c->trt;
-    for (void* p : {(void*)T.tptr, (void*)T.tcell, (void*)T.cptr, (void*)T.ccell, (void*)T.slot})
-        if (p) (void)hipFree(p);
-    T = TrTiles{};
+    tiles_free(c->trt);
     c->S.trt = nullptr;
 }
 template <class V>
@@ -617,6 +626,16 @@ void tre_build(mpas_ctx* c) {
     c->S.tre = &c->tre;
 }
 
+void tiles_free(TrTiles& T) {
+    for (void* p : {(void*)T.tptr, (void*)T.tcell, (void*)T.cptr, (void*)T.ccell, (void*)T.slot, (void*)T.teptr,
+                    (void*)T.tedge, (void*)T.erow})
+        if (p) (void)hipFree(p);
+    T = TrTiles{};
+}
+// the tiles (into T) of at most `cells` owned cells whose closure fits `clo_max` LDS columns;
+// false (T empty) when the mesh does not allow them
+bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max);
+
 void trt_build(mpas_ctx* c) {
     trt_free(c);
     tre_free(c);
@@ -624,6 +643,26 @@ void trt_build(mpas_ctx* c) {
     tre_build(c);
     if (!c->trtile) return;
     if (c->halo && !c->trt_ghosts) return;  // the tiles would read ghosts the local mesh lacks
+    if (tiles_build(c, c->trt, c->trt_cells, c->trt_clo)) c->S.trt = &c->trt;
+}
+
+// option "etile": dyn_tend's cell kernel E over tiles of cells with the tile's theta_m closure
+// in LDS (k_dyn_Et, k_dyn.hip); reference semantics, LP = 64, undecomposed
+void ett_free(mpas_ctx* c) {
+    tiles_free(c->ett);
+    c->S.ett = nullptr;
+}
+void ett_build(mpas_ctx* c) {
+    ett_free(c);
+    c->ett_dirty = false;
+    if (!c->etile || c->halo || c->S.LP != 64 || c->S.physics == 2) return;
+    if (tiles_build(c, c->ett, c->ett_cells, c->ett_clo)) c->S.ett = &c->ett;
+}
+void ett_ensure(mpas_ctx* c) {
+    if (c->ett_dirty) ett_build(c);
+}
+
+bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max) {
     hipcheck(hipSetDevice(c->device), "hipSetDevice");
     const DevState& S = c->S;
     const int nC = S.nCells, nE = S.nEdges, nCO = S.nCO;
@@ -635,9 +674,9 @@ void trt_build(mpas_ctx* c) {
     const auto nadv = dev_read<int>(S.f[F_nAdvCellsForEdge], (size_t)nE + 1);
     auto nedges = [&](int x) { return nEoC[x] > 0 ? nEoC[x] : 0; };
     for (int x = 0; x < nCO; x++) {
-        if (nEoC[x] > NF) return;
+        if (nEoC[x] > NF) return false;
         for (int i = 0; i < nedges(x); i++)
-            if (nadv[eoc[(size_t)x * 10 + i]] > AF) return;
+            if (nadv[eoc[(size_t)x * 10 + i]] > AF) return false;
     }
     // the columns cell x's kernels read: x, both cells of each edge, the edge's advCells
     auto need = [&](int x, auto&& f) {
@@ -654,6 +693,9 @@ void trt_build(mpas_ctx* c) {
     std::vector<int> tptr{0}, tcell, cptr{0}, ccell, queue, cells, clo;
     std::vector<int> slot;
     int stamp = 0, maxclo = 0, nt_int = 0;
+    std::vector<int> emark((size_t)nE + 1, -1), tedge, teptr{0};
+    std::vector<unsigned> erow;
+    int tebase = 0, maxte = 0;
     // launch classes: 0 = interior cells whose every column is owned (or the zero slot),
     // run beside a halo exchange; 1 = the rest (boundary cells, and interior cells that
     // reach a ghost through advCellsForEdge(edgesOnCell), which the halo's interior
@@ -673,14 +715,14 @@ void trt_build(mpas_ctx* c) {
             clo.clear();
             queue.assign(1, seed);
             inq[seed] = tid;
-            for (size_t qh = 0; qh < queue.size() && (int)cells.size() < c->trt_cells; qh++) {
+            for (size_t qh = 0; qh < queue.size() && (int)cells.size() < max_cells; qh++) {
                 const int x = queue[qh];
                 int add = 0;
                 stamp++;
                 need(x, [&](int y) {
                     if (mark[y] < 0 && seen[y] != stamp) seen[y] = stamp, add++;
                 });
-                if (!cells.empty() && (int)clo.size() + add > c->trt_clo) continue;
+                if (!cells.empty() && (int)clo.size() + add > clo_max) continue;
                 cells.push_back(x);
                 assigned[x] = 1;
                 need(x, [&](int y) {
@@ -694,6 +736,21 @@ void trt_build(mpas_ctx* c) {
                             inq[y] = tid, queue.push_back(y);
                     }
                 }
+            }
+            for (int x : cells) {  // the tile's edges (first use) and each cell's record of them (ETT_REC)
+                unsigned char r[ETT_REC] = {};
+                const int zero = (int)clo.size();  // (the zero column after the closure's)
+                for (int i = 0; i < NF; i++) {
+                    unsigned char* ri = r + i * ETT_EB;
+                    for (int j = 0; j < AF; j++) ri[1 + j] = (unsigned char)zero;
+                    if (i >= nedges(x)) continue;
+                    const int e = eoc[(size_t)x * 10 + i];
+                    if (emark[e] < 0) emark[e] = (int)tedge.size() - tebase, tedge.push_back(e);
+                    ri[0] = (unsigned char)emark[e];
+                    for (int j = 0; j < nadv[e]; j++) ri[1 + j] = (unsigned char)mark[adv[(size_t)e * 15 + j]];
+                }
+                const unsigned* rw = (const unsigned*)r;
+                erow.insert(erow.end(), rw, rw + ETT_REC / 4);
             }
             for (int x : cells) {  // the LDS rows
                 int row[TRT_ROW] = {};
@@ -709,13 +766,16 @@ void trt_build(mpas_ctx* c) {
                 tcell.push_back(x);
             }
             for (int y : clo) mark[y] = -1, ccell.push_back(y);
+            for (size_t q = tebase; q < tedge.size(); q++) emark[tedge[q]] = -1;
+            maxte = std::max(maxte, (int)tedge.size() - tebase);
+            tebase = (int)tedge.size();
+            teptr.push_back(tebase);
             maxclo = std::max(maxclo, (int)clo.size());
             tptr.push_back((int)tcell.size());
             cptr.push_back((int)ccell.size());
         }
         if (cls == 0) nt_int = (int)tptr.size() - 1;
     }
-    TrTiles& T = c->trt;
     T.ntiles = (int)tptr.size() - 1;
     T.nt_int = nt_int;
     T.nco = nCO;
@@ -726,7 +786,12 @@ void trt_build(mpas_ctx* c) {
     T.cptr = dev_copy(cptr);
     T.ccell = dev_copy(ccell);
     T.slot = dev_copy(slot);
-    c->S.trt = &c->trt;
+    T.nclo = (int)ccell.size();
+    T.teptr = dev_copy(teptr);
+    T.tedge = dev_copy(tedge);
+    T.erow = dev_copy(erow);
+    T.maxte = maxte;
+    return true;
 }
 void trt_ensure(mpas_ctx* c) {
     if (c->trt_dirty) trt_build(c);
@@ -1018,6 +1083,7 @@ void prepare_now(mpas_ctx* c) {
         c->dirty = false;
     }
     if (c->transport) trt_ensure(c);
+    ett_ensure(c);
 }
 
 // one atm_srk3 step: replayed from a captured HIP graph when possible
@@ -1229,6 +1295,7 @@ int mpas_ctx_destroy(mpas_ctx* c) {
     for (auto e : c->event_pool) (void)hipEventDestroy(e);
     graph_drop(c);
     trt_free(c);
+    ett_free(c);
     c->halo.reset();
     c->loopgrp.reset();
     for (auto p : c->gid_dev)
@@ -1295,6 +1362,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
                 throw Fail{MPAS_EINVAL, "physics must be 0 (reference), 1 (MPAS vertical solver) or 2 (MPAS dynamics)"};
             c->S.physics = (int)value;
             if (!value) c->transport = 0;
+            c->ett_dirty = true;
         } else if (name && std::strcmp(name, "trorder_e") == 0) {
             if (value < 0 || value > (1 << 20)) throw Fail{MPAS_EINVAL, "trorder_e must be 0 (trorder's), 1 or a run length >= 2"};
             c->S.troe = (int)value;
@@ -1316,21 +1384,32 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             c->S.ring1 = value ? 1 : 0;
         } else if (name && std::strcmp(name, "trtile") == 0) {
             c->trtile = value ? 1 : 0;
-            c->trt_dirty = true;
+            c->trt_dirty = c->ett_dirty = true;
         } else if (name && std::strcmp(name, "tredge") == 0) {
             c->tredge = value ? 1 : 0;
-            c->trt_dirty = true;
+            c->trt_dirty = c->ett_dirty = true;
         } else if (name && std::strcmp(name, "trtile_ghosts") == 0) {
             c->trt_ghosts = value ? 1 : 0;
-            c->trt_dirty = true;
+            c->trt_dirty = c->ett_dirty = true;
         } else if (name && std::strcmp(name, "trtcells") == 0) {
             if (value < 1 || value > 256) throw Fail{MPAS_EINVAL, "trtcells must be 1..256"};
             c->trt_cells = (int)value;
-            c->trt_dirty = true;
+            c->trt_dirty = c->ett_dirty = true;
         } else if (name && std::strcmp(name, "trtclo") == 0) {
             if (value < 1 + NF * (2 + AF) || value > 120) throw Fail{MPAS_EINVAL, "trtclo must be 67..120 (LDS columns)"};
             c->trt_clo = (int)value;
-            c->trt_dirty = true;
+            c->trt_dirty = c->ett_dirty = true;
+        } else if (name && std::strcmp(name, "etile") == 0) {
+            c->etile = value ? 1 : 0;
+            c->ett_dirty = true;
+        } else if (name && std::strcmp(name, "etcells") == 0) {
+            if (value < 1 || value > 40) throw Fail{MPAS_EINVAL, "etcells must be 1..40 (a tile's edges index in one byte)"};
+            c->ett_cells = (int)value;
+            c->ett_dirty = true;
+        } else if (name && std::strcmp(name, "etclo") == 0) {
+            if (value < 1 + NF * (2 + AF) || value > 160) throw Fail{MPAS_EINVAL, "etclo must be 67..160 (LDS columns)"};
+            c->ett_clo = (int)value;
+            c->ett_dirty = true;
         } else if (name && std::strcmp(name, "transport") == 0) {
             if (value && !c->S.physics) throw Fail{MPAS_EINVAL, "transport needs physics = 1 (it reads the recovered ruAvg, wwAvg, rho_zz)"};
             c->transport = value ? 1 : 0;
@@ -1386,6 +1465,22 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         } else if (name && std::strcmp(name, "trtile_count") == 0) {
             trt_ensure(c);
             *value = c->trt.ntiles;
+        }
+        else if (name && std::strcmp(name, "etile") == 0) *value = c->etile;
+        else if (name && std::strcmp(name, "etcells") == 0) *value = c->ett_cells;
+        else if (name && std::strcmp(name, "etclo") == 0) *value = c->ett_clo;
+        else if (name && std::strcmp(name, "etile_active") == 0) {  // dyn_tend tiles built for this mesh
+            ett_ensure(c);
+            *value = c->S.ett ? 1 : 0;
+        } else if (name && std::strcmp(name, "etile_count") == 0) {
+            ett_ensure(c);
+            *value = c->ett.ntiles;
+        } else if (name && std::strcmp(name, "etile_columns") == 0) {  // closure columns staged per launch
+            ett_ensure(c);
+            *value = c->ett.nclo;
+        } else if (name && std::strcmp(name, "etile_maxclo") == 0) {
+            ett_ensure(c);
+            *value = c->ett.maxclo;
         }
         else if (name && std::strcmp(name, "overlap") == 0) *value = c->overlap;
         else if (name && std::strcmp(name, "fusedamp") == 0) *value = c->fusedamp;
@@ -1461,7 +1556,7 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
                     hipcheck(launch_keep_refresh(c->S, c->stream, f, keep_kind(f)), "keep_refresh");
                 hipcheck(hipStreamSynchronize(c->stream), "hipStreamSynchronize");
                 c->dirty = true;
-                c->trt_dirty = true;
+                c->trt_dirty = c->ett_dirty = true;
                 graph_drop(c);
                 if (c->halo) c->halo->stale[f] = 0;
                 return;
@@ -1522,7 +1617,7 @@ int mpas_upload(mpas_ctx* c, int f, const void* host, int64_t se, int64_t sl, in
         }
         hipcheck(hipMemcpy(c->S.f[f], buf.data(), bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
         c->dirty = true;
-        c->trt_dirty = true;
+        c->trt_dirty = c->ett_dirty = true;
         graph_drop(c);
         if (c->halo) c->halo->stale[f] = 0;  // uploaded ghosts are the global values
         // derived mesh arrays: cos()/sin() on the host with the same libm as the oracle
@@ -1639,7 +1734,7 @@ int mpas_halo_owned(mpas_ctx* c, int32_t nCellsOwned, int32_t nEdgesOwned, int32
         c->S.nEO = nEdgesOwned;
         c->S.nVO = nVerticesOwned;
         c->dirty = true;
-        c->trt_dirty = true;
+        c->trt_dirty = c->ett_dirty = true;
     });
 }
 
@@ -1666,7 +1761,7 @@ int mpas_halo_interior(mpas_ctx* c, int32_t nCI, int32_t nEI, int32_t nVI) {
         h->nint[2] = nVI;
         h->interior = true;
         h->overlap = c->overlap;
-        c->trt_dirty = true;
+        c->trt_dirty = c->ett_dirty = true;
         if (!h->comm) {  // the halo stream, at the device's highest priority
             int least = 0, greatest = 0;
             hipcheck(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
@@ -1861,7 +1956,7 @@ int mpas_atm_adv_coef_compression(mpas_ctx* c) {
     return guarded(c, [&] {
         run_task(c, "atm_adv_coef_compression", [&] { return launch_adv_coef_compression(c->S, c->stream); });
         c->dirty = true;
-        c->trt_dirty = true;
+        c->trt_dirty = c->ett_dirty = true;
         graph_drop(c);
     });
 }
@@ -1882,7 +1977,7 @@ int mpas_atm_core_init(mpas_ctx* c) {
         run_task(c, "atm_compute_signs", [&] { return launch_compute_signs(S, st); });
         run_task(c, "atm_adv_coef_compression", [&] { return launch_adv_coef_compression(S, st); });
         c->dirty = true;  // (k_prepare re-derives the edge records before the next task)
-        c->trt_dirty = true;
+        c->trt_dirty = c->ett_dirty = true;
         graph_drop(c);
         run_task(c, "atm_couple_coef_3rd_order", [&] { return launch_couple_coef_3rd_order(S, st, 0.25); });
         run_task(c, "atm_init_coupled_diagnostics", [&] { return launch_init_coupled_diagnostics(S, st); });

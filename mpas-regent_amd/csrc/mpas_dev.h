@@ -156,6 +156,7 @@ struct DevState {
     Halo* halo;  // host-side halo exchanger of a decomposed mesh, nullptr otherwise
     const TrTiles* trt;  // host-side: the tiles of the tiled transport, nullptr = the three-kernel path
     const TrEdgeGroups* tre;  // host-side: the edge groups of k_tr_edge_lds, nullptr = k_tr_edge
+    const TrTiles* ett;  // host-side: the cell tiles of dyn_tend's tiled E (k_dyn_Et), nullptr = k_dyn_E
     const int* gid[3];  // device global ids of the local cells/edges/vertices (decomposed
                         // meshes: the synthetic fill hashes them), nullptr = identity
 };
@@ -417,12 +418,23 @@ struct TrTiles {
     int ntiles = 0, nt_int = 0;  // tiles; the first nt_int hold interior cells only
     int nco = 0, nint = 0;       // the owned / interior cell counts the tiles were built for
     int maxclo = 0;              // largest closure (LDS columns per block)
+    int nclo = 0;                // closure columns of all tiles (the staging loads)
     int* tptr = nullptr;         // ntiles + 1: first cell of each tile in tcell
     int* tcell = nullptr;        // the tiles' cells
     int* cptr = nullptr;         // ntiles + 1: first closure cell of each tile in ccell
     int* ccell = nullptr;        // closure cells, in LDS column order
     int* slot = nullptr;          // TRT_ROW LDS columns per tile cell (tcell order)
+    // dyn_tend's tiled E (k_dyn_Et): the tile's edges, and per tile cell one ETT_REC-byte record
+    int* teptr = nullptr;         // ntiles + 1: first edge of each tile in tedge
+    int* tedge = nullptr;         // the edges of the tile's cells, in first-use order
+    unsigned* erow = nullptr;     // per tile cell (tcell order), per edge slot i < NF, ETT_EB bytes: the
+                                  // edge's index among the tile's edges, then its AF advCells' closure
+                                  // columns (the zero column, index = closure size, past nAdvCellsForEdge
+                                  // and for slots past nEdgesOnCell)
+    int maxte = 0;                // most edges of a tile
 };
+constexpr int ETT_EB = 12;            // record bytes per edge slot (1 + AF, padded)
+constexpr int ETT_REC = NF * ETT_EB;  // 72: 18 dwords per tile cell
 
 // The transport's edge kernel with its scalars_old columns staged in LDS (k_tr_edge_lds,
 // option "tredge"): the owned edges in groups of TRE_GE consecutive ids (Morton-adjacent);

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import compare_states
+from helpers import ZERO_SLOT_WRITTEN, compare_states
 from mpasdyn import jw, lib
 from mpasdyn import mesh as M
 from mpasdyn import tasks as T
@@ -13,7 +13,7 @@ from mpasdyn import tasks as T
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("L", [26, 56])
+@pytest.mark.parametrize("L", [5, 26, 56])  # (5: the reference's default, constants.rg:26, BASELINE config 1)
 def test_jw_steps_match_oracle(x1_2562, L):
     st = jw.jw_state(M.zero_based(x1_2562), L)
     ref = st.copy()
@@ -29,6 +29,47 @@ def test_jw_steps_match_oracle(x1_2562, L):
         ctx.sync()
         ctx.download(got)
     bad = compare_states(got, ref, rtol=0.0)
+    assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("schedule", [0, 1])
+def test_jw_config1_fast_path(x1_2562, schedule):
+    """BASELINE config 1 (x1.2562 x 5 levels) from the JW state on the benchmark path (exact 0, graph
+    replay): within the fast path's step tolerance of the oracle, NaN / inf masks equal, for the
+    reference's driver schedule (0) and the MPAS one (1)"""
+    st = jw.jw_state(M.zero_based(x1_2562), 5)
+    ref = st.copy()
+    o = O.Oracle(ref)
+    for _ in range(3):
+        o.atm_srk3(720.0, schedule)
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.set_option("exact", 0)
+        ctx.upload(st)
+        for _ in range(3):
+            T.atm_srk3(ctx, 720.0, schedule)
+        ctx.sync()
+        ctx.download(got)
+    bad = compare_states(got, ref, rtol=1e-9)
+    assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("physics", [1, 2])
+def test_jw_config1_mpas(x1_2562, physics):
+    """the MPAS solver / dynamics from the JW state at 5 levels: exact mode = the oracle bit for bit but
+    for the pow of recover's exner / pressure_p (device pow against glibc's: 1e-14)"""
+    st = jw.jw_state(M.zero_based(x1_2562), 5)
+    ref = st.copy()
+    O.Oracle(ref).mpas_srk3(720.0, 1, physics=physics)
+    got = st.copy()
+    with lib.Context(*st.dims()) as ctx:
+        ctx.set_option("exact", 1)
+        ctx.set_option("physics", physics)
+        ctx.upload(st)
+        T.atm_srk3(ctx, 720.0, 1)
+        ctx.sync()
+        ctx.download(got)
+    bad = compare_states(got, ref, rtol=1e-14, tol_fields={"exner", "pressure_p"}, zero_slot_excluded=ZERO_SLOT_WRITTEN)
     assert not bad, bad[:6]
 
 

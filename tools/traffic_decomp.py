@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
-"""Traffic decomposition of atm_compute_dyn_tend_work: the HBM bytes its
-kernels move per launch set, measured (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, gfx950
+"""Traffic decomposition of atm_compute_dyn_tend_work: the HBM
+bytes its kernels move per launch, measured (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE, the gfx950
 correction of MI355X_MICROARCH.md), split into
 
     compulsory     the distinct arrays the whole task reads and writes, once each, at their
-                   stored (LP-padded) size  -- the floor of any implementation in this layout
+                   stored (LP-padded) size -- the floor of any implementation in this layout
     intermediates  sum over kernels of each kernel's distinct arrays, minus the compulsory:
                    scratch written by one kernel and read back by another (X_F, X_wc), outputs
                    read back by a later kernel (kdiff, dpdz, delsq_*, tend_*_euler), inputs
@@ -15,11 +15,18 @@ correction of MI355X_MICROARCH.md), split into
 
 and B_alg (unpadded, the reference's read/write sets; mpasdyn/roofline.py).
 
-usage: python tools/traffic_decomp.py KERNELS.txt [--dims 163842 491520 327680 56] [--lp 64]
-       [--layout r03|r04] [--json OUT]
-KERNELS.txt is tools/pmc_kernels.py output over FETCH_SIZE, WRITE_SIZE (and TCC) passes of one
-bench step (tools/gpu.sh pmc).  --layout names the kernel sequence: r03 = A B C D E at rk_step 0
-(D its own launch), r04 = option defer4 (no D; stage 1's B applies it)."""
+usage: python tools/traffic_decomp.py KERNELS.txt --layout r05|r06 [--round r06]
+       [--dims 163842 491520 327680 56] [--lp 64] [--json OUT]
+KERNELS.txt is tools/pmc_kernels.py output over the FETCH_SIZE and WRITE_SIZE (and TCC) passes of
+one bench step (tools/gpu.sh pmc).  Layouts (the kernels of the benchmark path, every variant by its
+template arguments):
+    r05  round 5's path: A, B (fast path: B forms each edge's theta flux H into X_F), C, E; rk_step 0
+         leaves D to stage 1's B (defer4: B's DIN variant), stage 2's B stores v (vdyn)
+    r06  option etile: B forms no flux (its NOF variant), the tiled E (k_dyn_Et) forms each edge's flux
+         from its tile's theta_m columns in LDS; no X_F
+The tool fails (exit status 2) when a dyn_tend kernel of the file matches no kernel of the layout,
+when a kernel of the layout is missing from the file, or when a kernel's measured bytes fall below
+its distinct bytes (a negative refetch: the layout's read / write set of that kernel is wrong)."""
 import argparse
 import json
 import os
@@ -29,70 +36,92 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "mpas-regent_amd")]
 
-# mesh rows a kernel loads, bytes per entity (the row_ld widths, not the stored widths)
-MESH = {
-    "A": ("C", 80 + 48 + 48 + 16 + 8 + 8 + 48 + 48),   # X_cR record, eocs, ce_dv, wfl, invArea, cosLat, defc_a/b (rk0)
-    "B": ("E", 96 + 80 + 72 + 72 + 8 * 6),              # X_eB record, woe, adv_coefs(_3rd), scalars
-    "C": ("C", 80 + 48 * 5),                            # + the vertex part below
-    "Cv": ("V", 12 + 24 + 24 + 8),
-    "D": ("E", 8 * 2 + 8 * 2 + 8 * 3),
-    "E": ("C", 80 + 48 * 5 + 16),
-}
+# A kernel name as pmc_kernels.py prints it, e.g. "k_dyn_B<64, false, false, true, true, false>":
+# the template arguments in order (bools as 0/1, ints as ints)
+def targs(name):
+    m = re.match(r"^(k_dyn_\w+)<([^>]*)>$", name.strip())
+    if not m:
+        return None, None
+    args = []
+    for a in m.group(2).split(","):
+        a = a.strip()
+        args.append(1 if a == "true" else 0 if a == "false" else int(a))
+    return m.group(1), tuple(args)
 
-# 3-D arrays per kernel (reads, writes) on the benchmark path: reference semantics, fast
-# path (HF: B forms H per edge), fusecopy at stage 0.  kind by registry
-KERN = {
-    "r03": {
-        "rk0": [
-            ("A", ["ru", "u", "v", "rw", "rho_zz", "uReconstructZonal", "uReconstructMeridional", "tend_rho_physics",
-                   "qtot", "rho_base", "rho_p_save"], ["kdiff", "h_divergence", "tend_rho", "dpdz", "X_wc"]),
-            ("B", ["u", "ru", "rho_edge", "pv_edge", "tend_ru_physics", "cqu", "zxu", "rw", "w", "ke", "h_divergence",
-                   "pressure_p", "zz", "dpdz", "divergence", "kdiff", "theta_m", "vorticity"],
-             ["X_F", "tend_u", "tend_u_euler", "delsq_u", "ru_save", "u_2"]),
-            ("C", ["delsq_u", "rho_edge", "kdiff", "X_wc", "theta_m"],
-             ["delsq_vorticity", "delsq_divergence", "delsq_w", "tend_w_euler", "delsq_theta", "tend_theta_euler"]),
-            ("D", ["rho_edge", "tend_u_euler", "tend_u", "tend_ru_physics", "delsq_divergence", "delsq_vorticity"],
-             ["tend_u_euler", "tend_u"]),
-            ("E", ["X_wc", "rw", "pressure_p", "dpdz", "rw_save", "theta_m_save", "theta_m", "tend_w_euler",
-                   "tend_theta_euler", "rho_zz", "rt_diabatic_tend", "tend_rtheta_physics", "cqw", "delsq_w",
-                   "delsq_theta", "X_F"],
-             ["w", "tend_rtheta_adv", "rthdynten", "tend_theta", "tend_w_euler", "tend_theta_euler"]),
+
+# Each kernel of a layout: (label, kernel, predicate over its template arguments, reads, writes, mesh)
+#   reads / writes: 3-D arrays; "f:C" = only nCells columns of the (edge) array f are touched
+#   mesh: (entity kind, bytes per entity) of the mesh rows and tables the kernel loads
+B_RK0_R = ["u", "ru", "rho_edge", "pv_edge", "tend_ru_physics", "cqu", "zxu", "rw", "w", "ke", "h_divergence",
+           "pressure_p", "zz", "dpdz", "divergence", "kdiff", "vorticity"]
+B_RK1_R = ["u", "ru", "rho_edge", "pv_edge", "tend_ru_physics", "tend_u_euler", "rw", "w", "ke", "h_divergence"]
+E_RK1_R = ["rw", "rw_save", "theta_m_save", "theta_m", "tend_w_euler", "tend_theta_euler", "rho_zz",
+           "rt_diabatic_tend", "tend_rtheta_physics", "uReconstructZonal", "uReconstructMeridional"]
+E_RK0_R = ["X_wc", "rw", "pressure_p", "dpdz", "rw_save", "theta_m_save", "theta_m", "tend_w_euler",
+           "tend_theta_euler", "rho_zz", "rt_diabatic_tend", "tend_rtheta_physics", "cqw", "delsq_w", "delsq_theta"]
+E_W = ["w", "tend_rtheta_adv", "rthdynten", "tend_theta"]
+E_EB = 96 + 4 + 8 + 8 * 6  # X_eB record, nEdgesOnEdge...: B's index record and per-edge scalars
+W_EDGE = 80                 # weightsOnEdge row (QF doubles)
+ADV_EDGE = 72 + 72          # adv_coefs, adv_coefs_3rd (AF doubles each)
+C_REC = 80 + 48 + 48         # X_cR record, edgesOnCell_sign, ce_dv
+A_KS = [
+    ("A", "k_dyn_A", lambda t: t[1] == 1, ["ru", "u", "v", "rw", "rho_zz", "uReconstructZonal",
+                                            "uReconstructMeridional", "tend_rho_physics", "qtot", "rho_base",
+                                            "rho_p_save"], ["kdiff", "h_divergence", "tend_rho", "dpdz", "X_wc"],
+     ("C", C_REC + 16 + 8 + 8 + 48 + 48)),
+]
+A_K1 = ("A", "k_dyn_A", lambda t: t[1] == 0, ["ru"], ["h_divergence"], ("C", C_REC + 8))
+C_K = ("C", "k_dyn_C12", lambda t: True, ["delsq_u", "rho_edge", "kdiff", "X_wc", "theta_m"],
+       ["delsq_vorticity", "delsq_divergence", "delsq_w", "tend_w_euler", "delsq_theta", "tend_theta_euler"],
+       ("C", C_REC + 48 * 3 + 12 * 0))
+LAYOUTS = {
+    "r05": {
+        "rk0": A_KS + [
+            ("B", "k_dyn_B", lambda t: t[1:] == (1, 0, 1, 0, 0), B_RK0_R + ["theta_m"],
+             ["X_F", "tend_u_euler", "delsq_u", "ru_save", "u_2"], ("E", E_EB + W_EDGE + ADV_EDGE)),
+            C_K,
+            ("E", "k_dyn_E", lambda t: t[1] == 1 and t[3:] == (0, 1), E_RK0_R + ["X_F"], E_W + ["tend_w_euler",
+                                                                                           "tend_theta_euler"],
+             ("C", C_REC + 48 * 2 + 8)),
+        ],
+        "rk1din": [
+            A_K1,
+            ("B", "k_dyn_B", lambda t: t[1:] == (0, 0, 1, 1, 0),
+             B_RK1_R + ["theta_m", "ru_save", "theta_m_save", "delsq_divergence", "delsq_vorticity"],
+             ["X_F", "tend_u", "tend_u_euler"], ("E", E_EB + W_EDGE + ADV_EDGE)),
+            ("E", "k_dyn_E", lambda t: t[1] == 0 and t[3:] == (0, 1), E_RK1_R + ["ru:C", "X_F"], E_W,
+             ("C", C_REC + 16 + 8 + 8)),
         ],
         "rk1": [
-            ("A", ["ru", "rw", "rho_zz", "uReconstructZonal", "uReconstructMeridional"], ["h_divergence", "X_wc"]),
-            ("B", ["u", "ru", "rho_edge", "pv_edge", "tend_ru_physics", "tend_u_euler", "ru_save", "rw", "w", "ke",
-                   "h_divergence", "theta_m", "theta_m_save"], ["X_F", "tend_u"]),
-            ("E", ["X_wc", "rw", "rw_save", "theta_m_save", "theta_m", "tend_w_euler", "tend_theta_euler", "rho_zz",
-                   "rt_diabatic_tend", "tend_rtheta_physics", "X_F"],
-             ["w", "tend_rtheta_adv", "rthdynten", "tend_theta"]),
+            A_K1,
+            ("B", "k_dyn_B", lambda t: t[1:] == (0, 0, 1, 0, 0), B_RK1_R + ["theta_m", "ru_save", "theta_m_save"],
+             ["X_F", "tend_u", "v"], ("E", E_EB + W_EDGE + ADV_EDGE)),
+            ("E", "k_dyn_E", lambda t: t[1] == 0 and t[3:] == (0, 1), E_RK1_R + ["ru:C", "X_F"], E_W,
+             ("C", C_REC + 16 + 8 + 8)),
         ],
     },
 }
-# option defer4 (r04): stage 0 runs A B C E (B stores no tend_u), stage 1's B applies D
-_r04 = {"rk0": [k for k in KERN["r03"]["rk0"] if k[0] != "D"], "rk1": list(KERN["r03"]["rk1"])}
-_r04["rk0"][1] = ("B", KERN["r03"]["rk0"][1][1], ["X_F", "tend_u_euler", "delsq_u", "ru_save", "u_2"])
-_r04["rk1din"] = [k if k[0] != "B" else
-                  ("B", k[1] + ["delsq_divergence", "delsq_vorticity"], k[2] + ["tend_u_euler"])
-                  for k in KERN["r03"]["rk1"]]
-# (the plain rk_step > 0 launch is stage 2's, whose B also stores v: option vdyn; E forms wc)
-_r04["rk1"] = [("A", ["ru"], ["h_divergence"]) if k[0] == "A" else
-               ("B", k[1], k[2] + ["v"]) if k[0] == "B" else
-               ("E", [f for f in k[1] if f != "X_wc"] + ["ru", "uReconstructZonal", "uReconstructMeridional"], k[2])
-               for k in KERN["r03"]["rk1"]]
-_r04["rk1din"] = [("A", ["ru"], ["h_divergence"]) if k[0] == "A" else
-                  ("E", [f for f in k[1] if f != "X_wc"] + ["ru", "uReconstructZonal", "uReconstructMeridional"], k[2])
-                  if k[0] == "E" else k for k in _r04["rk1din"]]
-KERN["r04"] = _r04
-
-# the kernel names of the rocprofv3 output per launch kind
-PAT = {
-    ("rk0", "A"): r"^k_dyn_A<64, true", ("rk0", "B"): r"^k_dyn_B<64, true", ("rk0", "C"): r"^k_dyn_C(12)?<64",
-    ("rk0", "D"): r"^k_dyn_D<64", ("rk0", "E"): r"^k_dyn_E<64, true",
-    ("rk1", "A"): r"^k_dyn_A<64, false", ("rk1", "B"): r"^k_dyn_B<64, false, false, true(, false)?>$",
-    ("rk1", "E"): r"^k_dyn_E<64, false",
-    ("rk1din", "A"): r"^k_dyn_A<64, false", ("rk1din", "B"): r"^k_dyn_B<64, false, false, true, true>",
-    ("rk1din", "E"): r"^k_dyn_E<64, false",
-}
+# r06 (option etile): B without the flux (NOF), the tiled E (k_dyn_Et<RK0, SELF, HF>) reads ru at every
+# edge of its cells, ru_save / theta_m_save at rk_step > 0 and the tile's theta_m closure; mesh: its
+# cell records (72 B), the tiles' edge lists and the edges' adv_coefs / adv_coefs_3rd rows
+ET_MESH_C = C_REC + 72 + 8 + 8
+_r06 = {"rk0": [], "rk1din": [], "rk1": []}
+for lk, ks in LAYOUTS["r05"].items():
+    for k in ks:
+        if k[0] == "B":
+            rd = [f for f in k[3] if f not in ("theta_m", "ru_save", "theta_m_save")]
+            wr = [f for f in k[4] if f != "X_F"]
+            pred = {"rk0": lambda t: t[1:] == (1, 0, 1, 0, 1), "rk1din": lambda t: t[1:] == (0, 0, 1, 1, 1),
+                    "rk1": lambda t: t[1:] == (0, 0, 1, 0, 1)}[lk]
+            _r06[lk].append(("B", "k_dyn_B", pred, rd, wr, ("E", E_EB + W_EDGE)))
+        elif k[0] == "E":
+            rd = [f for f in k[3] if f not in ("X_F", "ru:C")] + ["ru"] + ([] if lk == "rk0" else [])
+            pred = (lambda t: t[0] == 1 and t[2] == 1) if lk == "rk0" else (lambda t: t[0] == 0 and t[2] == 1)
+            _r06[lk].append(("E", "k_dyn_Et", pred, rd, k[4], ("C", ET_MESH_C, "E", ADV_EDGE + 8)))
+        else:
+            _r06[lk].append(k)
+LAYOUTS["r06"] = _r06
+SCRATCH = {"X_wc", "X_F"}
 
 
 def field_kind(name):
@@ -105,6 +134,8 @@ def field_kind(name):
 def parse_kernels(path):
     out, cur = {}, None
     for line in open(path):
+        if not line.strip():
+            continue
         if not line.startswith(" "):
             cur = line.strip()
             out[cur] = {}
@@ -114,95 +145,127 @@ def parse_kernels(path):
     return out
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("kernels")
-    ap.add_argument("--dims", type=int, nargs=4, default=[163842, 491520, 327680, 56])
-    ap.add_argument("--lp", type=int, default=64)
-    ap.add_argument("--layout", default="r03")
-    ap.add_argument("--json")
-    a = ap.parse_args()
-    nC, nE, nV, L = a.dims
-    n = {"C": nC, "E": nE, "V": nV}
-    col = lambda kind: 8.0 * n[kind] * a.lp  # noqa: E731
-    pmc = parse_kernels(a.kernels)
-    from mpasdyn import roofline
+class DecompError(Exception):
+    pass
 
+
+def decompose(pmc, layout, dims, lp=64):
+    """the decomposition of every launch kind of `layout` from the per-kernel counters `pmc`
+    ({kernel name: {counter: mean value}}, FETCH_SIZE / WRITE_SIZE in KB); raises DecompError on an
+    unmatched or missing kernel and on a negative refetch"""
+    from mpasdyn import roofline
+    nC, nE, nV, L = dims
+    n = {"C": nC, "E": nE, "V": nV}
+    lay = LAYOUTS[layout]
+
+    def col(f):
+        if f.endswith(":C"):
+            return 8.0 * nC * lp
+        return 8.0 * n[field_kind(f)] * lp
+
+    def fname(f):
+        return f.split(":")[0]
+
+    # every dyn_tend kernel of the file is claimed by exactly the kernels of the layout
+    claimed = {}
+    for name in pmc:
+        kern, t = targs(name)
+        if kern is None or not kern.startswith("k_dyn"):
+            continue
+        hits = [(lk, k[0]) for lk, ks in lay.items() for k in ks if k[1] == kern and k[2](t)]
+        if not hits:
+            raise DecompError(f"kernel {name} matches no kernel of layout {layout}")
+        claimed[name] = hits
     res = {}
-    kinds = ["rk0", "rk1"] + (["rk1din"] if a.layout == "r04" else [])
-    for lk in kinds:
-        kern = KERN[a.layout][lk]
+    for lk, ks in lay.items():
         per, tot_kernel, meas_tot = [], 0.0, 0.0
         task_r, task_w = set(), set()
-        for name, rd, wr in kern:
-            kind_mesh = MESH[name]
-            comp = sum(col(field_kind(f)) for f in set(rd)) + sum(col(field_kind(f)) for f in set(wr))
-            comp += kind_mesh[1] * n[kind_mesh[0]]
-            if name == "C":
-                comp += MESH["Cv"][1] * nV
-            task_r |= set(f for f in rd if f not in task_w)
-            task_w |= set(wr)
-            m = [v for kname, v in pmc.items() if re.search(PAT[(lk, name)], kname)]
-            # (every matching kernel summed: C is two launches, its vertex and its cell blocks)
+        for label, kern, pred, rd, wr, mesh in ks:
+            m = [v for name, v in pmc.items() if (lk, label) in claimed.get(name, ())]
             if not m:
-                meas = None
-            else:
-                meas = 1e3 * sum(2 * x["FETCH_SIZE"] + x["WRITE_SIZE"] for x in m)  # KB -> B; FETCH x 2 (gfx950)
+                raise DecompError(f"{lk} {label}: no {kern} kernel of layout {layout} in the counters")
+            comp = sum(col(f) for f in set(rd)) + sum(col(f) for f in set(wr))
+            for q in range(0, len(mesh), 2):
+                comp += mesh[q + 1] * n[mesh[q]]
+            if label == "C":
+                comp += (12 + 24 + 24 + 8) * nV  # the vertex blocks' rows
+            task_r |= set(fname(f) for f in rd if fname(f) not in task_w)
+            task_w |= set(wr)
+            meas = 1e3 * sum(2 * x["FETCH_SIZE"] + x["WRITE_SIZE"] for x in m)  # KB -> B; FETCH x 2 (gfx950)
             hit = None
-            if m and all("TCC_HIT_sum" in x for x in m):
+            if all("TCC_HIT_sum" in x for x in m):
                 h = sum(x["TCC_HIT_sum"] for x in m)
-                hit = h / (h + sum(x["TCC_MISS_sum"] for x in m))
-            per.append({"kernel": name, "compulsory_GB": comp / 1e9, "measured_GB": None if meas is None else meas / 1e9,
-                        "refetch_GB": None if meas is None else (meas - comp) / 1e9, "l2_hit": hit})
+                hit = h / max(h + sum(x["TCC_MISS_sum"] for x in m), 1.0)
+            if meas < comp:
+                raise DecompError(f"{lk} {label}: measured {meas / 1e9:.3f} GB below its distinct {comp / 1e9:.3f} GB "
+                                  f"(negative refetch: the layout's read / write set is wrong)")
+            per.append({"kernel": label, "names": sorted(nm for nm in claimed if (lk, label) in claimed[nm]),
+                        "compulsory_GB": comp / 1e9, "measured_GB": meas / 1e9, "refetch_GB": (meas - comp) / 1e9,
+                        "l2_hit": hit})
             tot_kernel += comp
-            meas_tot += meas or 0.0
-        scratch = {"X_wc", "X_F"}
-        task = sum(col(field_kind(f)) for f in task_r - scratch) + sum(col(field_kind(f)) for f in task_w - scratch)
-        task += sum(MESH[k[0]][1] * n[MESH[k[0]][0]] for k in kern)  # (mesh rows once per kernel: a floor)
+            meas_tot += meas
+        task = sum(col(f) for f in task_r - SCRATCH) + sum(col(f) for f in task_w - SCRATCH)
+        for k in ks:  # (mesh rows once per kernel: a floor)
+            for q in range(0, len(k[5]), 2):
+                task += k[5][q + 1] * n[k[5][q]]
         balg = roofline.b_alg("atm_compute_dyn_tend_work", (nC, nE, nV, L), rk_step=0 if lk == "rk0" else 1,
                               copy=(lk == "rk0"))
         res[lk] = {"kernels": per, "B_alg_GB": balg / 1e9, "compulsory_GB": task / 1e9,
                    "intermediates_GB": (tot_kernel - task) / 1e9, "refetch_GB": (meas_tot - tot_kernel) / 1e9,
                    "measured_GB": meas_tot / 1e9, "measured_over_B_alg": meas_tot / balg}
-    # per array: which kernel writes it, which read it, and the bytes it
-    # moves beyond its compulsory once -- each kernel touching it moves its stored size (the
-    # distinct bytes, no refetch); a scratch array (X_*) has no compulsory part
-    arrays = {}
-    for lk in kinds:
+        # per array: which kernel writes it, which read it, and the bytes it moves beyond its
+        # compulsory once (a scratch array X_* has no compulsory part)
         rows = {}
-        for name, rd, wr in KERN[a.layout][lk]:
+        for label, _, _, rd, wr, _ in ks:
             for f in dict.fromkeys(rd + wr):
-                r = rows.setdefault(f, {"writers": [], "readers": [], "GB": col(field_kind(f)) / 1e9})
+                r = rows.setdefault(fname(f), {"writers": [], "readers": [], "GB": col(fname(f)) / 1e9})
                 if f in wr:
-                    r["writers"].append(name)
+                    r["writers"].append(label)
                 if f in rd:
-                    r["readers"].append(name)
+                    r["readers"].append(label)
         for f, r in rows.items():
-            touches = len(set(r["writers"]) | set(r["readers"])) + sum(
-                1 for w in set(r["writers"]) if w in r["readers"])  # (read and written by one kernel: twice)
+            touches = len(set(r["writers"]) | set(r["readers"])) + sum(1 for w in set(r["writers"]) if w in r["readers"])
             r["extra_GB"] = r["GB"] * (touches - (0 if f.startswith("X_") else 1))
-        arrays[lk] = dict(sorted(((f, r) for f, r in rows.items() if r["extra_GB"] > 0),
-                                 key=lambda x: -x[1]["extra_GB"]))
-        res[lk]["arrays"] = arrays[lk]
-    print(f"dyn_tend traffic decomposition ({a.layout}), x1.{nC} x {L}, LP {a.lp}, GB per launch")
+        res[lk]["arrays"] = dict(sorted(((f, r) for f, r in rows.items() if r["extra_GB"] > 0),
+                                        key=lambda x: -x[1]["extra_GB"]))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("kernels")
+    ap.add_argument("--dims", type=int, nargs=4, default=[163842, 491520, 327680, 56])
+    ap.add_argument("--lp", type=int, default=64)
+    ap.add_argument("--layout", required=True, choices=sorted(LAYOUTS))
+    ap.add_argument("--round", default="", help="the round the counters were taken in (the header's label)")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    nC, nE, nV, L = a.dims
+    try:
+        res = decompose(parse_kernels(a.kernels), a.layout, a.dims, a.lp)
+    except DecompError as e:
+        print(f"traffic_decomp: {e}", file=sys.stderr)
+        return 2
+    rnd = f" {a.round}" if a.round else ""
+    print(f"dyn_tend traffic decomposition{rnd} (layout {a.layout}), x1.{nC} x {L}, LP {a.lp}, GB per launch")
     for lk, d in res.items():
         print(f"{lk:7s} measured {d['measured_GB']:6.2f} = compulsory {d['compulsory_GB']:5.2f} + intermediates "
               f"{d['intermediates_GB']:5.2f} + refetch {d['refetch_GB']:5.2f};  B_alg {d['B_alg_GB']:5.2f}, "
               f"measured / B_alg {d['measured_over_B_alg']:4.2f}")
         for k in d["kernels"]:
-            ms = "--" if k["measured_GB"] is None else f"{k['measured_GB']:5.2f}"
-            rf = "--" if k["refetch_GB"] is None else f"{k['refetch_GB']:5.2f}"
             l2 = "--" if k["l2_hit"] is None else f"{k['l2_hit']:.2f}"
-            print(f"    {k['kernel']}: measured {ms}  distinct {k['compulsory_GB']:5.2f}  refetch {rf}  L2 hit {l2}")
-    for lk, rows in arrays.items():
+            print(f"    {k['kernel']}: measured {k['measured_GB']:5.2f}  distinct {k['compulsory_GB']:5.2f}  "
+                  f"refetch {k['refetch_GB']:5.2f}  L2 hit {l2}  ({'; '.join(k['names'])})")
+    for lk, d in res.items():
         print(f"{lk}: arrays moved more than once (extra GB per launch beyond the compulsory once)")
-        for f, r in rows.items():
+        for f, r in d["arrays"].items():
             print(f"    {f:22s} {r['extra_GB']:5.3f}  written by {','.join(r['writers']) or '-':6s} "
                   f"read by {','.join(r['readers'])}")
-        print(f"    sum {sum(r['extra_GB'] for r in rows.values()):.2f}")
+        print(f"    sum {sum(r['extra_GB'] for r in d['arrays'].values()):.2f}")
     if a.json:
         json.dump(res, open(a.json, "w"), indent=1)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
