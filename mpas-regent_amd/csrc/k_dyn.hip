@@ -824,7 +824,8 @@ __global__ __launch_bounds__(256) void k_dyn_D(DevState S, DynK a) {
 // is formed here from LDS with B's expressions in B's order, instead of gathered from X_F
 struct EtTile {
     const double* lds;    // the closure's theta_m columns, then the zero column
-    const double* ldsw;   // per tile edge, per advCell j: B's weights ac + ac3, ac - ac3 (0, 0 past nAdv)
+    const double* ldsw;   // (exact) per tile edge, per advCell j: B's weights ac + ac3, ac - ac3 (0, 0 past nAdv);
+                          // (HF) per tile edge its flux H, one column (k_dyn_Et's edge phase)
     const unsigned* rec;  // the cell's ETT_REC-byte record (TrTiles::erow)
 };
 template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false>
@@ -868,7 +869,7 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     // (lanes k >= L: unmasked values, their sums are never used -- tend_theta takes tth where k < L)
     double tth = 0.0;
     double tru[NF], trus[NF], tt1[NF], tt2[NF];
-    if constexpr (TILE) {
+    if constexpr (TILE && !HF) {  // (HF: the tile's edge phase formed every edge's H)
         const double ts_own = SELF ? colk(tms_f, c) : 0.0;
 #pragma unroll
         for (int i = 0; i < NF; i += 2) {
@@ -953,7 +954,15 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
             dt2_[i] = ldz(kl && del4, dt2_[i]);
         }
     }
-    if constexpr (TILE) {
+    if constexpr (TILE && HF) {  // B's per-edge H, from the edge phase's LDS column of each edge
+        unsigned rw_[ETT_REC / 4];
+        row_ld(tl.rec, rw_);
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const int te = (int)((rw_[(i * ETT_EB) >> 2] >> (((i * ETT_EB) & 3) * 8)) & 0xffu);
+            tth = sub_if(i < ne, tth, eocs_[i] * tl.ldsw[te * LP + k]);
+        }
+    } else if constexpr (TILE) {
         // per edge: B's scalar weights (ac + sign ac3: the tile's LDS pair, picked per lane by the sign
         // of ru) times the advCells' columns from LDS, in B's order; the slots past nAdvCellsForEdge
         // add 0 * 0 (the zero column), which leaves the sum as B's masked add does (it is never -0)
@@ -1191,12 +1200,70 @@ __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk
 // column gathers per cell of B's flux become the tile's closure, ~4 columns per cell
 struct EtK {
     const int *tptr, *tcell, *cptr, *ccell, *teptr, *tedge;
-    const unsigned* erow;
+    const unsigned *erow, *terec;
     int maxclo;
 };
 constexpr int ET_THREADS = 512;
+
+// the fast path's edge phase: every edge of the tile gets B's H (k_dyn_B HF: ru F, + dvEdge (ru_save -
+// ru) theta_m_save at rk_step > 0) -- B's expressions in B's order on the same values, the advCells'
+// theta_m from the tile's LDS columns -- into its LDS column (level order; 0 from level L up, as X_F).
+// Two edges per wave at a time (their loads together)
+template <bool RK0>
+__device__ __forceinline__ void et_edges(const DevState& S, const DynK& a, const EtK& T, int eb, int nte,
+                                         const double* lds, double* ldsH, int w, int k) {
+    constexpr int LP = 64, NW = ET_THREADS / LP, U = 2;
+    const int L = S.L;
+    const bool kl = k < L;
+    const double *ru_f = fd(S, F_ru), *rus_f = fd(S, F_ru_save), *tms_f = fd(S, F_theta_m_save);
+    for (int q0 = w; q0 < nte; q0 += U * NW) {
+        int e[U];
+        double ru_e[U], rus_e[U], ts1[U], ts2[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int q = q0 + u * NW < nte ? q0 + u * NW : q0;
+            e[u] = ldc(T.tedge + eb + q);
+            if constexpr (RK0) {
+                ru_e[u] = colk(ru_f, e[u]);
+                rus_e[u] = ts1[u] = ts2[u] = 0.0;
+            } else {
+                const int c1 = ldc(fi(S, F_cellsOnEdge) + (size_t)e[u] * 2), c2 = ldc(fi(S, F_cellsOnEdge) + (size_t)e[u] * 2 + 1);
+                gather2<LP>(ru_f, e[u], rus_f, e[u], k, ru_e[u], rus_e[u]);
+                gather2s<LP>(tms_f, c1, c2, k, ts1[u], ts2[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int q = q0 + u * NW;
+            if (q >= nte) break;  // (wave-uniform)
+            unsigned r3[ETT_ER / 4];
+            row_ld(T.terec + (size_t)(eb + q) * (ETT_ER / 4), r3);
+            auto slot = [&](int j) { return (int)((r3[j >> 2] >> ((j & 3) * 8)) & 0xffu); };
+            const double *acr = fd(S, F_adv_coefs) + (size_t)e[u] * 15, *ac3r = fd(S, F_adv_coefs_3rd) + (size_t)e[u] * 15;
+            const int na = ldc(fi(S, F_nAdvCellsForEdge) + e[u]);
+            const double sg = copysign(1.0, ru_e[u]);
+            double flux_arr = 0.0;
+            if (na == AF) {  // (the usual list; past nAdv the zero column would add 0 * w)
+#pragma unroll
+                for (int j = 0; j < AF; j++)
+                    flux_arr = flux_arr + (ldc(acr + j) + sg * ldc(ac3r + j)) * lds[slot(j) * LP + k];
+            } else {
+#pragma unroll
+                for (int j = 0; j < AF; j++)
+                    flux_arr = add_if(j < na, flux_arr, (ldc(acr + j) + sg * ldc(ac3r + j)) * lds[slot(j) * LP + k]);
+            }
+            double h = ru_e[u] * flux_arr;
+            if constexpr (!RK0) {
+                const double rs = a.cp ? ru_e[u] : rus_e[u];  // (k_dyn_B's rule: the copy is setup's, ru_save = ru)
+                h += ldc(fd(S, F_dvEdge) + e[u]) * ((rs - ru_e[u]) * 0.5 * (ts2[u] + ts1[u]));
+            }
+            ldsH[q * LP + k] = kl ? h : 0.0;
+        }
+    }
+}
+
 template <bool RK0, bool SELF, bool HF>
-__global__ __launch_bounds__(ET_THREADS, 4) void k_dyn_Et(DevState S, DynK a, EtK T) {
+__global__ __launch_bounds__(ET_THREADS, HF && !RK0 ? 5 : 4) void k_dyn_Et(DevState S, DynK a, EtK T) {
     constexpr int LP = 64, NW = ET_THREADS / LP, U = 4;
     extern __shared__ double lds[];
     double* ldsw = lds + (size_t)(T.maxclo + 1) * LP;
@@ -1223,15 +1290,19 @@ __global__ __launch_bounds__(ET_THREADS, 4) void k_dyn_Et(DevState S, DynK a, Et
         }
     }
     if (w == NW - 1) lds[n * LP + k] = 0.0;
-    // B's scalar weights of the tile's edges (ac + s ac3 for s = +1, -1: exact in s, B's values)
     const int eb = ldc(T.teptr + tile), nte = ldc(T.teptr + tile + 1) - eb;
-    const double *acf = fd(S, F_adv_coefs), *ac3f = fd(S, F_adv_coefs_3rd);
-    for (int t = (int)threadIdx.x; t < nte * AF; t += ET_THREADS) {
-        const int q = t / AF, j = t - q * AF;
-        const int e = T.tedge[eb + q];
-        const bool on = j < fi(S, F_nAdvCellsForEdge)[e];
-        const double ac = acf[(size_t)e * 15 + j], ac3 = ac3f[(size_t)e * 15 + j];
-        *(double2*)(ldsw + 2 * t) = on ? make_double2(ac + 1.0 * ac3, ac + -1.0 * ac3) : make_double2(0.0, 0.0);
+    if constexpr (HF) {
+        __syncthreads();
+        et_edges<RK0>(S, a, T, eb, nte, lds, ldsw, w, k);
+    } else {  // B's scalar weights of the tile's edges (ac + s ac3 for s = +1, -1: exact in s, B's values)
+        const double *acf = fd(S, F_adv_coefs), *ac3f = fd(S, F_adv_coefs_3rd);
+        for (int t = (int)threadIdx.x; t < nte * AF; t += ET_THREADS) {
+            const int q = t / AF, j = t - q * AF;
+            const int e = T.tedge[eb + q];
+            const bool on = j < fi(S, F_nAdvCellsForEdge)[e];
+            const double ac = acf[(size_t)e * 15 + j], ac3 = ac3f[(size_t)e * 15 + j];
+            *(double2*)(ldsw + 2 * t) = on ? make_double2(ac + 1.0 * ac3, ac + -1.0 * ac3) : make_double2(0.0, 0.0);
+        }
     }
     __syncthreads();
     const int tb = ldc(T.tptr + tile), nt = ldc(T.tptr + tile + 1) - tb;
@@ -1355,8 +1426,9 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         if constexpr (LP == 64 && !MD) {
             if (et) {  // (tiles only undecomposed: X is the whole owned range)
                 const TrTiles& TT = *X.ett;
-                const EtK T{TT.tptr, TT.tcell, TT.cptr, TT.ccell, TT.teptr, TT.tedge, TT.erow, TT.maxclo};
-                const size_t shm = ((size_t)(TT.maxclo + 1) * LP + (size_t)TT.maxte * 2 * AF) * sizeof(double);
+                const EtK T{TT.tptr, TT.tcell, TT.cptr, TT.ccell, TT.teptr, TT.tedge, TT.erow, TT.terec, TT.maxclo};
+                // (the closure and its zero column; then per tile edge its H column, or in exact mode B's weights)
+                const size_t shm = ((size_t)(TT.maxclo + 1) * LP + (size_t)TT.maxte * (hf ? LP : 2 * AF)) * sizeof(double);
                 auto go = [&](auto hfc, auto rkc) {
                     constexpr bool H = decltype(hfc)::value, R = decltype(rkc)::value;
                     if (X.selfc) k_dyn_Et<R, true, H><<<TT.ntiles, ET_THREADS, shm, st>>>(X, a, T);

@@ -179,7 +179,7 @@ struct mpas_ctx {
     // kernel then forms no flux and the per-edge scratch X_F goes (reference semantics, LP = 64,
     // undecomposed; the same bits either way).  Options "etcells" / "etclo": tile size limits
     int etile = 0;
-    int ett_cells = 8, ett_clo = 96;
+    int ett_cells = 8, ett_clo = 56;
     bool ett_dirty = true;
     TrTiles ett;
 };
@@ -628,13 +628,13 @@ void tre_build(mpas_ctx* c) {
 
 void tiles_free(TrTiles& T) {
     for (void* p : {(void*)T.tptr, (void*)T.tcell, (void*)T.cptr, (void*)T.ccell, (void*)T.slot, (void*)T.teptr,
-                    (void*)T.tedge, (void*)T.erow})
+                    (void*)T.tedge, (void*)T.erow, (void*)T.terec})
         if (p) (void)hipFree(p);
     T = TrTiles{};
 }
 // the tiles (into T) of at most `cells` owned cells whose closure fits `clo_max` LDS columns;
 // false (T empty) when the mesh does not allow them
-bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max);
+bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max, int te_max = 1 << 30);
 
 void trt_build(mpas_ctx* c) {
     trt_free(c);
@@ -656,13 +656,14 @@ void ett_build(mpas_ctx* c) {
     ett_free(c);
     c->ett_dirty = false;
     if (!c->etile || c->halo || c->S.LP != 64 || c->S.physics == 2) return;
-    if (tiles_build(c, c->ett, c->ett_cells, c->ett_clo)) c->S.ett = &c->ett;
+    // (at most 96 edges per tile: the LDS of a block, (closure + 1 + edges) columns, stays < 160 KiB)
+    if (tiles_build(c, c->ett, c->ett_cells, c->ett_clo, 96)) c->S.ett = &c->ett;
 }
 void ett_ensure(mpas_ctx* c) {
     if (c->ett_dirty) ett_build(c);
 }
 
-bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max) {
+bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max, int te_max) {
     hipcheck(hipSetDevice(c->device), "hipSetDevice");
     const DevState& S = c->S;
     const int nC = S.nCells, nE = S.nEdges, nCO = S.nCO;
@@ -693,8 +694,8 @@ bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max) {
     std::vector<int> tptr{0}, tcell, cptr{0}, ccell, queue, cells, clo;
     std::vector<int> slot;
     int stamp = 0, maxclo = 0, nt_int = 0;
-    std::vector<int> emark((size_t)nE + 1, -1), tedge, teptr{0};
-    std::vector<unsigned> erow;
+    std::vector<int> emark((size_t)nE + 1, -1), tmark((size_t)nE + 1, -1), tedge, teptr{0};
+    std::vector<unsigned> erow, terec;
     int tebase = 0, maxte = 0;
     // launch classes: 0 = interior cells whose every column is owned (or the zero slot),
     // run beside a halo exchange; 1 = the rest (boundary cells, and interior cells that
@@ -715,14 +716,20 @@ bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max) {
             clo.clear();
             queue.assign(1, seed);
             inq[seed] = tid;
+            int nte = 0;  // the tile's edges so far (tmark: the tile id of an edge's last use)
             for (size_t qh = 0; qh < queue.size() && (int)cells.size() < max_cells; qh++) {
                 const int x = queue[qh];
-                int add = 0;
+                int add = 0, adde = 0;
                 stamp++;
                 need(x, [&](int y) {
                     if (mark[y] < 0 && seen[y] != stamp) seen[y] = stamp, add++;
                 });
-                if (!cells.empty() && (int)clo.size() + add > clo_max) continue;
+                for (int i = 0; i < nedges(x); i++) adde += tmark[eoc[(size_t)x * 10 + i]] != tid;
+                if (!cells.empty() && ((int)clo.size() + add > clo_max || nte + adde > te_max)) continue;
+                for (int i = 0; i < nedges(x); i++) {
+                    const int e = eoc[(size_t)x * 10 + i];
+                    if (tmark[e] != tid) tmark[e] = tid, nte++;
+                }
                 cells.push_back(x);
                 assigned[x] = 1;
                 need(x, [&](int y) {
@@ -745,7 +752,14 @@ bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max) {
                     for (int j = 0; j < AF; j++) ri[1 + j] = (unsigned char)zero;
                     if (i >= nedges(x)) continue;
                     const int e = eoc[(size_t)x * 10 + i];
-                    if (emark[e] < 0) emark[e] = (int)tedge.size() - tebase, tedge.push_back(e);
+                    if (emark[e] < 0) {
+                        emark[e] = (int)tedge.size() - tebase;
+                        tedge.push_back(e);
+                        unsigned char er[ETT_ER] = {};  // the edge's advCells' closure columns (zero column past nAdv)
+                        for (int j = 0; j < AF; j++) er[j] = (unsigned char)(j < nadv[e] ? mark[adv[(size_t)e * 15 + j]] : zero);
+                        const unsigned* ew = (const unsigned*)er;
+                        terec.insert(terec.end(), ew, ew + ETT_ER / 4);
+                    }
                     ri[0] = (unsigned char)emark[e];
                     for (int j = 0; j < nadv[e]; j++) ri[1 + j] = (unsigned char)mark[adv[(size_t)e * 15 + j]];
                 }
@@ -790,6 +804,7 @@ bool tiles_build(mpas_ctx* c, TrTiles& T, int max_cells, int clo_max) {
     T.teptr = dev_copy(teptr);
     T.tedge = dev_copy(tedge);
     T.erow = dev_copy(erow);
+    T.terec = dev_copy(terec);
     T.maxte = maxte;
     return true;
 }
@@ -1407,7 +1422,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
             c->ett_cells = (int)value;
             c->ett_dirty = true;
         } else if (name && std::strcmp(name, "etclo") == 0) {
-            if (value < 1 + NF * (2 + AF) || value > 160) throw Fail{MPAS_EINVAL, "etclo must be 67..160 (LDS columns)"};
+            if (value < 20 || value > 160) throw Fail{MPAS_EINVAL, "etclo must be 20..160 (LDS columns)"};
             c->ett_clo = (int)value;
             c->ett_dirty = true;
         } else if (name && std::strcmp(name, "transport") == 0) {

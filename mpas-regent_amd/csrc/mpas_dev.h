@@ -431,10 +431,12 @@ struct TrTiles {
                                   // edge's index among the tile's edges, then its AF advCells' closure
                                   // columns (the zero column, index = closure size, past nAdvCellsForEdge
                                   // and for slots past nEdgesOnCell)
+    unsigned* terec = nullptr;    // per tile edge (tedge order) ETT_ER bytes: its AF advCells' closure columns
     int maxte = 0;                // most edges of a tile
 };
 constexpr int ETT_EB = 12;            // record bytes per edge slot (1 + AF, padded)
 constexpr int ETT_REC = NF * ETT_EB;  // 72: 18 dwords per tile cell
+constexpr int ETT_ER = 12;            // record bytes per tile edge (AF, padded)
 
 // The transport's edge kernel with its scalars_old columns staged in LDS (k_tr_edge_lds,
 // option "tredge"): the owned edges in groups of TRE_GE consecutive ids (Morton-adjacent);

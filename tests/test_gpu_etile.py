@@ -63,7 +63,7 @@ def test_etile_dyn_tend_task(x1_2562, rk_step, exact):
         assert not bad, bad[:6]
 
 
-@pytest.mark.parametrize("cells,clo", [(1, 67), (4, 80), (16, 96), (40, 160)])
+@pytest.mark.parametrize("cells,clo", [(1, 20), (4, 40), (8, 56), (16, 96), (40, 160)])
 def test_etile_tile_sizes(x1_2562, cells, clo):
     """any tile size limit gives the same bits (one cell per tile up to the largest closure)"""
     st = make_state(x1_2562, 56, "physical")
