@@ -828,7 +828,11 @@ struct EtTile {
                           // (HF) per tile edge its flux H, one column (k_dyn_Et's edge phase)
     const unsigned* rec;  // the cell's ETT_REC-byte record (TrTiles::erow)
 };
-template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false>
+// ETM (TILE): 0 each edge's flux formed per cell (the cell's gathers of ru, ru_save and the
+// theta_m_save pairs issued with its own columns: one memory round trip), 1 the same with the flux
+// sum formed before the own columns are loaded (fewer registers, two round trips), 2 (HF) the
+// tile's edge phase formed every edge's H (k_dyn_Et et_edges)
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false, int ETM = 0>
 __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int c, int k, EtTile tl = {}) {
     static_assert(!TILE || (LP == 64 && !MD), "the tiled E: LP = 64, reference semantics");
     const int L = S.L;
@@ -869,7 +873,8 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     // (lanes k >= L: unmasked values, their sums are never used -- tend_theta takes tth where k < L)
     double tth = 0.0;
     double tru[NF], trus[NF], tt1[NF], tt2[NF];
-    if constexpr (TILE && !HF) {  // (HF: the tile's edge phase formed every edge's H)
+    constexpr bool EPH = HF && ETM == 2;  // (the edge phase formed every edge's H)
+    if constexpr (TILE && !EPH) {
         const double ts_own = SELF ? colk(tms_f, c) : 0.0;
 #pragma unroll
         for (int i = 0; i < NF; i += 2) {
@@ -880,6 +885,44 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
             }
         }
     }
+    auto tile_flux = [&]() {
+        // per edge: B's scalar weights (ac + sign ac3: the tile's LDS pair, picked per lane by the sign
+        // of ru) times the advCells' columns from LDS, in B's order; the slots past nAdvCellsForEdge
+        // add 0 * 0 (the zero column), which leaves the sum as B's masked add does (it is never -0)
+        unsigned rw_[ETT_REC / 4];
+        row_ld(tl.rec, rw_);
+        auto byte_at = [&](int b) { return (int)((rw_[b >> 2] >> ((b & 3) * 8)) & 0xffu); };
+#pragma unroll
+        for (int i = 0; i < NF; i++) {
+            const bool pos = copysign(1.0, tru[i]) > 0.0;
+            const double* wr = tl.ldsw + byte_at(i * ETT_EB) * (2 * AF) + (pos ? 0 : 1);
+            double flux_arr = 0.0;
+#pragma unroll
+            for (int j = 0; j < AF; j++) flux_arr = flux_arr + wr[2 * j] * tl.lds[byte_at(i * ETT_EB + 1 + j) * LP + k];
+            if constexpr (HF) {  // B's H: ru F (+ dvEdge (ru_save - ru) theta_m_save at the edge, rk > 0)
+                double h = tru[i] * flux_arr;
+                if constexpr (!RK0) {
+                    const double rus_e = a.cp ? tru[i] : trus[i];
+                    h += cdv_[i] * ((rus_e - tru[i]) * 0.5 * (tt2[i] + tt1[i]));
+                }
+                tth = sub_if(i < ne, tth, eocs_[i] * (kl ? h : 0.0));
+            } else {
+                tth = sub_if(i < ne, tth, eocs_[i] * tru[i] * (kl ? flux_arr : 0.0));
+            }
+            // one edge at a time (the asm ties tth to this point): the scheduler would otherwise hoist
+            // all 54 LDS reads of the cell and spill
+            asm volatile("" : "+v"(tth));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (!HF && !RK0) {  // :1347-1360
+#pragma unroll
+            for (int i = 0; i < NF; i++) {
+                double flux = eocs_[i] * cdv_[i] * (trus[i] - tru[i]) * 0.5 * (tt2[i] + tt1[i]);
+                tth = sub_if(i < ne, tth, flux);
+            }
+        }
+    };
+    if constexpr (TILE && !EPH && ETM == 1) tile_flux();
     // own columns (gather2: two columns per load instruction; the theta-section loads
     // too, ahead of the w stores that could alias them for the compiler)
     double wc, rw, pp, dpdz, rws, tms, tmv, twe, tte, rho_zz, rt_diab, trp, cqw = 0.0, dw_c = 0.0, dt_c = 0.0;
@@ -954,7 +997,7 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
             dt2_[i] = ldz(kl && del4, dt2_[i]);
         }
     }
-    if constexpr (TILE && HF) {  // B's per-edge H, from the edge phase's LDS column of each edge
+    if constexpr (TILE && EPH) {  // B's per-edge H, from the edge phase's LDS column of each edge
         unsigned rw_[ETT_REC / 4];
         row_ld(tl.rec, rw_);
 #pragma unroll
@@ -963,41 +1006,7 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
             tth = sub_if(i < ne, tth, eocs_[i] * tl.ldsw[te * LP + k]);
         }
     } else if constexpr (TILE) {
-        // per edge: B's scalar weights (ac + sign ac3: the tile's LDS pair, picked per lane by the sign
-        // of ru) times the advCells' columns from LDS, in B's order; the slots past nAdvCellsForEdge
-        // add 0 * 0 (the zero column), which leaves the sum as B's masked add does (it is never -0)
-        unsigned rw_[ETT_REC / 4];
-        row_ld(tl.rec, rw_);
-        auto byte_at = [&](int b) { return (int)((rw_[b >> 2] >> ((b & 3) * 8)) & 0xffu); };
-#pragma unroll
-        for (int i = 0; i < NF; i++) {
-            const bool pos = copysign(1.0, tru[i]) > 0.0;
-            const double* wr = tl.ldsw + byte_at(i * ETT_EB) * (2 * AF) + (pos ? 0 : 1);
-            double flux_arr = 0.0;
-#pragma unroll
-            for (int j = 0; j < AF; j++) flux_arr = flux_arr + wr[2 * j] * tl.lds[byte_at(i * ETT_EB + 1 + j) * LP + k];
-            if constexpr (HF) {  // B's H: ru F (+ dvEdge (ru_save - ru) theta_m_save at the edge, rk > 0)
-                double h = tru[i] * flux_arr;
-                if constexpr (!RK0) {
-                    const double rus_e = a.cp ? tru[i] : trus[i];
-                    h += cdv_[i] * ((rus_e - tru[i]) * 0.5 * (tt2[i] + tt1[i]));
-                }
-                tth = sub_if(i < ne, tth, eocs_[i] * (kl ? h : 0.0));
-            } else {
-                tth = sub_if(i < ne, tth, eocs_[i] * tru[i] * (kl ? flux_arr : 0.0));
-            }
-            // one edge at a time (the asm ties tth to this point): the scheduler would otherwise hoist
-            // all 54 LDS reads of the cell and spill
-            asm volatile("" : "+v"(tth));
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if constexpr (!HF && !RK0) {  // :1347-1360
-#pragma unroll
-            for (int i = 0; i < NF; i++) {
-                double flux = eocs_[i] * cdv_[i] * (trus[i] - tru[i]) * 0.5 * (tt2[i] + tt1[i]);
-                tth = sub_if(i < ne, tth, flux);
-            }
-        }
+        if constexpr (ETM == 0) tile_flux();
     }
     if constexpr (WCE) {  // dyn_A's w section (:1170-1218, Q13), the same operands in the same order
         const double ru_lm = lvl_dn<LP>(ru_l, k);
@@ -1203,16 +1212,15 @@ struct EtK {
     const unsigned *erow, *terec;
     int maxclo;
 };
-constexpr int ET_THREADS = 512;
 
 // the fast path's edge phase: every edge of the tile gets B's H (k_dyn_B HF: ru F, + dvEdge (ru_save -
 // ru) theta_m_save at rk_step > 0) -- B's expressions in B's order on the same values, the advCells'
 // theta_m from the tile's LDS columns -- into its LDS column (level order; 0 from level L up, as X_F).
 // Two edges per wave at a time (their loads together)
-template <bool RK0>
+template <bool RK0, int NT>
 __device__ __forceinline__ void et_edges(const DevState& S, const DynK& a, const EtK& T, int eb, int nte,
                                          const double* lds, double* ldsH, int w, int k) {
-    constexpr int LP = 64, NW = ET_THREADS / LP, U = 2;
+    constexpr int LP = 64, NW = NT / LP, U = 2;
     const int L = S.L;
     const bool kl = k < L;
     const double *ru_f = fd(S, F_ru), *rus_f = fd(S, F_ru_save), *tms_f = fd(S, F_theta_m_save);
@@ -1262,9 +1270,10 @@ __device__ __forceinline__ void et_edges(const DevState& S, const DynK& a, const
     }
 }
 
-template <bool RK0, bool SELF, bool HF>
-__global__ __launch_bounds__(ET_THREADS, HF && !RK0 ? 5 : 4) void k_dyn_Et(DevState S, DynK a, EtK T) {
-    constexpr int LP = 64, NW = ET_THREADS / LP, U = 4;
+template <bool RK0, bool SELF, bool HF, int ETM, int NT>
+__global__ __launch_bounds__(NT, ETM == 2 && !RK0 ? 5 : 4) void k_dyn_Et(DevState S, DynK a, EtK T) {
+    constexpr int LP = 64, NW = NT / LP, U = 4;
+    constexpr bool EPH = HF && ETM == 2;
     extern __shared__ double lds[];
     double* ldsw = lds + (size_t)(T.maxclo + 1) * LP;
     const int tile = xcd_block(S.xcd);
@@ -1291,12 +1300,12 @@ __global__ __launch_bounds__(ET_THREADS, HF && !RK0 ? 5 : 4) void k_dyn_Et(DevSt
     }
     if (w == NW - 1) lds[n * LP + k] = 0.0;
     const int eb = ldc(T.teptr + tile), nte = ldc(T.teptr + tile + 1) - eb;
-    if constexpr (HF) {
+    if constexpr (EPH) {
         __syncthreads();
-        et_edges<RK0>(S, a, T, eb, nte, lds, ldsw, w, k);
+        et_edges<RK0, NT>(S, a, T, eb, nte, lds, ldsw, w, k);
     } else {  // B's scalar weights of the tile's edges (ac + s ac3 for s = +1, -1: exact in s, B's values)
         const double *acf = fd(S, F_adv_coefs), *ac3f = fd(S, F_adv_coefs_3rd);
-        for (int t = (int)threadIdx.x; t < nte * AF; t += ET_THREADS) {
+        for (int t = (int)threadIdx.x; t < nte * AF; t += NT) {
             const int q = t / AF, j = t - q * AF;
             const int e = T.tedge[eb + q];
             const bool on = j < fi(S, F_nAdvCellsForEdge)[e];
@@ -1308,7 +1317,7 @@ __global__ __launch_bounds__(ET_THREADS, HF && !RK0 ? 5 : 4) void k_dyn_Et(DevSt
     const int tb = ldc(T.tptr + tile), nt = ldc(T.tptr + tile + 1) - tb;
     for (int q = w; q < nt; q += NW) {
         const int c = ldc(T.tcell + tb + q);
-        dyn_E_cell<LP, RK0, SELF, false, HF, true>(S, a, c, k, EtTile{lds, ldsw, T.erow + (size_t)(tb + q) * (ETT_REC / 4)});
+        dyn_E_cell<LP, RK0, SELF, false, HF, true, ETM>(S, a, c, k, EtTile{lds, ldsw, T.erow + (size_t)(tb + q) * (ETT_REC / 4)});
     }
 }
 
@@ -1428,16 +1437,31 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 const TrTiles& TT = *X.ett;
                 const EtK T{TT.tptr, TT.tcell, TT.cptr, TT.ccell, TT.teptr, TT.tedge, TT.erow, TT.terec, TT.maxclo};
                 // (the closure and its zero column; then per tile edge its H column, or in exact mode B's weights)
-                const size_t shm = ((size_t)(TT.maxclo + 1) * LP + (size_t)TT.maxte * (hf ? LP : 2 * AF)) * sizeof(double);
-                auto go = [&](auto hfc, auto rkc) {
+                const int etm = hf ? X.etm : 0, nt = hf ? X.etnt : 512;
+                const size_t shm = ((size_t)(TT.maxclo + 1) * LP + (size_t)TT.maxte * (hf && etm == 2 ? LP : 2 * AF)) * sizeof(double);
+                auto go = [&](auto hfc, auto rkc, auto mc, auto ntc) {
                     constexpr bool H = decltype(hfc)::value, R = decltype(rkc)::value;
-                    if (X.selfc) k_dyn_Et<R, true, H><<<TT.ntiles, ET_THREADS, shm, st>>>(X, a, T);
-                    else k_dyn_Et<R, false, H><<<TT.ntiles, ET_THREADS, shm, st>>>(X, a, T);
+                    constexpr int M = decltype(mc)::value, N = decltype(ntc)::value;
+                    if (X.selfc) k_dyn_Et<R, true, H, M, N><<<TT.ntiles, N, shm, st>>>(X, a, T);
+                    else k_dyn_Et<R, false, H, M, N><<<TT.ntiles, N, shm, st>>>(X, a, T);
                 };
-                if (hf && rk0) go(std::true_type{}, std::true_type{});
-                else if (hf) go(std::true_type{}, std::false_type{});
-                else if (rk0) go(std::false_type{}, std::true_type{});
-                else go(std::false_type{}, std::false_type{});
+                using I0 = std::integral_constant<int, 0>;
+                using I1 = std::integral_constant<int, 1>;
+                using I2 = std::integral_constant<int, 2>;
+                using N256 = std::integral_constant<int, 256>;
+                using N512 = std::integral_constant<int, 512>;
+                auto goh = [&](auto rkc) {
+                    if (etm == 2 && nt == 256) go(std::true_type{}, rkc, I2{}, N256{});
+                    else if (etm == 2) go(std::true_type{}, rkc, I2{}, N512{});
+                    else if (etm == 1 && nt == 256) go(std::true_type{}, rkc, I1{}, N256{});
+                    else if (etm == 1) go(std::true_type{}, rkc, I1{}, N512{});
+                    else if (nt == 256) go(std::true_type{}, rkc, I0{}, N256{});
+                    else go(std::true_type{}, rkc, I0{}, N512{});
+                };
+                if (hf && rk0) goh(std::true_type{});
+                else if (hf) goh(std::false_type{});
+                else if (rk0) go(std::false_type{}, std::true_type{}, I0{}, N512{});
+                else go(std::false_type{}, std::false_type{}, I0{}, N512{});
                 return;
             }
         }

@@ -1267,6 +1267,8 @@ int mpas_ctx_create(mpas_ctx** out, int device, const mpas_dims* dims) {
         c->S.trepw = 1;
         c->S.tro = 64;  // transport: pair-major within runs of 64 entities (profiles/r03/transport_v5: -1 to -3 %)
         c->S.bsplit = 2;  // dyn_tend's flux kernel split off under the MPAS dynamics (profiles/r05/bsplit)
+        c->S.etm = 1;  // (the tiled E's best form: profiles/r06/etile)
+        c->S.etnt = 256;
         hipcheck(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
         // Field f starts (f % 16) * stagger bytes into its allocation (env MPAS_ALLOC_STAGGER,
         // a multiple of 512: whole columns stay aligned; default 2048): equal-sized arrays
@@ -1417,6 +1419,12 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "etile") == 0) {
             c->etile = value ? 1 : 0;
             c->ett_dirty = true;
+        } else if (name && std::strcmp(name, "etmode") == 0) {
+            if (value < 0 || value > 2) throw Fail{MPAS_EINVAL, "etmode must be 0, 1 or 2"};
+            c->S.etm = (int)value;
+        } else if (name && std::strcmp(name, "etthreads") == 0) {
+            if (value != 256 && value != 512) throw Fail{MPAS_EINVAL, "etthreads must be 256 or 512"};
+            c->S.etnt = (int)value;
         } else if (name && std::strcmp(name, "etcells") == 0) {
             if (value < 1 || value > 40) throw Fail{MPAS_EINVAL, "etcells must be 1..40 (a tile's edges index in one byte)"};
             c->ett_cells = (int)value;
@@ -1483,6 +1491,8 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         }
         else if (name && std::strcmp(name, "etile") == 0) *value = c->etile;
         else if (name && std::strcmp(name, "etcells") == 0) *value = c->ett_cells;
+        else if (name && std::strcmp(name, "etmode") == 0) *value = c->S.etm;
+        else if (name && std::strcmp(name, "etthreads") == 0) *value = c->S.etnt;
         else if (name && std::strcmp(name, "etclo") == 0) *value = c->ett_clo;
         else if (name && std::strcmp(name, "etile_active") == 0) {  // dyn_tend tiles built for this mesh
             ett_ensure(c);

@@ -157,6 +157,8 @@ struct DevState {
     const TrTiles* trt;  // host-side: the tiles of the tiled transport, nullptr = the three-kernel path
     const TrEdgeGroups* tre;  // host-side: the edge groups of k_tr_edge_lds, nullptr = k_tr_edge
     const TrTiles* ett;  // host-side: the cell tiles of dyn_tend's tiled E (k_dyn_Et), nullptr = k_dyn_E
+    int etm, etnt;       // options "etmode" (the tiled E's flux form, k_dyn.hip dyn_E_cell ETM) and
+                         // "etthreads" (its block size, 256 or 512)
     const int* gid[3];  // device global ids of the local cells/edges/vertices (decomposed
                         // meshes: the synthetic fill hashes them), nullptr = identity
 };
