@@ -393,6 +393,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
             kw["copy"] = True
         if "+d4o" in tag:
             kw["defer_out"] = True
+        if "+ntu" in tag:
+            kw["ntu"] = True
         if "+v" in tag:
             kw["store_v"] = True
         if tag.endswith("-A"):
@@ -671,8 +673,9 @@ def main():
     fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
     fcopy = fsetup and bool(ctx.get_option("fusecopy"))  # (decomposed and MPAS forms too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
+    ntu = d4 and bool(ctx.get_option("ntu"))
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
-                                 smls)
+                                 smls, ntu)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -696,7 +699,7 @@ def main():
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy), "smlsum": int(smls),
-                      "fusesml": int(fsml), "defer4": int(d4), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
+                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}

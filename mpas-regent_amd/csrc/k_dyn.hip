@@ -224,8 +224,16 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // NOF (option "bsplit", fast path): the per-edge theta flux H (and the MD w flux) are left to
 // k_dyn_Bf, an edge kernel of their own: this one skips the advCells gathers.  Also (option
 // "etile", either path) when the tiled E forms each edge's flux itself: no X_F at all
-template <int LP, bool RK0, bool MD, bool HF, bool DIN = false, bool NOF = false>
+// NTU (atm_srk3, reference semantics, rk_step 0 with defer4 out): the call's tend_u is dead -- the next
+// stage's B rewrites it and no task in between reads it (set_smlstep reads u_tend, Q2; the acoustic
+// step ru_p, Q18) -- so, as D's tend_u there, it is not formed at all: no wduz, q, ke gradient,
+// curvature or Rayleigh term, none of their gathers (u and pv_edge over edgesOnEdge, rw, w, ke,
+// h_divergence at the cells, tend_ru_physics).  The kernel keeps what later kernels read:
+// tend_u_euler (the pressure gradient and del2, :964-970, :1030-1048), delsq_u, the theta flux,
+// setup's copies
+template <int LP, bool RK0, bool MD, bool HF, bool DIN = false, bool NOF = false, bool NTU = false>
 __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) {
+    static_assert(!NTU || (RK0 && !MD && !DIN), "the dead tend_u: reference semantics, rk_step 0");
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -243,16 +251,17 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     // ---- issue every independent load of the column first (gather2: two columns per load
     // instruction; the raw halves, swapped after the scheduling barrier below)
     double u, ru_e, rw1, rw2, w1, w2, rho_edge, pv;
+    const double2 z2 = make_double2(0.0, 0.0);
     const double2 g_uru = gather2_ld<LP>(u_f, e, fd(S, F_ru), e, k);
-    const double2 g_rw = gather2s_ld<LP>(fd(S, F_rw), cell1, cell2, k);
-    const double2 g_w = gather2s_ld<LP>(fd(S, F_w), cell1, cell2, k);
-    const double2 g_rp = gather2_ld<LP>(fd(S, F_rho_edge), e, pv_f, e, k);
+    const double2 g_rw = NTU ? z2 : gather2s_ld<LP>(fd(S, F_rw), cell1, cell2, k);
+    const double2 g_w = NTU ? z2 : gather2s_ld<LP>(fd(S, F_w), cell1, cell2, k);
+    const double2 g_rp = NTU ? make_double2(colk(fd(S, F_rho_edge), e), 0.0) : gather2_ld<LP>(fd(S, F_rho_edge), e, pv_f, e, k);
     // No level masks (ldz) in this kernel: lanes k >= L store nothing (k > L: PADW
     // zeros), so a value used in its own lane needs none, and the vertical shuffles
     // (lvl_up/dn) of u and w bring lanes k <= L only levels <= L -- exactly what the
     // masks kept.  (Each ldz is two v_cndmask per double; B was half VALU-bound.)
     // one value: the level-L slot (MD: MPAS-A's wduz(nVertLevels+1) = 0)
-    const double wduzL = MD ? 0.0 : fd(S, F_wduz)[(size_t)e * LP + lpos(LP, L)];
+    const double wduzL = (MD || NTU) ? 0.0 : fd(S, F_wduz)[(size_t)e * LP + lpos(LP, L)];
     const int neoe = rec[21];
     const int* eoe = fi(S, F_edgesOnEdge) + (size_t)e * 20;
     const double* woe = fd(S, F_weightsOnEdge) + (size_t)e * 20;
@@ -265,8 +274,8 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     double2 g_ue[QF / 2], g_pve[QF / 2];
 #pragma unroll
     for (int j = 0; j < QF; j += 2) {
-        g_ue[j / 2] = gather2s_ld<LP>(u_f, ee_[j], ee_[j + 1], k);
-        g_pve[j / 2] = gather2s_ld<LP>(pv_f, ee_[j], ee_[j + 1], k);
+        g_ue[j / 2] = NTU ? z2 : gather2s_ld<LP>(u_f, ee_[j], ee_[j + 1], k);
+        g_pve[j / 2] = NTU ? z2 : gather2s_ld<LP>(pv_f, ee_[j], ee_[j + 1], k);
     }
     // theta reconstruction at this edge (:1333-1340), consumed by E
     const int na = rec[22];
@@ -286,7 +295,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     if constexpr (!NOF) {
 #pragma unroll
         for (int j = 0; j < AF - 1; j += 2) g_tv[j / 2] = gather2s_ld<LP>(tm_f, ad_[j], ad_[j + 1], k);
-        g_tvl = gather2_ld<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k);
+        g_tvl = NTU ? make_double2(colk(tm_f, ad_[AF - 1]), 0.0) : gather2_ld<LP>(tm_f, ad_[AF - 1], fd(S, F_tend_ru_physics), e, k);
     }
 
     // MD: the state w at the advCells, for the w reconstruction flux_arr of this edge
@@ -302,8 +311,8 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     // for the compiler, which would then issue them only after it)
     const double *ke_f = fd(S, F_ke), *hd_f = fd(S, F_h_divergence);
     double ke1, ke2, hd1, hd2;
-    const double2 g_ke = gather2s_ld<LP>(ke_f, cell1, cell2, k);
-    const double2 g_hd = gather2s_ld<LP>(hd_f, cell1, cell2, k);
+    const double2 g_ke = NTU ? z2 : gather2s_ld<LP>(ke_f, cell1, cell2, k);
+    const double2 g_hd = NTU ? z2 : gather2s_ld<LP>(hd_f, cell1, cell2, k);
     // (the rk0-only loads stay in their section: hoisted they cost more in occupancy,
     // 138 VGPRs, than the second memory round trip)
     // HF (fast path): E's per-edge theta flux H formed here (rk > 0: with the
@@ -324,32 +333,60 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         g_dd = gather2s_ld<LP>(fd(S, F_delsq_divergence), cell1, cell2, k);
         g_dv = gather2s_ld<LP>(fd(S, F_delsq_vorticity), vertex1, vertex2, k);
     }
+    // NTU: the rk0 section's loads join the first batch (the tend_u loads they replace freed the registers)
+    double2 g0[7];
+    if constexpr (NTU) {
+        const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
+        g0[0] = gather2_ld<LP>(fd(S, F_cqu), e, fd(S, F_zxu), e, k);
+        g0[1] = gather2s_ld<LP>(fd(S, F_pressure_p), cell1, cell2, k);
+        g0[2] = gather2s_ld<LP>(fd(S, F_zz), cell1, cell2, k);
+        g0[3] = gather2s_ld<LP>(fd(S, F_dpdz), cell1, cell2, k);
+        g0[4] = gather2s_ld<LP>(fd(S, F_divergence), cell1, cell2, k);
+        g0[5] = gather2s_ld<LP>(fd(S, F_vorticity), vertex1, vertex2, k);
+        g0[6] = gather2s_ld<LP>(fd(S, F_kdiff), cell1, cell2, k);
+    }
     // every load above in flight before the first swap consumes one (the per-level
     // coefficients after it: cache hits, no registers held across the batch)
     __builtin_amdgcn_sched_barrier(0);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k], rdzw = fd(S, F_rdzw)[k];
     g2_fin<LP>(g_uru, u, ru_e);
-    g2_fin<LP>(g_rw, rw1, rw2);
-    g2_fin<LP>(g_w, w1, w2);
-    g2_fin<LP>(g_rp, rho_edge, pv);
+    if constexpr (NTU) {  // (not loaded as pairs: no swaps)
+        rw1 = rw2 = w1 = w2 = pv = 0.0;
+        rho_edge = g_rp.x;
 #pragma unroll
-    for (int j = 0; j < QF; j += 2) {
-        g2_fin<LP>(g_ue[j / 2], ue_[j], ue_[j + 1]);
-        g2_fin<LP>(g_pve[j / 2], pve_[j], pve_[j + 1]);
+        for (int j = 0; j < QF; j++) ue_[j] = pve_[j] = 0.0;
+    } else {
+        g2_fin<LP>(g_rw, rw1, rw2);
+        g2_fin<LP>(g_w, w1, w2);
+        g2_fin<LP>(g_rp, rho_edge, pv);
+#pragma unroll
+        for (int j = 0; j < QF; j += 2) {
+            g2_fin<LP>(g_ue[j / 2], ue_[j], ue_[j + 1]);
+            g2_fin<LP>(g_pve[j / 2], pve_[j], pve_[j + 1]);
+        }
     }
     if constexpr (NOF) {
         tr_phys = trp_in;
     } else {
 #pragma unroll
         for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_tv[j / 2], tv_[j], tv_[j + 1]);
-        g2_fin<LP>(g_tvl, tv_[AF - 1], tr_phys);
+        if constexpr (NTU) {
+            tv_[AF - 1] = g_tvl.x;
+            tr_phys = 0.0;
+        } else {
+            g2_fin<LP>(g_tvl, tv_[AF - 1], tr_phys);
+        }
     }
     if constexpr (MD && !NOF) {
 #pragma unroll
         for (int j = 0; j < AF - 1; j += 2) g2_fin<LP>(g_wv[j / 2], wv_[j], wv_[j + 1]);
     }
-    g2_fin<LP>(g_ke, ke1, ke2);
-    g2_fin<LP>(g_hd, hd1, hd2);
+    if constexpr (NTU) {
+        ke1 = ke2 = hd1 = hd2 = 0.0;
+    } else {
+        g2_fin<LP>(g_ke, ke1, ke2);
+        g2_fin<LP>(g_hd, hd1, hd2);
+    }
     if constexpr (!RK0 && HF && !NOF) {
         g2_fin<LP>(g_tr, tue_in, rus_e);
         if (a.cp) rus_e = ru_e;  // (the copy below is setup's: ru_save = ru, read after it)
@@ -366,14 +403,16 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         tue_in -= u_diffusion;
     }
 
-    const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
-    const double w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
-    // ---- wduz (:972-980); level L is never written by the reference: read it
-    double wduz = 0.0;
-    if (k == 1 || k == L - 1) wduz = 0.5 * (rw1 + rw2) * (fzm * u + fzp * u_m);
-    if (k > 1 && k < L - 1) wduz = flux3(u_m2, u_m, u, u_p, 0.5 * (rw1 + rw2), 1.0);
-    if (k == L) wduz = wduzL;
-    const double wduz_p = lvl_up<LP>(wduz, k);
+    double tend_u = 0.0, w1p = 0.0, w2p = 0.0, wduz = 0.0, wduz_p = 0.0;
+    if constexpr (!NTU) {
+        const double u_m = lvl_dn<LP>(u, k), u_m2 = lvl_dn2<LP>(u, k), u_p = lvl_up<LP>(u, k);
+        w1p = lvl_up<LP>(w1, k), w2p = lvl_up<LP>(w2, k);
+        // ---- wduz (:972-980); level L is never written by the reference: read it
+        if (k == 1 || k == L - 1) wduz = 0.5 * (rw1 + rw2) * (fzm * u + fzp * u_m);
+        if (k > 1 && k < L - 1) wduz = flux3(u_m2, u_m, u, u_p, 0.5 * (rw1 + rw2), 1.0);
+        if (k == L) wduz = wduzL;
+        wduz_p = lvl_up<LP>(wduz, k);
+    }
     // Every lane goes on (gather2 below needs all of them); level L is not stored, the
     // padding levels get 0.0 (PADW), the scratch F is stored whole.
 
@@ -416,7 +455,8 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     }
 
     // ---- tend_u (:987-1007)
-    double tend_u = -rdzw * (wduz_p - wduz);
+    if constexpr (!NTU) {
+    tend_u = -rdzw * (wduz_p - wduz);
     double q = 0.0;
     if (a.exact_q && !MD) {
         for (int j = 0; j < neoe; j++) {  // Q10 literal: each term added nVertLevels times
@@ -457,6 +497,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         if (MD) tend_u = tend_u - cA - cB;
         else tend_u -= cA - cB;
     }
+    }  // (!NTU)
 
     double tue;
     if (rk0) {
@@ -464,13 +505,23 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         const double *div = fd(S, F_divergence), *vor = fd(S, F_vorticity), *kdiff = fd(S, F_kdiff);
         const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
         double cqu, zxu, pp1, pp2, zz1, zz2, dz1, dz2, dv1, dv2, vo1, vo2, kf1, kf2;
-        gather2<LP>(fd(S, F_cqu), e, fd(S, F_zxu), e, k, cqu, zxu);
-        gather2s<LP>(pp, cell1, cell2, k, pp1, pp2);
-        gather2s<LP>(zz, cell1, cell2, k, zz1, zz2);
-        gather2s<LP>(dpdz, cell1, cell2, k, dz1, dz2);
-        gather2s<LP>(div, cell1, cell2, k, dv1, dv2);
-        gather2s<LP>(vor, vertex1, vertex2, k, vo1, vo2);
-        gather2s<LP>(kdiff, cell1, cell2, k, kf1, kf2);
+        if constexpr (NTU) {  // (loaded with the first batch)
+            g2_fin<LP>(g0[0], cqu, zxu);
+            g2_fin<LP>(g0[1], pp1, pp2);
+            g2_fin<LP>(g0[2], zz1, zz2);
+            g2_fin<LP>(g0[3], dz1, dz2);
+            g2_fin<LP>(g0[4], dv1, dv2);
+            g2_fin<LP>(g0[5], vo1, vo2);
+            g2_fin<LP>(g0[6], kf1, kf2);
+        } else {
+            gather2<LP>(fd(S, F_cqu), e, fd(S, F_zxu), e, k, cqu, zxu);
+            gather2s<LP>(pp, cell1, cell2, k, pp1, pp2);
+            gather2s<LP>(zz, cell1, cell2, k, zz1, zz2);
+            gather2s<LP>(dpdz, cell1, cell2, k, dz1, dz2);
+            gather2s<LP>(div, cell1, cell2, k, dv1, dv2);
+            gather2s<LP>(vor, vertex1, vertex2, k, vo1, vo2);
+            gather2s<LP>(kdiff, cell1, cell2, k, kf1, kf2);
+        }
         // ---- pressure gradient (:964-970)
         tue = -cqu * ((pp2 - pp1) * invDc / (0.5 * (zz2 + zz1)) - 0.5 * zxu * (dz1 + dz2));
         // ---- del2 (:1030-1048)
@@ -487,7 +538,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         tue = tue_in;
     }
     // ---- Rayleigh damping (:1152-1159)
-    if (a.rayleigh && k > L - kRayleighLevels + 1)
+    if (!NTU && a.rayleigh && k > L - kRayleighLevels + 1)
         tend_u -= rho_edge * u * (((double)k - (double)(L - kRayleighLevels)) * a.rayleigh_inv);
     if (a.tme) {  // X_tme for the stage's acoustic substeps: theta_m(cell2) + theta_m(cell1)
         double t2pt1;
@@ -1377,6 +1428,8 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     const bool din = !MD && a.h4d > 0.0;  // (defer4: this rk_step > 0 call applies rk_step 0's D)
     // option etile (reference semantics, LP = 64): E over cell tiles forms the fluxes; B none
     const bool et = !MD && LP == 64 && S.ett != nullptr;
+    // option ntu (atm_srk3, defer4 out): rk_step 0's tend_u is dead -- B forms none (k_dyn_B NTU)
+    const bool ntu = !MD && a.d4o && in.ntu;
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
@@ -1397,11 +1450,13 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
             else if (din) k_dyn_B<LP, false, MD, true, !MD, true><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_B<LP, false, MD, true, false, true><<<nb, 256, 0, st>>>(X, a);
         } else if (hf) {
-            if (rk0) k_dyn_B<LP, true, MD, true><<<nb, 256, 0, st>>>(X, a);
+            if (rk0 && ntu) k_dyn_B<LP, true, false, true, false, false, !MD><<<nb, 256, 0, st>>>(X, a);
+            else if (rk0) k_dyn_B<LP, true, MD, true><<<nb, 256, 0, st>>>(X, a);
             else if (din) k_dyn_B<LP, false, MD, true, !MD><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_B<LP, false, MD, true><<<nb, 256, 0, st>>>(X, a);
         } else {
-            if (rk0) k_dyn_B<LP, true, MD, false><<<nb, 256, 0, st>>>(X, a);
+            if (rk0 && ntu) k_dyn_B<LP, true, false, false, false, false, !MD><<<nb, 256, 0, st>>>(X, a);
+            else if (rk0) k_dyn_B<LP, true, MD, false><<<nb, 256, 0, st>>>(X, a);
             else if (din) k_dyn_B<LP, false, MD, false, !MD><<<nb, 256, 0, st>>>(X, a);
             else k_dyn_B<LP, false, MD, false><<<nb, 256, 0, st>>>(X, a);
         }

@@ -108,6 +108,9 @@ struct mpas_ctx {
                        // (reference semantics, edgesOnEdge_ECP = edgesOnEdge; same values)
     int defer4 = 1;    // option "defer4": atm_srk3 applies rk_step 0's del4 of tend_u_euler (dyn_tend D) in the
                        // next stage's rk_step > 0 edge kernel (reference semantics; same values)
+    int ntu = 1;       // option "ntu" (with defer4): that rk_step 0 call's whole tend_u is dead (the next stage's
+                       // edge kernel rewrites it, no task in between reads it): its edge kernel forms none of
+                       // it and skips its gathers (k_dyn_B NTU; the same values of everything read later)
     int fusedamp = 1;  // option "fusedamp": atm_srk3 applies each divergence damping inside the next
                        // acoustic launch (reference semantics, undecomposed; same bits)
     void* raw[X_COUNT] = {};  // the allocations behind S.f (S.f[f] = raw[f] + stagger)
@@ -957,6 +960,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         if (c->defer4 && S.physics == 0) {
             a.defer_out = (r < 2 && rk_of(r) == 0 && rk_of(r + 1) != 0) ? 1 : 0;
             a.defer_in = (r > 0 && rk_of(r - 1) == 0 && rk_of(r) != 0) ? 1 : 0;
+            a.ntu = (a.defer_out && c->ntu) ? 1 : 0;
         }
         return a;
     };
@@ -990,7 +994,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a_done = false;
         // timing key: the variant's read / write set (bench.py parses the tags)
         const std::string dname = std::string("atm_compute_dyn_tend_work[") + (a.rk_step == 0 ? "rk0" : "rk>0") +
-                                  (a.cp ? "+copy" : "") + (a.defer_out ? "+d4o" : "") + (a.defer_in ? "+d4i" : "") +
+                                  (a.cp ? "+copy" : "") + (a.defer_out ? (a.ntu ? "+d4o+ntu" : "+d4o") : "") + (a.defer_in ? "+d4i" : "") +
                                   (a.store_v ? "+v" : "") + (a.skipA ? "-A" : "") + "]";
         run_task(c, dname.c_str(), [&] { return launch_dyn_tend(S, st, a); });
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
@@ -1349,6 +1353,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusecopy") == 0) c->fusecopy = value ? 1 : 0;
         else if (name && std::strcmp(name, "defer4") == 0) c->defer4 = value ? 1 : 0;
+        else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value ? 1 : 0;
         else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
@@ -1512,6 +1517,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) *value = c->fusesetup;
         else if (name && std::strcmp(name, "fusecopy") == 0) *value = c->fusecopy;
         else if (name && std::strcmp(name, "defer4") == 0) *value = c->defer4;
+        else if (name && std::strcmp(name, "ntu") == 0) *value = c->ntu;
         else if (name && std::strcmp(name, "vdyn") == 0) *value = c->vdyn;
         else if (name && std::strcmp(name, "eoe_same") == 0) {
             prepare_now(c);

@@ -199,6 +199,9 @@ struct DynTendArgs {
     // is applied by the next stage's rk_step > 0 edge kernel, which reads tend_u_euler anyway
     int defer_out = 0;  // 1 (rk_step 0): no D; tend_u_euler left without its del4 part, tend_u not stored
     int defer_in = 0;   // 1 (rk_step > 0): apply the deferred del4 to tend_u_euler first, store it
+    // option "ntu" (with defer_out): that call's tend_u is dead altogether (the next stage's edge
+    // kernel rewrites it, no task in between reads it): the edge kernel forms none of it
+    int ntu = 0;
     // option "vdyn" (atm_srk3 stage 2, reference semantics): the edge kernel also stores
     // solve_diagnostics' v (:429-437, Q23) from the edgesOnEdge u it gathers (S.eoe_same)
     int store_v = 0;

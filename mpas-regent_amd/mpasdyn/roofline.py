@@ -16,7 +16,7 @@ roofline.achieved divides by the measured launch time.
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
-          ddx=False):
+          ddx=False, ntu=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -70,7 +70,7 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                     ["h_divergence", "kdiff", "tend_rho", "dpdz"])
         return reads, ["h_divergence"]
     if task == "atm_compute_dyn_tend_work" and noA:  # the rest after A ran in a combined launch
-        r, w = _sets(task, rk_step=rk_step, physics=physics, copy=copy, defer_out=defer_out, store_v=store_v)
+        r, w = _sets(task, rk_step=rk_step, physics=physics, copy=copy, defer_out=defer_out, store_v=store_v, ntu=ntu)
         ra, wa = _sets(task, rk_step=rk_step, part="A")
         return ([x for x in r if x not in ("uReconstructZonal", "uReconstructMeridional")] + wa,
                 [x for x in w if x not in wa])
@@ -103,6 +103,11 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             writes = writes + ["v"]
         if defer_out and rk_step == 0:  # option defer4: tend_u of this call is dead and not stored
             writes = [x for x in writes if x != "tend_u"]  # (its del4 runs in the next call: no credit taken)
+            if ntu:  # option ntu: none of that tend_u is formed -- the arrays only it reads are not read
+                dead = ("pv_edge", "tend_ru_physics", "ke", "w", "nEdgesOnEdge", "edgesOnEdge", "weightsOnEdge",
+                        "angleEdge", "latEdge")
+                reads = [x for x in reads if x not in dead]
+                mesh = [x for x in mesh if x not in dead]
         return reads + mesh, writes
     if task == "atm_set_smlstep_pert_variables_work" and part == "flux":
         # option smlsum (atm_srk3 fast path): the slope-flux sum, once per step (X_smlS, scratch)
@@ -226,7 +231,7 @@ def b_alg(task, dims, **kw):
 
 
 def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-                  fusecopy=False, defer4=False, smlsum=False):
+                  fusecopy=False, defer4=False, smlsum=False, ntu=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -264,7 +269,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
         out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
                ("atm_compute_vert_imp_coefs", {}, 2)]
     if schedule == 1:
-        out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, "defer_out": defer4}, 1),
+        out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, "defer_out": defer4, "ntu": bool(defer4 and ntu)}, 1),
                 ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
     # (fusedamp: only the step's last acoustic launch stores rtheta_pp_old, wold)
     if fusedamp and fusesml:
@@ -296,7 +301,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
 
 
 def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-               fusecopy=False, defer4=False, smlsum=False):
+               fusecopy=False, defer4=False, smlsum=False, ntu=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
                                                                         fusesetup, fusesml, fusecopy, defer4,
-                                                                        smlsum))
+                                                                        smlsum, ntu))

@@ -252,3 +252,21 @@ def test_roofline_smlsum_accounting():
     assert ac == roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=0, damp=True, sml=True, smls=True,
                                 wold=False) - dd
     assert abs(t["atm_advance_acoustic_step_work"]["b_alg_GB_per_step"] - 2 * ac / 1e9) < 1e-3
+
+
+def test_b_alg_ntu():
+    """option ntu: the rk_step 0 launch takes no credit for the arrays only its dead tend_u read"""
+    from mpasdyn import roofline
+    dims = (163842, 491520, 327680, 56)
+    a = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True, defer_out=True)
+    b = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True, defer_out=True, ntu=True)
+    e3, c3 = 8 * dims[1] * dims[3], 8 * dims[0] * dims[3]
+    assert a - b >= 2 * e3 + 2 * c3  # pv_edge, tend_ru_physics, ke, w (+ their mesh rows)
+    r, _ = roofline._sets("atm_compute_dyn_tend_work", rk_step=0, defer_out=True, ntu=True)
+    assert "pv_edge" not in r and "ke" not in r and "u" in r and "theta_m" in r
+    # without defer_out the option changes nothing (the tend_u is live)
+    assert roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, ntu=True) == \
+        roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0)
+    s0 = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, True, True, False)
+    s1 = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, True, True, True)
+    assert s0 - s1 == a - b

@@ -109,3 +109,40 @@ def test_etile_keep_check_fast(x1_2562):
         ctx.upload(st)
         T.atm_srk3(ctx, 720.0, 1)
         ctx.sync()
+
+
+# ---------------------------------------------------------------- option ntu
+@pytest.mark.parametrize("variant", ["random", "physical"])
+@pytest.mark.parametrize("exact", [0, 1])
+@pytest.mark.parametrize("L", [5, 56])
+def test_ntu_steps_bit_identical(x1_2562, L, exact, variant):
+    """option ntu (atm_srk3, defer4 out): rk_step 0's edge kernel forms no tend_u -- dead there, the
+    next stage's edge kernel rewrites it and no task in between reads it -- so every field after the
+    step, tend_u included, has the same bits with the option on and off; exact mode = the oracle"""
+    st = make_state(x1_2562, L, variant)
+    steps = lambda ctx: [T.atm_srk3(ctx, 720.0, 1) for _ in range(2)]  # noqa: E731
+    a, _ = _run(st, 0, exact, steps, ntu=0)
+    b, _ = _run(st, 0, exact, steps, ntu=1)
+    bad = compare_states(b, a, rtol=0.0)
+    assert not bad, bad[:6]
+    if exact:
+        ref = st.copy()
+        o = O.Oracle(ref)
+        for _ in range(2):
+            o.atm_srk3(720.0, 1)
+        bad = compare_states(b, ref, rtol=0.0)
+        assert not bad, bad[:6]
+
+
+def test_ntu_only_where_dead(x1_2562):
+    """the standalone task (no next stage) and the reference's driver schedule (schedule 0: no
+    rk_step 0 stage) keep the whole tend_u: the same bits as the oracle with the option on"""
+    st = make_state(x1_2562, 56, "random")
+    got, _ = _run(st, 0, 1, lambda ctx: T.atm_compute_dyn_tend_work(ctx, 0, 720.0), ntu=1)
+    ref = st.copy()
+    O.Oracle(ref).atm_compute_dyn_tend_work(0, 720.0)
+    assert not compare_states(got, ref, rtol=0.0)
+    got, _ = _run(st, 0, 1, lambda ctx: T.atm_srk3(ctx, 720.0, 0), ntu=1)
+    ref = st.copy()
+    O.Oracle(ref).atm_srk3(720.0, 0)
+    assert not compare_states(got, ref, rtol=0.0)
