@@ -393,7 +393,7 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
             kw["copy"] = True
         if "+d4o" in tag:
             kw["defer_out"] = True
-        if "+ntu" in tag:
+        if "+ntu" in tag:  # (option ntu: a stage before the step's last, its dead tendencies not formed)
             kw["ntu"] = True
         if "+v" in tag:
             kw["store_v"] = True
@@ -673,7 +673,7 @@ def main():
     fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
     fcopy = fsetup and bool(ctx.get_option("fusecopy"))  # (decomposed and MPAS forms too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
-    ntu = d4 and bool(ctx.get_option("ntu"))
+    ntu = bool(ctx.get_option("ntu")) and not args.physics
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
                                  smls, ntu)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9

@@ -233,7 +233,7 @@ __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
 // setup's copies
 template <int LP, bool RK0, bool MD, bool HF, bool DIN = false, bool NOF = false, bool NTU = false>
 __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState S, DynK a) {
-    static_assert(!NTU || (RK0 && !MD && !DIN), "the dead tend_u: reference semantics, rk_step 0");
+    static_assert(!NTU || !MD, "the dead tend_u: reference semantics");
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -291,7 +291,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     static_assert(AF == 9, "tv_ pairing below");
     double tr_phys;
     double2 g_tv[AF / 2], g_tvl = make_double2(0.0, 0.0);
-    const double trp_in = NOF ? colk(fd(S, F_tend_ru_physics), e) : 0.0;
+    const double trp_in = (NOF && !NTU) ? colk(fd(S, F_tend_ru_physics), e) : 0.0;
     if constexpr (!NOF) {
 #pragma unroll
         for (int j = 0; j < AF - 1; j += 2) g_tv[j / 2] = gather2s_ld<LP>(tm_f, ad_[j], ad_[j + 1], k);
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     }
     // NTU: the rk0 section's loads join the first batch (the tend_u loads they replace freed the registers)
     double2 g0[7];
-    if constexpr (NTU) {
+    if constexpr (NTU && RK0) {
         const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
         g0[0] = gather2_ld<LP>(fd(S, F_cqu), e, fd(S, F_zxu), e, k);
         g0[1] = gather2s_ld<LP>(fd(S, F_pressure_p), cell1, cell2, k);
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
         const double *div = fd(S, F_divergence), *vor = fd(S, F_vorticity), *kdiff = fd(S, F_kdiff);
         const int vertex1 = fi(S, F_verticesOnEdge)[(size_t)e * 2], vertex2 = fi(S, F_verticesOnEdge)[(size_t)e * 2 + 1];
         double cqu, zxu, pp1, pp2, zz1, zz2, dz1, dz2, dv1, dv2, vo1, vo2, kf1, kf2;
-        if constexpr (NTU) {  // (loaded with the first batch)
+        if constexpr (NTU && RK0) {  // (loaded with the first batch)
             g2_fin<LP>(g0[0], cqu, zxu);
             g2_fin<LP>(g0[1], pp1, pp2);
             g2_fin<LP>(g0[2], zz1, zz2);
@@ -574,11 +574,15 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
                 put2<LP>(tueo, e, tuo, e, k, PADW(tue), PADW(tend_u), k != L, k != L);
             }
         } else {
-            tend_u += tue + tr_phys;  // :1161-1163 (rk > 0: tue is the tend_u_euler read)
-            if constexpr (NOF) {
-                if (k != L) colk(tuo, e) = PADW(tend_u);
+            if constexpr (NTU) {  // (the dead tend_u is not stored; the flux alone, whole)
+                if constexpr (!NOF) colk(Fo, e) = Hv;
             } else {
-                put2<LP>(Fo, e, tuo, e, k, Hv, PADW(tend_u), true, k != L);
+                tend_u += tue + tr_phys;  // :1161-1163 (rk > 0: tue is the tend_u_euler read)
+                if constexpr (NOF) {
+                    if (k != L) colk(tuo, e) = PADW(tend_u);
+                } else {
+                    put2<LP>(Fo, e, tuo, e, k, Hv, PADW(tend_u), true, k != L);
+                }
             }
             if (rk0) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, PADW(tue), dsq, k != L, k != L);
             if (DIN && k != L) colk(tueo, e) = PADW(tue);
@@ -588,11 +592,11 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
     if (k == L) return;
     if (rk0 && a.h4 > 0.0) {  // D finishes tend_u after the del4 part of tend_u_euler
         colk(fw(S, F_tend_u_euler), e) = PADW(tue);
-        if (!a.d4o) colk(fw(S, F_tend_u), e) = PADW(tend_u);
+        if (!NTU && !a.d4o) colk(fw(S, F_tend_u), e) = PADW(tend_u);
     } else {
         if (rk0 || DIN) colk(fw(S, F_tend_u_euler), e) = PADW(tue);
         tend_u += tue + tr_phys;  // :1161-1163
-        colk(fw(S, F_tend_u), e) = PADW(tend_u);
+        if (!NTU) colk(fw(S, F_tend_u), e) = PADW(tend_u);
     }
 }
 
@@ -883,8 +887,14 @@ struct EtTile {
 // theta_m_save pairs issued with its own columns: one memory round trip), 1 the same with the flux
 // sum formed before the own columns are loaded (fewer registers, two round trips), 2 (HF) the
 // tile's edge phase formed every edge's H (k_dyn_Et et_edges)
-template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false, int ETM = 0>
+// NTH (atm_srk3, reference semantics, a stage before the step's last): the call's theta tendency
+// outputs (tend_theta, tend_rtheta_adv, rthdynten) are dead -- the last stage rewrites them and no task
+// in between reads them (the acoustic step reads theta_m as its tend_rt, Q8) -- so the theta
+// advection, wdtz and those stores go, with B's per-edge flux (X_F) that only they read; w, and at
+// rk_step 0 tend_w_euler / tend_theta_euler (read by the later stages), are formed as always
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false, int ETM = 0, bool NTH = false>
 __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int c, int k, EtTile tl = {}) {
+    static_assert(!NTH || (!MD && !TILE), "the dead theta tendency: reference semantics, untiled");
     static_assert(!TILE || (LP == 64 && !MD), "the tiled E: LP = 64, reference semantics");
     const int L = S.L;
     const size_t p = (size_t)c * LP + lpos(LP, k);
@@ -1000,10 +1010,12 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     }
     if (rk0) gather2<LP>(fd(S, F_pressure_p), c, fd(S, F_dpdz), c, k, pp, dpdz);
     else pp = dpdz = 0.0;
-    gather2<LP>(fd(S, F_rw_save), c, tms_f, c, k, rws, tms);
+    if constexpr (NTH) rws = tms = 0.0;  // (wdtz's, dead)
+    else gather2<LP>(fd(S, F_rw_save), c, tms_f, c, k, rws, tms);
     gather2<LP>(tm, c, fd(S, F_tend_w_euler), c, k, tmv, twe);
     gather2<LP>(fd(S, F_tend_theta_euler), c, fd(S, F_rho_zz), c, k, tte, rho_zz);
-    gather2<LP>(fd(S, F_rt_diabatic_tend), c, fd(S, F_tend_rtheta_physics), c, k, rt_diab, trp);
+    if constexpr (NTH) rt_diab = trp = 0.0;
+    else gather2<LP>(fd(S, F_rt_diabatic_tend), c, fd(S, F_tend_rtheta_physics), c, k, rt_diab, trp);
     if (rk0) {
         if (SELF) gather2<LP>(fd(S, F_cqw), c, dw, c, k, cqw, dw_c);
         else cqw = colk(fd(S, F_cqw), c);
@@ -1013,16 +1025,16 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     // HF: F holds B's per-edge flux H (ru F + the rk > 0 perturbation flux): ru, ru_save
     // and the theta_m_save pairs are not gathered here
     // (TILE: the theta advection sum tth was formed above; no ru, ru_save, theta_m_save or X_F here)
-    constexpr bool GRU = !HF && !TILE;
+    constexpr bool GRU = !HF && !TILE && !NTH;
 #pragma unroll
     for (int i = 0; i < NF; i += 2) {
         if (GRU) gather2s<LP>(ru, e_[i], e_[i + 1], k, ru_[i], ru_[i + 1]);
-        if (!TILE) gather2s<LP>(Ff, e_[i], e_[i + 1], k, F_[i], F_[i + 1]);
+        if (!TILE && !NTH) gather2s<LP>(Ff, e_[i], e_[i + 1], k, F_[i], F_[i + 1]);
     }
 #pragma unroll
     for (int i = 0; i < NF; i++) {
         ru_[i] = GRU ? ldz(kl, ru_[i]) : 0.0;
-        F_[i] = TILE ? 0.0 : ldz(kl, F_[i]);
+        F_[i] = (TILE || NTH) ? 0.0 : ldz(kl, F_[i]);
         rus_[i] = ts1_[i] = ts2_[i] = dw1_[i] = dw2_[i] = dt1_[i] = dt2_[i] = 0.0;
     }
     if (!rk0 && GRU) {
@@ -1091,7 +1103,7 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     tte = ldz(kl, tte);
     // level-L slots (MD: MPAS-A's top fluxes are 0)
     const double wdwzL = MD ? 0.0 : fd(S, F_wdwz)[(size_t)c * LP + lpos(LP, L)];
-    const double wdtzL = MD ? 0.0 : fd(S, F_wdtz)[(size_t)c * LP + lpos(LP, L)];
+    const double wdtzL = (MD || NTH) ? 0.0 : fd(S, F_wdtz)[(size_t)c * LP + lpos(LP, L)];
 
     // ================= W =================
     if (del4 && kl) {  // :1258-1272
@@ -1158,6 +1170,29 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     }
 
     // ================= theta =================
+    if constexpr (NTH) {  // the live outputs only: w, and at rk_step 0 the euler tendencies (del4 of theta)
+        if (rk0 && kl && del4) {  // :1384-1400
+            double r_areaCell = a.h4 * a.prandtl_inv * invA;
+#pragma unroll
+            for (int i = 0; i < NF; i++) {
+                double edge_sign = cmsd4_[i] * r_areaCell * cdv_[i] * eocs_[i] * cidc_[i];
+                tte = sub_if(i < ne, tte, edge_sign * (dt2_[i] - dt1_[i]));
+            }
+            for (int i = NF; i < ne; i++) {
+                double edge_sign = cmsd4[i] * r_areaCell * cdv[i] * eocs[i] * cidc[i];
+                tte -= edge_sign * (colk(dth, cc2[i]) - colk(dth, cc1[i]));
+            }
+        }
+        if constexpr (HF) {
+            colk(fw(S, F_w), c) = KEEPW(w, kl_w);
+            if (rk0)
+                put2f<LP>(fw(S, F_tend_w_euler), c, fw(S, F_tend_theta_euler), c, k, KEEPW(twe, kl_twe),
+                         KEEPW(tte, kl_tte));
+        } else if (rk0 && k != L) {  // (w and tend_w_euler stored above)
+            colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
+        }
+        return;
+    }
     double tend_theta = 0.0;  // :1328-1344
     if (TILE) {  // (formed above)
         if (kl) tend_theta = tth;
@@ -1245,11 +1280,11 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
-template <int LP, bool RK0, bool SELF, bool MD, bool HF>
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool NTH = false>
 __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk bk) {
     ColMap<LP> m(S, KC, bk);
     if (m.ent >= S.nCO) return;
-    dyn_E_cell<LP, RK0, SELF, MD, HF>(S, a, m.ent, m.k);
+    dyn_E_cell<LP, RK0, SELF, MD, HF, false, 0, NTH>(S, a, m.ent, m.k);
 }
 
 // option "etile" (reference semantics, LP = 64): E over the tiles of TrTiles (mpas_dev.h; the
@@ -1374,9 +1409,9 @@ __global__ __launch_bounds__(NT, ETM == 2 && !RK0 ? 5 : 4) void k_dyn_Et(DevStat
 
 // (rk_step > 0, reference semantics, LP = 64: 4 waves per SIMD, as before E formed wc itself;
 // at LP < 64 that cap spilled 10-22 VGPRs)
-template <int LP, bool RK0, bool SELF, bool MD, bool HF>
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool NTH = false>
 __global__ __launch_bounds__(256, LP == 64 && !RK0 && !MD ? 4 : 1) void k_dyn_E(DevState S, DynK a) {
-    dyn_E_body<LP, RK0, SELF, MD, HF>(S, a, this_blk());
+    dyn_E_body<LP, RK0, SELF, MD, HF, NTH>(S, a, this_blk());
 }
 // D and E of rk_step 0 in one grid (option "hfuse": neither reads what the other writes)
 template <int LP, bool SELF, bool MD, bool HF>
@@ -1428,8 +1463,11 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     const bool din = !MD && a.h4d > 0.0;  // (defer4: this rk_step > 0 call applies rk_step 0's D)
     // option etile (reference semantics, LP = 64): E over cell tiles forms the fluxes; B none
     const bool et = !MD && LP == 64 && S.ett != nullptr;
-    // option ntu (atm_srk3, defer4 out): rk_step 0's tend_u is dead -- B forms none (k_dyn_B NTU)
-    const bool ntu = !MD && a.d4o && in.ntu;
+    // option ntu (atm_srk3, reference semantics, a stage before the step's last): the call's tend_u
+    // is dead -- B forms none (k_dyn_B NTU; never where D runs in this call and reads it) -- and so
+    // are its theta tendencies -- E forms none (k_dyn_E NTH) and B no flux for them (NOF)
+    const bool ntu = !MD && in.ntu && !(rk0 && del4 && !a.d4o);
+    const bool nth = !MD && in.nth;
     auto kB = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (!nb) return;
@@ -1442,6 +1480,29 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 if (rk0) k_dyn_B<LP, true, MD, false, false, true><<<nb, 256, 0, st>>>(X, a);
                 else if (din) k_dyn_B<LP, false, MD, false, !MD, true><<<nb, 256, 0, st>>>(X, a);
                 else k_dyn_B<LP, false, MD, false, false, true><<<nb, 256, 0, st>>>(X, a);
+            }
+        } else if (!MD && (nth || ntu)) {
+            if constexpr (!MD) {
+                using T_ = std::true_type;
+                using F_ = std::false_type;
+                auto go = [&](auto R, auto H, auto Di, auto Nf, auto Nt) {
+                    k_dyn_B<LP, decltype(R)::value, false, decltype(H)::value, decltype(Di)::value, decltype(Nf)::value,
+                            decltype(Nt)::value><<<nb, 256, 0, st>>>(X, a);
+                };
+                auto go4 = [&](auto R, auto H, auto Di) {
+                    if (nth && ntu) go(R, H, Di, T_{}, T_{});
+                    else if (nth) go(R, H, Di, T_{}, F_{});
+                    else go(R, H, Di, F_{}, T_{});
+                };
+                auto go3 = [&](auto R, auto Di) {
+                    if (hf) go4(R, T_{}, Di);
+                    else go4(R, F_{}, Di);
+                };
+                if (rk0) go3(T_{}, F_{});
+                else if (din) go3(F_{}, T_{});
+                else if (!(nth && ntu) || a.vB || a.tme || a.cp) go3(F_{}, F_{});
+                // (else: nothing of this rk_step > 0 edge kernel is live -- no launch; setup's copies, fusecopy,
+                // would be: a reference-driver stage 0 at rk_step > 0 keeps the launch for them)
             }
         } else if (hf && (X.bsplit == 1 || (X.bsplit == 2 && MD))) {  // (option bsplit: the fluxes in k_dyn_Bf first)
             if (rk0) k_dyn_Bf<LP, true, MD><<<nb, 256, 0, st>>>(X, a);
@@ -1520,6 +1581,23 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 return;
             }
         }
+        if constexpr (!MD) {
+            if (nth) {  // (k_dyn_E NTH: the theta tendencies dead in this call)
+                auto go = [&](auto hfc) {
+                    constexpr bool H = decltype(hfc)::value;
+                    if (rk0) {
+                        if (X.selfc) k_dyn_E<LP, true, true, false, H, true><<<nb, 256, 0, st>>>(X, a);
+                        else k_dyn_E<LP, true, false, false, H, true><<<nb, 256, 0, st>>>(X, a);
+                    } else {
+                        if (X.selfc) k_dyn_E<LP, false, true, false, H, true><<<nb, 256, 0, st>>>(X, a);
+                        else k_dyn_E<LP, false, false, false, H, true><<<nb, 256, 0, st>>>(X, a);
+                    }
+                };
+                if (hf) go(std::true_type{});
+                else go(std::false_type{});
+                return;
+            }
+        }
         auto go = [&](auto hfc) {
             constexpr bool H = decltype(hfc)::value;
             if (rk0) {
@@ -1537,6 +1615,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     // (u and v only for the Smagorinsky deformation of rk_step 0: a gather declared but not
     // made would cost an exchange whenever v is stale)
     if (in.skipA) {  // (A ran in the previous combined launch, atm_srk3 hfuse; no halo)
+    } else if (ntu && !rk0) {  // (A's one output at rk_step > 0, h_divergence, feeds only the dead tend_u)
     } else if (rk0 && a.horiz_mixing == 0) {
         HALO_RUN(S, st, kA, F_ru, F_u, F_v);
     } else {
@@ -1545,8 +1624,11 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz);
     if (!MD && rk0) HALO_WROTE(S, X_wc);
     if (rk0) {
-        HALO_RUN_R1(S, st, kB, F_vorticity, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p,
-                    F_zz, F_dpdz, F_divergence, F_kdiff, F_vorticity);  // (vorticity at vertices of owned edges)
+        if (ntu && nth)  // (the pressure gradient and del2 alone)
+            HALO_RUN_R1(S, st, kB, F_vorticity, F_pressure_p, F_zz, F_dpdz, F_divergence, F_kdiff, F_vorticity);
+        else
+            HALO_RUN_R1(S, st, kB, F_vorticity, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_pressure_p,
+                        F_zz, F_dpdz, F_divergence, F_kdiff, F_vorticity);  // (vorticity at vertices of owned edges)
         HALO_WROTE(S, X_F, F_tend_u, F_tend_u_euler, F_delsq_u);
         if (MD) HALO_WROTE(S, X_Fw);
         if (MD) HALO_RUN(S, st, kC, F_delsq_u, F_rho_edge, F_kdiff, F_w, F_theta_m);
@@ -1554,7 +1636,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
                    F_tend_theta_euler);
         const bool runD = del4 && !a.d4o;  // (defer4: D runs in the next call's B)
-        if (runD && in.hfuse && !S.halo && !et) {  // D beside E, one grid
+        if (runD && in.hfuse && !S.halo && !et && !nth) {  // D beside E, one grid
             const int nb1 = col_blocks<LP>(S, KE), nb = nb1 + col_blocks<LP>(S, KC);
             auto go = [&](auto hfc) {
                 constexpr bool H = decltype(hfc)::value;
@@ -1570,12 +1652,15 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
                 HALO_WROTE(S, F_tend_u_euler, F_tend_u);
             }
-            if (et) HALO_RUN(S, st, kE, F_ru, F_theta_m, F_delsq_w, F_delsq_theta);
+            if (nth) HALO_RUN(S, st, kE, F_delsq_w, F_delsq_theta);
+            else if (et) HALO_RUN(S, st, kE, F_ru, F_theta_m, F_delsq_w, F_delsq_theta);
             else if (hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta);  // (X_Fw: MD only written)
             else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
         }
     } else {
-        if (din && hf)
+        if (ntu && nth)  // (the deferred del4 of tend_u_euler alone, or nothing)
+            HALO_RUN(S, st, kB, F_delsq_divergence, F_delsq_vorticity);
+        else if (din && hf)
             HALO_RUN(S, st, kB, F_rw, F_w, F_ke, F_h_divergence, F_pv_edge, F_u, F_theta_m, F_theta_m_save,
                      F_delsq_divergence, F_delsq_vorticity);
         else if (din)
@@ -1587,7 +1672,8 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         if (din) HALO_WROTE(S, F_tend_u_euler);
         if (a.vB) HALO_WROTE(S, F_v);
         if (MD) HALO_WROTE(S, X_Fw);
-        if (et) HALO_RUN(S, st, kE, F_ru, F_ru_save, F_theta_m, F_theta_m_save);
+        if (nth) HALO_RUN(S, st, kE, F_ru);
+        else if (et) HALO_RUN(S, st, kE, F_ru, F_ru_save, F_theta_m, F_theta_m_save);
         else if (hf) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw);  // (ru: wc at the cell's last edge, reference semantics)
         else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);
     }

@@ -960,11 +960,29 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         if (c->defer4 && S.physics == 0) {
             a.defer_out = (r < 2 && rk_of(r) == 0 && rk_of(r + 1) != 0) ? 1 : 0;
             a.defer_in = (r > 0 && rk_of(r - 1) == 0 && rk_of(r) != 0) ? 1 : 0;
-            a.ntu = (a.defer_out && c->ntu) ? 1 : 0;
+            // (option ntu: the stages before the last read no tend_u_euler -- their edge kernels form no
+            // tend_u -- so the deferred del4 goes to the last stage's edge kernel, the first that reads it;
+            // its operands, delsq_divergence / delsq_vorticity / rho_edge, are unchanged until then)
+            if (c->ntu) {
+                const bool pending = (rk_of(0) == 0 && rk_of(1) != 0) || (rk_of(1) == 0 && rk_of(2) != 0);
+                a.defer_in = (r == 2 && pending) ? 1 : 0;
+            }
+        }
+        // option ntu (reference semantics): a stage before the step's last leaves dead tendencies -- the last
+        // stage rewrites tend_u, tend_theta, tend_rtheta_adv and rthdynten, and no task in between reads them
+        // (set_smlstep reads u_tend, Q2; the acoustic step reads neither tend_u, Q18, nor tend_theta: theta_m
+        // is its tend_rt, Q8): that dyn_tend forms none of them (tend_u only where its D, reading it, does not run)
+        if (c->ntu && S.physics == 0 && r < 2) {
+            a.nth = 1;
+            a.ntu = 1;  // (launch_dyn_tend keeps it off where D runs in the call)
         }
         return a;
     };
     bool flux_done = false;  // (option smlsum: the step's flux sum, beside setup and A on small grids)
+    // option ntu: stage 0's solve_diagnostics is dead where stage 1 runs at rk_step > 0 (a stage before the last
+    // reads nothing it writes; an rk_step 0 stage 1 would read divergence and vorticity)
+    const int rk1 = schedule == 0 ? (int)rk_sub_timestep[1] : 1;
+    const bool solve0_dead = c->ntu && S.physics == 0 && !hf && rk1 != 0;
     if (c->fusesetup && S.physics == 0 && hf2) {  // + stage 0's dyn_tend A in the same launch
         run_task(c, smls ? "hfuse[setup+dyn_A+sml_flux]" : "hfuse[setup+dyn_A]", [&] {
             return launch_hf_setup_dyn_A(S, st, stage_args(0), rk_sub_timestep[0], fcopy ? 0 : 1, smls ? 1 : 0);
@@ -994,7 +1012,7 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a_done = false;
         // timing key: the variant's read / write set (bench.py parses the tags)
         const std::string dname = std::string("atm_compute_dyn_tend_work[") + (a.rk_step == 0 ? "rk0" : "rk>0") +
-                                  (a.cp ? "+copy" : "") + (a.defer_out ? (a.ntu ? "+d4o+ntu" : "+d4o") : "") + (a.defer_in ? "+d4i" : "") +
+                                  (a.cp ? "+copy" : "") + (a.defer_out ? "+d4o" : "") + (a.ntu ? "+ntu" : "") + (a.defer_in ? "+d4i" : "") +
                                   (a.store_v ? "+v" : "") + (a.skipA ? "-A" : "") + "]";
         run_task(c, dname.c_str(), [&] { return launch_dyn_tend(S, st, a); });
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
@@ -1058,6 +1076,10 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             if (rk_step == 0) vi_done = true;
             a_done = true;
             vc_done = false;
+        } else if (rk_step == 0 && solve0_dead) {
+            // option ntu: stage 0's solve_diagnostics is dead -- stage 1's dyn_tend (a stage before the last:
+            // no A, no tend_u) reads none of its outputs, no other task reads them, and stage 1's and 2's
+            // solve_diagnostics rewrite every one (h_edge, ke_edge, pv_edge, divergence, ke, vorticity, pv_vertex)
         } else if (hf && rk_step == 0) {  // the edge kernel beside stage 1's vert_imp
             run_task(c, "atm_compute_solve_diagnostics[vc]", [&] { return launch_solve_diagnostics(S, st, 0, 0, 1); });
             run_task(c, "hfuse[solve_e+vert_imp]",

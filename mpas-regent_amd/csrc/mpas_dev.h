@@ -202,6 +202,10 @@ struct DynTendArgs {
     // option "ntu" (with defer_out): that call's tend_u is dead altogether (the next stage's edge
     // kernel rewrites it, no task in between reads it): the edge kernel forms none of it
     int ntu = 0;
+    // option "ntu" (atm_srk3, reference semantics, a stage before the step's last): the call's theta
+    // tendencies are dead as well (the last stage rewrites them; the acoustic step reads theta_m as
+    // its tend_rt, Q8): E forms none of them, B no per-edge flux for them
+    int nth = 0;
     // option "vdyn" (atm_srk3 stage 2, reference semantics): the edge kernel also stores
     // solve_diagnostics' v (:429-437, Q23) from the edgesOnEdge u it gathers (S.eoe_same)
     int store_v = 0;

@@ -103,11 +103,22 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             writes = writes + ["v"]
         if defer_out and rk_step == 0:  # option defer4: tend_u of this call is dead and not stored
             writes = [x for x in writes if x != "tend_u"]  # (its del4 runs in the next call: no credit taken)
-            if ntu:  # option ntu: none of that tend_u is formed -- the arrays only it reads are not read
-                dead = ("pv_edge", "tend_ru_physics", "ke", "w", "nEdgesOnEdge", "edgesOnEdge", "weightsOnEdge",
-                        "angleEdge", "latEdge")
-                reads = [x for x in reads if x not in dead]
-                mesh = [x for x in mesh if x not in dead]
+        if ntu and not md:
+            # option ntu (atm_srk3, a stage before the step's last): the call's tend_u and theta tendencies
+            # are dead and not formed -- no credit for them nor for the arrays only they read (B's tend_u
+            # terms and flux, E's theta advection and wdtz); at rk_step > 0 no A either (its h_divergence
+            # feeds only that tend_u) and B only applies the deferred del4 (no credit, as defer4's)
+            dead_w = {"tend_u", "tend_theta", "tend_rtheta_adv", "rthdynten"}
+            dead_r = {"pv_edge", "tend_ru_physics", "ke", "w", "rw_save", "theta_m_save", "rt_diabatic_tend",
+                      "tend_rtheta_physics", "ru_save", "nEdgesOnEdge", "edgesOnEdge", "weightsOnEdge", "angleEdge",
+                      "latEdge", "nAdvCellsForEdge", "advCellsForEdge", "adv_coefs", "adv_coefs_3rd"}
+            if rk_step != 0:
+                dead_w |= {"h_divergence"}
+                dead_r |= {"u", "rho_edge", "theta_m", "tend_theta_euler", "tend_u_euler", "cellsOnEdge",
+                           "verticesOnEdge", "dvEdge", "invDcEdge"}
+            writes = [x for x in writes if x not in dead_w]
+            reads = [x for x in reads if x not in dead_r]
+            mesh = [x for x in mesh if x not in dead_r]
         return reads + mesh, writes
     if task == "atm_set_smlstep_pert_variables_work" and part == "flux":
         # option smlsum (atm_srk3 fast path): the slope-flux sum, once per step (X_smlS, scratch)
@@ -269,8 +280,9 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
         out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
                ("atm_compute_vert_imp_coefs", {}, 2)]
     if schedule == 1:
-        out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, "defer_out": defer4, "ntu": bool(defer4 and ntu)}, 1),
-                ("atm_compute_dyn_tend_work", {"rk_step": 1}, 2)]
+        out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, "defer_out": defer4, "ntu": bool(ntu)}, 1),
+                ("atm_compute_dyn_tend_work", {"rk_step": 1, "ntu": bool(ntu)}, 1),
+                ("atm_compute_dyn_tend_work", {"rk_step": 1}, 1)]
     # (fusedamp: only the step's last acoustic launch stores rtheta_pp_old, wold)
     if fusedamp and fusesml:
         sm = {"sml": True, "smls": bool(smlsum)}
@@ -294,8 +306,10 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                 ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1}, 4),
                 ("atm_divergence_damping_3d", {}, 7)]
+    # (option ntu: stage 0's solve_diagnostics is dead and not run)
     out += [
-            ("atm_compute_solve_diagnostics", {}, 2), ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
+            ("atm_compute_solve_diagnostics", {}, 1 if ntu else 2),
+            ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
             ("atm_rk_dynamics_substep_finish", {}, 1)]
     return out
 

@@ -262,11 +262,17 @@ def test_b_alg_ntu():
     b = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, copy=True, defer_out=True, ntu=True)
     e3, c3 = 8 * dims[1] * dims[3], 8 * dims[0] * dims[3]
     assert a - b >= 2 * e3 + 2 * c3  # pv_edge, tend_ru_physics, ke, w (+ their mesh rows)
-    r, _ = roofline._sets("atm_compute_dyn_tend_work", rk_step=0, defer_out=True, ntu=True)
+    r, w = roofline._sets("atm_compute_dyn_tend_work", rk_step=0, defer_out=True, ntu=True)
     assert "pv_edge" not in r and "ke" not in r and "u" in r and "theta_m" in r
-    # without defer_out the option changes nothing (the tend_u is live)
-    assert roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, ntu=True) == \
-        roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0)
+    assert "tend_theta" not in w and "tend_theta_euler" in w and "w" in w and "tend_u_euler" in w
+    r1, w1 = roofline._sets("atm_compute_dyn_tend_work", rk_step=1, ntu=True)
+    assert set(w1) == {"w"} and "ru" in r1 and "tend_w_euler" in r1 and "theta_m" not in r1
+    # under the MPAS forms the option changes nothing (the tendencies are live)
+    assert roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, ntu=True, physics=2) == \
+        roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=0, physics=2)
     s0 = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, True, True, False)
     s1 = roofline.b_alg_step(dims, 1, 0, 0, True, True, True, True, True, True, True)
-    assert s0 - s1 == a - b
+    b1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1)
+    c1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1, ntu=True)
+    sd = roofline.b_alg("atm_compute_solve_diagnostics", dims)
+    assert s0 - s1 == (a - b) + (b1 - c1) + sd  # (+ stage 0's dead solve_diagnostics)
