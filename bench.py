@@ -372,6 +372,7 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
              "hfuse[damp+solve_vc]": {"pair": "damp+solve_vc"}, "hfuse[solve_e+finish]": {"pair": "solve_e+finish"},
              "hfuse[solve_e-v+finish]": {"pair": "solve_e-v+finish"},
              "atm_compute_solve_diagnostics[e-v]": {"part": "e"}, "atm_compute_solve_diagnostics[-v]": {},
+             "atm_compute_solve_diagnostics[live]": {"live": True},
              "hfuse[solve_e+vert_imp]": {"pair": "solve_e+vert_imp"},
              "hfuse[acoustic+solve_vc]": {"pair": "acoustic+solve_vc"},
              "hfuse[solve_e+dyn_A]": {"pair": "solve_e+dyn_A"},

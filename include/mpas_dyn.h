@@ -86,7 +86,15 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * (default) applies rk_step 0's del4 of tend_u_euler (dyn_tend kernel D) in the next stage's
  * rk_step > 0 edge kernel; "vdyn" = 1 (default) has the last stage's dyn_tend edge kernel store
  * solve_diagnostics' v from the u it gathers (when edgesOnEdge_ECP = edgesOnEdge, read-only
- * "eoe_same"); "bsplit" (fast path, speed only) puts dyn_tend's per-edge theta flux (and the MPAS dynamics' w
+ * "eoe_same"); "ntu" = 1 (default; reference semantics, with defer4) leaves out what the stages
+ * before the step's last would compute only for values no task reads before the last stage
+ * rewrites them: their dyn_tend forms no tend_u and no theta tendencies (tend_theta,
+ * tend_rtheta_adv, rthdynten), stage 0's solve_diagnostics is not run and stage 1's stores ke and
+ * pv_edge alone (its divergence, vorticity, h_edge and ke_edge are dead); every field after a step
+ * is bit-identical with it off; 2 = the same with stage 1's solve_diagnostics whole (A/B);
+ * "etile" = 1 (default 0, measured, not kept) forms dyn_tend's theta advection fluxes from tiles
+ * of cells in LDS ("etcells", "etclo", "etmode", "etthreads"; read-only "etile_active");
+ * "bsplit" (fast path, speed only) puts dyn_tend's per-edge theta flux (and the MPAS dynamics' w
  * flux) in an edge kernel of its own beside the edge kernel B: 1 always, 2 (default) under
  * "physics" = 2 only, where B's registers would otherwise hold it to 3 waves per SIMD, 0 never.
  * "keep_check" = 1 (default 0; debug, slow) compares every field's keep tail -- the value of

@@ -257,8 +257,13 @@ __device__ __forceinline__ void finish64_body(const DevState& S, int substep, in
 // MD: the MPAS dynamics (physics = 2, ora_mpas_solve_diagnostics): divergence += s * u (Q9),
 // h = rho_zz and rho_edge = h_edge (Q2: MPAS-A passes diag%rho_edge as h_edge), v over
 // every edgesOnEdge entry (Q23)
-template <int LP, int EPW, bool MD>
+// LIVE (atm_srk3 option ntu, reference semantics: stage 1's call, the step's last stage at rk_step > 0):
+// only what the last stage's dyn_tend reads is stored -- ke, and pv_vertex for pv_edge.  vorticity,
+// divergence, h_edge and ke_edge have no reader before the last stage's solve_diagnostics rewrites them
+// (dyn_tend reads divergence and vorticity at rk_step 0 only; nothing reads h_edge or ke_edge)
+template <int LP, int EPW, bool MD, bool LIVE = false>
 __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int hollingsworth_part, Blk bk) {
+    static_assert(!LIVE || !MD, "the dead diagnostics: reference semantics");
     const int L = S.L;
     const double* u = fd(S, F_u);
     const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
@@ -296,7 +301,11 @@ __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int ho
             vort *= iat[j];
             // (one paired 16-B store, every lane; level L keeps its value)
             // (level L left unwritten, as the reference: the keep tails cost this kernel 12 %)
-            put2<LP>(fw(S, F_vorticity), v, fw(S, F_pv_vertex), v, k, PADW(vort), PADW(fv[j] + vort), k != L, k != L);
+            if constexpr (LIVE) {
+                if (k != L) colk(fw(S, F_pv_vertex), v) = PADW(fv[j] + vort);
+            } else {
+                put2<LP>(fw(S, F_vorticity), v, fw(S, F_pv_vertex), v, k, PADW(vort), PADW(fv[j] + vort), k != L, k != L);
+            }
             if (k == L) continue;
             if (hollingsworth_part) {
                 double r = 0.25 * iat[j];
@@ -360,15 +369,21 @@ __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int ho
         div *= invA[j];
         ke *= invA[j];
         // (one paired 16-B store, every lane; level L keeps its value)
-        put2<LP>(fw(S, F_divergence), c, fw(S, F_ke), c, k, PADW(div), PADW(ke), k != L, k != L);
+        if constexpr (LIVE) {
+            if (k != L) colk(fw(S, F_ke), c) = PADW(ke);
+        } else {
+            put2<LP>(fw(S, F_divergence), c, fw(S, F_ke), c, k, PADW(div), PADW(ke), k != L, k != L);
+        }
     }
 }
 
 // EPW consecutive edges per column slot (option "epw"): the loads of all of them are issued
 // before the first store; the paired 16-B stores write h_edge with ke_edge and pv_edge with
 // v (or alone) -- every lane takes part (put2), level L keeps its value
-template <int LP, bool RECON_V, bool MD, int EPW>
+// LIVE (see solve_vc_body): pv_edge alone
+template <int LP, bool RECON_V, bool MD, int EPW, bool LIVE = false>
 __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
+    static_assert(!LIVE || (!MD && !RECON_V), "the dead diagnostics: reference semantics, no v");
     ColMapN<LP, EPW> m(S, KE, bk);
     const int L = S.L, k = m.k;
     const double *h = fd(S, MD ? F_rho_zz : F_h), *u = fd(S, F_u), *pvv = fd(S, F_pv_vertex);
@@ -380,7 +395,8 @@ __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
         ee[j] = e;
         const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
         const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
-        gather2s<LP>(h, coe[0], coe[1], k, h1[j], h2[j]);
+        if constexpr (LIVE) h1[j] = h2[j] = 0.0;
+        else gather2s<LP>(h, coe[0], coe[1], k, h1[j], h2[j]);
         gather2s<LP>(pvv, voe[0], voe[1], k, pv1[j], pv2[j]);
     }
 #pragma unroll
@@ -411,7 +427,7 @@ __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
             for (int i = QF; i < neoe; i++) v += wts[i] * colk(u, eoe[i]);
             vv[j] = v;
         } else {
-            uu[j] = colk(u, e);
+            uu[j] = LIVE ? 0.0 : colk(u, e);
         }
     }
 #pragma unroll
@@ -421,6 +437,10 @@ __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
         const double efac = fd(S, F_dcEdge)[e] * fd(S, F_dvEdge)[e];
         // (padding levels k > L: zeros; level L: the kept values, keep tails in mpas_dev.h)
         auto kL = [&](int f) { return keepv<LP>(S, f, KE, e); };
+        if constexpr (LIVE) {
+            colk(fw(S, F_pv_edge), e) = KEEPW(0.5 * (pv1[j] + pv2[j]), kL(F_pv_edge));
+            continue;
+        }
         put2f<LP>(fw(S, F_h_edge), e, fw(S, F_ke_edge), e, k, KEEPW(0.5 * (h1[j] + h2[j]), kL(F_h_edge)),
                  KEEPW(efac * (uu[j] * uu[j]), kL(F_ke_edge)));
         if (MD) colk(fw(S, F_rho_edge), e) = KEEPW(0.5 * (h1[j] + h2[j]), kL(F_rho_edge));

@@ -15,9 +15,9 @@
 
 namespace mpas {
 
-template <int LP, int EPW, bool MD>
+template <int LP, int EPW, bool MD, bool LIVE = false>
 __global__ __launch_bounds__(256) void k_solve_vc(DevState S, int nVB, int hollingsworth_part) {
-    solve_vc_body<LP, EPW, MD>(S, nVB, hollingsworth_part, this_blk());
+    solve_vc_body<LP, EPW, MD, LIVE>(S, nVB, hollingsworth_part, this_blk());
 }
 
 // hollingsworth second half (:405-417): cells, needs ke_vertex of the whole mesh
@@ -40,24 +40,26 @@ __global__ __launch_bounds__(256) void k_solve_holl(DevState S) {
     colk(fw(S, F_ke), c) = ke;
 }
 
-template <int LP, bool RECON_V, bool MD, int EPW>
+template <int LP, bool RECON_V, bool MD, int EPW, bool LIVE = false>
 __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
-    solve_e_body<LP, RECON_V, MD, EPW>(S, this_blk());
+    solve_e_body<LP, RECON_V, MD, EPW, LIVE>(S, this_blk());
 }
 
 template <int LP, bool MD>
 static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts, int no_v) {
+    // parts & 4 (atm_srk3 option ntu): the stored diagnostics the step's last stage reads, alone
+    const bool live = !MD && (parts & 4) && !hollingsworth;
     auto kvc = [&](const DevState& X) {  // vertex blocks, then cell blocks
-        if (X.epw == 4) {
-            const int nv = col_blocks_n<LP, 4>(X, KV), nb = nv + col_blocks_n<LP, 4>(X, KC);
-            if (nb) k_solve_vc<LP, 4, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
-        } else if (X.epw == 2) {
-            const int nv = col_blocks_n<LP, 2>(X, KV), nb = nv + col_blocks_n<LP, 2>(X, KC);
-            if (nb) k_solve_vc<LP, 2, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
-        } else {
-            const int nv = col_blocks_n<LP, 1>(X, KV), nb = nv + col_blocks_n<LP, 1>(X, KC);
-            if (nb) k_solve_vc<LP, 1, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
-        }
+        auto go = [&](auto epw) {
+            constexpr int E = decltype(epw)::value;
+            const int nv = col_blocks_n<LP, E>(X, KV), nb = nv + col_blocks_n<LP, E>(X, KC);
+            if (!nb) return;
+            if (live) k_solve_vc<LP, E, false, true><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+            else k_solve_vc<LP, E, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+        };
+        if (X.epw == 4) go(std::integral_constant<int, 4>{});
+        else if (X.epw == 2) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 1>{});
     };
     auto kh = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
@@ -69,7 +71,8 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
             constexpr int E = decltype(epw)::value;
             const int nb = col_blocks_n<LP, E>(X, KE);
             if (!nb) return;
-            if (rv) k_solve_e<LP, true, MD, E><<<nb, 256, 0, st>>>(X);
+            if (live && !rv) k_solve_e<LP, false, false, E, true><<<nb, 256, 0, st>>>(X);
+            else if (rv) k_solve_e<LP, true, MD, E><<<nb, 256, 0, st>>>(X);
             else k_solve_e<LP, false, MD, E><<<nb, 256, 0, st>>>(X);
         };
         if (X.epw == 4) go(std::integral_constant<int, 4>{});
@@ -86,10 +89,17 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
         kvc(Y);
     };
     if (!(parts & 1)) {  // (the vertex / cell kernel ran in a combined launch, atm_srk3 hfuse)
+    } else if (r1 && live) {
+        HALO_RUN(S, st, kvc1, F_u);
+        S.halo->wrote_ring1({F_pv_vertex});
+        HALO_WROTE(S, F_ke);
     } else if (r1) {
         HALO_RUN(S, st, kvc1, F_u);
         S.halo->wrote_ring1({F_vorticity, F_pv_vertex});
         HALO_WROTE(S, F_ke_vertex, F_divergence, F_ke);
+    } else if (live) {
+        HALO_RUN(S, st, kvc, F_u);
+        HALO_WROTE(S, F_pv_vertex, F_ke);
     } else {
         HALO_RUN(S, st, kvc, F_u);
         HALO_WROTE(S, F_vorticity, F_pv_vertex, F_ke_vertex, F_divergence, F_ke);
@@ -103,6 +113,11 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
         HALO_RUN_R1(S, st, ke, F_pv_vertex, F_rho_zz, F_u, F_pv_vertex);
         HALO_WROTE(S, F_h_edge, F_rho_edge, F_ke_edge, F_v, F_pv_edge);
     } else {
+        if (live && !(rk_step == -1 || rk_step == 2)) {
+            HALO_RUN_R1(S, st, ke, F_pv_vertex, F_pv_vertex);
+            HALO_WROTE(S, F_pv_edge);
+            return hipGetLastError();
+        }
         HALO_RUN_R1(S, st, ke, F_pv_vertex, F_h, F_u, F_pv_vertex);
         HALO_WROTE(S, F_h_edge, F_ke_edge, F_pv_edge);
         if (!no_v && (rk_step == -1 || rk_step == 2)) HALO_WROTE(S, F_v);

@@ -1087,8 +1087,15 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             vi_done = true;
         } else {
             const int nv = (rk_step == 2 && vdyn_on) ? 1 : 0;
-            run_task(c, nv ? "atm_compute_solve_diagnostics[-v]" : "atm_compute_solve_diagnostics",
-                     [&] { return launch_solve_diagnostics(S, st, 0, rk_step, 3, nv); });
+            // option ntu: stage 1's call stores only what the last stage (rk_step > 0) reads -- ke and
+            // pv_edge; its divergence, vorticity, h_edge and ke_edge have no reader before the last stage's
+            // solve_diagnostics rewrites them (dyn_tend reads divergence and vorticity at rk_step 0 only)
+            const int rk2 = schedule == 0 ? (int)rk_sub_timestep[2] : 2;
+            // (ntu = 2: the dead tendencies alone, every diagnostic stored -- the A/B of this part)
+            const bool live = c->ntu == 1 && S.physics == 0 && rk_step == 1 && rk2 != 0;
+            run_task(c, live ? "atm_compute_solve_diagnostics[live]"
+                             : nv ? "atm_compute_solve_diagnostics[-v]" : "atm_compute_solve_diagnostics",
+                     [&] { return launch_solve_diagnostics(S, st, 0, rk_step, live ? 7 : 3, nv); });
         }
     }
     if (c->transport)  // after the last stage's recover: ruAvg / wwAvg / rho_zz of the step
@@ -1375,7 +1382,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusecopy") == 0) c->fusecopy = value ? 1 : 0;
         else if (name && std::strcmp(name, "defer4") == 0) c->defer4 = value ? 1 : 0;
-        else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value ? 1 : 0;
+        else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value < 0 ? 0 : value > 2 ? 2 : value;
         else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;

@@ -16,7 +16,7 @@ roofline.achieved divides by the measured launch time.
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
-          ddx=False, ntu=False):
+          ddx=False, ntu=False, live=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -171,6 +171,13 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             reads += ["edgesOnEdge_ECP", "nEdgesOnEdge", "weightsOnEdge"]
             writes.append("v")
         return reads, writes
+    if task == "atm_compute_solve_diagnostics" and live:
+        # option ntu (stage 1's call, the last stage at rk_step > 0): the diagnostics that stage's dyn_tend
+        # reads, alone -- ke, pv_edge (pv_vertex, read back by the edge kernel); no credit for the dead
+        # h_edge, ke_edge, divergence, vorticity nor for h, which only h_edge reads
+        return (["u", "cellsOnEdge", "dcEdge", "dvEdge", "verticesOnEdge", "edgesOnCell", "edgesOnCellSign",
+                 "invAreaCell", "nEdgesOnCell", "edgesOnVertex", "edgesOnVertexSign", "fVertex", "invAreaTriangle"],
+                ["pv_edge", "ke", "pv_vertex"])
     if task == "atm_compute_solve_diagnostics":
         writes = ["h_edge", "ke_edge", "pv_edge", "divergence", "ke", "vorticity", "pv_vertex"]
         if reconstruct_v:
@@ -306,9 +313,9 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                 ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1}, 4),
                 ("atm_divergence_damping_3d", {}, 7)]
-    # (option ntu: stage 0's solve_diagnostics is dead and not run)
+    # (option ntu: stage 0's solve_diagnostics is dead and not run, stage 1's stores what stage 2 reads)
     out += [
-            ("atm_compute_solve_diagnostics", {}, 1 if ntu else 2),
+            ("atm_compute_solve_diagnostics", {"live": True} if ntu else {}, 1 if ntu else 2),
             ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
             ("atm_rk_dynamics_substep_finish", {}, 1)]
     return out

@@ -275,4 +275,9 @@ def test_b_alg_ntu():
     b1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1)
     c1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1, ntu=True)
     sd = roofline.b_alg("atm_compute_solve_diagnostics", dims)
-    assert s0 - s1 == (a - b) + (b1 - c1) + sd  # (+ stage 0's dead solve_diagnostics)
+    sl = roofline.b_alg("atm_compute_solve_diagnostics", dims, live=True)
+    # (+ stage 0's dead solve_diagnostics, and the dead stores and reads of stage 1's)
+    assert s0 - s1 == (a - b) + (b1 - c1) + sd + (sd - sl)
+    r, w = roofline._sets("atm_compute_solve_diagnostics", live=True)
+    assert set(w) == {"ke", "pv_edge", "pv_vertex"} and "h" not in r and "u" in r
+    assert sd - sl >= 2 * e3 + 3 * c3  # h_edge, ke_edge, divergence, h (+ vorticity at the vertices)

@@ -112,18 +112,19 @@ def test_etile_keep_check_fast(x1_2562):
 
 
 # ---------------------------------------------------------------- option ntu
+@pytest.mark.parametrize("ntu", [1, 2])  # (2: stage 1's solve_diagnostics stores every diagnostic)
 @pytest.mark.parametrize("hfuse", [0, 2])  # (0: the large grids' launches, stage 0's solve_diagnostics skipped)
 @pytest.mark.parametrize("variant", ["random", "physical"])
 @pytest.mark.parametrize("exact", [0, 1])
 @pytest.mark.parametrize("L", [5, 56])
-def test_ntu_steps_bit_identical(x1_2562, L, exact, variant, hfuse):
+def test_ntu_steps_bit_identical(x1_2562, L, exact, variant, hfuse, ntu):
     """option ntu (atm_srk3, defer4 out): rk_step 0's edge kernel forms no tend_u -- dead there, the
     next stage's edge kernel rewrites it and no task in between reads it -- so every field after the
     step, tend_u included, has the same bits with the option on and off; exact mode = the oracle"""
     st = make_state(x1_2562, L, variant)
     steps = lambda ctx: [T.atm_srk3(ctx, 720.0, 1) for _ in range(2)]  # noqa: E731
     a, _ = _run(st, 0, exact, steps, ntu=0, hfuse=hfuse)
-    b, _ = _run(st, 0, exact, steps, ntu=1, hfuse=hfuse)
+    b, _ = _run(st, 0, exact, steps, ntu=ntu, hfuse=hfuse)
     bad = compare_states(b, a, rtol=0.0)
     assert not bad, bad[:6]
     if exact:
@@ -143,7 +144,9 @@ def test_ntu_only_where_dead(x1_2562):
     ref = st.copy()
     O.Oracle(ref).atm_compute_dyn_tend_work(0, 720.0)
     assert not compare_states(got, ref, rtol=0.0)
-    for dt in (720.0, 1.0):  # (dt = 1: stages 0 and 1 at rk_step 0, Q4 -- stage 0's solve is live)
+    # (dt = 1: stages 0 and 1 at rk_step 0, Q4 -- stage 0's solve is live; dt = 0.5: every stage at
+    # rk_step 0 -- stage 1's whole solve is live too)
+    for dt in (720.0, 1.0, 0.5):
         got, _ = _run(st, 0, 1, lambda ctx: T.atm_srk3(ctx, dt, 0), ntu=1, hfuse=0)
         ref = st.copy()
         O.Oracle(ref).atm_srk3(dt, 0)

@@ -21,6 +21,10 @@ NAMES = {
     "r06": ["k_dyn_A<64, true, false>", "k_dyn_A<64, false, false>", "k_dyn_B<64, true, false, true, false, true>",
             "k_dyn_B<64, false, false, true, true, true>", "k_dyn_B<64, false, false, true, false, true>",
             "k_dyn_C12<64, false, 4>", "k_dyn_Et<true, false, true>", "k_dyn_Et<false, false, true>"],
+    "r06ntu": ["k_dyn_A<64, true, false>", "k_dyn_E<64, false, false, false, true, true>",
+               "k_dyn_B<64, true, false, true, false, true, true>", "k_dyn_A<64, false, false>",
+               "k_dyn_B<64, false, false, true, true, false, false>", "k_dyn_C12<64, false, 4>",
+               "k_dyn_E<64, true, false, false, true, true>", "k_dyn_E<64, false, false, false, true, false>"],
 }
 
 
@@ -49,7 +53,7 @@ def _write(tmp_path, pmc):
     return str(p)
 
 
-@pytest.mark.parametrize("layout", ["r05", "r06"])
+@pytest.mark.parametrize("layout", ["r05", "r06", "r06ntu"])
 def test_every_kernel_measured(tmp_path, layout):
     pmc = _fixture(layout)
     res = TD.decompose(TD.parse_kernels(_write(tmp_path, pmc)), layout, DIMS)
@@ -63,7 +67,7 @@ def test_every_kernel_measured(tmp_path, layout):
         assert all("X_F" not in d["arrays"] for d in res.values())
 
 
-@pytest.mark.parametrize("layout", ["r05", "r06"])
+@pytest.mark.parametrize("layout", ["r05", "r06", "r06ntu"])
 def test_fails_on_unmatched_missing_negative(tmp_path, layout):
     pmc = _fixture(layout)
     extra = dict(pmc, **{"k_dyn_B<64, false, true, true, false, true>": pmc[NAMES[layout][2]]})  # an MD B

@@ -15,7 +15,7 @@ correction of MI355X_MICROARCH.md), split into
 
 and B_alg (unpadded, the reference's read/write sets; mpasdyn/roofline.py).
 
-usage: python tools/traffic_decomp.py KERNELS.txt --layout r05|r06 [--round r06]
+usage: python tools/traffic_decomp.py KERNELS.txt --layout r05|r06|r06ntu [--round r06]
        [--dims 163842 491520 327680 56] [--lp 64] [--json OUT]
 KERNELS.txt is tools/pmc_kernels.py output over the FETCH_SIZE and WRITE_SIZE (and TCC) passes of
 one bench step (tools/gpu.sh pmc).  Layouts (the kernels of the benchmark path, every variant by its
@@ -24,6 +24,8 @@ template arguments):
          leaves D to stage 1's B (defer4: B's DIN variant), stage 2's B stores v (vdyn)
     r06  option etile: B forms no flux (its NOF variant), the tiled E (k_dyn_Et) forms each edge's flux
          from its tile's theta_m columns in LDS; no X_F
+    r06ntu  option ntu (round 6's default path): stage 0's B forms no tend_u and no flux, its E no theta
+         tendency; stage 1 is E's w alone; stage 2's B applies the deferred del4 and stores v
 The tool fails (exit status 2) when a dyn_tend kernel of the file matches no kernel of the layout,
 when a kernel of the layout is missing from the file, or when a kernel's measured bytes fall below
 its distinct bytes (a negative refetch: the layout's read / write set of that kernel is wrong)."""
@@ -121,6 +123,39 @@ for lk, ks in LAYOUTS["r05"].items():
         else:
             _r06[lk].append(k)
 LAYOUTS["r06"] = _r06
+# r06ntu (option ntu, the round-6 default path; k_dyn_B<LP, RK0, MD, HF, DIN, NOF, NTU>,
+# k_dyn_E<LP, RK0, SELF, MD, HF, NTH>): stage 0 (rk_step 0) -- B forms no tend_u and no flux (NOF, NTU:
+# the pressure gradient, del2 and setup's copies), E no theta tendency (NTH: w, tend_w_euler and
+# tend_theta_euler with their del4); stage 1 (rk_step > 0) -- E's w alone; stage 2 -- A, B with the
+# deferred del4 (DIN) and v (vdyn), E
+B_RK0_NTU_R = ["u", "ru", "rho_edge", "cqu", "zxu", "pressure_p", "zz", "dpdz", "divergence", "kdiff", "vorticity"]
+E_RK0_NTH_R = ["X_wc", "rw", "pressure_p", "dpdz", "theta_m", "tend_w_euler", "tend_theta_euler", "rho_zz", "cqw",
+               "delsq_w", "delsq_theta"]
+E_RK1_NTH_R = ["uReconstructZonal", "uReconstructMeridional", "rw", "ru:C", "theta_m", "tend_w_euler",
+               "tend_theta_euler", "rho_zz"]
+LAYOUTS["r06ntu"] = {
+    "rk0": A_KS + [
+        ("B", "k_dyn_B", lambda t: t[1:] == (1, 0, 1, 0, 1, 1), B_RK0_NTU_R,
+         ["tend_u_euler", "delsq_u", "ru_save", "u_2"], ("E", E_EB)),
+        C_K,
+        ("E", "k_dyn_E", lambda t: t[1] == 1 and t[3:] == (0, 1, 1), E_RK0_NTH_R,
+         ["w", "tend_w_euler", "tend_theta_euler"], ("C", C_REC + 48 * 2 + 8)),
+    ],
+    "rk1ntu": [
+        ("E", "k_dyn_E", lambda t: t[1] == 0 and t[3:] == (0, 1, 1), E_RK1_NTH_R, ["w"], ("C", C_REC + 16 + 8 + 8)),
+    ],
+    "rk1dinv": [
+        A_K1,
+        ("B", "k_dyn_B", lambda t: t[1:] == (0, 0, 1, 1, 0, 0),
+         B_RK1_R + ["theta_m", "ru_save", "theta_m_save", "delsq_divergence", "delsq_vorticity"],
+         ["X_F", "tend_u", "tend_u_euler", "v"], ("E", E_EB + W_EDGE + ADV_EDGE)),
+        ("E", "k_dyn_E", lambda t: t[1] == 0 and t[3:] == (0, 1, 0), E_RK1_R + ["ru:C", "X_F"], E_W,
+         ("C", C_REC + 16 + 8 + 8)),
+    ],
+}
+# B_alg of each launch kind (mpasdyn/roofline.py); default: rk_step and stage 0's copies
+BALG_KW = {"r06ntu": {"rk0": {"rk_step": 0, "copy": True, "defer_out": True, "ntu": True},
+                      "rk1ntu": {"rk_step": 1, "ntu": True}, "rk1dinv": {"rk_step": 1, "store_v": True}}}
 SCRATCH = {"X_wc", "X_F"}
 
 
@@ -208,8 +243,8 @@ def decompose(pmc, layout, dims, lp=64):
         for k in ks:  # (mesh rows once per kernel: a floor)
             for q in range(0, len(k[5]), 2):
                 task += k[5][q + 1] * n[k[5][q]]
-        balg = roofline.b_alg("atm_compute_dyn_tend_work", (nC, nE, nV, L), rk_step=0 if lk == "rk0" else 1,
-                              copy=(lk == "rk0"))
+        kw = BALG_KW.get(layout, {}).get(lk, {"rk_step": 0 if lk == "rk0" else 1, "copy": lk == "rk0"})
+        balg = roofline.b_alg("atm_compute_dyn_tend_work", (nC, nE, nV, L), **kw)
         res[lk] = {"kernels": per, "B_alg_GB": balg / 1e9, "compulsory_GB": task / 1e9,
                    "intermediates_GB": (tot_kernel - task) / 1e9, "refetch_GB": (meas_tot - tot_kernel) / 1e9,
                    "measured_GB": meas_tot / 1e9, "measured_over_B_alg": meas_tot / balg}
