@@ -375,6 +375,7 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
              "atm_compute_solve_diagnostics[live]": {"live": True},
              "hfuse[solve_e+vert_imp]": {"pair": "solve_e+vert_imp"},
              "hfuse[acoustic+solve_vc]": {"pair": "acoustic+solve_vc"},
+             "hfuse[acoustic-st+solve_vc]": {"pair": "acoustic-st+solve_vc"},
              "hfuse[solve_e+dyn_A]": {"pair": "solve_e+dyn_A"},
              "hfuse[solve_e+vert_imp+dyn_A]": {"pair": "solve_e+vert_imp+dyn_A"},
              "atm_compute_dyn_tend_work[rk>0-A]": {"rk_step": 1, "noA": True},
@@ -405,13 +406,19 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
     variants, tasks = {}, {}
     for name, (calls, ms) in rep.items():
         task = name.split("[")[0]
+        # ("-st]": option ntu's acoustic launch that stores no acoustic state, the last substep of a stage
+        # before the step's last)
+        base, nst = (name[:-4] + "]", True) if name.endswith("-st]") else (name, False)
         if task == NORTH_STAR and "[" in name:
             kw = dyn_kw(name)
-        elif name.endswith("-old]"):  # a fused acoustic launch that leaves rtheta_pp_old (mpas_ctx.cpp)
-            kw = dict(kw_of.get(name[:-5] + "]", {}), wold=False)
+        elif base.endswith("-old]"):  # a fused acoustic launch that leaves rtheta_pp_old (mpas_ctx.cpp)
+            kw = dict(kw_of.get(base[:-5] + "]", {}), wold=False)
         else:
-            kw = dict(kw_of.get(name, {}))
-        if ddx and (task == "atm_advance_acoustic_step_work" or name == "hfuse[acoustic+solve_vc]"):
+            kw = dict(kw_of.get(base, {}))
+        if nst:
+            kw["nst"] = True
+        if ddx and (task == "atm_advance_acoustic_step_work" or name in ("hfuse[acoustic+solve_vc]",
+                                                                         "hfuse[acoustic-st+solve_vc]")):
             kw["ddx"] = True  # (option smlsum: the acoustic launches read rw_save - rw from X_Dd)
         if physics and task == "atm_advance_acoustic_step_work":
             kw["physics"] = 1  # the acoustic task's MPAS form also updates ru_p / ruAvg

@@ -89,9 +89,12 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * "eoe_same"); "ntu" = 1 (default; reference semantics, with defer4) leaves out what the stages
  * before the step's last would compute only for values no task reads before the last stage
  * rewrites them: their dyn_tend forms no tend_u and no theta tendencies (tend_theta,
- * tend_rtheta_adv, rthdynten), stage 0's solve_diagnostics is not run and stage 1's stores ke and
+ * tend_rtheta_adv, rthdynten), the last acoustic substep of stages 0 and 1 stores no rho_pp,
+ * rtheta_pp, rw_p or wwAvg (the next stage's first substep sets them; the damping reads the div
+ * that substep stores), stage 0's solve_diagnostics is not run and stage 1's stores ke and
  * pv_edge alone (its divergence, vorticity, h_edge and ke_edge are dead); every field after a step
- * is bit-identical with it off; 2 = the same with stage 1's solve_diagnostics whole (A/B);
+ * is bit-identical with it off; 2 = the same with stage 1's solve_diagnostics whole, 3 = with the
+ * acoustic state stored (A/Bs);
  * "etile" = 1 (default 0, measured, not kept) forms dyn_tend's theta advection fluxes from tiles
  * of cells in LDS ("etcells", "etclo", "etmode", "etthreads"; read-only "etile_active");
  * "bsplit" (fast path, speed only) puts dyn_tend's per-edge theta flux (and the MPAS dynamics' w

@@ -263,8 +263,12 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
 
     // :1615-1636
     const double rtpo = (small_step == 0) ? 0 : rtp;
+    // wold bit 1 (atm_srk3 option ntu, MODE != 0: the last substep of a stage before the step's last):
+    // this substep's rho_pp, rtheta_pp, rw_p and wwAvg are dead -- the next stage's first substep sets
+    // them (:1615-1636) before any task reads them, and the damping reads this substep's div (X_dvA)
+    const bool nst = MODE != 0 && (wold & 2);
     // (level L: the kept value, keep tails in mpas_dev.h -- every line of the column whole)
-    if (MODE == 0 || wold) colk(fw(S, F_rtheta_pp_old), c) = KEEPW(rtpo, keepv<LP>(S, F_rtheta_pp_old, KC, c));
+    if (MODE == 0 || (wold & 1)) colk(fw(S, F_rtheta_pp_old), c) = KEEPW(rtpo, keepv<LP>(S, F_rtheta_pp_old, KC, c));
     // MODE 1/2: this substep's div (:1755) for the damping applied by the next substep
     auto store_div = [&](double rtp_new) {
         if constexpr (MODE != 0) colk(fw(S, X_dvA), c) = kl ? -(rtp_new - rtpo) : 0.0;
@@ -285,10 +289,12 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             rwp = rwp + dts * tw;
             ww = ww + 0.5 * (1.0 + epssm) * rwp;
         }
-        colk(rpp_f, c) = KEEPW(rpp, keepv<LP>(S, F_rho_pp, KC, c));
-        colk(rtp_f, c) = KEEPW(rtp, keepv<LP>(S, F_rtheta_pp, KC, c));
-        colk(rwp_f, c) = PADW(rwp);
-        colk(ww_f, c) = PADW(ww);
+        if (!nst) {
+            colk(rpp_f, c) = KEEPW(rpp, keepv<LP>(S, F_rho_pp, KC, c));
+            colk(rtp_f, c) = KEEPW(rtp, keepv<LP>(S, F_rtheta_pp, KC, c));
+            colk(rwp_f, c) = PADW(rwp);
+            colk(ww_f, c) = PADW(ww);
+        }
         store_div(rtp);
         return;
     }
@@ -452,9 +458,11 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
     if (k < L && k > 0) ww = ww + 0.5 * (1.0 - epssm) * rwold + 0.5 * (1.0 + epssm) * x;
     // (paired 16-B stores, every lane; level L of rho_pp / rtheta_pp keeps its value)
     const double rtp_new = ts - rdzw * (coftz_p * rwp_p - coftz * x);
-    put2f<LP>(rpp_f, c, rtp_f, c, k, KEEPW(rs - cofrz * (rwp_p - x), keepv<LP>(S, F_rho_pp, KC, c)),
-             KEEPW(rtp_new, keepv<LP>(S, F_rtheta_pp, KC, c)));
-    put2f<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww));
+    if (!nst) {
+        put2f<LP>(rpp_f, c, rtp_f, c, k, KEEPW(rs - cofrz * (rwp_p - x), keepv<LP>(S, F_rho_pp, KC, c)),
+                 KEEPW(rtp_new, keepv<LP>(S, F_rtheta_pp, KC, c)));
+        put2f<LP>(rwp_f, c, ww_f, c, k, PADW((k < L) ? x : rwp), PADW(ww));
+    }
     store_div(rtp_new);
 }
 template <int LP, bool EXACT, bool SELF, bool FIRST, bool MPASV, int MODE, bool TME, int SML>
@@ -662,8 +670,8 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     else if (mode == 2) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, X_dvB);
     else if (sml == 1) HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m, F_u_tend);
     else HALO_RUN_R1(S, st, run, F_ru_p, F_ru_p, F_theta_m);
-    if (mode == 0 || wold) HALO_WROTE(S, F_rtheta_pp_old);
-    HALO_WROTE(S, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);
+    if (mode == 0 || (wold & 1)) HALO_WROTE(S, F_rtheta_pp_old);
+    if (!(mode && (wold & 2))) HALO_WROTE(S, F_rho_pp, F_rtheta_pp, F_rw_p, F_wwAvg);  // (wold bit 1: not stored)
     if (sml) HALO_WROTE(S, F_w);
     if (mode) HALO_WROTE(S, X_dvA);
     // MODE 2: the damped ru_p of every edge an owned cell owns (X_eown) -- the owned edges

@@ -1026,14 +1026,22 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                 const int sm = (sml && small_step == 0) ? (smls ? 2 : 1) : 0;
                 // rtheta_pp_old is read by the separate damping only: the fused one reads the
                 // stored div, so the step's last substep alone leaves it (option fusedamp)
-                const int wold = (done_acoustic + 1 == n_acoustic) ? 1 : 0;
+                // option ntu (bit 1): a stage's last substep before the step's last stage leaves rho_pp,
+                // rtheta_pp, rw_p and wwAvg unstored -- the next stage's first substep sets them before
+                // any task reads them (:1615-1636), and the damping reads the stored div
+                const int nst = (c->ntu == 1 || c->ntu == 2) && rk_step < 2 && small_step == n_small - 1 ? 2 : 0;
+                const int wold = ((done_acoustic + 1 == n_acoustic) ? 1 : 0) | nst;
                 if (hf2 && rk_step < 2 && mode == 2 && small_step > 0 && small_step == n_small - 1) {
-                    run_task(c, "hfuse[acoustic+solve_vc]", [&] {
+                    run_task(c, nst ? "hfuse[acoustic-st+solve_vc]" : "hfuse[acoustic+solve_vc]", [&] {
                         return launch_hf_acoustic_solve_vc(S, st, dts, small_step, c->exact, coef_prev, wold, smls ? 1 : 0);
                     });
                     vc_done = true;
                 } else {
-                    run_task(c, acoustic_name(small_step, pending, sm, !wold),
+                    // ("-st": option ntu's launch that stores no acoustic state, bench.py's accounting)
+                    const std::string an = nst ? std::string(acoustic_name(small_step, pending, sm, !(wold & 1))).insert(
+                                                     std::strlen(acoustic_name(small_step, pending, sm, !(wold & 1))) - 1, "-st")
+                                               : std::string(acoustic_name(small_step, pending, sm, !(wold & 1)));
+                    run_task(c, an.c_str(),
                              [&] { return launch_acoustic(S, st, dts, small_step, c->exact, mode, coef_prev, tme, sm, wold,
                                                           smls ? 1 : 0); });
                 }
@@ -1091,8 +1099,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             // pv_edge; its divergence, vorticity, h_edge and ke_edge have no reader before the last stage's
             // solve_diagnostics rewrites them (dyn_tend reads divergence and vorticity at rk_step 0 only)
             const int rk2 = schedule == 0 ? (int)rk_sub_timestep[2] : 2;
-            // (ntu = 2: the dead tendencies alone, every diagnostic stored -- the A/B of this part)
-            const bool live = c->ntu == 1 && S.physics == 0 && rk_step == 1 && rk2 != 0;
+            // (ntu = 2: every diagnostic stored, 3: every acoustic state stored -- the A/Bs of these parts)
+            const bool live = (c->ntu == 1 || c->ntu == 3) && S.physics == 0 && rk_step == 1 && rk2 != 0;
             run_task(c, live ? "atm_compute_solve_diagnostics[live]"
                              : nv ? "atm_compute_solve_diagnostics[-v]" : "atm_compute_solve_diagnostics",
                      [&] { return launch_solve_diagnostics(S, st, 0, rk_step, live ? 7 : 3, nv); });
@@ -1382,7 +1390,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusesetup") == 0) c->fusesetup = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusecopy") == 0) c->fusecopy = value ? 1 : 0;
         else if (name && std::strcmp(name, "defer4") == 0) c->defer4 = value ? 1 : 0;
-        else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value < 0 ? 0 : value > 2 ? 2 : value;
+        else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value < 0 ? 0 : value > 3 ? 3 : value;
         else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;

@@ -16,7 +16,7 @@ roofline.achieved divides by the measured launch time.
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
-          ddx=False, ntu=False, live=False):
+          ddx=False, ntu=False, live=False, nst=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -30,6 +30,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                  "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False,
                                                                            "ddx": ddx}),
                                        ("atm_compute_solve_diagnostics", {"part": "vc"})),
+                 "acoustic-st+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True,
+                                                                              "wold": False, "ddx": ddx, "nst": True}),
+                                          ("atm_compute_solve_diagnostics", {"part": "vc", "live": True})),
                  "solve_e+dyn_A": (e, dA),
                  "solve_e+vert_imp+dyn_A": (e, vi, dA),
                  "setup+dyn_A": (("atm_rk_integration_setup", {"fused": True, "copy": True}),
@@ -141,6 +144,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         # (wold False: a fused launch of option fusedamp other than the step's last, which leaves
         # rtheta_pp_old unwritten -- the fused damping reads the stored div instead)
         writes = (["rtheta_pp_old"] if wold else []) + ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+        if nst:  # option ntu: a stage's last substep before the last stage -- its acoustic state is dead
+            writes = [w for w in writes if w not in ("rho_pp", "rtheta_pp", "rw_p", "wwAvg")]
+            reads = [r for r in reads if r != "wwAvg"]  # (read only for the dead wwAvg)
         if physics:  # the MPAS form (option physics = 1): the ru_p / ruAvg update of :1581-1613
             reads += ["tend_u", "tend_theta", "c_tri", "gamma_tri", "specZoneMaskEdge"]
             if small_step != 0:
@@ -160,6 +166,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
     if task == "atm_divergence_damping_3d":
         return (["rtheta_pp", "rtheta_pp_old", "theta_m", "ru_p", "cellsOnEdge", "isShared", "specZoneMaskEdge"],
                 ["ru_p"])
+    if task == "atm_compute_solve_diagnostics" and part == "vc" and live:  # (ntu: ke, pv_vertex alone)
+        return (["u", "dcEdge", "dvEdge", "edgesOnCell", "edgesOnCellSign", "invAreaCell", "nEdgesOnCell",
+                 "edgesOnVertex", "edgesOnVertexSign", "fVertex", "invAreaTriangle"], ["ke", "pv_vertex"])
     if task == "atm_compute_solve_diagnostics" and part == "vc":  # its vertex / cell kernel alone
         return (["u", "dcEdge", "dvEdge", "edgesOnCell", "edgesOnCellSign", "invAreaCell", "nEdgesOnCell",
                  "edgesOnVertex", "edgesOnVertexSign", "fVertex", "invAreaTriangle"],
@@ -298,14 +307,14 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
             out += [("atm_set_smlstep_pert_variables_work", {"part": "flux"}, 1)]
         out += [("atm_advance_acoustic_step_work", {"small_step": 0, **sm, "wold": False, **dd}, 1),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, **sm, "wold": False, **dd}, 2),
-                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False, **dd}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False, **dd}, 1 if ntu else 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, **dd}, 1),
                 ("atm_divergence_damping_3d", {}, 1)]
     elif fusedamp:
         out += [("atm_set_smlstep_pert_variables_work", {}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "wold": False}, 1),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "damp": True, "wold": False}, 2),
-                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False}, 1 if ntu else 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True}, 1),
                 ("atm_divergence_damping_3d", {}, 1)]
     else:
@@ -313,7 +322,11 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                 ("atm_advance_acoustic_step_work", {"small_step": 0}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1}, 4),
                 ("atm_divergence_damping_3d", {}, 7)]
-    # (option ntu: stage 0's solve_diagnostics is dead and not run, stage 1's stores what stage 2 reads)
+    # (option ntu: the last substep of stages 0 and 1 stores no acoustic state; stage 0's
+    # solve_diagnostics is dead and not run, stage 1's stores what stage 2 reads)
+    if ntu and fusedamp:
+        out += [("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False, "nst": True,
+                                                    "ddx": bool(fusesml and smlsum)}, 2)]
     out += [
             ("atm_compute_solve_diagnostics", {"live": True} if ntu else {}, 1 if ntu else 2),
             ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),

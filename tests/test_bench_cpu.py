@@ -276,8 +276,12 @@ def test_b_alg_ntu():
     c1 = roofline.b_alg("atm_compute_dyn_tend_work", dims, rk_step=1, ntu=True)
     sd = roofline.b_alg("atm_compute_solve_diagnostics", dims)
     sl = roofline.b_alg("atm_compute_solve_diagnostics", dims, live=True)
-    # (+ stage 0's dead solve_diagnostics, and the dead stores and reads of stage 1's)
-    assert s0 - s1 == (a - b) + (b1 - c1) + sd + (sd - sl)
+    # (+ stage 0's dead solve_diagnostics, the dead stores and reads of stage 1's, and the acoustic
+    # state the last substep of stages 0 and 1 leaves unstored)
+    ac = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=1, damp=True, wold=False, ddx=True)
+    an = roofline.b_alg("atm_advance_acoustic_step_work", dims, small_step=1, damp=True, wold=False, ddx=True, nst=True)
+    assert ac - an == 5 * c3  # rho_pp, rtheta_pp, rw_p, wwAvg; the wwAvg read
+    assert s0 - s1 == (a - b) + (b1 - c1) + sd + (sd - sl) + 2 * (ac - an)
     r, w = roofline._sets("atm_compute_solve_diagnostics", live=True)
     assert set(w) == {"ke", "pv_edge", "pv_vertex"} and "h" not in r and "u" in r
     assert sd - sl >= 2 * e3 + 3 * c3  # h_edge, ke_edge, divergence, h (+ vorticity at the vertices)

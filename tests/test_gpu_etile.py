@@ -112,7 +112,8 @@ def test_etile_keep_check_fast(x1_2562):
 
 
 # ---------------------------------------------------------------- option ntu
-@pytest.mark.parametrize("ntu", [1, 2])  # (2: stage 1's solve_diagnostics stores every diagnostic)
+# (2: stage 1's solve_diagnostics stores every diagnostic; 3: the stages' last substeps store the acoustic state)
+@pytest.mark.parametrize("ntu", [1, 2, 3])
 @pytest.mark.parametrize("hfuse", [0, 2])  # (0: the large grids' launches, stage 0's solve_diagnostics skipped)
 @pytest.mark.parametrize("variant", ["random", "physical"])
 @pytest.mark.parametrize("exact", [0, 1])
