@@ -214,7 +214,7 @@ def decompose(pmc, layout, dims, lp=64):
     res = {}
     for lk, ks in lay.items():
         per, tot_kernel, meas_tot = [], 0.0, 0.0
-        task_r, task_w = set(), set()
+        task_r, task_w = {}, set()  # (task_r: array -> its bytes; "f:C" counts nCells columns unless read whole)
         for label, kern, pred, rd, wr, mesh in ks:
             m = [v for name, v in pmc.items() if (lk, label) in claimed.get(name, ())]
             if not m:
@@ -224,7 +224,9 @@ def decompose(pmc, layout, dims, lp=64):
                 comp += mesh[q + 1] * n[mesh[q]]
             if label == "C":
                 comp += (12 + 24 + 24 + 8) * nV  # the vertex blocks' rows
-            task_r |= set(fname(f) for f in rd if fname(f) not in task_w)
+            for f in rd:
+                if fname(f) not in task_w:
+                    task_r[fname(f)] = max(task_r.get(fname(f), 0.0), col(f))
             task_w |= set(wr)
             meas = 1e3 * sum(2 * x["FETCH_SIZE"] + x["WRITE_SIZE"] for x in m)  # KB -> B; FETCH x 2 (gfx950)
             hit = None
@@ -239,7 +241,7 @@ def decompose(pmc, layout, dims, lp=64):
                         "l2_hit": hit})
             tot_kernel += comp
             meas_tot += meas
-        task = sum(col(f) for f in task_r - SCRATCH) + sum(col(f) for f in task_w - SCRATCH)
+        task = sum(b for f, b in task_r.items() if f not in SCRATCH) + sum(col(f) for f in task_w - SCRATCH)
         for k in ks:  # (mesh rows once per kernel: a floor)
             for q in range(0, len(k[5]), 2):
                 task += k[5][q + 1] * n[k[5][q]]
