@@ -387,7 +387,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
              "atm_advance_acoustic_step_work[ss0+sml+damp]": {"small_step": 0, "damp": True, "sml": True},
              "atm_advance_acoustic_step_work[ss>0+damp]": {"small_step": 1, "damp": True},
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
-             "atm_recover_large_step_variables_work[rk2]": {"rk_step": 2}}
+             "atm_recover_large_step_variables_work[rk2]": {"rk_step": 2},
+             "atm_recover_large_step_variables_work[rk<2-avg]": {"rk_step": 0, "navg": True}}
     def dyn_kw(name):  # atm_compute_dyn_tend_work[rk0|rk>0 (+copy) (+d4o) (+d4i) (-A)] (mpas_ctx.cpp srk3)
         tag = name[name.index("[") + 1:-1]
         kw = {"rk_step": 0 if tag.startswith("rk0") else 1}
@@ -681,7 +682,7 @@ def main():
     fsml = fused and bool(ctx.get_option("fusesml")) and not args.physics
     fcopy = fsetup and bool(ctx.get_option("fusecopy"))  # (decomposed and MPAS forms too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
-    ntu = bool(ctx.get_option("ntu")) and not args.physics
+    ntu = bool(ctx.get_option("ntu"))  # (the MPAS forms: the dead diagnostics and averages only)
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
                                  smls, ntu)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9

@@ -257,13 +257,13 @@ __device__ __forceinline__ void finish64_body(const DevState& S, int substep, in
 // MD: the MPAS dynamics (physics = 2, ora_mpas_solve_diagnostics): divergence += s * u (Q9),
 // h = rho_zz and rho_edge = h_edge (Q2: MPAS-A passes diag%rho_edge as h_edge), v over
 // every edgesOnEdge entry (Q23)
-// LIVE (atm_srk3 option ntu, reference semantics: stage 1's call, the step's last stage at rk_step > 0):
-// only what the last stage's dyn_tend reads is stored -- ke, and pv_vertex for pv_edge.  vorticity,
-// divergence, h_edge and ke_edge have no reader before the last stage's solve_diagnostics rewrites them
-// (dyn_tend reads divergence and vorticity at rk_step 0 only; nothing reads h_edge or ke_edge)
+// LIVE (atm_srk3 option ntu: a call before the last stage's, the next stage at rk_step > 0): only what
+// the next stage's dyn_tend reads is stored -- ke, and pv_vertex for pv_edge (MD: rho_edge too).
+// vorticity, divergence, h_edge and ke_edge have no reader before the last stage's solve_diagnostics
+// rewrites them (dyn_tend reads divergence and vorticity at rk_step 0 only; nothing reads h_edge or
+// ke_edge)
 template <int LP, int EPW, bool MD, bool LIVE = false>
 __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int hollingsworth_part, Blk bk) {
-    static_assert(!LIVE || !MD, "the dead diagnostics: reference semantics");
     const int L = S.L;
     const double* u = fd(S, F_u);
     const double *dcEdge = fd(S, F_dcEdge), *dvEdge = fd(S, F_dvEdge);
@@ -380,10 +380,10 @@ __device__ __forceinline__ void solve_vc_body(const DevState& S, int nVB, int ho
 // EPW consecutive edges per column slot (option "epw"): the loads of all of them are issued
 // before the first store; the paired 16-B stores write h_edge with ke_edge and pv_edge with
 // v (or alone) -- every lane takes part (put2), level L keeps its value
-// LIVE (see solve_vc_body): pv_edge alone
+// LIVE (see solve_vc_body): pv_edge alone (MD: and rho_edge)
 template <int LP, bool RECON_V, bool MD, int EPW, bool LIVE = false>
 __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
-    static_assert(!LIVE || (!MD && !RECON_V), "the dead diagnostics: reference semantics, no v");
+    static_assert(!LIVE || !RECON_V, "the dead diagnostics: no v");
     ColMapN<LP, EPW> m(S, KE, bk);
     const int L = S.L, k = m.k;
     const double *h = fd(S, MD ? F_rho_zz : F_h), *u = fd(S, F_u), *pvv = fd(S, F_pv_vertex);
@@ -395,7 +395,7 @@ __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
         ee[j] = e;
         const int* coe = fi(S, F_cellsOnEdge) + (size_t)e * 2;
         const int* voe = fi(S, F_verticesOnEdge) + (size_t)e * 2;
-        if constexpr (LIVE) h1[j] = h2[j] = 0.0;
+        if constexpr (LIVE && !MD) h1[j] = h2[j] = 0.0;
         else gather2s<LP>(h, coe[0], coe[1], k, h1[j], h2[j]);
         gather2s<LP>(pvv, voe[0], voe[1], k, pv1[j], pv2[j]);
     }
@@ -438,6 +438,7 @@ __device__ __forceinline__ void solve_e_body(const DevState& S, Blk bk) {
         // (padding levels k > L: zeros; level L: the kept values, keep tails in mpas_dev.h)
         auto kL = [&](int f) { return keepv<LP>(S, f, KE, e); };
         if constexpr (LIVE) {
+            if (MD) colk(fw(S, F_rho_edge), e) = KEEPW(0.5 * (h1[j] + h2[j]), kL(F_rho_edge));
             colk(fw(S, F_pv_edge), e) = KEEPW(0.5 * (pv1[j] + pv2[j]), kL(F_pv_edge));
             continue;
         }

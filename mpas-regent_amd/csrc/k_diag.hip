@@ -26,7 +26,9 @@ struct RecK {
 // recovered values (:1800-1820 with Q24 fixed), w(0) = w(L) = 0, rw / wwAvg at levels 0 and L
 // the values they hold (wwAvg: just loaded; rw: its keep tails), every other field at level L
 // its keep tail, the padding levels 0.0 (mpas_dev.h keep tails)
-template <int LP>
+// NAVG (atm_srk3 option ntu, a stage before the last): wwAvg is dead -- the next stage's first
+// acoustic substep sets it (:1625-1630) before any task reads it -- and is neither read nor stored
+template <int LP, bool NAVG = false>
 __device__ __forceinline__ void recover_cells_mpas(const DevState& S, const RecK& a, int c, int k, double zz,
                                                    double zz_m, double fzm, double fzp, double rps, double rpp,
                                                    double rb, double ww, double rws, double rwp, double rtps,
@@ -42,7 +44,7 @@ __device__ __forceinline__ void recover_cells_mpas(const DevState& S, const RecK
     const double w = rw / (fzm * zz + fzp * zz_m);
     colk(fw(S, F_rho_p), c) = KEEPW(rho_p, kL(F_rho_p));
     colk(fw(S, F_rho_zz), c) = KEEPW(rho_zz, kL(F_rho_zz));
-    colk(fw(S, F_wwAvg), c) = (k == 0 || k == L) ? ww : PADW(wwAvg);
+    if (!NAVG) colk(fw(S, F_wwAvg), c) = (k == 0 || k == L) ? ww : PADW(wwAvg);
     colk(fw(S, F_rw), c) = KEEPW0(rw, keepv<LP>(S, F_rw, KC, c, true), kL(F_rw));
     colk(fw(S, F_w), c) = (k == 0 || k >= L) ? 0.0 : w;
     if (a.rk_step == 2) {
@@ -59,8 +61,9 @@ __device__ __forceinline__ void recover_cells_mpas(const DevState& S, const RecK
     }
 }
 
-template <int LP, bool MPASV>
+template <int LP, bool MPASV, bool NAVG = false>
 __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
+    static_assert(!NAVG || MPASV, "the dead averages: the MPAS forms (the reference semantics never recover)");
     ColMap<LP> m(S, KC);
     const int L = S.L, k = m.k, c = m.ent;
     if (m.blk == 0 && (int)threadIdx.x < L) fw(S, F_rho_zz)[(size_t)S.nCells * LP + lpos(LP, threadIdx.x)] = 1.0;
@@ -69,7 +72,7 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double zz = col_rd<LP>(fd(S, F_zz), c, k, L), zz_m = lvl_dn<LP>(zz, k);
     const double rps = colk(fd(S, F_rho_p_save), c), rpp = colk(fd(S, F_rho_pp), c), rb = colk(fd(S, F_rho_base), c);
-    const double ww = colk(fd(S, F_wwAvg), c), rws = colk(fd(S, F_rw_save), c), rwp = colk(fd(S, F_rw_p), c);
+    const double ww = NAVG ? 0.0 : colk(fd(S, F_wwAvg), c), rws = colk(fd(S, F_rw_save), c), rwp = colk(fd(S, F_rw_p), c);
     const double rtps = colk(fd(S, F_rtheta_p_save), c), rtpp = colk(fd(S, F_rtheta_pp), c);
     const double rtb = colk(fd(S, F_rtheta_base), c);
     const double rtd = a.rk_step == 2 ? colk(fd(S, F_rt_diabatic_tend), c) : 0.0;
@@ -77,7 +80,7 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
     if (MPASV && k == L) keep_put<LP>(S, F_w, KC, c, 0.0);  // (w's level L changes: its keep tail too)
     if (MPASV) {  // every level of every column written (level L / 0 with their kept values, the
                   // padding with zeros: keep tails, mpas_dev.h) -- no partially written line
-        recover_cells_mpas<LP>(S, a, c, k, zz, zz_m, fzm, fzp, rps, rpp, rb, ww, rws, rwp, rtps, rtpp, rtb, rtd, exb);
+        recover_cells_mpas<LP, NAVG>(S, a, c, k, zz, zz_m, fzm, fzp, rps, rpp, rb, ww, rws, rwp, rtps, rtpp, rtb, rtd, exb);
         return;
     }
     if (!kl) return;
@@ -112,22 +115,25 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
 }
 
 // :1830-1837: ruAvg, ru (Q24: ru_save * ru_p; MPASV: ru_save + ru_p), u from the new rho_zz
-template <int LP, bool MPASV>
+// NAVG (see recover_cells_mpas): ruAvg is dead -- the next stage's first substep sets it
+// (k_acoustic_ru FIRST) -- and is neither read nor stored
+template <int LP, bool MPASV, bool NAVG = false>
 __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
+    static_assert(!NAVG || MPASV, "the dead averages: the MPAS forms");
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO || (!MPASV && k >= L)) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
     const double* rz = fd(S, F_rho_zz);
     const double rz1 = colk(rz, cell1), rz2 = colk(rz, cell2);
-    const double ra = colk(fd(S, F_ruAvg), e), rus = colk(fd(S, F_ru_save), e), rup = colk(fd(S, F_ru_p), e);
+    const double ra = NAVG ? 0.0 : colk(fd(S, F_ruAvg), e), rus = colk(fd(S, F_ru_save), e), rup = colk(fd(S, F_ru_p), e);
     double ruAvg = ra;
     ruAvg *= a.invNs;
     ruAvg += rus;
     const double ru = MPASV ? rus + rup : rus * rup;
     if (MPASV) {  // (every level written: level L with the values it holds -- ruAvg just loaded, ru / u
                   // their keep tails -- the padding with zeros; mpas_dev.h keep tails)
-        colk(fw(S, F_ruAvg), e) = KEEPW(ruAvg, ra);
+        if (!NAVG) colk(fw(S, F_ruAvg), e) = KEEPW(ruAvg, ra);
         colk(fw(S, F_ru), e) = KEEPW(ru, keepv<LP>(S, F_ru, KE, e));
         colk(fw(S, F_u), e) = KEEPW(2 * ru / (rz1 + rz2), keepv<LP>(S, F_u, KE, e));
         return;
@@ -223,7 +229,7 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
 }
 
 template <int LP>
-static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_step, double dt) {
+static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg) {
     RecK a;
     a.invNs = 1 / (double)ns;
     a.dt = dt;
@@ -232,16 +238,21 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
     a.rcv = kRgas / (kCp - kRgas);
     a.rk_step = rk_step;
     const int nCB = col_blocks<LP>(S, KC);
-    if (nCB && S.physics) k_recover_cells<LP, true><<<nCB, 256, 0, st>>>(S, a);
+    const bool na = navg && S.physics;  // (option ntu: the averages of a stage before the last are dead)
+    if (nCB && na) k_recover_cells<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
+    else if (nCB && S.physics) k_recover_cells<LP, true><<<nCB, 256, 0, st>>>(S, a);
     else if (nCB) k_recover_cells<LP, false><<<nCB, 256, 0, st>>>(S, a);
-    HALO_WROTE(S, F_rho_p, F_rho_zz, F_wwAvg, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
+    HALO_WROTE(S, F_rho_p, F_rho_zz, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
+    if (!na) HALO_WROTE(S, F_wwAvg);
     auto ke = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
-        if (nb && X.physics) k_recover_edges<LP, true><<<nb, 256, 0, st>>>(X, a);
+        if (nb && na) k_recover_edges<LP, true, true><<<nb, 256, 0, st>>>(X, a);
+        else if (nb && X.physics) k_recover_edges<LP, true><<<nb, 256, 0, st>>>(X, a);
         else if (nb) k_recover_edges<LP, false><<<nb, 256, 0, st>>>(X, a);
     };
     HALO_RUN(S, st, ke, F_rho_zz);
-    HALO_WROTE(S, F_ruAvg, F_ru, F_u);
+    HALO_WROTE(S, F_ru, F_u);
+    if (!na) HALO_WROTE(S, F_ruAvg);
     auto kw = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KC);
         if (nb && X.physics) k_recover_w<LP, true><<<nb, 256, 0, st>>>(X);
@@ -251,8 +262,8 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
     HALO_WROTE(S, F_w);
     return hipGetLastError();
 }
-hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt) {
-    MPAS_LP_DISPATCH(S.LP, recover_lp, S, st, ns, rk_step, dt);
+hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg) {
+    MPAS_LP_DISPATCH(S.LP, recover_lp, S, st, ns, rk_step, dt, navg);
 }
 
 // ---------------------------------------------------------------- damping coefficients

@@ -48,13 +48,13 @@ __global__ __launch_bounds__(256) void k_solve_e(DevState S) {
 template <int LP, bool MD>
 static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts, int no_v) {
     // parts & 4 (atm_srk3 option ntu): the stored diagnostics the step's last stage reads, alone
-    const bool live = !MD && (parts & 4) && !hollingsworth;
+    const bool live = (parts & 4) && !hollingsworth;
     auto kvc = [&](const DevState& X) {  // vertex blocks, then cell blocks
         auto go = [&](auto epw) {
             constexpr int E = decltype(epw)::value;
             const int nv = col_blocks_n<LP, E>(X, KV), nb = nv + col_blocks_n<LP, E>(X, KC);
             if (!nb) return;
-            if (live) k_solve_vc<LP, E, false, true><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
+            if (live) k_solve_vc<LP, E, MD, true><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
             else k_solve_vc<LP, E, MD><<<nb, 256, 0, st>>>(X, nv, hollingsworth);
         };
         if (X.epw == 4) go(std::integral_constant<int, 4>{});
@@ -71,7 +71,7 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
             constexpr int E = decltype(epw)::value;
             const int nb = col_blocks_n<LP, E>(X, KE);
             if (!nb) return;
-            if (live && !rv) k_solve_e<LP, false, false, E, true><<<nb, 256, 0, st>>>(X);
+            if (live && !rv) k_solve_e<LP, false, MD, E, true><<<nb, 256, 0, st>>>(X);
             else if (rv) k_solve_e<LP, true, MD, E><<<nb, 256, 0, st>>>(X);
             else k_solve_e<LP, false, MD, E><<<nb, 256, 0, st>>>(X);
         };
@@ -109,7 +109,10 @@ static hipError_t solve_lp_md(const DevState& S, hipStream_t st, int hollingswor
         HALO_WROTE(S, F_ke);
     }
     if (!(parts & 2)) return hipGetLastError();
-    if (MD) {
+    if (MD && live && !(rk_step == -1 || rk_step == 2)) {
+        HALO_RUN_R1(S, st, ke, F_pv_vertex, F_rho_zz, F_pv_vertex);
+        HALO_WROTE(S, F_rho_edge, F_pv_edge);
+    } else if (MD) {
         HALO_RUN_R1(S, st, ke, F_pv_vertex, F_rho_zz, F_u, F_pv_vertex);
         HALO_WROTE(S, F_h_edge, F_rho_edge, F_ke_edge, F_v, F_pv_edge);
     } else {

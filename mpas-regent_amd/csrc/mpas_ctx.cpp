@@ -1063,9 +1063,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                      [&] { return launch_acoustic(S, st, dts, small_step, c->exact, 0, 0.0, tme); });
             run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, dts, small_step == 0); });
         }
-        if (S.physics)  // rk_timestep.rg:460, commented out in the reference (Q7)
-            run_task(c, recover_name(rk_step),
-                     [&] { return launch_recover_large_step(S, st, number_sub_steps[rk_step], rk_step, dt); });
+        if (S.physics) {  // rk_timestep.rg:460, commented out in the reference (Q7)
+            // option ntu: a stage before the last leaves ruAvg / wwAvg dead -- the next stage's first
+            // acoustic substep sets both before any task reads them
+            const bool navg = (c->ntu == 1 || c->ntu == 2) && rk_step < 2;
+            run_task(c, navg ? "atm_recover_large_step_variables_work[rk<2-avg]" : recover_name(rk_step),
+                     [&] { return launch_recover_large_step(S, st, number_sub_steps[rk_step], rk_step, dt, navg ? 1 : 0); });
+        }
         if (hf && fuse && rk_step == 2 && S.LP == 64 && !c->transport) {
             // (the vertex / cell kernel ran beside the last damping) the edge kernel beside
             // atm_rk_dynamics_substep_finish, which follows below
@@ -1095,12 +1099,13 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             vi_done = true;
         } else {
             const int nv = (rk_step == 2 && vdyn_on) ? 1 : 0;
-            // option ntu: stage 1's call stores only what the last stage (rk_step > 0) reads -- ke and
-            // pv_edge; its divergence, vorticity, h_edge and ke_edge have no reader before the last stage's
-            // solve_diagnostics rewrites them (dyn_tend reads divergence and vorticity at rk_step 0 only)
-            const int rk2 = schedule == 0 ? (int)rk_sub_timestep[2] : 2;
+            // option ntu: a call before the last stage's, the next stage at rk_step > 0, stores only what
+            // that stage reads -- ke and pv_edge (the MPAS forms: rho_edge too); its divergence, vorticity,
+            // h_edge and ke_edge have no reader before the last stage's solve_diagnostics rewrites them
+            // (dyn_tend reads divergence and vorticity at rk_step 0 only; nothing reads h_edge, ke_edge)
+            const int rk_next = rk_step == 2 ? 0 : schedule == 0 ? (int)rk_sub_timestep[rk_step + 1] : rk_step + 1;
             // (ntu = 2: every diagnostic stored, 3: every acoustic state stored -- the A/Bs of these parts)
-            const bool live = (c->ntu == 1 || c->ntu == 3) && S.physics == 0 && rk_step == 1 && rk2 != 0;
+            const bool live = (c->ntu == 1 || c->ntu == 3) && rk_step < 2 && rk_next != 0;
             run_task(c, live ? "atm_compute_solve_diagnostics[live]"
                              : nv ? "atm_compute_solve_diagnostics[-v]" : "atm_compute_solve_diagnostics",
                      [&] { return launch_solve_diagnostics(S, st, 0, rk_step, live ? 7 : 3, nv); });

@@ -284,7 +284,7 @@ hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t see
 hipError_t launch_keep_refresh(const DevState& S, hipStream_t st, int f, int kind);
 hipError_t launch_keep_check(const DevState& S, hipStream_t st, int f, int kind, int lev0, int* flag);
 hipError_t launch_prepare(DevState& S, hipStream_t st);
-hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt);
+hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg = 0);
 hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
 hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
 hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt);

@@ -16,7 +16,7 @@ roofline.achieved divides by the measured launch time.
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
-          ddx=False, ntu=False, live=False, nst=False):
+          ddx=False, ntu=False, live=False, nst=False, navg=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -184,9 +184,10 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         # option ntu (stage 1's call, the last stage at rk_step > 0): the diagnostics that stage's dyn_tend
         # reads, alone -- ke, pv_edge (pv_vertex, read back by the edge kernel); no credit for the dead
         # h_edge, ke_edge, divergence, vorticity nor for h, which only h_edge reads
+        # (the MPAS forms: also rho_edge = h_edge, from rho_zz; stage 0's call too)
         return (["u", "cellsOnEdge", "dcEdge", "dvEdge", "verticesOnEdge", "edgesOnCell", "edgesOnCellSign",
-                 "invAreaCell", "nEdgesOnCell", "edgesOnVertex", "edgesOnVertexSign", "fVertex", "invAreaTriangle"],
-                ["pv_edge", "ke", "pv_vertex"])
+                 "invAreaCell", "nEdgesOnCell", "edgesOnVertex", "edgesOnVertexSign", "fVertex", "invAreaTriangle"]
+                + (["rho_zz"] if md else []), ["pv_edge", "ke", "pv_vertex"] + (["rho_edge"] if md else []))
     if task == "atm_compute_solve_diagnostics":
         writes = ["h_edge", "ke_edge", "pv_edge", "divergence", "ke", "vorticity", "pv_vertex"]
         if reconstruct_v:
@@ -204,6 +205,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         if rk_step == 2:
             reads += ["rt_diabatic_tend", "exner_base"]
             writes += ["exner", "pressure_p"]
+        if navg:  # option ntu, a stage before the last: the averages are dead (the next stage's first substep sets them)
+            reads = [r for r in reads if r not in ("wwAvg", "ruAvg")]
+            writes = [w for w in writes if w not in ("wwAvg", "ruAvg")]
         return reads, writes
     if task == "atm_rk_dynamics_substep_finish":
         # (:1951-2007 with dynamics_substep = dynamics_split = 1, as atm_srk3 calls it: the
@@ -280,9 +284,9 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "physics": 1}, 1),
                 ("atm_divergence_damping_3d", {}, 4),
-                ("atm_recover_large_step_variables_work", {"rk_step": 0}, 2),
+                ("atm_recover_large_step_variables_work", {"rk_step": 0, "navg": bool(ntu)}, 2),
                 ("atm_recover_large_step_variables_work", {"rk_step": 2}, 1),
-                ("atm_compute_solve_diagnostics", p, 2),
+                ("atm_compute_solve_diagnostics", {"live": bool(ntu), **p}, 2),
                 ("atm_compute_solve_diagnostics", {"reconstruct_v": True, **p}, 1),
                 ("atm_rk_dynamics_substep_finish", p, 1)]
         if physics == 2:

@@ -244,3 +244,32 @@ def test_mpas_fusesetup_bit_identical(x1_2562, physics, L):
             out[fused] = got
         bad = compare_states(out[1], out[0], rtol=0.0)
         assert not bad, f"exact={exact}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("physics,transport", [(1, 1), (2, 0), (2, 1)])
+@pytest.mark.parametrize("L", [5, 56])
+def test_ntu_mpas_forms_bit_identical(x1_2562, physics, transport, L):
+    """option ntu under the MPAS forms: the stages before the last recover no ruAvg / wwAvg (the next
+    stage's first acoustic substep sets both before any task reads them) and their solve_diagnostics
+    store ke, pv_edge and rho_edge alone (divergence, vorticity, h_edge and ke_edge have no reader
+    before the last stage's call rewrites them) -- every field after three steps, the transport's
+    scalars included, has the same bits with the option on and off (2, 3: each part alone)"""
+    st = state(x1_2562, L, "mpas0")
+    for exact in (1, 0):
+        out = {}
+        for ntu in (0, 1, 2, 3):
+            got = st.copy()
+            with lib.Context(*st.dims()) as ctx:
+                ctx.set_option("exact", exact)
+                ctx.set_option("physics", physics)
+                ctx.set_option("transport", transport)
+                ctx.set_option("ntu", ntu)
+                ctx.upload(st)
+                for _ in range(3):
+                    T.atm_srk3(ctx, 720.0, 1)
+                ctx.sync()
+                ctx.download(got)
+            out[ntu] = got
+        for ntu in (1, 2, 3):
+            bad = compare_states(out[ntu], out[0], rtol=0.0)
+            assert not bad, f"exact={exact} ntu={ntu}: {bad[:6]}"
