@@ -388,7 +388,11 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
              "atm_advance_acoustic_step_work[ss>0+damp]": {"small_step": 1, "damp": True},
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
              "atm_recover_large_step_variables_work[rk2]": {"rk_step": 2},
-             "atm_recover_large_step_variables_work[rk<2-avg]": {"rk_step": 0, "navg": True}}
+             "atm_recover_large_step_variables_work[rk<2-avg]": {"rk_step": 0, "navg": True},
+             # (option mdamp: the stage's last divergence damping in the recover edge kernel)
+             "atm_recover_large_step_variables_work[rk<2-avg+damp]": {"rk_step": 0, "navg": True, "damp": True},
+             "atm_recover_large_step_variables_work[rk<2+damp]": {"rk_step": 0, "damp": True},
+             "atm_recover_large_step_variables_work[rk2+damp]": {"rk_step": 2, "damp": True}}
     def dyn_kw(name):  # atm_compute_dyn_tend_work[rk0|rk>0 (+copy) (+d4o) (+d4i) (-A)] (mpas_ctx.cpp srk3)
         tag = name[name.index("[") + 1:-1]
         kw = {"rk_step": 0 if tag.startswith("rk0") else 1}
@@ -683,8 +687,9 @@ def main():
     fcopy = fsetup and bool(ctx.get_option("fusecopy"))  # (decomposed and MPAS forms too, as srk3 does)
     d4 = bool(ctx.get_option("defer4")) and not args.physics
     ntu = bool(ctx.get_option("ntu"))  # (the MPAS forms: the dead diagnostics and averages only)
+    mdamp = bool(ctx.get_option("mdamp")) and bool(args.physics)
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
-                                 smls, ntu)
+                                 smls, ntu, mdamp)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -708,7 +713,7 @@ def main():
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy), "smlsum": int(smls),
-                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
+                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "mdamp": int(mdamp), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}

@@ -522,8 +522,13 @@ hipError_t launch_sml_flux(const DevState& S, hipStream_t st) { MPAS_LP_DISPATCH
 // edge, before the cell kernel reads ru_p.  FIRST (small_step 0): ru_p = dts tend_u and
 // ruAvg = ru_p need tend_u alone -- the old ru_p / ruAvg columns are not read (their level L,
 // stored back as it is, comes by one scalar load each), nor cqu / zxu: 2 of 6 column streams
-template <int LP, bool FIRST>
-__global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int small_step, double c2) {
+// DAMP (option mdamp, small_step > 0): the previous substep's atm_divergence_damping_3d (:1742-1762,
+// coefficient coefd) applied to the ru_p read here, before this substep's update -- divdamp_body's
+// expression on the same values (its rtheta_pp is the one gathered for the pressure gradient; OLD0:
+// rtheta_pp_old = 0 after a stage's first substep), so the same bits; the damping launch goes
+template <int LP, bool FIRST, bool DAMP = false, bool OLD0 = false>
+__global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int small_step, double c2, double coefd) {
+    static_assert(!DAMP || !FIRST, "the previous substep's damping: small_step > 0");
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO) return;
@@ -549,6 +554,14 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
         gather2s<LP>(fd(S, F_exner), cell1, cell2, k, x1, x2);
         gather2s<LP>(fd(S, F_rho_pp), cell1, cell2, k, r1, r2);
         const double invDc = fd(S, F_invDcEdge)[e], spec = fd(S, F_specZoneMaskEdge)[e];
+        if constexpr (DAMP) {
+            double o1 = 0.0, o2 = 0.0, m1, m2;
+            if (!OLD0) gather2s<LP>(fd(S, F_rtheta_pp_old), cell1, cell2, k, o1, o2);
+            gather2s<LP>(fd(S, F_theta_m), cell1, cell2, k, m1, m2);
+            const int sh1 = fi(S, F_isShared)[cell1], sh2 = fi(S, F_isShared)[cell2];
+            const double divCell1 = -(t1 - o1), divCell2 = -(t2 - o2);
+            if (k < L && !(sh1 && sh2)) rp = rp + coefd * (divCell2 - divCell1) * (1.0 - spec) / (m1 + m2);
+        }
         double pgrad = ((t2 - t1) * invDc) / (0.5 * (z2 + z1));
         pgrad = cqu * 0.5 * c2 * (x1 + x2) * pgrad;
         pgrad = pgrad + 0.5 * zxu * kGravity * (r1 + r2);
@@ -565,8 +578,9 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
 
 template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                              double coef_prev, int tme, int sml, int wold, int ddx) {
+                              double coef_prev, int tme, int sml, int wold, int ddx, int mdamp) {
     if ((tme && (S.physics || S.halo)) || (sml && S.physics)) return hipErrorInvalidValue;  // (atm_srk3, reference semantics)
+    if (mdamp && (!S.physics || small_step == 0)) return hipErrorInvalidValue;
     if (sml && (small_step != 0 || mode == 0)) return hipErrorInvalidValue;
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
@@ -574,12 +588,19 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     if (ddx && S.physics) return hipErrorInvalidValue;   // (X_Dd: atm_srk3's reference semantics only)
     if (S.physics) {  // Q18: the edges first
         const double rcv = kRgas / (kCp - kRgas), c2 = kCp * rcv;
+        // (mdamp, option mdamp: the previous substep's damping here, coefficient coef_prev; 2: that
+        // substep was the stage's first, rtheta_pp_old = 0)
+        const bool dmp = mdamp != 0, old0 = mdamp == 2;
         auto ru = [&](const DevState& X) {
             const int nb = col_blocks<LP>(X, KE);
-            if (nb && small_step == 0) k_acoustic_ru<LP, true><<<nb, 256, 0, st>>>(X, dts, small_step, c2);
-            else if (nb) k_acoustic_ru<LP, false><<<nb, 256, 0, st>>>(X, dts, small_step, c2);
+            if (!nb) return;
+            if (small_step == 0) k_acoustic_ru<LP, true><<<nb, 256, 0, st>>>(X, dts, small_step, c2, 0.0);
+            else if (old0) k_acoustic_ru<LP, false, true, true><<<nb, 256, 0, st>>>(X, dts, small_step, c2, coef_prev);
+            else if (dmp) k_acoustic_ru<LP, false, true, false><<<nb, 256, 0, st>>>(X, dts, small_step, c2, coef_prev);
+            else k_acoustic_ru<LP, false><<<nb, 256, 0, st>>>(X, dts, small_step, c2, 0.0);
         };
         if (small_step == 0) HALO_RUN(S, st, ru);  // (own columns only: no ghost read)
+        else if (dmp) HALO_RUN(S, st, ru, F_rtheta_pp, F_zz, F_exner, F_rho_pp, F_rtheta_pp_old, F_theta_m);
         else HALO_RUN(S, st, ru, F_rtheta_pp, F_zz, F_exner, F_rho_pp);
         HALO_WROTE(S, F_ru_p, F_ruAvg);
     }
@@ -681,8 +702,8 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                           double coef_prev, int tme, int sml, int wold, int ddx) {
-    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml, wold, ddx);
+                           double coef_prev, int tme, int sml, int wold, int ddx, int mdamp) {
+    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml, wold, ddx, mdamp);
 }
 template <int LP>
 static hipError_t hf_ac_vc_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact,

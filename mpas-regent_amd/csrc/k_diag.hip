@@ -16,6 +16,7 @@ namespace mpas {
 struct RecK {
     double invNs, dt, rgas_p0, rgas, rcv;
     int rk_step;
+    double coef_divdamp;  // (DAMP: the stage's last atm_divergence_damping_3d, option mdamp)
 };
 
 // :1788-1820 (the loop over cells and levels 0..nVertLevels-1), and the "garbage cell"
@@ -117,16 +118,46 @@ __global__ __launch_bounds__(256) void k_recover_cells(DevState S, RecK a) {
 // :1830-1837: ruAvg, ru (Q24: ru_save * ru_p; MPASV: ru_save + ru_p), u from the new rho_zz
 // NAVG (see recover_cells_mpas): ruAvg is dead -- the next stage's first substep sets it
 // (k_acoustic_ru FIRST) -- and is neither read nor stored
-template <int LP, bool MPASV, bool NAVG = false>
+// DAMP (option mdamp, the MPAS forms): the stage's last atm_divergence_damping_3d (:1742-1762) applied
+// here to the ru_p this kernel reads -- divdamp_body's expression on the same values (rtheta_pp,
+// rtheta_pp_old, theta_m of the acoustic step: this launch runs before k_recover_cells, which rewrites
+// theta_m; OLD0: rtheta_pp_old = 0 after a stage's first substep), so the same bits -- and rho_zz of
+// the edge's cells formed as k_recover_cells forms it ((rho_p_save + rho_pp) + rho_base; the garbage
+// cell's 1.0, :1790-1792).  The damped ru_p is stored unless NAVG (a stage before the last: the next
+// stage's first substep sets ru_p from tend_u)
+template <int LP, bool MPASV, bool NAVG = false, bool DAMP = false, bool OLD0 = false>
 __global__ __launch_bounds__(256) void k_recover_edges(DevState S, RecK a) {
     static_assert(!NAVG || MPASV, "the dead averages: the MPAS forms");
+    static_assert(!DAMP || MPASV, "the damping in recover: the MPAS forms");
     ColMap<LP> m(S, KE);
     const int L = S.L, k = m.k, e = m.ent;
     if (e >= S.nEO || (!MPASV && k >= L)) return;
     const int cell1 = fi(S, F_cellsOnEdge)[(size_t)e * 2], cell2 = fi(S, F_cellsOnEdge)[(size_t)e * 2 + 1];
-    const double* rz = fd(S, F_rho_zz);
-    const double rz1 = colk(rz, cell1), rz2 = colk(rz, cell2);
-    const double ra = NAVG ? 0.0 : colk(fd(S, F_ruAvg), e), rus = colk(fd(S, F_ru_save), e), rup = colk(fd(S, F_ru_p), e);
+    double rz1, rz2, rup;
+    const double ra = NAVG ? 0.0 : colk(fd(S, F_ruAvg), e), rus = colk(fd(S, F_ru_save), e);
+    if constexpr (DAMP) {
+        double ps1, ps2, pp1, pp2, rb1, rb2, r1, r2, ro1 = 0.0, ro2 = 0.0, t1, t2;
+        gather2s<LP>(fd(S, F_rho_p_save), cell1, cell2, k, ps1, ps2);
+        gather2s<LP>(fd(S, F_rho_pp), cell1, cell2, k, pp1, pp2);
+        gather2s<LP>(fd(S, F_rho_base), cell1, cell2, k, rb1, rb2);
+        gather2s<LP>(fd(S, F_rtheta_pp), cell1, cell2, k, r1, r2);
+        if (!OLD0) gather2s<LP>(fd(S, F_rtheta_pp_old), cell1, cell2, k, ro1, ro2);
+        gather2s<LP>(fd(S, F_theta_m), cell1, cell2, k, t1, t2);
+        const int sh1 = fi(S, F_isShared)[cell1], sh2 = fi(S, F_isShared)[cell2];
+        const double spec = fd(S, F_specZoneMaskEdge)[e];
+        const double ru0 = colk(fd(S, F_ru_p), e);
+        const double rp1 = ps1 + pp1, rp2 = ps2 + pp2;
+        rz1 = (cell1 == S.nCells) ? 1.0 : rp1 + rb1;
+        rz2 = (cell2 == S.nCells) ? 1.0 : rp2 + rb2;
+        const double divCell1 = -(r1 - ro1), divCell2 = -(r2 - ro2);
+        rup = (k < L && !(sh1 && sh2)) ? ru0 + a.coef_divdamp * (divCell2 - divCell1) * (1.0 - spec) / (t1 + t2) : ru0;
+        if (!NAVG) colk(fw(S, F_ru_p), e) = k < L ? rup : PADW(ru0);
+    } else {
+        const double* rz = fd(S, F_rho_zz);
+        rz1 = colk(rz, cell1);
+        rz2 = colk(rz, cell2);
+        rup = colk(fd(S, F_ru_p), e);
+    }
     double ruAvg = ra;
     ruAvg *= a.invNs;
     ruAvg += rus;
@@ -229,7 +260,8 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
 }
 
 template <int LP>
-static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg) {
+static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg,
+                             int damp, double damp_dts) {
     RecK a;
     a.invNs = 1 / (double)ns;
     a.dt = dt;
@@ -237,8 +269,35 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
     a.rgas_p0 = kRgas / 100000;
     a.rcv = kRgas / (kCp - kRgas);
     a.rk_step = rk_step;
+    a.coef_divdamp = damp ? divdamp_coef(damp_dts) : 0.0;
     const int nCB = col_blocks<LP>(S, KC);
     const bool na = navg && S.physics;  // (option ntu: the averages of a stage before the last are dead)
+    if (damp && !S.physics) return hipErrorInvalidValue;
+    if (damp) {  // (option mdamp) the edges first, with the stage's last damping; then the cells and w
+        auto kd = [&](const DevState& X) {
+            const int nb = col_blocks<LP>(X, KE);
+            if (!nb) return;
+            if (na && damp == 2) k_recover_edges<LP, true, true, true, true><<<nb, 256, 0, st>>>(X, a);
+            else if (na) k_recover_edges<LP, true, true, true, false><<<nb, 256, 0, st>>>(X, a);
+            else if (damp == 2) k_recover_edges<LP, true, false, true, true><<<nb, 256, 0, st>>>(X, a);
+            else k_recover_edges<LP, true, false, true, false><<<nb, 256, 0, st>>>(X, a);
+        };
+        if (damp == 2) HALO_RUN(S, st, kd, F_rho_p_save, F_rho_pp, F_rho_base, F_rtheta_pp, F_theta_m);
+        else HALO_RUN(S, st, kd, F_rho_p_save, F_rho_pp, F_rho_base, F_rtheta_pp, F_rtheta_pp_old, F_theta_m);
+        HALO_WROTE(S, F_ru, F_u);
+        if (!na) HALO_WROTE(S, F_ruAvg, F_ru_p);
+        if (nCB && na) k_recover_cells<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
+        else if (nCB) k_recover_cells<LP, true><<<nCB, 256, 0, st>>>(S, a);
+        HALO_WROTE(S, F_rho_p, F_rho_zz, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
+        if (!na) HALO_WROTE(S, F_wwAvg);
+        auto kw = [&](const DevState& X) {
+            const int nb = col_blocks<LP>(X, KC);
+            if (nb) k_recover_w<LP, true><<<nb, 256, 0, st>>>(X);
+        };
+        HALO_RUN(S, st, kw, F_ru);
+        HALO_WROTE(S, F_w);
+        return hipGetLastError();
+    }
     if (nCB && na) k_recover_cells<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
     else if (nCB && S.physics) k_recover_cells<LP, true><<<nCB, 256, 0, st>>>(S, a);
     else if (nCB) k_recover_cells<LP, false><<<nCB, 256, 0, st>>>(S, a);
@@ -262,8 +321,9 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
     HALO_WROTE(S, F_w);
     return hipGetLastError();
 }
-hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg) {
-    MPAS_LP_DISPATCH(S.LP, recover_lp, S, st, ns, rk_step, dt, navg);
+hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg,
+                                     int damp, double damp_dts) {
+    MPAS_LP_DISPATCH(S.LP, recover_lp, S, st, ns, rk_step, dt, navg, damp, damp_dts);
 }
 
 // ---------------------------------------------------------------- damping coefficients

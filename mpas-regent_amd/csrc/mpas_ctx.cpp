@@ -108,6 +108,8 @@ struct mpas_ctx {
                        // (reference semantics, edgesOnEdge_ECP = edgesOnEdge; same values)
     int defer4 = 1;    // option "defer4": atm_srk3 applies rk_step 0's del4 of tend_u_euler (dyn_tend D) in the
                        // next stage's rk_step > 0 edge kernel (reference semantics; same values)
+    int mdamp = 1;     // option "mdamp" (the MPAS forms): each divergence damping applied by the kernel that next
+                       // reads ru_p -- the next substep's k_acoustic_ru, or the stage's recover edge kernel
     int ntu = 1;       // option "ntu" (with defer4): that rk_step 0 call's whole tend_u is dead (the next stage's
                        // edge kernel rewrites it, no task in between reads it): its edge kernel forms none of
                        // it and skips its gathers (k_dyn_B NTU; the same values of everything read later)
@@ -1059,16 +1061,28 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
                 }
                 continue;
             }
-            run_task(c, acoustic_name(small_step),
-                     [&] { return launch_acoustic(S, st, dts, small_step, c->exact, 0, 0.0, tme); });
-            run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, dts, small_step == 0); });
+            // option mdamp (the MPAS forms): the previous substep's damping in this substep's ru_p kernel, the
+            // stage's last one in the recover edge kernel -- each read-modify-write of ru_p goes
+            const bool md_fold = c->mdamp && S.physics;
+            const int mdp = (md_fold && small_step > 0) ? (small_step == 1 ? 2 : 1) : 0;
+            const double cprev = mdp ? divdamp_coef(dts) : 0.0;
+            run_task(c, mdp ? "atm_advance_acoustic_step_work[ss>0+damp]" : acoustic_name(small_step),
+                     [&] { return launch_acoustic(S, st, dts, small_step, c->exact, 0, cprev, tme, 0, 1, 0, mdp); });
+            if (!md_fold)
+                run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, dts, small_step == 0); });
         }
         if (S.physics) {  // rk_timestep.rg:460, commented out in the reference (Q7)
             // option ntu: a stage before the last leaves ruAvg / wwAvg dead -- the next stage's first
             // acoustic substep sets both before any task reads them
             const bool navg = (c->ntu == 1 || c->ntu == 2) && rk_step < 2;
-            run_task(c, navg ? "atm_recover_large_step_variables_work[rk<2-avg]" : recover_name(rk_step),
-                     [&] { return launch_recover_large_step(S, st, number_sub_steps[rk_step], rk_step, dt, navg ? 1 : 0); });
+            // (option mdamp: the stage's last damping in the edge kernel; 2: that substep was the stage's first)
+            const int ns_r = number_sub_steps[rk_step];
+            const int dmp = (c->mdamp && ns_r > 0) ? (ns_r == 1 ? 2 : 1) : 0;
+            const std::string rn = std::string(navg ? "atm_recover_large_step_variables_work[rk<2-avg]" : recover_name(rk_step));
+            const std::string rnd = dmp ? rn.substr(0, rn.size() - 1) + "+damp]" : rn;
+            run_task(c, rnd.c_str(), [&] {
+                return launch_recover_large_step(S, st, ns_r, rk_step, dt, navg ? 1 : 0, dmp, rk_sub_timestep[rk_step]);
+            });
         }
         if (hf && fuse && rk_step == 2 && S.LP == 64 && !c->transport) {
             // (the vertex / cell kernel ran beside the last damping) the edge kernel beside
@@ -1396,6 +1410,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "fusecopy") == 0) c->fusecopy = value ? 1 : 0;
         else if (name && std::strcmp(name, "defer4") == 0) c->defer4 = value ? 1 : 0;
         else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value < 0 ? 0 : value > 3 ? 3 : value;
+        else if (name && std::strcmp(name, "mdamp") == 0) c->mdamp = value ? 1 : 0;
         else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
@@ -1560,6 +1575,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "fusecopy") == 0) *value = c->fusecopy;
         else if (name && std::strcmp(name, "defer4") == 0) *value = c->defer4;
         else if (name && std::strcmp(name, "ntu") == 0) *value = c->ntu;
+        else if (name && std::strcmp(name, "mdamp") == 0) *value = c->mdamp;
         else if (name && std::strcmp(name, "vdyn") == 0) *value = c->vdyn;
         else if (name && std::strcmp(name, "eoe_same") == 0) {
             prepare_now(c);

@@ -258,7 +258,8 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st, int exact);
 // this launch stores instead, so only the step's last substep leaves rtheta_pp_old
 // ddx: rw_save - rw from X_Dd (atm_srk3 with option smlsum: launch_sml_flux formed it this step)
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode = 0,
-                           double coef_prev = 0.0, int tme = 0, int sml = 0, int wold = 1, int ddx = 0);
+                           double coef_prev = 0.0, int tme = 0, int sml = 0, int wold = 1, int ddx = 0,
+                           int mdamp = 0);  // (mdamp: the MPAS forms, the previous substep's damping folded in)
 // X_smlS = the sum of set_smlstep's slope-flux terms per cell and level (atm_srk3 fast path,
 // once per step: u_tend / zb_cell / zb3_cell are not written within a step)
 hipError_t launch_sml_flux(const DevState& S, hipStream_t st);
@@ -284,7 +285,10 @@ hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t see
 hipError_t launch_keep_refresh(const DevState& S, hipStream_t st, int f, int kind);
 hipError_t launch_keep_check(const DevState& S, hipStream_t st, int f, int kind, int lev0, int* flag);
 hipError_t launch_prepare(DevState& S, hipStream_t st);
-hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg = 0);
+// damp (option mdamp, the MPAS forms): 1 the stage's last divergence damping (coefficient of damp_dts)
+// applied by the edge kernel, 2 the same with rtheta_pp_old = 0 (the stage's last substep was its first)
+hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg = 0,
+                                     int damp = 0, double damp_dts = 0.0);
 hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
 hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
 hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt);

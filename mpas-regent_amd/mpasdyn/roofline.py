@@ -205,9 +205,13 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         if rk_step == 2:
             reads += ["rt_diabatic_tend", "exner_base"]
             writes += ["exner", "pressure_p"]
-        if navg:  # option ntu, a stage before the last: the averages are dead (the next stage's first substep sets them)
+        if damp:  # option mdamp: the stage's last divergence damping in the edge kernel (ru_p updated in place)
+            reads += ["rtheta_pp", "rtheta_pp_old", "theta_m", "isShared", "specZoneMaskEdge"]
+            writes += ["ru_p"]
+        if navg:  # option ntu, a stage before the last: the averages are dead (the next stage's first substep sets
+            # them), and so is a damped ru_p (the next stage's first substep sets it from tend_u)
             reads = [r for r in reads if r not in ("wwAvg", "ruAvg")]
-            writes = [w for w in writes if w not in ("wwAvg", "ruAvg")]
+            writes = [w for w in writes if w not in ("wwAvg", "ruAvg", "ru_p")]
         return reads, writes
     if task == "atm_rk_dynamics_substep_finish":
         # (:1951-2007 with dynamics_substep = dynamics_split = 1, as atm_srk3 calls it: the
@@ -262,7 +266,7 @@ def b_alg(task, dims, **kw):
 
 
 def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-                  fusecopy=False, defer4=False, smlsum=False, ntu=False):
+                  fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -280,12 +284,15 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
         if schedule == 1:
             out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, **p}, 1),
                     ("atm_compute_dyn_tend_work", {"rk_step": 1, **p}, 2)]
+        # (option mdamp: each damping applied by the next kernel that reads ru_p -- the next substep's
+        # ru_p kernel or the stage's recover)
+        d = {"damp": bool(mdamp)}
         out += [("atm_set_smlstep_pert_variables_work", p, 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 1, "physics": 1}, 1),
-                ("atm_divergence_damping_3d", {}, 4),
-                ("atm_recover_large_step_variables_work", {"rk_step": 0, "navg": bool(ntu)}, 2),
-                ("atm_recover_large_step_variables_work", {"rk_step": 2}, 1),
+                ("atm_advance_acoustic_step_work", {"small_step": 1, "physics": 1, **d}, 1),
+                ("atm_divergence_damping_3d", {}, 0 if mdamp else 4),
+                ("atm_recover_large_step_variables_work", {"rk_step": 0, "navg": bool(ntu), **d}, 2),
+                ("atm_recover_large_step_variables_work", {"rk_step": 2, **d}, 1),
                 ("atm_compute_solve_diagnostics", {"live": bool(ntu), **p}, 2),
                 ("atm_compute_solve_diagnostics", {"reconstruct_v": True, **p}, 1),
                 ("atm_rk_dynamics_substep_finish", p, 1)]
@@ -339,7 +346,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
 
 
 def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-               fusecopy=False, defer4=False, smlsum=False, ntu=False):
+               fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
                                                                         fusesetup, fusesml, fusecopy, defer4,
-                                                                        smlsum, ntu))
+                                                                        smlsum, ntu, mdamp))

@@ -273,3 +273,33 @@ def test_ntu_mpas_forms_bit_identical(x1_2562, physics, transport, L):
         for ntu in (1, 2, 3):
             bad = compare_states(out[ntu], out[0], rtol=0.0)
             assert not bad, f"exact={exact} ntu={ntu}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("physics,transport", [(1, 1), (2, 0)])
+@pytest.mark.parametrize("L", [5, 56])
+def test_mdamp_bit_identical(x1_2562, physics, transport, L):
+    """option mdamp (the MPAS forms): each divergence damping applied by the kernel that next reads
+    ru_p -- the next substep's ru_p kernel, or the stage's recover edge kernel (before its cell kernel
+    rewrites theta_m; rho_zz of the edge's cells formed as that kernel forms it) -- instead of a launch
+    of its own: every field after three steps (number_of_sub_steps 2: a damping inside a stage and at
+    each stage's end) has the same bits as the separate launches, with ntu on and off"""
+    st = state(x1_2562, L, "mpas0")
+    for exact in (1, 0):
+        out = {}
+        for mdamp, ntu in ((0, 0), (1, 0), (1, 1)):
+            got = st.copy()
+            with lib.Context(*st.dims()) as ctx:
+                ctx.set_option("exact", exact)
+                ctx.set_option("physics", physics)
+                ctx.set_option("transport", transport)
+                ctx.set_option("mdamp", mdamp)
+                ctx.set_option("ntu", ntu)
+                ctx.upload(st)
+                for _ in range(3):
+                    T.atm_srk3(ctx, 720.0, 1)
+                ctx.sync()
+                ctx.download(got)
+            out[(mdamp, ntu)] = got
+        for key in ((1, 0), (1, 1)):
+            bad = compare_states(out[key], out[(0, 0)], rtol=0.0)
+            assert not bad, f"exact={exact} mdamp, ntu={key}: {bad[:6]}"
