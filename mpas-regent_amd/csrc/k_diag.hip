@@ -193,12 +193,10 @@ __device__ __forceinline__ void recover_w_slot(double r, double z, double z3, do
 // The level-0 term (cf1..cf3 flux) is added to w(cell, 0) at every one of the nVertLevels
 // level iterations of the cell; lane 0 replays that sequence in the reference's order.
 // MPASV: the level-0 term once per edge, flux2 = fzm ru(k) + fzp ru(k-1) (Q24).
+// (rz, w: rho_zz and w of the column as k_recover_cells stored them, read back)
 template <int LP, bool MPASV>
-__global__ __launch_bounds__(256) void k_recover_w(DevState S) {
-    ColMap<LP> m(S, KC);
-    const int L = S.L, k = m.k, c = m.ent;
-    if (c >= S.nCO) return;
-    if (fi(S, F_bdyMaskCell)[c] > kRelaxZone) return;
+__device__ __forceinline__ void recover_w_col(const DevState& S, int c, int k, double rz, double w) {
+    const int L = S.L;
     const int ne = fi(S, F_nEdgesOnCell)[c];
     const int* eoc = fi(S, F_edgesOnCell) + (size_t)c * 10;
     const double* sgn = fd(S, F_edgesOnCell_sign) + (size_t)c * 10;
@@ -209,8 +207,6 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
     const double *ru = fd(S, F_ru), *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
     const double fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
     const double cf1 = fd(S, F_cf1)[0], cf2 = fd(S, F_cf2)[0], cf3 = fd(S, F_cf3)[0];
-    double rz, w;
-    col_rd2<LP>(fd(S, F_rho_zz), fd(S, F_w), c, k, L, rz, w);
     const double w_in = w;  // (level L: stored back as loaded -- the column's lines written whole)
     const double rz_m = lvl_dn<LP>(rz, k), rz1 = __shfl(rz, 1, LP), rz2 = __shfl(rz, 2, LP);
     // the first NF slots: loads issued unconditionally, in pairs (every lane is active);
@@ -258,6 +254,20 @@ __global__ __launch_bounds__(256) void k_recover_w(DevState S) {
     }
     colk(fw(S, F_w), c) = k < L ? w : PADW(w_in);
 }
+template <int LP, bool MPASV>
+__global__ __launch_bounds__(256) void k_recover_w(DevState S) {
+    ColMap<LP> m(S, KC);
+    const int L = S.L, k = m.k, c = m.ent;
+    if (c >= S.nCO) return;
+    if (fi(S, F_bdyMaskCell)[c] > kRelaxZone) return;
+    double rz, w;
+    col_rd2<LP>(fd(S, F_rho_zz), fd(S, F_w), c, k, L, rz, w);
+    recover_w_col<LP, MPASV>(S, c, k, rz, w);
+}
+
+// (option mdamp: the cell part and the w recovery in one kernel -- ru is ready once the edge kernel
+// runs first -- was measured slower, 1.58 -> 1.83 ms for the two stage-0/1 recovers: the fused
+// kernel's registers halve its occupancy; profiles/r06/mdamp/kbench_recover_cw_tried.json)
 
 template <int LP>
 static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_step, double dt, int navg,
