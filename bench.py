@@ -389,6 +389,7 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
              "atm_recover_large_step_variables_work[rk<2]": {"rk_step": 0},
              "atm_recover_large_step_variables_work[rk2]": {"rk_step": 2},
              "atm_recover_large_step_variables_work[rk<2-avg]": {"rk_step": 0, "navg": True},
+             "atm_advance_scalars_mono[save]": {"save": True},
              # (option mdamp: the stage's last divergence damping in the recover edge kernel)
              "atm_recover_large_step_variables_work[rk<2-avg+damp]": {"rk_step": 0, "navg": True, "damp": True},
              "atm_recover_large_step_variables_work[rk<2+damp]": {"rk_step": 0, "damp": True},
@@ -688,8 +689,11 @@ def main():
     d4 = bool(ctx.get_option("defer4")) and not args.physics
     ntu = bool(ctx.get_option("ntu"))  # (the MPAS forms: the dead diagnostics and averages only)
     mdamp = bool(ctx.get_option("mdamp")) and bool(args.physics)
+    # (option trsave: scalars_save folded into the transport, undecomposed with the default transport kernels)
+    trsave = bool(args.transport) and bool(ctx.get_option("trsave")) and not decomposed and not any(
+        ctx.get_option(o) for o in ("trtile", "tredge", "trsu"))
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
-                                 smls, ntu, mdamp)
+                                 smls, ntu, mdamp, trsave)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -713,7 +717,7 @@ def main():
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy), "smlsum": int(smls),
-                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "mdamp": int(mdamp), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
+                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "mdamp": int(mdamp), "trsave": int(trsave), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}

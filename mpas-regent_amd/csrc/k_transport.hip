@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void k_tr_edge_n(DevState S) {
 #pragma unroll
     for (int i = 0; i < EPW; i++) tr_map(S, KE, s0 + i, e_[i], p_[i]);
     if (e_[0] >= S.nEO) return;
-    const double* so = fd(S, F_scalars_old);
+    const double* so = fd(S, S.trsave ? F_scalars : F_scalars_old);  // (trsave: scalars holds the old values)
     int na_[EPW], c1_[EPW], c2_[EPW], adv[EPW][AF];
     double ac[EPW][AF], ac3[EPW][AF], dv_[EPW], u_[EPW], xa[EPW][AF], xb[EPW][AF];
 #pragma unroll
@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void k_tr_edge(DevState S) {
     row_ld(fd(S, F_adv_coefs) + (size_t)e * 15, ac);
     row_ld(fd(S, F_adv_coefs_3rd) + (size_t)e * 15, ac3);
     const double dv = fd(S, F_dvEdge)[e];
-    const double* so = fd(S, F_scalars_old);
+    const double* so = fd(S, S.trsave ? F_scalars : F_scalars_old);  // (trsave: scalars holds the old values)
     const double u = colk(fd(S, F_ruAvg), e);
     double xa[AF], xb[AF], s1a, s1b, s2a, s2b;
 #pragma unroll
@@ -452,10 +452,20 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     tr_slots(S, c, t);
     const double invA = fd(S, F_invAreaCell)[c];
     const double rdzw = fd(S, F_rdzw)[k], fzm = fd(S, F_fzm)[k], fzp = fd(S, F_fzp)[k];
-    const double *so = fd(S, F_scalars_old), *ru = fd(S, F_ruAvg);
+    // (trsave, wave-uniform: scalars holds the old values; the cell's whole pair column, every level and
+    // the padding, is stored to scalars_old at the end -- scalars_save's copy of it)
+    const bool save = S.trsave != 0;
+    const double *so = fd(S, save ? F_scalars : F_scalars_old), *ru = fd(S, F_ruAvg);
     const double* Ah = fd(S, X_Ah);
-    double sa, sb;
-    ld2<LP>(XP, so, c, p, k, sa, sb);
+    const Px XF{LP, LP};
+    double sa, sb, fa = 0.0, fb = 0.0;
+    if (save) {
+        ld2<LP>(XF, so, c, p, k, fa, fb);
+        sa = k < L ? fa : 0.0;
+        sb = k < L ? fb : 0.0;
+    } else {
+        ld2<LP>(XP, so, c, p, k, sa, sb);
+    }
     const double w = colk(fd(S, F_wwAvg), c), r_o = colk(fd(S, F_rho_zz_old_split), c), r_n = colk(fd(S, F_rho_zz), c);
     double u_[NF], x1a[NF], x2a[NF], x1b[NF], x2b[NF], Aa[NF], Ab[NF];
 #pragma unroll
@@ -501,6 +511,14 @@ __global__ __launch_bounds__(256) void k_tr_bounds(DevState S, double dt) {
     st2<LP>(XS, fw(S, X_Rp), c, p, k, Rpa, Rpb);
     st2<LP>(XS, fw(S, X_Rm), c, p, k, Rma, Rmb);
     if constexpr (!SU) st2<LP>(XS, fw(S, X_su), c, p, k, sua, sub);
+    if (save) {
+        st2<LP>(XF, fw(S, F_scalars_old), c, p, k, fa, fb);
+        if (c == S.nCells - 1) {  // (and the zero slot's column, as the copy of the whole array)
+            double za, zb;
+            ld2<LP>(XF, so, S.nCells, p, k, za, zb);
+            st2<LP>(XF, fw(S, F_scalars_old), S.nCells, p, k, za, zb);
+        }
+    }
 }
 
 // the limited update of one scalar
@@ -889,7 +907,9 @@ static hipError_t transport_tiled(const DevState& S, hipStream_t st, double dt) 
 }
 
 template <int LP>
-static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
+static hipError_t transport_lp(const DevState& S0, hipStream_t st, double dt, int fold) {
+    DevState S = S0;
+    S.trsave = fold;
     constexpr int COLS = 256 / LP;  // column slots per block; a slot = one entity, two scalars
     auto blocks = [](const DevState& X, int kind) {
         const int end = kind == KC ? X.nCO : X.nEO;
@@ -948,9 +968,11 @@ static hipError_t transport_lp(const DevState& S, hipStream_t st, double dt) {
     HALO_WROTE(S, F_scalars);
     return hipGetLastError();
 }
-hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt) {
+hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt, int fold) {
+    // (fold: only the default kernels -- undecomposed, no tiles, no LDS edge groups, su stored)
+    if (fold && (S.halo || S.trt || S.tre || S.trsu)) return hipErrorInvalidValue;
     if (S.trt) MPAS_LP_DISPATCH(S.LP, transport_tiled, S, st, dt);
-    MPAS_LP_DISPATCH(S.LP, transport_lp, S, st, dt);
+    MPAS_LP_DISPATCH(S.LP, transport_lp, S, st, dt, fold);
 }
 
 }  // namespace mpas

@@ -178,6 +178,11 @@ struct mpas_ctx {
     // with scalars_old staged in LDS per group of consecutive edges (undecomposed contexts;
     // rebuilt with the tiles)
     int tredge = 0;
+    // option "trsave" (default 1; atm_srk3 with the transport, undecomposed, the default transport
+    // kernels): scalars_save's copy folded into the transport -- its edge and bounds kernels read the old
+    // scalars from scalars itself (nothing writes scalars before the transport's update) and the bounds
+    // kernel stores them to scalars_old
+    int trsave = 1;
     TrEdgeGroups tre;
     // option "etile" (default 1): dyn_tend's cell kernel E over compact tiles of cells, the tile's
     // theta_m closure staged in LDS, each edge's advCells flux formed there (k_dyn_Et) -- the edge
@@ -902,7 +907,10 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     number_sub_steps[2] = number_of_sub_steps;
     const DevState& S = c->S;
     hipStream_t st = c->stream;
-    if (c->transport) {
+    // option trsave: the copy below folded into the transport's bounds kernel (its tables decided here:
+    // the tiled and LDS-edge forms need none of them built, su stored)
+    const bool trfold = c->transport && c->trsave && !c->halo && !c->trtile && !c->tredge && !S.trsu;
+    if (c->transport && !trfold) {
         // the time level the transport starts from (MPAS-A scalars(time level 1)); the
         // copy carries the ghosts of scalars, fresh or not, so scalars_old is as stale
         run_task(c, "scalars_save", [&] {
@@ -1126,9 +1134,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         }
     }
     if (c->transport)  // after the last stage's recover: ruAvg / wwAvg / rho_zz of the step
-        run_task(c, "atm_advance_scalars_mono", [&] {
+        run_task(c, trfold ? "atm_advance_scalars_mono[save]" : "atm_advance_scalars_mono", [&] {
             trt_ensure(c);  // (built before a capture by prepare_now)
-            return launch_advance_scalars_mono(S, st, dt);
+            return launch_advance_scalars_mono(S, st, dt, trfold ? 1 : 0);
         });
     if (S.physics == 2)  // the MPAS dynamics: cell-centre winds for the next step's curvature
         run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });  // (:487, commented)
@@ -1464,6 +1472,8 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         } else if (name && std::strcmp(name, "trtile") == 0) {
             c->trtile = value ? 1 : 0;
             c->trt_dirty = c->ett_dirty = true;
+        } else if (name && std::strcmp(name, "trsave") == 0) {
+            c->trsave = value ? 1 : 0;
         } else if (name && std::strcmp(name, "tredge") == 0) {
             c->tredge = value ? 1 : 0;
             c->trt_dirty = c->ett_dirty = true;
@@ -1533,6 +1543,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "trorder_e") == 0) *value = c->S.troe;
         else if (name && std::strcmp(name, "trtile") == 0) *value = c->trtile;
         else if (name && std::strcmp(name, "tredge") == 0) *value = c->tredge;
+        else if (name && std::strcmp(name, "trsave") == 0) *value = c->trsave;
         else if (name && std::strcmp(name, "tredge_active") == 0) {  // edge groups built for this mesh
             trt_ensure(c);
             *value = c->S.tre != nullptr;

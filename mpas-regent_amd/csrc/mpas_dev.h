@@ -132,6 +132,8 @@ struct DevState {
     int bsplit;  // option "bsplit": dyn_tend's per-edge theta / w fluxes in an edge kernel of their own
                  // (fast path): 1 always, 2 under the MPAS dynamics only, 0 never
     int trsu;     // option "trsu": the transport's update forms su again instead of reading X_su
+    int trsave;   // (atm_srk3, option "trsave"; set per launch) the transport reads the step's old scalars from
+                  // scalars itself and its bounds kernel stores scalars_old: scalars_save folded in
     int trepw;    // option "trepw": transport edge slots per wavefront (1, 2)
     int troe;     // option "trorder_e": the transport edge kernel's slot order (0: trorder's)
     int tro;      // transport slot order (k_transport.hip tr_slot): 0 entity-major, 1 pair-major
@@ -291,7 +293,9 @@ hipError_t launch_recover_large_step(const DevState& S, hipStream_t st, int ns, 
                                      int damp = 0, double damp_dts = 0.0);
 hipError_t launch_reconstruct_2d(const DevState& S, hipStream_t st, int on_a_sphere);
 hipError_t launch_output_diagnostics(const DevState& S, hipStream_t st);
-hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt);
+// fold (atm_srk3, option "trsave"): scalars_save not run before -- scalars still holds the old values,
+// and the bounds kernel stores them to scalars_old (undecomposed, default kernels only)
+hipError_t launch_advance_scalars_mono(const DevState& S, hipStream_t st, double dt, int fold = 0);
 hipError_t launch_damping_coefs(const DevState& S, hipStream_t st, double zd, double xnutr);
 hipError_t launch_compute_signs(const DevState& S, hipStream_t st);
 // strided device view <-> LP-padded 3-D field (elem 8: fp64, 1: uint8 masks)

@@ -16,7 +16,7 @@ roofline.achieved divides by the measured launch time.
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
-          ddx=False, ntu=False, live=False, nst=False, navg=False):
+          ddx=False, ntu=False, live=False, nst=False, navg=False, save=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -222,9 +222,10 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             return ["wwAvg", "ruAvg"], ["wwAvg_split", "ruAvg_split"]
         return ["wwAvg", "rho_zz_old_split", "ruAvg"], ["wwAvg_split", "rho_zz", "ruAvg_split"]
     if task == "atm_advance_scalars_mono":  # k_transport.hip (Q26: MPAS-A's, not the reference's)
-        return (["scalars_old", "ruAvg", "wwAvg", "rho_zz_old_split", "rho_zz", "cellsOnEdge", "advCellsForEdge",
-                 "nAdvCellsForEdge", "adv_coefs", "adv_coefs_3rd", "dvEdge", "edgesOnCell", "nEdgesOnCell",
-                 "invAreaCell"], ["scalars"])
+        # (save, option trsave: scalars_save folded in -- the old values read from scalars, scalars_old stored)
+        return (["scalars" if save else "scalars_old", "ruAvg", "wwAvg", "rho_zz_old_split", "rho_zz", "cellsOnEdge",
+                 "advCellsForEdge", "nAdvCellsForEdge", "adv_coefs", "adv_coefs_3rd", "dvEdge", "edgesOnCell",
+                 "nEdgesOnCell", "invAreaCell"], ["scalars"] + (["scalars_old"] if save else []))
     if task == "scalars_save":  # srk3 with transport: scalars_old = scalars
         return ["scalars"], ["scalars_old"]
     if task == "mpas_reconstruct_2d":
@@ -266,7 +267,7 @@ def b_alg(task, dims, **kw):
 
 
 def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-                  fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False):
+                  fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -298,7 +299,9 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
                 ("atm_rk_dynamics_substep_finish", p, 1)]
         if physics == 2:
             out.append(("mpas_reconstruct_2d", {}, 1))
-        if transport:
+        if transport and trsave:  # (option trsave: scalars_save folded into the transport)
+            out += [("atm_advance_scalars_mono", {"save": True}, 1)]
+        elif transport:
             out += [("scalars_save", {}, 1), ("atm_advance_scalars_mono", {}, 1)]
         return out
     if fusesetup:
@@ -346,7 +349,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
 
 
 def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-               fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False):
+               fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
                                                                         fusesetup, fusesml, fusecopy, defer4,
-                                                                        smlsum, ntu, mdamp))
+                                                                        smlsum, ntu, mdamp, trsave))

@@ -221,3 +221,32 @@ def test_edge_groups_equal_direct(x1_2562, variant, L):
     assert not bad, bad[:6]
     bad = compare_states(outs[1], ref, rtol=0.0)
     assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("physics", [1, 2])
+@pytest.mark.parametrize("L", [5, 56])
+def test_trsave_bit_identical(x1_2562, physics, L):
+    """option trsave (atm_srk3 with the transport): scalars_save's copy folded into the transport --
+    its edge and bounds kernels read the old scalars from scalars, the bounds kernel stores every
+    level of each pair column (and the zero slot's) to scalars_old -- the same bits in every field,
+    scalars_old included, as the separate copy; two steps, exact and fast"""
+    from mpasdyn import mesh as M
+    st = make_state(M.zero_based(x1_2562), L, "random")
+    for exact in (1, 0):
+        out = {}
+        for save in (0, 1):
+            got = st.copy()
+            with lib.Context(*st.dims()) as ctx:
+                ctx.set_option("exact", exact)
+                ctx.set_option("physics", physics)
+                ctx.set_option("transport", 1)
+                ctx.set_option("trsave", save)
+                ctx.upload(st)
+                for _ in range(2):
+                    T.atm_srk3(ctx, 720.0, 1)
+                ctx.sync()
+                ctx.download(got)
+            out[save] = got
+        bad = compare_states(out[1], out[0], rtol=0.0)
+        assert not bad, f"exact={exact}: {bad[:6]}"
+        assert np.array_equal(out[1]["scalars_old"], out[0]["scalars_old"])
