@@ -130,7 +130,11 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * within runs of R consecutive entities, one run per XCD (default 64); "trorder_e" the same
  * for the transport's edge kernel alone (0, the default: trorder's).  "trsu" = 1 (speed only; measured
  * slower, default 0): the transport's update forms the upwind update su again instead of
- * storing and reading it.  "trepw" = 2 (speed only; measured within 2 %, default 1): two
+ * storing and reading it.  "trsave" = 1 (default; speed only) folds mpas_atm_srk3's scalars_save
+ * copy into the transport (undecomposed, the default transport kernels): they read the old scalars
+ * from scalars and the bounds kernel stores scalars_old.  "mdamp" = 1 (default; speed only; the MPAS
+ * forms) applies each divergence damping in the kernel that next reads ru_p (the next substep's ru_p
+ * kernel, the stage's recover edge kernel).  "trepw" = 2 (speed only; measured within 2 %, default 1): two
  * edges per wavefront in the transport's edge kernel.  "trtile" = 1
  * (speed only, default 0) runs the transport as two tiled kernels with the scalars of
  * compact cell tiles in LDS and no edge scratch, when every cell has at most 6 edges with
