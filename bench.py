@@ -392,6 +392,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
              "atm_advance_scalars_mono[save]": {"save": True},
              # (option mdamp: the stage's last divergence damping in the recover edge kernel)
              "atm_recover_large_step_variables_work[rk<2-avg+damp]": {"rk_step": 0, "navg": True, "damp": True},
+             "atm_recover_large_step_variables_work[rk1-avg+damp]": {"rk_step": 1, "navg": True, "damp": True},
+             "atm_recover_large_step_variables_work[rk1-avg]": {"rk_step": 1, "navg": True},
              "atm_recover_large_step_variables_work[rk<2+damp]": {"rk_step": 0, "damp": True},
              "atm_recover_large_step_variables_work[rk2+damp]": {"rk_step": 2, "damp": True}}
     def dyn_kw(name):  # atm_compute_dyn_tend_work[rk0|rk>0 (+copy) (+d4o) (+d4i) (-A)] (mpas_ctx.cpp srk3)
@@ -415,6 +417,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
         # ("-st]": option ntu's acoustic launch that stores no acoustic state, the last substep of a stage
         # before the step's last)
         base, nst = (name[:-4] + "]", True) if name.endswith("-st]") else (name, False)
+        # ("-ww]": the MPAS forms' counterpart, wwAvg alone unstored; "-avg+damp]" style recover tags below)
+        base, nww = (base[:-4] + "]", True) if base.endswith("-ww]") else (base, False)
         if task == NORTH_STAR and "[" in name:
             kw = dyn_kw(name)
         elif base.endswith("-old]"):  # a fused acoustic launch that leaves rtheta_pp_old (mpas_ctx.cpp)
@@ -423,6 +427,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
             kw = dict(kw_of.get(base, {}))
         if nst:
             kw["nst"] = True
+        if nww:
+            kw["nww"] = True
         if ddx and (task == "atm_advance_acoustic_step_work" or name in ("hfuse[acoustic+solve_vc]",
                                                                          "hfuse[acoustic-st+solve_vc]")):
             kw["ddx"] = True  # (option smlsum: the acoustic launches read rw_save - rw from X_Dd)

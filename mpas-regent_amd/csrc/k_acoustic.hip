@@ -293,7 +293,7 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
             colk(rpp_f, c) = KEEPW(rpp, keepv<LP>(S, F_rho_pp, KC, c));
             colk(rtp_f, c) = KEEPW(rtp, keepv<LP>(S, F_rtheta_pp, KC, c));
             colk(rwp_f, c) = PADW(rwp);
-            colk(ww_f, c) = PADW(ww);
+            if (!(MPASV && (wold & 2))) colk(ww_f, c) = PADW(ww);  // (MPASV, wold bit 1: wwAvg dead)
         }
         store_div(rtp);
         return;
@@ -385,7 +385,10 @@ __device__ __forceinline__ void acoustic_body(const DevState& S, double dts, int
         // (paired 16-B stores, every lane; level L of rho_pp / rtheta_pp keeps its value)
         put2f<LP>(rpp_f, c, rtp_f, c, k, KEEPW(rs - cofrz * (r_p - r), keepv<LP>(S, F_rho_pp, KC, c)),
                  KEEPW(ts - rdzw * (coftz_p * r_p - coftz * r), keepv<LP>(S, F_rtheta_pp, KC, c)));
-        put2f<LP>(rwp_f, c, ww_f, c, k, PADW(r), PADW(ww));
+        // (wold bit 1, option ntu: a stage's last substep before the last stage -- its wwAvg is dead: the
+        // stage's recover leaves the average alone and the next stage's first substep sets it)
+        if (wold & 2) colk(rwp_f, c) = PADW(r);
+        else put2f<LP>(rwp_f, c, ww_f, c, k, PADW(r), PADW(ww));
         return;
     }
 

@@ -43,7 +43,10 @@ __device__ __forceinline__ void recover_cells_mpas(const DevState& S, const RecK
     wwAvg += rws;
     const double rw = rws + rwp;
     const double w = rw / (fzm * zz + fzp * zz_m);
-    colk(fw(S, F_rho_p), c) = KEEPW(rho_p, kL(F_rho_p));
+    // (NAVG, a stage before the last: rho_p is dead too -- only setup reads it, and the last stage's
+    // recover rewrites it first; rtheta_p after stage 1 likewise -- vert_imp, its reader, runs at the
+    // start of stage 1 only)
+    if (!NAVG) colk(fw(S, F_rho_p), c) = KEEPW(rho_p, kL(F_rho_p));
     colk(fw(S, F_rho_zz), c) = KEEPW(rho_zz, kL(F_rho_zz));
     if (!NAVG) colk(fw(S, F_wwAvg), c) = (k == 0 || k == L) ? ww : PADW(wwAvg);
     colk(fw(S, F_rw), c) = KEEPW0(rw, keepv<LP>(S, F_rw, KC, c, true), kL(F_rw));
@@ -57,7 +60,7 @@ __device__ __forceinline__ void recover_cells_mpas(const DevState& S, const RecK
         colk(fw(S, F_pressure_p), c) = KEEPW(zz * a.rgas * (exner * rtheta_p + rtb * (exner - exb)), kL(F_pressure_p));
     } else {
         const double rtheta_p = rtps + rtpp;
-        colk(fw(S, F_rtheta_p), c) = KEEPW(rtheta_p, kL(F_rtheta_p));
+        if (!(NAVG && a.rk_step == 1)) colk(fw(S, F_rtheta_p), c) = KEEPW(rtheta_p, kL(F_rtheta_p));
         colk(fw(S, F_theta_m), c) = KEEPW((rtheta_p + rtb) / rho_zz, kL(F_theta_m));
     }
 }
@@ -298,8 +301,9 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
         if (!na) HALO_WROTE(S, F_ruAvg, F_ru_p);
         if (nCB && na) k_recover_cells<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
         else if (nCB) k_recover_cells<LP, true><<<nCB, 256, 0, st>>>(S, a);
-        HALO_WROTE(S, F_rho_p, F_rho_zz, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
-        if (!na) HALO_WROTE(S, F_wwAvg);
+        HALO_WROTE(S, F_rho_zz, F_rw, F_w, F_theta_m, F_exner, F_pressure_p);
+        if (!na) HALO_WROTE(S, F_wwAvg, F_rho_p);
+        if (!(na && rk_step == 1)) HALO_WROTE(S, F_rtheta_p);
         auto kw = [&](const DevState& X) {
             const int nb = col_blocks<LP>(X, KC);
             if (nb) k_recover_w<LP, true><<<nb, 256, 0, st>>>(X);
@@ -311,8 +315,9 @@ static hipError_t recover_lp(const DevState& S, hipStream_t st, int ns, int rk_s
     if (nCB && na) k_recover_cells<LP, true, true><<<nCB, 256, 0, st>>>(S, a);
     else if (nCB && S.physics) k_recover_cells<LP, true><<<nCB, 256, 0, st>>>(S, a);
     else if (nCB) k_recover_cells<LP, false><<<nCB, 256, 0, st>>>(S, a);
-    HALO_WROTE(S, F_rho_p, F_rho_zz, F_rw, F_w, F_rtheta_p, F_theta_m, F_exner, F_pressure_p);
-    if (!na) HALO_WROTE(S, F_wwAvg);
+    HALO_WROTE(S, F_rho_zz, F_rw, F_w, F_theta_m, F_exner, F_pressure_p);
+    if (!na) HALO_WROTE(S, F_wwAvg, F_rho_p);
+    if (!(na && rk_step == 1)) HALO_WROTE(S, F_rtheta_p);
     auto ke = [&](const DevState& X) {
         const int nb = col_blocks<LP>(X, KE);
         if (nb && na) k_recover_edges<LP, true, true><<<nb, 256, 0, st>>>(X, a);

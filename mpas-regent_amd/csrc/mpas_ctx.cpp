@@ -1074,8 +1074,14 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             const bool md_fold = c->mdamp && S.physics;
             const int mdp = (md_fold && small_step > 0) ? (small_step == 1 ? 2 : 1) : 0;
             const double cprev = mdp ? divdamp_coef(dts) : 0.0;
-            run_task(c, mdp ? "atm_advance_acoustic_step_work[ss>0+damp]" : acoustic_name(small_step),
-                     [&] { return launch_acoustic(S, st, dts, small_step, c->exact, 0, cprev, tme, 0, 1, 0, mdp); });
+            // (option ntu: the last substep of a stage before the last leaves wwAvg unstored -- its recover
+            // does not read it (the averages are dead there) and the next stage's first substep sets it)
+            const bool nww = S.physics && (c->ntu == 1 || c->ntu == 2) && rk_step < 2 && small_step == n_small - 1;
+            const std::string an = std::string(mdp ? "atm_advance_acoustic_step_work[ss>0+damp]" : acoustic_name(small_step));
+            const std::string anw = nww ? an.substr(0, an.size() - 1) + "-ww]" : an;
+            run_task(c, anw.c_str(), [&] {
+                return launch_acoustic(S, st, dts, small_step, c->exact, 0, cprev, tme, 0, nww ? 3 : 1, 0, mdp);
+            });
             if (!md_fold)
                 run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, dts, small_step == 0); });
         }
@@ -1086,7 +1092,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             // (option mdamp: the stage's last damping in the edge kernel; 2: that substep was the stage's first)
             const int ns_r = number_sub_steps[rk_step];
             const int dmp = (c->mdamp && ns_r > 0) ? (ns_r == 1 ? 2 : 1) : 0;
-            const std::string rn = std::string(navg ? "atm_recover_large_step_variables_work[rk<2-avg]" : recover_name(rk_step));
+            const std::string rn = std::string(navg ? (rk_step == 1 ? "atm_recover_large_step_variables_work[rk1-avg]"
+                                                                   : "atm_recover_large_step_variables_work[rk<2-avg]")
+                                                    : recover_name(rk_step));
             const std::string rnd = dmp ? rn.substr(0, rn.size() - 1) + "+damp]" : rn;
             run_task(c, rnd.c_str(), [&] {
                 return launch_recover_large_step(S, st, ns_r, rk_step, dt, navg ? 1 : 0, dmp, rk_sub_timestep[rk_step]);

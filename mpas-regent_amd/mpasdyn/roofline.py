@@ -16,7 +16,7 @@ roofline.achieved divides by the measured launch time.
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
-          ddx=False, ntu=False, live=False, nst=False, navg=False, save=False):
+          ddx=False, ntu=False, live=False, nst=False, navg=False, save=False, nww=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -144,6 +144,9 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         # (wold False: a fused launch of option fusedamp other than the step's last, which leaves
         # rtheta_pp_old unwritten -- the fused damping reads the stored div instead)
         writes = (["rtheta_pp_old"] if wold else []) + ["rho_pp", "rtheta_pp", "rw_p", "wwAvg"]
+        if nww:  # option ntu, the MPAS forms: a stage's last substep before the last -- its wwAvg is dead
+            writes = [w for w in writes if w != "wwAvg"]
+            reads = [r for r in reads if r != "wwAvg"]
         if nst:  # option ntu: a stage's last substep before the last stage -- its acoustic state is dead
             writes = [w for w in writes if w not in ("rho_pp", "rtheta_pp", "rw_p", "wwAvg")]
             reads = [r for r in reads if r != "wwAvg"]  # (read only for the dead wwAvg)
@@ -209,9 +212,11 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             reads += ["rtheta_pp", "rtheta_pp_old", "theta_m", "isShared", "specZoneMaskEdge"]
             writes += ["ru_p"]
         if navg:  # option ntu, a stage before the last: the averages are dead (the next stage's first substep sets
-            # them), and so is a damped ru_p (the next stage's first substep sets it from tend_u)
+            # them), and so is a damped ru_p (the next stage's first substep sets it from tend_u), rho_p (read
+            # by setup only) and, after stage 1, rtheta_p (read by stage 1's vert_imp only)
             reads = [r for r in reads if r not in ("wwAvg", "ruAvg")]
-            writes = [w for w in writes if w not in ("wwAvg", "ruAvg", "ru_p")]
+            writes = [w for w in writes if w not in ("wwAvg", "ruAvg", "ru_p", "rho_p")
+                      and not (w == "rtheta_p" and rk_step == 1)]
         return reads, writes
     if task == "atm_rk_dynamics_substep_finish":
         # (:1951-2007 with dynamics_substep = dynamics_split = 1, as atm_srk3 calls it: the
@@ -289,10 +294,12 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
         # ru_p kernel or the stage's recover)
         d = {"damp": bool(mdamp)}
         out += [("atm_set_smlstep_pert_variables_work", p, 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 1 if ntu else 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1, "nww": True}, 2 if ntu else 0),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "physics": 1, **d}, 1),
                 ("atm_divergence_damping_3d", {}, 0 if mdamp else 4),
-                ("atm_recover_large_step_variables_work", {"rk_step": 0, "navg": bool(ntu), **d}, 2),
+                ("atm_recover_large_step_variables_work", {"rk_step": 0, "navg": bool(ntu), **d}, 1),
+                ("atm_recover_large_step_variables_work", {"rk_step": 1, "navg": bool(ntu), **d}, 1),
                 ("atm_recover_large_step_variables_work", {"rk_step": 2, **d}, 1),
                 ("atm_compute_solve_diagnostics", {"live": bool(ntu), **p}, 2),
                 ("atm_compute_solve_diagnostics", {"reconstruct_v": True, **p}, 1),
