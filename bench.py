@@ -407,6 +407,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
             kw["ntu"] = True
         if "+v" in tag:
             kw["store_v"] = True
+        if "+ru" in tag:  # (option mru: the first substep's ru_p / ruAvg stored here)
+            kw["ru"] = True
         if tag.endswith("-A"):
             kw["noA"] = True
         return kw
@@ -416,9 +418,11 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
         task = name.split("[")[0]
         # ("-st]": option ntu's acoustic launch that stores no acoustic state, the last substep of a stage
         # before the step's last)
-        base, nst = (name[:-4] + "]", True) if name.endswith("-st]") else (name, False)
-        # ("-ww]": the MPAS forms' counterpart, wwAvg alone unstored; "-avg+damp]" style recover tags below)
+        # ("-ru]", outermost: option mru, the first substep's ru_p / ruAvg stored by dyn_tend; "-ww]": the MPAS
+        # forms' counterpart of "-st", wwAvg alone unstored)
+        base, rud = (name[:-4] + "]", True) if name.endswith("-ru]") else (name, False)
         base, nww = (base[:-4] + "]", True) if base.endswith("-ww]") else (base, False)
+        base, nst = (base[:-4] + "]", True) if base.endswith("-st]") else (base, False)
         if task == NORTH_STAR and "[" in name:
             kw = dyn_kw(name)
         elif base.endswith("-old]"):  # a fused acoustic launch that leaves rtheta_pp_old (mpas_ctx.cpp)
@@ -429,6 +433,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
             kw["nst"] = True
         if nww:
             kw["nww"] = True
+        if rud:
+            kw["rudone"] = True
         if ddx and (task == "atm_advance_acoustic_step_work" or name in ("hfuse[acoustic+solve_vc]",
                                                                          "hfuse[acoustic-st+solve_vc]")):
             kw["ddx"] = True  # (option smlsum: the acoustic launches read rw_save - rw from X_Dd)
@@ -698,8 +704,9 @@ def main():
     # (option trsave: scalars_save folded into the transport, undecomposed with the default transport kernels)
     trsave = bool(args.transport) and bool(ctx.get_option("trsave")) and not decomposed and not any(
         ctx.get_option(o) for o in ("trtile", "tredge", "trsu"))
+    mru = bool(ctx.get_option("mru")) and int(args.physics) == 2 and not args.exact
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
-                                 smls, ntu, mdamp, trsave)
+                                 smls, ntu, mdamp, trsave, mru)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -723,7 +730,7 @@ def main():
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy), "smlsum": int(smls),
-                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "mdamp": int(mdamp), "trsave": int(trsave), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
+                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "mdamp": int(mdamp), "trsave": int(trsave), "mru": int(mru), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}

@@ -581,9 +581,10 @@ __global__ __launch_bounds__(256) void k_acoustic_ru(DevState S, double dts, int
 
 template <int LP>
 static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                              double coef_prev, int tme, int sml, int wold, int ddx, int mdamp) {
+                              double coef_prev, int tme, int sml, int wold, int ddx, int mdamp, int rudone) {
     if ((tme && (S.physics || S.halo)) || (sml && S.physics)) return hipErrorInvalidValue;  // (atm_srk3, reference semantics)
     if (mdamp && (!S.physics || small_step == 0)) return hipErrorInvalidValue;
+    if (rudone && (S.physics != 2 || small_step != 0)) return hipErrorInvalidValue;
     if (sml && (small_step != 0 || mode == 0)) return hipErrorInvalidValue;
     double epssm = kEpssm;
     double resm = (1.0 - epssm) / (1.0 + epssm);
@@ -602,7 +603,8 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
             else if (dmp) k_acoustic_ru<LP, false, true, false><<<nb, 256, 0, st>>>(X, dts, small_step, c2, coef_prev);
             else k_acoustic_ru<LP, false><<<nb, 256, 0, st>>>(X, dts, small_step, c2, 0.0);
         };
-        if (small_step == 0) HALO_RUN(S, st, ru);  // (own columns only: no ghost read)
+        if (small_step == 0 && rudone) {  // (option mru: this stage's dyn_tend stored ru_p / ruAvg)
+        } else if (small_step == 0) HALO_RUN(S, st, ru);  // (own columns only: no ghost read)
         else if (dmp) HALO_RUN(S, st, ru, F_rtheta_pp, F_zz, F_exner, F_rho_pp, F_rtheta_pp_old, F_theta_m);
         else HALO_RUN(S, st, ru, F_rtheta_pp, F_zz, F_exner, F_rho_pp);
         HALO_WROTE(S, F_ru_p, F_ruAvg);
@@ -705,8 +707,9 @@ static hipError_t acoustic_lp(const DevState& S, hipStream_t st, double dts, int
     return hipGetLastError();
 }
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode,
-                           double coef_prev, int tme, int sml, int wold, int ddx, int mdamp) {
-    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml, wold, ddx, mdamp);
+                           double coef_prev, int tme, int sml, int wold, int ddx, int mdamp, int rudone) {
+    MPAS_LP_DISPATCH(S.LP, acoustic_lp, S, st, dts, small_step, exact, mode, coef_prev, tme, sml, wold, ddx, mdamp,
+                     rudone);
 }
 template <int LP>
 static hipError_t hf_ac_vc_lp(const DevState& S, hipStream_t st, double dts, int small_step, int exact,

@@ -53,7 +53,22 @@ struct DynK {
     int rk_step, horiz_mixing, rayleigh, exact_q, tme, cp, d4o, vB;
     double cs_l2, cap, cam_coef, h4, inv_r_earth, r_earth, rayleigh_inv, prandtl_inv;
     double h4d;  // DIN: the h4 of the rk_step 0 call whose del4 of tend_u_euler this call applies
+    double rud;  // (option mru, the MPAS dynamics, fast path) the stage's dts: the kernel forming the final
+                 // tend_u also stores the first substep's ru_p = dts tend_u and ruAvg = ru_p
 };
+
+// option mru (the MPAS dynamics, atm_srk3 fast path): the stage's first acoustic substep begins with
+// ru_p = dts tend_u, ruAvg = ru_p on every edge (k_acoustic_ru FIRST, :1581-1613 restored, Q18) -- formed
+// here by the kernel that forms the final tend_u, from the value it stores (the same expressions; level
+// L and the padding as k_acoustic_ru stores them), and that launch goes
+template <int LP>
+__device__ __forceinline__ void ru_first(const DevState& S, double dts, int e, int k, int L, double tu) {
+    const size_t pL = (size_t)e * LP + lpos(LP, L);
+    const double rp0 = ldc(fd(S, F_ru_p) + pL), ra0 = ldc(fd(S, F_ruAvg) + pL);
+    const double rp = dts * tu;
+    colk(fw(S, F_ru_p), e) = KEEPW(rp, rp0);
+    colk(fw(S, F_ruAvg), e) = KEEPW(rp, ra0);
+}
 
 
 // ------------------------------------------------------------------------ A (cells)
@@ -583,6 +598,9 @@ __global__ __launch_bounds__(256, LP == 64 && DIN ? 4 : 1) void k_dyn_B(DevState
                 } else {
                     put2<LP>(Fo, e, tuo, e, k, Hv, PADW(tend_u), true, k != L);
                 }
+                if constexpr (MD) {  // (option mru; rp at level L and above is not the stored tend_u's: KEEPW)
+                    if (a.rud != 0.0) ru_first<LP>(S, a.rud, e, k, L, PADW(tend_u));
+                }
             }
             if (rk0) put2<LP>(tueo, e, fw(S, F_delsq_u), e, k, PADW(tue), dsq, k != L, k != L);
             if (DIN && k != L) colk(tueo, e) = PADW(tue);
@@ -865,6 +883,7 @@ __device__ __forceinline__ void dyn_D_body(const DevState& S, const DynK& a, Blk
     tend_u += tue + trp;
     // (padding levels: zeros, PADW; level L keeps its value; one paired 16-B store, every lane)
     put2f<LP>(fw(S, F_tend_u_euler), e, fw(S, F_tend_u), e, k, KEEPW(tue, kl_tue), KEEPW(tend_u, kl_tu));
+    if (a.rud != 0.0) ru_first<LP>(S, a.rud, e, k, L, KEEPW(tend_u, kl_tu));  // (option mru)
 }
 
 // ------------------------------------------------------------------------ E (cells)
@@ -1442,6 +1461,7 @@ static DynK make_dynk(const DevState& S, const DynTendArgs& in) {
     a.d4o = (in.defer_out && in.rk_step == 0 && a.h4 > 0.0) ? 1 : 0;
     a.vB = (in.store_v && S.eoe_same && S.physics != 2) ? 1 : 0;
     a.h4d = (in.defer_in && in.rk_step != 0 && in.horiz_mixing == 0) ? kVisc4_2dsmag * (kLenDisp * kLenDisp * kLenDisp) : 0.0;
+    a.rud = (S.physics == 2 && !in.exact_q) ? in.rud : 0.0;  // (option mru: the fast path's HF kernels, and D)
     return a;
 }
 
@@ -1680,6 +1700,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     HALO_WROTE(S, F_tend_w_euler, F_tend_rtheta_adv, F_rthdynten, F_tend_theta, F_tend_theta_euler);
     HALO_WROTE(S, MD ? F_tend_w : F_w);
     if (a.cp) HALO_WROTE(S, F_ru_save, F_u_2);
+    if (a.rud != 0.0) HALO_WROTE(S, F_ru_p, F_ruAvg);  // (option mru)
     return hipGetLastError();
 }
 template <int LP>

@@ -108,6 +108,8 @@ struct mpas_ctx {
                        // (reference semantics, edgesOnEdge_ECP = edgesOnEdge; same values)
     int defer4 = 1;    // option "defer4": atm_srk3 applies rk_step 0's del4 of tend_u_euler (dyn_tend D) in the
                        // next stage's rk_step > 0 edge kernel (reference semantics; same values)
+    int mru = 1;       // option "mru" (the MPAS dynamics, fast path): the kernel forming a stage's final tend_u
+                       // stores its first acoustic substep's ru_p / ruAvg (k_acoustic_ru FIRST skipped)
     int mdamp = 1;     // option "mdamp" (the MPAS forms): each divergence damping applied by the kernel that next
                        // reads ru_p -- the next substep's k_acoustic_ru, or the stage's recover edge kernel
     int ntu = 1;       // option "ntu" (with defer4): that rk_step 0 call's whole tend_u is dead (the next stage's
@@ -986,6 +988,10 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             a.nth = 1;
             a.ntu = 1;  // (launch_dyn_tend keeps it off where D runs in the call)
         }
+        // option mru (the MPAS dynamics, fast path): the kernel that forms the stage's final tend_u also
+        // stores the first acoustic substep's ru_p = dts tend_u and ruAvg = ru_p (nothing in between reads
+        // or writes them; set_smlstep reads tend_u only)
+        if (c->mru && S.physics == 2 && !c->exact && number_sub_steps[r] > 0) a.rud = rk_sub_timestep[r];
         return a;
     };
     bool flux_done = false;  // (option smlsum: the step's flux sum, beside setup and A on small grids)
@@ -1023,8 +1029,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         // timing key: the variant's read / write set (bench.py parses the tags)
         const std::string dname = std::string("atm_compute_dyn_tend_work[") + (a.rk_step == 0 ? "rk0" : "rk>0") +
                                   (a.cp ? "+copy" : "") + (a.defer_out ? "+d4o" : "") + (a.ntu ? "+ntu" : "") + (a.defer_in ? "+d4i" : "") +
-                                  (a.store_v ? "+v" : "") + (a.skipA ? "-A" : "") + "]";
+                                  (a.store_v ? "+v" : "") + (a.rud != 0.0 ? "+ru" : "") + (a.skipA ? "-A" : "") + "]";
         run_task(c, dname.c_str(), [&] { return launch_dyn_tend(S, st, a); });
+        const bool ru_done = a.rud != 0.0;  // (option mru: the first substep's ru_p / ruAvg stored)
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
         const bool sml = fuse && c->fusesml;
         if (!sml) run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st, c->exact); });
@@ -1078,9 +1085,12 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
             // does not read it (the averages are dead there) and the next stage's first substep sets it)
             const bool nww = S.physics && (c->ntu == 1 || c->ntu == 2) && rk_step < 2 && small_step == n_small - 1;
             const std::string an = std::string(mdp ? "atm_advance_acoustic_step_work[ss>0+damp]" : acoustic_name(small_step));
-            const std::string anw = nww ? an.substr(0, an.size() - 1) + "-ww]" : an;
+            const std::string an1 = nww ? an.substr(0, an.size() - 1) + "-ww]" : an;
+            // ("-ru": option mru, this first substep's ru_p / ruAvg were stored by the stage's dyn_tend)
+            const std::string anw = (small_step == 0 && ru_done) ? an1.substr(0, an1.size() - 1) + "-ru]" : an1;
             run_task(c, anw.c_str(), [&] {
-                return launch_acoustic(S, st, dts, small_step, c->exact, 0, cprev, tme, 0, nww ? 3 : 1, 0, mdp);
+                return launch_acoustic(S, st, dts, small_step, c->exact, 0, cprev, tme, 0, nww ? 3 : 1, 0, mdp,
+                                       (small_step == 0 && ru_done) ? 1 : 0);
             });
             if (!md_fold)
                 run_task(c, "atm_divergence_damping_3d", [&] { return launch_div_damping(S, st, dts, small_step == 0); });
@@ -1427,6 +1437,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "defer4") == 0) c->defer4 = value ? 1 : 0;
         else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value < 0 ? 0 : value > 3 ? 3 : value;
         else if (name && std::strcmp(name, "mdamp") == 0) c->mdamp = value ? 1 : 0;
+        else if (name && std::strcmp(name, "mru") == 0) c->mru = value ? 1 : 0;
         else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
@@ -1595,6 +1606,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "defer4") == 0) *value = c->defer4;
         else if (name && std::strcmp(name, "ntu") == 0) *value = c->ntu;
         else if (name && std::strcmp(name, "mdamp") == 0) *value = c->mdamp;
+        else if (name && std::strcmp(name, "mru") == 0) *value = c->mru;
         else if (name && std::strcmp(name, "vdyn") == 0) *value = c->vdyn;
         else if (name && std::strcmp(name, "eoe_same") == 0) {
             prepare_now(c);

@@ -204,6 +204,9 @@ struct DynTendArgs {
     // option "ntu" (with defer_out): that call's tend_u is dead altogether (the next stage's edge
     // kernel rewrites it, no task in between reads it): the edge kernel forms none of it
     int ntu = 0;
+    // option "mru" (atm_srk3, the MPAS dynamics, fast path): the stage's dts -- the kernel forming the final
+    // tend_u stores the first acoustic substep's ru_p and ruAvg (k_acoustic_ru FIRST then skipped)
+    double rud = 0.0;
     // option "ntu" (atm_srk3, reference semantics, a stage before the step's last): the call's theta
     // tendencies are dead as well (the last stage rewrites them; the acoustic step reads theta_m as
     // its tend_rt, Q8): E forms none of them, B no per-edge flux for them
@@ -261,7 +264,8 @@ hipError_t launch_set_smlstep(const DevState& S, hipStream_t st, int exact);
 // ddx: rw_save - rw from X_Dd (atm_srk3 with option smlsum: launch_sml_flux formed it this step)
 hipError_t launch_acoustic(const DevState& S, hipStream_t st, double dts, int small_step, int exact, int mode = 0,
                            double coef_prev = 0.0, int tme = 0, int sml = 0, int wold = 1, int ddx = 0,
-                           int mdamp = 0);  // (mdamp: the MPAS forms, the previous substep's damping folded in)
+                           int mdamp = 0,   // (mdamp: the MPAS forms, the previous substep's damping folded in)
+                           int rudone = 0);  // (rudone: option mru -- this stage's dyn_tend stored ru_p / ruAvg)
 // X_smlS = the sum of set_smlstep's slope-flux terms per cell and level (atm_srk3 fast path,
 // once per step: u_tend / zb_cell / zb3_cell are not written within a step)
 hipError_t launch_sml_flux(const DevState& S, hipStream_t st);

@@ -16,7 +16,8 @@ roofline.achieved divides by the measured launch time.
 # name -> (reads, writes); each a list of field names of the registry
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
-          ddx=False, ntu=False, live=False, nst=False, navg=False, save=False, nww=False):
+          ddx=False, ntu=False, live=False, nst=False, navg=False, save=False, nww=False, ru=False,
+          rudone=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -102,6 +103,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             reads += ["uReconstructZonal", "uReconstructMeridional", "w"]
         if copy:  # option fusecopy (stage 0): setup's ru_save = ru, u_2 = u (ru, u already read)
             writes = writes + ["ru_save", "u_2"]
+        if ru:  # option mru (the MPAS dynamics): the first acoustic substep's ru_p, ruAvg from the final tend_u
+            writes = writes + ["ru_p", "ruAvg"]
         if store_v:  # option vdyn (stage 2): solve_diagnostics' v from the gathered edgesOnEdge u
             writes = writes + ["v"]
         if defer_out and rk_step == 0:  # option defer4: tend_u of this call is dead and not stored
@@ -151,10 +154,12 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             writes = [w for w in writes if w not in ("rho_pp", "rtheta_pp", "rw_p", "wwAvg")]
             reads = [r for r in reads if r != "wwAvg"]  # (read only for the dead wwAvg)
         if physics:  # the MPAS form (option physics = 1): the ru_p / ruAvg update of :1581-1613
-            reads += ["tend_u", "tend_theta", "c_tri", "gamma_tri", "specZoneMaskEdge"]
+            reads += ["tend_theta", "c_tri", "gamma_tri", "specZoneMaskEdge"]
+            if not rudone:  # (option mru: the first substep's ru_p / ruAvg stored by dyn_tend)
+                reads += ["tend_u"]
+                writes += ["ru_p", "ruAvg"]
             if small_step != 0:
                 reads += ["ru_p", "ruAvg", "exner", "cqu", "zxu", "invDcEdge"]
-            writes += ["ru_p", "ruAvg"]
         if damp:  # option fusedamp: the previous substep's atm_divergence_damping_3d applied here
             reads += ["rtheta_pp", "rtheta_pp_old", "isShared", "specZoneMaskEdge"]
             writes += ["ru_p"]
@@ -272,7 +277,7 @@ def b_alg(task, dims, **kw):
 
 
 def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-                  fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False):
+                  fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False, mru=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -287,15 +292,17 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
         else:
             out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
                    ("atm_compute_vert_imp_coefs", {}, 2)]
+        r = {"ru": True} if mru else {}  # (option mru: the first substep's ru_p / ruAvg stored by dyn_tend)
         if schedule == 1:
-            out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, **p}, 1),
-                    ("atm_compute_dyn_tend_work", {"rk_step": 1, **p}, 2)]
+            out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, **p, **r}, 1),
+                    ("atm_compute_dyn_tend_work", {"rk_step": 1, **p, **r}, 2)]
         # (option mdamp: each damping applied by the next kernel that reads ru_p -- the next substep's
         # ru_p kernel or the stage's recover)
         d = {"damp": bool(mdamp)}
         out += [("atm_set_smlstep_pert_variables_work", p, 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1}, 1 if ntu else 3),
-                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1, "nww": True}, 2 if ntu else 0),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1, "rudone": bool(mru)}, 1 if ntu else 3),
+                ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1, "nww": True, "rudone": bool(mru)},
+                 2 if ntu else 0),
                 ("atm_advance_acoustic_step_work", {"small_step": 1, "physics": 1, **d}, 1),
                 ("atm_divergence_damping_3d", {}, 0 if mdamp else 4),
                 ("atm_recover_large_step_variables_work", {"rk_step": 0, "navg": bool(ntu), **d}, 1),
@@ -356,7 +363,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
 
 
 def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-               fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False):
+               fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False, mru=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
                                                                         fusesetup, fusesml, fusecopy, defer4,
-                                                                        smlsum, ntu, mdamp, trsave))
+                                                                        smlsum, ntu, mdamp, trsave, mru))

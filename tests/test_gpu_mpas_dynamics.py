@@ -303,3 +303,28 @@ def test_mdamp_bit_identical(x1_2562, physics, transport, L):
         for key in ((1, 0), (1, 1)):
             bad = compare_states(out[key], out[(0, 0)], rtol=0.0)
             assert not bad, f"exact={exact} mdamp, ntu={key}: {bad[:6]}"
+
+
+@pytest.mark.parametrize("transport", [0, 1])
+@pytest.mark.parametrize("L", [5, 56])
+def test_mru_bit_identical(x1_2562, transport, L):
+    """option mru (the MPAS dynamics, fast path): the kernel forming each stage's final tend_u (B, or D
+    at rk_step 0) also stores the first acoustic substep's ru_p = dts tend_u and ruAvg = ru_p, and that
+    substep's ru_p kernel goes -- every field after three steps has the same bits as with the kernel"""
+    st = state(x1_2562, L, "mpas0")
+    out = {}
+    for mru in (0, 1):
+        got = st.copy()
+        with lib.Context(*st.dims()) as ctx:
+            ctx.set_option("exact", 0)
+            ctx.set_option("physics", 2)
+            ctx.set_option("transport", transport)
+            ctx.set_option("mru", mru)
+            ctx.upload(st)
+            for _ in range(3):
+                T.atm_srk3(ctx, 720.0, 1)
+            ctx.sync()
+            ctx.download(got)
+        out[mru] = got
+    bad = compare_states(out[1], out[0], rtol=0.0)
+    assert not bad, bad[:6]
