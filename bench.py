@@ -420,7 +420,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
         # before the step's last)
         # ("-ru]", outermost: option mru, the first substep's ru_p / ruAvg stored by dyn_tend; "-ww]": the MPAS
         # forms' counterpart of "-st", wwAvg alone unstored)
-        base, rud = (name[:-4] + "]", True) if name.endswith("-ru]") else (name, False)
+        base, nbc = (name[:-4] + "]", True) if name.endswith("-bc]") else (name, False)  # (ntu: b_tri / c_tri)
+        base, rud = (base[:-4] + "]", True) if base.endswith("-ru]") else (base, False)
         base, nww = (base[:-4] + "]", True) if base.endswith("-ww]") else (base, False)
         base, nst = (base[:-4] + "]", True) if base.endswith("-st]") else (base, False)
         if task == NORTH_STAR and "[" in name:
@@ -435,6 +436,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
             kw["nww"] = True
         if rud:
             kw["rudone"] = True
+        if nbc:
+            kw["nbc"] = True
         if ddx and (task == "atm_advance_acoustic_step_work" or name in ("hfuse[acoustic+solve_vc]",
                                                                          "hfuse[acoustic-st+solve_vc]")):
             kw["ddx"] = True  # (option smlsum: the acoustic launches read rw_save - rw from X_Dd)

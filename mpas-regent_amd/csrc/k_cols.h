@@ -43,7 +43,10 @@ __device__ __forceinline__ void st64k(double* d, size_t i, double2 v, Pair64 q, 
 template <int LP, bool MPASV>
 __device__ __forceinline__ void vi_column(const DevState& S, int c, int k, double zz, double exner, double tm, double cqw,
                                           double qtot, double rb, double rtb, double rtp, double exb, double gamma_old,
-                                          double coftz_old, double dtseps, double rcv, double c2, bool live = true) {
+                                          double coftz_old, double dtseps, double rcv, double c2, bool live = true,
+                                          bool nbc = false) {
+    // (nbc, atm_srk3 option ntu: stage 0's vert_imp -- b_tri and c_tri are dead there: stage 1's vert_imp
+    // rewrites both and no task reads them in between, nor does that vert_imp; not stored)
     const int L = S.L;
     const double *fzm_a = fd(S, F_fzm), *fzp_a = fd(S, F_fzp), *rdzu_a = fd(S, F_rdzu), *rdzw_a = fd(S, F_rdzw);
     const double fzm = fzm_a[k], fzp = fzp_a[k], rdzu = rdzu_a[k], rdzw = rdzw_a[k];
@@ -119,10 +122,17 @@ __device__ __forceinline__ void vi_column(const DevState& S, int c, int k, doubl
     put2<LP>(fw(S, F_coftz), c, fw(S, F_cofwt), c, k, KEEPW(coftz, kL(F_coftz)), KEEPW(cofwt, kL(F_cofwt)), live, live);
     put2<LP>(fw(S, F_cofwr), c, fw(S, F_cofwz), c, k, KEEPW0(cofwr, k0(F_cofwr), kL(F_cofwr)),
              KEEPW0(cofwz, k0(F_cofwz), kL(F_cofwz)), live, live);
-    put2<LP>(fw(S, F_a_tri), c, fw(S, F_b_tri), c, k, KEEPW0(a, k0(F_a_tri), kL(F_a_tri)),
-             KEEPW0(b, k0(F_b_tri), kL(F_b_tri)), live, live);
-    put2<LP>(fw(S, F_c_tri), c, fw(S, F_alpha_tri), c, k, KEEPW0(cc, k0(F_c_tri), kL(F_c_tri)),
-             KEEPW0(alpha, k0(F_alpha_tri), kL(F_alpha_tri)), live, live);
+    if (nbc) {
+        if (live) {
+            colk(fw(S, F_a_tri), c) = KEEPW0(a, k0(F_a_tri), kL(F_a_tri));
+            colk(fw(S, F_alpha_tri), c) = KEEPW0(alpha, k0(F_alpha_tri), kL(F_alpha_tri));
+        }
+    } else {
+        put2<LP>(fw(S, F_a_tri), c, fw(S, F_b_tri), c, k, KEEPW0(a, k0(F_a_tri), kL(F_a_tri)),
+                 KEEPW0(b, k0(F_b_tri), kL(F_b_tri)), live, live);
+        put2<LP>(fw(S, F_c_tri), c, fw(S, F_alpha_tri), c, k, KEEPW0(cc, k0(F_c_tri), kL(F_c_tri)),
+                 KEEPW0(alpha, k0(F_alpha_tri), kL(F_alpha_tri)), live, live);
+    }
     if (live) colk(fw(S, F_gamma_tri), c) = k == 0 ? 0.0 : KEEPW(gamma, kL(F_gamma_tri));
     if (live && c == 0 && k < L) fw(S, F_cofrz)[k] = cofrz;
 }
@@ -520,7 +530,7 @@ __device__ __forceinline__ void setup_vi_body(const DevState& S, int ncb, double
     if (blk >= ncb) {  // :767-771 ru_save = ru, u_2 = u (every level but L)
         const int e = col_of<LP>(xcd_block_n(S.xcd, blk - ncb, bk.n - ncb)) + S.lo[KE];
         if (e >= S.nEO) return;
-        if (copies) {
+        if (copies & 1) {
             double ru, u;
             gather2<LP>(fd(S, F_ru), e, fd(S, F_u), e, k, ru, u);
             put2f<LP>(fw(S, F_ru_save), e, fw(S, F_u_2), e, k, KEEPW(ru, keepv<LP>(S, F_ru_save, KE, e)),
@@ -563,6 +573,6 @@ __device__ __forceinline__ void setup_vi_body(const DevState& S, int ncb, double
              KEEPW0(cqw, keepv<LP>(S, F_cqw, KC, c, true), kL(F_cqw)), live, live);
     // (cqw is used at 0 < k < L only, qtot at k < L: the values just written)
     vi_column<LP, MPASV>(S, c, k, zz, exner, tm, cqw, qtot, rb, rtb, rtp, exb, gamma_old, coftz_old, dtseps, rcv, c2,
-                         live);
+                         live, (copies & 2) != 0);  // (copies bit 1: b_tri / c_tri dead, atm_srk3 option ntu)
 }
 }  // namespace mpas

@@ -166,13 +166,13 @@ __global__ __launch_bounds__(256) void k_setup_vi(DevState S, int ncb, double dt
     setup_vi_body<LP, MPASV, MD>(S, ncb, dtseps, rcv, c2, this_blk(), copies);
 }
 template <int LP>
-static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts, bool edges) {
+static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts, bool edges, int nbc) {
     double dtseps = .5 * dts * (1.0 + kEpssm);
     double rcv = kRgas / (kCp - kRgas);
     double c2 = kCp * rcv;
     const bool md = S.physics == 2;
     const int ncb = col_blocks<LP>(S, KC), neb = (edges || md) ? col_blocks<LP>(S, KE) : 0;
-    const int cp = edges ? 1 : 0;
+    const int cp = (edges ? 1 : 0) | (nbc ? 2 : 0);
     if (ncb + neb) {
         if (md) k_setup_vi<LP, true, true><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2, cp);
         else if (S.physics) k_setup_vi<LP, true, false><<<ncb + neb, 256, 0, st>>>(S, ncb, dtseps, rcv, c2, cp);
@@ -182,11 +182,12 @@ static hipError_t setup_vi_lp(const DevState& S, hipStream_t st, double dts, boo
     if (edges) HALO_WROTE(S, F_ru_save, F_u_2);
     HALO_WROTE(S, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w_2, F_theta_m_2, F_rho_zz_2, F_rho_zz_old_split, F_qtot,
                F_cqw);
-    HALO_WROTE(S, F_coftz, F_cofwt, F_gamma_tri, F_cofwr, F_cofwz, F_a_tri, F_b_tri, F_c_tri, F_alpha_tri);
+    HALO_WROTE(S, F_coftz, F_cofwt, F_gamma_tri, F_cofwr, F_cofwz, F_a_tri, F_alpha_tri);
+    if (!nbc) HALO_WROTE(S, F_b_tri, F_c_tri);
     return hipGetLastError();
 }
-hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts, bool edges) {
-    MPAS_LP_DISPATCH(S.LP, setup_vi_lp, S, st, dts, edges);
+hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts, bool edges, int nbc) {
+    MPAS_LP_DISPATCH(S.LP, setup_vi_lp, S, st, dts, edges, nbc);
 }
 
 template <int LP, bool MPASV>

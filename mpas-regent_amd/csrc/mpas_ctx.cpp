@@ -1006,8 +1006,12 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         a_done = true;
         flux_done = smls;
     } else if (c->fusesetup) {  // :404-417 as one column-local launch (same values; MPAS forms under physics)
-        run_task(c, fcopy ? "atm_rk_integration_setup[cells+moist+vert_imp]" : "atm_rk_integration_setup[+moist+vert_imp]",
-                 [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0], !fcopy); });
+        // (option ntu: stage 0's vert_imp leaves b_tri / c_tri unstored -- no task reads them and stage 1's
+        // vert_imp, which always runs, rewrites both; "-bc")
+        const bool nbc = c->ntu == 1 || c->ntu == 2;
+        run_task(c, fcopy ? (nbc ? "atm_rk_integration_setup[cells+moist+vert_imp-bc]" : "atm_rk_integration_setup[cells+moist+vert_imp]")
+                          : (nbc ? "atm_rk_integration_setup[+moist+vert_imp-bc]" : "atm_rk_integration_setup[+moist+vert_imp]"),
+                 [&] { return launch_setup_moist_vert_imp(S, st, rk_sub_timestep[0], !fcopy, nbc ? 1 : 0); });
     } else {
         run_task(c, "atm_rk_integration_setup", [&] { return launch_rk_integration_setup(S, st); });
         run_task(c, "atm_compute_moist_coefficients", [&] { return launch_moist_coefficients(S, st); });

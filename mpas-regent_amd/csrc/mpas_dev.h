@@ -238,7 +238,8 @@ hipError_t launch_rk_integration_setup(const DevState& S, hipStream_t st);
 hipError_t launch_moist_coefficients(const DevState& S, hipStream_t st);
 hipError_t launch_vert_imp_coefs(const DevState& S, hipStream_t st, double dts);
 // setup + moist + vert_imp(dts) in one launch (option "fusesetup", reference semantics)
-hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts, bool edges = true);
+// (nbc, atm_srk3 option ntu: vert_imp's b_tri / c_tri not stored -- stage 1's vert_imp rewrites them)
+hipError_t launch_setup_moist_vert_imp(const DevState& S, hipStream_t st, double dts, bool edges = true, int nbc = 0);
 // option hfuse (atm_srk3, reference semantics, undecomposed): a stage's last acoustic launch
 // (mode 2) beside its solve_diagnostics vertex / cell kernel; the stage's solve_diagnostics
 // edge kernel beside the next stage's dyn_tend A (and stage 1's vert_imp after stage 0)

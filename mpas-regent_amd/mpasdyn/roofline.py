@@ -17,7 +17,7 @@ roofline.achieved divides by the measured launch time.
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
           ddx=False, ntu=False, live=False, nst=False, navg=False, save=False, nww=False, ru=False,
-          rudone=False):
+          rudone=False, nbc=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -55,6 +55,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         if copy:  # option fusecopy: the edge copies ru_save = ru, u_2 = u moved to dyn_tend
             reads = [r for r in reads if r not in ("ru", "u")]
             writes = [w for w in writes if w not in ("ru_save", "u_2")]
+        if nbc:  # option ntu: stage 0's b_tri / c_tri are dead (stage 1's vert_imp rewrites them)
+            writes = [w for w in writes if w not in ("b_tri", "c_tri")]
         return reads, writes
     if task == "atm_rk_integration_setup":
         return (["rho_p", "rho_zz", "rtheta_p", "rw", "theta_m", "w", "ru", "u"],
@@ -287,7 +289,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     if physics:
         p = {"physics": physics}
         if fusesetup:  # stage 0's setup + moist + vert_imp in one launch (MPAS forms)
-            out = [("atm_rk_integration_setup", {"fused": True, "copy": copy, **p}, 1),
+            out = [("atm_rk_integration_setup", {"fused": True, "copy": copy, "nbc": bool(ntu), **p}, 1),
                    ("atm_compute_vert_imp_coefs", {}, 1)]
         else:
             out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
@@ -319,7 +321,8 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
             out += [("scalars_save", {}, 1), ("atm_advance_scalars_mono", {}, 1)]
         return out
     if fusesetup:
-        out = [("atm_rk_integration_setup", {"fused": True, "copy": copy}, 1), ("atm_compute_vert_imp_coefs", {}, 1)]
+        out = [("atm_rk_integration_setup", {"fused": True, "copy": copy, "nbc": bool(ntu)}, 1),
+               ("atm_compute_vert_imp_coefs", {}, 1)]
     else:
         out = [("atm_rk_integration_setup", {}, 1), ("atm_compute_moist_coefficients", {}, 1),
                ("atm_compute_vert_imp_coefs", {}, 2)]
