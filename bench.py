@@ -371,6 +371,9 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
              "atm_compute_solve_diagnostics[vc]": {"part": "vc"}, "atm_compute_solve_diagnostics[e]": {"part": "e"},
              "hfuse[damp+solve_vc]": {"pair": "damp+solve_vc"}, "hfuse[solve_e+finish]": {"pair": "solve_e+finish"},
              "hfuse[solve_e-v+finish]": {"pair": "solve_e-v+finish"},
+             "hfuse[solve_e+finish-rz]": {"pair": "solve_e+finish-rz"},
+             "hfuse[solve_e-v+finish-rz]": {"pair": "solve_e-v+finish-rz"},
+             "atm_rk_dynamics_substep_finish[-rz]": {"norz": True},
              "atm_compute_solve_diagnostics[e-v]": {"part": "e"}, "atm_compute_solve_diagnostics[-v]": {},
              "atm_compute_solve_diagnostics[live]": {"live": True},
              "hfuse[solve_e+vert_imp]": {"pair": "solve_e+vert_imp"},

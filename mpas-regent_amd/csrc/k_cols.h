@@ -218,8 +218,11 @@ __device__ __forceinline__ void divdamp_body(const DevState& S, double coef_divd
 // (CELLS a template argument: every keep tail is addressed with a constant entity kind -- a runtime
 // kind select in keep_tail was miscompiled once, mpas_dev.h k_keep_refresh)
 template <bool CELLS>
+// (norz, atm_srk3 in the reference semantics: the copy rho_zz = rho_zz_old_split is the identity -- this
+// step's setup made rho_zz_old_split from rho_zz, with the same levels and keep tails, and nothing writes
+// either in between -- so it is not made)
 __device__ __forceinline__ void finish64_part(const DevState& S, int substep, int split, double inv_split, Pair64 q,
-                                              int b, int nb) {
+                                              int b, int nb, int norz = 0) {
     constexpr bool cells = CELLS;
     constexpr int kind = CELLS ? KC : KE;
     const size_t n = (size_t)(cells ? S.nCO : S.nEO) * 32;
@@ -253,13 +256,13 @@ __device__ __forceinline__ void finish64_part(const DevState& S, int substep, in
         }
         st64k(avgS, i, sv, q, keepv<64>(S, cells ? F_wwAvg_split : F_ruAvg_split, kind, col));
         if (last && !same) st64k(avg, i, make_double2(sv.x * inv_split, sv.y * inv_split), q, q.el ? a.y : a.x);
-        if (cells && last && S.physics != 2) cp(F_rho_zz_old_split, F_rho_zz);
+        if (cells && last && S.physics != 2 && !norz) cp(F_rho_zz_old_split, F_rho_zz);
     }
 }
 __device__ __forceinline__ void finish64_body(const DevState& S, int substep, int split, double inv_split, Pair64 q,
-                                              bool cells, int b, int nb) {
-    if (cells) finish64_part<true>(S, substep, split, inv_split, q, b, nb);
-    else finish64_part<false>(S, substep, split, inv_split, q, b, nb);
+                                              bool cells, int b, int nb, int norz = 0) {
+    if (cells) finish64_part<true>(S, substep, split, inv_split, q, b, nb, norz);
+    else finish64_part<false>(S, substep, split, inv_split, q, b, nb, norz);
 }
 
 

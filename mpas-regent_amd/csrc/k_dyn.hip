@@ -55,6 +55,7 @@ struct DynK {
     double h4d;  // DIN: the h4 of the rk_step 0 call whose del4 of tend_u_euler this call applies
     double rud;  // (option mru, the MPAS dynamics, fast path) the stage's dts: the kernel forming the final
                  // tend_u also stores the first substep's ru_p = dts tend_u and ruAvg = ru_p
+    int nhd;     // (option ntu, rk_step 0 with B forming no tend_u) A's h_divergence is dead: not stored
 };
 
 // option mru (the MPAS dynamics, atm_srk3 fast path): the stage's first acoustic substep begins with
@@ -218,7 +219,8 @@ __device__ __forceinline__ void dyn_A_body(const DevState& S, const DynK& a, Blk
         wc += (rz * fzm + rz_m * fzp) * ((aa * aa) + (bb * bb)) / a.r_earth +
               2.0 * kOmega * coslat * (fzm * urz + fzp * urz_m) * (rz * fzm + rz_m * fzp);
     }
-    put2f<LP>(fw(S, F_h_divergence), c, fw(S, X_wc), c, k, KEEPW(hd, kl_hd), k < L ? wc : 0.0);
+    if (a.nhd) colk(fw(S, X_wc), c) = k < L ? wc : 0.0;  // (option ntu: h_divergence read by no kernel)
+    else put2f<LP>(fw(S, F_h_divergence), c, fw(S, X_wc), c, k, KEEPW(hd, kl_hd), k < L ? wc : 0.0);
 }
 template <int LP, bool RK0, bool MD>
 __global__ __launch_bounds__(256) void k_dyn_A(DevState S, DynK a) {
@@ -1462,6 +1464,9 @@ static DynK make_dynk(const DevState& S, const DynTendArgs& in) {
     a.vB = (in.store_v && S.eoe_same && S.physics != 2) ? 1 : 0;
     a.h4d = (in.defer_in && in.rk_step != 0 && in.horiz_mixing == 0) ? kVisc4_2dsmag * (kLenDisp * kLenDisp * kLenDisp) : 0.0;
     a.rud = (S.physics == 2 && !in.exact_q) ? in.rud : 0.0;  // (option mru: the fast path's HF kernels, and D)
+    // (option ntu at rk_step 0 where B forms no tend_u -- dyn_lp_md's `ntu`: h_divergence, which only tend_u
+    // reads, is dead; the last stage's A rewrites it)
+    a.nhd = (S.physics == 0 && in.ntu && in.rk_step == 0 && !(a.h4 > 0.0 && !a.d4o)) ? 1 : 0;
     return a;
 }
 
@@ -1641,7 +1646,8 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
     } else {
         HALO_RUN(S, st, kA, F_ru);
     }
-    HALO_WROTE(S, F_kdiff, F_h_divergence, F_tend_rho, F_dpdz);
+    HALO_WROTE(S, F_kdiff, F_tend_rho, F_dpdz);
+    if (!a.nhd) HALO_WROTE(S, F_h_divergence);
     if (!MD && rk0) HALO_WROTE(S, X_wc);
     if (rk0) {
         if (ntu && nth)  // (the pressure gradient and del2 alone)

@@ -419,15 +419,17 @@ __global__ __launch_bounds__(256) void k_finish_cells(DevState S, int substep, i
 // LP = 64 form of both finish kernels in one launch (blockIdx.y: 0 edges, 1 cells), 16-B
 // position pairs.  With substep = split = 1 (atm_srk3) the average is s * 1.0 = s: its
 // store back is skipped (the same bits)
-__global__ __launch_bounds__(256) void k_finish64(DevState S, int substep, int split, double inv_split, Pair64 q) {
-    finish64_body(S, substep, split, inv_split, q, blockIdx.y == 1, (int)blockIdx.x, (int)gridDim.x);
+__global__ __launch_bounds__(256) void k_finish64(DevState S, int substep, int split, double inv_split, Pair64 q,
+                                                  int norz) {
+    finish64_body(S, substep, split, inv_split, q, blockIdx.y == 1, (int)blockIdx.x, (int)gridDim.x, norz);
 }
 
-hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split) {
+hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split, int norz) {
     double inv = 1.0 / (double)split;
+    if (norz && (S.physics || substep != split || S.LP != 64)) return hipErrorInvalidValue;
     if (S.LP == 64) {
         const int gx = (stream_grid((size_t)S.nEO * 32) + 3) / 4;
-        k_finish64<<<dim3(gx, 2), 256, 0, st>>>(S, substep, split, inv, Pair64(S.L));
+        k_finish64<<<dim3(gx, 2), 256, 0, st>>>(S, substep, split, inv, Pair64(S.L), norz);
     } else {
         k_finish_edges<<<stream_grid((size_t)S.nEO * S.LP), 256, 0, st>>>(S, substep, split, inv);
         k_finish_cells<<<stream_grid((size_t)S.nCO * S.LP), 256, 0, st>>>(S, substep, split, inv);
@@ -438,7 +440,7 @@ hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep,
     if (substep < split)
         HALO_WROTE(S, F_ru_save, F_u, F_rw_save, F_rtheta_p_save, F_rho_p_save, F_w, F_theta_m, F_rho_zz);
     HALO_WROTE(S, F_ruAvg, F_ruAvg_split, F_wwAvg, F_wwAvg_split);
-    if (substep == split && S.physics != 2) HALO_WROTE(S, F_rho_zz);
+    if (substep == split && S.physics != 2 && !norz) HALO_WROTE(S, F_rho_zz);
     return hipGetLastError();
 }
 

@@ -154,14 +154,14 @@ __global__ __launch_bounds__(256) void k_hf_damp_vc(DevState S, double coef, int
 }
 template <int EPW, bool RV>
 __global__ __launch_bounds__(256) void k_hf_e_finish(DevState S, int nb1, int gx, int substep, int split, double inv,
-                                                     Pair64 q) {
+                                                     Pair64 q, int norz) {
     const int b = (int)blockIdx.x;
     if (b < nb1) {
         solve_e_body<64, RV, false, EPW>(S, Blk{b, nb1});
     } else {
         const int r = b - nb1;
         const bool cells = r >= gx;
-        finish64_body(S, substep, split, inv, q, cells, cells ? r - gx : r, gx);
+        finish64_body(S, substep, split, inv, q, cells, cells ? r - gx : r, gx, norz);
     }
 }
 template <int LP, int EPW>
@@ -196,15 +196,15 @@ static hipError_t hf_damp_vc_lp(const DevState& S, hipStream_t st, double dts, i
 hipError_t launch_hf_damp_solve_vc(const DevState& S, hipStream_t st, double dts, int tme) {
     MPAS_LP_DISPATCH(S.LP, hf_damp_vc_lp, S, st, dts, tme);
 }
-hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st, int recon_v) {
+hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st, int recon_v, int norz) {
     if (!hf_ok(S) || S.LP != 64) return hipErrorInvalidValue;
     const int gx = (stream_grid_((size_t)S.nEO * 32) + 3) / 4;
     hipError_t e = hipSuccess;
     epw_go<64>(S, [&](auto epw) {
         constexpr int E = decltype(epw)::value;
         const int nb1 = col_blocks_n<64, E>(S, KE);
-        if (recon_v) k_hf_e_finish<E, true><<<nb1 + 2 * gx, 256, 0, st>>>(S, nb1, gx, 1, 1, 1.0, Pair64(S.L));
-        else k_hf_e_finish<E, false><<<nb1 + 2 * gx, 256, 0, st>>>(S, nb1, gx, 1, 1, 1.0, Pair64(S.L));
+        if (recon_v) k_hf_e_finish<E, true><<<nb1 + 2 * gx, 256, 0, st>>>(S, nb1, gx, 1, 1, 1.0, Pair64(S.L), norz);
+        else k_hf_e_finish<E, false><<<nb1 + 2 * gx, 256, 0, st>>>(S, nb1, gx, 1, 1, 1.0, Pair64(S.L), norz);
     });
     return e == hipSuccess ? hipGetLastError() : e;
 }

@@ -999,6 +999,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     // reads nothing it writes; an rk_step 0 stage 1 would read divergence and vorticity)
     const int rk1 = schedule == 0 ? (int)rk_sub_timestep[1] : 1;
     const bool solve0_dead = c->ntu && S.physics == 0 && !hf && rk1 != 0;
+    // option ntu (reference semantics): the substep finish's rho_zz = rho_zz_old_split is the identity --
+    // this step's setup made rho_zz_old_split from rho_zz and nothing writes either in between -- not made
+    const bool norz = (c->ntu == 1 || c->ntu == 2) && S.physics == 0 && S.LP == 64 && dynamics_split == 1;
     if (c->fusesetup && S.physics == 0 && hf2) {  // + stage 0's dyn_tend A in the same launch
         run_task(c, smls ? "hfuse[setup+dyn_A+sml_flux]" : "hfuse[setup+dyn_A]", [&] {
             return launch_hf_setup_dyn_A(S, st, stage_args(0), rk_sub_timestep[0], fcopy ? 0 : 1, smls ? 1 : 0);
@@ -1117,8 +1120,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         if (hf && fuse && rk_step == 2 && S.LP == 64 && !c->transport) {
             // (the vertex / cell kernel ran beside the last damping) the edge kernel beside
             // atm_rk_dynamics_substep_finish, which follows below
-            run_task(c, vdyn_on ? "hfuse[solve_e-v+finish]" : "hfuse[solve_e+finish]",
-                     [&] { return launch_hf_solve_e_finish(S, st, vdyn_on ? 0 : 1); });
+            run_task(c, vdyn_on ? (norz ? "hfuse[solve_e-v+finish-rz]" : "hfuse[solve_e-v+finish]")
+                                : (norz ? "hfuse[solve_e+finish-rz]" : "hfuse[solve_e+finish]"),
+                     [&] { return launch_hf_solve_e_finish(S, st, vdyn_on ? 0 : 1, norz ? 1 : 0); });
         } else if (hf && fuse && rk_step == 2) {
             run_task(c, vdyn_on ? "atm_compute_solve_diagnostics[e-v]" : "atm_compute_solve_diagnostics[e]",
                      [&] { return launch_solve_diagnostics(S, st, 0, 2, 2, vdyn_on ? 1 : 0); });
@@ -1163,7 +1167,8 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
     if (S.physics == 2)  // the MPAS dynamics: cell-centre winds for the next step's curvature
         run_task(c, "mpas_reconstruct_2d", [&] { return launch_reconstruct_2d(S, st, 1); });  // (:487, commented)
     if (!(hf && fuse && S.LP == 64 && !c->transport))  // (else it ran beside solve_diagnostics' edges)
-        run_task(c, "atm_rk_dynamics_substep_finish", [&] { return launch_substep_finish(S, st, 1, dynamics_split); });
+        run_task(c, norz ? "atm_rk_dynamics_substep_finish[-rz]" : "atm_rk_dynamics_substep_finish",
+                 [&] { return launch_substep_finish(S, st, 1, dynamics_split, norz ? 1 : 0); });
     fb.finish();
     // :492 summarize_timestep(cr, er, false, false, false) (constants.rg:67-69): prints only
 }

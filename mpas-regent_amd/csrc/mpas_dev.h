@@ -278,14 +278,15 @@ hipError_t launch_div_damping_div(const DevState& S, hipStream_t st, double dts,
 double divdamp_coef(double dts);
 // combined launches of independent neighbours (option "hfuse", k_solve.hip)
 hipError_t launch_hf_damp_solve_vc(const DevState& S, hipStream_t st, double dts, int tme);
-hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st, int recon_v = 1);
+hipError_t launch_hf_solve_e_finish(const DevState& S, hipStream_t st, int recon_v = 1, int norz = 0);
 hipError_t launch_hf_solve_e_vert_imp(const DevState& S, hipStream_t st, double dts);
 // parts: 1 the vertex / cell kernel, 2 the edge kernel, 3 both (the task)
 // no_v: v (rk_step -1 / 2) is not reconstructed here (atm_srk3 option "vdyn": stage 2's dyn_tend
 // edge kernel has stored it from the same u)
 hipError_t launch_solve_diagnostics(const DevState& S, hipStream_t st, int hollingsworth, int rk_step, int parts = 3,
                                     int no_v = 0);
-hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split);
+// (norz: atm_srk3, reference semantics, LP = 64 -- rho_zz = rho_zz_old_split is the identity there, not made)
+hipError_t launch_substep_finish(const DevState& S, hipStream_t st, int substep, int split, int norz = 0);
 hipError_t launch_fill_synthetic(const DevState& S, hipStream_t st, uint64_t seed);
 // keep tails (below): set both tails of field f from the field; compare one tail (level 0 or
 // L) with the field on the owned entities, *flag = 2 f + lev0 + 1 on a mismatch

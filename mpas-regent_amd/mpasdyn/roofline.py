@@ -17,7 +17,7 @@ roofline.achieved divides by the measured launch time.
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
           ddx=False, ntu=False, live=False, nst=False, navg=False, save=False, nww=False, ru=False,
-          rudone=False, nbc=False):
+          rudone=False, nbc=False, norz=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -27,6 +27,10 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
                                     ("atm_rk_dynamics_substep_finish", {})),
                  "solve_e-v+finish": (("atm_compute_solve_diagnostics", {"part": "e"}),
                                       ("atm_rk_dynamics_substep_finish", {})),
+                 "solve_e+finish-rz": (("atm_compute_solve_diagnostics", {"part": "e", "reconstruct_v": True}),
+                                       ("atm_rk_dynamics_substep_finish", {"norz": True})),
+                 "solve_e-v+finish-rz": (("atm_compute_solve_diagnostics", {"part": "e"}),
+                                         ("atm_rk_dynamics_substep_finish", {"norz": True})),
                  "solve_e+vert_imp": (e, vi),
                  "acoustic+solve_vc": (("atm_advance_acoustic_step_work", {"small_step": 1, "damp": True, "wold": False,
                                                                            "ddx": ddx}),
@@ -116,12 +120,11 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             # are dead and not formed -- no credit for them nor for the arrays only they read (B's tend_u
             # terms and flux, E's theta advection and wdtz); at rk_step > 0 no A either (its h_divergence
             # feeds only that tend_u) and B only applies the deferred del4 (no credit, as defer4's)
-            dead_w = {"tend_u", "tend_theta", "tend_rtheta_adv", "rthdynten"}
+            dead_w = {"tend_u", "tend_theta", "tend_rtheta_adv", "rthdynten", "h_divergence"}  # (h_divergence: tend_u's)
             dead_r = {"pv_edge", "tend_ru_physics", "ke", "w", "rw_save", "theta_m_save", "rt_diabatic_tend",
                       "tend_rtheta_physics", "ru_save", "nEdgesOnEdge", "edgesOnEdge", "weightsOnEdge", "angleEdge",
                       "latEdge", "nAdvCellsForEdge", "advCellsForEdge", "adv_coefs", "adv_coefs_3rd"}
             if rk_step != 0:
-                dead_w |= {"h_divergence"}
                 dead_r |= {"u", "rho_edge", "theta_m", "tend_theta_euler", "tend_u_euler", "cellsOnEdge",
                            "verticesOnEdge", "dvEdge", "invDcEdge"}
             writes = [x for x in writes if x not in dead_w]
@@ -230,7 +233,7 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
         # averages are copied to the *_split fields and divided by 1 -- the kernel stores no
         # unchanged average (no credit for bytes not moved); rho_zz = rho_zz_old_split in the
         # reference semantics, kept under the MPAS dynamics)
-        if md:
+        if md or norz:  # (norz, option ntu: rho_zz = rho_zz_old_split is the identity in atm_srk3 -- not made)
             return ["wwAvg", "ruAvg"], ["wwAvg_split", "ruAvg_split"]
         return ["wwAvg", "rho_zz_old_split", "ruAvg"], ["wwAvg_split", "rho_zz", "ruAvg_split"]
     if task == "atm_advance_scalars_mono":  # k_transport.hip (Q26: MPAS-A's, not the reference's)
@@ -361,7 +364,7 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
     out += [
             ("atm_compute_solve_diagnostics", {"live": True} if ntu else {}, 1 if ntu else 2),
             ("atm_compute_solve_diagnostics", {"reconstruct_v": True}, 1),
-            ("atm_rk_dynamics_substep_finish", {}, 1)]
+            ("atm_rk_dynamics_substep_finish", {"norz": bool(ntu)}, 1)]
     return out
 
 
