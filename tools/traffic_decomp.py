@@ -133,8 +133,10 @@ E_RK0_NTH_R = ["X_wc", "rw", "pressure_p", "dpdz", "theta_m", "tend_w_euler", "t
                "delsq_w", "delsq_theta"]
 E_RK1_NTH_R = ["uReconstructZonal", "uReconstructMeridional", "rw", "ru:C", "theta_m", "tend_w_euler",
                "tend_theta_euler", "rho_zz"]
+# (A at rk_step 0 stores no h_divergence: B forms no tend_u, its only reader)
+A_KS_NTU = [(k[0], k[1], k[2], k[3], [f for f in k[4] if f != "h_divergence"], k[5]) for k in A_KS]
 LAYOUTS["r06ntu"] = {
-    "rk0": A_KS + [
+    "rk0": A_KS_NTU + [
         ("B", "k_dyn_B", lambda t: t[1:] == (1, 0, 1, 0, 1, 1), B_RK0_NTU_R,
          ["tend_u_euler", "delsq_u", "ru_save", "u_2"], ("E", E_EB)),
         C_K,
