@@ -412,6 +412,8 @@ def task_table(rep, work_dims, n_prof, physics, ddx=False):
             kw["store_v"] = True
         if "+ru" in tag:  # (option mru: the first substep's ru_p / ruAvg stored here)
             kw["ru"] = True
+        if "+sml" in tag:  # (option msml: the stage's set_smlstep in E)
+            kw["smle"] = True
         if tag.endswith("-A"):
             kw["noA"] = True
         return kw
@@ -711,8 +713,9 @@ def main():
     trsave = bool(args.transport) and bool(ctx.get_option("trsave")) and not decomposed and not any(
         ctx.get_option(o) for o in ("trtile", "tredge", "trsu"))
     mru = bool(ctx.get_option("mru")) and int(args.physics) == 2 and not args.exact
+    msml = bool(ctx.get_option("msml")) and int(args.physics) == 2
     b_step = roofline.b_alg_step(work_dims, 1, int(args.physics), int(args.transport), fused, fsetup, fsml, fcopy, d4,
-                                 smls, ntu, mdamp, trsave, mru)
+                                 smls, ntu, mdamp, trsave, mru, msml)
     step_gbs = b_step / (ms_step * 1e-3) / 1e9
 
     value = (1 if decomposed else world) * ncells / (ms_step * 1e-3) / 1e6
@@ -736,7 +739,7 @@ def main():
                                                  f"replicas{world}" if world > 1 else "single-gpu"),
                       "exact": args.exact, "physics": int(args.physics), "transport": int(args.transport),
                       "graph": ctx.get_option("graph") if not decomposed else 0, "fusedamp": int(fused), "fusesetup": int(fsetup), "fusecopy": int(fcopy), "smlsum": int(smls),
-                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "mdamp": int(mdamp), "trsave": int(trsave), "mru": int(mru), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
+                      "fusesml": int(fsml), "defer4": int(d4), "ntu": int(ntu), "mdamp": int(mdamp), "trsave": int(trsave), "mru": int(mru), "msml": int(msml), "tmedge": int(fused and bool(ctx.get_option("tmedge"))),
                       "hfuse": int(bool(ctx.get_option("hfuse_active")))},
            "step_b_alg_GB": round(b_step / 1e9, 3), "step_achieved_GBs": round(step_gbs, 1),
            "roofline": roof, "tasks": tasks_out}

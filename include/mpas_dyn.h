@@ -134,7 +134,10 @@ int mpas_get_stream(mpas_ctx* ctx, void** stream);
  * copy into the transport (undecomposed, the default transport kernels): they read the old scalars
  * from scalars and the bounds kernel stores scalars_old.  "mdamp" = 1 (default; speed only; the MPAS
  * forms) applies each divergence damping in the kernel that next reads ru_p (the next substep's ru_p
- * kernel, the stage's recover edge kernel).  "trepw" = 2 (speed only; measured within 2 %, default 1): two
+ * kernel, the stage's recover edge kernel); "mru" = 1 (default; the MPAS dynamics, fast path) has
+ * the kernel forming a stage's final tend_u store its first acoustic substep's ru_p and ruAvg;
+ * "msml" = 1 (default; the MPAS dynamics) applies each stage's set_smlstep in dyn_tend's cell
+ * kernel.  "trepw" = 2 (speed only; measured within 2 %, default 1): two
  * edges per wavefront in the transport's edge kernel.  "trtile" = 1
  * (speed only, default 0) runs the transport as two tiled kernels with the scalars of
  * compact cell tiles in LDS and no edge scratch, when every cell has at most 6 edges with

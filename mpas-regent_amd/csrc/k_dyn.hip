@@ -913,7 +913,11 @@ struct EtTile {
 // in between reads them (the acoustic step reads theta_m as its tend_rt, Q8) -- so the theta
 // advection, wdtz and those stores go, with B's per-edge flux (X_F) that only they read; w, and at
 // rk_step 0 tend_w_euler / tend_theta_euler (read by the later stages), are formed as always
-template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false, int ETM = 0, bool NTH = false>
+// SMLF (option msml, the MPAS dynamics): the stage's atm_set_smlstep_pert_variables_work applied to the
+// tend_w formed here (k_set_smlstep's MD form: the same loads and the same order of operations, from the
+// value it would read back), so its launch and the tend_w round trip go
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool TILE = false, int ETM = 0, bool NTH = false,
+          bool SMLF = false>
 __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int c, int k, EtTile tl = {}) {
     static_assert(!NTH || (!MD && !TILE), "the dead theta tendency: reference semantics, untiled");
     static_assert(!TILE || (LP == 64 && !MD), "the tiled E: LP = 64, reference semantics");
@@ -1176,7 +1180,43 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
             if (rk0) twe -= cqw * (rdzu * (pp - pp_m) - (fzm * dpdz + fzp * dpdz_m));
             w += twe;
         }
-        colk(fw(S, F_tend_w), c) = PADW(w);
+        if constexpr (SMLF) {  // :1503-1528 with the MPAS forms (k_set_smlstep<MD>), on the tend_w just formed
+            static_assert(MD, "set_smlstep in E: the MPAS dynamics");
+            const double w_in = ldz(k <= L, PADW(w));  // (the value k_set_smlstep would read back)
+            const double* ut_f = fd(S, F_tend_u);
+            const double *zb = fd(S, F_zb_cell), *zb3 = fd(S, F_zb3_cell);
+            const double zzv = col_rd<LP>(fd(S, F_zz), c, k, L), zz_m = lvl_dn<LP>(zzv, k);
+            double ut_[NF], utm_[NF], zb_[NF], zb3_[NF];
+#pragma unroll
+            for (int i = 0; i < NF; i += 2) gather2s<LP>(ut_f, e_[i], e_[i + 1], k, ut_[i], ut_[i + 1]);
+#pragma unroll
+            for (int i = 0; i < NF; i++) {
+                ut_[i] = ldz(k <= L, ut_[i]);
+                gather2<LP>(zb, c * 10 + i, zb3, c * 10 + i, k, zb_[i], zb3_[i]);
+            }
+#pragma unroll
+            for (int i = 0; i < NF; i++) utm_[i] = lvl_dn<LP>(ut_[i], k);
+            double ws = w_in;
+#pragma unroll
+            for (int i = 0; i < NF; i++) {
+                double flux = eocs_[i] * (fzm * ut_[i] + fzp * utm_[i]);
+                const double t = (zb_[i] + copysign(1.0, ut_[i]) * zb3_[i]) * flux;
+                ws = sub_if(i < ne, ws, t);
+            }
+            for (int i = NF; i < ne; i++) {
+                int iEdge = eoc[i];
+                double ut = col_rd<LP>(ut_f, iEdge, k, L);
+                double ut_m = lvl_dn<LP>(ut, k);
+                double flux = eocs[i] * (fzm * ut + fzp * ut_m);
+                size_t q = ((size_t)c * 10 + i) * LP + lpos(LP, k);
+                ws -= (zb[q] + copysign(1.0, ut) * zb3[q]) * flux;
+            }
+            ws *= (fzm * zzv + fzp * zz_m);
+            const bool in_zone = fi(S, F_bdyMaskCell)[c] <= kRelaxZone;
+            colk(fw(S, F_tend_w), c) = in_zone ? ((k >= 1 && k < L) ? ws : PADW(w_in)) : PADW(w);
+        } else {
+            colk(fw(S, F_tend_w), c) = PADW(w);
+        }
         if (rk0) colk(fw(S, F_tend_w_euler), c) = KEEPW(twe, kl_twe);
     } else {
         if (k > 0 && kl) {  // :1289-1302 (Q14 literal), :1318-1322
@@ -1301,11 +1341,11 @@ __device__ __forceinline__ void dyn_E_cell(const DevState& S, const DynK& a, int
     if (rk0) colk(fw(S, F_tend_theta_euler), c) = PADW(tte);
 }
 
-template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool NTH = false>
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool NTH = false, bool SMLF = false>
 __device__ __forceinline__ void dyn_E_body(const DevState& S, const DynK& a, Blk bk) {
     ColMap<LP> m(S, KC, bk);
     if (m.ent >= S.nCO) return;
-    dyn_E_cell<LP, RK0, SELF, MD, HF, false, 0, NTH>(S, a, m.ent, m.k);
+    dyn_E_cell<LP, RK0, SELF, MD, HF, false, 0, NTH, SMLF>(S, a, m.ent, m.k);
 }
 
 // option "etile" (reference semantics, LP = 64): E over the tiles of TrTiles (mpas_dev.h; the
@@ -1430,9 +1470,9 @@ __global__ __launch_bounds__(NT, ETM == 2 && !RK0 ? 5 : 4) void k_dyn_Et(DevStat
 
 // (rk_step > 0, reference semantics, LP = 64: 4 waves per SIMD, as before E formed wc itself;
 // at LP < 64 that cap spilled 10-22 VGPRs)
-template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool NTH = false>
+template <int LP, bool RK0, bool SELF, bool MD, bool HF, bool NTH = false, bool SMLF = false>
 __global__ __launch_bounds__(256, LP == 64 && !RK0 && !MD ? 4 : 1) void k_dyn_E(DevState S, DynK a) {
-    dyn_E_body<LP, RK0, SELF, MD, HF, NTH>(S, a, this_blk());
+    dyn_E_body<LP, RK0, SELF, MD, HF, NTH, SMLF>(S, a, this_blk());
 }
 // D and E of rk_step 0 in one grid (option "hfuse": neither reads what the other writes)
 template <int LP, bool SELF, bool MD, bool HF>
@@ -1625,6 +1665,15 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         }
         auto go = [&](auto hfc) {
             constexpr bool H = decltype(hfc)::value;
+            if constexpr (MD) {
+                if (in.smlE) {  // (option msml: the stage's set_smlstep in E)
+                    if (rk0 && X.selfc) k_dyn_E<LP, true, true, MD, H, false, true><<<nb, 256, 0, st>>>(X, a);
+                    else if (rk0) k_dyn_E<LP, true, false, MD, H, false, true><<<nb, 256, 0, st>>>(X, a);
+                    else if (X.selfc) k_dyn_E<LP, false, true, MD, H, false, true><<<nb, 256, 0, st>>>(X, a);
+                    else k_dyn_E<LP, false, false, MD, H, false, true><<<nb, 256, 0, st>>>(X, a);
+                    return;
+                }
+            }
             if (rk0) {
                 if (X.selfc) k_dyn_E<LP, true, true, MD, H><<<nb, 256, 0, st>>>(X, a);
                 else k_dyn_E<LP, true, false, MD, H><<<nb, 256, 0, st>>>(X, a);
@@ -1662,7 +1711,7 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         HALO_WROTE(S, F_delsq_vorticity, F_delsq_divergence, F_delsq_w, F_tend_w_euler, F_delsq_theta,
                    F_tend_theta_euler);
         const bool runD = del4 && !a.d4o;  // (defer4: D runs in the next call's B)
-        if (runD && in.hfuse && !S.halo && !et && !nth) {  // D beside E, one grid
+        if (runD && in.hfuse && !S.halo && !et && !nth && !in.smlE) {  // D beside E, one grid
             const int nb1 = col_blocks<LP>(S, KE), nb = nb1 + col_blocks<LP>(S, KC);
             auto go = [&](auto hfc) {
                 constexpr bool H = decltype(hfc)::value;
@@ -1678,7 +1727,9 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
                 HALO_RUN(S, st, kD, F_delsq_divergence, F_delsq_vorticity);
                 HALO_WROTE(S, F_tend_u_euler, F_tend_u);
             }
-            if (nth) HALO_RUN(S, st, kE, F_delsq_w, F_delsq_theta);
+            if (in.smlE && hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta, F_tend_u);  // (msml)
+            else if (in.smlE) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta, F_tend_u);
+            else if (nth) HALO_RUN(S, st, kE, F_delsq_w, F_delsq_theta);
             else if (et) HALO_RUN(S, st, kE, F_ru, F_theta_m, F_delsq_w, F_delsq_theta);
             else if (hf) HALO_RUN(S, st, kE, X_F, X_Fw, F_delsq_w, F_delsq_theta);  // (X_Fw: MD only written)
             else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_delsq_w, F_delsq_theta);
@@ -1698,7 +1749,9 @@ static hipError_t dyn_lp_md(const DevState& S, hipStream_t st, const DynTendArgs
         if (din) HALO_WROTE(S, F_tend_u_euler);
         if (a.vB) HALO_WROTE(S, F_v);
         if (MD) HALO_WROTE(S, X_Fw);
-        if (nth) HALO_RUN(S, st, kE, F_ru);
+        if (in.smlE && hf) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_tend_u);  // (msml: tend_u at the cells' edges)
+        else if (in.smlE) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save, F_tend_u);
+        else if (nth) HALO_RUN(S, st, kE, F_ru);
         else if (et) HALO_RUN(S, st, kE, F_ru, F_ru_save, F_theta_m, F_theta_m_save);
         else if (hf) HALO_RUN(S, st, kE, F_ru, X_F, X_Fw);  // (ru: wc at the cell's last edge, reference semantics)
         else HALO_RUN(S, st, kE, F_ru, X_F, X_Fw, F_ru_save, F_theta_m_save);

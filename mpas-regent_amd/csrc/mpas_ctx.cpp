@@ -108,6 +108,8 @@ struct mpas_ctx {
                        // (reference semantics, edgesOnEdge_ECP = edgesOnEdge; same values)
     int defer4 = 1;    // option "defer4": atm_srk3 applies rk_step 0's del4 of tend_u_euler (dyn_tend D) in the
                        // next stage's rk_step > 0 edge kernel (reference semantics; same values)
+    int msml = 1;      // option "msml" (the MPAS dynamics): each stage's set_smlstep applied by dyn_tend's E to
+                       // the tend_w it forms (no task reads tend_w in between)
     int mru = 1;       // option "mru" (the MPAS dynamics, fast path): the kernel forming a stage's final tend_u
                        // stores its first acoustic substep's ru_p / ruAvg (k_acoustic_ru FIRST skipped)
     int mdamp = 1;     // option "mdamp" (the MPAS forms): each divergence damping applied by the kernel that next
@@ -992,6 +994,9 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         // stores the first acoustic substep's ru_p = dts tend_u and ruAvg = ru_p (nothing in between reads
         // or writes them; set_smlstep reads tend_u only)
         if (c->mru && S.physics == 2 && !c->exact && number_sub_steps[r] > 0) a.rud = rk_sub_timestep[r];
+        // option msml (the MPAS dynamics): the stage's set_smlstep (:1503-1528) applied by E to the tend_w it
+        // forms -- set_smlstep follows dyn_tend directly and reads tend_u, which B / D have finished
+        if (c->msml && S.physics == 2) a.smlE = 1;
         return a;
     };
     bool flux_done = false;  // (option smlsum: the step's flux sum, beside setup and A on small grids)
@@ -1036,12 +1041,14 @@ void srk3(mpas_ctx* c, double dt, int schedule) {
         // timing key: the variant's read / write set (bench.py parses the tags)
         const std::string dname = std::string("atm_compute_dyn_tend_work[") + (a.rk_step == 0 ? "rk0" : "rk>0") +
                                   (a.cp ? "+copy" : "") + (a.defer_out ? "+d4o" : "") + (a.ntu ? "+ntu" : "") + (a.defer_in ? "+d4i" : "") +
-                                  (a.store_v ? "+v" : "") + (a.rud != 0.0 ? "+ru" : "") + (a.skipA ? "-A" : "") + "]";
+                                  (a.store_v ? "+v" : "") + (a.rud != 0.0 ? "+ru" : "") + (a.smlE ? "+sml" : "") +
+                                  (a.skipA ? "-A" : "") + "]";
         run_task(c, dname.c_str(), [&] { return launch_dyn_tend(S, st, a); });
         const bool ru_done = a.rud != 0.0;  // (option mru: the first substep's ru_p / ruAvg stored)
         // option fusesml (with fusedamp): the stage's first acoustic launch runs it first
         const bool sml = fuse && c->fusesml;
-        if (!sml) run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st, c->exact); });
+        if (!sml && !a.smlE)  // (option msml: run by E)
+            run_task(c, "atm_set_smlstep_pert_variables_work", [&] { return launch_set_smlstep(S, st, c->exact); });
         const int n_small = number_sub_steps[rk_step] + (S.physics ? 0 : 1);  // Q5 (the MPAS form: n)
         for (int small_step = 0; small_step < n_small; small_step++) {
             const double dts = rk_sub_timestep[rk_step];
@@ -1447,6 +1454,7 @@ int mpas_set_option(mpas_ctx* c, const char* name, int64_t value) {
         else if (name && std::strcmp(name, "ntu") == 0) c->ntu = value < 0 ? 0 : value > 3 ? 3 : value;
         else if (name && std::strcmp(name, "mdamp") == 0) c->mdamp = value ? 1 : 0;
         else if (name && std::strcmp(name, "mru") == 0) c->mru = value ? 1 : 0;
+        else if (name && std::strcmp(name, "msml") == 0) c->msml = value ? 1 : 0;
         else if (name && std::strcmp(name, "vdyn") == 0) c->vdyn = value ? 1 : 0;
         else if (name && std::strcmp(name, "tmedge") == 0) c->tmedge = value ? 1 : 0;
         else if (name && std::strcmp(name, "fusesml") == 0) c->fusesml = value ? 1 : 0;
@@ -1616,6 +1624,7 @@ int mpas_get_option(mpas_ctx* c, const char* name, int64_t* value) {
         else if (name && std::strcmp(name, "ntu") == 0) *value = c->ntu;
         else if (name && std::strcmp(name, "mdamp") == 0) *value = c->mdamp;
         else if (name && std::strcmp(name, "mru") == 0) *value = c->mru;
+        else if (name && std::strcmp(name, "msml") == 0) *value = c->msml;
         else if (name && std::strcmp(name, "vdyn") == 0) *value = c->vdyn;
         else if (name && std::strcmp(name, "eoe_same") == 0) {
             prepare_now(c);

@@ -207,6 +207,8 @@ struct DynTendArgs {
     // option "mru" (atm_srk3, the MPAS dynamics, fast path): the stage's dts -- the kernel forming the final
     // tend_u stores the first acoustic substep's ru_p and ruAvg (k_acoustic_ru FIRST then skipped)
     double rud = 0.0;
+    // option "msml" (atm_srk3, the MPAS dynamics): E applies the stage's set_smlstep to the tend_w it forms
+    int smlE = 0;
     // option "ntu" (atm_srk3, reference semantics, a stage before the step's last): the call's theta
     // tendencies are dead as well (the last stage rewrites them; the acoustic step reads theta_m as
     // its tend_rt, Q8): E forms none of them, B no per-edge flux for them

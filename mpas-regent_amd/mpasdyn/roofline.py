@@ -17,7 +17,7 @@ roofline.achieved divides by the measured launch time.
 def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=False, fused=False, sml=False,
           part=None, pair=None, copy=False, noA=False, defer_out=False, store_v=False, wold=True, smls=False,
           ddx=False, ntu=False, live=False, nst=False, navg=False, save=False, nww=False, ru=False,
-          rudone=False, nbc=False, norz=False):
+          rudone=False, nbc=False, norz=False, smle=False):
     md = physics == 2  # the MPAS dynamics (include/mpas_dyn.h option physics = 2)
     if task == "hfuse":  # option hfuse: independent kernels of the step in one launch
         e, vi, dA = ("atm_compute_solve_diagnostics", {"part": "e"}), ("atm_compute_vert_imp_coefs", {}), \
@@ -111,6 +111,8 @@ def _sets(task, rk_step=0, small_step=1, reconstruct_v=False, physics=0, damp=Fa
             writes = writes + ["ru_save", "u_2"]
         if ru:  # option mru (the MPAS dynamics): the first acoustic substep's ru_p, ruAvg from the final tend_u
             writes = writes + ["ru_p", "ruAvg"]
+        if smle:  # option msml (the MPAS dynamics): the stage's set_smlstep in E (tend_w corrected in place)
+            reads = reads + ["tend_u", "zb_cell", "zb3_cell", "zz", "bdyMaskCell"]
         if store_v:  # option vdyn (stage 2): solve_diagnostics' v from the gathered edgesOnEdge u
             writes = writes + ["v"]
         if defer_out and rk_step == 0:  # option defer4: tend_u of this call is dead and not stored
@@ -282,7 +284,8 @@ def b_alg(task, dims, **kw):
 
 
 def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-                  fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False, mru=False):
+                  fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False, mru=False,
+                  msml=False):
     """(task, kwargs, launches) of one atm_srk3 step (rk_timestep.rg:404-481); physics = 1
     (the MPAS vertical solver): number_sub_steps acoustic substeps (4 per step) and
     recover after each stage; transport = 1 adds the scalar save and the transport;
@@ -298,13 +301,15 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
             out = [("atm_rk_integration_setup", p, 1), ("atm_compute_moist_coefficients", p, 1),
                    ("atm_compute_vert_imp_coefs", {}, 2)]
         r = {"ru": True} if mru else {}  # (option mru: the first substep's ru_p / ruAvg stored by dyn_tend)
+        if msml and physics == 2:  # (option msml: each stage's set_smlstep in dyn_tend's E)
+            r = dict(r, smle=True)
         if schedule == 1:
             out += [("atm_compute_dyn_tend_work", {"rk_step": 0, "copy": copy, **p, **r}, 1),
                     ("atm_compute_dyn_tend_work", {"rk_step": 1, **p, **r}, 2)]
         # (option mdamp: each damping applied by the next kernel that reads ru_p -- the next substep's
         # ru_p kernel or the stage's recover)
         d = {"damp": bool(mdamp)}
-        out += [("atm_set_smlstep_pert_variables_work", p, 3),
+        out += [("atm_set_smlstep_pert_variables_work", p, 0 if (msml and physics == 2) else 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1, "rudone": bool(mru)}, 1 if ntu else 3),
                 ("atm_advance_acoustic_step_work", {"small_step": 0, "physics": 1, "nww": True, "rudone": bool(mru)},
                  2 if ntu else 0),
@@ -369,7 +374,8 @@ def step_schedule(schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=
 
 
 def b_alg_step(dims, schedule=1, physics=0, transport=0, fusedamp=False, fusesetup=False, fusesml=False,
-               fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False, mru=False):
+               fusecopy=False, defer4=False, smlsum=False, ntu=False, mdamp=False, trsave=False, mru=False,
+               msml=False):
     return sum(b_alg(t, dims, **kw) * n for t, kw, n in step_schedule(schedule, physics, transport, fusedamp,
                                                                         fusesetup, fusesml, fusecopy, defer4,
-                                                                        smlsum, ntu, mdamp, trsave, mru))
+                                                                        smlsum, ntu, mdamp, trsave, mru, msml))

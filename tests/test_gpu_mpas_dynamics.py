@@ -328,3 +328,29 @@ def test_mru_bit_identical(x1_2562, transport, L):
         out[mru] = got
     bad = compare_states(out[1], out[0], rtol=0.0)
     assert not bad, bad[:6]
+
+
+@pytest.mark.parametrize("transport", [0, 1])
+@pytest.mark.parametrize("L", [5, 56])
+def test_msml_bit_identical(x1_2562, transport, L):
+    """option msml (the MPAS dynamics): each stage's set_smlstep applied by dyn_tend's E to the tend_w
+    it forms (k_set_smlstep's loads and order of operations) instead of a launch of its own -- every
+    field after three steps has the same bits, exact and fast"""
+    st = state(x1_2562, L, "mpas0")
+    for exact in (1, 0):
+        out = {}
+        for msml in (0, 1):
+            got = st.copy()
+            with lib.Context(*st.dims()) as ctx:
+                ctx.set_option("exact", exact)
+                ctx.set_option("physics", 2)
+                ctx.set_option("transport", transport)
+                ctx.set_option("msml", msml)
+                ctx.upload(st)
+                for _ in range(3):
+                    T.atm_srk3(ctx, 720.0, 1)
+                ctx.sync()
+                ctx.download(got)
+            out[msml] = got
+        bad = compare_states(out[1], out[0], rtol=0.0)
+        assert not bad, f"exact={exact}: {bad[:6]}"
