@@ -6,7 +6,9 @@ achieved HBM bandwidth of the dominant task against the 8 TB/s roofline.
 
 One step = one atm_srk3 call: setup, moist, 2x vert_imp, 3x dyn_tend (rk_step 0,1,2 --
 the MPAS schedule of SURVEY §8.5), 3x smlstep, 7x acoustic + 7x divergence damping,
-3x solve_diagnostics, substep_finish (28 tasks).  Inputs are resident in HBM before the
+3x solve_diagnostics, substep_finish (28 tasks of the reference schedule; the library's
+fusions and option ntu's liveness launch fewer kernels for the same results -- every field
+after the step is bit-identical).  Inputs are resident in HBM before the
 timed region: the x1.163842 icosahedral mesh (mpasdyn.mesh) with its one-time
 precompute uploaded from the host, and the 3-D state filled on the device by the
 seeded generator (data: synthetic, seed 20211015).
